@@ -1,0 +1,71 @@
+/*
+ * spg.h — C-ABI of the MI355X-native Spartan prover hot path (libspg.so).
+ *
+ * Drop-in boundary for scroll-tech/spartan-parallel (reference snapshot under /root/reference).
+ * Every entry point replaces one internal seam of the Rust crate; the seam is cited per function.
+ * A Rust maintainer binds these with a `#[link(name = "spg")] extern "C"` block.
+ *
+ * Conventions
+ *   - Scalars cross as the reference's in-memory layout of `Scalar`: four little-endian u64 limbs in
+ *     Montgomery form with R = 2^256 (src/scalar/ristretto255.rs:193-199), i.e. `uint64_t[4]`.
+ *   - Group elements cross only as 32-byte CompressedRistretto encodings (src/group.rs:7).
+ *   - Every function returns 0 on success or a negative SPG_E_* code; spg_last_error() describes it.
+ *   - All calls on one spg_ctx are issued on that context's HIP stream and return after their
+ *     results are in the caller's buffers. Distinct contexts may be used from different threads.
+ *   - The library never draws randomness; callers own all host buffers.
+ */
+#ifndef SPG_H
+#define SPG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPG_OK 0
+#define SPG_E_ARG -1       /* bad size / null pointer / inconsistent shapes */
+#define SPG_E_NOMEM -2     /* device allocation failed */
+#define SPG_E_HIP -3       /* HIP runtime error */
+#define SPG_E_POINT -4     /* invalid compressed point (ProofVerifyError::DecompressionError) */
+#define SPG_E_NODEVICE -5  /* no usable gfx950 device */
+
+typedef struct spg_ctx spg_ctx;
+typedef struct spg_gens spg_gens;
+
+/* ---- context ------------------------------------------------------------------------------- */
+int spg_init(int device, spg_ctx** out);
+int spg_free(spg_ctx* ctx);
+const char* spg_last_error(const spg_ctx* ctx);
+/* device-side wall time of the most recent compute call, in microseconds (HIP events on the stream) */
+double spg_last_kernel_us(const spg_ctx* ctx);
+
+/* ---- generators ------------------------------------------------------------------------------
+ * MultiCommitGens::new(n, label) (src/commitments.rs:15-33): n+1 points from SHAKE256(label ||
+ * RISTRETTO_BASEPOINT_COMPRESSED) mapped with RistrettoPoint::from_uniform_bytes; G = first n, h = last.
+ * The handle keeps the points resident in HBM together with fixed-base window tables. */
+int spg_gens_derive(spg_ctx* ctx, const uint8_t* label, size_t label_len, size_t n, spg_gens** out);
+/* upload n+1 compressed points (G_0..G_{n-1}, h) instead of deriving them */
+int spg_gens_upload(spg_ctx* ctx, const uint8_t* compressed, size_t n, spg_gens** out);
+/* (n+1) x 32 bytes: G_0 .. G_{n-1}, h */
+int spg_gens_download(spg_ctx* ctx, const spg_gens* g, uint8_t* out);
+size_t spg_gens_n(const spg_gens* g);
+int spg_gens_free(spg_ctx* ctx, spg_gens* g);
+
+/* ---- multi-scalar multiplication ---------------------------------------------------------------
+ * GroupElement::vartime_multiscalar_mul (src/group.rs:98-116) against generators
+ * G[gen_offset .. gen_offset + n), plus blind * h when blind_mont != NULL
+ * (Commitments::commit for [Scalar], src/commitments.rs:87-92). out: 32-byte compression. */
+int spg_msm(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont, size_t n,
+            const uint64_t* blind_mont, uint8_t out[32]);
+/* Hyrax row commitments, DensePolynomial::commit_inner (src/dense_mlpoly.rs:184-212):
+ * for i < L: out[i] = compress( sum_j Z[R*i + j] * G[j] + blinds[i] * h ); blinds may be NULL (zeros,
+ * the `random_tape = None` case every SNARK::prove commit uses). Z is L*R scalars, row-major. */
+int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* Z_mont, size_t L, size_t R,
+                    const uint64_t* blinds_mont, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPG_H */

@@ -1,0 +1,188 @@
+"""ORACLE loader — test infrastructure only.
+
+ctypes bindings over oracle/build/liboracle.so, the CPU restatement of the reference's algorithms
+(see the headers in oracle/*.hpp for the reference file:line each function follows). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the product
+(spartan-parallel_amd/) never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def u64s(x):
+    return np.ascontiguousarray(x, dtype=np.uint64)
+
+
+# ---------------- Fq ----------------
+_OPS = {"add": 0, "sub": 1, "mul": 2, "neg": 3, "square": 4, "invert": 5}
+
+
+def fq_op(op, a, b=None):
+    a = u64s(a).reshape(-1, 4)
+    n = a.shape[0]
+    out = np.zeros_like(a)
+    bb = None if b is None else u64s(b).reshape(-1, 4)
+    lib().orc_fq_binop(ctypes.c_int(_OPS[op]), _p(a), None if bb is None else _p(bb), _p(out), ctypes.c_size_t(n))
+    return out
+
+
+def fq_to_bytes(a):
+    a = u64s(a).reshape(-1, 4)
+    out = np.zeros((a.shape[0], 32), dtype=np.uint8)
+    lib().orc_fq_to_bytes(_p(a), _p(out), ctypes.c_size_t(a.shape[0]))
+    return out
+
+
+def fq_from_bytes(b32):
+    b = np.frombuffer(bytes(b32), dtype=np.uint8).copy()
+    out = np.zeros(4, dtype=np.uint64)
+    ok = lib().orc_fq_from_bytes(_p(b), _p(out))
+    return out, bool(ok)
+
+
+def fq_from_bytes_wide(b):
+    b = np.frombuffer(bytes(b), dtype=np.uint8).copy().reshape(-1, 64)
+    out = np.zeros((b.shape[0], 4), dtype=np.uint64)
+    lib().orc_fq_from_bytes_wide(_p(b), _p(out), ctypes.c_size_t(b.shape[0]))
+    return out
+
+
+def fq_from_u512(limbs):
+    l8 = u64s(limbs)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().orc_fq_from_u512(_p(l8), _p(out))
+    return out
+
+
+def fq_from_raw(limbs):
+    l4 = u64s(limbs)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().orc_fq_from_raw(_p(l4), _p(out))
+    return out
+
+
+def fq_from_u64(x):
+    out = np.zeros(4, dtype=np.uint64)
+    lib().orc_fq_from_u64(ctypes.c_uint64(x), _p(out))
+    return out
+
+
+def fq_batch_invert(a):
+    a = u64s(a).reshape(-1, 4).copy()
+    allinv = np.zeros(4, dtype=np.uint64)
+    lib().orc_fq_batch_invert(_p(a), ctypes.c_size_t(a.shape[0]), _p(allinv))
+    return a, allinv
+
+
+# ---------------- hashing ----------------
+def keccak_f1600(state200):
+    s = np.frombuffer(bytes(state200), dtype=np.uint8).copy()
+    lib().orc_keccak_f1600(_p(s))
+    return s.tobytes()
+
+
+def shake256(data, n):
+    d = np.frombuffer(bytes(data) or b"\0", dtype=np.uint8).copy()
+    out = np.zeros(n, dtype=np.uint8)
+    lib().orc_shake256(_p(d), ctypes.c_size_t(len(data)), _p(out), ctypes.c_size_t(n))
+    return out.tobytes()
+
+
+def merlin_simple(label, l1, m1, l2, n):
+    out = np.zeros(n, dtype=np.uint8)
+    m = np.frombuffer(bytes(m1) or b"\0", dtype=np.uint8).copy()
+    lib().orc_merlin_simple(ctypes.c_char_p(label), ctypes.c_char_p(l1), _p(m), ctypes.c_size_t(len(m1)),
+                            ctypes.c_char_p(l2), _p(out), ctypes.c_size_t(n))
+    return out.tobytes()
+
+
+# ---------------- ristretto ----------------
+def ristretto_consts():
+    out = np.zeros(6 * 32, dtype=np.uint8)
+    lib().orc_ristretto_consts(_p(out))
+    return [out[32 * i:32 * i + 32].tobytes() for i in range(6)]
+
+
+def ge_roundtrip(b32):
+    i = np.frombuffer(bytes(b32), dtype=np.uint8).copy()
+    out = np.zeros(32, dtype=np.uint8)
+    ok = lib().orc_ge_decompress_compress(_p(i), _p(out))
+    return out.tobytes() if ok else None
+
+
+def ge_from_uniform_bytes(b64):
+    b = np.frombuffer(bytes(b64), dtype=np.uint8).copy()
+    n = len(b) // 64
+    out = np.zeros(32 * n, dtype=np.uint8)
+    lib().orc_ge_from_uniform_bytes(_p(b), _p(out), ctypes.c_size_t(n))
+    return [out[32 * k:32 * k + 32].tobytes() for k in range(n)]
+
+
+def ge_add(a, b):
+    x = np.frombuffer(bytes(a), dtype=np.uint8).copy()
+    y = np.frombuffer(bytes(b), dtype=np.uint8).copy()
+    out = np.zeros(32, dtype=np.uint8)
+    ok = lib().orc_ge_add(_p(x), _p(y), _p(out))
+    return out.tobytes() if ok else None
+
+
+def ge_scalarmul(P, k32):
+    x = np.frombuffer(bytes(P), dtype=np.uint8).copy()
+    k = np.frombuffer(bytes(k32), dtype=np.uint8).copy()
+    out = np.zeros(32, dtype=np.uint8)
+    ok = lib().orc_ge_scalarmul(_p(x), _p(k), _p(out))
+    return out.tobytes() if ok else None
+
+
+def gens_stream(label, count):
+    out = np.zeros(32 * count, dtype=np.uint8)
+    lb = np.frombuffer(bytes(label), dtype=np.uint8).copy()
+    lib().orc_gens_stream(_p(lb), ctypes.c_size_t(len(label)), ctypes.c_size_t(count), _p(out))
+    return out.reshape(count, 32)
+
+
+def msm(bases, scalars):
+    bases = np.ascontiguousarray(bases, dtype=np.uint8).reshape(-1, 32)
+    s = u64s(scalars).reshape(-1, 4)
+    assert bases.shape[0] == s.shape[0]
+    out = np.zeros(32, dtype=np.uint8)
+    ok = lib().orc_msm(_p(bases), _p(s), ctypes.c_size_t(s.shape[0]), _p(out))
+    assert ok
+    return out.tobytes()
+
+
+def commit_rows(bases, h, Z, L, R, blinds=None):
+    bases = np.ascontiguousarray(bases, dtype=np.uint8).reshape(-1, 32)
+    hh = np.frombuffer(bytes(h), dtype=np.uint8).copy()
+    Z = u64s(Z).reshape(-1, 4)
+    assert Z.shape[0] == L * R
+    out = np.zeros((L, 32), dtype=np.uint8)
+    bl = None if blinds is None else u64s(blinds).reshape(-1, 4)
+    ok = lib().orc_commit_rows(_p(bases), ctypes.c_size_t(bases.shape[0]), _p(hh), _p(Z), ctypes.c_size_t(L),
+                               ctypes.c_size_t(R), None if bl is None else _p(bl), _p(out))
+    assert ok
+    return out

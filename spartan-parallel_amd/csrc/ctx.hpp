@@ -1,0 +1,57 @@
+// spg — per-context state: device, stream, error text, timing events and a growable HBM workspace.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/spg.h"
+#include "curve.hpp"
+
+struct spg_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_us = 0.0;
+  std::string err;
+  // workspace slots: grown on demand, reused across calls (no allocation in steady state)
+  struct Slot {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::vector<Slot> ws;
+};
+
+struct spg_gens {
+  size_t n = 0;                  // number of G points; h is point n
+  spg::Niels* niels = nullptr;   // n+1 affine Niels points (device)
+  spg::Niels* table = nullptr;   // [254][n+1] : table[k][i] = 2^k * P_i (device)
+  uint8_t* compressed = nullptr; // (n+1) x 32 host copy
+};
+
+namespace spg {
+
+static const int kTableRows = 254;  // bit offsets 0..253 cover every window of a 253-bit scalar
+
+int set_err(spg_ctx* c, int code, const std::string& msg);
+
+#define SPG_HIP(ctx, call)                                                                     \
+  do {                                                                                         \
+    hipError_t e_ = (call);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return spg::set_err(ctx, SPG_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define SPG_CHECK(ctx, cond, msg) \
+  do {                            \
+    if (!(cond)) return spg::set_err(ctx, SPG_E_ARG, msg); \
+  } while (0)
+
+// returns a device buffer of at least `bytes` for workspace slot `slot` (contents undefined)
+void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
+
+// timing bracket on the context stream
+void timer_start(spg_ctx* c);
+void timer_stop(spg_ctx* c);
+
+}  // namespace spg

@@ -1,0 +1,380 @@
+// spg — MI355X-native Spartan prover hot path.
+// Exact modular arithmetic for the two fields of ristretto255, written for CDNA4's 32-bit VALU
+// (v_mad_u64_u32 / v_add_co_ci_u32 chains), usable from host code too (__host__ __device__).
+//
+//  * Fq : scalar field, q = 2^252 + 27742317777372353535851937790883648493. Montgomery form with
+//         R = 2^256 over 8 little-endian u32 limbs. Because R is the same as the reference's
+//         (src/scalar/ristretto255.rs:193-199, four u64 limbs), the limb bytes are identical to the
+//         reference's in-memory / serde layout and every result is the unique canonical value in [0,q).
+//         CIOS Montgomery multiplication; q's limbs 4..6 are zero and limb 7 is 2^28, which the
+//         reduction exploits.
+//  * Fp : GF(2^255-19) for curve points. Loose representation in [0, 2^256) with 2^256 = 38 (mod p);
+//         canonicalised only for encoding and comparisons.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SPG_HD __host__ __device__ __forceinline__
+#else
+#define SPG_HD inline
+#endif
+
+namespace spg {
+
+// ---------------------------------------------------------------- carry helpers
+SPG_HD uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+  uint64_t s = (uint64_t)a + b + cin;
+  cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+SPG_HD uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+  uint64_t d = (uint64_t)a - b - bin;
+  bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+// (hi:lo) = a*b + c + d ; never overflows 64 bits
+SPG_HD uint64_t mad(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return (uint64_t)a * b + c + d;
+}
+
+// ================================================================= Fq (Montgomery, R = 2^256)
+struct Fq {
+  uint32_t l[8];
+};
+
+#define SPG_Q0 0x5cf5d3edu
+#define SPG_Q1 0x5812631au
+#define SPG_Q2 0xa2f79cd6u
+#define SPG_Q3 0x14def9deu
+#define SPG_Q7 0x10000000u
+#define SPG_QINV 0x12547e1bu  // -q^{-1} mod 2^32
+
+SPG_HD Fq fq_zero() { Fq r; for (int i = 0; i < 8; i++) r.l[i] = 0; return r; }
+// R mod q = Montgomery one
+SPG_HD Fq fq_one() {
+  Fq r;
+  r.l[0] = 0x8d98951du; r.l[1] = 0xd6ec3174u; r.l[2] = 0x737dcf70u; r.l[3] = 0xc6ef5bf4u;
+  r.l[4] = 0xfffffffeu; r.l[5] = 0xffffffffu; r.l[6] = 0xffffffffu; r.l[7] = 0x0fffffffu;
+  return r;
+}
+SPG_HD Fq fq_r2() {
+  Fq r;
+  r.l[0] = 0x449c0f01u; r.l[1] = 0xa40611e3u; r.l[2] = 0x68859347u; r.l[3] = 0xd00e1ba7u;
+  r.l[4] = 0x17f5be65u; r.l[5] = 0xceec73d2u; r.l[6] = 0x7c309a3du; r.l[7] = 0x0399411bu;
+  return r;
+}
+SPG_HD Fq fq_r3() {
+  Fq r;
+  r.l[0] = 0x7b83a2dbu; r.l[1] = 0x2a9e4968u; r.l[2] = 0xaef7f3ecu; r.l[3] = 0x278324e6u;
+  r.l[4] = 0x04ec5b65u; r.l[5] = 0x8065dc6cu; r.l[6] = 0x3599cec7u; r.l[7] = 0x0e530b77u;
+  return r;
+}
+SPG_HD bool fq_is_zero(const Fq& a) {
+  uint32_t o = 0;
+  for (int i = 0; i < 8; i++) o |= a.l[i];
+  return o == 0;
+}
+SPG_HD bool fq_eq(const Fq& a, const Fq& b) {
+  uint32_t o = 0;
+  for (int i = 0; i < 8; i++) o |= a.l[i] ^ b.l[i];
+  return o == 0;
+}
+
+// t (9 limbs, value < 2q) -> canonical: subtract q if t >= q
+SPG_HD Fq fq_cond_sub(const uint32_t t[8], uint32_t t8) {
+  const uint32_t Q[8] = {SPG_Q0, SPG_Q1, SPG_Q2, SPG_Q3, 0u, 0u, 0u, SPG_Q7};
+  uint32_t d[8], b = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = subb(t[i], Q[i], b, b);
+  // borrow out of the 9-limb subtraction <=> t < q
+  uint32_t b9;
+  subb(t8, 0u, b, b9);
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = b9 ? t[i] : d[i];
+  return r;
+}
+
+SPG_HD Fq fq_add(const Fq& a, const Fq& b) {
+  uint32_t t[8], c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = addc(a.l[i], b.l[i], c, c);
+  return fq_cond_sub(t, c);
+}
+SPG_HD Fq fq_sub(const Fq& a, const Fq& b) {
+  const uint32_t Q[8] = {SPG_Q0, SPG_Q1, SPG_Q2, SPG_Q3, 0u, 0u, 0u, SPG_Q7};
+  uint32_t t[8], bo = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = subb(a.l[i], b.l[i], bo, bo);
+  uint32_t mask = 0u - bo, c = 0;
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = addc(t[i], Q[i] & mask, c, c);
+  return r;
+}
+SPG_HD Fq fq_neg(const Fq& a) { return fq_sub(fq_zero(), a); }
+SPG_HD Fq fq_dbl(const Fq& a) { return fq_add(a, a); }
+
+// CIOS Montgomery product a*b*2^-256 mod q
+SPG_HD Fq fq_mul(const Fq& a, const Fq& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t bi = b.l[i];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint64_t v = mad(a.l[j], bi, t[j], c);
+      t[j] = (uint32_t)v;
+      c = (uint32_t)(v >> 32);
+    }
+    uint32_t c2;
+    t[8] = addc(t[8], c, 0, c2);
+    t[9] = c2;
+    uint32_t m = t[0] * SPG_QINV;
+    uint64_t v = mad(m, SPG_Q0, t[0], 0);
+    c = (uint32_t)(v >> 32);
+    v = mad(m, SPG_Q1, t[1], c); t[0] = (uint32_t)v; c = (uint32_t)(v >> 32);
+    v = mad(m, SPG_Q2, t[2], c); t[1] = (uint32_t)v; c = (uint32_t)(v >> 32);
+    v = mad(m, SPG_Q3, t[3], c); t[2] = (uint32_t)v; c = (uint32_t)(v >> 32);
+    t[3] = addc(t[4], c, 0, c);
+    t[4] = addc(t[5], c, 0, c);
+    t[5] = addc(t[6], c, 0, c);
+    // limb 7 of q is 2^28: m*q7 = m << 28 spread over two limbs
+    uint64_t w = ((uint64_t)m << 28) + t[7] + c;
+    t[6] = (uint32_t)w;
+    c = (uint32_t)(w >> 32);
+    t[7] = addc(t[8], c, 0, c);
+    t[8] = t[9] + c;
+  }
+  return fq_cond_sub(t, t[8]);
+}
+SPG_HD Fq fq_sqr(const Fq& a) { return fq_mul(a, a); }
+// Montgomery -> canonical integer limbs (a * 2^-256 mod q), i.e. Scalar::to_bytes as limbs
+SPG_HD Fq fq_from_mont(const Fq& a) {
+  Fq one;
+  for (int i = 0; i < 8; i++) one.l[i] = 0;
+  one.l[0] = 1;
+  return fq_mul(a, one);
+}
+SPG_HD Fq fq_to_mont(const Fq& a) { return fq_mul(a, fq_r2()); }
+SPG_HD Fq fq_from_u64(uint64_t x) {
+  Fq t = fq_zero();
+  t.l[0] = (uint32_t)x;
+  t.l[1] = (uint32_t)(x >> 32);
+  return fq_to_mont(t);
+}
+// x^(q-2) by 4-bit fixed windows over the exponent
+SPG_HD Fq fq_inv(const Fq& a) {
+  // q - 2 limbs (little-endian u32)
+  const uint32_t E[8] = {SPG_Q0 - 2u, SPG_Q1, SPG_Q2, SPG_Q3, 0u, 0u, 0u, SPG_Q7};
+  Fq tab[16];
+  tab[0] = fq_one();
+  tab[1] = a;
+  for (int i = 2; i < 16; i++) tab[i] = fq_mul(tab[i - 1], a);
+  Fq r = fq_one();
+  for (int i = 63; i >= 0; i--) {
+    r = fq_sqr(fq_sqr(fq_sqr(fq_sqr(r))));
+    uint32_t nib = (E[i >> 3] >> ((i & 7) * 4)) & 15u;
+    if (nib) r = fq_mul(r, tab[nib]);
+  }
+  return r;
+}
+
+// ================================================================= Fp = GF(2^255 - 19)
+struct Fp {
+  uint32_t l[8];
+};
+
+SPG_HD Fp fp_zero() { Fp r; for (int i = 0; i < 8; i++) r.l[i] = 0; return r; }
+SPG_HD Fp fp_one() { Fp r = fp_zero(); r.l[0] = 1; return r; }
+SPG_HD Fp fp_small(uint32_t x) { Fp r = fp_zero(); r.l[0] = x; return r; }
+
+// add c*38 (c small) into t with carry; returns the final carry
+SPG_HD uint32_t fp_fold38(uint32_t t[8], uint32_t c) {
+  uint64_t v = (uint64_t)c * 38u + t[0];
+  t[0] = (uint32_t)v;
+  uint32_t cc = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int i = 1; i < 8; i++) t[i] = addc(t[i], 0, cc, cc);
+  return cc;
+}
+SPG_HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = addc(a.l[i], b.l[i], c, c);
+  c = fp_fold38(r.l, c);
+  fp_fold38(r.l, c);
+  return r;
+}
+SPG_HD Fp fp_sub(const Fp& a, const Fp& b) {
+  Fp r;
+  uint32_t bo = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = subb(a.l[i], b.l[i], bo, bo);
+  // wrapped by 2^256 = 38 (mod p): subtract 38 per wrap (at most twice)
+  uint32_t s = bo * 38u, b2 = 0;
+  r.l[0] = subb(r.l[0], s, 0, b2);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.l[i] = subb(r.l[i], 0, b2, b2);
+  s = b2 * 38u;
+  uint32_t b3 = 0;
+  r.l[0] = subb(r.l[0], s, 0, b3);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.l[i] = subb(r.l[i], 0, b3, b3);
+  return r;
+}
+SPG_HD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
+
+SPG_HD Fp fp_reduce512(uint32_t t[16]) {
+  Fp r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = mad(t[8 + i], 38u, t[i], c);
+    r.l[i] = (uint32_t)v;
+    c = (uint32_t)(v >> 32);
+  }
+  c = fp_fold38(r.l, c);
+  fp_fold38(r.l, c);
+  return r;
+}
+SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint64_t v = mad(a.l[j], b.l[i], t[i + j], c);
+      t[i + j] = (uint32_t)v;
+      c = (uint32_t)(v >> 32);
+    }
+    t[i + 8] = c;
+  }
+  return fp_reduce512(t);
+}
+SPG_HD Fp fp_sqr(const Fp& a) {
+  // off-diagonal products once, doubled, plus the diagonal
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; j++) {
+      uint64_t v = mad(a.l[i], a.l[j], t[i + j], c);
+      t[i + j] = (uint32_t)v;
+      c = (uint32_t)(v >> 32);
+    }
+    t[i + 8] = c;
+  }
+  uint32_t top = 0;
+#pragma unroll
+  for (int i = 1; i < 16; i++) {
+    uint32_t nt = t[i] >> 31;
+    t[i] = (t[i] << 1) | top;
+    top = nt;
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = (uint64_t)a.l[i] * a.l[i];
+    t[2 * i] = addc(t[2 * i], (uint32_t)v, c, c);
+    t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(v >> 32), c, c);
+  }
+  return fp_reduce512(t);
+}
+SPG_HD Fp fp_mul_small(const Fp& a, uint32_t k) {
+  Fp r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = mad(a.l[i], k, c, 0);
+    r.l[i] = (uint32_t)v;
+    c = (uint32_t)(v >> 32);
+  }
+  c = fp_fold38(r.l, c);
+  fp_fold38(r.l, c);
+  return r;
+}
+// canonical representative in [0, p)
+SPG_HD Fp fp_canon(const Fp& a) {
+  Fp r = a;
+  // fold bit 255: v = (v mod 2^255) + 19*(v >> 255)
+  uint32_t top = r.l[7] >> 31;
+  r.l[7] &= 0x7fffffffu;
+  uint32_t c = 0;
+  r.l[0] = addc(r.l[0], top * 19u, 0, c);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.l[i] = addc(r.l[i], 0, c, c);
+  // now r < 2^255 + 19 ; subtract p if r >= p (p = 2^255 - 19)
+  const uint32_t P[8] = {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                         0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu};
+  uint32_t d[8], b = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = subb(r.l[i], P[i], b, b);
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = b ? r.l[i] : d[i];
+  return r;
+}
+SPG_HD bool fp_is_zero(const Fp& a) {
+  Fp c = fp_canon(a);
+  uint32_t o = 0;
+  for (int i = 0; i < 8; i++) o |= c.l[i];
+  return o == 0;
+}
+SPG_HD bool fp_eq(const Fp& a, const Fp& b) { return fp_is_zero(fp_sub(a, b)); }
+SPG_HD bool fp_is_negative(const Fp& a) { return fp_canon(a).l[0] & 1u; }
+SPG_HD Fp fp_cneg(const Fp& a, bool neg) { return neg ? fp_neg(a) : a; }
+SPG_HD Fp fp_abs(const Fp& a) { return fp_cneg(a, fp_is_negative(a)); }
+SPG_HD Fp fp_sqrn(Fp a, int n) {
+  for (int i = 0; i < n; i++) a = fp_sqr(a);
+  return a;
+}
+// a^(2^252 - 3)
+SPG_HD Fp fp_pow22523(const Fp& z) {
+  Fp z2 = fp_sqr(z);
+  Fp z9 = fp_mul(fp_sqrn(z2, 2), z);
+  Fp z11 = fp_mul(z9, z2);
+  Fp z2_5_0 = fp_mul(fp_sqr(z11), z9);
+  Fp z2_10_0 = fp_mul(fp_sqrn(z2_5_0, 5), z2_5_0);
+  Fp z2_20_0 = fp_mul(fp_sqrn(z2_10_0, 10), z2_10_0);
+  Fp z2_40_0 = fp_mul(fp_sqrn(z2_20_0, 20), z2_20_0);
+  Fp z2_50_0 = fp_mul(fp_sqrn(z2_40_0, 10), z2_10_0);
+  Fp z2_100_0 = fp_mul(fp_sqrn(z2_50_0, 50), z2_50_0);
+  Fp z2_200_0 = fp_mul(fp_sqrn(z2_100_0, 100), z2_100_0);
+  Fp z2_250_0 = fp_mul(fp_sqrn(z2_200_0, 50), z2_50_0);
+  return fp_mul(fp_sqrn(z2_250_0, 2), z);
+}
+SPG_HD Fp fp_inv(const Fp& z) {
+  // z^(p-2) = (z^(2^252-3))^8 * z^3
+  Fp t = fp_sqrn(fp_pow22523(z), 3);
+  return fp_mul(t, fp_mul(fp_sqr(z), z));
+}
+SPG_HD Fp fp_from_bytes(const uint8_t b[32]) {
+  Fp r;
+  for (int i = 0; i < 8; i++)
+    r.l[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+             ((uint32_t)b[4 * i + 3] << 24);
+  r.l[7] &= 0x7fffffffu;  // dalek FieldElement::from_bytes ignores the top bit
+  return r;
+}
+SPG_HD void fp_to_bytes(const Fp& a, uint8_t out[32]) {
+  Fp c = fp_canon(a);
+  for (int i = 0; i < 8; i++) {
+    out[4 * i] = (uint8_t)c.l[i];
+    out[4 * i + 1] = (uint8_t)(c.l[i] >> 8);
+    out[4 * i + 2] = (uint8_t)(c.l[i] >> 16);
+    out[4 * i + 3] = (uint8_t)(c.l[i] >> 24);
+  }
+}
+
+}  // namespace spg

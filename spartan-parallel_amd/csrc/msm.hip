@@ -1,0 +1,497 @@
+// spg — generators and multi-scalar multiplication on MI355X (gfx950).
+//
+// Replaces GroupElement::vartime_multiscalar_mul (src/group.rs:98-116), Commitments::commit
+// (src/commitments.rs:69-92), DensePolynomial::commit_inner (src/dense_mlpoly.rs:184-212) and
+// MultiCommitGens::new (src/commitments.rs:15-33).
+//
+// Design (all commitment bases in Spartan are fixed generator sets, so the MSM is fixed-base):
+//   * Every spg_gens keeps, resident in HBM, table[k][i] = 2^k * P_i in affine Niels form for all
+//     bit offsets k < 254 (96 B per entry). A c-bit signed-digit window w of a scalar then selects
+//     table[w*c][i] directly, so all windows of all scalars of one MSM share ONE bucket set of
+//     2^(c-1) buckets and no per-window doublings are needed.
+//   * Pipeline per batch of B MSMs (B Hyrax rows, or B = 1):
+//       k_count   : Montgomery -> canonical, signed c-bit digits, histogram of (msm, |digit|)
+//       scan      : exclusive prefix sums (hipCUB) of counts and of ceil(count / K) work items
+//       k_scatter : counting-sort scatter of (table index | sign) into bucket order
+//       k_items   : one thread per K-entry slice of a bucket: mixed Niels additions (7M each)
+//       k_segments: running sums over bucket segments (sum v * B_v split in 64 segments per MSM)
+//       k_final   : one wave per MSM combines its 64 segments (LDS suffix scan + tree) and encodes
+//     Skewed scalar distributions (0/1-heavy witnesses) only lengthen the item list, never a thread.
+#include <hipcub/hipcub.hpp>
+
+#include <string.h>
+
+#include <vector>
+
+#include "ctx.hpp"
+#include "keccak.hpp"
+
+namespace spg {
+
+static const int kItemK = 16;  // entries summed per work item
+static const int kSegs = 64;   // bucket segments per MSM (one wave in k_final)
+
+// ------------------------------------------------------------------ generators
+__global__ void k_map_uniform(const uint8_t* __restrict__ uni, Niels* __restrict__ out, uint8_t* __restrict__ comp,
+                              int n1) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n1) return;
+  uint8_t b[64];
+  for (int k = 0; k < 64; k++) b[k] = uni[64 * (size_t)i + k];
+  Ext P = ristretto_from_uniform_bytes(b);
+  out[i] = ext_to_niels(P);
+  uint8_t c[32];
+  ext_compress(P, c);
+  for (int k = 0; k < 32; k++) comp[32 * (size_t)i + k] = c[k];
+}
+
+__global__ void k_decompress(const uint8_t* __restrict__ comp, Niels* __restrict__ out, int* __restrict__ bad,
+                             int n1) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n1) return;
+  uint8_t c[32];
+  for (int k = 0; k < 32; k++) c[k] = comp[32 * (size_t)i + k];
+  Ext P;
+  if (!ext_decompress(c, P)) {
+    atomicExch(bad, 1);
+    P = ext_identity();
+  }
+  out[i] = ext_to_niels(P);
+}
+
+__global__ void k_table(const Niels* __restrict__ base, Niels* __restrict__ tab, int n1) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n1 * kTableRows) return;
+  int k = (int)(t / n1), g = (int)(t % n1);
+  Ext P = niels_to_ext(base[g]);
+  for (int j = 0; j < k; j++) P = ext_dbl(P);
+  tab[t] = ext_to_niels(P);
+}
+
+// ------------------------------------------------------------------ MSM kernels
+struct MsmArgs {
+  const Fq* scalars;  // B x n (Montgomery)
+  const Fq* blinds;   // B or null
+  int B, n, n1;       // n scalars per MSM, n1 = gens count incl. h
+  int gen_offset;     // generator index of scalar 0
+  int h_index;        // generator index of h
+  uint32_t* hist;     // B*NB
+  const uint32_t* off;
+  uint32_t* cursor;
+  uint32_t* entries;
+};
+
+// canonical limbs of a Montgomery scalar (Scalar::to_bytes / decompress_scalar, src/scalar/mod.rs:32-36)
+template <int C>
+__device__ __forceinline__ void emit_digits(const Fq& s_mont, int b, uint32_t gidx, int n1, const MsmArgs& a,
+                                            bool count) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  Fq k = fq_from_mont(s_mont);
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int bit = w * C;
+    const int li = bit >> 5, of = bit & 31;
+    uint32_t v = k.l[li] >> of;
+    if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+    int d = (int)(v & MASK) + carry;
+    carry = d > NB ? 1 : 0;
+    d -= carry << C;
+    if (d != 0) {
+      uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+      uint32_t key = (uint32_t)b * NB + (mag - 1);
+      if (count) {
+        atomicAdd(&a.hist[key], 1u);
+      } else {
+        uint32_t slot = a.off[key] + atomicAdd(&a.cursor[key], 1u);
+        uint32_t e = (uint32_t)bit * (uint32_t)n1 + gidx;
+        a.entries[slot] = e | (d < 0 ? 0x80000000u : 0u);
+      }
+    }
+  }
+}
+
+template <int C>
+__global__ void k_digits(MsmArgs a, bool count) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int per = a.n + (a.blinds ? 1 : 0);
+  if (t >= (size_t)a.B * per) return;
+  int b = (int)(t / per), i = (int)(t % per);
+  Fq s;
+  uint32_t gidx;
+  if (i < a.n) {
+    s = a.scalars[(size_t)b * a.n + i];
+    gidx = (uint32_t)(a.gen_offset + i);
+  } else {
+    s = a.blinds[b];
+    gidx = (uint32_t)a.h_index;
+  }
+  emit_digits<C>(s, b, gidx, a.n1, a, count);
+}
+
+__global__ void k_item_counts(const uint32_t* __restrict__ hist, uint32_t* __restrict__ items, int nkeys) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nkeys) return;
+  items[i] = i < nkeys ? (hist[i] + kItemK - 1) / kItemK : 0u;
+}
+
+__global__ void k_item_keys(const uint32_t* __restrict__ item_off, uint32_t* __restrict__ item_key, int nkeys) {
+  int key = blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >= nkeys) return;
+  for (uint32_t it = item_off[key]; it < item_off[key + 1]; it++) item_key[it] = (uint32_t)key;
+}
+
+__device__ __forceinline__ Ext load_signed(const Niels* __restrict__ tab, uint32_t e) {
+  Niels q = tab[e & 0x7fffffffu];
+  if (e >> 31) {
+    Fp t = q.ypx;
+    q.ypx = q.ymx;
+    q.ymx = t;
+    q.t2d = fp_neg(q.t2d);
+  }
+  return niels_to_ext(q);
+}
+
+__global__ void __launch_bounds__(256) k_items(const uint32_t* __restrict__ item_key,
+                                               const uint32_t* __restrict__ item_off,
+                                               const uint32_t* __restrict__ off, const uint32_t* __restrict__ hist,
+                                               const uint32_t* __restrict__ entries, const Niels* __restrict__ tab,
+                                               Ext* __restrict__ partial, const uint32_t* __restrict__ total_items) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= *total_items) return;
+  uint32_t key = item_key[t];
+  uint32_t j = t - item_off[key];
+  uint32_t start = off[key] + j * kItemK;
+  uint32_t end = off[key] + hist[key];
+  if (end > start + kItemK) end = start + kItemK;
+  Ext P = load_signed(tab, entries[start]);
+  for (uint32_t s = start + 1; s < end; s++) {
+    uint32_t e = entries[s];
+    P = ext_madd(P, tab[e & 0x7fffffffu], (e >> 31) != 0);
+  }
+  partial[t] = P;
+}
+
+// thread per (msm, segment): bucket values v in [lo, hi] (1-based), m = NB / kSegs buckets each
+__global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ item_off, const Ext* __restrict__ partial,
+                                                 Ext* __restrict__ segT, Ext* __restrict__ segS, int B, int NB,
+                                                 int m) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  int S = NB / m;
+  if (t >= B * S) return;
+  int b = t / S, j = t % S;
+  int lo = j * m + 1, hi = j * m + m;
+  Ext run = ext_identity(), T = ext_identity();
+  bool any = false;
+  for (int v = hi; v >= lo; v--) {
+    uint32_t key = (uint32_t)b * NB + (v - 1);
+    for (uint32_t it = item_off[key]; it < item_off[key + 1]; it++) {
+      run = any ? ext_add(run, partial[it]) : partial[it];
+      any = true;
+    }
+    if (any) T = ext_add(T, run);
+  }
+  segT[t] = T;
+  segS[t] = run;
+}
+
+// one 64-lane wave per MSM: total = sum_j T_j + m * sum_{j>=1} suffix_j(S)
+__global__ void __launch_bounds__(64) k_final(const Ext* __restrict__ segT, const Ext* __restrict__ segS,
+                                              uint8_t* __restrict__ out, int S, int log2m) {
+  __shared__ Ext sh[kSegs];
+  int b = blockIdx.x, j = threadIdx.x;
+  Ext suf = j < S ? segS[(size_t)b * S + j] : ext_identity();
+  // inclusive suffix scan (Hillis-Steele) over the lanes
+  for (int d = 1; d < S; d <<= 1) {
+    sh[j] = suf;
+    __syncthreads();
+    if (j + d < S) suf = ext_add(suf, sh[j + d]);
+    __syncthreads();
+  }
+  Ext v = j < S ? segT[(size_t)b * S + j] : ext_identity();
+  if (j >= 1 && j < S) {
+    for (int k = 0; k < log2m; k++) suf = ext_dbl(suf);
+    v = ext_add(v, suf);
+  }
+  // tree reduction
+  for (int d = kSegs / 2; d >= 1; d >>= 1) {
+    sh[j] = v;
+    __syncthreads();
+    if (j < d) v = ext_add(v, sh[j + d]);
+    __syncthreads();
+  }
+  if (j == 0) {
+    uint8_t c[32];
+    ext_compress(v, c);
+    for (int k = 0; k < 32; k++) out[32 * (size_t)b + k] = c[k];
+  }
+}
+
+// ------------------------------------------------------------------ host orchestration
+static int pick_window(size_t n_per_msm) {
+  int best = 4;
+  double best_cost = 1e300;
+  for (int c = 4; c <= 16; c++) {
+    int W = 253 / c + 1;
+    double cost = (double)n_per_msm * W * 7.0 + (double)(1 << c) * 9.0;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
+
+template <int C>
+static void launch_digits(const MsmArgs& a, bool count, hipStream_t s) {
+  size_t per = a.n + (a.blinds ? 1 : 0);
+  size_t nt = (size_t)a.B * per;
+  hipLaunchKernelGGL(k_digits<C>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a, count);
+}
+static void dispatch_digits(int c, const MsmArgs& a, bool count, hipStream_t s) {
+  switch (c) {
+    case 4: launch_digits<4>(a, count, s); break;
+    case 5: launch_digits<5>(a, count, s); break;
+    case 6: launch_digits<6>(a, count, s); break;
+    case 7: launch_digits<7>(a, count, s); break;
+    case 8: launch_digits<8>(a, count, s); break;
+    case 9: launch_digits<9>(a, count, s); break;
+    case 10: launch_digits<10>(a, count, s); break;
+    case 11: launch_digits<11>(a, count, s); break;
+    case 12: launch_digits<12>(a, count, s); break;
+    case 13: launch_digits<13>(a, count, s); break;
+    case 14: launch_digits<14>(a, count, s); break;
+    case 15: launch_digits<15>(a, count, s); break;
+    default: launch_digits<16>(a, count, s); break;
+  }
+}
+
+// B MSMs of n scalars each (device pointers), out_dev: B x 32 bytes (device)
+int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                     const Fq* d_blinds, uint8_t* d_out) {
+  hipStream_t s = ctx->stream;
+  const int c = pick_window(n + (d_blinds ? 1 : 0));
+  const int NB = 1 << (c - 1);
+  const int W = 253 / c + 1;
+  const size_t nkeys = B * (size_t)NB;
+  const size_t per = n + (d_blinds ? 1 : 0);
+  const size_t max_entries = B * per * (size_t)W;
+  const size_t max_items = max_entries / kItemK + nkeys + 1;
+  SPG_CHECK(ctx, max_entries < 0x7fffffffULL, "msm batch too large");
+  SPG_CHECK(ctx, (size_t)kTableRows * (g->n + 1) < 0x7fffffffULL, "generator table too large");
+
+  uint32_t* hist = (uint32_t*)ws_get(ctx, 1, (nkeys + 1) * 4);
+  uint32_t* off = (uint32_t*)ws_get(ctx, 2, (nkeys + 1) * 4);
+  uint32_t* cursor = (uint32_t*)ws_get(ctx, 3, (nkeys + 1) * 4);
+  uint32_t* items = (uint32_t*)ws_get(ctx, 4, (nkeys + 1) * 4);
+  uint32_t* item_off = (uint32_t*)ws_get(ctx, 5, (nkeys + 1) * 4);
+  uint32_t* entries = (uint32_t*)ws_get(ctx, 6, max_entries * 4 + 4);
+  uint32_t* item_key = (uint32_t*)ws_get(ctx, 7, max_items * 4);
+  Ext* partial = (Ext*)ws_get(ctx, 8, max_items * sizeof(Ext));
+  const int S = NB < kSegs ? NB : kSegs;
+  const int m = NB / S;
+  int log2m = 0;
+  while ((1 << log2m) < m) log2m++;
+  Ext* segT = (Ext*)ws_get(ctx, 9, B * (size_t)S * sizeof(Ext));
+  Ext* segS = (Ext*)ws_get(ctx, 10, B * (size_t)S * sizeof(Ext));
+  if (!hist || !off || !cursor || !items || !item_off || !entries || !item_key || !partial || !segT || !segS)
+    return set_err(ctx, SPG_E_NOMEM, "msm workspace allocation failed");
+
+  SPG_HIP(ctx, hipMemsetAsync(hist, 0, (nkeys + 1) * 4, s));
+  SPG_HIP(ctx, hipMemsetAsync(cursor, 0, (nkeys + 1) * 4, s));
+
+  MsmArgs a;
+  a.scalars = d_scalars;
+  a.blinds = d_blinds;
+  a.B = (int)B;
+  a.n = (int)n;
+  a.n1 = (int)(g->n + 1);
+  a.gen_offset = (int)gen_offset;
+  a.h_index = (int)g->n;
+  a.hist = hist;
+  a.off = off;
+  a.cursor = cursor;
+  a.entries = entries;
+
+  dispatch_digits(c, a, true, s);
+  SPG_HIP(ctx, hipGetLastError());
+
+  // scans over nkeys+1 entries (hist[nkeys] == 0 so off[nkeys] = total entries)
+  size_t tmp_bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, hist, off, (int)(nkeys + 1), s);
+  void* tmp = ws_get(ctx, 11, tmp_bytes + 16);
+  if (!tmp) return set_err(ctx, SPG_E_NOMEM, "scan workspace");
+  SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hist, off, (int)(nkeys + 1), s));
+  hipLaunchKernelGGL(k_item_counts, dim3((unsigned)((nkeys + 1 + 255) / 256)), dim3(256), 0, s, hist, items,
+                     (int)nkeys);
+  SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, items, item_off, (int)(nkeys + 1), s));
+
+  dispatch_digits(c, a, false, s);
+  hipLaunchKernelGGL(k_item_keys, dim3((unsigned)((nkeys + 255) / 256)), dim3(256), 0, s, item_off, item_key,
+                     (int)nkeys);
+  // the item count is only known on the device: launch the upper bound, threads past item_off[nkeys] exit
+  hipLaunchKernelGGL(k_items, dim3((unsigned)((max_items + 255) / 256)), dim3(256), 0, s, item_key, item_off, off,
+                     hist, entries, g->table, partial, item_off + nkeys);
+  hipLaunchKernelGGL(k_segments, dim3((unsigned)((B * S + 63) / 64)), dim3(64), 0, s, item_off, partial, segT, segS,
+                     (int)B, NB, m);
+  hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(kSegs), 0, s, segT, segS, d_out, S, log2m);
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ generator handles
+static int gens_finish(spg_ctx* ctx, spg_gens* g) {
+  hipStream_t s = ctx->stream;
+  size_t n1 = g->n + 1;
+  size_t tab_entries = n1 * (size_t)kTableRows;
+  SPG_HIP(ctx, hipMalloc(&g->table, tab_entries * sizeof(Niels)));
+  hipLaunchKernelGGL(k_table, dim3((unsigned)((tab_entries + 255) / 256)), dim3(256), 0, s, g->niels, g->table,
+                     (int)n1);
+  SPG_HIP(ctx, hipGetLastError());
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  return 0;
+}
+
+}  // namespace spg
+
+using namespace spg;
+
+extern "C" int spg_gens_derive(spg_ctx* ctx, const uint8_t* label, size_t label_len, size_t n, spg_gens** out) {
+  if (!ctx || !out || (!label && label_len)) return SPG_E_ARG;
+  size_t n1 = n + 1;
+  if (n1 * (size_t)kTableRows >= 0x7fffffffULL) return set_err(ctx, SPG_E_ARG, "too many generators");
+  // SHAKE256(label || basepoint) stream, 64 bytes per point (host; sequential XOF)
+  std::vector<uint8_t> uni(64 * n1);
+  {
+    Shake256 sh;
+    sh.update(label, label_len);
+    static const uint8_t B[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
+                                  0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
+                                  0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
+    sh.update(B, 32);
+    sh.read(uni.data(), uni.size());
+  }
+  spg_gens* g = new spg_gens();
+  g->n = n;
+  g->compressed = new uint8_t[32 * n1];
+  hipStream_t s = ctx->stream;
+  uint8_t* d_uni = nullptr;
+  uint8_t* d_comp = nullptr;
+  if (hipMalloc(&d_uni, uni.size()) != hipSuccess || hipMalloc(&d_comp, 32 * n1) != hipSuccess ||
+      hipMalloc(&g->niels, n1 * sizeof(Niels)) != hipSuccess) {
+    delete g;
+    return set_err(ctx, SPG_E_NOMEM, "gens allocation");
+  }
+  SPG_HIP(ctx, hipMemcpyAsync(d_uni, uni.data(), uni.size(), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_map_uniform, dim3((unsigned)((n1 + 63) / 64)), dim3(64), 0, s, d_uni, g->niels, d_comp,
+                     (int)n1);
+  SPG_HIP(ctx, hipGetLastError());
+  SPG_HIP(ctx, hipMemcpyAsync(g->compressed, d_comp, 32 * n1, hipMemcpyDeviceToHost, s));
+  int rc = gens_finish(ctx, g);
+  hipFree(d_uni);
+  hipFree(d_comp);
+  if (rc) {
+    spg_gens_free(ctx, g);
+    return rc;
+  }
+  *out = g;
+  return SPG_OK;
+}
+
+extern "C" int spg_gens_upload(spg_ctx* ctx, const uint8_t* compressed, size_t n, spg_gens** out) {
+  if (!ctx || !out || !compressed) return SPG_E_ARG;
+  size_t n1 = n + 1;
+  if (n1 * (size_t)kTableRows >= 0x7fffffffULL) return set_err(ctx, SPG_E_ARG, "too many generators");
+  spg_gens* g = new spg_gens();
+  g->n = n;
+  g->compressed = new uint8_t[32 * n1];
+  memcpy(g->compressed, compressed, 32 * n1);
+  hipStream_t s = ctx->stream;
+  uint8_t* d_comp = nullptr;
+  int* d_bad = nullptr;
+  if (hipMalloc(&d_comp, 32 * n1) != hipSuccess || hipMalloc(&d_bad, sizeof(int)) != hipSuccess ||
+      hipMalloc(&g->niels, n1 * sizeof(Niels)) != hipSuccess) {
+    delete g;
+    return set_err(ctx, SPG_E_NOMEM, "gens allocation");
+  }
+  SPG_HIP(ctx, hipMemcpyAsync(d_comp, compressed, 32 * n1, hipMemcpyHostToDevice, s));
+  SPG_HIP(ctx, hipMemsetAsync(d_bad, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_decompress, dim3((unsigned)((n1 + 63) / 64)), dim3(64), 0, s, d_comp, g->niels, d_bad,
+                     (int)n1);
+  int bad = 0;
+  SPG_HIP(ctx, hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  hipFree(d_comp);
+  hipFree(d_bad);
+  if (bad) {
+    spg_gens_free(ctx, g);
+    return set_err(ctx, SPG_E_POINT, "invalid compressed generator");
+  }
+  int rc = gens_finish(ctx, g);
+  if (rc) {
+    spg_gens_free(ctx, g);
+    return rc;
+  }
+  *out = g;
+  return SPG_OK;
+}
+
+extern "C" int spg_gens_download(spg_ctx* ctx, const spg_gens* g, uint8_t* out) {
+  if (!ctx || !g || !out) return SPG_E_ARG;
+  memcpy(out, g->compressed, 32 * (g->n + 1));
+  return SPG_OK;
+}
+
+extern "C" size_t spg_gens_n(const spg_gens* g) { return g ? g->n : 0; }
+
+extern "C" int spg_gens_free(spg_ctx* ctx, spg_gens* g) {
+  (void)ctx;
+  if (!g) return SPG_OK;
+  if (g->niels) hipFree(g->niels);
+  if (g->table) hipFree(g->table);
+  delete[] g->compressed;
+  delete g;
+  return SPG_OK;
+}
+
+static int msm_host(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars, size_t n, size_t B,
+                    const uint64_t* blinds, uint8_t* out) {
+  if (!ctx || !g || !out || (!scalars && n)) return SPG_E_ARG;
+  if (n == 0 && !blinds) {
+    // empty MSM: identity, whose encoding is 32 zero bytes
+    memset(out, 0, 32 * B);
+    return SPG_OK;
+  }
+  if (gen_offset + n > g->n) return set_err(ctx, SPG_E_ARG, "MSM longer than the generator set");
+  hipStream_t s = ctx->stream;
+  size_t sb = B * n * sizeof(Fq);
+  Fq* d_s = (Fq*)ws_get(ctx, 0, sb + B * sizeof(Fq) + B * 32 + 64);
+  if (!d_s) return set_err(ctx, SPG_E_NOMEM, "scalar upload");
+  Fq* d_bl = blinds ? d_s + B * n : nullptr;
+  uint8_t* d_out = (uint8_t*)(d_s + B * n + B);
+  if (n) SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, s));
+  if (blinds) SPG_HIP(ctx, hipMemcpyAsync(d_bl, blinds, B * sizeof(Fq), hipMemcpyHostToDevice, s));
+  timer_start(ctx);
+  int rc = msm_batch_device(ctx, g, gen_offset, d_s, n, B, d_bl, d_out);
+  if (rc) return rc;
+  timer_stop(ctx);
+  SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  ctx->last_us = ms * 1000.0;
+  return SPG_OK;
+}
+
+extern "C" int spg_msm(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont, size_t n,
+                       const uint64_t* blind_mont, uint8_t out[32]) {
+  return msm_host(ctx, g, gen_offset, scalars_mont, n, 1, blind_mont, out);
+}
+
+extern "C" int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* Z_mont, size_t L, size_t R,
+                               const uint64_t* blinds_mont, uint8_t* out) {
+  if (L == 0) return SPG_OK;
+  return msm_host(ctx, g, 0, Z_mont, R, L, blinds_mont, out);
+}

@@ -1,0 +1,133 @@
+"""ctypes binding of libspg.so — the MI355X-native Spartan prover hot path (C-ABI in include/spg.h).
+
+Mirrors the reference crate's seams with the same argument meaning:
+  * Gens(n, label)            ~ MultiCommitGens::new(n, label)          (src/commitments.rs:15-33)
+  * Gens.msm(scalars, blind)  ~ GroupElement::vartime_multiscalar_mul   (src/group.rs:98-116)
+                                + blind * h                              (src/commitments.rs:87-92)
+  * Gens.commit_rows(Z, L, R) ~ DensePolynomial::commit_inner           (src/dense_mlpoly.rs:184-212)
+Scalars are numpy uint64 arrays of shape (..., 4): the reference's Montgomery limbs.
+There is no CPU fallback: constructing a Context without a gfx950 device raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libspg.so")
+
+SPG_ERRORS = {-1: "SPG_E_ARG", -2: "SPG_E_NOMEM", -3: "SPG_E_HIP", -4: "SPG_E_POINT", -5: "SPG_E_NODEVICE"}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libspg.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.spg_last_error.restype = ctypes.c_char_p
+        _lib.spg_last_kernel_us.restype = ctypes.c_double
+        _lib.spg_gens_n.restype = ctypes.c_size_t
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class SpgError(RuntimeError):
+    pass
+
+
+class Context:
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        rc = lib().spg_init(ctypes.c_int(device), ctypes.byref(self._h))
+        if rc != 0:
+            raise SpgError(f"spg_init({device}) failed: {SPG_ERRORS.get(rc, rc)} (no gfx950 device?)")
+
+    def check(self, rc, what):
+        if rc != 0:
+            msg = lib().spg_last_error(self._h).decode(errors="replace")
+            raise SpgError(f"{what}: {SPG_ERRORS.get(rc, rc)}: {msg}")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def last_kernel_us(self):
+        return lib().spg_last_kernel_us(self._h)
+
+    def close(self):
+        if self._h:
+            lib().spg_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _scalars(x):
+    a = np.ascontiguousarray(x, dtype=np.uint64)
+    if a.shape[-1] != 4:
+        a = a.reshape(-1, 4)
+    return a
+
+
+class Gens:
+    """Device-resident MultiCommitGens (G_0..G_{n-1}, h) with fixed-base window tables."""
+
+    def __init__(self, ctx, n, label=None, compressed=None):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        if compressed is not None:
+            comp = np.ascontiguousarray(compressed, dtype=np.uint8).reshape(-1, 32)
+            assert comp.shape[0] == n + 1
+            rc = lib().spg_gens_upload(ctx.handle, _p(comp), ctypes.c_size_t(n), ctypes.byref(self._h))
+            ctx.check(rc, "spg_gens_upload")
+        else:
+            lb = np.frombuffer(bytes(label), dtype=np.uint8).copy() if label else np.zeros(1, np.uint8)
+            rc = lib().spg_gens_derive(ctx.handle, _p(lb), ctypes.c_size_t(len(label or b"")), ctypes.c_size_t(n),
+                                       ctypes.byref(self._h))
+            ctx.check(rc, "spg_gens_derive")
+        self.n = n
+
+    def compressed(self):
+        out = np.zeros((self.n + 1, 32), dtype=np.uint8)
+        self.ctx.check(lib().spg_gens_download(self.ctx.handle, self._h, _p(out)), "spg_gens_download")
+        return out
+
+    def msm(self, scalars, blind=None, gen_offset=0):
+        s = _scalars(scalars)
+        out = np.zeros(32, dtype=np.uint8)
+        bl = None if blind is None else _scalars(blind)
+        rc = lib().spg_msm(self.ctx.handle, self._h, ctypes.c_size_t(gen_offset), _p(s), ctypes.c_size_t(s.shape[0]),
+                           None if bl is None else _p(bl), _p(out))
+        self.ctx.check(rc, "spg_msm")
+        return out.tobytes()
+
+    def commit_rows(self, Z, L, R, blinds=None):
+        z = _scalars(Z)
+        assert z.shape[0] == L * R
+        out = np.zeros((L, 32), dtype=np.uint8)
+        bl = None if blinds is None else _scalars(blinds)
+        rc = lib().spg_commit_rows(self.ctx.handle, self._h, _p(z), ctypes.c_size_t(L), ctypes.c_size_t(R),
+                                   None if bl is None else _p(bl), _p(out))
+        self.ctx.check(rc, "spg_commit_rows")
+        return out
+
+    def free(self):
+        if self._h:
+            lib().spg_gens_free(self.ctx.handle, self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

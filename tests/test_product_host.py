@@ -1,0 +1,119 @@
+"""The product's field / curve / transcript headers (spartan-parallel_amd/csrc/*.hpp) compiled for the
+host (lib/libspg_hostcheck.so) and compared bit-for-bit with the CPU oracle. These are the same
+sources the HIP kernels compile, so a disagreement here is a kernel bug caught without a GPU."""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HC = os.path.join(ROOT, "spartan-parallel_amd", "lib", "libspg_hostcheck.so")
+Q = 2**252 + 27742317777372353535851937790883648493
+P = 2**255 - 19
+
+
+@pytest.fixture(scope="module")
+def hc():
+    if not os.path.exists(HC):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "spartan-parallel_amd"), "lib/libspg_hostcheck.so"])
+    return ctypes.CDLL(HC)
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def rand_fq(oracle, rng, n):
+    return oracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * n, dtype=np.uint8).tobytes())
+
+
+@pytest.mark.parametrize("op,code", [("add", 0), ("sub", 1), ("mul", 2), ("neg", 3), ("square", 4), ("invert", 5)])
+def test_fq_ops(oracle, hc, op, code):
+    rng = np.random.default_rng(code)
+    n = 4000 if code != 5 else 200
+    a, b = rand_fq(oracle, rng, n), rand_fq(oracle, rng, n)
+    a[0] = 0
+    a[1] = oracle.fq_from_u64(1)
+    b[2] = oracle.fq_op("neg", oracle.fq_from_u64(1))[0]
+    if code == 5:
+        a[0] = oracle.fq_from_u64(3)
+    out = np.zeros_like(a)
+    hc.spgh_fq_op(code, _p(a), _p(b), _p(out), ctypes.c_size_t(n))
+    ref = oracle.fq_op(op, a, b) if op in ("add", "sub", "mul") else oracle.fq_op(op, a)
+    assert np.array_equal(out, ref)
+
+
+def test_fq_mont_conversion(oracle, hc):
+    rng = np.random.default_rng(5)
+    a = rand_fq(oracle, rng, 1000)
+    out = np.zeros_like(a)
+    hc.spgh_fq_op(6, _p(a), None, _p(out), ctypes.c_size_t(1000))
+    ref = oracle.fq_to_bytes(a).view(np.uint64).reshape(-1, 4)
+    assert np.array_equal(out, ref)
+
+
+def test_fp_ops_against_bigint(hc):
+    rng = np.random.default_rng(9)
+    n = 2000
+    # loose inputs anywhere in [0, 2^256), including values >= p and near 2^256
+    A = rng.integers(0, 2**32, size=(n, 8), dtype=np.uint64).astype(np.uint32)
+    B = rng.integers(0, 2**32, size=(n, 8), dtype=np.uint64).astype(np.uint32)
+    A[0] = 0xFFFFFFFF
+    B[1] = 0xFFFFFFFF
+    A[2] = np.array([0xFFFFFFED] + [0xFFFFFFFF] * 6 + [0x7FFFFFFF], dtype=np.uint32)  # p
+    B[3] = 0
+    toint = lambda r: sum(int(x) << (32 * i) for i, x in enumerate(r))
+    for code, f in [(0, lambda a, b: (a + b) % P), (1, lambda a, b: (a - b) % P), (2, lambda a, b: a * b % P),
+                    (3, lambda a, b: a * a % P), (5, lambda a, b: a % P)]:
+        out = np.zeros_like(A)
+        hc.spgh_fp_op(code, _p(A), _p(B), _p(out), ctypes.c_size_t(n))
+        for i in range(n):
+            assert toint(out[i]) == f(toint(A[i]), toint(B[i])), (code, i)
+    out = np.zeros_like(A)
+    hc.spgh_fp_op(4, _p(A[4:104]), None, _p(out), ctypes.c_size_t(100))
+    for i in range(100):
+        a = toint(A[4 + i]) % P
+        assert toint(out[i]) == pow(a, P - 2, P)
+
+
+def test_curve_ops(oracle, hc):
+    rng = np.random.default_rng(12)
+    u = rng.integers(0, 256, 64 * 64, dtype=np.uint8)
+    out = np.zeros(32 * 64, np.uint8)
+    hc.spgh_from_uniform(_p(u), _p(out), ctypes.c_size_t(64))
+    ref = oracle.ge_from_uniform_bytes(u.tobytes())
+    assert [out[32 * i:32 * i + 32].tobytes() for i in range(64)] == ref
+    l_minus_1 = (Q - 1).to_bytes(32, "little")
+    for i in range(32):
+        A = np.frombuffer(ref[i], np.uint8).copy()
+        B = np.frombuffer(ref[i + 1], np.uint8).copy()
+        o = np.zeros(32, np.uint8)
+        for op in range(4):
+            assert hc.spgh_point_op(op, _p(A), _p(B), _p(o)) == 1
+            if op in (0, 2):
+                exp = oracle.ge_add(ref[i], ref[i + 1])
+            elif op == 1:
+                exp = oracle.ge_add(ref[i], ref[i])
+            else:
+                exp = oracle.ge_add(ref[i], oracle.ge_scalarmul(ref[i + 1], l_minus_1))
+            assert o.tobytes() == exp
+        assert hc.spgh_niels_roundtrip(_p(A), _p(o)) == 1 and o.tobytes() == ref[i]
+        assert hc.spgh_roundtrip(_p(A), _p(o)) == 1 and o.tobytes() == ref[i]
+    bad = np.frombuffer(b"\x01" + bytes(31), np.uint8).copy()
+    assert hc.spgh_roundtrip(_p(bad), _p(o)) == 0
+
+
+def test_shake_and_merlin(hc):
+    for msg in [b"", b"abc", bytes(range(256)) * 3]:
+        o = np.zeros(400, np.uint8)
+        m = np.frombuffer(msg or b"\0", np.uint8).copy()
+        hc.spgh_shake256(_p(m), ctypes.c_size_t(len(msg)), _p(o), ctypes.c_size_t(400))
+        assert o.tobytes() == hashlib.shake_256(msg).digest(400)
+    o = np.zeros(32, np.uint8)
+    m1 = np.frombuffer(b"some data", np.uint8).copy()
+    hc.spgh_merlin_simple(b"test protocol", b"some label", _p(m1), ctypes.c_size_t(9), b"challenge", _p(o),
+                          ctypes.c_size_t(32))
+    assert o.tobytes().hex() == "d5a21972d0d5fe320c0d263fac7fffb8145aa640af6e9bca177c03c7efcf0615"
