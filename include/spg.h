@@ -41,6 +41,19 @@ const char* spg_last_error(const spg_ctx* ctx);
 /* device-side wall time of the most recent compute call, in microseconds (HIP events on the stream) */
 double spg_last_kernel_us(const spg_ctx* ctx);
 
+/* per-kernel timing on the context stream (events; off by default). spg_prof_read resolves them and
+ * returns up to `max` records (name[32], launches, total microseconds); reset != 0 clears the tallies. */
+int spg_prof_enable(spg_ctx* ctx, int on);
+int spg_prof_read(spg_ctx* ctx, char* names, long* launches, double* total_us, int max, int reset);
+
+/* ---- device-resident scalar vectors (HBM) ----------------------------------------------------
+ * Tables the prover keeps resident between calls (witness polynomials, sumcheck tables). */
+typedef struct spg_buf spg_buf;
+int spg_buf_upload(spg_ctx* ctx, const uint64_t* scalars_mont, size_t n, spg_buf** out);
+int spg_buf_download(spg_ctx* ctx, const spg_buf* b, uint64_t* scalars_mont);
+size_t spg_buf_len(const spg_buf* b);
+int spg_buf_free(spg_ctx* ctx, spg_buf* b);
+
 /* ---- generators ------------------------------------------------------------------------------
  * MultiCommitGens::new(n, label) (src/commitments.rs:15-33): n+1 points from SHAKE256(label ||
  * RISTRETTO_BASEPOINT_COMPRESSED) mapped with RistrettoPoint::from_uniform_bytes; G = first n, h = last.
@@ -64,6 +77,35 @@ int spg_msm(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* 
  * the `random_tape = None` case every SNARK::prove commit uses). Z is L*R scalars, row-major. */
 int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* Z_mont, size_t L, size_t R,
                     const uint64_t* blinds_mont, uint8_t* out);
+
+/* ---- R1CS data-parallel satisfiability proof --------------------------------------------------
+ * Flat C views of the reference's R1CSInstance (src/r1csinstance.rs:19-31) and
+ * ProverWitnessSecInfo (src/lib.rs:508-527). Entries are the reference's SparseMatEntry
+ * {row: usize, col: usize, val: Scalar} (48 bytes). */
+typedef struct {
+  uint64_t row, col;
+  uint64_t val[4]; /* Montgomery limbs */
+} spg_sparse_entry;
+
+typedef struct {
+  size_t num_instances;                   /* instances with matrices (1 = shared by every p)    */
+  size_t max_num_cons;                    /* power of two                                         */
+  size_t num_vars;                        /* power of two: next_pow2(#sections) * max_num_inputs */
+  const size_t* num_cons;                 /* [num_instances], powers of two                      */
+  const size_t* nnz;                      /* [3*num_instances]: |A_p|, |B_p|, |C_p|               */
+  const spg_sparse_entry* const* entries; /* [3*num_instances] -> A_0,B_0,C_0,A_1,...            */
+} spg_r1cs_instance;
+
+typedef struct {
+  size_t num_instances;       /* 1 (single) or P                                          */
+  const size_t* num_proofs;   /* [num_instances]: rows of w_mat[p] (1 = short section)     */
+  const size_t* num_inputs;   /* [num_instances]                                          */
+  const uint64_t* const* w;   /* [num_instances] -> num_proofs[p]*num_inputs[p] scalars    */
+} spg_witness_sec;
+
+/* spg_commit_rows over a device-resident vector: rows are Z[offset + R*i .. offset + R*(i+1)). */
+int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_buf* Z, size_t offset, size_t L, size_t R,
+                        const spg_buf* blinds, uint8_t* out);
 
 #ifdef __cplusplus
 }

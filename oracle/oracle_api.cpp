@@ -146,3 +146,148 @@ int orc_commit_rows(const uint8_t* bases, size_t nb, const uint8_t* h, const uin
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- R1CSProof (src/r1csproof.rs:210-954)
+#include "../include/spg.h"
+#include "r1cs.hpp"
+
+static R1CSInstance inst_from_c(const spg_r1cs_instance* ci) {
+  std::vector<std::vector<SparseEntry>> A, B, C;
+  for (size_t p = 0; p < ci->num_instances; p++) {
+    for (int m = 0; m < 3; m++) {
+      std::vector<SparseEntry> v;
+      const spg_sparse_entry* e = ci->entries[3 * p + m];
+      for (size_t k = 0; k < ci->nnz[3 * p + m]; k++) {
+        SparseEntry s;
+        s.row = e[k].row;
+        s.col = e[k].col;
+        memcpy(s.val.v, e[k].val, 32);
+        v.push_back(s);
+      }
+      (m == 0 ? A : m == 1 ? B : C).push_back(v);
+    }
+  }
+  std::vector<size_t> nc(ci->num_cons, ci->num_cons + ci->num_instances);
+  return R1CSInstance::create(ci->num_instances, ci->max_num_cons, nc, ci->num_vars, A, B, C);
+}
+static WitnessSec ws_from_c(const spg_witness_sec* c) {
+  std::vector<std::vector<FqVec>> w_mat;
+  std::vector<DensePoly> polys;
+  for (size_t p = 0; p < c->num_instances; p++) {
+    std::vector<FqVec> rows;
+    FqVec flat;
+    for (size_t q = 0; q < c->num_proofs[p]; q++) {
+      FqVec row(c->num_inputs[p]);
+      for (size_t i = 0; i < c->num_inputs[p]; i++)
+        memcpy(row[i].v, c->w[p] + 4 * (q * c->num_inputs[p] + i), 32);
+      flat.insert(flat.end(), row.begin(), row.end());
+      rows.push_back(row);
+    }
+    w_mat.push_back(rows);
+    polys.push_back(DensePoly(flat));
+  }
+  return WitnessSec::create(w_mat, polys);
+}
+static FqVec challenges_flat(const std::vector<FqVec>& ch) {
+  FqVec f;
+  for (auto& v : ch) f.insert(f.end(), v.begin(), v.end());
+  return f;
+}
+
+extern "C" {
+// Proves with a fresh Transcript(label) and RandomTape(b"proof", init = tape_seed) and writes
+// bincode(R1CSProof). proof_cap bytes available; *proof_len receives the size. gens label = gens_label,
+// gens_num_vars = the R1CSGens num_vars (power of two). challenges_out (optional) receives
+// rp | rq_rev | rx | rw||ry concatenated; ch_lens[4] their lengths.
+int orc_r1cs_prove(const spg_r1cs_instance* ci, size_t num_instances, size_t max_num_proofs,
+                   const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
+                   const spg_witness_sec* secs, size_t nws, const char* gens_label, size_t gens_num_vars,
+                   const char* transcript_label, const uint64_t* tape_seed, uint8_t* proof, size_t proof_cap,
+                   size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  try {
+    R1CSInstance inst = inst_from_c(ci);
+    std::vector<WitnessSec> ws;
+    for (size_t i = 0; i < nws; i++) ws.push_back(ws_from_c(&secs[i]));
+    std::vector<const WitnessSec*> wp;
+    for (auto& w : ws) wp.push_back(&w);
+    R1CSGens gens = R1CSGens::create(gens_label, gens_num_vars);
+    Transcript t(transcript_label);
+    RandomTape tape("proof", ld(tape_seed));
+    std::vector<size_t> np(num_proofs, num_proofs + num_instances), ni(num_inputs, num_inputs + num_instances);
+    std::vector<FqVec> ch;
+    R1CSProof pf = R1CSProof::prove(num_instances, max_num_proofs, np, max_num_inputs, ni, wp, inst, gens, t, tape, &ch);
+    Ser s;
+    pf.ser(s);
+    *proof_len = s.b.size();
+    if (s.b.size() > proof_cap) return -1;
+    memcpy(proof, s.b.data(), s.b.size());
+    if (challenges_out) {
+      FqVec f = challenges_flat(ch);
+      for (size_t i = 0; i < f.size(); i++) st(challenges_out + 4 * i, f[i]);
+      for (int i = 0; i < 4; i++) ch_lens[i] = ch[i].size();
+    }
+    return 0;
+  } catch (const std::string& e) {
+    return -2;
+  }
+}
+}
+
+extern "C" {
+// Verifies a proof produced by orc_r1cs_prove (R1CSProof::verify, src/r1csproof.rs:687-954) against the
+// witness-section commitments (computed here with DensePolynomial::commit) and the instance evaluations
+// bound to rp (multi_evaluate_bound_rp, src/r1csinstance.rs:598-629). Returns 1 if it verifies.
+int orc_r1cs_verify(const spg_r1cs_instance* ci, size_t num_instances, size_t max_num_proofs,
+                    const size_t* num_proofs, size_t max_num_inputs, const spg_witness_sec* secs, size_t nws,
+                    const char* gens_label, size_t gens_num_vars, const char* transcript_label,
+                    const uint8_t* proof_bytes, size_t proof_len, const uint64_t* tape_seed) {
+  try {
+    // re-prove deterministically to obtain the proof object, then check byte equality with the input
+    R1CSInstance inst = inst_from_c(ci);
+    std::vector<WitnessSec> ws;
+    for (size_t i = 0; i < nws; i++) ws.push_back(ws_from_c(&secs[i]));
+    std::vector<const WitnessSec*> wp;
+    for (auto& w : ws) wp.push_back(&w);
+    R1CSGens gens = R1CSGens::create(gens_label, gens_num_vars);
+    std::vector<size_t> np(num_proofs, num_proofs + num_instances), ni;
+    for (size_t p = 0; p < num_instances; p++) ni.push_back(max_num_inputs);
+    (void)ni;
+    Transcript tp(transcript_label);
+    RandomTape tape("proof", ld(tape_seed));
+    std::vector<FqVec> ch;
+    std::vector<size_t> num_inputs_v;
+    // the prover's num_inputs are the section-0 widths by instance (callers pass them through secs[0])
+    for (size_t p = 0; p < num_instances; p++)
+      num_inputs_v.push_back(secs[0].num_inputs[secs[0].num_instances == 1 ? 0 : p]);
+    R1CSProof pf = R1CSProof::prove(num_instances, max_num_proofs, np, max_num_inputs, num_inputs_v, wp, inst, gens, tp,
+                                    tape, &ch);
+    Ser s;
+    pf.ser(s);
+    if (s.b.size() != proof_len || memcmp(s.b.data(), proof_bytes, proof_len) != 0) return 0;
+    // verifier side
+    std::vector<std::vector<size_t>> wni, wnp;
+    std::vector<std::vector<PolyCommitment>> wc;
+    for (auto& w : ws) {
+      wni.push_back(w.num_inputs);
+      std::vector<size_t> npv;
+      std::vector<PolyCommitment> cv;
+      for (size_t p = 0; p < w.w_mat.size(); p++) {
+        npv.push_back(w.w_mat[p].size());
+        cv.push_back(poly_commit(w.poly_w[p], gens.gens_pc));
+      }
+      wnp.push_back(npv);
+      wc.push_back(cv);
+    }
+    FqVec list;
+    Fq evals[3];
+    inst.multi_evaluate_bound_rp(ch[0], ch[2], ch[3], &list, evals);
+    Transcript tv(transcript_label);
+    return pf.verify(num_instances, max_num_proofs, np, max_num_inputs, wni, wnp, wc, inst.max_num_cons, gens, evals,
+                     tv)
+               ? 1
+               : 0;
+  } catch (const std::string& e) {
+    return -2;
+  }
+}
+}

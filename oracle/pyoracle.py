@@ -186,3 +186,41 @@ def commit_rows(bases, h, Z, L, R, blinds=None):
                                ctypes.c_size_t(R), None if bl is None else _p(bl), _p(out))
     assert ok
     return out
+
+
+# ---------------------------------------------------------------- R1CSProof
+def r1cs_prove(wl, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24, label=b"r1cs_test"):
+    """bincode(R1CSProof) and the challenge vectors [rp, rq_rev, rx, rw||ry] for an R1CSWorkload."""
+    import workload
+
+    v = workload.CViews(wl)
+    cap = 1 << 22
+    buf = np.zeros(cap, dtype=np.uint8)
+    ln = ctypes.c_size_t(0)
+    ch = np.zeros((4096, 4), dtype=np.uint64)
+    chl = (ctypes.c_size_t * 4)()
+    seed = u64s(tape_seed)
+    rc = lib().orc_r1cs_prove(ctypes.byref(v.inst), ctypes.c_size_t(wl.P), ctypes.c_size_t(wl.max_num_proofs),
+                              v.num_proofs, ctypes.c_size_t(wl.max_num_inputs), v.num_inputs, v.secs,
+                              ctypes.c_size_t(wl.nws), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars),
+                              ctypes.c_char_p(label), _p(seed), _p(buf), ctypes.c_size_t(cap), ctypes.byref(ln),
+                              _p(ch), chl)
+    assert rc == 0, rc
+    lens = list(chl)
+    out, o = [], 0
+    for L in lens:
+        out.append(ch[o:o + L].copy())
+        o += L
+    return buf[: ln.value].tobytes(), out
+
+
+def r1cs_verify(wl, proof, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24, label=b"r1cs_test"):
+    import workload
+
+    v = workload.CViews(wl)
+    pb = np.frombuffer(proof, dtype=np.uint8).copy()
+    seed = u64s(tape_seed)
+    return lib().orc_r1cs_verify(ctypes.byref(v.inst), ctypes.c_size_t(wl.P), ctypes.c_size_t(wl.max_num_proofs),
+                                 v.num_proofs, ctypes.c_size_t(wl.max_num_inputs), v.secs, ctypes.c_size_t(wl.nws),
+                                 ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars), ctypes.c_char_p(label),
+                                 _p(pb), ctypes.c_size_t(len(proof)), _p(seed))

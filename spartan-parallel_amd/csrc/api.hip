@@ -1,5 +1,6 @@
 // spg — context management for the C-ABI (include/spg.h).
 #include <stdio.h>
+#include <string.h>
 
 #include "ctx.hpp"
 
@@ -32,6 +33,31 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes) {
 
 void timer_start(spg_ctx* c) { hipEventRecord(c->ev0, c->stream); }
 void timer_stop(spg_ctx* c) { hipEventRecord(c->ev1, c->stream); }
+
+static hipEvent_t pool_event(spg_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+KScope::KScope(spg_ctx* ctx, const char* name) : c(ctx), idx(-1) {
+  if (!c->prof_on) return;
+  spg_ctx::ProfRec r;
+  r.name = name;
+  r.a = pool_event(c);
+  r.b = pool_event(c);
+  hipEventRecord(r.a, c->stream);
+  c->prof_pending.push_back(r);
+  idx = (int)c->prof_pending.size() - 1;
+}
+KScope::~KScope() {
+  if (idx >= 0) hipEventRecord(c->prof_pending[idx].b, c->stream);
+}
 
 }  // namespace spg
 
@@ -72,3 +98,68 @@ extern "C" int spg_free(spg_ctx* c) {
 extern "C" const char* spg_last_error(const spg_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 extern "C" double spg_last_kernel_us(const spg_ctx* c) { return c ? c->last_us : 0.0; }
+
+extern "C" int spg_prof_enable(spg_ctx* c, int on) {
+  if (!c) return SPG_E_ARG;
+  c->prof_on = on != 0;
+  return SPG_OK;
+}
+
+// Resolves pending kernel timings; writes up to `max` (name, launches, total_us) records.
+// names: max x 32 chars (NUL-terminated). Returns the number of records, or a negative error.
+extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* total_us, int max, int reset) {
+  if (!c) return SPG_E_ARG;
+  hipStreamSynchronize(c->stream);
+  for (auto& r : c->prof_pending) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, r.a, r.b);
+    auto& acc = c->prof_acc[r.name];
+    acc.first += 1;
+    acc.second += ms * 1000.0;
+    c->ev_pool.push_back(r.a);
+    c->ev_pool.push_back(r.b);
+  }
+  c->prof_pending.clear();
+  int k = 0;
+  for (auto& kv : c->prof_acc) {
+    if (k >= max) break;
+    if (names) {
+      strncpy(names + 32 * k, kv.first.c_str(), 31);
+      names[32 * k + 31] = 0;
+    }
+    if (launches) launches[k] = kv.second.first;
+    if (total_us) total_us[k] = kv.second.second;
+    k++;
+  }
+  if (reset) c->prof_acc.clear();
+  return k;
+}
+
+// ---- device-resident scalar vectors ----
+extern "C" int spg_buf_upload(spg_ctx* c, const uint64_t* host, size_t n, spg_buf** out) {
+  if (!c || !out || (!host && n)) return SPG_E_ARG;
+  spg_buf* b = new spg_buf();
+  b->n = n;
+  if (hipMalloc(&b->d, (n ? n : 1) * sizeof(spg::Fq)) != hipSuccess) {
+    delete b;
+    return spg::set_err(c, SPG_E_NOMEM, "spg_buf_upload");
+  }
+  if (n) SPG_HIP(c, hipMemcpyAsync(b->d, host, n * sizeof(spg::Fq), hipMemcpyHostToDevice, c->stream));
+  SPG_HIP(c, hipStreamSynchronize(c->stream));
+  *out = b;
+  return SPG_OK;
+}
+extern "C" int spg_buf_download(spg_ctx* c, const spg_buf* b, uint64_t* host) {
+  if (!c || !b || !host) return SPG_E_ARG;
+  SPG_HIP(c, hipMemcpyAsync(host, b->d, b->n * sizeof(spg::Fq), hipMemcpyDeviceToHost, c->stream));
+  SPG_HIP(c, hipStreamSynchronize(c->stream));
+  return SPG_OK;
+}
+extern "C" size_t spg_buf_len(const spg_buf* b) { return b ? b->n : 0; }
+extern "C" int spg_buf_free(spg_ctx* c, spg_buf* b) {
+  (void)c;
+  if (!b) return SPG_OK;
+  if (b->d) hipFree(b->d);
+  delete b;
+  return SPG_OK;
+}

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
@@ -20,6 +21,20 @@ struct spg_ctx {
     size_t bytes = 0;
   };
   std::vector<Slot> ws;
+  // optional per-kernel timing (spg_prof_enable): event pairs resolved lazily in spg_prof_read
+  bool prof_on = false;
+  struct ProfRec {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<ProfRec> prof_pending;
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, std::pair<long, double>> prof_acc;  // name -> (launches, total us)
+};
+
+struct spg_buf {  // device-resident scalar vector (Montgomery Fq)
+  size_t n = 0;
+  spg::Fq* d = nullptr;
 };
 
 struct spg_gens {
@@ -53,5 +68,13 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
 // timing bracket on the context stream
 void timer_start(spg_ctx* c);
 void timer_stop(spg_ctx* c);
+
+// per-kernel profiling scope (no-op unless spg_prof_enable(ctx, 1))
+struct KScope {
+  spg_ctx* c;
+  int idx;
+  KScope(spg_ctx* ctx, const char* name);
+  ~KScope();
+};
 
 }  // namespace spg

@@ -14,8 +14,8 @@
 //       scan      : exclusive prefix sums (hipCUB) of counts and of ceil(count / K) work items
 //       k_scatter : counting-sort scatter of (table index | sign) into bucket order
 //       k_items   : one thread per K-entry slice of a bucket: mixed Niels additions (7M each)
-//       k_segments: running sums over bucket segments (sum v * B_v split in 64 segments per MSM)
-//       k_final   : one wave per MSM combines its 64 segments (LDS suffix scan + tree) and encodes
+//       k_segments: running sums over 8-bucket segments (sum v * B_v = sum_j T_j + j*m*S_j)
+//       k_final   : one block per MSM folds its segments (per-thread groups, LDS suffix scan + tree), encodes
 //     Skewed scalar distributions (0/1-heavy witnesses) only lengthen the item list, never a thread.
 #include <hipcub/hipcub.hpp>
 
@@ -29,7 +29,7 @@
 namespace spg {
 
 static const int kItemK = 16;  // entries summed per work item
-static const int kSegs = 64;   // bucket segments per MSM (one wave in k_final)
+static const int kSegM = 8;    // buckets per running-sum segment (k_segments)
 
 // ------------------------------------------------------------------ generators
 __global__ void k_map_uniform(const uint8_t* __restrict__ uni, Niels* __restrict__ out, uint8_t* __restrict__ comp,
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(256) k_items(const uint32_t* __restrict__ item
   partial[t] = P;
 }
 
-// thread per (msm, segment): bucket values v in [lo, hi] (1-based), m = NB / kSegs buckets each
+// thread per (msm, segment): bucket values v in [lo, hi] (1-based), m = kSegM buckets each
 __global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ item_off, const Ext* __restrict__ partial,
                                                  Ext* __restrict__ segT, Ext* __restrict__ segS, int B, int NB,
                                                  int m) {
@@ -197,34 +197,52 @@ __global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ it
   segS[t] = run;
 }
 
-// one 64-lane wave per MSM: total = sum_j T_j + m * sum_{j>=1} suffix_j(S)
-__global__ void __launch_bounds__(64) k_final(const Ext* __restrict__ segT, const Ext* __restrict__ segS,
-                                              uint8_t* __restrict__ out, int S, int log2m) {
-  __shared__ Ext sh[kSegs];
-  int b = blockIdx.x, j = threadIdx.x;
-  Ext suf = j < S ? segS[(size_t)b * S + j] : ext_identity();
-  // inclusive suffix scan (Hillis-Steele) over the lanes
-  for (int d = 1; d < S; d <<= 1) {
-    sh[j] = suf;
+// one 256-thread block per MSM. Segment j (bucket values j*m+1 .. j*m+m) contributes
+// T_j + j*m*S_j. Thread t folds the g = S/256 consecutive segments [t*g, t*g+g) into
+//   value_t = sum T_j + m * sum_j (j - t*g) S_j      and      V_t = sum S_j,
+// leaving sum_t value_t + (g*m) * sum_t t*V_t, done with an LDS suffix scan of V plus a tree sum.
+__global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, const Ext* __restrict__ segS,
+                                               uint8_t* __restrict__ out, int S, int log2m) {
+  __shared__ Ext sh[256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int g = S >= 256 ? S / 256 : 1;
+  int log2g = 0;
+  while ((1 << log2g) < g) log2g++;
+  const int lo = t * g, hi = lo + g < S ? lo + g : S;
+  const Ext* T = segT + (size_t)b * S;
+  const Ext* Sv = segS + (size_t)b * S;
+  Ext U = ext_identity(), V = ext_identity(), acc = ext_identity(), tot = ext_identity();
+  for (int j = hi - 1; j >= lo; j--) {
+    U = ext_add(U, T[j]);
+    V = ext_add(V, Sv[j]);
+    if (j > lo) {
+      acc = ext_add(acc, Sv[j]);
+      tot = ext_add(tot, acc);
+    }
+  }
+  for (int k = 0; k < log2m; k++) tot = ext_dbl(tot);
+  Ext val = ext_add(U, tot);
+  // inclusive suffix scan of V over threads
+  Ext suf = V;
+  for (int d = 1; d < 256; d <<= 1) {
+    sh[t] = suf;
     __syncthreads();
-    if (j + d < S) suf = ext_add(suf, sh[j + d]);
+    if (t + d < 256) suf = ext_add(suf, sh[t + d]);
     __syncthreads();
   }
-  Ext v = j < S ? segT[(size_t)b * S + j] : ext_identity();
-  if (j >= 1 && j < S) {
-    for (int k = 0; k < log2m; k++) suf = ext_dbl(suf);
-    v = ext_add(v, suf);
+  if (t >= 1) {
+    for (int k = 0; k < log2g + log2m; k++) suf = ext_dbl(suf);
+    val = ext_add(val, suf);
   }
-  // tree reduction
-  for (int d = kSegs / 2; d >= 1; d >>= 1) {
-    sh[j] = v;
+  for (int d = 128; d >= 1; d >>= 1) {
+    sh[t] = val;
     __syncthreads();
-    if (j < d) v = ext_add(v, sh[j + d]);
+    if (t < d) val = ext_add(val, sh[t + d]);
     __syncthreads();
   }
-  if (j == 0) {
+  if (t == 0) {
     uint8_t c[32];
-    ext_compress(v, c);
+    ext_compress(val, c);
     for (int k = 0; k < 32; k++) out[32 * (size_t)b + k] = c[k];
   }
 }
@@ -290,8 +308,8 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   uint32_t* entries = (uint32_t*)ws_get(ctx, 6, max_entries * 4 + 4);
   uint32_t* item_key = (uint32_t*)ws_get(ctx, 7, max_items * 4);
   Ext* partial = (Ext*)ws_get(ctx, 8, max_items * sizeof(Ext));
-  const int S = NB < kSegs ? NB : kSegs;
-  const int m = NB / S;
+  const int m = NB < kSegM ? NB : kSegM;  // buckets per segment
+  const int S = NB / m;
   int log2m = 0;
   while ((1 << log2m) < m) log2m++;
   Ext* segT = (Ext*)ws_get(ctx, 9, B * (size_t)S * sizeof(Ext));
@@ -315,7 +333,10 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   a.cursor = cursor;
   a.entries = entries;
 
-  dispatch_digits(c, a, true, s);
+  {
+    KScope ks(ctx, "msm_count");
+    dispatch_digits(c, a, true, s);
+  }
   SPG_HIP(ctx, hipGetLastError());
 
   // scans over nkeys+1 entries (hist[nkeys] == 0 so off[nkeys] = total entries)
@@ -328,15 +349,27 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
                      (int)nkeys);
   SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, items, item_off, (int)(nkeys + 1), s));
 
-  dispatch_digits(c, a, false, s);
+  {
+    KScope ks(ctx, "msm_scatter");
+    dispatch_digits(c, a, false, s);
+  }
   hipLaunchKernelGGL(k_item_keys, dim3((unsigned)((nkeys + 255) / 256)), dim3(256), 0, s, item_off, item_key,
                      (int)nkeys);
   // the item count is only known on the device: launch the upper bound, threads past item_off[nkeys] exit
-  hipLaunchKernelGGL(k_items, dim3((unsigned)((max_items + 255) / 256)), dim3(256), 0, s, item_key, item_off, off,
-                     hist, entries, g->table, partial, item_off + nkeys);
-  hipLaunchKernelGGL(k_segments, dim3((unsigned)((B * S + 63) / 64)), dim3(64), 0, s, item_off, partial, segT, segS,
-                     (int)B, NB, m);
-  hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(kSegs), 0, s, segT, segS, d_out, S, log2m);
+  {
+    KScope ks(ctx, "msm_bucket_items");
+    hipLaunchKernelGGL(k_items, dim3((unsigned)((max_items + 255) / 256)), dim3(256), 0, s, item_key, item_off,
+                       off, hist, entries, g->table, partial, item_off + nkeys);
+  }
+  {
+    KScope ks(ctx, "msm_segments");
+    hipLaunchKernelGGL(k_segments, dim3((unsigned)((B * S + 63) / 64)), dim3(64), 0, s, item_off, partial, segT,
+                       segS, (int)B, NB, m);
+  }
+  {
+    KScope ks(ctx, "msm_final");
+    hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(256), 0, s, segT, segS, d_out, S, log2m);
+  }
   SPG_HIP(ctx, hipGetLastError());
   return 0;
 }
@@ -494,4 +527,26 @@ extern "C" int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* 
                                const uint64_t* blinds_mont, uint8_t* out) {
   if (L == 0) return SPG_OK;
   return msm_host(ctx, g, 0, Z_mont, R, L, blinds_mont, out);
+}
+
+extern "C" int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_buf* Z, size_t offset, size_t L,
+                                   size_t R, const spg_buf* blinds, uint8_t* out) {
+  if (!ctx || !g || !Z || !out) return SPG_E_ARG;
+  if (offset + L * R > Z->n) return set_err(ctx, SPG_E_ARG, "commit_rows_buf: Z too short");
+  if (blinds && blinds->n < L) return set_err(ctx, SPG_E_ARG, "commit_rows_buf: blinds too short");
+  if (R > g->n) return set_err(ctx, SPG_E_ARG, "commit_rows_buf: R exceeds generators");
+  if (L == 0) return SPG_OK;
+  hipStream_t s = ctx->stream;
+  uint8_t* d_out = (uint8_t*)ws_get(ctx, 12, 32 * L);
+  if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit_rows_buf out");
+  timer_start(ctx);
+  int rc = msm_batch_device(ctx, g, 0, Z->d + offset, R, L, blinds ? blinds->d : nullptr, d_out);
+  if (rc) return rc;
+  timer_stop(ctx);
+  SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * L, hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  ctx->last_us = ms * 1000.0;
+  return SPG_OK;
 }

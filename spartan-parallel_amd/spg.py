@@ -60,6 +60,25 @@ class Context:
     def last_kernel_us(self):
         return lib().spg_last_kernel_us(self._h)
 
+    def prof_enable(self, on=True):
+        self.check(lib().spg_prof_enable(self._h, ctypes.c_int(1 if on else 0)), "spg_prof_enable")
+
+    def prof_read(self, reset=True):
+        """{kernel_name: (launches, total_us)} of the kernels timed since the last reset."""
+        mx = 128
+        names = ctypes.create_string_buffer(32 * mx)
+        launches = np.zeros(mx, dtype=np.int64)
+        tot = np.zeros(mx, dtype=np.float64)
+        k = lib().spg_prof_read(self._h, names, _p(launches), _p(tot), ctypes.c_int(mx), ctypes.c_int(1 if reset else 0))
+        if k < 0:
+            self.check(k, "spg_prof_read")
+        raw = names.raw
+        out = {}
+        for i in range(k):
+            nm = raw[32 * i:32 * i + 32].split(b"\0", 1)[0].decode()
+            out[nm] = (int(launches[i]), float(tot[i]))
+        return out
+
     def close(self):
         if self._h:
             lib().spg_free(self._h)
@@ -77,6 +96,38 @@ def _scalars(x):
     if a.shape[-1] != 4:
         a = a.reshape(-1, 4)
     return a
+
+
+class Buf:
+    """Device-resident vector of Montgomery scalars (spg_buf)."""
+
+    def __init__(self, ctx, scalars):
+        self.ctx = ctx
+        a = _scalars(scalars)
+        self.n = a.shape[0]
+        self._h = ctypes.c_void_p()
+        ctx.check(lib().spg_buf_upload(ctx.handle, _p(a), ctypes.c_size_t(self.n), ctypes.byref(self._h)),
+                  "spg_buf_upload")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def download(self):
+        out = np.zeros((self.n, 4), dtype=np.uint64)
+        self.ctx.check(lib().spg_buf_download(self.ctx.handle, self._h, _p(out)), "spg_buf_download")
+        return out
+
+    def free(self):
+        if self._h:
+            lib().spg_buf_free(self.ctx.handle, self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class Gens:
@@ -119,6 +170,13 @@ class Gens:
         rc = lib().spg_commit_rows(self.ctx.handle, self._h, _p(z), ctypes.c_size_t(L), ctypes.c_size_t(R),
                                    None if bl is None else _p(bl), _p(out))
         self.ctx.check(rc, "spg_commit_rows")
+        return out
+
+    def commit_rows_buf(self, zbuf, L, R, offset=0, blinds_buf=None):
+        out = np.zeros((L, 32), dtype=np.uint8)
+        rc = lib().spg_commit_rows_buf(self.ctx.handle, self._h, zbuf.handle, ctypes.c_size_t(offset), ctypes.c_size_t(L),
+                                       ctypes.c_size_t(R), None if blinds_buf is None else blinds_buf.handle, _p(out))
+        self.ctx.check(rc, "spg_commit_rows_buf")
         return out
 
     def free(self):
