@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark: R1CS constraints/sec of the GPU-resident R1CSProof::prove (libspg.so) on MI355X.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched under
+torch.distributed.run, one rank per GPU. Prints ONE JSON line on rank 0.
+
+Workload (SURVEY.md 8d, config 3 shape): the data-parallel R1CS satisfiability proof that SNARK::prove
+runs for its blocks (src/r1csproof.rs:210-685, called from src/lib.rs:2259-2490): P = 2 block instances,
+X = 2^10 constraints each, Q = 2^9 executions each -> N = 2^20 constraints, synthetic chain-of-squarings
+circuit (spartan-parallel_amd/workload.py). A step is one full R1CSProof::prove with the instance,
+witness and generators already resident in HBM; the proof bytes are produced in every step.
+Multi-GPU: every rank proves its own 2^20-constraint instance (independent proofs, no collective on the
+data path) -> weak scaling; value = all ranks' constraints / max-over-ranks time.
+
+`roofline` is computed for the kernel with the largest device time among those with an algorithmic
+byte model (libspg's per-launch HIP-event timing on the context stream, spg_prof_read), `cpu_baseline`
+is the C++ CPU restatement of the reference (oracle/, 1 thread) on rank 0 at N = 1, which also checks
+that the GPU proof bytes equal the CPU proof bytes on the same workload and seed.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (/opt/skills/guides/MI355X_MICROARCH.md)
+GENS_LABEL = b"gens_r1cs_sat"
+GENS_NUM_VARS = 1 << 24  # TOTAL_NUM_VARS_BOUND = 10^7 -> 2^24 (examples/interface.rs:557-563)
+CONFIGS = {
+    # name: (num_cons per instance, num_proofs per instance, witness sections)
+    "r1cs_2e20": ([1024, 1024], [512, 512], 1),
+    "r1cs_2e16": ([1024, 1024], [32, 32], 1),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="r1cs_2e20", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+                    help="per-launch HBM bytes from rocprofv3 --pmc (scripts/pmc_traffic.py), if present")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+
+    import spg
+    import workload
+
+    nc, npf, nws = CONFIGS[a.config]
+    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, seed=0x5350415254414E31 + rank)
+    seed = workload.tape_seed()
+    ctx = spg.Context(local)
+    gens = spg.R1CSGens(ctx, GENS_LABEL, GENS_NUM_VARS)
+    views = workload.CViews(wl)
+    inst = spg.R1CSInst(ctx, views.inst)
+
+    def upload():
+        return spg.R1CSWitness(ctx, views.secs, wl.nws)
+
+    wit = upload()
+
+    def step():
+        t = spg.Transcript(b"r1cs_bench")
+        tape = spg.RandomTape(b"proof", seed)
+        return spg.r1cs_prove(ctx, gens, inst, wit, wl.P, wl.max_num_proofs, wl.num_proofs, wl.max_num_inputs,
+                              wl.num_inputs, t, tape)
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    sync()
+    ctx.prof_enable(True)
+    ctx.prof_read(reset=True)
+    sync()
+    t0 = time.perf_counter()
+    proofs = set()
+    for _ in range(a.steps):
+        pf, ch = step()
+        proofs.add(hashlib.sha256(pf).hexdigest())
+    sync()
+    dt = time.perf_counter() - t0
+    prof = ctx.prof_read(reset=True)
+    ctx.prof_enable(False)
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    assert len(proofs) == 1, "proof bytes changed between steps"
+
+    # PCIe-inclusive variant: witness upload + prove (reported beside value, never as value)
+    t1 = time.perf_counter()
+    wit = upload()
+    step()
+    t_incl = time.perf_counter() - t1
+
+    N = wl.total_constraints
+    value = N * world * a.steps / dt
+    ms = dt / a.steps * 1e3
+
+    # roofline of the dominant modelled kernel (per-launch average, HIP events on the context stream)
+    modelled = {k: v for k, v in prof.items() if v[2] > 0}
+    dom = max(modelled, key=lambda k: modelled[k][1])
+    launches, us, nbytes = modelled[dom]
+    achieved = (nbytes / launches) / (us / launches * 1e-6) / 1e9
+    traffic = None
+    if os.path.exists(a.traffic):
+        tr = json.load(open(a.traffic))
+        if dom in tr.get("kernels", {}):
+            traffic = tr["kernels"][dom]["hbm_bytes_per_launch"]
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": nbytes / launches, "avg_launch_us": us / launches, "launches": launches}
+    device_ms = sum(v[1] for v in prof.values()) / a.steps / 1e3
+    top = sorted(prof.items(), key=lambda kv: -kv[1][1])[:8]
+    kernels = {k: {"launches_per_step": v[0] / a.steps, "ms_per_step": round(v[1] / a.steps / 1e3, 3),
+                   "GBps": round(v[2] / (v[1] * 1e-6) / 1e9, 1) if v[2] else None} for k, v in top}
+
+    cpu = None
+    bitexact = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle  # the checker / CPU baseline only
+
+        pyoracle.build()
+        tc = time.perf_counter()
+        ref, _ = pyoracle.r1cs_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS,
+                                     label=b"r1cs_bench")
+        tcpu = time.perf_counter() - tc
+        cpu = {"value": round(N / tcpu, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
+               "sample": f"full workload ({N} constraints), one R1CSProof::prove incl. R1CSGens derivation, "
+                         f"{tcpu:.2f} s on 1 host thread"}
+        bitexact = hashlib.sha256(ref).hexdigest() in proofs
+
+    if rank == 0:
+        out = {
+            "metric": "R1CS constraints/sec (SNARK::prove) at 2^20 vars; proof bytes bit-exact",
+            "value": round(value, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255",
+            "data": "synthetic (chain-of-squarings R1CS, seeded), random-tape seed fixed",
+            "config": {"workload": "R1CSProof::prove, block-sat proof of SNARK::prove (src/r1csproof.rs:210-685)",
+                       "num_instances": wl.P, "num_cons": nc, "num_proofs": npf, "witness_sections": nws,
+                       "constraints_per_gpu": N, "max_num_inputs": wl.max_num_inputs,
+                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "proof_bitexact_vs_cpu": bitexact,
+            "proof_sha256": sorted(proofs)[0][:16], "device_busy_ms_per_step": round(device_ms, 3),
+            "value_incl_witness_upload": round(N * world / t_incl, 1), "kernels": kernels,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

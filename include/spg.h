@@ -42,9 +42,10 @@ const char* spg_last_error(const spg_ctx* ctx);
 double spg_last_kernel_us(const spg_ctx* ctx);
 
 /* per-kernel timing on the context stream (events; off by default). spg_prof_read resolves them and
- * returns up to `max` records (name[32], launches, total microseconds); reset != 0 clears the tallies. */
+ * returns up to `max` records (name[32], launches, total microseconds, algorithmic HBM bytes moved
+ * by those launches as modelled in DESIGN.md, 0 where not modelled); reset != 0 clears the tallies. */
 int spg_prof_enable(spg_ctx* ctx, int on);
-int spg_prof_read(spg_ctx* ctx, char* names, long* launches, double* total_us, int max, int reset);
+int spg_prof_read(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, int max, int reset);
 
 /* ---- device-resident scalar vectors (HBM) ----------------------------------------------------
  * Tables the prover keeps resident between calls (witness polynomials, sumcheck tables). */
@@ -106,6 +107,50 @@ typedef struct {
 /* spg_commit_rows over a device-resident vector: rows are Z[offset + R*i .. offset + R*(i+1)). */
 int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_buf* Z, size_t offset, size_t L, size_t R,
                         const spg_buf* blinds, uint8_t* out);
+
+/* ---- Fiat-Shamir transcript and prover randomness (host objects) -----------------------------
+ * ProofTranscript over merlin::Transcript (src/transcript.rs:5-63) and RandomTape
+ * (src/random.rs:7-29). RandomTape::new draws its init scalar from OsRng in the reference; here the
+ * caller supplies it (the one seam that makes proofs reproducible). Labels are NUL-terminated. */
+typedef struct spg_transcript spg_transcript;
+typedef struct spg_random_tape spg_random_tape;
+int spg_transcript_new(const char* label, spg_transcript** out);
+int spg_transcript_append_message(spg_transcript* t, const char* label, const uint8_t* msg, size_t len);
+/* ProofTranscript::append_scalar: label, Scalar::to_bytes (canonical LE) */
+int spg_transcript_append_scalar(spg_transcript* t, const char* label, const uint64_t* scalar_mont);
+/* ProofTranscript::challenge_scalar: from_bytes_wide of 64 challenge bytes */
+int spg_transcript_challenge_scalar(spg_transcript* t, const char* label, uint64_t* out_mont);
+int spg_transcript_challenge_bytes(spg_transcript* t, const char* label, uint8_t* out, size_t len);
+int spg_transcript_free(spg_transcript* t);
+int spg_random_tape_new(const char* name, const uint64_t* init_mont, spg_random_tape** out);
+int spg_random_tape_scalar(spg_random_tape* tp, const char* label, uint64_t* out_mont);
+int spg_random_tape_free(spg_random_tape* tp);
+
+/* ---- R1CSProof::prove (src/r1csproof.rs:210-685) ----------------------------------------------
+ * R1CSGens::new(label, _, num_vars) (src/r1csproof.rs:71-79): gens_pc = PolyCommitmentGens for
+ * log2(num_vars) variables; gens_1 = gens_pc.gens_1, gens_4 = MultiCommitGens::new(4, label). All of
+ * them are prefixes of the same SHAKE256 stream, held once in HBM. */
+typedef struct spg_r1cs_gens spg_r1cs_gens;
+typedef struct spg_r1cs_inst spg_r1cs_inst;
+typedef struct spg_r1cs_witness spg_r1cs_witness;
+int spg_r1cs_gens_new(spg_ctx* ctx, const uint8_t* label, size_t label_len, size_t num_vars, spg_r1cs_gens** out);
+/* *count = number of stream points held; out (optional) receives count x 32 bytes */
+int spg_r1cs_gens_download(spg_ctx* ctx, const spg_r1cs_gens* g, uint8_t* out, size_t* count);
+int spg_r1cs_gens_free(spg_ctx* ctx, spg_r1cs_gens* g);
+/* the R1CSInstance, uploaded once (CSR + merged CSC in HBM) */
+int spg_r1cs_inst_new(spg_ctx* ctx, const spg_r1cs_instance* inst, spg_r1cs_inst** out);
+int spg_r1cs_inst_free(spg_ctx* ctx, spg_r1cs_inst* inst);
+/* the witness sections (Vec<&ProverWitnessSecInfo>), uploaded to HBM */
+int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, spg_r1cs_witness** out);
+int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* w);
+/* R1CSProof::prove(num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs, witness_secs,
+ * inst, gens, transcript, random_tape). Writes bincode(R1CSProof) into proof (proof_cap bytes;
+ * *proof_len = size even when it does not fit) and, when challenges_out != NULL, the returned
+ * challenges rp | rq_rev | rx | rw||ry (Montgomery limbs) with their lengths in ch_lens[4]. */
+int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst, size_t num_instances,
+                   size_t max_num_proofs, const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
+                   const spg_r1cs_witness* witness, spg_transcript* transcript, spg_random_tape* tape,
+                   uint8_t* proof, size_t proof_cap, size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens);
 
 #ifdef __cplusplus
 }

@@ -280,7 +280,12 @@ int orc_r1cs_verify(const spg_r1cs_instance* ci, size_t num_instances, size_t ma
     }
     FqVec list;
     Fq evals[3];
-    inst.multi_evaluate_bound_rp(ch[0], ch[2], ch[3], &list, evals);
+    if (inst.num_instances == 1) {  // R1CSInstance::evaluate, "used if there is only one instance" (r1csinstance.rs:631-641)
+      FqVec e = inst.multi_evaluate(ch[2], ch[3]);
+      for (int i = 0; i < 3; i++) evals[i] = e[i];
+    } else {
+      inst.multi_evaluate_bound_rp(ch[0], ch[2], ch[3], &list, evals);
+    }
     Transcript tv(transcript_label);
     return pf.verify(num_instances, max_num_proofs, np, max_num_inputs, wni, wnp, wc, inst.max_num_cons, gens, evals,
                      tv)

@@ -38,7 +38,7 @@ for (label, n, L, R) in [(b"spg_bench_msm", 1 << 16, 1, 1 << 16), (b"gens_r1cs_s
     prof = ctx.prof_read(reset=True)
     ctx.prof_enable(False)
     print(f"L={L} R={R}: device {np.median(us):.1f} us/call, wall {wall*1e6:.1f} us; points/s {L*R/(np.median(us)*1e-6):.3e}")
-    for k, (c, t) in sorted(prof.items(), key=lambda x: -x[1][1]):
+    for k, (c, t, _b) in sorted(prof.items(), key=lambda x: -x[1][1]):
         print(f"    {k:20s} {t/c:10.1f} us x{c}")
     g.free()
     zb.free()

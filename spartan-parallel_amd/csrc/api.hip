@@ -45,10 +45,11 @@ static hipEvent_t pool_event(spg_ctx* c) {
   return e;
 }
 
-KScope::KScope(spg_ctx* ctx, const char* name) : c(ctx), idx(-1) {
+KScope::KScope(spg_ctx* ctx, const char* name, double bytes) : c(ctx), idx(-1) {
   if (!c->prof_on) return;
   spg_ctx::ProfRec r;
   r.name = name;
+  r.bytes = bytes;
   r.a = pool_event(c);
   r.b = pool_event(c);
   hipEventRecord(r.a, c->stream);
@@ -105,17 +106,19 @@ extern "C" int spg_prof_enable(spg_ctx* c, int on) {
   return SPG_OK;
 }
 
-// Resolves pending kernel timings; writes up to `max` (name, launches, total_us) records.
+// Resolves pending kernel timings; writes up to `max` (name, launches, total_us, bytes) records.
 // names: max x 32 chars (NUL-terminated). Returns the number of records, or a negative error.
-extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* total_us, int max, int reset) {
+extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, int max,
+                             int reset) {
   if (!c) return SPG_E_ARG;
   hipStreamSynchronize(c->stream);
   for (auto& r : c->prof_pending) {
     float ms = 0.f;
     hipEventElapsedTime(&ms, r.a, r.b);
     auto& acc = c->prof_acc[r.name];
-    acc.first += 1;
-    acc.second += ms * 1000.0;
+    acc.launches += 1;
+    acc.us += ms * 1000.0;
+    acc.bytes += r.bytes;
     c->ev_pool.push_back(r.a);
     c->ev_pool.push_back(r.b);
   }
@@ -127,8 +130,9 @@ extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* to
       strncpy(names + 32 * k, kv.first.c_str(), 31);
       names[32 * k + 31] = 0;
     }
-    if (launches) launches[k] = kv.second.first;
-    if (total_us) total_us[k] = kv.second.second;
+    if (launches) launches[k] = kv.second.launches;
+    if (total_us) total_us[k] = kv.second.us;
+    if (bytes) bytes[k] = kv.second.bytes;
     k++;
   }
   if (reset) c->prof_acc.clear();

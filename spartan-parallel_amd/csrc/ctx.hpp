@@ -26,10 +26,15 @@ struct spg_ctx {
   struct ProfRec {
     std::string name;
     hipEvent_t a, b;
+    double bytes;  // algorithmic HBM bytes of the launch (0 = not modelled)
+  };
+  struct ProfAcc {
+    long launches = 0;
+    double us = 0.0, bytes = 0.0;
   };
   std::vector<ProfRec> prof_pending;
   std::vector<hipEvent_t> ev_pool;
-  std::map<std::string, std::pair<long, double>> prof_acc;  // name -> (launches, total us)
+  std::map<std::string, ProfAcc> prof_acc;  // name -> totals
 };
 
 struct spg_buf {  // device-resident scalar vector (Montgomery Fq)
@@ -69,11 +74,17 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
 void timer_start(spg_ctx* c);
 void timer_stop(spg_ctx* c);
 
+// B fixed-base MSMs of n scalars (device pointers) against generator table g; scalar i of MSM b uses
+// generator d_idx[b*n+i] when d_idx is given, else gen_offset + i; d_blinds (B) multiply generator
+// h_index (-1: g->n). d_out: B x 32 compressed bytes (device). Stream-ordered, no host sync.
+int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                     const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index);
+
 // per-kernel profiling scope (no-op unless spg_prof_enable(ctx, 1))
 struct KScope {
   spg_ctx* c;
   int idx;
-  KScope(spg_ctx* ctx, const char* name);
+  KScope(spg_ctx* ctx, const char* name, double bytes = 0.0);
   ~KScope();
 };
 

@@ -1,0 +1,165 @@
+// spg — host-side pieces of the prover: Fiat-Shamir transcript, bincode writer, and the O(1)-size
+// commitments of the sigma protocols (<= 5 fixed generators), which stay on the host because they
+// sit between sequential transcript challenges. Every commitment whose size depends on the input goes
+// through the GPU MSM (msm.hip).
+//
+//   ProofTranscript        src/transcript.rs:5-63   (merlin, keccak.hpp)
+//   RandomTape (seedable)  src/random.rs:7-29
+//   Scalar byte codecs     src/scalar/ristretto255.rs:391-466
+#pragma once
+#include <string.h>
+
+#include <map>
+#include <vector>
+
+#include "curve.hpp"
+#include "keccak.hpp"
+
+namespace spg {
+
+typedef std::vector<Fq> FqV;
+
+struct Pt {
+  uint8_t b[32];
+  bool operator==(const Pt& o) const { return memcmp(b, o.b, 32) == 0; }
+};
+
+inline void fq_le_bytes(const Fq& a, uint8_t out[32]) {
+  Fq c = fq_from_mont(a);
+  for (int i = 0; i < 8; i++)
+    for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(c.l[i] >> (8 * k));
+}
+// Scalar::from_bytes_wide: d0 * R2 + d1 * R3 (ristretto255.rs:449-466)
+inline Fq fq_from_wide(const uint8_t b[64]) {
+  Fq d0, d1;
+  for (int i = 0; i < 8; i++) {
+    d0.l[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+              ((uint32_t)b[4 * i + 3] << 24);
+    d1.l[i] = (uint32_t)b[32 + 4 * i] | ((uint32_t)b[33 + 4 * i] << 8) | ((uint32_t)b[34 + 4 * i] << 16) |
+              ((uint32_t)b[35 + 4 * i] << 24);
+  }
+  return fq_add(fq_mul(d0, fq_r2()), fq_mul(d1, fq_r3()));
+}
+inline Fq fq_u64(uint64_t x) { return fq_from_u64(x); }
+
+struct Writer {
+  std::vector<uint8_t> out;
+  void u64(uint64_t x) {
+    for (int i = 0; i < 8; i++) out.push_back((uint8_t)(x >> (8 * i)));
+  }
+  void fq(const Fq& a) {  // serde of Scalar([u64;4]): the Montgomery limbs
+    for (int i = 0; i < 8; i++)
+      for (int k = 0; k < 4; k++) out.push_back((uint8_t)(a.l[i] >> (8 * k)));
+  }
+  void pt(const Pt& p) { out.insert(out.end(), p.b, p.b + 32); }
+  void fqs(const FqV& v) {
+    u64(v.size());
+    for (auto& a : v) fq(a);
+  }
+  void pts(const std::vector<Pt>& v) {
+    u64(v.size());
+    for (auto& p : v) pt(p);
+  }
+};
+
+struct Tr {
+  Merlin m;
+  explicit Tr(const char* label) : m(label) {}
+  void msg(const char* label, const char* s) { m.message(label, s, strlen(s)); }
+  void protocol(const char* name) { msg("protocol-name", name); }
+  void scalar(const char* label, const Fq& a) {
+    uint8_t b[32];
+    fq_le_bytes(a, b);
+    m.message(label, b, 32);
+  }
+  void point(const char* label, const Pt& p) { m.message(label, p.b, 32); }
+  void u64(const char* label, uint64_t x) {
+    uint8_t b[8];
+    for (int i = 0; i < 8; i++) b[i] = (uint8_t)(x >> (8 * i));
+    m.message(label, b, 8);
+  }
+  Fq challenge(const char* label) {
+    uint8_t b[64];
+    m.challenge(label, b, 64);
+    return fq_from_wide(b);
+  }
+  FqV challenges(const char* label, size_t n) {
+    FqV v;
+    for (size_t i = 0; i < n; i++) v.push_back(challenge(label));
+    return v;
+  }
+  void scalars(const char* label, const FqV& v) {  // [Scalar]::append_to_transcript
+    msg(label, "begin_append_vector");
+    for (auto& a : v) scalar(label, a);
+    msg(label, "end_append_vector");
+  }
+};
+
+struct Tape {
+  Tr t;
+  Tape(const char* name, const Fq& init) : t(name) { t.scalar("init_randomness", init); }
+  Fq scalar(const char* label) { return t.challenge(label); }
+  FqV vec(const char* label, size_t n) { return t.challenges(label, n); }
+};
+
+inline Pt compress(const Ext& p) {
+  Pt c;
+  ext_compress(p, c.b);
+  return c;
+}
+
+// Fixed-base host scalar multiplication: table[w][j] = j * 2^(8w) * P, 32 windows of 8 bits.
+struct FixedBase {
+  std::vector<Ext> tab;  // 32 * 256
+  void build(const Ext& P) {
+    tab.assign(32 * 256, ext_identity());
+    Ext base = P;
+    for (int w = 0; w < 32; w++) {
+      tab[w * 256 + 1] = base;
+      for (int j = 2; j < 256; j++) tab[w * 256 + j] = ext_add(tab[w * 256 + j - 1], base);
+      for (int k = 0; k < 8; k++) base = ext_dbl(base);
+    }
+  }
+  // acc += k * P   (k Montgomery)
+  void mul_add(Ext& acc, bool& started, const Fq& k) const {
+    uint8_t b[32];
+    fq_le_bytes(k, b);
+    for (int w = 0; w < 32; w++) {
+      if (!b[w]) continue;
+      const Ext& e = tab[w * 256 + b[w]];
+      acc = started ? ext_add(acc, e) : e;
+      started = true;
+    }
+  }
+};
+
+// Host view of a generator set for the sigma protocols: fixed-base tables for a few indices.
+struct HostGens {
+  std::map<size_t, FixedBase> fb;
+  std::vector<uint8_t> comp;  // compressed stream points (index -> 32 bytes); decompressed on first use
+  void init(const uint8_t* compressed, size_t count) { comp.assign(compressed, compressed + 32 * count); }
+  const FixedBase& get(size_t idx) {
+    auto it = fb.find(idx);
+    if (it != fb.end()) return it->second;
+    Ext P;
+    ext_decompress(comp.data() + 32 * idx, P);
+    FixedBase& f = fb[idx];
+    f.build(P);
+    return f;
+  }
+  // sum_i s_i * P_{idx_i}
+  Ext msm(const std::vector<size_t>& idx, const FqV& s) {
+    Ext acc = ext_identity();
+    bool started = false;
+    for (size_t i = 0; i < idx.size(); i++) get(idx[i]).mul_add(acc, started, s[i]);
+    return acc;
+  }
+};
+
+// variable-base scalar multiplication (k Montgomery), used once per ProductProof (gens_X)
+inline Ext var_mul(const Ext& P, const Fq& k) {
+  Fq c = fq_from_mont(k);
+  return ext_scalar_mul(P, c.l);
+}
+
+}  // namespace spg

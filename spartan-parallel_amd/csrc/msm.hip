@@ -75,6 +75,7 @@ struct MsmArgs {
   int B, n, n1;       // n scalars per MSM, n1 = gens count incl. h
   int gen_offset;     // generator index of scalar 0
   int h_index;        // generator index of h
+  const uint32_t* idx;  // optional: explicit generator index per scalar (B x n), overrides gen_offset
   uint32_t* hist;     // B*NB
   const uint32_t* off;
   uint32_t* cursor;
@@ -123,7 +124,7 @@ __global__ void k_digits(MsmArgs a, bool count) {
   uint32_t gidx;
   if (i < a.n) {
     s = a.scalars[(size_t)b * a.n + i];
-    gidx = (uint32_t)(a.gen_offset + i);
+    gidx = a.idx ? a.idx[(size_t)b * a.n + i] : (uint32_t)(a.gen_offset + i);
   } else {
     s = a.blinds[b];
     gidx = (uint32_t)a.h_index;
@@ -288,7 +289,7 @@ static void dispatch_digits(int c, const MsmArgs& a, bool count, hipStream_t s) 
 
 // B MSMs of n scalars each (device pointers), out_dev: B x 32 bytes (device)
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
-                     const Fq* d_blinds, uint8_t* d_out) {
+                     const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index) {
   hipStream_t s = ctx->stream;
   const int c = pick_window(n + (d_blinds ? 1 : 0));
   const int NB = 1 << (c - 1);
@@ -327,7 +328,8 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   a.n = (int)n;
   a.n1 = (int)(g->n + 1);
   a.gen_offset = (int)gen_offset;
-  a.h_index = (int)g->n;
+  a.h_index = h_index < 0 ? (int)g->n : (int)h_index;
+  a.idx = d_idx;
   a.hist = hist;
   a.off = off;
   a.cursor = cursor;
@@ -507,7 +509,7 @@ static int msm_host(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const ui
   if (n) SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, s));
   if (blinds) SPG_HIP(ctx, hipMemcpyAsync(d_bl, blinds, B * sizeof(Fq), hipMemcpyHostToDevice, s));
   timer_start(ctx);
-  int rc = msm_batch_device(ctx, g, gen_offset, d_s, n, B, d_bl, d_out);
+  int rc = msm_batch_device(ctx, g, gen_offset, d_s, n, B, d_bl, d_out, nullptr, -1);
   if (rc) return rc;
   timer_stop(ctx);
   SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, s));
@@ -540,7 +542,7 @@ extern "C" int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_bu
   uint8_t* d_out = (uint8_t*)ws_get(ctx, 12, 32 * L);
   if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit_rows_buf out");
   timer_start(ctx);
-  int rc = msm_batch_device(ctx, g, 0, Z->d + offset, R, L, blinds ? blinds->d : nullptr, d_out);
+  int rc = msm_batch_device(ctx, g, 0, Z->d + offset, R, L, blinds ? blinds->d : nullptr, d_out, nullptr, -1);
   if (rc) return rc;
   timer_stop(ctx);
   SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * L, hipMemcpyDeviceToHost, s));

@@ -1,0 +1,119 @@
+// spg — prover-side protocol objects and their bincode encoding (serde derive order of the reference):
+//   KnowledgeProof / EqualityProof / ProductProof / DotProductProof  src/nizk/mod.rs:16-404
+//   DotProductProofLog + BulletReductionProof                          src/nizk/mod.rs:420-523, bullet.rs:32-132
+//   PolyEvalProof                                                       src/dense_mlpoly.rs:427-1130
+//   ZKSumcheckInstanceProof / SumcheckInstanceProof                     src/sumcheck.rs:28-92
+//   R1CSProof                                                           src/r1csproof.rs:24-43
+#pragma once
+#include <vector>
+
+#include "ctx.hpp"
+#include "host.hpp"
+
+namespace spg {
+
+struct KnowledgeProofP {
+  Pt alpha;
+  Fq z1, z2;
+  void ser(Writer& w) const { w.pt(alpha); w.fq(z1); w.fq(z2); }
+};
+struct EqualityProofP {
+  Pt alpha;
+  Fq z;
+  void ser(Writer& w) const { w.pt(alpha); w.fq(z); }
+};
+struct ProductProofP {
+  Pt alpha, beta, delta;
+  Fq z[5];
+  void ser(Writer& w) const {
+    w.pt(alpha); w.pt(beta); w.pt(delta);
+    for (int i = 0; i < 5; i++) w.fq(z[i]);
+  }
+};
+struct DotProductProofP {
+  Pt delta, beta;
+  FqV z;
+  Fq z_delta, z_beta;
+  void ser(Writer& w) const { w.pt(delta); w.pt(beta); w.fqs(z); w.fq(z_delta); w.fq(z_beta); }
+};
+struct DotProductProofLogP {
+  std::vector<Pt> L, R;
+  Pt delta, beta;
+  Fq z1, z2;
+  void ser(Writer& w) const { w.pts(L); w.pts(R); w.pt(delta); w.pt(beta); w.fq(z1); w.fq(z2); }
+};
+struct ZKSumcheckP {
+  std::vector<Pt> comm_polys, comm_evals;
+  std::vector<DotProductProofP> proofs;
+  void ser(Writer& w) const {
+    w.pts(comm_polys);
+    w.pts(comm_evals);
+    w.u64(proofs.size());
+    for (auto& p : proofs) p.ser(w);
+  }
+};
+struct SumcheckP {
+  std::vector<FqV> polys;  // compressed: coefficients except the linear term
+  void ser(Writer& w) const {
+    w.u64(polys.size());
+    for (auto& p : polys) w.fqs(p);
+  }
+};
+struct R1CSProofP {
+  ZKSumcheckP sc1;
+  Pt claims_phase2[4];
+  KnowledgeProofP pok;
+  ProductProofP prod;
+  EqualityProofP eq1;
+  ZKSumcheckP sc2;
+  std::vector<std::vector<Pt>> comm_vars_at_ry_list;
+  Pt comm_vars_at_ry;
+  std::vector<DotProductProofLogP> evals;
+  EqualityProofP eq2;
+  void ser(Writer& w) const {
+    sc1.ser(w);
+    for (int i = 0; i < 4; i++) w.pt(claims_phase2[i]);
+    pok.ser(w);
+    prod.ser(w);
+    eq1.ser(w);
+    sc2.ser(w);
+    w.u64(comm_vars_at_ry_list.size());
+    for (auto& v : comm_vars_at_ry_list) w.pts(v);
+    w.pt(comm_vars_at_ry);
+    w.u64(evals.size());
+    for (auto& e : evals) e.ser(w);
+    eq2.ser(w);
+  }
+};
+
+// A commitment key inside one derived generator stream: G indices + h index (MultiCommitGens view).
+struct KeyView {
+  std::vector<size_t> G;
+  size_t h;
+};
+
+// Generators of one label: device handle (all stream points, window tables) + host fixed-base tables.
+struct ProverGens {
+  spg_gens* dev = nullptr;  // stream points 0 .. count-1
+  HostGens host;
+  size_t n_pc = 0;          // DotProductProofGens n (gens_pc.gens.gens_n.n)
+  KeyView gens_n, gens_1, gens_4;
+};
+
+// ---- sigma protocols (host; O(1) points) ----
+Ext commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& blind);
+KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C);
+EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& v1, const Fq& s1,
+                              const Fq& v2, const Fq& s2);
+ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& rX, const Fq& y,
+                            const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z);
+DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyView& kn, Tr& t, Tape& tape, const FqV& x,
+                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y);
+// ---- DotProductProofLog with all MSMs on the GPU over the original generators ----
+int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const FqV& x, const Fq& blind_x, const FqV& a,
+                         const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy);
+// device MSMs of B x n scalars over explicit generator indices (host buffers), outputs B points
+int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars, const std::vector<std::vector<uint32_t>>& idx,
+                   std::vector<Pt>* out);
+
+}  // namespace spg

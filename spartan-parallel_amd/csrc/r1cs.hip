@@ -1,0 +1,1078 @@
+// spg — R1CSProof::prove (src/r1csproof.rs:210-685) with every O(N) table resident in HBM.
+//
+// Device work (HIP, this file + sumcheck.hip + msm.hip):
+//   z_mat assembly into the (p, q_rev, w, x_rev) Z layout        r1csproof.rs:278-293, custom_dense_mlpoly.rs:67-111
+//   multiply_vec_block (CSR SpMV for A, B, C at once)             r1csinstance.rs:363-436, sparse_mlpoly.rs:454-472
+//   phase-1 / phase-2 round evaluation and folds                  sumcheck.rs:1067-1380, :788-1065
+//   compute_eval_table_sparse_disjoint_rounds (CSC, eq-weighted)  r1csinstance.rs:484-534, sparse_mlpoly.rs:524-541
+//   bound_poly_vars_rq on Z                                       custom_dense_mlpoly.rs:300-304
+//   DensePolynomial::bound / evaluate of the witness sections     dense_mlpoly.rs:258-265, :361-367
+//   Bulletproof L/R/delta MSMs                                    proto.hip
+// Host work: the Fiat-Shamir transcript, the round polynomials (4 scalars), the sigma protocols over
+// <= 5 fixed generators, and the bincode writer. Per sumcheck round exactly three scalars come back.
+#include "proto.hpp"
+#include "sumcheck.hpp"
+
+struct spg_transcript {
+  spg::Tr t;
+  explicit spg_transcript(const char* l) : t(l) {}
+};
+struct spg_random_tape {
+  spg::Tape t;
+  spg_random_tape(const char* n, const spg::Fq& s) : t(n, s) {}
+};
+struct spg_r1cs_gens {
+  spg::ProverGens g;
+};
+
+// R1CSInstance resident in HBM: per matrix instance p, CSR of A_p, B_p, C_p (SpMV) and one merged CSC
+// (rows tagged 0/1/2) for the transposed eq-weighted product.
+struct spg_r1cs_inst {
+  size_t num_instances = 0, max_num_cons = 0, num_vars = 0;
+  std::vector<size_t> num_cons;
+  std::vector<uint64_t> rp_off, cp_off;  // [3p+m] offsets into rowptr ; [p] offsets into colptr
+  std::vector<size_t> nnz;               // [3p+m]
+  uint32_t* d_rowptr = nullptr;          // absolute entry indices
+  uint32_t* d_col = nullptr;
+  spg::Fq* d_val = nullptr;
+  uint32_t* d_colptr = nullptr;
+  uint32_t* d_crow = nullptr;            // row * 4 + tag
+  spg::Fq* d_cval = nullptr;
+};
+
+// ProverWitnessSecInfo list resident in HBM: w_mat[p] flattened (q-major), sections concatenated.
+struct spg_r1cs_witness {
+  size_t nws = 0;
+  std::vector<std::vector<size_t>> num_proofs, num_inputs;  // [w][p]
+  std::vector<std::vector<uint64_t>> off;                   // [w][p] element offset into d_w
+  spg::Fq* d_w = nullptr;
+  size_t total = 0;
+};
+
+namespace spg {
+
+// ------------------------------------------------------------------------------------ kernels
+__device__ __forceinline__ uint32_t brev(uint32_t v, uint32_t lg) { return lg ? (__brev(v) >> (32 - lg)) : 0u; }
+
+template <class D>
+__device__ __forceinline__ int find_desc(const D* d, int P, uint64_t t) {
+  int lo = 0, hi = P - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (d[mid].dom_off <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+struct ZDesc {
+  uint64_t dom_off, z_off;
+  uint32_t lg_q, ni, lg_ni, pad;
+};
+struct SecDesc {
+  uint64_t off;
+  uint32_t np, ni;
+};
+
+// Z[p][q_rev][w][x_rev] = w_mat_w[pw][qw][x]  (zero beyond the section's width)
+__global__ void k_z_fill(const ZDesc* __restrict__ zd, int P, const SecDesc* __restrict__ sd, int nws,
+                         const Fq* __restrict__ wbuf, Fq* __restrict__ Z, uint64_t total) {
+  uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  int p = find_desc(zd, P, t);
+  const ZDesc d = zd[p];
+  uint64_t loc = t - d.dom_off;
+  uint32_t i = (uint32_t)(loc % d.ni);
+  uint64_t rest = loc / d.ni;
+  uint32_t w = (uint32_t)(rest % nws), q = (uint32_t)(rest / nws);
+  const SecDesc s = sd[(size_t)w * P + p];
+  Fq v = fq_zero();
+  if (i < s.ni) v = wbuf[s.off + (size_t)(s.np == 1 ? 0 : q) * s.ni + i];
+  Z[d.z_off + ((size_t)brev(q, d.lg_q) * nws + w) * d.ni + brev(i, d.lg_ni)] = v;
+}
+
+struct SpDesc {
+  uint64_t dom_off, out_off, z_off;
+  uint32_t pi, lg_q, nrows, lg_rows, ni, lg_ni;
+};
+struct MatDesc {
+  uint64_t rp[3];
+  uint64_t cp;
+};
+
+// Az/Bz/Cz[p][q_rev][x_rev] = sum_e val_e * z[p][q][col_e / Y][col_e % Y]
+__global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int P, const MatDesc* __restrict__ md,
+                                              const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
+                                              const Fq* __restrict__ val, const Fq* __restrict__ Z, int nws, uint32_t Y,
+                                              Fq* __restrict__ Az, Fq* __restrict__ Bz, Fq* __restrict__ Cz,
+                                              uint64_t total) {
+  uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  int p = find_desc(sd, P, t);
+  const SpDesc d = sd[p];
+  uint64_t loc = t - d.dom_off;
+  uint32_t row = (uint32_t)(loc % d.nrows), q = (uint32_t)(loc / d.nrows);
+  uint32_t qr = brev(q, d.lg_q);
+  const Fq* zq = Z + d.z_off + (size_t)qr * nws * d.ni;
+  size_t o = d.out_off + (size_t)qr * d.nrows + brev(row, d.lg_rows);
+  Fq* outs[3] = {Az, Bz, Cz};
+#pragma unroll
+  for (int m = 0; m < 3; m++) {
+    const uint32_t* rp = rowptr + md[d.pi].rp[m];
+    uint32_t e0 = rp[row], e1 = rp[row + 1];
+    Fq s = fq_zero();
+    for (uint32_t e = e0; e < e1; e++) {
+      uint32_t c = col[e];
+      uint32_t w = c / Y, i = c % Y;
+      if (w < (uint32_t)nws && i < d.ni) s = fq_add(s, fq_mul(val[e], zq[(size_t)w * d.ni + brev(i, d.lg_ni)]));
+    }
+    outs[m][o] = s;
+  }
+}
+
+struct AbcDesc {
+  uint64_t dom_off, out_off;
+  uint32_t pi, ni, lg_ni, pad;
+};
+
+// ABC[p][w][x_rev] = sum_{M in A,B,C} r_M * sum_{e in M_p, col_e = w*Y + x} eq_rx[row_e] * val_e
+__global__ void __launch_bounds__(256) k_abc(const AbcDesc* __restrict__ ad, int Pm, const MatDesc* __restrict__ md,
+                                             const uint32_t* __restrict__ colptr, const uint32_t* __restrict__ crow,
+                                             const Fq* __restrict__ cval, const Fq* __restrict__ eq, uint32_t Y,
+                                             Fq rA, Fq rB, Fq rC, Fq* __restrict__ ABC, uint64_t total) {
+  uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  int p = find_desc(ad, Pm, t);
+  const AbcDesc d = ad[p];
+  uint64_t loc = t - d.dom_off;
+  uint32_t i = (uint32_t)(loc % d.ni), w = (uint32_t)(loc / d.ni);
+  const uint32_t* cp = colptr + md[d.pi].cp;
+  uint32_t c = w * Y + i;
+  Fq acc[3] = {fq_zero(), fq_zero(), fq_zero()};
+  for (uint32_t e = cp[c]; e < cp[c + 1]; e++) {
+    uint32_t rt = crow[e];
+    Fq v = fq_mul(cval[e], eq[rt >> 2]);
+    uint32_t tag = rt & 3;
+    if (tag == 0) acc[0] = fq_add(acc[0], v);
+    else if (tag == 1) acc[1] = fq_add(acc[1], v);
+    else acc[2] = fq_add(acc[2], v);
+  }
+  Fq r = fq_add(fq_add(fq_mul(rA, acc[0]), fq_mul(rB, acc[1])), fq_mul(rC, acc[2]));
+  ABC[d.out_off + (size_t)w * d.ni + brev(i, d.lg_ni)] = r;
+}
+
+// DensePolynomial::bound: out[i] = sum_j L[j] * Z[j * Rs + i], split over gridDim.y chunks of j
+__global__ void __launch_bounds__(256) k_bound_part(const Fq* __restrict__ Z, const Fq* __restrict__ L, uint32_t Ls,
+                                                    uint32_t Rs, uint32_t chunk, Fq* __restrict__ part) {
+  uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Rs) return;
+  uint32_t j0 = blockIdx.y * chunk, j1 = min(Ls, j0 + chunk);
+  Fq acc = fq_zero();
+  for (uint32_t j = j0; j < j1; j++) acc = fq_add(acc, fq_mul(L[j], Z[(size_t)j * Rs + i]));
+  part[(size_t)blockIdx.y * Rs + i] = acc;
+}
+__global__ void k_sum_cols(const Fq* __restrict__ part, uint32_t S, uint32_t Rs, Fq* __restrict__ out) {
+  uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Rs) return;
+  Fq acc = fq_zero();
+  for (uint32_t y = 0; y < S; y++) acc = fq_add(acc, part[(size_t)y * Rs + i]);
+  out[i] = acc;
+}
+
+// ------------------------------------------------------------------------------------ host helpers
+static size_t lg2(size_t x) {  // src/math.rs:14-21 (rounds up)
+  size_t r = 0;
+  while (((size_t)1 << r) < x) r++;
+  return r;
+}
+static size_t npow2(size_t x) {
+  size_t r = 1;
+  while (r < x) r <<= 1;
+  return r;
+}
+static bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
+
+// EqPolynomial::evals (dense_mlpoly.rs:76-92)
+static FqV eq_evals_host(const FqV& r) {
+  FqV e((size_t)1 << r.size(), fq_one());
+  size_t size = 1;
+  for (size_t j = 0; j < r.size(); j++) {
+    size *= 2;
+    for (size_t i = size - 1;; i -= 2) {
+      Fq s = e[i / 2];
+      e[i] = fq_mul(s, r[j]);
+      e[i - 1] = fq_sub(s, e[i]);
+      if (i < 2) break;
+    }
+  }
+  return e;
+}
+// DensePolynomial::new(z).evaluate(r) for short host vectors
+static Fq dense_eval_host(FqV z, const FqV& r) {
+  z.resize((size_t)1 << r.size(), fq_zero());
+  FqV chi = eq_evals_host(r);
+  Fq s = fq_zero();
+  for (size_t i = 0; i < z.size(); i++) s = fq_add(s, fq_mul(z[i], chi[i]));
+  return s;
+}
+
+// UniPoly::from_evals for degree 3 (unipoly.rs:23-54) and evaluate (:72-80)
+static FqV uni_from_evals3(const Fq e[4]) {
+  static const Fq two_inv = fq_inv(fq_from_u64(2)), six_inv = fq_inv(fq_from_u64(6));
+  Fq d = e[0];
+  Fq three_e1 = fq_add(fq_add(e[1], e[1]), e[1]), three_e2 = fq_add(fq_add(e[2], e[2]), e[2]);
+  Fq a = fq_mul(six_inv, fq_sub(fq_add(fq_sub(e[3], three_e2), three_e1), e[0]));
+  Fq four_e2 = fq_dbl(fq_dbl(e[2]));
+  Fq five_e1 = fq_add(fq_dbl(fq_dbl(e[1])), e[1]);
+  Fq b = fq_mul(two_inv, fq_sub(fq_add(fq_sub(fq_dbl(e[0]), five_e1), four_e2), e[3]));
+  Fq c = fq_sub(fq_sub(fq_sub(e[1], d), a), b);
+  return {d, c, b, a};
+}
+static Fq uni_eval(const FqV& c, const Fq& r) {
+  Fq ev = c[0], pw = r;
+  for (size_t i = 1; i < c.size(); i++) {
+    ev = fq_add(ev, fq_mul(pw, c[i]));
+    pw = fq_mul(pw, r);
+  }
+  return ev;
+}
+
+// ZK sumcheck round bookkeeping shared by phase 1 and phase 2 (sumcheck.rs:1247-1370)
+struct ZKRounds {
+  FqV blinds_poly, blinds_evals;
+  Fq claim, blind_claim;
+  Pt comm_claim;
+  ZKSumcheckP out;
+  FqV poly;
+  void init(ProverGens& g, Tape& tape, size_t rounds, const Fq& c, const Fq& b) {
+    blinds_poly = tape.vec("blinds_poly", rounds);
+    blinds_evals = tape.vec("blinds_evals", rounds);
+    claim = c;
+    blind_claim = b;
+    comm_claim = compress(commit_host(g, g.gens_1, {c}, b));
+  }
+  // commit the round polynomial and draw r_j
+  Fq begin(ProverGens& g, Tr& t, size_t j, const Fq e[3]) {
+    Fq ev[4] = {e[0], fq_sub(claim, e[0]), e[1], e[2]};
+    poly = uni_from_evals3(ev);
+    Pt cp = compress(commit_host(g, g.gens_4, poly, blinds_poly[j]));
+    t.point("comm_poly", cp);
+    out.comm_polys.push_back(cp);
+    return t.challenge("challenge_nextround");
+  }
+  void finish(ProverGens& g, Tr& t, Tape& tape, size_t j, const Fq& r_j) {
+    Fq eval = uni_eval(poly, r_j);
+    Pt comm_eval = compress(commit_host(g, g.gens_1, {eval}, blinds_evals[j]));
+    t.point("comm_claim_per_round", comm_claim);
+    t.point("comm_eval", comm_eval);
+    FqV w = t.challenges("combine_two_claims_to_one", 2);
+    Fq target = fq_add(fq_mul(w[0], claim), fq_mul(w[1], eval));
+    Fq blind_sc = j == 0 ? blind_claim : blinds_evals[j - 1];
+    Fq blind = fq_add(fq_mul(w[0], blind_sc), fq_mul(w[1], blinds_evals[j]));
+    size_t n = poly.size();
+    FqV a(n);
+    Fq pw = fq_one();
+    for (size_t k = 0; k < n; k++) {
+      Fq a_sc = k == 0 ? fq_dbl(fq_one()) : fq_one();
+      a[k] = fq_add(fq_mul(w[0], a_sc), fq_mul(w[1], pw));
+      pw = fq_mul(pw, r_j);
+    }
+    out.proofs.push_back(dotproduct_prove(g, g.gens_1, g.gens_4, t, tape, poly, blinds_poly[j], a, target, blind));
+    claim = eval;
+    comm_claim = comm_eval;
+    out.comm_evals.push_back(comm_eval);
+  }
+};
+
+static int d2h_fq(spg_ctx* ctx, const Fq* d, Fq* h, size_t n = 1) {
+  SPG_HIP(ctx, hipMemcpyAsync(h, d, n * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+static unsigned blocks_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+// device eq table of a host vector (uploads through the kernel argument)
+static int eq_table(spg_ctx* ctx, const FqV& r, Fq* out) { return dev_eq_table(ctx, r.data(), (int)r.size(), out); }
+
+// workspace slots used here (msm.hip uses 0..12, proto.hip 20..22)
+enum {
+  WS_AZ = 30, WS_BZ, WS_CZ, WS_Z, WS_ABC, WS_TP, WS_TQ, WS_TX, WS_EQRX, WS_EQP, WS_PART, WS_OUT3, WS_DESC,
+  WS_L, WS_BPART, WS_BOUT
+};
+
+struct Prover {
+  spg_ctx* ctx;
+  ProverGens& g;
+  const spg_r1cs_inst& inst;
+  const spg_r1cs_witness& wit;
+  size_t P, max_np, Y, nws;
+  std::vector<size_t> num_proofs, num_inputs;
+  Tr& t;
+  Tape& tape;
+  R1CSProofP pf;
+  std::vector<FqV> challenges;
+  // device descriptor staging (kept alive until the stream is synchronised)
+  std::vector<uint8_t> desc_host;
+
+  Prover(spg_ctx* c, ProverGens& gg, const spg_r1cs_inst& in, const spg_r1cs_witness& w, Tr& tt, Tape& tp)
+      : ctx(c), g(gg), inst(in), wit(w), t(tt), tape(tp) {}
+
+  template <class D>
+  int upload_desc(const std::vector<D>& v, size_t byte_off, D** dptr) {
+    uint8_t* base = (uint8_t*)ws_get(ctx, WS_DESC, 1 << 20);
+    if (!base) return set_err(ctx, SPG_E_NOMEM, "descriptor buffer");
+    size_t bytes = v.size() * sizeof(D);
+    if (byte_off + bytes > (1 << 20)) return set_err(ctx, SPG_E_ARG, "too many descriptors");
+    if (desc_host.size() < byte_off + bytes) desc_host.resize(byte_off + bytes);
+    memcpy(desc_host.data() + byte_off, v.data(), bytes);
+    SPG_HIP(ctx, hipMemcpyAsync(base + byte_off, desc_host.data() + byte_off, bytes, hipMemcpyHostToDevice,
+                                ctx->stream));
+    *dptr = (D*)(base + byte_off);
+    return 0;
+  }
+
+  int run();
+};
+
+int Prover::run() {
+  hipStream_t s = ctx->stream;
+  t.protocol("R1CS proof");
+  size_t num_cons = inst.max_num_cons;
+  std::vector<size_t> block_num_cons(P);
+  for (size_t p = 0; p < P; p++) block_num_cons[p] = inst.num_cons[inst.num_instances == 1 ? 0 : p];
+  size_t np = lg2(npow2(P)), nq = lg2(max_np), nx = lg2(num_cons), nw = lg2(nws), ny = lg2(Y);
+
+  // ---- Z table (p, q_rev, w, x_rev)
+  PqxDev Zp;
+  Zp.zlen = P;
+  Zp.off.resize(P);
+  Zp.anp = num_proofs;
+  Zp.anw.assign(P, nws);
+  Zp.ani = num_inputs;
+  size_t ztot = 0;
+  for (size_t p = 0; p < P; p++) {
+    Zp.off[p] = ztot;
+    ztot += num_proofs[p] * nws * num_inputs[p];
+  }
+  Zp.total = ztot;
+  Zp.num_instances = npow2(P);
+  Zp.max_num_proofs = max_np;
+  Zp.num_witness_secs = npow2(nws);
+  Zp.max_num_inputs = Y;
+  Zp.num_proofs = num_proofs;
+  Zp.num_inputs = num_inputs;
+  Zp.d = (Fq*)ws_get(ctx, WS_Z, ztot * sizeof(Fq) + 64);
+  if (!Zp.d) return set_err(ctx, SPG_E_NOMEM, "Z table");
+  {
+    std::vector<ZDesc> zd(P);
+    std::vector<SecDesc> sd(nws * P);
+    for (size_t p = 0; p < P; p++) {
+      zd[p].dom_off = Zp.off[p];
+      zd[p].z_off = Zp.off[p];
+      zd[p].lg_q = (uint32_t)lg2(num_proofs[p]);
+      zd[p].ni = (uint32_t)num_inputs[p];
+      zd[p].lg_ni = (uint32_t)lg2(num_inputs[p]);
+      for (size_t w = 0; w < nws; w++) {
+        size_t pw = wit.num_proofs[w].size() == 1 ? 0 : p;
+        sd[w * P + p].off = wit.off[w][pw];
+        sd[w * P + p].np = (uint32_t)wit.num_proofs[w][pw];
+        sd[w * P + p].ni = (uint32_t)wit.num_inputs[w][pw];
+      }
+    }
+    ZDesc* dz;
+    SecDesc* ds;
+    int rc = upload_desc(zd, 0, &dz);
+    if (!rc) rc = upload_desc(sd, 65536, &ds);
+    if (rc) return rc;
+    KScope ks(ctx, "z_fill", 64.0 * ztot);
+    hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, s, dz, (int)P, ds, (int)nws, wit.d_w, Zp.d,
+                       (uint64_t)ztot);
+    SPG_HIP(ctx, hipGetLastError());
+  }
+
+  // ---- tau tables
+  FqV tau_p = t.challenges("challenge_tau_p", np);
+  FqV tau_q = t.challenges("challenge_tau_q", nq);
+  FqV tau_x = t.challenges("challenge_tau_x", nx);
+  Fq* Ap = (Fq*)ws_get(ctx, WS_TP, (sizeof(Fq) << np) + 64);
+  Fq* Aq = (Fq*)ws_get(ctx, WS_TQ, (sizeof(Fq) << nq) + 64);
+  Fq* Ax = (Fq*)ws_get(ctx, WS_TX, (sizeof(Fq) << nx) + 64);
+  if (!Ap || !Aq || !Ax) return set_err(ctx, SPG_E_NOMEM, "eq tables");
+  int rc = eq_table(ctx, tau_p, Ap);
+  if (!rc) rc = eq_table(ctx, tau_q, Aq);
+  if (!rc) rc = eq_table(ctx, tau_x, Ax);
+  if (rc) return rc;
+
+  // ---- Az, Bz, Cz = multiply_vec_block (p, q_rev, 0, x_rev)
+  PqxDev Az;
+  Az.zlen = P;
+  Az.off.resize(P);
+  Az.anp = num_proofs;
+  Az.anw.assign(P, 1);
+  Az.ani = block_num_cons;
+  size_t atot = 0;
+  for (size_t p = 0; p < P; p++) {
+    Az.off[p] = atot;
+    atot += num_proofs[p] * block_num_cons[p];
+  }
+  Az.total = atot;
+  Az.num_instances = npow2(P);
+  Az.max_num_proofs = max_np;
+  Az.num_witness_secs = 1;
+  Az.max_num_inputs = num_cons;
+  Az.num_proofs = num_proofs;
+  Az.num_inputs = block_num_cons;
+  Az.d = (Fq*)ws_get(ctx, WS_AZ, atot * sizeof(Fq) + 64);
+  Fq* Bz = (Fq*)ws_get(ctx, WS_BZ, atot * sizeof(Fq) + 64);
+  Fq* Cz = (Fq*)ws_get(ctx, WS_CZ, atot * sizeof(Fq) + 64);
+  if (!Az.d || !Bz || !Cz) return set_err(ctx, SPG_E_NOMEM, "Az/Bz/Cz");
+  std::vector<MatDesc> md(inst.num_instances);
+  for (size_t p = 0; p < inst.num_instances; p++) {
+    for (int m = 0; m < 3; m++) md[p].rp[m] = inst.rp_off[3 * p + m];
+    md[p].cp = inst.cp_off[p];
+  }
+  MatDesc* dmd;
+  rc = upload_desc(md, 2 * 65536, &dmd);
+  if (rc) return rc;
+  {
+    std::vector<SpDesc> sd(P);
+    for (size_t p = 0; p < P; p++) {
+      sd[p].dom_off = Az.off[p];
+      sd[p].out_off = Az.off[p];
+      sd[p].z_off = Zp.off[p];
+      sd[p].pi = (uint32_t)(inst.num_instances == 1 ? 0 : p);
+      sd[p].lg_q = (uint32_t)lg2(num_proofs[p]);
+      sd[p].nrows = (uint32_t)block_num_cons[p];
+      sd[p].lg_rows = (uint32_t)lg2(block_num_cons[p]);
+      sd[p].ni = (uint32_t)num_inputs[p];
+      sd[p].lg_ni = (uint32_t)lg2(num_inputs[p]);
+    }
+    SpDesc* dsd;
+    rc = upload_desc(sd, 3 * 65536, &dsd);
+    if (rc) return rc;
+    // outputs, CSR row pointers, and per visited entry its column, value and z gather
+    double visits = 0;
+    for (size_t p = 0; p < P; p++) {
+      size_t pi = inst.num_instances == 1 ? 0 : p;
+      visits += (double)num_proofs[p] * (inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2]);
+    }
+    KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
+    hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)P, dmd, inst.d_rowptr, inst.d_col,
+                       inst.d_val, Zp.d, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
+    SPG_HIP(ctx, hipGetLastError());
+  }
+
+  Fq* partials = (Fq*)ws_get(ctx, WS_PART, 3 * 1024 * sizeof(Fq) + 64);
+  Fq* d_out3 = (Fq*)ws_get(ctx, WS_OUT3, 4 * sizeof(Fq) + 64);
+  if (!partials || !d_out3) return set_err(ctx, SPG_E_NOMEM, "partials");
+
+  // ---- phase 1 (sumcheck.rs:1067-1380)
+  FqV rx_all;
+  Fq blind_post1;
+  Fq claims1[4];
+  {
+    size_t rounds = nx + nq + np;
+    ZKRounds zk;
+    zk.init(g, tape, rounds, fq_zero(), fq_zero());
+    size_t cons_len = (size_t)1 << nx, proof_len = (size_t)1 << nq, instance_len = (size_t)1 << np;
+    size_t lenP = instance_len, lenQ = proof_len, lenX = cons_len;
+    std::vector<size_t> sc_np = num_proofs, sc_nc = block_num_cons;
+    for (size_t j = 0; j < rounds; j++) {
+      int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
+      if (cons_len > 1) cons_len /= 2;
+      else if (proof_len > 1) proof_len /= 2;
+      else instance_len /= 2;
+      for (size_t p = 0; p < std::min(instance_len, sc_np.size()); p++) {
+        if (mode == MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
+        if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
+      }
+      Fq e[3];
+      rc = phase1_eval(ctx, Az, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap, Aq, Ax, Az.d, Bz, Cz,
+                       partials, d_out3, e);
+      if (rc) return rc;
+      Fq r_j = zk.begin(g, t, j, e);
+      if (mode == MODE_P) { rc = dev_fold_top(ctx, Ap, lenP, r_j); lenP /= 2; }
+      else if (mode == MODE_Q) { rc = dev_fold_top(ctx, Aq, lenQ, r_j); lenQ /= 2; }
+      else { rc = dev_fold_top(ctx, Ax, lenX, r_j); lenX /= 2; }
+      if (!rc) rc = pqx_bound(ctx, Az, Bz, Cz, r_j, mode);
+      if (rc) return rc;
+      zk.finish(g, t, tape, j, r_j);
+      rx_all.push_back(r_j);
+    }
+    Fq a[3];
+    rc = d2h_fq(ctx, Ap, &a[0]);
+    if (!rc) rc = d2h_fq(ctx, Aq, &a[1]);
+    if (!rc) rc = d2h_fq(ctx, Ax, &a[2]);
+    if (!rc) rc = d2h_fq(ctx, Az.d, &claims1[1]);
+    if (!rc) rc = d2h_fq(ctx, Bz, &claims1[2]);
+    if (!rc) rc = d2h_fq(ctx, Cz, &claims1[3]);
+    if (rc) return rc;
+    claims1[0] = fq_mul(fq_mul(a[0], a[1]), a[2]);
+    blind_post1 = zk.blinds_evals[rounds - 1];
+    pf.sc1 = std::move(zk.out);
+  }
+  Fq tau_claim = claims1[0], Az_claim = claims1[1], Bz_claim = claims1[2], Cz_claim = claims1[3];
+  Fq Az_blind = tape.scalar("Az_blind"), Bz_blind = tape.scalar("Bz_blind"), Cz_blind = tape.scalar("Cz_blind"),
+     prod_blind = tape.scalar("prod_Az_Bz_blind");
+  Pt comm_Cz, comm_Az, comm_Bz, comm_prod;
+  pf.pok = knowledge_prove(g, g.gens_1, t, tape, Cz_claim, Cz_blind, &comm_Cz);
+  Fq prod = fq_mul(Az_claim, Bz_claim);
+  pf.prod = product_prove(g, g.gens_1, t, tape, Az_claim, Az_blind, Bz_claim, Bz_blind, prod, prod_blind, &comm_Az,
+                          &comm_Bz, &comm_prod);
+  t.point("comm_Az_claim", comm_Az);
+  t.point("comm_Bz_claim", comm_Bz);
+  t.point("comm_Cz_claim", comm_Cz);
+  t.point("comm_prod_Az_Bz_claims", comm_prod);
+  Fq blind_expected1 = fq_mul(tau_claim, fq_sub(prod_blind, Cz_blind));
+  Fq claim_post1 = fq_mul(fq_sub(prod, Cz_claim), tau_claim);
+  pf.eq1 = equality_prove(g, g.gens_1, t, tape, claim_post1, blind_expected1, claim_post1, blind_post1);
+  FqV rx_rev(rx_all.begin(), rx_all.begin() + nx), rq_rev(rx_all.begin() + nx, rx_all.begin() + nx + nq),
+      rp(rx_all.begin() + nx + nq, rx_all.end());
+  FqV rx(rx_rev.rbegin(), rx_rev.rend()), rq(rq_rev.rbegin(), rq_rev.rend());
+
+  // ---- phase 2 inputs
+  Fq r_A = t.challenge("challenge_Az"), r_B = t.challenge("challenge_Bz"), r_C = t.challenge("challenge_Cz");
+  Fq claim2 = fq_add(fq_add(fq_mul(r_A, Az_claim), fq_mul(r_B, Bz_claim)), fq_mul(r_C, Cz_claim));
+  Fq blind2 = fq_add(fq_add(fq_mul(r_A, Az_blind), fq_mul(r_B, Bz_blind)), fq_mul(r_C, Cz_blind));
+  Fq* eq_rx = (Fq*)ws_get(ctx, WS_EQRX, (sizeof(Fq) << nx) + 64);
+  if (!eq_rx) return set_err(ctx, SPG_E_NOMEM, "eq(rx)");
+  rc = eq_table(ctx, rx, eq_rx);
+  if (rc) return rc;
+  size_t Pm = inst.num_instances;
+  PqxDev ABC;
+  ABC.zlen = Pm;
+  ABC.off.resize(Pm);
+  ABC.anp.assign(Pm, 1);
+  ABC.anw.assign(Pm, nws);
+  ABC.ani.assign(num_inputs.begin(), num_inputs.begin() + Pm);
+  size_t btot = 0;
+  for (size_t p = 0; p < Pm; p++) {
+    ABC.off[p] = btot;
+    btot += nws * num_inputs[p];
+  }
+  ABC.total = btot;
+  ABC.num_instances = npow2(Pm);
+  ABC.max_num_proofs = 1;
+  ABC.num_witness_secs = npow2(nws);
+  ABC.max_num_inputs = Y;
+  ABC.num_proofs.assign(P, 1);
+  ABC.num_inputs = num_inputs;
+  ABC.d = (Fq*)ws_get(ctx, WS_ABC, btot * sizeof(Fq) + 64);
+  if (!ABC.d) return set_err(ctx, SPG_E_NOMEM, "ABC");
+  {
+    std::vector<AbcDesc> ad(Pm);
+    for (size_t p = 0; p < Pm; p++) {
+      ad[p].dom_off = ABC.off[p];
+      ad[p].out_off = ABC.off[p];
+      ad[p].pi = (uint32_t)p;
+      ad[p].ni = (uint32_t)num_inputs[p];
+      ad[p].lg_ni = (uint32_t)lg2(num_inputs[p]);
+    }
+    AbcDesc* dad;
+    rc = upload_desc(ad, 4 * 65536, &dad);
+    if (rc) return rc;
+    double visits = 0;
+    for (size_t p = 0; p < Pm; p++) visits += inst.nnz[3 * p] + inst.nnz[3 * p + 1] + inst.nnz[3 * p + 2];
+    KScope ks(ctx, "eval_table_abc", 32.0 * btot + 4.0 * btot + 68.0 * visits);
+    hipLaunchKernelGGL(k_abc, dim3(blocks_for(btot)), dim3(256), 0, s, dad, (int)Pm, dmd, inst.d_colptr, inst.d_crow,
+                       inst.d_cval, eq_rx, (uint32_t)Y, r_A, r_B, r_C, ABC.d, (uint64_t)btot);
+    SPG_HIP(ctx, hipGetLastError());
+  }
+  for (size_t k = 0; k < rq_rev.size(); k++) {  // Z.bound_poly_vars_rq(rq_rev)
+    rc = pqx_bound(ctx, Zp, nullptr, nullptr, rq_rev[k], MODE_Q);
+    if (rc) return rc;
+  }
+  Fq* eq_p = (Fq*)ws_get(ctx, WS_EQP, (sizeof(Fq) << np) + 64);
+  if (!eq_p) return set_err(ctx, SPG_E_NOMEM, "eq(rp)");
+  rc = eq_table(ctx, rp, eq_p);
+  if (rc) return rc;
+
+  // ---- phase 2 (sumcheck.rs:788-1065)
+  FqV ry_all;
+  Fq claims2[3], blind_post2;
+  bool single = inst.num_instances == 1;
+  {
+    size_t rounds = ny + nw + np;
+    ZKRounds zk;
+    zk.init(g, tape, rounds, claim2, blind2);
+    size_t inputs_len = (size_t)1 << ny, ws_len = (size_t)1 << nw, instance_len = (size_t)1 << np;
+    size_t lenP = instance_len;
+    std::vector<size_t> sc_ni = num_inputs;
+    for (size_t j = 0; j < rounds; j++) {
+      int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
+      if (inputs_len > 1) inputs_len /= 2;
+      else if (ws_len > 1) ws_len /= 2;
+      else instance_len /= 2;
+      for (size_t p = 0; p < std::min(instance_len, sc_ni.size()); p++)
+        if (mode == MODE_X && sc_ni[p] > 1) sc_ni[p] /= 2;
+      Fq e[3];
+      rc = phase2_eval(ctx, ABC, Zp, mode, instance_len, ws_len, nws, single, sc_ni, eq_p, partials, d_out3, e);
+      if (rc) return rc;
+      Fq r_j = zk.begin(g, t, j, e);
+      if (mode == MODE_P) { rc = dev_fold_top(ctx, eq_p, lenP, r_j); lenP /= 2; }
+      if (!rc && (mode != MODE_P || !single)) rc = pqx_bound(ctx, ABC, nullptr, nullptr, r_j, mode);
+      if (!rc) rc = pqx_bound(ctx, Zp, nullptr, nullptr, r_j, mode);
+      if (rc) return rc;
+      zk.finish(g, t, tape, j, r_j);
+      ry_all.push_back(r_j);
+    }
+    rc = d2h_fq(ctx, eq_p, &claims2[0]);
+    if (!rc) rc = d2h_fq(ctx, ABC.d, &claims2[1]);
+    if (!rc) rc = d2h_fq(ctx, Zp.d, &claims2[2]);
+    if (rc) return rc;
+    blind_post2 = zk.blinds_evals[rounds - 1];
+    pf.sc2 = std::move(zk.out);
+  }
+  FqV ry_rev(ry_all.begin(), ry_all.begin() + ny), rw(ry_all.begin() + ny, ry_all.begin() + ny + nw),
+      rp2(ry_all.begin() + ny + nw, ry_all.end());
+  FqV ry(ry_rev.rbegin(), ry_rev.rend());
+
+  // ---- witness-section evaluations and their batched opening (r1csproof.rs:518-639)
+  FqV ry_factors(ny + 1, fq_one());
+  for (size_t i = 0; i < ny; i++) ry_factors[i + 1] = fq_mul(ry_factors[i], fq_sub(fq_one(), ry[i]));
+  struct PolyRef {
+    size_t w, p, np, ni;
+    FqV LZ, R;
+    Fq ev;
+  };
+  std::vector<PolyRef> polys;
+  std::vector<FqV> eval_list(nws);
+  pf.comm_vars_at_ry_list.assign(nws, {});
+  for (size_t i = 0; i < nws; i++) {
+    eval_list.push_back({});
+    pf.comm_vars_at_ry_list.push_back({});
+    for (size_t p = 0; p < wit.num_proofs[i].size(); p++) {
+      PolyRef pr;
+      pr.w = i;
+      pr.p = p;
+      pr.np = wit.num_proofs[i][p];
+      pr.ni = wit.num_inputs[i][p];
+      size_t lnp = lg2(pr.np), lni = lg2(pr.ni);
+      FqV r(rq.begin() + (nq - lnp), rq.end());
+      if (pr.ni >= Y) {
+        r.insert(r.end(), lni - ny, fq_zero());
+        r.insert(r.end(), ry.begin(), ry.end());
+      } else {
+        r.insert(r.end(), ry.begin() + (ny - lni), ry.end());
+      }
+      size_t nv = r.size(), ln = nv / 2;
+      FqV rl(r.begin(), r.begin() + ln), rr(r.begin() + ln, r.end());
+      size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
+      pr.R = eq_evals_host(rr);
+      // LZ = bound(L) on the device
+      Fq* dL = (Fq*)ws_get(ctx, WS_L, Ls * sizeof(Fq) + 64);
+      uint32_t nbx = (uint32_t)((Rs + 255) / 256);
+      uint32_t S = (uint32_t)std::min<size_t>(Ls, std::max<size_t>(1, 2048 / nbx));
+      uint32_t chunk = (uint32_t)((Ls + S - 1) / S);
+      S = (uint32_t)((Ls + chunk - 1) / chunk);
+      Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, (size_t)S * Rs * sizeof(Fq) + 64);
+      Fq* dout = (Fq*)ws_get(ctx, WS_BOUT, Rs * sizeof(Fq) + 64);
+      if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "bound");
+      rc = eq_table(ctx, rl, dL);
+      if (rc) return rc;
+      {
+        KScope ks(ctx, "poly_bound", 32.0 * Ls * Rs + 32.0 * Ls + 64.0 * S * Rs);
+        hipLaunchKernelGGL(k_bound_part, dim3(nbx, S), dim3(256), 0, s, wit.d_w + wit.off[i][p], dL, (uint32_t)Ls,
+                           (uint32_t)Rs, chunk, dpart);
+        hipLaunchKernelGGL(k_sum_cols, dim3(nbx), dim3(256), 0, s, dpart, S, (uint32_t)Rs, dout);
+      }
+      SPG_HIP(ctx, hipGetLastError());
+      pr.LZ.resize(Rs);
+      rc = d2h_fq(ctx, dout, pr.LZ.data(), Rs);
+      if (rc) return rc;
+      Fq ev = fq_zero();
+      for (size_t k = 0; k < Rs; k++) ev = fq_add(ev, fq_mul(pr.LZ[k], pr.R[k]));
+      pr.ev = ev;
+      eval_list[i].push_back(pr.ni >= Y ? ev : fq_mul(ev, ry_factors[ny - lni]));
+      pf.comm_vars_at_ry_list[i].push_back(compress(commit_host(g, g.gens_1, {ev}, fq_zero())));
+      polys.push_back(std::move(pr));
+    }
+  }
+  // PolyEvalProof::prove_batched_instances_disjoint_rounds (dense_mlpoly.rs:861-960)
+  {
+    t.protocol("polynomial evaluation proof");
+    std::vector<std::pair<size_t, size_t>> keys;
+    std::vector<FqV> LZ_list, R_list;
+    FqV Zc;
+    Fq c_base = t.challenge("challenge_c");
+    Fq c = fq_one();
+    for (auto& pr : polys) {
+      std::pair<size_t, size_t> key = {pr.np, pr.ni};
+      size_t idx = keys.size();
+      for (size_t k = 0; k < keys.size(); k++)
+        if (keys[k] == key) { idx = k; break; }
+      if (idx < keys.size()) {
+        c = fq_mul(c, c_base);
+        for (size_t k = 0; k < pr.LZ.size(); k++) LZ_list[idx][k] = fq_add(LZ_list[idx][k], fq_mul(c, pr.LZ[k]));
+        Zc[idx] = fq_add(Zc[idx], fq_mul(c, pr.ev));
+      } else {
+        keys.push_back(key);
+        Zc.push_back(pr.ev);
+        LZ_list.push_back(pr.LZ);
+        R_list.push_back(pr.R);
+      }
+    }
+    for (size_t k = 0; k < LZ_list.size(); k++) {
+      DotProductProofLogP dp;
+      Pt cy;
+      rc = dotproduct_log_prove(ctx, g, t, tape, LZ_list[k], fq_zero(), R_list[k], Zc[k], fq_zero(), &dp, &cy);
+      if (rc) return rc;
+      pf.evals.push_back(std::move(dp));
+    }
+  }
+  // prefix_list (r1csproof.rs:577-606) and the combined evaluation
+  FqV prefix;
+  {
+    Fq one = fq_one();
+    size_t W2 = npow2(nws);
+    if (W2 == 1) prefix = {one};
+    else if (W2 == 2) prefix = {fq_sub(one, rw[0]), rw[0]};
+    else if (W2 == 4)
+      prefix = {fq_mul(fq_sub(one, rw[0]), fq_sub(one, rw[1])), fq_mul(fq_sub(one, rw[0]), rw[1]),
+                fq_mul(rw[0], fq_sub(one, rw[1])), fq_mul(rw[0], rw[1])};
+    else
+      for (int i = 0; i < 8; i++) {
+        Fq a = (i & 4) ? rw[0] : fq_sub(one, rw[0]);
+        Fq b = (i & 2) ? rw[1] : fq_sub(one, rw[1]);
+        Fq cc = (i & 1) ? rw[2] : fq_sub(one, rw[2]);
+        prefix.push_back(fq_mul(fq_mul(a, b), cc));
+      }
+  }
+  FqV comb_list;
+  for (size_t p = 0; p < P; p++) {
+    Fq comb = fq_zero();
+    for (size_t i = 0; i < nws; i++) {
+      size_t pw = wit.num_proofs[i].size() == 1 ? 0 : p;
+      comb = fq_add(comb, fq_mul(prefix[i], eval_list[i][pw]));
+    }
+    for (size_t q = 0; q < nq - lg2(num_proofs[p]); q++) comb = fq_mul(comb, fq_sub(fq_one(), rq[q]));
+    comb_list.push_back(comb);
+  }
+  Fq eval_vars_at_ry = dense_eval_host(comb_list, rp2);
+  pf.comm_vars_at_ry = compress(commit_host(g, g.gens_1, {eval_vars_at_ry}, fq_zero()));
+  Fq claim_post2 = fq_mul(fq_mul(claims2[0], claims2[1]), claims2[2]);
+  pf.eq2 = equality_prove(g, g.gens_1, t, tape, claim_post2, fq_zero(), claim_post2, blind_post2);
+  pf.claims_phase2[0] = comm_Az;
+  pf.claims_phase2[1] = comm_Bz;
+  pf.claims_phase2[2] = comm_Cz;
+  pf.claims_phase2[3] = comm_prod;
+  FqV rwry(rw);
+  rwry.insert(rwry.end(), ry.begin(), ry.end());
+  challenges = {rp2, rq_rev, rx, rwry};
+  return 0;
+}
+
+static Fq ld_fq(const uint64_t* v) {
+  Fq a;
+  for (int i = 0; i < 4; i++) {
+    a.l[2 * i] = (uint32_t)v[i];
+    a.l[2 * i + 1] = (uint32_t)(v[i] >> 32);
+  }
+  return a;
+}
+static void st_fq(uint64_t* v, const Fq& a) {
+  for (int i = 0; i < 4; i++) v[i] = (uint64_t)a.l[2 * i] | ((uint64_t)a.l[2 * i + 1] << 32);
+}
+
+}  // namespace spg
+
+using namespace spg;
+
+// ------------------------------------------------------------------------------------ C-ABI
+extern "C" int spg_transcript_new(const char* label, spg_transcript** out) {
+  if (!label || !out) return SPG_E_ARG;
+  *out = new spg_transcript(label);
+  return SPG_OK;
+}
+extern "C" int spg_transcript_append_message(spg_transcript* t, const char* label, const uint8_t* msg, size_t len) {
+  if (!t || !label || (!msg && len)) return SPG_E_ARG;
+  t->t.m.message(label, msg, len);
+  return SPG_OK;
+}
+extern "C" int spg_transcript_append_scalar(spg_transcript* t, const char* label, const uint64_t* scalar_mont) {
+  if (!t || !label || !scalar_mont) return SPG_E_ARG;
+  t->t.scalar(label, ld_fq(scalar_mont));
+  return SPG_OK;
+}
+extern "C" int spg_transcript_challenge_scalar(spg_transcript* t, const char* label, uint64_t* out_mont) {
+  if (!t || !label || !out_mont) return SPG_E_ARG;
+  st_fq(out_mont, t->t.challenge(label));
+  return SPG_OK;
+}
+extern "C" int spg_transcript_challenge_bytes(spg_transcript* t, const char* label, uint8_t* out, size_t len) {
+  if (!t || !label || (!out && len)) return SPG_E_ARG;
+  t->t.m.challenge(label, out, len);
+  return SPG_OK;
+}
+extern "C" int spg_transcript_free(spg_transcript* t) {
+  delete t;
+  return SPG_OK;
+}
+extern "C" int spg_random_tape_new(const char* name, const uint64_t* init_mont, spg_random_tape** out) {
+  if (!name || !init_mont || !out) return SPG_E_ARG;
+  *out = new spg_random_tape(name, ld_fq(init_mont));
+  return SPG_OK;
+}
+extern "C" int spg_random_tape_scalar(spg_random_tape* tp, const char* label, uint64_t* out_mont) {
+  if (!tp || !label || !out_mont) return SPG_E_ARG;
+  st_fq(out_mont, tp->t.scalar(label));
+  return SPG_OK;
+}
+extern "C" int spg_random_tape_free(spg_random_tape* tp) {
+  delete tp;
+  return SPG_OK;
+}
+
+extern "C" int spg_r1cs_gens_new(spg_ctx* ctx, const uint8_t* label, size_t label_len, size_t num_vars,
+                                 spg_r1cs_gens** out) {
+  if (!ctx || !label || !out || num_vars == 0) return SPG_E_ARG;
+  size_t nv = lg2(num_vars);
+  size_t n_pc = (size_t)1 << (nv - nv / 2);  // poly_commit_gens_new: 2^right
+  spg_r1cs_gens* rg = new spg_r1cs_gens();
+  ProverGens& g = rg->g;
+  size_t n = std::max<size_t>(n_pc + 1, 4);
+  int rc = spg_gens_derive(ctx, label, label_len, n, &g.dev);
+  if (rc) {
+    delete rg;
+    return rc;
+  }
+  g.host.init(g.dev->compressed, n + 1);
+  g.n_pc = n_pc;
+  g.gens_n.G.resize(n_pc);
+  for (size_t i = 0; i < n_pc; i++) g.gens_n.G[i] = i;
+  g.gens_n.h = n_pc + 1;
+  g.gens_1.G = {n_pc};
+  g.gens_1.h = n_pc + 1;
+  g.gens_4.G = {0, 1, 2, 3};
+  g.gens_4.h = 4;
+  // warm the host fixed-base tables of the sigma-protocol generators
+  for (size_t i : {(size_t)0, (size_t)1, (size_t)2, (size_t)3, (size_t)4, n_pc, n_pc + 1}) g.host.get(i);
+  *out = rg;
+  return SPG_OK;
+}
+extern "C" int spg_r1cs_gens_free(spg_ctx* ctx, spg_r1cs_gens* g) {
+  if (!g) return SPG_OK;
+  spg_gens_free(ctx, g->g.dev);
+  delete g;
+  return SPG_OK;
+}
+extern "C" int spg_r1cs_gens_download(spg_ctx* ctx, const spg_r1cs_gens* g, uint8_t* out, size_t* count) {
+  if (!ctx || !g || !count) return SPG_E_ARG;
+  *count = g->g.dev->n + 1;
+  if (out) memcpy(out, g->g.dev->compressed, 32 * (g->g.dev->n + 1));
+  return SPG_OK;
+}
+
+extern "C" int spg_r1cs_inst_new(spg_ctx* ctx, const spg_r1cs_instance* ci, spg_r1cs_inst** out) {
+  if (!ctx || !ci || !out || !ci->num_instances || !ci->num_cons || !ci->nnz || !ci->entries) return SPG_E_ARG;
+  if (!is_pow2(ci->max_num_cons) || !is_pow2(ci->num_vars))
+    return set_err(ctx, SPG_E_ARG, "max_num_cons and num_vars must be powers of two");
+  size_t Pm = ci->num_instances;
+  std::vector<uint32_t> rowptr, col, colptr, crow;
+  std::vector<Fq> val, cval;
+  spg_r1cs_inst* I = new spg_r1cs_inst();
+  I->num_instances = Pm;
+  I->max_num_cons = ci->max_num_cons;
+  I->num_vars = ci->num_vars;
+  I->num_cons.assign(ci->num_cons, ci->num_cons + Pm);
+  for (size_t p = 0; p < Pm; p++) {
+    size_t nc = ci->num_cons[p];
+    if (!is_pow2(nc) || nc > ci->max_num_cons) {
+      delete I;
+      return set_err(ctx, SPG_E_ARG, "num_cons must be powers of two <= max_num_cons");
+    }
+    // CSR per matrix (counting sort by row, stable in entry order)
+    for (int m = 0; m < 3; m++) {
+      size_t nnz = ci->nnz[3 * p + m];
+      I->nnz.push_back(nnz);
+      const spg_sparse_entry* E = ci->entries[3 * p + m];
+      if (nnz && !E) {
+        delete I;
+        return SPG_E_ARG;
+      }
+      std::vector<uint32_t> cnt(nc + 1, 0);
+      for (size_t e = 0; e < nnz; e++) {
+        if (E[e].row >= nc || E[e].col >= ci->num_vars) {
+          delete I;
+          return set_err(ctx, SPG_E_ARG, "sparse entry out of range");
+        }
+        cnt[E[e].row + 1]++;
+      }
+      for (size_t r = 0; r < nc; r++) cnt[r + 1] += cnt[r];
+      I->rp_off.push_back(rowptr.size());
+      size_t base = col.size();
+      for (size_t r = 0; r <= nc; r++) rowptr.push_back((uint32_t)(base + cnt[r]));
+      col.resize(base + nnz);
+      val.resize(base + nnz);
+      std::vector<uint32_t> fill(cnt.begin(), cnt.end() - 1);
+      for (size_t e = 0; e < nnz; e++) {
+        size_t d = base + fill[E[e].row]++;
+        col[d] = (uint32_t)E[e].col;
+        val[d] = ld_fq(E[e].val);
+      }
+    }
+    // merged CSC over A, B, C with tagged rows
+    size_t ncol = ci->num_vars;
+    std::vector<uint32_t> cnt(ncol + 1, 0);
+    for (int m = 0; m < 3; m++)
+      for (size_t e = 0; e < ci->nnz[3 * p + m]; e++) cnt[ci->entries[3 * p + m][e].col + 1]++;
+    for (size_t c = 0; c < ncol; c++) cnt[c + 1] += cnt[c];
+    I->cp_off.push_back(colptr.size());
+    size_t base = crow.size();
+    for (size_t c = 0; c <= ncol; c++) colptr.push_back((uint32_t)(base + cnt[c]));
+    crow.resize(base + cnt[ncol]);
+    cval.resize(base + cnt[ncol]);
+    std::vector<uint32_t> fill(cnt.begin(), cnt.end() - 1);
+    for (int m = 0; m < 3; m++)
+      for (size_t e = 0; e < ci->nnz[3 * p + m]; e++) {
+        const spg_sparse_entry& en = ci->entries[3 * p + m][e];
+        size_t d = base + fill[en.col]++;
+        crow[d] = (uint32_t)(en.row * 4 + m);
+        cval[d] = ld_fq(en.val);
+      }
+  }
+  if (col.size() >= 0xffffffffULL || crow.size() >= 0xffffffffULL || ci->max_num_cons >= (1ull << 30)) {
+    delete I;
+    return set_err(ctx, SPG_E_ARG, "instance too large");
+  }
+  auto up = [&](void** d, const void* h, size_t bytes) -> int {
+    if (hipMalloc(d, bytes ? bytes : 16) != hipSuccess) return SPG_E_NOMEM;
+    if (bytes && hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice) != hipSuccess) return SPG_E_HIP;
+    return 0;
+  };
+  int rc = up((void**)&I->d_rowptr, rowptr.data(), rowptr.size() * 4);
+  if (!rc) rc = up((void**)&I->d_col, col.data(), col.size() * 4);
+  if (!rc) rc = up((void**)&I->d_val, val.data(), val.size() * sizeof(Fq));
+  if (!rc) rc = up((void**)&I->d_colptr, colptr.data(), colptr.size() * 4);
+  if (!rc) rc = up((void**)&I->d_crow, crow.data(), crow.size() * 4);
+  if (!rc) rc = up((void**)&I->d_cval, cval.data(), cval.size() * sizeof(Fq));
+  if (rc) {
+    spg_r1cs_inst_free(ctx, I);
+    return set_err(ctx, rc, "instance upload");
+  }
+  *out = I;
+  return SPG_OK;
+}
+extern "C" int spg_r1cs_inst_free(spg_ctx* ctx, spg_r1cs_inst* I) {
+  (void)ctx;
+  if (!I) return SPG_OK;
+  hipFree(I->d_rowptr);
+  hipFree(I->d_col);
+  hipFree(I->d_val);
+  hipFree(I->d_colptr);
+  hipFree(I->d_crow);
+  hipFree(I->d_cval);
+  delete I;
+  return SPG_OK;
+}
+
+extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, spg_r1cs_witness** out) {
+  if (!ctx || !secs || !out || nws == 0) return SPG_E_ARG;
+  if (nws > 8) return set_err(ctx, SPG_E_ARG, "at most 8 witness sections (prefix_list)");
+  spg_r1cs_witness* W = new spg_r1cs_witness();
+  W->nws = nws;
+  W->num_proofs.resize(nws);
+  W->num_inputs.resize(nws);
+  W->off.resize(nws);
+  size_t total = 0;
+  for (size_t w = 0; w < nws; w++) {
+    const spg_witness_sec& s = secs[w];
+    if (!s.num_instances || !s.num_proofs || !s.num_inputs || !s.w) {
+      delete W;
+      return SPG_E_ARG;
+    }
+    for (size_t p = 0; p < s.num_instances; p++) {
+      if (!is_pow2(s.num_proofs[p]) || !is_pow2(s.num_inputs[p])) {
+        delete W;
+        return set_err(ctx, SPG_E_ARG, "witness section sizes must be powers of two");
+      }
+      W->num_proofs[w].push_back(s.num_proofs[p]);
+      W->num_inputs[w].push_back(s.num_inputs[p]);
+      W->off[w].push_back(total);
+      total += s.num_proofs[p] * s.num_inputs[p];
+    }
+  }
+  W->total = total;
+  if (hipMalloc(&W->d_w, total * sizeof(Fq) + 64) != hipSuccess) {
+    delete W;
+    return set_err(ctx, SPG_E_NOMEM, "witness upload");
+  }
+  for (size_t w = 0; w < nws; w++)
+    for (size_t p = 0; p < secs[w].num_instances; p++) {
+      size_t n = W->num_proofs[w][p] * W->num_inputs[w][p];
+      // Scalar([u64; 4]) and Fq(u32[8]) share the little-endian byte image
+      if (hipMemcpyAsync(W->d_w + W->off[w][p], secs[w].w[p], n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream) !=
+          hipSuccess) {
+        spg_r1cs_witness_free(ctx, W);
+        return set_err(ctx, SPG_E_HIP, "witness upload");
+      }
+    }
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    spg_r1cs_witness_free(ctx, W);
+    return set_err(ctx, SPG_E_HIP, "witness upload");
+  }
+  *out = W;
+  return SPG_OK;
+}
+extern "C" int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* W) {
+  (void)ctx;
+  if (!W) return SPG_OK;
+  hipFree(W->d_w);
+  delete W;
+  return SPG_OK;
+}
+
+extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst,
+                              size_t num_instances, size_t max_num_proofs, const size_t* num_proofs,
+                              size_t max_num_inputs, const size_t* num_inputs, const spg_r1cs_witness* wit,
+                              spg_transcript* transcript, spg_random_tape* tape, uint8_t* proof, size_t proof_cap,
+                              size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  if (!ctx || !gens || !inst || !num_proofs || !num_inputs || !wit || !transcript || !tape || !proof_len)
+    return SPG_E_ARG;
+  if (!num_instances || !is_pow2(max_num_proofs) || !is_pow2(max_num_inputs))
+    return set_err(ctx, SPG_E_ARG, "bad sizes");
+  if (inst->num_instances != 1 && inst->num_instances != num_instances)
+    return set_err(ctx, SPG_E_ARG, "instance count mismatch");
+  if (num_instances > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances for one launch");
+  if (wit->nws * max_num_inputs > inst->num_vars) return set_err(ctx, SPG_E_ARG, "witness wider than num_vars");
+  for (size_t p = 0; p < num_instances; p++) {
+    if (!is_pow2(num_proofs[p]) || num_proofs[p] > max_num_proofs || !is_pow2(num_inputs[p]) ||
+        num_inputs[p] > max_num_inputs)
+      return set_err(ctx, SPG_E_ARG, "num_proofs / num_inputs must be powers of two within the maxima");
+  }
+  for (size_t w = 0; w < wit->nws; w++) {
+    if (wit->num_proofs[w].size() != 1 && wit->num_proofs[w].size() != num_instances)
+      return set_err(ctx, SPG_E_ARG, "witness section instance count mismatch");
+    for (size_t p = 0; p < num_instances; p++) {
+      size_t pw = wit->num_proofs[w].size() == 1 ? 0 : p;
+      if (wit->num_proofs[w][pw] != 1 && wit->num_proofs[w][pw] < num_proofs[p])
+        return set_err(ctx, SPG_E_ARG, "witness section has fewer rows than num_proofs");
+      if (wit->num_proofs[w][pw] > max_num_proofs) return set_err(ctx, SPG_E_ARG, "witness section too tall");
+    }
+  }
+  Prover pr(ctx, const_cast<spg_r1cs_gens*>(gens)->g, *inst, *wit, transcript->t, tape->t);
+  pr.P = num_instances;
+  pr.max_np = max_num_proofs;
+  pr.Y = max_num_inputs;
+  pr.nws = wit->nws;
+  pr.num_proofs.assign(num_proofs, num_proofs + num_instances);
+  pr.num_inputs.assign(num_inputs, num_inputs + num_instances);
+  timer_start(ctx);
+  int rc = pr.run();
+  timer_stop(ctx);
+  if (rc) return rc;
+  Writer wr;
+  pr.pf.ser(wr);
+  *proof_len = wr.out.size();
+  if (challenges_out && ch_lens) {
+    size_t k = 0;
+    for (int i = 0; i < 4; i++) {
+      ch_lens[i] = pr.challenges[i].size();
+      for (auto& c : pr.challenges[i]) st_fq(challenges_out + 4 * k++, c);
+    }
+  }
+  if (!proof || wr.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
+  memcpy(proof, wr.out.data(), wr.out.size());
+  return SPG_OK;
+}

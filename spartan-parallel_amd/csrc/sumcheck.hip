@@ -1,0 +1,416 @@
+// spg — sumcheck round evaluation and folding on MI355X.
+//
+// Replaces the inner loops of
+//   ZKSumcheckInstanceProof::prove_cubic_with_additive_term_disjoint_rounds (src/sumcheck.rs:1173-1245)
+//   ZKSumcheckInstanceProof::prove_cubic_disjoint_rounds                     (src/sumcheck.rs:881-941)
+//   SumcheckInstanceProof::prove_cubic_batched                               (src/sumcheck.rs:300-367)
+// and the folds DensePolynomial::bound_poly_var_top (src/dense_mlpoly.rs:267-275) and
+// DensePolynomialPqx::bound_poly_{p,q,w,x} (src/custom_dense_mlpoly.rs:205-289).
+//
+// Every round is one streaming pass over HBM-resident tables: each thread accumulates exact Fq
+// partial sums of (e0, e2, e3) over a grid-stride slice, a 256-thread block tree-reduces them in LDS
+// and a one-block kernel sums the block partials. Reduction order is irrelevant (exact arithmetic).
+#include "sumcheck.hpp"
+
+namespace spg {
+
+__device__ __forceinline__ int find_inst(const PqxArgs& a, uint32_t t) {
+  int p = 0;
+  for (int k = 1; k < a.P; k++)
+    if (a.in[k].dom_off <= t) p = k;
+  return p;
+}
+
+__device__ __forceinline__ void block_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict__ partials) {
+  __shared__ Fq sh[3][256];
+  int t = threadIdx.x;
+  sh[0][t] = v0;
+  sh[1][t] = v1;
+  sh[2][t] = v2;
+  __syncthreads();
+  for (int d = 128; d >= 1; d >>= 1) {
+    if (t < d) {
+      sh[0][t] = fq_add(sh[0][t], sh[0][t + d]);
+      sh[1][t] = fq_add(sh[1][t], sh[1][t + d]);
+      sh[2][t] = fq_add(sh[2][t], sh[2][t + d]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    partials[3 * blockIdx.x] = sh[0][0];
+    partials[3 * blockIdx.x + 1] = sh[1][0];
+    partials[3 * blockIdx.x + 2] = sh[2][0];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_reduce3(const Fq* __restrict__ partials, int nb, Fq* __restrict__ out) {
+  Fq a = fq_zero(), b = fq_zero(), c = fq_zero();
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    a = fq_add(a, partials[3 * i]);
+    b = fq_add(b, partials[3 * i + 1]);
+    c = fq_add(c, partials[3 * i + 2]);
+  }
+  block_reduce3(a, b, c, out);
+}
+
+// EqPolynomial::evals (src/dense_mlpoly.rs:76-92): out[b] = prod_j (bit_{ell-1-j}(b) ? r_j : 1 - r_j)
+__global__ void k_eq_table(FqArg32 r, Fq* __restrict__ out, size_t n) {
+  size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  Fq acc = fq_one();
+  for (int j = 0; j < r.n; j++) {
+    bool bit = (b >> (r.n - 1 - j)) & 1;
+    acc = fq_mul(acc, bit ? r.v[j] : fq_sub(fq_one(), r.v[j]));
+  }
+  out[b] = acc;
+}
+
+// bound_poly_var_top on a dense vector of length 2n (in place, first n outputs)
+__global__ void k_fold_top(Fq* __restrict__ v, size_t n, Fq r) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fq lo = v[i];
+  v[i] = fq_add(lo, fq_mul(r, fq_sub(v[i + n], lo)));
+}
+
+// ---------------------------------------------------------------- phase 1 round evaluation
+__global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32_t total, uint32_t proof_len,
+                                                     uint32_t cons_len, uint32_t instance_len,
+                                                     const Fq* __restrict__ Ap, const Fq* __restrict__ Aq,
+                                                     const Fq* __restrict__ Ax, const Fq* __restrict__ B,
+                                                     const Fq* __restrict__ C, const Fq* __restrict__ D,
+                                                     Fq* __restrict__ partials) {
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    int p = find_inst(a, t);
+    const PqxInst& d = a.in[p];
+    uint32_t loc = t - d.dom_off;
+    uint32_t q = loc / d.sc_ni, x = loc % d.sc_ni;
+    Fq apq = fq_mul(Ap[p], Aq[q * d.step_q]);
+    Fq a_lo = fq_mul(apq, Ax[x * d.step_x]);
+    Fq a_hi;
+    if (mode == MODE_P) a_hi = fq_mul(fq_mul(Ap[p + instance_len], Aq[q * d.step_q]), Ax[x * d.step_x]);
+    else if (mode == MODE_Q) a_hi = fq_mul(fq_mul(Ap[p], Aq[q * d.step_q + proof_len]), Ax[x * d.step_x]);
+    else a_hi = fq_mul(apq, Ax[x * d.step_x + cons_len]);
+    size_t base = pqx_off(d) + (size_t)q * d.anw * d.ani + x;
+    Fq b_lo = B[base], c_lo = C[base], d_lo = D[base];
+    Fq b_hi, c_hi, d_hi;
+    bool zero_hi;
+    size_t hi;
+    if (mode == MODE_X) {
+      zero_hi = d.ni == 1;
+      hi = base + d.ni / 2;
+    } else if (mode == MODE_Q) {
+      zero_hi = d.np == 1;
+      hi = base + (size_t)(d.np / 2) * d.anw * d.ani;
+    } else {
+      int ph = p + a.ninst / 2;
+      zero_hi = ph >= a.zlen;
+      hi = zero_hi ? 0 : pqx_off(a.in[ph]) + (size_t)q * a.in[ph].anw * a.in[ph].ani + x;
+    }
+    if (zero_hi) {
+      b_hi = fq_zero(); c_hi = fq_zero(); d_hi = fq_zero();
+    } else {
+      b_hi = B[hi]; c_hi = C[hi]; d_hi = D[hi];
+    }
+    // comb(A, B, C, D) = A * (B*C - D) at X = 0, 2, 3
+    e0 = fq_add(e0, fq_mul(a_lo, fq_sub(fq_mul(b_lo, c_lo), d_lo)));
+    Fq a2 = fq_sub(fq_dbl(a_hi), a_lo), b2 = fq_sub(fq_dbl(b_hi), b_lo);
+    Fq c2 = fq_sub(fq_dbl(c_hi), c_lo), d2 = fq_sub(fq_dbl(d_hi), d_lo);
+    e2 = fq_add(e2, fq_mul(a2, fq_sub(fq_mul(b2, c2), d2)));
+    Fq a3 = fq_sub(fq_add(a2, a_hi), a_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo);
+    Fq c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
+    e3 = fq_add(e3, fq_mul(a3, fq_sub(fq_mul(b3, c3), d3)));
+  }
+  block_reduce3(e0, e2, e3, partials);
+}
+
+// ---------------------------------------------------------------- phase 2 round evaluation
+// domain: p < Pd, w < W, y < sc_ni[p] ; B = ABC table (instance pi = single ? 0 : p), C = Z table
+__device__ __forceinline__ Fq pqx_get(const PqxArgs& a, const Fq* T, int p, uint32_t w, uint32_t y) {
+  if (p >= a.zlen) return fq_zero();
+  const PqxInst& d = a.in[p];
+  if (w >= d.anw || y >= d.ani) return fq_zero();
+  return T[pqx_off(d) + (size_t)w * d.ani + y];
+}
+__device__ __forceinline__ Fq pqx_get_high(const PqxArgs& a, const Fq* T, int p, uint32_t w, uint32_t y, int mode) {
+  const PqxInst& d = a.in[p];
+  if (mode == MODE_X) return d.ni == 1 ? fq_zero() : T[pqx_off(d) + (size_t)w * d.ani + y + d.ni / 2];
+  if (mode == MODE_W) {
+    uint32_t wh = w + a.nws / 2;
+    return wh < d.anw ? T[pqx_off(d) + (size_t)wh * d.ani + y] : fq_zero();
+  }
+  int ph = p + a.ninst / 2;
+  return ph < a.zlen ? T[pqx_off(a.in[ph]) + (size_t)w * a.in[ph].ani + y] : fq_zero();
+}
+
+__global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int mode, uint32_t total, int W,
+                                                     bool single, uint32_t instance_len, const Fq* __restrict__ eq,
+                                                     const Fq* __restrict__ B, const Fq* __restrict__ C,
+                                                     Fq* __restrict__ partials) {
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    int p = find_inst(zz, t);
+    uint32_t loc = t - zz.in[p].dom_off;
+    uint32_t ny = zz.in[p].sc_ni;
+    uint32_t w = loc / ny, y = loc % ny;
+    (void)W;
+    int pi = single ? 0 : p;
+    Fq a_lo = eq[p];
+    Fq a_hi = mode == MODE_P ? eq[p + instance_len] : a_lo;
+    Fq b_lo = pqx_get(ab, B, pi, w, y), c_lo = pqx_get(zz, C, p, w, y);
+    Fq b_hi = pqx_get_high(ab, B, pi, w, y, mode), c_hi = pqx_get_high(zz, C, p, w, y, mode);
+    e0 = fq_add(e0, fq_mul(fq_mul(a_lo, b_lo), c_lo));
+    Fq a2 = fq_sub(fq_dbl(a_hi), a_lo), b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo);
+    e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
+    Fq a3 = fq_sub(fq_add(a2, a_hi), a_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo);
+    e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
+  }
+  block_reduce3(e0, e2, e3, partials);
+}
+
+// ---------------------------------------------------------------- Pqx folds (custom_dense_mlpoly.rs:205-289)
+// domain per instance: np_cur[p] (rows to fold) x nw_cur x n_cols, flattened with dom_off.
+// sc_np = rows, sc_ni = columns written, step_q = nw (sections visited)
+__global__ void k_pqx_fold(PqxArgs a, int mode, uint32_t total, Fq r, Fq* __restrict__ T0, Fq* __restrict__ T1,
+                           Fq* __restrict__ T2) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  int p = find_inst(a, t);
+  const PqxInst& d = a.in[p];
+  uint32_t loc = t - d.dom_off;
+  uint32_t ncol = d.sc_ni, nw = d.step_q;
+  uint32_t x = loc % ncol;
+  uint32_t rest = loc / ncol;
+  uint32_t w = rest % nw, q = rest / nw;
+  size_t base = pqx_off(d) + ((size_t)q * d.anw + w) * d.ani + x;
+  size_t hi;
+  bool scale = false, zero_hi = false;
+  if (mode == MODE_X) {
+    if (d.ni == 1) scale = true;
+    hi = base + d.ni / 2;
+  } else if (mode == MODE_Q) {
+    if (d.np == 1) scale = true;
+    hi = base + (size_t)(d.np / 2) * d.anw * d.ani;
+  } else if (mode == MODE_W) {
+    uint32_t wh = w + a.nws;  // a.nws already halved by the host
+    zero_hi = wh >= d.anw;
+    hi = zero_hi ? 0 : pqx_off(d) + ((size_t)q * d.anw + wh) * d.ani + x;
+  } else {
+    int ph = p + a.ninst;  // a.ninst already halved by the host
+    zero_hi = ph >= a.zlen;
+    hi = zero_hi ? 0 : pqx_off(a.in[ph]) + ((size_t)q * a.in[ph].anw + w) * a.in[ph].ani + x;
+  }
+  Fq* Ts[3] = {T0, T1, T2};
+  Fq omr = fq_sub(fq_one(), r);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    Fq* T = Ts[k];
+    if (!T) continue;
+    Fq lo = T[base];
+    if (scale) {
+      T[base] = fq_mul(omr, lo);
+    } else {
+      Fq h = zero_hi ? fq_zero() : T[hi];
+      T[base] = fq_add(lo, fq_mul(r, fq_sub(h, lo)));
+    }
+  }
+}
+
+// ---------------------------------------------------------------- plain cubic (product trees), A*B*C
+__global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, const Fq* __restrict__ B,
+                                                    const Fq* __restrict__ C, uint32_t len, Fq* __restrict__ partials) {
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < len; i += gridDim.x * 256) {
+    Fq al = A[i], ah = A[i + len], bl = B[i], bh = B[i + len], cl = C[i], ch = C[i + len];
+    e0 = fq_add(e0, fq_mul(fq_mul(al, bl), cl));
+    Fq a2 = fq_sub(fq_dbl(ah), al), b2 = fq_sub(fq_dbl(bh), bl), c2 = fq_sub(fq_dbl(ch), cl);
+    e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
+    Fq a3 = fq_sub(fq_add(a2, ah), al), b3 = fq_sub(fq_add(b2, bh), bl), c3 = fq_sub(fq_add(c2, ch), cl);
+    e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
+  }
+  block_reduce3(e0, e2, e3, partials);
+}
+
+// ---------------------------------------------------------------- host launchers
+static int grid_for(uint32_t total) {
+  int nb = (int)((total + 255) / 256);
+  if (nb > 1024) nb = 1024;
+  return nb < 1 ? 1 : nb;
+}
+
+int eval_reduce_finish(spg_ctx* ctx, Fq* partials, int nb, Fq* d_out3, Fq out3[3]) {
+  hipLaunchKernelGGL(k_reduce3, dim3(1), dim3(256), 0, ctx->stream, partials, nb, d_out3);
+  SPG_HIP(ctx, hipMemcpyAsync(out3, d_out3, 3 * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out) {
+  if (ell > 32) return set_err(ctx, SPG_E_ARG, "eq table: too many variables");
+  FqArg32 a;
+  a.n = ell;
+  for (int i = 0; i < ell; i++) a.v[i] = r[i];
+  size_t n = (size_t)1 << ell;
+  KScope ks(ctx, "eq_table", 32.0 * n);
+  hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, a, out, n);
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r) {
+  size_t n = len / 2;
+  if (n == 0) return 0;
+  KScope ks(ctx, "fold_dense", 96.0 * n);
+  hipLaunchKernelGGL(k_fold_top, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, v, n, r);
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+void pqx_fill_args(const PqxDev& T, PqxArgs& a) {
+  a.zlen = (int)T.zlen;
+  a.ninst = (int)T.num_instances;
+  a.nws = (int)T.num_witness_secs;
+  for (size_t p = 0; p < T.zlen && p < (size_t)kMaxP; p++) {
+    PqxInst& d = a.in[p];
+    d.off_lo = (uint32_t)T.off[p];
+    d.off_hi = (uint32_t)(T.off[p] >> 32);
+    d.anp = (uint32_t)T.anp[p];
+    d.anw = (uint32_t)T.anw[p];
+    d.ani = (uint32_t)T.ani[p];
+    d.np = (uint32_t)T.num_proofs[p];
+    d.ni = (uint32_t)T.num_inputs[p];
+    d.dom_off = 0;
+    d.sc_np = d.sc_ni = d.step_q = d.step_x = 1;
+  }
+}
+
+int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
+                const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
+                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* d_out3, Fq out3[3]) {
+  PqxArgs a;
+  pqx_fill_args(T, a);
+  size_t P = std::min(instance_len, sc_np.size());
+  if (P > (size_t)kMaxP || T.zlen > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
+  a.P = (int)P;
+  size_t dom = 0;
+  for (size_t p = 0; p < P; p++) {
+    PqxInst& d = a.in[p];
+    d.dom_off = (uint32_t)dom;
+    d.sc_np = (uint32_t)sc_np[p];
+    d.sc_ni = (uint32_t)sc_nc[p];
+    d.step_q = (uint32_t)(proof_len / sc_np[p]);
+    d.step_x = (uint32_t)(cons_len / sc_nc[p]);
+    dom += sc_np[p] * sc_nc[p];
+  }
+  if (dom >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "phase-1 domain too large");
+  int nb = grid_for((uint32_t)dom);
+  {
+    // B, C, D lo+hi per domain point, plus the three eq factor tables once
+    KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len));
+    hipLaunchKernelGGL(k_phase1_eval, dim3(nb), dim3(256), 0, ctx->stream, a, mode, (uint32_t)dom,
+                       (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq, Ax, B, C, D,
+                       partials);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return eval_reduce_finish(ctx, partials, nb, d_out3, out3);
+}
+
+int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
+                size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
+                const Fq* eq, Fq* partials, Fq* d_out3, Fq out3[3]) {
+  PqxArgs ab, zz;
+  pqx_fill_args(AB, ab);
+  pqx_fill_args(Z, zz);
+  size_t P = std::min(instance_len, sc_ni.size());
+  if (P > (size_t)kMaxP || Z.zlen > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
+  ab.P = (int)AB.zlen;
+  zz.P = (int)P;
+  size_t W = std::min(witness_secs_len, nws_actual);
+  size_t dom = 0;
+  for (size_t p = 0; p < P; p++) {
+    zz.in[p].dom_off = (uint32_t)dom;
+    zz.in[p].sc_ni = (uint32_t)sc_ni[p];
+    dom += W * sc_ni[p];
+  }
+  int nb = grid_for((uint32_t)dom);
+  {
+    KScope ks(ctx, "sc_phase2_eval", 128.0 * dom);  // ABC and Z, lo+hi per domain point
+    hipLaunchKernelGGL(k_phase2_eval, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, (int)W,
+                       single, (uint32_t)instance_len, eq, AB.d, Z.d, partials);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return eval_reduce_finish(ctx, partials, nb, d_out3, out3);
+}
+
+// DensePolynomialPqx::bound_poly(r, mode) applied to up to three tables of identical shape (T[0] owns shape)
+int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode) {
+  PqxArgs a;
+  size_t P = std::min(T.num_instances, T.zlen);
+  // host-side size bookkeeping first (mirrors the reference's field updates)
+  if (mode == MODE_P) {
+    T.num_instances /= 2;
+    P = T.num_instances;
+  } else if (mode == MODE_Q) {
+    T.max_num_proofs /= 2;
+  } else if (mode == MODE_W) {
+    T.num_witness_secs /= 2;
+  } else {
+    T.max_num_inputs /= 2;
+  }
+  pqx_fill_args(T, a);  // a.ninst / a.nws are the *new* values
+  if (P > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
+  a.P = (int)P;
+  size_t dom = 0;
+  std::vector<size_t> np_after(T.num_proofs), ni_after(T.num_inputs);
+  for (size_t p = 0; p < P; p++) {
+    PqxInst& d = a.in[p];
+    size_t rows, nw, cols;
+    if (mode == MODE_P) {
+      rows = 1;
+      nw = std::min(T.num_witness_secs, T.anw[p]);
+      cols = 1;
+    } else if (mode == MODE_Q) {
+      nw = std::min(T.num_witness_secs, T.anw[p]);
+      cols = T.num_inputs[p];
+      if (T.num_proofs[p] == 1) rows = 1;
+      else { rows = T.num_proofs[p] / 2; np_after[p] = rows; }
+    } else if (mode == MODE_W) {
+      rows = T.num_proofs[p];
+      nw = T.num_witness_secs;
+      cols = T.num_inputs[p];
+    } else {
+      rows = T.num_proofs[p];
+      nw = std::min(T.num_witness_secs, T.anw[p]);
+      if (T.num_inputs[p] == 1) cols = 1;
+      else { cols = T.num_inputs[p] / 2; ni_after[p] = cols; }
+    }
+    d.dom_off = (uint32_t)dom;
+    d.sc_ni = (uint32_t)cols;
+    d.step_q = (uint32_t)nw;
+    dom += rows * nw * cols;
+  }
+  if (dom) {
+    double nt = 1.0 + (d1 ? 1.0 : 0.0) + (d2 ? 1.0 : 0.0);
+    KScope ks(ctx, "sc_fold", 96.0 * nt * dom);  // read lo+hi, write lo, per table
+    hipLaunchKernelGGL(k_pqx_fold, dim3((unsigned)((dom + 255) / 256)), dim3(256), 0, ctx->stream, a, mode,
+                       (uint32_t)dom, r, T.d, d1, d2);
+    SPG_HIP(ctx, hipGetLastError());
+  }
+  T.num_proofs = np_after;
+  T.num_inputs = ni_after;
+  return 0;
+}
+
+int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials, Fq* d_out3,
+               Fq out3[3]) {
+  int nb = grid_for((uint32_t)len_half);
+  {
+    KScope ks(ctx, "sc_cubic_eval", 192.0 * len_half);
+    hipLaunchKernelGGL(k_cubic_eval, dim3(nb), dim3(256), 0, ctx->stream, A, B, C, (uint32_t)len_half, partials);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return eval_reduce_finish(ctx, partials, nb, d_out3, out3);
+}
+
+}  // namespace spg

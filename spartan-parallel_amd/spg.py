@@ -64,19 +64,21 @@ class Context:
         self.check(lib().spg_prof_enable(self._h, ctypes.c_int(1 if on else 0)), "spg_prof_enable")
 
     def prof_read(self, reset=True):
-        """{kernel_name: (launches, total_us)} of the kernels timed since the last reset."""
+        """{kernel_name: (launches, total_us, algorithmic_bytes)} of the kernels timed since the last reset."""
         mx = 128
         names = ctypes.create_string_buffer(32 * mx)
         launches = np.zeros(mx, dtype=np.int64)
         tot = np.zeros(mx, dtype=np.float64)
-        k = lib().spg_prof_read(self._h, names, _p(launches), _p(tot), ctypes.c_int(mx), ctypes.c_int(1 if reset else 0))
+        nbytes = np.zeros(mx, dtype=np.float64)
+        k = lib().spg_prof_read(self._h, names, _p(launches), _p(tot), _p(nbytes), ctypes.c_int(mx),
+                                ctypes.c_int(1 if reset else 0))
         if k < 0:
             self.check(k, "spg_prof_read")
         raw = names.raw
         out = {}
         for i in range(k):
             nm = raw[32 * i:32 * i + 32].split(b"\0", 1)[0].decode()
-            out[nm] = (int(launches[i]), float(tot[i]))
+            out[nm] = (int(launches[i]), float(tot[i]), float(nbytes[i]))
         return out
 
     def close(self):
@@ -189,3 +191,169 @@ class Gens:
             self.free()
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------- Fiat-Shamir objects
+class Transcript:
+    """ProofTranscript over merlin (src/transcript.rs:5-63), host object in libspg."""
+
+    def __init__(self, label):
+        self._h = ctypes.c_void_p()
+        rc = lib().spg_transcript_new(ctypes.c_char_p(bytes(label)), ctypes.byref(self._h))
+        if rc != 0:
+            raise SpgError(f"spg_transcript_new: {SPG_ERRORS.get(rc, rc)}")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def append_message(self, label, msg):
+        m = np.frombuffer(bytes(msg), dtype=np.uint8).copy() if msg else np.zeros(1, np.uint8)
+        assert lib().spg_transcript_append_message(self._h, ctypes.c_char_p(bytes(label)), _p(m),
+                                                   ctypes.c_size_t(len(msg))) == 0
+
+    def append_scalar(self, label, s):
+        a = _scalars(s)
+        assert lib().spg_transcript_append_scalar(self._h, ctypes.c_char_p(bytes(label)), _p(a)) == 0
+
+    def challenge_scalar(self, label):
+        out = np.zeros(4, dtype=np.uint64)
+        assert lib().spg_transcript_challenge_scalar(self._h, ctypes.c_char_p(bytes(label)), _p(out)) == 0
+        return out
+
+    def challenge_bytes(self, label, n):
+        out = np.zeros(max(n, 1), dtype=np.uint8)
+        assert lib().spg_transcript_challenge_bytes(self._h, ctypes.c_char_p(bytes(label)), _p(out),
+                                                    ctypes.c_size_t(n)) == 0
+        return out[:n].tobytes()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_transcript_free(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+class RandomTape:
+    """RandomTape (src/random.rs:7-29) with a caller-supplied init scalar (Montgomery limbs)."""
+
+    def __init__(self, name, init_scalar):
+        self._h = ctypes.c_void_p()
+        a = _scalars(init_scalar)
+        rc = lib().spg_random_tape_new(ctypes.c_char_p(bytes(name)), _p(a), ctypes.byref(self._h))
+        if rc != 0:
+            raise SpgError(f"spg_random_tape_new: {SPG_ERRORS.get(rc, rc)}")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def random_scalar(self, label):
+        out = np.zeros(4, dtype=np.uint64)
+        assert lib().spg_random_tape_scalar(self._h, ctypes.c_char_p(bytes(label)), _p(out)) == 0
+        return out
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_random_tape_free(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- R1CSProof
+class R1CSGens:
+    """R1CSGens::new(label, _, num_vars) (src/r1csproof.rs:71-79), resident in HBM."""
+
+    def __init__(self, ctx, label, num_vars):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        lb = np.frombuffer(bytes(label), dtype=np.uint8).copy()
+        ctx.check(lib().spg_r1cs_gens_new(ctx.handle, _p(lb), ctypes.c_size_t(len(label)), ctypes.c_size_t(num_vars),
+                                          ctypes.byref(self._h)), "spg_r1cs_gens_new")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def compressed(self):
+        cnt = ctypes.c_size_t(0)
+        self.ctx.check(lib().spg_r1cs_gens_download(self.ctx.handle, self._h, None, ctypes.byref(cnt)), "download")
+        out = np.zeros((cnt.value, 32), dtype=np.uint8)
+        self.ctx.check(lib().spg_r1cs_gens_download(self.ctx.handle, self._h, _p(out), ctypes.byref(cnt)), "download")
+        return out
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_r1cs_gens_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+class R1CSInst:
+    """R1CSInstance uploaded once (CSR + merged CSC in HBM). `cinst` is a workload.CViews().inst."""
+
+    def __init__(self, ctx, cinst):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        ctx.check(lib().spg_r1cs_inst_new(ctx.handle, ctypes.byref(cinst), ctypes.byref(self._h)), "spg_r1cs_inst_new")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_r1cs_inst_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+class R1CSWitness:
+    """Witness sections (Vec<&ProverWitnessSecInfo>) resident in HBM. `secs` is workload.CViews().secs."""
+
+    def __init__(self, ctx, secs, nws):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        ctx.check(lib().spg_r1cs_witness_new(ctx.handle, secs, ctypes.c_size_t(nws), ctypes.byref(self._h)),
+                  "spg_r1cs_witness_new")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_r1cs_witness_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+def r1cs_prove(ctx, gens, inst, witness, num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs,
+               transcript, tape, cap=1 << 22):
+    """R1CSProof::prove -> (bincode bytes, [rp, rq_rev, rx, rw||ry] as (k, 4) uint64 arrays)."""
+    buf = np.zeros(cap, dtype=np.uint8)
+    ln = ctypes.c_size_t(0)
+    ch = np.zeros((4096, 4), dtype=np.uint64)
+    chl = (ctypes.c_size_t * 4)()
+    npf = (ctypes.c_size_t * num_instances)(*num_proofs)
+    nin = (ctypes.c_size_t * num_instances)(*num_inputs)
+    rc = lib().spg_r1cs_prove(ctx.handle, gens.handle, inst.handle, ctypes.c_size_t(num_instances),
+                              ctypes.c_size_t(max_num_proofs), npf, ctypes.c_size_t(max_num_inputs), nin,
+                              witness.handle, transcript.handle, tape.handle, _p(buf), ctypes.c_size_t(cap),
+                              ctypes.byref(ln), _p(ch), chl)
+    ctx.check(rc, "spg_r1cs_prove")
+    out, o = [], 0
+    for L in list(chl):
+        out.append(ch[o:o + L].copy())
+        o += L
+    return buf[: ln.value].tobytes(), out

@@ -176,3 +176,11 @@ class CViews:
         self.secs = secs
         self.num_proofs = _sz(wl.num_proofs)
         self.num_inputs = _sz(wl.num_inputs)
+
+
+def tape_seed(label=b"spg-tape-seed-0"):
+    """RandomTape init scalar = Scalar::from_bytes_wide(SHAKE256(label)[0..64]) as Montgomery limbs."""
+    import hashlib
+
+    b = hashlib.shake_256(label).digest(64)
+    return to_mont_limbs([int.from_bytes(b, "little") % Q])[0]

@@ -162,8 +162,27 @@ def msm_fixture(lib, rng, label, n, with_edges=True):
     return {"label": label.decode(), "n": n, "scalars_mont": [[int(x) for x in row] for row in s], "out": res.hex()}
 
 
+def r1cs_fixture():
+    """sha256 of bincode(R1CSProof) from the oracle for tests/r1cs_cases.py, each after prove -> verify."""
+    sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import workload
+    from r1cs_cases import CASES
+
+    out = {}
+    for name, (nc, npf, nws, shared) in sorted(CASES.items()):
+        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+        pf, _ = O.r1cs_prove(wl, workload.tape_seed())
+        assert O.r1cs_verify(wl, pf, workload.tape_seed()) == 1, name
+        out[name] = {"len": len(pf), "sha256": hashlib.sha256(pf).hexdigest()}
+    return out
+
+
 def main():
     O.build()
+    if sys.argv[1:] == ["r1cs"]:
+        json.dump(r1cs_fixture(), open(os.path.join(HERE, "r1cs_proofs.json"), "w"), indent=1)
+        return
     rng = np.random.default_rng(0x5350415254414E31)
     lib = sodium()
     w = lambda name, obj: json.dump(obj, open(os.path.join(HERE, name), "w"), indent=1)
@@ -173,6 +192,7 @@ def main():
     w("gens_spg_bench_msm_first16.json", gens_fixture(lib, b"spg_bench_msm", 16))
     w("msm_64.json", msm_fixture(lib, rng, b"gens_r1cs_sat", 64))
     w("msm_256.json", msm_fixture(lib, rng, b"spg_bench_msm", 256))
+    w("r1cs_proofs.json", r1cs_fixture())
     print("golden fixtures written to", HERE)
 
 

@@ -1,0 +1,17 @@
+"""Shared R1CSProof parity cases (shape only; the data comes from workload.R1CSWorkload).
+(num_cons per instance, num_proofs per instance, witness sections, shared instance)"""
+CASES = {
+    "p2_x4_q2": ([4, 4], [2, 2], 1, False),
+    "p3_ragged_3secs": ([8, 4, 2], [4, 2, 1], 3, False),
+    "p2_q_single_5secs": ([16, 16], [8, 1], 5, False),
+    "shared_p2": ([64, 64], [16, 16], 1, True),
+    "p2_x256_2secs": ([256, 256], [64, 64], 2, False),
+    "p1_x32": ([32], [8], 1, False),
+    "p4_ragged_8secs": ([32, 16, 8, 4], [8, 4, 2, 1], 8, False),
+    "p5_q1": ([8, 8, 8, 8, 8], [1, 1, 1, 1, 1], 2, False),
+}
+# larger shapes checked on the GPU only (oracle still finishes in seconds)
+GPU_CASES = {
+    "p2_x1024_q64": ([1024, 1024], [64, 64], 1, False),
+    "p8_x256_q32_shared": ([256] * 8, [32] * 8, 1, True),
+}

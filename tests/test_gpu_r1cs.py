@@ -1,0 +1,65 @@
+"""R1CSProof::prove on the GPU (libspg.so, spg_r1cs_prove) vs the CPU oracle: identical bincode bytes
+and identical challenge vectors under the same transcript label and RandomTape seed."""
+import numpy as np
+import pytest
+
+from r1cs_cases import CASES, GPU_CASES
+
+pytestmark = pytest.mark.gpu
+ALL = dict(CASES, **GPU_CASES)
+GENS_LABEL = b"gens_r1cs_sat"
+GENS_NV = 1 << 24  # TOTAL_NUM_VARS_BOUND = 10^7 -> 2^24 (examples/interface.rs:557-563)
+
+
+@pytest.fixture(scope="module")
+def r1cs_gens(ctx):
+    import spg
+
+    return spg.R1CSGens(ctx, GENS_LABEL, GENS_NV)
+
+
+def test_r1cs_gens_match_oracle(ctx, oracle, r1cs_gens):
+    comp = r1cs_gens.compressed()
+    ref = oracle.gens_stream(GENS_LABEL, comp.shape[0])
+    assert comp.shape[0] == 4098 and np.array_equal(comp, ref)
+
+
+def gpu_prove(ctx, gens, wl, seed, label=b"r1cs_test"):
+    import spg
+    import workload
+
+    v = workload.CViews(wl)
+    inst = spg.R1CSInst(ctx, v.inst)
+    wit = spg.R1CSWitness(ctx, v.secs, wl.nws)
+    t = spg.Transcript(label)
+    tape = spg.RandomTape(b"proof", seed)
+    return spg.r1cs_prove(ctx, gens, inst, wit, wl.P, wl.max_num_proofs, wl.num_proofs, wl.max_num_inputs,
+                          wl.num_inputs, t, tape)
+
+
+@pytest.mark.parametrize("case", sorted(ALL))
+def test_r1cs_proof_bytes_match_oracle(ctx, oracle, r1cs_gens, case):
+    import workload
+
+    nc, npf, nws, shared = ALL[case]
+    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+    seed = workload.tape_seed()
+    ref, ref_ch = oracle.r1cs_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NV)
+    got, got_ch = gpu_prove(ctx, r1cs_gens, wl, seed)
+    for a, b in zip(got_ch, ref_ch):
+        assert np.array_equal(a, b)
+    assert len(got) == len(ref)
+    if got != ref:
+        from proof_layout import first_diff
+
+        pytest.fail(f"proof bytes differ first at field {first_diff(got, ref)}")
+
+
+def test_r1cs_proof_is_repeatable(ctx, r1cs_gens):
+    import workload
+
+    wl = workload.R1CSWorkload([64, 64], [8, 8], num_sections=2)
+    a, _ = gpu_prove(ctx, r1cs_gens, wl, workload.tape_seed())
+    b, _ = gpu_prove(ctx, r1cs_gens, wl, workload.tape_seed())
+    c, _ = gpu_prove(ctx, r1cs_gens, wl, workload.tape_seed(b"x"))
+    assert a == b and a != c
