@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the libspg kernels from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section)
+FETCH_SIZE on gfx950 reports half the bytes of wide coalesced reads, so reads are doubled; WRITE_SIZE is
+taken as is. Both counters count Infinity-Cache hits as traffic (upper bound on HBM bytes).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+# device kernel symbol -> libspg profiling scope name (spg_prof_read)
+NAMES = {
+    "k_phase1_eval": "sc_phase1_eval", "k_phase2_eval": "sc_phase2_eval", "k_pqx_fold": "sc_fold",
+    "k_spmv": "spmv_block", "k_z_fill": "z_fill", "k_abc": "eval_table_abc", "k_bound_part": "poly_bound",
+    "k_fold_top": "fold_dense", "k_eq_table": "eq_table", "k_cubic_eval": "sc_cubic_eval",
+    "k_final": "msm_final", "k_segments": "msm_segments", "k_items": "msm_bucket_items",
+}
+
+
+def scope(kname):
+    for k, v in NAMES.items():
+        if k + "(" in kname or kname.endswith(k) or ("::" + k) in kname:
+            return v
+    return None
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != counter:
+                continue
+            s = scope(row.get("Kernel_Name", ""))
+            if s:
+                acc[s].append(float(row["Counter_Value"]))
+    return acc
+
+
+def main():
+    fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
+    out = {"note": "hbm_bytes_per_launch = 2*FETCH_SIZE + WRITE_SIZE (KiB->bytes), gfx950 correction per "
+                   "MI355X_MICROARCH.md; averages over every launch of the profiled bench run", "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, []), write.get(k, [])
+        fa = sum(f) / len(f) * 1024 if f else 0.0
+        wa = sum(w) / len(w) * 1024 if w else 0.0
+        out["kernels"][k] = {"launches": max(len(f), len(w)), "fetch_bytes_raw": fa, "write_bytes": wa,
+                             "hbm_bytes_per_launch": 2 * fa + wa}
+    json.dump(out, open(sys.argv[3], "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
