@@ -75,7 +75,9 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   spg_ctx* c = new spg_ctx();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipHostMalloc(&c->pinned, 4096) != hipSuccess || hipMalloc(&c->d_counter, 64) != hipSuccess ||
+      hipMemset(c->d_counter, 0, 64) != hipSuccess) {
     delete c;
     return SPG_E_HIP;
   }
@@ -89,6 +91,8 @@ extern "C" int spg_free(spg_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (auto& s : c->ws)
     if (s.p) hipFree(s.p);
+  if (c->pinned) hipHostFree(c->pinned);
+  if (c->d_counter) hipFree(c->d_counter);
   hipEventDestroy(c->ev0);
   hipEventDestroy(c->ev1);
   hipStreamDestroy(c->stream);

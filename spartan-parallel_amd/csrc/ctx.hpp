@@ -13,6 +13,8 @@ struct spg_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  void* pinned = nullptr;          // 4 KiB page-locked host staging for per-round device->host scalars
+  unsigned* d_counter = nullptr;   // grid-reduction ticket (zero between launches)
   double last_us = 0.0;
   std::string err;
   // workspace slots: grown on demand, reused across calls (no allocation in steady state)
@@ -79,6 +81,11 @@ void timer_stop(spg_ctx* c);
 // h_index (-1: g->n). d_out: B x 32 compressed bytes (device). Stream-ordered, no host sync.
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index);
+
+// latency path for small batches (B * n up to a few thousand): same inputs, results left in extended
+// coordinates in d_out (B x Ext, device); the caller encodes them (host).
+int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                     const Fq* d_blinds, Ext* d_out, const uint32_t* d_idx, long h_index);
 
 // per-kernel profiling scope (no-op unless spg_prof_enable(ctx, 1))
 struct KScope {

@@ -116,8 +116,8 @@ SPG_HD Fq fq_sub(const Fq& a, const Fq& b) {
 SPG_HD Fq fq_neg(const Fq& a) { return fq_sub(fq_zero(), a); }
 SPG_HD Fq fq_dbl(const Fq& a) { return fq_add(a, a); }
 
-// CIOS Montgomery product a*b*2^-256 mod q
-SPG_HD Fq fq_mul(const Fq& a, const Fq& b) {
+// CIOS Montgomery product a*b*2^-256 mod q over 8 x 32-bit limbs (the device form: v_mad_u64_u32)
+SPG_HD Fq fq_mul32(const Fq& a, const Fq& b) {
   uint32_t t[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) t[i] = 0;
@@ -151,6 +151,75 @@ SPG_HD Fq fq_mul(const Fq& a, const Fq& b) {
     t[8] = t[9] + c;
   }
   return fq_cond_sub(t, t[8]);
+}
+#if !defined(__HIP_DEVICE_COMPILE__)
+// The same Montgomery product on the host CPU over 4 x 64-bit limbs (64x64->128 multiplies), several
+// times faster there; the Montgomery representative is unique, so both forms agree bit for bit.
+inline Fq fq_mul_host64(const Fq& A, const Fq& B) {
+  typedef unsigned __int128 u128;
+  static const uint64_t q[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0ULL, 0x1000000000000000ULL};
+  const uint64_t INV = 0xd2b51da312547e1bULL;  // -q^{-1} mod 2^64
+  uint64_t a[4], b[4];
+  for (int i = 0; i < 4; i++) {
+    a[i] = (uint64_t)A.l[2 * i] | ((uint64_t)A.l[2 * i + 1] << 32);
+    b[i] = (uint64_t)B.l[2 * i] | ((uint64_t)B.l[2 * i + 1] << 32);
+  }
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 c = (u128)a[0] * b[i] + t0;
+    t0 = (uint64_t)c;
+    c = (c >> 64) + (u128)a[1] * b[i] + t1;
+    t1 = (uint64_t)c;
+    c = (c >> 64) + (u128)a[2] * b[i] + t2;
+    t2 = (uint64_t)c;
+    c = (c >> 64) + (u128)a[3] * b[i] + t3;
+    t3 = (uint64_t)c;
+    c = (c >> 64) + t4;
+    t4 = (uint64_t)c;
+    uint64_t t5 = (uint64_t)(c >> 64);
+    uint64_t m = t0 * INV;
+    c = ((u128)m * q[0] + t0) >> 64;
+    c += (u128)m * q[1] + t1;
+    t0 = (uint64_t)c;
+    c = (c >> 64) + t2;  // q[2] == 0
+    t1 = (uint64_t)c;
+    c = (c >> 64) + (u128)m * q[3] + t3;
+    t2 = (uint64_t)c;
+    c = (c >> 64) + t4;
+    t3 = (uint64_t)c;
+    t4 = t5 + (uint64_t)(c >> 64);
+  }
+  // t < 2q: subtract q once if t >= q
+  uint64_t r[4];
+  u128 d = (u128)t0 - q[0];
+  r[0] = (uint64_t)d;
+  uint64_t bw = (uint64_t)(d >> 64) & 1;
+  d = (u128)t1 - q[1] - bw;
+  r[1] = (uint64_t)d;
+  bw = (uint64_t)(d >> 64) & 1;
+  d = (u128)t2 - q[2] - bw;
+  r[2] = (uint64_t)d;
+  bw = (uint64_t)(d >> 64) & 1;
+  d = (u128)t3 - q[3] - bw;
+  r[3] = (uint64_t)d;
+  bw = (uint64_t)(d >> 64) & 1;
+  const bool keep = bw && !t4;  // t < q
+  const uint64_t o[4] = {keep ? t0 : r[0], keep ? t1 : r[1], keep ? t2 : r[2], keep ? t3 : r[3]};
+  Fq out;
+  for (int i = 0; i < 4; i++) {
+    out.l[2 * i] = (uint32_t)o[i];
+    out.l[2 * i + 1] = (uint32_t)(o[i] >> 32);
+  }
+  return out;
+}
+#endif
+
+SPG_HD Fq fq_mul(const Fq& a, const Fq& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fq_mul32(a, b);
+#else
+  return fq_mul_host64(a, b);
+#endif
 }
 SPG_HD Fq fq_sqr(const Fq& a) { return fq_mul(a, a); }
 // Montgomery -> canonical integer limbs (a * 2^-256 mod q), i.e. Scalar::to_bytes as limbs

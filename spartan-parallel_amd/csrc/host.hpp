@@ -9,10 +9,13 @@
 #pragma once
 #include <string.h>
 
+#include <functional>
 #include <map>
 #include <vector>
 
 #include "curve.hpp"
+#include "hcurve.hpp"
+#include "hpool.hpp"
 #include "keccak.hpp"
 
 namespace spg {
@@ -102,64 +105,93 @@ struct Tape {
   FqV vec(const char* label, size_t n) { return t.challenges(label, n); }
 };
 
-inline Pt compress(const Ext& p) {
+inline Pt compress(const h::HExt& p) {
   Pt c;
-  ext_compress(p, c.b);
+  h::hext_compress(p, c.b);
   return c;
 }
 
-// Fixed-base host scalar multiplication: table[w][j] = j * 2^(8w) * P, 32 windows of 8 bits.
+// Fixed-base host scalar multiplication: tab[w][j] = j * 2^(8w) * P (affine Niels), 32 windows of 8
+// bits, so k * P costs at most 32 mixed additions.
 struct FixedBase {
-  std::vector<Ext> tab;  // 32 * 256
-  void build(const Ext& P) {
-    tab.assign(32 * 256, ext_identity());
-    Ext base = P;
+  std::vector<h::HNiels> tab;  // 32 * 256 (entry 0 of each window unused)
+  void build(const h::HExt& P) {
+    std::vector<h::HExt> ext(32 * 256, h::hext_identity());
+    h::HExt base = P;
     for (int w = 0; w < 32; w++) {
-      tab[w * 256 + 1] = base;
-      for (int j = 2; j < 256; j++) tab[w * 256 + j] = ext_add(tab[w * 256 + j - 1], base);
-      for (int k = 0; k < 8; k++) base = ext_dbl(base);
+      ext[w * 256 + 1] = base;
+      for (int j = 2; j < 256; j++) ext[w * 256 + j] = h::hext_add(ext[w * 256 + j - 1], base);
+      for (int k = 0; k < 8; k++) base = h::hext_dbl(base);
     }
+    h::hext_batch_to_niels(ext, tab);
   }
   // acc += k * P   (k Montgomery)
-  void mul_add(Ext& acc, bool& started, const Fq& k) const {
+  void mul_add(h::HExt& acc, const Fq& k) const {
     uint8_t b[32];
     fq_le_bytes(k, b);
-    for (int w = 0; w < 32; w++) {
-      if (!b[w]) continue;
-      const Ext& e = tab[w * 256 + b[w]];
-      acc = started ? ext_add(acc, e) : e;
-      started = true;
-    }
+    for (int w = 0; w < 32; w++)
+      if (b[w]) acc = h::hext_madd(acc, tab[w * 256 + b[w]]);
   }
 };
 
-// Host view of a generator set for the sigma protocols: fixed-base tables for a few indices.
+// Host view of a generator set for the sigma protocols: fixed-base tables for the few indices used.
 struct HostGens {
   std::map<size_t, FixedBase> fb;
   std::vector<uint8_t> comp;  // compressed stream points (index -> 32 bytes); decompressed on first use
   void init(const uint8_t* compressed, size_t count) { comp.assign(compressed, compressed + 32 * count); }
+  h::HExt point(size_t idx) const {
+    h::HExt P;
+    h::hext_decompress(comp.data() + 32 * idx, P);
+    return P;
+  }
   const FixedBase& get(size_t idx) {
     auto it = fb.find(idx);
     if (it != fb.end()) return it->second;
-    Ext P;
-    ext_decompress(comp.data() + 32 * idx, P);
     FixedBase& f = fb[idx];
-    f.build(P);
+    f.build(point(idx));
     return f;
   }
   // sum_i s_i * P_{idx_i}
-  Ext msm(const std::vector<size_t>& idx, const FqV& s) {
-    Ext acc = ext_identity();
-    bool started = false;
-    for (size_t i = 0; i < idx.size(); i++) get(idx[i]).mul_add(acc, started, s[i]);
+  h::HExt msm(const std::vector<size_t>& idx, const FqV& s) {
+    h::HExt acc = h::hext_identity();
+    for (size_t i = 0; i < idx.size(); i++) get(idx[i]).mul_add(acc, s[i]);
     return acc;
+  }
+  // several independent commitments (index list, scalars) at once on the host pool, encoded
+  std::vector<Pt> commit_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs) {
+    std::vector<std::pair<size_t, size_t>> terms;  // (job, term)
+    for (size_t j = 0; j < jobs.size(); j++) {
+      for (size_t i = 0; i < jobs[j].first.size(); i++) {
+        get(jobs[j].first[i]);  // build tables on this thread (map insertion is not thread-safe)
+        terms.push_back({j, i});
+      }
+    }
+    // the pool only pays for larger bursts: waking workers costs about as much as one scalar multiple
+    const bool par = terms.size() > 16;
+    std::vector<h::HExt> part(terms.size());
+    auto run = [&](int n, const std::function<void(int)>& f) {
+      if (par) pool().parallel_for(n, f);
+      else for (int i = 0; i < n; i++) f(i);
+    };
+    run((int)terms.size(), [&](int k) {
+      const auto& jb = jobs[terms[k].first];
+      h::HExt acc = h::hext_identity();
+      fb.find(jb.first[terms[k].second])->second.mul_add(acc, jb.second[terms[k].second]);
+      part[k] = acc;
+    });
+    std::vector<h::HExt> sum(jobs.size(), h::hext_identity());
+    for (size_t k = 0; k < terms.size(); k++) sum[terms[k].first] = h::hext_add(sum[terms[k].first], part[k]);
+    std::vector<Pt> out(jobs.size());
+    run((int)jobs.size(), [&](int j) { out[j] = compress(sum[j]); });
+    return out;
   }
 };
 
 // variable-base scalar multiplication (k Montgomery), used once per ProductProof (gens_X)
-inline Ext var_mul(const Ext& P, const Fq& k) {
-  Fq c = fq_from_mont(k);
-  return ext_scalar_mul(P, c.l);
+inline h::HExt var_mul(const h::HExt& P, const Fq& k) {
+  uint8_t b[32];
+  fq_le_bytes(k, b);
+  return h::hext_scalar_mul(P, b);
 }
 
 }  // namespace spg

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include "curve.hpp"
+#include "hcurve.hpp"
 #include "keccak.hpp"
 
 using namespace spg;
@@ -90,6 +91,54 @@ void spgh_merlin_simple(const char* label, const char* l1, const uint8_t* m1, si
   Merlin t(label);
   t.message(l1, m1, m1n);
   t.challenge(l2, out, m);
+}
+
+// Host radix-2^51 curve (hcurve.hpp) against the device-form curve on the same inputs: for n uniform
+// 64-byte strings, P_i = from_uniform_bytes; checks compress, decompress->compress, add, dbl, mixed add
+// through batch-normalised Niels, and scalar multiplication by the 32-byte scalars k. Returns the
+// number of mismatches.
+int spgh_hcurve_check(const uint8_t* uni, const uint8_t* k, size_t n) {
+  using namespace spg;
+  int bad = 0;
+  std::vector<Ext> P(n);
+  std::vector<h::HExt> H(n);
+  for (size_t i = 0; i < n; i++) {
+    P[i] = ristretto_from_uniform_bytes(uni + 64 * i);
+    H[i] = h::hext_from_dev(P[i]);
+  }
+  std::vector<h::HNiels> N;
+  h::hext_batch_to_niels(H, N);
+  for (size_t i = 0; i < n; i++) {
+    uint8_t a[32], b[32];
+    ext_compress(P[i], a);
+    h::hext_compress(H[i], b);
+    bad += memcmp(a, b, 32) != 0;
+    h::HExt D;
+    bad += !h::hext_decompress(a, D);
+    h::hext_compress(D, b);
+    bad += memcmp(a, b, 32) != 0;
+    size_t j = (i + 1) % n;
+    ext_compress(ext_add(P[i], P[j]), a);
+    h::hext_compress(h::hext_add(H[i], H[j]), b);
+    bad += memcmp(a, b, 32) != 0;
+    h::hext_compress(h::hext_madd(H[i], N[j]), b);
+    bad += memcmp(a, b, 32) != 0;
+    ext_compress(ext_dbl(P[i]), a);
+    h::hext_compress(h::hext_dbl(H[i]), b);
+    bad += memcmp(a, b, 32) != 0;
+    uint32_t kk[8];
+    for (int w = 0; w < 8; w++)
+      kk[w] = (uint32_t)k[32 * i + 4 * w] | ((uint32_t)k[32 * i + 4 * w + 1] << 8) |
+              ((uint32_t)k[32 * i + 4 * w + 2] << 16) | ((uint32_t)k[32 * i + 4 * w + 3] << 24);
+    ext_compress(ext_scalar_mul(P[i], kk), a);
+    h::hext_compress(h::hext_scalar_mul(H[i], k + 32 * i), b);
+    bad += memcmp(a, b, 32) != 0;
+  }
+  uint8_t bad_enc[32];
+  memset(bad_enc, 0xff, 32);
+  h::HExt X;
+  bad += h::hext_decompress(bad_enc, X);  // non-canonical must be rejected
+  return bad;
 }
 
 }  // extern "C"

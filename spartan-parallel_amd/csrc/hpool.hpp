@@ -1,0 +1,100 @@
+// spg — a small persistent host worker pool for the prover's sequential-protocol work.
+// Between two Fiat-Shamir challenges the prover computes a handful of independent fixed-base
+// commitments and point encodings (tens of microseconds each); running them on several host cores
+// shortens every sumcheck round. Workers park on a condition variable between bursts.
+//
+// Task indices are claimed with a CAS on one 64-bit word holding (burst generation, next index), and
+// every worker works from a snapshot (generation, function, count) taken under the mutex, so a worker
+// that wakes late can never run a task of a newer burst with an older function or vice versa.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace spg {
+
+class Pool {
+ public:
+  explicit Pool(int nthreads) {
+    for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+  // runs f(0) .. f(n-1) on the pool and the calling thread; returns when all are done
+  void parallel_for(int n, const std::function<void(int)>& f) {
+    if (n <= 1 || threads_.empty()) {
+      for (int i = 0; i < n; i++) f(i);
+      return;
+    }
+    std::lock_guard<std::mutex> call(call_mu_);  // one burst at a time
+    uint32_t g;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      g = ++gen_;
+      fn_ = &f;
+      n_ = n;
+      remaining_.store(n);
+      next_.store((uint64_t)g << 32);
+    }
+    cv_.notify_all();
+    work(g, &f, n);
+    while (remaining_.load() > 0) std::this_thread::yield();
+  }
+
+ private:
+  void work(uint32_t g, const std::function<void(int)>* f, int n) {
+    for (;;) {
+      uint64_t v = next_.load();
+      if ((uint32_t)(v >> 32) != g || (int)(uint32_t)v >= n) return;
+      if (!next_.compare_exchange_weak(v, v + 1)) continue;
+      (*f)((int)(uint32_t)v);
+      remaining_.fetch_sub(1);
+    }
+  }
+  void worker() {
+    uint32_t seen = 0;
+    for (;;) {
+      uint32_t g;
+      const std::function<void(int)>* f;
+      int n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = g = gen_;
+        f = fn_;
+        n = n_;
+      }
+      work(g, f, n);
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0;
+  uint32_t gen_ = 0;
+  std::atomic<uint64_t> next_{0};
+  std::atomic<int> remaining_{0};
+  bool quit_ = false;
+};
+
+inline Pool& pool() {
+  static Pool p([] {
+    unsigned hw = std::thread::hardware_concurrency();
+    int n = hw > 1 ? (int)hw - 1 : 0;
+    return n > 7 ? 7 : n;
+  }());
+  return p;
+}
+
+}  // namespace spg

@@ -24,12 +24,15 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "hcurve.hpp"
 #include "keccak.hpp"
 
 namespace spg {
 
 static const int kItemK = 16;  // entries summed per work item
 static const int kSegM = 8;    // buckets per running-sum segment (k_segments)
+static const size_t kSmallMaxB = 4;       // latency path: at most this many MSMs per call ...
+static const size_t kSmallMaxN = 16384;   // ... of at most this many points each
 
 // ------------------------------------------------------------------ generators
 __global__ void k_map_uniform(const uint8_t* __restrict__ uni, Niels* __restrict__ out, uint8_t* __restrict__ comp,
@@ -246,6 +249,140 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
     ext_compress(val, c);
     for (int k = 0; k < 32; k++) out[32 * (size_t)b + k] = c[k];
   }
+}
+
+// ------------------------------------------------------------------ latency path for small MSMs
+// Bullet rounds and single commitments are MSMs of ~10^3 points whose cost is the depth of the
+// dependent group additions, not their count. One block per (msm, bucket value v): every thread
+// scans a slice of the scalars, recomputes their signed c-bit digits and mixed-adds the table entry
+// of every digit with |d| == v; an LDS tree sums the block. A second kernel forms sum_v v * B_v with
+// an LDS suffix scan + tree. Results stay in extended coordinates: the host encodes them (the
+// inverse square root of the encoding is ~250 dependent squarings, cheap on a CPU core, slow on one
+// GPU lane).
+// `blinds` must be a valid pointer even when has_blind == 0: blinds[b] has a wave-uniform address, so
+// the compiler issues it as a scalar load inside a divergent branch, and scalar loads are not masked
+// by EXEC when the branch is skipped (a null pointer there faults).
+template <int C>
+__global__ void __launch_bounds__(256) k_smsm_bucket(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
+                                                     const Fq* __restrict__ blinds, int has_blind, int n, int n1,
+                                                     int gen_offset, int h_index, const Niels* __restrict__ tab,
+                                                     Ext* __restrict__ buckets) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  __shared__ Ext sh[256];
+  const int v = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x;
+  const int per = n + has_blind;
+  Ext acc = ext_identity();
+  for (int i = t; i < per; i += 256) {
+    Fq s;
+    uint32_t gidx;
+    if (i < n) {
+      s = scalars[(size_t)b * n + i];
+      gidx = idx ? idx[(size_t)b * n + i] : (uint32_t)(gen_offset + i);
+    } else {
+      s = blinds[b];
+      gidx = (uint32_t)h_index;
+    }
+    Fq k = fq_from_mont(s);
+    int carry = 0;
+    uint64_t hit = 0, neg = 0;  // windows whose digit is +-v (W <= 64)
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int bit = w * C;
+      const int li = bit >> 5, of = bit & 31;
+      uint32_t x = k.l[li] >> of;
+      if (of + C > 32 && li + 1 < 8) x |= k.l[li + 1] << (32 - of);
+      int d = (int)(x & MASK) + carry;
+      carry = d > NB ? 1 : 0;
+      d -= carry << C;
+      if (d == v || d == -v) hit |= 1ull << w;
+      if (d == -v) neg |= 1ull << w;
+    }
+    while (hit) {
+      const int w = __ffsll((long long)hit) - 1;
+      hit &= hit - 1;
+#ifdef SPG_CHECKED
+      if (w < 0 || w >= W || gidx >= (uint32_t)n1) {
+        printf("k_smsm_bucket<%d>: bad index w=%d gidx=%u n1=%d i=%d b=%d v=%d\n", C, w, gidx, n1, i, b, v);
+        continue;
+      }
+#endif
+      acc = ext_madd(acc, tab[(size_t)(w * C) * n1 + gidx], (neg >> w) & 1);
+    }
+  }
+  for (int d = 128; d >= 1; d >>= 1) {
+    sh[t] = acc;
+    __syncthreads();
+    if (t < d) acc = ext_add(acc, sh[t + d]);
+    __syncthreads();
+  }
+  if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
+}
+
+// one block of NB threads per MSM: sum_v v * B_v = sum_t (sum_{u >= t} B_u)
+__global__ void __launch_bounds__(256) k_smsm_final(const Ext* __restrict__ buckets, int NB, Ext* __restrict__ out) {
+  __shared__ Ext sh[256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  Ext suf = buckets[(size_t)b * NB + t];
+  for (int d = 1; d < NB; d <<= 1) {
+    sh[t] = suf;
+    __syncthreads();
+    if (t + d < NB) suf = ext_add(suf, sh[t + d]);
+    __syncthreads();
+  }
+  for (int d = NB / 2; d >= 1; d >>= 1) {
+    sh[t] = suf;
+    __syncthreads();
+    if (t < d) suf = ext_add(suf, sh[t + d]);
+    __syncthreads();
+  }
+  if (t == 0) out[b] = suf;
+}
+
+static int pick_small_window(size_t per) {
+  const char* e = getenv("SPG_SMSM_C");
+  if (e) {
+    int c = atoi(e);
+    if (c >= 4 && c <= 9) return c;
+  }
+  // measured on MI355X (scripts/perf_small_msm.py): n = 130 -> c = 7, n = 1028 and 4098 -> c = 8
+  return per <= 512 ? 7 : 8;
+}
+
+template <int C>
+static void launch_small(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const Fq* bl, int n, int n1, int off, int h, const Niels* tab,
+                         Ext* bk, Ext* out, int B, hipStream_t s) {
+  constexpr int NB = 1 << (C - 1);
+  {
+    KScope ks(ctx, "msm_small_bucket");
+    hipLaunchKernelGGL(k_smsm_bucket<C>, dim3(NB, B), dim3(256), 0, s, sc, idx, bl ? bl : sc, bl ? 1 : 0, n, n1, off,
+                       h, tab, bk);
+  }
+  KScope ks(ctx, "msm_small_final");
+  hipLaunchKernelGGL(k_smsm_final, dim3(B), dim3(NB), 0, s, bk, NB, out);
+}
+
+int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                     const Fq* d_blinds, Ext* d_out, const uint32_t* d_idx, long h_index) {
+  hipStream_t s = ctx->stream;
+  const size_t per = n + (d_blinds ? 1 : 0);
+  const int c = pick_small_window(per);
+  const int NB = 1 << (c - 1);
+  SPG_CHECK(ctx, B <= 65535, "msm batch too large for the latency path");
+  Ext* bk = (Ext*)ws_get(ctx, 13, B * (size_t)NB * sizeof(Ext) + 64);
+  if (!bk) return set_err(ctx, SPG_E_NOMEM, "small msm workspace");
+  const int n1 = (int)(g->n + 1), off = (int)gen_offset, h = h_index < 0 ? (int)g->n : (int)h_index;
+  switch (c) {
+    case 4: launch_small<4>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
+    case 5: launch_small<5>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
+    case 6: launch_small<6>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
+    case 7: launch_small<7>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
+    case 8: launch_small<8>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
+    default: launch_small<9>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
 }
 
 // ------------------------------------------------------------------ host orchestration
@@ -508,12 +645,23 @@ static int msm_host(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const ui
   uint8_t* d_out = (uint8_t*)(d_s + B * n + B);
   if (n) SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, s));
   if (blinds) SPG_HIP(ctx, hipMemcpyAsync(d_bl, blinds, B * sizeof(Fq), hipMemcpyHostToDevice, s));
+  const bool small = B <= kSmallMaxB && n + (blinds ? 1 : 0) <= kSmallMaxN;
+  Ext* d_ext = small ? (Ext*)ws_get(ctx, 14, B * sizeof(Ext) + 64) : nullptr;
+  if (small && !d_ext) return set_err(ctx, SPG_E_NOMEM, "msm output");
   timer_start(ctx);
-  int rc = msm_batch_device(ctx, g, gen_offset, d_s, n, B, d_bl, d_out, nullptr, -1);
+  int rc = small ? msm_small_device(ctx, g, gen_offset, d_s, n, B, d_bl, d_ext, nullptr, -1)
+                 : msm_batch_device(ctx, g, gen_offset, d_s, n, B, d_bl, d_out, nullptr, -1);
   if (rc) return rc;
   timer_stop(ctx);
-  SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, s));
-  SPG_HIP(ctx, hipStreamSynchronize(s));
+  if (small) {
+    std::vector<Ext> r(B);
+    SPG_HIP(ctx, hipMemcpyAsync(r.data(), d_ext, B * sizeof(Ext), hipMemcpyDeviceToHost, s));
+    SPG_HIP(ctx, hipStreamSynchronize(s));
+    for (size_t b = 0; b < B; b++) h::hext_compress(h::hext_from_dev(r[b]), out + 32 * b);
+  } else {
+    SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, s));
+    SPG_HIP(ctx, hipStreamSynchronize(s));
+  }
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
   ctx->last_us = ms * 1000.0;

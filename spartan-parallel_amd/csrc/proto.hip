@@ -5,6 +5,8 @@
 // per-generator weights cw that are products of u / u^-1. So every L, R (and the final g_hat) is a
 // fixed-base MSM over the generator table already resident in HBM (msm.hip); no curve point is ever
 // folded and the group elements produced are identical to the reference's.
+#include <functional>
+
 #include "proto.hpp"
 
 namespace spg {
@@ -15,7 +17,7 @@ static Fq dot(const FqV& a, const FqV& b, size_t ao, size_t bo, size_t n) {
   return s;
 }
 
-Ext commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& blind) {
+h::HExt commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& blind) {
   std::vector<size_t> idx(k.G.begin(), k.G.begin() + x.size());
   idx.push_back(k.h);
   FqV s(x);
@@ -23,18 +25,36 @@ Ext commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& blind) 
   return g.host.msm(idx, s);
 }
 
+// independent commitments computed together on the host pool (Commitments::commit, src/commitments.rs:69-92)
+std::vector<Pt> commit_batch(ProverGens& g, const std::vector<CJob>& jobs) {
+  std::vector<std::pair<std::vector<size_t>, FqV>> j2;
+  for (auto& j : jobs) {
+    std::vector<size_t> idx;
+    FqV s;
+    if (j.k) {
+      idx.assign(j.k->G.begin(), j.k->G.begin() + j.x.size());
+      s = j.x;
+    }
+    idx.push_back(j.h);
+    s.push_back(j.blind);
+    j2.push_back({idx, s});
+  }
+  return g.host.commit_many(j2);
+}
+
 // src/nizk/mod.rs:27-53
 KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C) {
   t.protocol("knowledge proof");
   Fq t1 = tape.scalar("t1"), t2 = tape.scalar("t2");
-  *C = compress(commit_host(g, k, {x}, r));
+  std::vector<Pt> c = commit_batch(g, {CJob(k, {x}, r), CJob(k, {t1}, t2)});
+  *C = c[0];
   t.point("C", *C);
   KnowledgeProofP p;
-  p.alpha = compress(commit_host(g, k, {t1}, t2));
+  p.alpha = c[1];
   t.point("alpha", p.alpha);
-  Fq c = t.challenge("c");
-  p.z1 = fq_add(fq_mul(x, c), t1);
-  p.z2 = fq_add(fq_mul(r, c), t2);
+  Fq ch = t.challenge("c");
+  p.z1 = fq_add(fq_mul(x, ch), t1);
+  p.z2 = fq_add(fq_mul(r, ch), t2);
   return p;
 }
 
@@ -43,15 +63,14 @@ EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape
                               const Fq& v2, const Fq& s2) {
   t.protocol("equality proof");
   Fq r = tape.scalar("r");
-  Pt C1 = compress(commit_host(g, k, {v1}, s1));
-  t.point("C1", C1);
-  Pt C2 = compress(commit_host(g, k, {v2}, s2));
-  t.point("C2", C2);
+  std::vector<Pt> c = commit_batch(g, {CJob(k, {v1}, s1), CJob(k, {v2}, s2), CJob(k.h, r)});
+  t.point("C1", c[0]);
+  t.point("C2", c[1]);
   EqualityProofP p;
-  p.alpha = compress(g.host.msm({k.h}, {r}));
+  p.alpha = c[2];
   t.point("alpha", p.alpha);
-  Fq c = t.challenge("c");
-  p.z = fq_add(fq_mul(c, fq_sub(s1, s2)), r);
+  Fq ch = t.challenge("c");
+  p.z = fq_add(fq_mul(ch, fq_sub(s1, s2)), r);
   return p;
 }
 
@@ -61,57 +80,79 @@ ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, 
   t.protocol("product proof");
   Fq b1 = tape.scalar("b1"), b2 = tape.scalar("b2"), b3 = tape.scalar("b3"), b4 = tape.scalar("b4"),
      b5 = tape.scalar("b5");
-  Ext Xe = commit_host(g, k, {x}, rX);
-  *X = compress(Xe);
+  std::vector<Pt> c = commit_batch(
+      g, {CJob(k, {x}, rX), CJob(k, {y}, rY), CJob(k, {z}, rZ), CJob(k, {b1}, b2), CJob(k, {b3}, b4)});
+  *X = c[0];
+  *Y = c[1];
+  *Z = c[2];
   t.point("X", *X);
-  *Y = compress(commit_host(g, k, {y}, rY));
   t.point("Y", *Y);
-  *Z = compress(commit_host(g, k, {z}, rZ));
   t.point("Z", *Z);
   ProductProofP p;
-  p.alpha = compress(commit_host(g, k, {b1}, b2));
+  p.alpha = c[3];
   t.point("alpha", p.alpha);
-  p.beta = compress(commit_host(g, k, {b3}, b4));
+  p.beta = c[4];
   t.point("beta", p.beta);
   // gens_X = {G: [X.decompress()], h}: X is used through its encoding, as the reference does
-  Ext Xd;
-  ext_decompress(X->b, Xd);
-  Ext dl = ext_add(var_mul(Xd, b3), g.host.msm({k.h}, {b5}));
+  h::HExt Xd;
+  h::hext_decompress(X->b, Xd);
+  h::HExt dl = h::hext_add(var_mul(Xd, b3), g.host.msm({k.h}, {b5}));
   p.delta = compress(dl);
   t.point("delta", p.delta);
-  Fq c = t.challenge("c");
-  p.z[0] = fq_add(b1, fq_mul(c, x));
-  p.z[1] = fq_add(b2, fq_mul(c, rX));
-  p.z[2] = fq_add(b3, fq_mul(c, y));
-  p.z[3] = fq_add(b4, fq_mul(c, rY));
-  p.z[4] = fq_add(b5, fq_mul(c, fq_sub(rZ, fq_mul(rX, y))));
+  Fq ch = t.challenge("c");
+  p.z[0] = fq_add(b1, fq_mul(ch, x));
+  p.z[1] = fq_add(b2, fq_mul(ch, rX));
+  p.z[2] = fq_add(b3, fq_mul(ch, y));
+  p.z[3] = fq_add(b4, fq_mul(ch, rY));
+  p.z[4] = fq_add(b5, fq_mul(ch, fq_sub(rZ, fq_mul(rX, y))));
   return p;
 }
 
-// src/nizk/mod.rs:306-370 (n = 4 in every sumcheck round)
+// src/nizk/mod.rs:306-370 (n = 4 in every sumcheck round). Cx_known: the caller already holds
+// x.commit(blind_x, gens_n) (the sumcheck round's comm_poly is exactly that commitment).
 DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyView& kn, Tr& t, Tape& tape, const FqV& x,
-                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y) {
+                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y, const Pt* Cx_known) {
   t.protocol("dot product proof");
   size_t n = x.size();
   FqV d = tape.vec("d_vec", n);
   Fq r_delta = tape.scalar("r_delta"), r_beta = tape.scalar("r_beta");
-  Pt Cx = compress(commit_host(g, kn, x, blind_x));
+  Fq ad = dot(a, d, 0, 0, n);
+  std::vector<CJob> jobs = {CJob(k1, {y}, blind_y), CJob(kn, d, r_delta), CJob(k1, {ad}, r_beta)};
+  if (!Cx_known) jobs.push_back(CJob(kn, x, blind_x));
+  std::vector<Pt> c = commit_batch(g, jobs);
+  Pt Cx = Cx_known ? *Cx_known : c[3];
   t.point("Cx", Cx);
-  Pt Cy = compress(commit_host(g, k1, {y}, blind_y));
-  t.point("Cy", Cy);
+  t.point("Cy", c[0]);
   t.scalars("a", a);
   DotProductProofP p;
-  p.delta = compress(commit_host(g, kn, d, r_delta));
+  p.delta = c[1];
   t.point("delta", p.delta);
-  Fq ad = dot(a, d, 0, 0, n);
-  p.beta = compress(commit_host(g, k1, {ad}, r_beta));
+  p.beta = c[2];
   t.point("beta", p.beta);
-  Fq c = t.challenge("c");
+  Fq ch = t.challenge("c");
   p.z.resize(n);
-  for (size_t i = 0; i < n; i++) p.z[i] = fq_add(fq_mul(c, x[i]), d[i]);
-  p.z_delta = fq_add(fq_mul(c, blind_x), r_delta);
-  p.z_beta = fq_add(fq_mul(c, blind_y), r_beta);
+  for (size_t i = 0; i < n; i++) p.z[i] = fq_add(fq_mul(ch, x[i]), d[i]);
+  p.z_delta = fq_add(fq_mul(ch, blind_x), r_delta);
+  p.z_beta = fq_add(fq_mul(ch, blind_y), r_beta);
   return p;
+}
+
+// B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
+static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& hs, size_t n, size_t B,
+                           const uint32_t* d_idx, std::vector<Pt>* out) {
+  hipStream_t s = ctx->stream;
+  Fq* d_s = (Fq*)ws_get(ctx, 20, hs.size() * sizeof(Fq) + 64);
+  Ext* d_o = (Ext*)ws_get(ctx, 22, sizeof(Ext) * B + 64);
+  if (!d_s || !d_o) return set_err(ctx, SPG_E_NOMEM, "device_msm");
+  SPG_HIP(ctx, hipMemcpyAsync(d_s, hs.data(), hs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
+  int rc = msm_small_device(ctx, g.dev, 0, d_s, n, B, nullptr, d_o, d_idx, -1);
+  if (rc) return rc;
+  std::vector<Ext> res(B);
+  SPG_HIP(ctx, hipMemcpyAsync(res.data(), d_o, sizeof(Ext) * B, hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  out->resize(B);
+  pool().parallel_for((int)B, [&](int b) { (*out)[b] = compress(h::hext_from_dev(res[b])); });
+  return 0;
 }
 
 int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars,
@@ -127,19 +168,16 @@ int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars,
       hi[b * n + i] = idx[b][i];
     }
   }
-  hipStream_t s = ctx->stream;
-  Fq* d_s = (Fq*)ws_get(ctx, 20, hs.size() * sizeof(Fq) + 64);
   uint32_t* d_i = (uint32_t*)ws_get(ctx, 21, hi.size() * 4 + 64);
-  uint8_t* d_o = (uint8_t*)ws_get(ctx, 22, 32 * B + 64);
-  if (!d_s || !d_i || !d_o) return set_err(ctx, SPG_E_NOMEM, "device_msm_idx");
-  SPG_HIP(ctx, hipMemcpyAsync(d_s, hs.data(), hs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
-  SPG_HIP(ctx, hipMemcpyAsync(d_i, hi.data(), hi.size() * 4, hipMemcpyHostToDevice, s));
-  int rc = msm_batch_device(ctx, g.dev, 0, d_s, n, B, nullptr, d_o, d_i, -1);
-  if (rc) return rc;
-  out->resize(B);
-  SPG_HIP(ctx, hipMemcpyAsync(out->data(), d_o, 32 * B, hipMemcpyDeviceToHost, s));
-  SPG_HIP(ctx, hipStreamSynchronize(s));
-  return 0;
+  if (!d_i) return set_err(ctx, SPG_E_NOMEM, "device_msm_idx");
+  SPG_HIP(ctx, hipMemcpyAsync(d_i, hi.data(), hi.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  return device_msm_flat(ctx, g, hs, n, B, d_i, out);
+}
+
+// runs f(lo, hi) over [0, n) in chunks on the host pool
+static void par_range(size_t n, const std::function<void(size_t, size_t)>& f) {
+  const size_t chunks = n >= 256 ? 8 : 1;
+  pool().parallel_for((int)chunks, [&](int c) { f(n * c / chunks, n * (c + 1) / chunks); });
 }
 
 // src/nizk/mod.rs:439-523 + src/nizk/bullet.rs:32-132
@@ -157,22 +195,29 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   FqV v2 = tape.vec("blinds_vec_2", 2 * lg);
   const KeyView& kn = g.gens_n;
   const uint32_t G1 = (uint32_t)g.gens_1.G[0], H = (uint32_t)kn.h;
-  std::vector<uint32_t> idx_full(n + 2);
-  for (size_t j = 0; j < n; j++) idx_full[j] = (uint32_t)kn.G[j];
-  idx_full[n] = G1;
-  idx_full[n + 1] = H;
+  // generator indices G_0..G_{n-1}, G_1, h for B = 2 MSMs, uploaded once for all rounds
+  const size_t n2 = n + 2;
+  std::vector<uint32_t> idx2(2 * n2);
+  for (size_t b = 0; b < 2; b++) {
+    for (size_t j = 0; j < n; j++) idx2[b * n2 + j] = (uint32_t)kn.G[j];
+    idx2[b * n2 + n] = G1;
+    idx2[b * n2 + n + 1] = H;
+  }
+  uint32_t* d_idx = (uint32_t*)ws_get(ctx, 21, idx2.size() * 4 + 64);
+  if (!d_idx) return set_err(ctx, SPG_E_NOMEM, "bullet indices");
+  SPG_HIP(ctx, hipMemcpyAsync(d_idx, idx2.data(), idx2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   // Cx = x.commit(blind_x, gens_n)
   std::vector<Pt> pts;
+  std::vector<Fq> hs(2 * n2, fq_zero());
   {
-    FqV s(x);
-    s.push_back(fq_zero());
-    s.push_back(blind_x);
-    int rc = device_msm_idx(ctx, g, {s}, {idx_full}, &pts);
+    std::copy(x.begin(), x.end(), hs.begin());
+    hs[n + 1] = blind_x;
+    int rc = device_msm_flat(ctx, g, std::vector<Fq>(hs.begin(), hs.begin() + n2), n2, 1, d_idx, &pts);
     if (rc) return rc;
   }
   Pt Cx = pts[0];
   t.point("Cx", Cx);
-  Pt Cy = compress(commit_host(g, g.gens_1, {y}, blind_y));
+  Pt Cy = commit_batch(g, {CJob(g.gens_1, {y}, blind_y)})[0];
   t.point("Cy", Cy);
   t.scalars("a", a);
   Fq r = t.challenge("r");
@@ -183,27 +228,38 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     size_t nh = nk / 2;
     Fq cL = dot(aa, bb, 0, nh, nh), cR = dot(aa, bb, nh, 0, nh);
     Fq blind_L = v1[k], blind_R = v2[k];
-    FqV sL(n + 2, fq_zero()), sR(n + 2, fq_zero());
-    for (size_t j = 0; j < n; j++) {
-      size_t m = j % nk;
-      if (m >= nh) sL[j] = fq_mul(aa[m - nh], cw[j]);
-      else sR[j] = fq_mul(aa[m + nh], cw[j]);
-    }
-    sL[n] = fq_mul(cL, r);
-    sL[n + 1] = blind_L;
-    sR[n] = fq_mul(cR, r);
-    sR[n + 1] = blind_R;
-    int rc = device_msm_idx(ctx, g, {sL, sR}, {idx_full, idx_full}, &pts);
+    // L scalars in hs[0 .. n2), R scalars in hs[n2 .. 2 n2)
+    par_range(n, [&](size_t lo, size_t hi) {
+      for (size_t j = lo; j < hi; j++) {
+        size_t m = j % nk;
+        if (m >= nh) {
+          hs[j] = fq_mul(aa[m - nh], cw[j]);
+          hs[n2 + j] = fq_zero();
+        } else {
+          hs[j] = fq_zero();
+          hs[n2 + j] = fq_mul(aa[m + nh], cw[j]);
+        }
+      }
+    });
+    hs[n] = fq_mul(cL, r);
+    hs[n + 1] = blind_L;
+    hs[n2 + n] = fq_mul(cR, r);
+    hs[n2 + n + 1] = blind_R;
+    int rc = device_msm_flat(ctx, g, hs, n2, 2, d_idx, &pts);
     if (rc) return rc;
     t.point("L", pts[0]);
     t.point("R", pts[1]);
     Fq u = t.challenge("u");
     Fq uinv = fq_inv(u);
-    for (size_t i = 0; i < nh; i++) {
-      aa[i] = fq_add(fq_mul(aa[i], u), fq_mul(uinv, aa[i + nh]));
-      bb[i] = fq_add(fq_mul(bb[i], uinv), fq_mul(u, bb[i + nh]));
-    }
-    for (size_t j = 0; j < n; j++) cw[j] = fq_mul(cw[j], (j % nk) < nh ? uinv : u);
+    par_range(nh, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; i++) {
+        aa[i] = fq_add(fq_mul(aa[i], u), fq_mul(uinv, aa[i + nh]));
+        bb[i] = fq_add(fq_mul(bb[i], uinv), fq_mul(u, bb[i + nh]));
+      }
+    });
+    par_range(n, [&](size_t lo, size_t hi) {
+      for (size_t j = lo; j < hi; j++) cw[j] = fq_mul(cw[j], (j % nk) < nh ? uinv : u);
+    });
     blind_fin = fq_add(fq_add(blind_fin, fq_mul(fq_mul(blind_L, u), u)), fq_mul(fq_mul(blind_R, uinv), uinv));
     out->L.push_back(pts[0]);
     out->R.push_back(pts[1]);
@@ -215,15 +271,17 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   Fq y_hat = fq_mul(x_hat, a_hat);
   // delta = d * g_hat + r_delta * h with g_hat = sum_j cw[j] G_j
   {
-    FqV s(n + 2, fq_zero());
-    for (size_t j = 0; j < n; j++) s[j] = fq_mul(d, cw[j]);
+    std::vector<Fq> s(n2, fq_zero());
+    par_range(n, [&](size_t lo, size_t hi) {
+      for (size_t j = lo; j < hi; j++) s[j] = fq_mul(d, cw[j]);
+    });
     s[n + 1] = r_delta;
-    int rc = device_msm_idx(ctx, g, {s}, {idx_full}, &pts);
+    int rc = device_msm_flat(ctx, g, s, n2, 1, d_idx, &pts);
     if (rc) return rc;
   }
   out->delta = pts[0];
   t.point("delta", out->delta);
-  out->beta = compress(g.host.msm({G1, H}, {fq_mul(d, r), r_beta}));
+  out->beta = g.host.commit_many({{{(size_t)G1, (size_t)H}, {fq_mul(d, r), r_beta}}})[0];
   t.point("beta", out->beta);
   Fq c = t.challenge("c");
   out->z1 = fq_add(d, fq_mul(c, y_hat));

@@ -101,14 +101,25 @@ struct ProverGens {
 };
 
 // ---- sigma protocols (host; O(1) points) ----
-Ext commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& blind);
+h::HExt commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& blind);
+// one commitment x.commit(blind, k) (or blind * h alone when k is null)
+struct CJob {
+  const KeyView* k = nullptr;
+  size_t h = 0;
+  FqV x;
+  Fq blind;
+  CJob(const KeyView& kv, const FqV& xx, const Fq& b) : k(&kv), h(kv.h), x(xx), blind(b) {}
+  CJob(size_t h_index, const Fq& b) : k(nullptr), h(h_index), blind(b) {}
+};
+std::vector<Pt> commit_batch(ProverGens& g, const std::vector<CJob>& jobs);
 KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C);
 EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& v1, const Fq& s1,
                               const Fq& v2, const Fq& s2);
 ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& rX, const Fq& y,
                             const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z);
 DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyView& kn, Tr& t, Tape& tape, const FqV& x,
-                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y);
+                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y,
+                                  const Pt* Cx_known = nullptr);
 // ---- DotProductProofLog with all MSMs on the GPU over the original generators ----
 int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const FqV& x, const Fq& blind_x, const FqV& a,
                          const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy);

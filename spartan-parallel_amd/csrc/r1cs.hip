@@ -10,6 +10,10 @@
 //   Bulletproof L/R/delta MSMs                                    proto.hip
 // Host work: the Fiat-Shamir transcript, the round polynomials (4 scalars), the sigma protocols over
 // <= 5 fixed generators, and the bincode writer. Per sumcheck round exactly three scalars come back.
+#include <chrono>
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "proto.hpp"
 #include "sumcheck.hpp"
 
@@ -244,25 +248,26 @@ struct ZKRounds {
   Pt comm_claim;
   ZKSumcheckP out;
   FqV poly;
+  Pt comm_poly;
   void init(ProverGens& g, Tape& tape, size_t rounds, const Fq& c, const Fq& b) {
     blinds_poly = tape.vec("blinds_poly", rounds);
     blinds_evals = tape.vec("blinds_evals", rounds);
     claim = c;
     blind_claim = b;
-    comm_claim = compress(commit_host(g, g.gens_1, {c}, b));
+    comm_claim = commit_batch(g, {CJob(g.gens_1, {c}, b)})[0];
   }
   // commit the round polynomial and draw r_j
   Fq begin(ProverGens& g, Tr& t, size_t j, const Fq e[3]) {
     Fq ev[4] = {e[0], fq_sub(claim, e[0]), e[1], e[2]};
     poly = uni_from_evals3(ev);
-    Pt cp = compress(commit_host(g, g.gens_4, poly, blinds_poly[j]));
-    t.point("comm_poly", cp);
-    out.comm_polys.push_back(cp);
+    comm_poly = commit_batch(g, {CJob(g.gens_4, poly, blinds_poly[j])})[0];
+    t.point("comm_poly", comm_poly);
+    out.comm_polys.push_back(comm_poly);
     return t.challenge("challenge_nextround");
   }
   void finish(ProverGens& g, Tr& t, Tape& tape, size_t j, const Fq& r_j) {
     Fq eval = uni_eval(poly, r_j);
-    Pt comm_eval = compress(commit_host(g, g.gens_1, {eval}, blinds_evals[j]));
+    Pt comm_eval = commit_batch(g, {CJob(g.gens_1, {eval}, blinds_evals[j])})[0];
     t.point("comm_claim_per_round", comm_claim);
     t.point("comm_eval", comm_eval);
     FqV w = t.challenges("combine_two_claims_to_one", 2);
@@ -277,7 +282,8 @@ struct ZKRounds {
       a[k] = fq_add(fq_mul(w[0], a_sc), fq_mul(w[1], pw));
       pw = fq_mul(pw, r_j);
     }
-    out.proofs.push_back(dotproduct_prove(g, g.gens_1, g.gens_4, t, tape, poly, blinds_poly[j], a, target, blind));
+    out.proofs.push_back(
+        dotproduct_prove(g, g.gens_1, g.gens_4, t, tape, poly, blinds_poly[j], a, target, blind, &comm_poly));
     claim = eval;
     comm_claim = comm_eval;
     out.comm_evals.push_back(comm_eval);
@@ -291,6 +297,33 @@ static int d2h_fq(spg_ctx* ctx, const Fq* d, Fq* h, size_t n = 1) {
 }
 
 static unsigned blocks_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+// host wall-clock breakdown of one prove (printed to stderr when SPG_TRACE is set)
+struct Laps {
+  bool on = getenv("SPG_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::vector<std::pair<std::string, double>> acc;
+  void lap(const char* name) {
+    if (!on) return;
+    auto now = std::chrono::steady_clock::now();
+    double us = std::chrono::duration<double, std::micro>(now - t).count();
+    t = now;
+    for (auto& a : acc)
+      if (a.first == name) {
+        a.second += us;
+        return;
+      }
+    acc.push_back({name, us});
+  }
+  void print() {
+    if (!on) return;
+    double tot = 0;
+    for (auto& a : acc) tot += a.second;
+    fprintf(stderr, "[spg] R1CSProof::prove host breakdown (us):");
+    for (auto& a : acc) fprintf(stderr, " %s=%.0f", a.first.c_str(), a.second);
+    fprintf(stderr, " total=%.0f\n", tot);
+  }
+};
 
 // device eq table of a host vector (uploads through the kernel argument)
 static int eq_table(spg_ctx* ctx, const FqV& r, Fq* out) { return dev_eq_table(ctx, r.data(), (int)r.size(), out); }
@@ -333,9 +366,17 @@ struct Prover {
   }
 
   int run();
+  int run_inner(Laps& lp);
 };
 
 int Prover::run() {
+  Laps lp;
+  int rc0 = run_inner(lp);
+  lp.print();
+  return rc0;
+}
+
+int Prover::run_inner(Laps& lp) {
   hipStream_t s = ctx->stream;
   t.protocol("R1CS proof");
   size_t num_cons = inst.max_num_cons;
@@ -463,6 +504,7 @@ int Prover::run() {
     SPG_HIP(ctx, hipGetLastError());
   }
 
+  lp.lap("setup");
   Fq* partials = (Fq*)ws_get(ctx, WS_PART, 3 * 1024 * sizeof(Fq) + 64);
   Fq* d_out3 = (Fq*)ws_get(ctx, WS_OUT3, 4 * sizeof(Fq) + 64);
   if (!partials || !d_out3) return set_err(ctx, SPG_E_NOMEM, "partials");
@@ -478,7 +520,9 @@ int Prover::run() {
     size_t cons_len = (size_t)1 << nx, proof_len = (size_t)1 << nq, instance_len = (size_t)1 << np;
     size_t lenP = instance_len, lenQ = proof_len, lenX = cons_len;
     std::vector<size_t> sc_np = num_proofs, sc_nc = block_num_cons;
-    for (size_t j = 0; j < rounds; j++) {
+    // round j's evaluation is enqueued right after round j-1's folds, so it runs on the device while the
+    // host finishes round j-1's proof (comm_eval, DotProductProof); eval_wait then collects (e0, e2, e3)
+    auto launch_eval = [&](size_t j) -> int {
       int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       if (cons_len > 1) cons_len /= 2;
       else if (proof_len > 1) proof_len /= 2;
@@ -487,17 +531,28 @@ int Prover::run() {
         if (mode == MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
         if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
       }
+      return phase1_eval(ctx, Az, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap, Aq, Ax, Az.d, Bz, Cz,
+                         partials, d_out3, nullptr);
+    };
+    if (rounds) rc = launch_eval(0);
+    if (rc) return rc;
+    for (size_t j = 0; j < rounds; j++) {
+      int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       Fq e[3];
-      rc = phase1_eval(ctx, Az, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap, Aq, Ax, Az.d, Bz, Cz,
-                       partials, d_out3, e);
+      rc = eval_wait(ctx, e);
       if (rc) return rc;
+      lp.lap("p1_eval");
       Fq r_j = zk.begin(g, t, j, e);
+      lp.lap("p1_host");
       if (mode == MODE_P) { rc = dev_fold_top(ctx, Ap, lenP, r_j); lenP /= 2; }
       else if (mode == MODE_Q) { rc = dev_fold_top(ctx, Aq, lenQ, r_j); lenQ /= 2; }
       else { rc = dev_fold_top(ctx, Ax, lenX, r_j); lenX /= 2; }
       if (!rc) rc = pqx_bound(ctx, Az, Bz, Cz, r_j, mode);
+      if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
       if (rc) return rc;
+      lp.lap("p1_fold");
       zk.finish(g, t, tape, j, r_j);
+      lp.lap("p1_host");
       rx_all.push_back(r_j);
     }
     Fq a[3];
@@ -512,6 +567,7 @@ int Prover::run() {
     blind_post1 = zk.blinds_evals[rounds - 1];
     pf.sc1 = std::move(zk.out);
   }
+  lp.lap("p1_claims");
   Fq tau_claim = claims1[0], Az_claim = claims1[1], Bz_claim = claims1[2], Cz_claim = claims1[3];
   Fq Az_blind = tape.scalar("Az_blind"), Bz_blind = tape.scalar("Bz_blind"), Cz_blind = tape.scalar("Cz_blind"),
      prod_blind = tape.scalar("prod_Az_Bz_blind");
@@ -531,6 +587,7 @@ int Prover::run() {
       rp(rx_all.begin() + nx + nq, rx_all.end());
   FqV rx(rx_rev.rbegin(), rx_rev.rend()), rq(rq_rev.rbegin(), rq_rev.rend());
 
+  lp.lap("sigma1");
   // ---- phase 2 inputs
   Fq r_A = t.challenge("challenge_Az"), r_B = t.challenge("challenge_Bz"), r_C = t.challenge("challenge_Cz");
   Fq claim2 = fq_add(fq_add(fq_mul(r_A, Az_claim), fq_mul(r_B, Bz_claim)), fq_mul(r_C, Cz_claim));
@@ -588,6 +645,7 @@ int Prover::run() {
   rc = eq_table(ctx, rp, eq_p);
   if (rc) return rc;
 
+  lp.lap("p2_prep");
   // ---- phase 2 (sumcheck.rs:788-1065)
   FqV ry_all;
   Fq claims2[3], blind_post2;
@@ -599,22 +657,34 @@ int Prover::run() {
     size_t inputs_len = (size_t)1 << ny, ws_len = (size_t)1 << nw, instance_len = (size_t)1 << np;
     size_t lenP = instance_len;
     std::vector<size_t> sc_ni = num_inputs;
-    for (size_t j = 0; j < rounds; j++) {
+    auto launch_eval = [&](size_t j) -> int {
       int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       if (inputs_len > 1) inputs_len /= 2;
       else if (ws_len > 1) ws_len /= 2;
       else instance_len /= 2;
       for (size_t p = 0; p < std::min(instance_len, sc_ni.size()); p++)
         if (mode == MODE_X && sc_ni[p] > 1) sc_ni[p] /= 2;
+      return phase2_eval(ctx, ABC, Zp, mode, instance_len, ws_len, nws, single, sc_ni, eq_p, partials, d_out3,
+                         nullptr);
+    };
+    if (rounds) rc = launch_eval(0);
+    if (rc) return rc;
+    for (size_t j = 0; j < rounds; j++) {
+      int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       Fq e[3];
-      rc = phase2_eval(ctx, ABC, Zp, mode, instance_len, ws_len, nws, single, sc_ni, eq_p, partials, d_out3, e);
+      rc = eval_wait(ctx, e);
       if (rc) return rc;
+      lp.lap("p2_eval");
       Fq r_j = zk.begin(g, t, j, e);
+      lp.lap("p2_host");
       if (mode == MODE_P) { rc = dev_fold_top(ctx, eq_p, lenP, r_j); lenP /= 2; }
       if (!rc && (mode != MODE_P || !single)) rc = pqx_bound(ctx, ABC, nullptr, nullptr, r_j, mode);
       if (!rc) rc = pqx_bound(ctx, Zp, nullptr, nullptr, r_j, mode);
+      if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
       if (rc) return rc;
+      lp.lap("p2_fold");
       zk.finish(g, t, tape, j, r_j);
+      lp.lap("p2_host");
       ry_all.push_back(r_j);
     }
     rc = d2h_fq(ctx, eq_p, &claims2[0]);
@@ -663,7 +733,7 @@ int Prover::run() {
       // LZ = bound(L) on the device
       Fq* dL = (Fq*)ws_get(ctx, WS_L, Ls * sizeof(Fq) + 64);
       uint32_t nbx = (uint32_t)((Rs + 255) / 256);
-      uint32_t S = (uint32_t)std::min<size_t>(Ls, std::max<size_t>(1, 2048 / nbx));
+      uint32_t S = (uint32_t)std::min<size_t>(Ls, 32);  // 32 partial rows: short column sums
       uint32_t chunk = (uint32_t)((Ls + S - 1) / S);
       S = (uint32_t)((Ls + chunk - 1) / chunk);
       Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, (size_t)S * Rs * sizeof(Fq) + 64);
@@ -685,10 +755,11 @@ int Prover::run() {
       for (size_t k = 0; k < Rs; k++) ev = fq_add(ev, fq_mul(pr.LZ[k], pr.R[k]));
       pr.ev = ev;
       eval_list[i].push_back(pr.ni >= Y ? ev : fq_mul(ev, ry_factors[ny - lni]));
-      pf.comm_vars_at_ry_list[i].push_back(compress(commit_host(g, g.gens_1, {ev}, fq_zero())));
+      pf.comm_vars_at_ry_list[i].push_back(commit_batch(g, {CJob(g.gens_1, {ev}, fq_zero())})[0]);
       polys.push_back(std::move(pr));
     }
   }
+  lp.lap("polyeval_bound");
   // PolyEvalProof::prove_batched_instances_disjoint_rounds (dense_mlpoly.rs:861-960)
   {
     t.protocol("polynomial evaluation proof");
@@ -721,6 +792,7 @@ int Prover::run() {
       pf.evals.push_back(std::move(dp));
     }
   }
+  lp.lap("polyeval_dotlog");
   // prefix_list (r1csproof.rs:577-606) and the combined evaluation
   FqV prefix;
   {
@@ -750,7 +822,7 @@ int Prover::run() {
     comb_list.push_back(comb);
   }
   Fq eval_vars_at_ry = dense_eval_host(comb_list, rp2);
-  pf.comm_vars_at_ry = compress(commit_host(g, g.gens_1, {eval_vars_at_ry}, fq_zero()));
+  pf.comm_vars_at_ry = commit_batch(g, {CJob(g.gens_1, {eval_vars_at_ry}, fq_zero())})[0];
   Fq claim_post2 = fq_mul(fq_mul(claims2[0], claims2[1]), claims2[2]);
   pf.eq2 = equality_prove(g, g.gens_1, t, tape, claim_post2, fq_zero(), claim_post2, blind_post2);
   pf.claims_phase2[0] = comm_Az;
@@ -760,6 +832,7 @@ int Prover::run() {
   FqV rwry(rw);
   rwry.insert(rwry.end(), ry.begin(), ry.end());
   challenges = {rp2, rq_rev, rx, rwry};
+  lp.lap("final");
   return 0;
 }
 

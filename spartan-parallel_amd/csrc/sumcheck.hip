@@ -10,6 +10,8 @@
 // Every round is one streaming pass over HBM-resident tables: each thread accumulates exact Fq
 // partial sums of (e0, e2, e3) over a grid-stride slice, a 256-thread block tree-reduces them in LDS
 // and a one-block kernel sums the block partials. Reduction order is irrelevant (exact arithmetic).
+#include <string.h>
+
 #include "sumcheck.hpp"
 
 namespace spg {
@@ -21,7 +23,8 @@ __device__ __forceinline__ int find_inst(const PqxArgs& a, uint32_t t) {
   return p;
 }
 
-__device__ __forceinline__ void block_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict__ partials) {
+// block-wide sums of three Fq values; the result is valid in thread 0
+__device__ __forceinline__ void block_sum3(Fq& v0, Fq& v1, Fq& v2) {
   __shared__ Fq sh[3][256];
   int t = threadIdx.x;
   sh[0][t] = v0;
@@ -36,21 +39,49 @@ __device__ __forceinline__ void block_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restric
     }
     __syncthreads();
   }
-  if (t == 0) {
-    partials[3 * blockIdx.x] = sh[0][0];
-    partials[3 * blockIdx.x + 1] = sh[1][0];
-    partials[3 * blockIdx.x + 2] = sh[2][0];
-  }
+  v0 = sh[0][0];
+  v1 = sh[1][0];
+  v2 = sh[2][0];
+  __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) k_reduce3(const Fq* __restrict__ partials, int nb, Fq* __restrict__ out) {
+// Grid-wide (e0, e2, e3): every block publishes its partial sums; the last block to finish (ticket on
+// `counter`) adds all partials and writes out3, then re-arms the counter. One launch per round.
+// Cross-XCD hand-off: plain stores + agent-scope release before the ticket, agent-scope acquire in
+// the reducer before plain loads (MI355X L2s are per-XCD and not coherent).
+__device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict__ partials,
+                                             unsigned* __restrict__ counter, Fq* __restrict__ out3) {
+  __shared__ bool last;
+  block_sum3(v0, v1, v2);
+  const int t = threadIdx.x;
+  if (t == 0) {
+    partials[3 * blockIdx.x] = v0;
+    partials[3 * blockIdx.x + 1] = v1;
+    partials[3 * blockIdx.x + 2] = v2;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
   Fq a = fq_zero(), b = fq_zero(), c = fq_zero();
-  for (int i = threadIdx.x; i < nb; i += 256) {
+  for (unsigned i = t; i < gridDim.x; i += 256) {
     a = fq_add(a, partials[3 * i]);
     b = fq_add(b, partials[3 * i + 1]);
     c = fq_add(c, partials[3 * i + 2]);
   }
-  block_reduce3(a, b, c, out);
+  block_sum3(a, b, c);
+  if (t == 0) {
+    out3[0] = a;
+    out3[1] = b;
+    out3[2] = c;
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // EqPolynomial::evals (src/dense_mlpoly.rs:76-92): out[b] = prod_j (bit_{ell-1-j}(b) ? r_j : 1 - r_j)
@@ -79,7 +110,8 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
                                                      const Fq* __restrict__ Ap, const Fq* __restrict__ Aq,
                                                      const Fq* __restrict__ Ax, const Fq* __restrict__ B,
                                                      const Fq* __restrict__ C, const Fq* __restrict__ D,
-                                                     Fq* __restrict__ partials) {
+                                                     Fq* __restrict__ partials, unsigned* __restrict__ counter,
+                                                     Fq* __restrict__ out3) {
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(a, t);
@@ -122,7 +154,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
     Fq c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
     e3 = fq_add(e3, fq_mul(a3, fq_sub(fq_mul(b3, c3), d3)));
   }
-  block_reduce3(e0, e2, e3, partials);
+  grid_reduce3(e0, e2, e3, partials, counter, out3);
 }
 
 // ---------------------------------------------------------------- phase 2 round evaluation
@@ -147,7 +179,8 @@ __device__ __forceinline__ Fq pqx_get_high(const PqxArgs& a, const Fq* T, int p,
 __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int mode, uint32_t total, int W,
                                                      bool single, uint32_t instance_len, const Fq* __restrict__ eq,
                                                      const Fq* __restrict__ B, const Fq* __restrict__ C,
-                                                     Fq* __restrict__ partials) {
+                                                     Fq* __restrict__ partials, unsigned* __restrict__ counter,
+                                                     Fq* __restrict__ out3) {
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(zz, t);
@@ -166,7 +199,7 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
     Fq a3 = fq_sub(fq_add(a2, a_hi), a_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo);
     e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
   }
-  block_reduce3(e0, e2, e3, partials);
+  grid_reduce3(e0, e2, e3, partials, counter, out3);
 }
 
 // ---------------------------------------------------------------- Pqx folds (custom_dense_mlpoly.rs:205-289)
@@ -219,7 +252,8 @@ __global__ void k_pqx_fold(PqxArgs a, int mode, uint32_t total, Fq r, Fq* __rest
 
 // ---------------------------------------------------------------- plain cubic (product trees), A*B*C
 __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, const Fq* __restrict__ B,
-                                                    const Fq* __restrict__ C, uint32_t len, Fq* __restrict__ partials) {
+                                                    const Fq* __restrict__ C, uint32_t len, Fq* __restrict__ partials,
+                                                    unsigned* __restrict__ counter, Fq* __restrict__ out3) {
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < len; i += gridDim.x * 256) {
     Fq al = A[i], ah = A[i + len], bl = B[i], bh = B[i + len], cl = C[i], ch = C[i + len];
@@ -229,7 +263,7 @@ __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, co
     Fq a3 = fq_sub(fq_add(a2, ah), al), b3 = fq_sub(fq_add(b2, bh), bl), c3 = fq_sub(fq_add(c2, ch), cl);
     e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
   }
-  block_reduce3(e0, e2, e3, partials);
+  grid_reduce3(e0, e2, e3, partials, counter, out3);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -239,10 +273,15 @@ static int grid_for(uint32_t total) {
   return nb < 1 ? 1 : nb;
 }
 
-int eval_reduce_finish(spg_ctx* ctx, Fq* partials, int nb, Fq* d_out3, Fq out3[3]) {
-  hipLaunchKernelGGL(k_reduce3, dim3(1), dim3(256), 0, ctx->stream, partials, nb, d_out3);
-  SPG_HIP(ctx, hipMemcpyAsync(out3, d_out3, 3 * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+// device -> pinned host copy of the round's three scalars (written by the last block of the eval kernel);
+// out3 == nullptr only enqueues the copy (collect it with eval_wait), so host work can overlap the round
+int eval_reduce_finish(spg_ctx* ctx, Fq* d_out3, Fq* out3) {
+  SPG_HIP(ctx, hipMemcpyAsync(ctx->pinned, d_out3, 3 * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+  return out3 ? eval_wait(ctx, out3) : 0;
+}
+int eval_wait(spg_ctx* ctx, Fq* out3) {
   SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(out3, ctx->pinned, 3 * sizeof(Fq));
   return 0;
 }
 
@@ -287,7 +326,7 @@ void pqx_fill_args(const PqxDev& T, PqxArgs& a) {
 
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
-                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* d_out3, Fq out3[3]) {
+                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* d_out3, Fq* out3) {
   PqxArgs a;
   pqx_fill_args(T, a);
   size_t P = std::min(instance_len, sc_np.size());
@@ -310,15 +349,15 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
     KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len));
     hipLaunchKernelGGL(k_phase1_eval, dim3(nb), dim3(256), 0, ctx->stream, a, mode, (uint32_t)dom,
                        (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq, Ax, B, C, D,
-                       partials);
+                       partials, ctx->d_counter, d_out3);
   }
   SPG_HIP(ctx, hipGetLastError());
-  return eval_reduce_finish(ctx, partials, nb, d_out3, out3);
+  return eval_reduce_finish(ctx, d_out3, out3);
 }
 
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
-                const Fq* eq, Fq* partials, Fq* d_out3, Fq out3[3]) {
+                const Fq* eq, Fq* partials, Fq* d_out3, Fq* out3) {
   PqxArgs ab, zz;
   pqx_fill_args(AB, ab);
   pqx_fill_args(Z, zz);
@@ -337,10 +376,10 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
   {
     KScope ks(ctx, "sc_phase2_eval", 128.0 * dom);  // ABC and Z, lo+hi per domain point
     hipLaunchKernelGGL(k_phase2_eval, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, (int)W,
-                       single, (uint32_t)instance_len, eq, AB.d, Z.d, partials);
+                       single, (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, d_out3);
   }
   SPG_HIP(ctx, hipGetLastError());
-  return eval_reduce_finish(ctx, partials, nb, d_out3, out3);
+  return eval_reduce_finish(ctx, d_out3, out3);
 }
 
 // DensePolynomialPqx::bound_poly(r, mode) applied to up to three tables of identical shape (T[0] owns shape)
@@ -403,14 +442,15 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode) {
 }
 
 int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials, Fq* d_out3,
-               Fq out3[3]) {
+               Fq* out3) {
   int nb = grid_for((uint32_t)len_half);
   {
     KScope ks(ctx, "sc_cubic_eval", 192.0 * len_half);
-    hipLaunchKernelGGL(k_cubic_eval, dim3(nb), dim3(256), 0, ctx->stream, A, B, C, (uint32_t)len_half, partials);
+    hipLaunchKernelGGL(k_cubic_eval, dim3(nb), dim3(256), 0, ctx->stream, A, B, C, (uint32_t)len_half, partials,
+                       ctx->d_counter, d_out3);
   }
   SPG_HIP(ctx, hipGetLastError());
-  return eval_reduce_finish(ctx, partials, nb, d_out3, out3);
+  return eval_reduce_finish(ctx, d_out3, out3);
 }
 
 }  // namespace spg

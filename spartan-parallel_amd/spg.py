@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libspg.so")
+LIB_PATH = os.environ.get("SPG_LIB") or os.path.join(_HERE, "lib", "libspg.so")
 
 SPG_ERRORS = {-1: "SPG_E_ARG", -2: "SPG_E_NOMEM", -3: "SPG_E_HIP", -4: "SPG_E_POINT", -5: "SPG_E_NODEVICE"}
 

@@ -117,3 +117,17 @@ def test_shake_and_merlin(hc):
     hc.spgh_merlin_simple(b"test protocol", b"some label", _p(m1), ctypes.c_size_t(9), b"challenge", _p(o),
                           ctypes.c_size_t(32))
     assert o.tobytes().hex() == "d5a21972d0d5fe320c0d263fac7fffb8145aa640af6e9bca177c03c7efcf0615"
+
+
+def test_host_radix51_curve_matches_device_form(hc):
+    """hcurve.hpp (host prover arithmetic, radix 2^51) against the device-form curve (8 x u32 limbs):
+    compress, decompress, add, mixed add through batch-normalised Niels, dbl, scalar mul."""
+    lib = hc
+    rng = np.random.default_rng(7)
+    n = 64
+    uni = rng.integers(0, 256, 64 * n, dtype=np.uint8)
+    k = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+    k[31::32] &= 0x0F
+    bad = lib.spgh_hcurve_check(uni.ctypes.data_as(ctypes.c_void_p), k.ctypes.data_as(ctypes.c_void_p),
+                                ctypes.c_size_t(n))
+    assert bad == 0
