@@ -41,6 +41,13 @@ const char* spg_last_error(const spg_ctx* ctx);
 /* device-side wall time of the most recent compute call, in microseconds (HIP events on the stream) */
 double spg_last_kernel_us(const spg_ctx* ctx);
 
+/* Multi-process proving: one process (and context) per GPU. R1CSProof::prove is then sharded by instance
+ * p: rank r holds instances [r*ceil(P/n), (r+1)*ceil(P/n)) and every rank runs the same Fiat-Shamir
+ * transcript. fn(user, send, bytes, recv) must place the `bytes` sent by rank k at recv + k*bytes on every
+ * rank (an allgather, e.g. RCCL / torch.distributed); it returns 0 on success. nranks == 1 clears it. */
+typedef int (*spg_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
+int spg_set_comm(spg_ctx* ctx, int rank, int nranks, spg_allgather_fn fn, void* user);
+
 /* per-kernel timing on the context stream (events; off by default). spg_prof_read resolves them and
  * returns up to `max` records (name[32], launches, total microseconds, algorithmic HBM bytes moved
  * by those launches as modelled in DESIGN.md, 0 where not modelled); reset != 0 clears the tallies. */
@@ -142,6 +149,10 @@ int spg_r1cs_inst_new(spg_ctx* ctx, const spg_r1cs_instance* inst, spg_r1cs_inst
 int spg_r1cs_inst_free(spg_ctx* ctx, spg_r1cs_inst* inst);
 /* the witness sections (Vec<&ProverWitnessSecInfo>), uploaded to HBM */
 int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, spg_r1cs_witness** out);
+/* the same for a sharded prover: only instances [p0, p1) of sections with num_instances > 1 are uploaded
+ * (w may hold NULL for the others); single sections are uploaded whole */
+int spg_r1cs_witness_new_shard(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, size_t p0, size_t p1,
+                               spg_r1cs_witness** out);
 int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* w);
 /* R1CSProof::prove(num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs, witness_secs,
  * inst, gens, transcript, random_tape). Writes bincode(R1CSProof) into proof (proof_cap bytes;
@@ -151,6 +162,13 @@ int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst*
                    size_t max_num_proofs, const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
                    const spg_r1cs_witness* witness, spg_transcript* transcript, spg_random_tape* tape,
                    uint8_t* proof, size_t proof_cap, size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens);
+
+/* R1CSInstance::multi_evaluate (src/r1csinstance.rs:583-596) via SparseMatPolynomial::evaluate_with_tables
+ * (src/sparse_mlpoly.rs:427-450): out[3p + m] = M_p(rx, ry), M in (A, B, C), for every matrix instance p
+ * of the uploaded instance; 2^rx_len >= max_num_cons, 2^ry_len >= num_vars. (With one instance this is
+ * R1CSInstance::evaluate, :632-641; multi_evaluate_bound_rp folds out[] with eq(rp) on the caller's side.) */
+int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, const uint64_t* rx, size_t rx_len,
+                            const uint64_t* ry, size_t ry_len, uint64_t* out);
 
 #ifdef __cplusplus
 }

@@ -296,3 +296,17 @@ int orc_r1cs_verify(const spg_r1cs_instance* ci, size_t num_instances, size_t ma
   }
 }
 }
+
+extern "C" {
+// R1CSInstance::multi_evaluate (src/r1csinstance.rs:583-596): out = [A_0(rx,ry), B_0, C_0, A_1, ...]
+int orc_r1cs_multi_evaluate(const spg_r1cs_instance* ci, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                            size_t ry_len, uint64_t* out) {
+  R1CSInstance inst = inst_from_c(ci);
+  FqVec vx, vy;
+  for (size_t i = 0; i < rx_len; i++) vx.push_back(ld(rx + 4 * i));
+  for (size_t i = 0; i < ry_len; i++) vy.push_back(ld(ry + 4 * i));
+  FqVec e = inst.multi_evaluate(vx, vy);
+  for (size_t i = 0; i < e.size(); i++) memcpy(out + 4 * i, e[i].v, 32);
+  return 0;
+}
+}

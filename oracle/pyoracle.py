@@ -224,3 +224,17 @@ def r1cs_verify(wl, proof, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars
                                  v.num_proofs, ctypes.c_size_t(wl.max_num_inputs), v.secs, ctypes.c_size_t(wl.nws),
                                  ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars), ctypes.c_char_p(label),
                                  _p(pb), ctypes.c_size_t(len(proof)), _p(seed))
+
+
+def r1cs_multi_evaluate(wl, rx, ry):
+    """R1CSInstance::multi_evaluate (src/r1csinstance.rs:583-596) -> (3 * num_instances, 4) limbs"""
+    import workload
+
+    v = workload.CViews(wl)
+    rx = u64s(rx).reshape(-1, 4)
+    ry = u64s(ry).reshape(-1, 4)
+    out = np.zeros((3 * len(wl.entries), 4), dtype=np.uint64)
+    rc = lib().orc_r1cs_multi_evaluate(ctypes.byref(v.inst), _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
+                                       ctypes.c_size_t(ry.shape[0]), _p(out))
+    assert rc == 0
+    return out

@@ -104,6 +104,15 @@ extern "C" const char* spg_last_error(const spg_ctx* c) { return c ? c->err.c_st
 
 extern "C" double spg_last_kernel_us(const spg_ctx* c) { return c ? c->last_us : 0.0; }
 
+extern "C" int spg_set_comm(spg_ctx* c, int rank, int nranks, spg_allgather_fn fn, void* user) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return SPG_E_ARG;
+  c->rank = rank;
+  c->nranks = nranks;
+  c->allgather = fn;
+  c->comm_user = user;
+  return SPG_OK;
+}
+
 extern "C" int spg_prof_enable(spg_ctx* c, int on) {
   if (!c) return SPG_E_ARG;
   c->prof_on = on != 0;

@@ -15,6 +15,10 @@ struct spg_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* pinned = nullptr;          // 4 KiB page-locked host staging for per-round device->host scalars
   unsigned* d_counter = nullptr;   // grid-reduction ticket (zero between launches)
+  // multi-process proving (spg_set_comm): this process' rank and an allgather provided by the caller
+  int rank = 0, nranks = 1;
+  spg_allgather_fn allgather = nullptr;
+  void* comm_user = nullptr;
   double last_us = 0.0;
   std::string err;
   // workspace slots: grown on demand, reused across calls (no allocation in steady state)

@@ -3,6 +3,8 @@
 // without a GPU. Not part of the proving path.
 #include <string.h>
 
+#include <vector>
+
 #include "curve.hpp"
 #include "hcurve.hpp"
 #include "keccak.hpp"
@@ -139,6 +141,25 @@ int spgh_hcurve_check(const uint8_t* uni, const uint8_t* k, size_t n) {
   h::HExt X;
   bad += h::hext_decompress(bad_enc, X);  // non-canonical must be rejected
   return bad;
+}
+
+// The cross-rank step of the sharded R1CSProof (r1cs.hip, Prover::sum_ranks): gather every rank's three
+// partial round sums through the caller's allgather and add them mod q.
+int spgh_allgather_sum(int (*fn)(void*, const void*, size_t, void*), void* user, int nranks, const uint64_t* mine,
+                       uint64_t* out) {
+  using namespace spg;
+  std::vector<uint8_t> recv(96 * (size_t)nranks);
+  if (fn(user, mine, 96, recv.data()) != 0) return -1;
+  for (int k = 0; k < 3; k++) {
+    Fq acc = fq_zero();
+    for (int r = 0; r < nranks; r++) {
+      Fq v;
+      memcpy(v.l, recv.data() + 96 * r + 32 * k, 32);
+      acc = fq_add(acc, v);
+    }
+    memcpy(out + 4 * k, acc.l, 32);
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -45,6 +45,7 @@ struct spg_r1cs_inst {
 };
 
 // ProverWitnessSecInfo list resident in HBM: w_mat[p] flattened (q-major), sections concatenated.
+static const uint64_t kNotResident = ~0ULL;  // instance held by another rank
 struct spg_r1cs_witness {
   size_t nws = 0;
   std::vector<std::vector<size_t>> num_proofs, num_inputs;  // [w][p]
@@ -181,6 +182,45 @@ __global__ void k_sum_cols(const Fq* __restrict__ part, uint32_t S, uint32_t Rs,
   Fq acc = fq_zero();
   for (uint32_t y = 0; y < S; y++) acc = fq_add(acc, part[(size_t)y * Rs + i]);
   out[i] = acc;
+}
+
+// SparseMatPolynomial::evaluate_with_tables (src/sparse_mlpoly.rs:427-436) for every matrix of the
+// instance at once: segment s = 3p + m (A, B, C of matrix instance p); one thread per CSR row computes
+// eq_rx[row] * sum_e val_e * eq_ry[col_e]; blocks publish partial sums, k_sum_segments adds them.
+__device__ __forceinline__ Fq block_sum1(Fq v) {
+  __shared__ Fq sh[256];
+  int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int d = 128; d >= 1; d >>= 1) {
+    if (t < d) sh[t] = fq_add(sh[t], sh[t + d]);
+    __syncthreads();
+  }
+  Fq r = sh[0];
+  __syncthreads();
+  return r;
+}
+__global__ void __launch_bounds__(256) k_sparse_eval(const MatDesc* __restrict__ md, const uint32_t* __restrict__ nrows,
+                                                     const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
+                                                     const Fq* __restrict__ val, const Fq* __restrict__ eq_rx,
+                                                     const Fq* __restrict__ eq_ry, Fq* __restrict__ partials) {
+  const int seg = blockIdx.y, p = seg / 3, m = seg % 3;
+  const uint32_t row = blockIdx.x * 256 + threadIdx.x;
+  Fq acc = fq_zero();
+  if (row < nrows[p]) {
+    const uint32_t* rp = rowptr + md[p].rp[m];
+    Fq sr = fq_zero();
+    for (uint32_t e = rp[row]; e < rp[row + 1]; e++) sr = fq_add(sr, fq_mul(val[e], eq_ry[col[e]]));
+    acc = fq_mul(eq_rx[row], sr);
+  }
+  acc = block_sum1(acc);
+  if (threadIdx.x == 0) partials[(size_t)seg * gridDim.x + blockIdx.x] = acc;
+}
+__global__ void __launch_bounds__(256) k_sum_segments(const Fq* __restrict__ partials, int nblk, Fq* __restrict__ out) {
+  Fq acc = fq_zero();
+  for (int i = threadIdx.x; i < nblk; i += 256) acc = fq_add(acc, partials[(size_t)blockIdx.x * nblk + i]);
+  acc = block_sum1(acc);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
 // ------------------------------------------------------------------------------------ host helpers
@@ -331,7 +371,7 @@ static int eq_table(spg_ctx* ctx, const FqV& r, Fq* out) { return dev_eq_table(c
 // workspace slots used here (msm.hip uses 0..12, proto.hip 20..22)
 enum {
   WS_AZ = 30, WS_BZ, WS_CZ, WS_Z, WS_ABC, WS_TP, WS_TQ, WS_TX, WS_EQRX, WS_EQP, WS_PART, WS_OUT3, WS_DESC,
-  WS_L, WS_BPART, WS_BOUT
+  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2
 };
 
 struct Prover {
@@ -365,6 +405,12 @@ struct Prover {
     return 0;
   }
 
+  // instance shard of this rank (R1CSProof sharded by instance p over nranks processes)
+  size_t rank = 0, nranks = 1, p0 = 0, p1 = 0;
+  int allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv);
+  int sum_ranks(Fq e[3]);
+  int gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full);
+
   int run();
   int run_inner(Laps& lp);
 };
@@ -376,6 +422,73 @@ int Prover::run() {
   return rc0;
 }
 
+// ---- cross-rank exchange (identity when nranks == 1)
+int Prover::allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv) {
+  recv.resize(bytes * nranks);
+  if (nranks == 1) {
+    memcpy(recv.data(), send, bytes);
+    return 0;
+  }
+  if (!ctx->allgather) return set_err(ctx, SPG_E_ARG, "no communicator set (spg_set_comm)");
+  if (ctx->allgather(ctx->comm_user, send, bytes, recv.data()) != 0)
+    return set_err(ctx, SPG_E_HIP, "allgather callback failed");
+  return 0;
+}
+// (e0, e2, e3) summed over the ranks' instance shards
+int Prover::sum_ranks(Fq e[3]) {
+  if (nranks == 1) return 0;
+  std::vector<uint8_t> r;
+  int rc = allgather(e, 3 * sizeof(Fq), r);
+  if (rc) return rc;
+  const Fq* v = (const Fq*)r.data();
+  for (int k = 0; k < 3; k++) {
+    Fq acc = fq_zero();
+    for (size_t q = 0; q < nranks; q++) acc = fq_add(acc, v[3 * q + k]);
+    e[k] = acc;
+  }
+  return 0;
+}
+// per local instance p, the element (p, 0, 0, 0) of each table -> the same for all P instances, on the host
+int Prover::gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full) {
+  const size_t k = tabs.size(), PL = (P + nranks - 1) / nranks;
+  std::vector<Fq> mine(PL * k, fq_zero());
+  for (size_t i = 0; i < k; i++) {
+    const PqxDev& T = *tabs[i];
+    for (size_t p = 0; p < T.zlen; p++) {
+      int rc = d2h_fq(ctx, T.d + T.off[p], &mine[i * PL + p]);
+      if (rc) return rc;
+    }
+  }
+  std::vector<uint8_t> r;
+  int rc = allgather(mine.data(), mine.size() * sizeof(Fq), r);
+  if (rc) return rc;
+  const Fq* v = (const Fq*)r.data();
+  full.assign(k, std::vector<Fq>(P, fq_zero()));
+  for (size_t q = 0; q < nranks; q++)
+    for (size_t i = 0; i < k; i++)
+      for (size_t p = 0; p < PL && q * PL + p < P; p++) full[i][q * PL + p] = v[q * PL * k + i * PL + p];
+  return 0;
+}
+// a table of n instances holding one element each (what remains of a Pqx table when only the instance
+// variables are left unbound); its index / index_high behave exactly like the full table's at (p,0,0,0)
+static PqxDev compact_table(Fq* d, size_t n, size_t P) {
+  PqxDev T;
+  T.d = d;
+  T.zlen = n;
+  T.total = n;
+  for (size_t p = 0; p < n; p++) T.off.push_back(p);
+  T.anp.assign(n, 1);
+  T.anw.assign(n, 1);
+  T.ani.assign(n, 1);
+  T.num_instances = npow2(n);
+  T.max_num_proofs = 1;
+  T.num_witness_secs = 1;
+  T.max_num_inputs = 1;
+  T.num_proofs.assign(P, 1);
+  T.num_inputs.assign(P, 1);
+  return T;
+}
+
 int Prover::run_inner(Laps& lp) {
   hipStream_t s = ctx->stream;
   t.protocol("R1CS proof");
@@ -383,42 +496,48 @@ int Prover::run_inner(Laps& lp) {
   std::vector<size_t> block_num_cons(P);
   for (size_t p = 0; p < P; p++) block_num_cons[p] = inst.num_cons[inst.num_instances == 1 ? 0 : p];
   size_t np = lg2(npow2(P)), nq = lg2(max_np), nx = lg2(num_cons), nw = lg2(nws), ny = lg2(Y);
+  // this rank's instances [p0, p1): everything O(N) lives only here; nranks == 1 -> all of them
+  const size_t PLn = p1 - p0;
+  std::vector<size_t> l_proofs(num_proofs.begin() + p0, num_proofs.begin() + p1);
+  std::vector<size_t> l_inputs(num_inputs.begin() + p0, num_inputs.begin() + p1);
+  std::vector<size_t> l_cons(block_num_cons.begin() + p0, block_num_cons.begin() + p1);
 
   // ---- Z table (p, q_rev, w, x_rev)
   PqxDev Zp;
-  Zp.zlen = P;
-  Zp.off.resize(P);
-  Zp.anp = num_proofs;
-  Zp.anw.assign(P, nws);
-  Zp.ani = num_inputs;
+  Zp.zlen = PLn;
+  Zp.off.resize(PLn);
+  Zp.anp = l_proofs;
+  Zp.anw.assign(PLn, nws);
+  Zp.ani = l_inputs;
   size_t ztot = 0;
-  for (size_t p = 0; p < P; p++) {
+  for (size_t p = 0; p < PLn; p++) {
     Zp.off[p] = ztot;
-    ztot += num_proofs[p] * nws * num_inputs[p];
+    ztot += l_proofs[p] * nws * l_inputs[p];
   }
   Zp.total = ztot;
   Zp.num_instances = npow2(P);
   Zp.max_num_proofs = max_np;
   Zp.num_witness_secs = npow2(nws);
   Zp.max_num_inputs = Y;
-  Zp.num_proofs = num_proofs;
-  Zp.num_inputs = num_inputs;
+  Zp.num_proofs = l_proofs;
+  Zp.num_inputs = l_inputs;
   Zp.d = (Fq*)ws_get(ctx, WS_Z, ztot * sizeof(Fq) + 64);
   if (!Zp.d) return set_err(ctx, SPG_E_NOMEM, "Z table");
   {
-    std::vector<ZDesc> zd(P);
-    std::vector<SecDesc> sd(nws * P);
-    for (size_t p = 0; p < P; p++) {
+    std::vector<ZDesc> zd(PLn);
+    std::vector<SecDesc> sd(nws * PLn);
+    for (size_t p = 0; p < PLn; p++) {
       zd[p].dom_off = Zp.off[p];
       zd[p].z_off = Zp.off[p];
-      zd[p].lg_q = (uint32_t)lg2(num_proofs[p]);
-      zd[p].ni = (uint32_t)num_inputs[p];
-      zd[p].lg_ni = (uint32_t)lg2(num_inputs[p]);
+      zd[p].lg_q = (uint32_t)lg2(l_proofs[p]);
+      zd[p].ni = (uint32_t)l_inputs[p];
+      zd[p].lg_ni = (uint32_t)lg2(l_inputs[p]);
       for (size_t w = 0; w < nws; w++) {
-        size_t pw = wit.num_proofs[w].size() == 1 ? 0 : p;
-        sd[w * P + p].off = wit.off[w][pw];
-        sd[w * P + p].np = (uint32_t)wit.num_proofs[w][pw];
-        sd[w * P + p].ni = (uint32_t)wit.num_inputs[w][pw];
+        size_t pw = wit.num_proofs[w].size() == 1 ? 0 : p0 + p;
+        if (wit.off[w][pw] == kNotResident) return set_err(ctx, SPG_E_ARG, "witness shard does not hold instance");
+        sd[w * PLn + p].off = wit.off[w][pw];
+        sd[w * PLn + p].np = (uint32_t)wit.num_proofs[w][pw];
+        sd[w * PLn + p].ni = (uint32_t)wit.num_inputs[w][pw];
       }
     }
     ZDesc* dz;
@@ -427,12 +546,12 @@ int Prover::run_inner(Laps& lp) {
     if (!rc) rc = upload_desc(sd, 65536, &ds);
     if (rc) return rc;
     KScope ks(ctx, "z_fill", 64.0 * ztot);
-    hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, s, dz, (int)P, ds, (int)nws, wit.d_w, Zp.d,
+    hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, s, dz, (int)PLn, ds, (int)nws, wit.d_w, Zp.d,
                        (uint64_t)ztot);
     SPG_HIP(ctx, hipGetLastError());
   }
 
-  // ---- tau tables
+  // ---- tau tables (identical on every rank)
   FqV tau_p = t.challenges("challenge_tau_p", np);
   FqV tau_q = t.challenges("challenge_tau_q", nq);
   FqV tau_x = t.challenges("challenge_tau_x", nx);
@@ -445,25 +564,25 @@ int Prover::run_inner(Laps& lp) {
   if (!rc) rc = eq_table(ctx, tau_x, Ax);
   if (rc) return rc;
 
-  // ---- Az, Bz, Cz = multiply_vec_block (p, q_rev, 0, x_rev)
+  // ---- Az, Bz, Cz = multiply_vec_block (p, q_rev, 0, x_rev) for the local instances
   PqxDev Az;
-  Az.zlen = P;
-  Az.off.resize(P);
-  Az.anp = num_proofs;
-  Az.anw.assign(P, 1);
-  Az.ani = block_num_cons;
+  Az.zlen = PLn;
+  Az.off.resize(PLn);
+  Az.anp = l_proofs;
+  Az.anw.assign(PLn, 1);
+  Az.ani = l_cons;
   size_t atot = 0;
-  for (size_t p = 0; p < P; p++) {
+  for (size_t p = 0; p < PLn; p++) {
     Az.off[p] = atot;
-    atot += num_proofs[p] * block_num_cons[p];
+    atot += l_proofs[p] * l_cons[p];
   }
   Az.total = atot;
   Az.num_instances = npow2(P);
   Az.max_num_proofs = max_np;
   Az.num_witness_secs = 1;
   Az.max_num_inputs = num_cons;
-  Az.num_proofs = num_proofs;
-  Az.num_inputs = block_num_cons;
+  Az.num_proofs = l_proofs;
+  Az.num_inputs = l_cons;
   Az.d = (Fq*)ws_get(ctx, WS_AZ, atot * sizeof(Fq) + 64);
   Fq* Bz = (Fq*)ws_get(ctx, WS_BZ, atot * sizeof(Fq) + 64);
   Fq* Cz = (Fq*)ws_get(ctx, WS_CZ, atot * sizeof(Fq) + 64);
@@ -477,29 +596,27 @@ int Prover::run_inner(Laps& lp) {
   rc = upload_desc(md, 2 * 65536, &dmd);
   if (rc) return rc;
   {
-    std::vector<SpDesc> sd(P);
-    for (size_t p = 0; p < P; p++) {
+    std::vector<SpDesc> sd(PLn);
+    double visits = 0;
+    for (size_t p = 0; p < PLn; p++) {
+      size_t pi = inst.num_instances == 1 ? 0 : p0 + p;
       sd[p].dom_off = Az.off[p];
       sd[p].out_off = Az.off[p];
       sd[p].z_off = Zp.off[p];
-      sd[p].pi = (uint32_t)(inst.num_instances == 1 ? 0 : p);
-      sd[p].lg_q = (uint32_t)lg2(num_proofs[p]);
-      sd[p].nrows = (uint32_t)block_num_cons[p];
-      sd[p].lg_rows = (uint32_t)lg2(block_num_cons[p]);
-      sd[p].ni = (uint32_t)num_inputs[p];
-      sd[p].lg_ni = (uint32_t)lg2(num_inputs[p]);
+      sd[p].pi = (uint32_t)pi;
+      sd[p].lg_q = (uint32_t)lg2(l_proofs[p]);
+      sd[p].nrows = (uint32_t)l_cons[p];
+      sd[p].lg_rows = (uint32_t)lg2(l_cons[p]);
+      sd[p].ni = (uint32_t)l_inputs[p];
+      sd[p].lg_ni = (uint32_t)lg2(l_inputs[p]);
+      visits += (double)l_proofs[p] * (inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2]);
     }
     SpDesc* dsd;
     rc = upload_desc(sd, 3 * 65536, &dsd);
     if (rc) return rc;
     // outputs, CSR row pointers, and per visited entry its column, value and z gather
-    double visits = 0;
-    for (size_t p = 0; p < P; p++) {
-      size_t pi = inst.num_instances == 1 ? 0 : p;
-      visits += (double)num_proofs[p] * (inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2]);
-    }
     KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
-    hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)P, dmd, inst.d_rowptr, inst.d_col,
+    hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr, inst.d_col,
                        inst.d_val, Zp.d, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
     SPG_HIP(ctx, hipGetLastError());
   }
@@ -519,7 +636,12 @@ int Prover::run_inner(Laps& lp) {
     zk.init(g, tape, rounds, fq_zero(), fq_zero());
     size_t cons_len = (size_t)1 << nx, proof_len = (size_t)1 << nq, instance_len = (size_t)1 << np;
     size_t lenP = instance_len, lenQ = proof_len, lenX = cons_len;
-    std::vector<size_t> sc_np = num_proofs, sc_nc = block_num_cons;
+    std::vector<size_t> sc_np = l_proofs, sc_nc = l_cons;  // local; P rounds use all-ones of length P
+    PqxDev Ac;  // compact Az for the instance rounds; Bc/Cc share its shape
+    Fq *Bc = nullptr, *Cc = nullptr;
+    PqxDev* T = &Az;
+    Fq *TB = Bz, *TC = Cz;
+    const Fq* Ap_l = Ap + p0;  // eq(tau_p) indexed by the global instance in the x / q rounds
     // round j's evaluation is enqueued right after round j-1's folds, so it runs on the device while the
     // host finishes round j-1's proof (comm_eval, DotProductProof); eval_wait then collects (e0, e2, e3)
     auto launch_eval = [&](size_t j) -> int {
@@ -527,19 +649,47 @@ int Prover::run_inner(Laps& lp) {
       if (cons_len > 1) cons_len /= 2;
       else if (proof_len > 1) proof_len /= 2;
       else instance_len /= 2;
-      for (size_t p = 0; p < std::min(instance_len, sc_np.size()); p++) {
+      if (mode == MODE_P) {
+        std::vector<size_t> ones(P, 1);
+        return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, ones, ones, Ap, Aq, Ax, T->d, TB, TC,
+                           partials, d_out3, nullptr);
+      }
+      for (size_t p = 0; p < sc_np.size(); p++) {  // instance_len >= P here: every instance takes part
         if (mode == MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
         if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
       }
-      return phase1_eval(ctx, Az, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap, Aq, Ax, Az.d, Bz, Cz,
-                         partials, d_out3, nullptr);
+      return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap_l, Aq, Ax, T->d, TB,
+                         TC, partials, d_out3, nullptr);
     };
-    if (rounds) rc = launch_eval(0);
+    // before the first instance round: collect every instance's remaining (Az, Bz, Cz) value
+    auto to_compact = [&]() -> int {
+      std::vector<std::vector<Fq>> full;
+      PqxDev Bt = Az, Ct = Az;
+      Bt.d = Bz;
+      Ct.d = Cz;
+      int r2 = gather_first({&Az, &Bt, &Ct}, full);
+      if (r2) return r2;
+      Fq* buf = (Fq*)ws_get(ctx, WS_C1, 3 * P * sizeof(Fq) + 64);
+      if (!buf) return set_err(ctx, SPG_E_NOMEM, "compact tables");
+      for (int i = 0; i < 3; i++)
+        SPG_HIP(ctx, hipMemcpyAsync(buf + i * P, full[i].data(), P * sizeof(Fq), hipMemcpyHostToDevice, s));
+      SPG_HIP(ctx, hipStreamSynchronize(s));
+      Ac = compact_table(buf, P, P);
+      Bc = buf + P;
+      Cc = buf + 2 * P;
+      T = &Ac;
+      TB = Bc;
+      TC = Cc;
+      return 0;
+    };
+    if (rounds && nx + nq == 0) rc = to_compact();
+    if (!rc && rounds) rc = launch_eval(0);
     if (rc) return rc;
     for (size_t j = 0; j < rounds; j++) {
       int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       Fq e[3];
       rc = eval_wait(ctx, e);
+      if (!rc && mode != MODE_P) rc = sum_ranks(e);
       if (rc) return rc;
       lp.lap("p1_eval");
       Fq r_j = zk.begin(g, t, j, e);
@@ -547,7 +697,8 @@ int Prover::run_inner(Laps& lp) {
       if (mode == MODE_P) { rc = dev_fold_top(ctx, Ap, lenP, r_j); lenP /= 2; }
       else if (mode == MODE_Q) { rc = dev_fold_top(ctx, Aq, lenQ, r_j); lenQ /= 2; }
       else { rc = dev_fold_top(ctx, Ax, lenX, r_j); lenX /= 2; }
-      if (!rc) rc = pqx_bound(ctx, Az, Bz, Cz, r_j, mode);
+      if (!rc) rc = pqx_bound(ctx, *T, TB, TC, r_j, mode);
+      if (!rc && j + 1 == nx + nq && np > 0) rc = to_compact();
       if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
       if (rc) return rc;
       lp.lap("p1_fold");
@@ -559,9 +710,16 @@ int Prover::run_inner(Laps& lp) {
     rc = d2h_fq(ctx, Ap, &a[0]);
     if (!rc) rc = d2h_fq(ctx, Aq, &a[1]);
     if (!rc) rc = d2h_fq(ctx, Ax, &a[2]);
-    if (!rc) rc = d2h_fq(ctx, Az.d, &claims1[1]);
-    if (!rc) rc = d2h_fq(ctx, Bz, &claims1[2]);
-    if (!rc) rc = d2h_fq(ctx, Cz, &claims1[3]);
+    if (rc) return rc;
+    if (np == 0) {  // a single instance: it sits on this (only) rank's local tables
+      rc = d2h_fq(ctx, Az.d, &claims1[1]);
+      if (!rc) rc = d2h_fq(ctx, Bz, &claims1[2]);
+      if (!rc) rc = d2h_fq(ctx, Cz, &claims1[3]);
+    } else {
+      rc = d2h_fq(ctx, T->d, &claims1[1]);
+      if (!rc) rc = d2h_fq(ctx, TB, &claims1[2]);
+      if (!rc) rc = d2h_fq(ctx, TC, &claims1[3]);
+    }
     if (rc) return rc;
     claims1[0] = fq_mul(fq_mul(a[0], a[1]), a[2]);
     blind_post1 = zk.blinds_evals[rounds - 1];
@@ -596,43 +754,46 @@ int Prover::run_inner(Laps& lp) {
   if (!eq_rx) return set_err(ctx, SPG_E_NOMEM, "eq(rx)");
   rc = eq_table(ctx, rx, eq_rx);
   if (rc) return rc;
-  size_t Pm = inst.num_instances;
+  const bool single = inst.num_instances == 1;
+  // ABC: the shared matrix once (every rank), or this rank's instances
+  const size_t Ab0 = single ? 0 : p0, Abn = single ? 1 : PLn;
   PqxDev ABC;
-  ABC.zlen = Pm;
-  ABC.off.resize(Pm);
-  ABC.anp.assign(Pm, 1);
-  ABC.anw.assign(Pm, nws);
-  ABC.ani.assign(num_inputs.begin(), num_inputs.begin() + Pm);
+  ABC.zlen = Abn;
+  ABC.off.resize(Abn);
+  ABC.anp.assign(Abn, 1);
+  ABC.anw.assign(Abn, nws);
+  ABC.ani.assign(num_inputs.begin() + Ab0, num_inputs.begin() + Ab0 + Abn);
   size_t btot = 0;
-  for (size_t p = 0; p < Pm; p++) {
+  for (size_t p = 0; p < Abn; p++) {
     ABC.off[p] = btot;
-    btot += nws * num_inputs[p];
+    btot += nws * num_inputs[Ab0 + p];
   }
   ABC.total = btot;
-  ABC.num_instances = npow2(Pm);
+  ABC.num_instances = npow2(inst.num_instances);
   ABC.max_num_proofs = 1;
   ABC.num_witness_secs = npow2(nws);
   ABC.max_num_inputs = Y;
   ABC.num_proofs.assign(P, 1);
-  ABC.num_inputs = num_inputs;
+  ABC.num_inputs.assign(num_inputs.begin() + Ab0, num_inputs.end());
   ABC.d = (Fq*)ws_get(ctx, WS_ABC, btot * sizeof(Fq) + 64);
   if (!ABC.d) return set_err(ctx, SPG_E_NOMEM, "ABC");
   {
-    std::vector<AbcDesc> ad(Pm);
-    for (size_t p = 0; p < Pm; p++) {
+    std::vector<AbcDesc> ad(Abn);
+    double visits = 0;
+    for (size_t p = 0; p < Abn; p++) {
       ad[p].dom_off = ABC.off[p];
       ad[p].out_off = ABC.off[p];
-      ad[p].pi = (uint32_t)p;
-      ad[p].ni = (uint32_t)num_inputs[p];
-      ad[p].lg_ni = (uint32_t)lg2(num_inputs[p]);
+      ad[p].pi = (uint32_t)(Ab0 + p);
+      ad[p].ni = (uint32_t)num_inputs[Ab0 + p];
+      ad[p].lg_ni = (uint32_t)lg2(num_inputs[Ab0 + p]);
+      size_t pi = Ab0 + p;
+      visits += inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2];
     }
     AbcDesc* dad;
     rc = upload_desc(ad, 4 * 65536, &dad);
     if (rc) return rc;
-    double visits = 0;
-    for (size_t p = 0; p < Pm; p++) visits += inst.nnz[3 * p] + inst.nnz[3 * p + 1] + inst.nnz[3 * p + 2];
     KScope ks(ctx, "eval_table_abc", 32.0 * btot + 4.0 * btot + 68.0 * visits);
-    hipLaunchKernelGGL(k_abc, dim3(blocks_for(btot)), dim3(256), 0, s, dad, (int)Pm, dmd, inst.d_colptr, inst.d_crow,
+    hipLaunchKernelGGL(k_abc, dim3(blocks_for(btot)), dim3(256), 0, s, dad, (int)Abn, dmd, inst.d_colptr, inst.d_crow,
                        inst.d_cval, eq_rx, (uint32_t)Y, r_A, r_B, r_C, ABC.d, (uint64_t)btot);
     SPG_HIP(ctx, hipGetLastError());
   }
@@ -649,37 +810,66 @@ int Prover::run_inner(Laps& lp) {
   // ---- phase 2 (sumcheck.rs:788-1065)
   FqV ry_all;
   Fq claims2[3], blind_post2;
-  bool single = inst.num_instances == 1;
   {
     size_t rounds = ny + nw + np;
     ZKRounds zk;
     zk.init(g, tape, rounds, claim2, blind2);
     size_t inputs_len = (size_t)1 << ny, ws_len = (size_t)1 << nw, instance_len = (size_t)1 << np;
     size_t lenP = instance_len;
-    std::vector<size_t> sc_ni = num_inputs;
+    std::vector<size_t> sc_ni = l_inputs;
+    PqxDev Zc, ABCc;
+    PqxDev *TZ = &Zp, *TA = &ABC;
+    const Fq* eq_l = eq_p + p0;
     auto launch_eval = [&](size_t j) -> int {
       int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       if (inputs_len > 1) inputs_len /= 2;
       else if (ws_len > 1) ws_len /= 2;
       else instance_len /= 2;
-      for (size_t p = 0; p < std::min(instance_len, sc_ni.size()); p++)
+      if (mode == MODE_P) {
+        std::vector<size_t> ones(P, 1);
+        return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, ones, eq_p, partials, d_out3,
+                           nullptr);
+      }
+      for (size_t p = 0; p < sc_ni.size(); p++)
         if (mode == MODE_X && sc_ni[p] > 1) sc_ni[p] /= 2;
-      return phase2_eval(ctx, ABC, Zp, mode, instance_len, ws_len, nws, single, sc_ni, eq_p, partials, d_out3,
+      return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, sc_ni, eq_l, partials, d_out3,
                          nullptr);
     };
-    if (rounds) rc = launch_eval(0);
+    auto to_compact = [&]() -> int {
+      std::vector<std::vector<Fq>> full;
+      int r2 = single ? gather_first({&Zp}, full) : gather_first({&Zp, &ABC}, full);
+      if (r2) return r2;
+      Fq* buf = (Fq*)ws_get(ctx, WS_C2, 2 * P * sizeof(Fq) + 64);
+      if (!buf) return set_err(ctx, SPG_E_NOMEM, "compact tables");
+      SPG_HIP(ctx, hipMemcpyAsync(buf, full[0].data(), P * sizeof(Fq), hipMemcpyHostToDevice, s));
+      if (single) {  // the shared ABC keeps its single (0,0,0,0) element
+        SPG_HIP(ctx, hipMemcpyAsync(buf + P, ABC.d, sizeof(Fq), hipMemcpyDeviceToDevice, s));
+      } else {
+        SPG_HIP(ctx, hipMemcpyAsync(buf + P, full[1].data(), P * sizeof(Fq), hipMemcpyHostToDevice, s));
+      }
+      SPG_HIP(ctx, hipStreamSynchronize(s));
+      Zc = compact_table(buf, P, P);
+      ABCc = compact_table(buf + P, single ? 1 : P, P);
+      TZ = &Zc;
+      TA = &ABCc;
+      return 0;
+    };
+    if (rounds && ny + nw == 0) rc = to_compact();
+    if (!rc && rounds) rc = launch_eval(0);
     if (rc) return rc;
     for (size_t j = 0; j < rounds; j++) {
       int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       Fq e[3];
       rc = eval_wait(ctx, e);
+      if (!rc && mode != MODE_P) rc = sum_ranks(e);
       if (rc) return rc;
       lp.lap("p2_eval");
       Fq r_j = zk.begin(g, t, j, e);
       lp.lap("p2_host");
       if (mode == MODE_P) { rc = dev_fold_top(ctx, eq_p, lenP, r_j); lenP /= 2; }
-      if (!rc && (mode != MODE_P || !single)) rc = pqx_bound(ctx, ABC, nullptr, nullptr, r_j, mode);
-      if (!rc) rc = pqx_bound(ctx, Zp, nullptr, nullptr, r_j, mode);
+      if (!rc && (mode != MODE_P || !single)) rc = pqx_bound(ctx, *TA, nullptr, nullptr, r_j, mode);
+      if (!rc) rc = pqx_bound(ctx, *TZ, nullptr, nullptr, r_j, mode);
+      if (!rc && j + 1 == ny + nw && np > 0) rc = to_compact();
       if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
       if (rc) return rc;
       lp.lap("p2_fold");
@@ -688,8 +878,8 @@ int Prover::run_inner(Laps& lp) {
       ry_all.push_back(r_j);
     }
     rc = d2h_fq(ctx, eq_p, &claims2[0]);
-    if (!rc) rc = d2h_fq(ctx, ABC.d, &claims2[1]);
-    if (!rc) rc = d2h_fq(ctx, Zp.d, &claims2[2]);
+    if (!rc) rc = d2h_fq(ctx, TA->d, &claims2[1]);
+    if (!rc) rc = d2h_fq(ctx, TZ->d, &claims2[2]);
     if (rc) return rc;
     blind_post2 = zk.blinds_evals[rounds - 1];
     pf.sc2 = std::move(zk.out);
@@ -702,22 +892,33 @@ int Prover::run_inner(Laps& lp) {
   FqV ry_factors(ny + 1, fq_one());
   for (size_t i = 0; i < ny; i++) ry_factors[i + 1] = fq_mul(ry_factors[i], fq_sub(fq_one(), ry[i]));
   struct PolyRef {
-    size_t w, p, np, ni;
+    size_t w, p, np, ni, Rs;
+    bool mine;
     FqV LZ, R;
     Fq ev;
   };
   std::vector<PolyRef> polys;
-  std::vector<FqV> eval_list(nws);
-  pf.comm_vars_at_ry_list.assign(nws, {});
+  size_t lz_total = 0;
   for (size_t i = 0; i < nws; i++) {
-    eval_list.push_back({});
-    pf.comm_vars_at_ry_list.push_back({});
     for (size_t p = 0; p < wit.num_proofs[i].size(); p++) {
       PolyRef pr;
       pr.w = i;
       pr.p = p;
       pr.np = wit.num_proofs[i][p];
       pr.ni = wit.num_inputs[i][p];
+      size_t lnp = lg2(pr.np), lni = lg2(pr.ni);
+      size_t nv = lnp + (pr.ni >= Y ? lni : lni);
+      pr.Rs = (size_t)1 << (nv - nv / 2);
+      pr.mine = wit.num_proofs[i].size() == 1 ? rank == 0 : (p >= p0 && p < p1);
+      lz_total += pr.Rs;
+      polys.push_back(std::move(pr));
+    }
+  }
+  // LZ = bound(L) of each owned polynomial on this rank's device, then shared with every rank
+  std::vector<Fq> lz_mine(lz_total, fq_zero());
+  {
+    size_t o = 0;
+    for (auto& pr : polys) {
       size_t lnp = lg2(pr.np), lni = lg2(pr.ni);
       FqV r(rq.begin() + (nq - lnp), rq.end());
       if (pr.ni >= Y) {
@@ -730,33 +931,59 @@ int Prover::run_inner(Laps& lp) {
       FqV rl(r.begin(), r.begin() + ln), rr(r.begin() + ln, r.end());
       size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
       pr.R = eq_evals_host(rr);
-      // LZ = bound(L) on the device
-      Fq* dL = (Fq*)ws_get(ctx, WS_L, Ls * sizeof(Fq) + 64);
-      uint32_t nbx = (uint32_t)((Rs + 255) / 256);
-      uint32_t S = (uint32_t)std::min<size_t>(Ls, 32);  // 32 partial rows: short column sums
-      uint32_t chunk = (uint32_t)((Ls + S - 1) / S);
-      S = (uint32_t)((Ls + chunk - 1) / chunk);
-      Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, (size_t)S * Rs * sizeof(Fq) + 64);
-      Fq* dout = (Fq*)ws_get(ctx, WS_BOUT, Rs * sizeof(Fq) + 64);
-      if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "bound");
-      rc = eq_table(ctx, rl, dL);
-      if (rc) return rc;
-      {
-        KScope ks(ctx, "poly_bound", 32.0 * Ls * Rs + 32.0 * Ls + 64.0 * S * Rs);
-        hipLaunchKernelGGL(k_bound_part, dim3(nbx, S), dim3(256), 0, s, wit.d_w + wit.off[i][p], dL, (uint32_t)Ls,
-                           (uint32_t)Rs, chunk, dpart);
-        hipLaunchKernelGGL(k_sum_cols, dim3(nbx), dim3(256), 0, s, dpart, S, (uint32_t)Rs, dout);
+      if (pr.mine) {
+        Fq* dL = (Fq*)ws_get(ctx, WS_L, Ls * sizeof(Fq) + 64);
+        uint32_t nbx = (uint32_t)((Rs + 255) / 256);
+        uint32_t S = (uint32_t)std::min<size_t>(Ls, 32);  // 32 partial rows: short column sums
+        uint32_t chunk = (uint32_t)((Ls + S - 1) / S);
+        S = (uint32_t)((Ls + chunk - 1) / chunk);
+        Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, (size_t)S * Rs * sizeof(Fq) + 64);
+        Fq* dout = (Fq*)ws_get(ctx, WS_BOUT, Rs * sizeof(Fq) + 64);
+        if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "bound");
+        rc = eq_table(ctx, rl, dL);
+        if (rc) return rc;
+        {
+          KScope ks(ctx, "poly_bound", 32.0 * Ls * Rs + 32.0 * Ls + 64.0 * S * Rs);
+          hipLaunchKernelGGL(k_bound_part, dim3(nbx, S), dim3(256), 0, s, wit.d_w + wit.off[pr.w][pr.p], dL,
+                             (uint32_t)Ls, (uint32_t)Rs, chunk, dpart);
+          hipLaunchKernelGGL(k_sum_cols, dim3(nbx), dim3(256), 0, s, dpart, S, (uint32_t)Rs, dout);
+        }
+        SPG_HIP(ctx, hipGetLastError());
+        rc = d2h_fq(ctx, dout, lz_mine.data() + o, Rs);
+        if (rc) return rc;
       }
-      SPG_HIP(ctx, hipGetLastError());
-      pr.LZ.resize(Rs);
-      rc = d2h_fq(ctx, dout, pr.LZ.data(), Rs);
-      if (rc) return rc;
-      Fq ev = fq_zero();
-      for (size_t k = 0; k < Rs; k++) ev = fq_add(ev, fq_mul(pr.LZ[k], pr.R[k]));
-      pr.ev = ev;
-      eval_list[i].push_back(pr.ni >= Y ? ev : fq_mul(ev, ry_factors[ny - lni]));
-      pf.comm_vars_at_ry_list[i].push_back(commit_batch(g, {CJob(g.gens_1, {ev}, fq_zero())})[0]);
-      polys.push_back(std::move(pr));
+      o += Rs;
+    }
+  }
+  {
+    std::vector<uint8_t> r;
+    rc = allgather(lz_mine.data(), lz_total * sizeof(Fq), r);
+    if (rc) return rc;
+    const Fq* v = (const Fq*)r.data();
+    size_t o = 0;
+    for (auto& pr : polys) {
+      size_t owner = 0;
+      if (wit.num_proofs[pr.w].size() != 1) owner = pr.p / ((P + nranks - 1) / nranks);
+      pr.LZ.assign(v + owner * lz_total + o, v + owner * lz_total + o + pr.Rs);
+      o += pr.Rs;
+    }
+  }
+  std::vector<FqV> eval_list(nws);
+  pf.comm_vars_at_ry_list.assign(nws, {});
+  {
+    size_t k = 0;
+    for (size_t i = 0; i < nws; i++) {
+      eval_list.push_back({});
+      pf.comm_vars_at_ry_list.push_back({});
+      for (size_t p = 0; p < wit.num_proofs[i].size(); p++, k++) {
+        PolyRef& pr = polys[k];
+        Fq ev = fq_zero();
+        for (size_t m = 0; m < pr.Rs; m++) ev = fq_add(ev, fq_mul(pr.LZ[m], pr.R[m]));
+        pr.ev = ev;
+        size_t lni = lg2(pr.ni);
+        eval_list[i].push_back(pr.ni >= Y ? ev : fq_mul(ev, ry_factors[ny - lni]));
+        pf.comm_vars_at_ry_list[i].push_back(commit_batch(g, {CJob(g.gens_1, {ev}, fq_zero())})[0]);
+      }
     }
   }
   lp.lap("polyeval_bound");
@@ -1040,7 +1267,8 @@ extern "C" int spg_r1cs_inst_free(spg_ctx* ctx, spg_r1cs_inst* I) {
   return SPG_OK;
 }
 
-extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, spg_r1cs_witness** out) {
+static int witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, size_t p0, size_t p1,
+                       spg_r1cs_witness** out) {
   if (!ctx || !secs || !out || nws == 0) return SPG_E_ARG;
   if (nws > 8) return set_err(ctx, SPG_E_ARG, "at most 8 witness sections (prefix_list)");
   spg_r1cs_witness* W = new spg_r1cs_witness();
@@ -1062,8 +1290,13 @@ extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, s
       }
       W->num_proofs[w].push_back(s.num_proofs[p]);
       W->num_inputs[w].push_back(s.num_inputs[p]);
-      W->off[w].push_back(total);
-      total += s.num_proofs[p] * s.num_inputs[p];
+      bool here = s.num_instances == 1 || (p >= p0 && p < p1);
+      if (here && !s.w[p]) {
+        delete W;
+        return set_err(ctx, SPG_E_ARG, "missing witness data for a resident instance");
+      }
+      W->off[w].push_back(here ? total : kNotResident);
+      if (here) total += s.num_proofs[p] * s.num_inputs[p];
     }
   }
   W->total = total;
@@ -1073,6 +1306,7 @@ extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, s
   }
   for (size_t w = 0; w < nws; w++)
     for (size_t p = 0; p < secs[w].num_instances; p++) {
+      if (W->off[w][p] == kNotResident) continue;
       size_t n = W->num_proofs[w][p] * W->num_inputs[w][p];
       // Scalar([u64; 4]) and Fq(u32[8]) share the little-endian byte image
       if (hipMemcpyAsync(W->d_w + W->off[w][p], secs[w].w[p], n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream) !=
@@ -1087,6 +1321,13 @@ extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, s
   }
   *out = W;
   return SPG_OK;
+}
+extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, spg_r1cs_witness** out) {
+  return witness_new(ctx, secs, nws, 0, ~(size_t)0, out);
+}
+extern "C" int spg_r1cs_witness_new_shard(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, size_t p0,
+                                          size_t p1, spg_r1cs_witness** out) {
+  return witness_new(ctx, secs, nws, p0, p1, out);
 }
 extern "C" int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* W) {
   (void)ctx;
@@ -1125,6 +1366,15 @@ extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg
     }
   }
   Prover pr(ctx, const_cast<spg_r1cs_gens*>(gens)->g, *inst, *wit, transcript->t, tape->t);
+  pr.rank = (size_t)ctx->rank;
+  pr.nranks = (size_t)ctx->nranks;
+  if (pr.nranks > num_instances) return set_err(ctx, SPG_E_ARG, "more ranks than instances");
+  {
+    size_t PL = (num_instances + pr.nranks - 1) / pr.nranks;
+    pr.p0 = std::min(num_instances, pr.rank * PL);
+    pr.p1 = std::min(num_instances, pr.p0 + PL);
+    if (pr.p0 >= pr.p1) return set_err(ctx, SPG_E_ARG, "rank holds no instance (use fewer ranks)");
+  }
   pr.P = num_instances;
   pr.max_np = max_num_proofs;
   pr.Y = max_num_inputs;
@@ -1147,5 +1397,64 @@ extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg
   }
   if (!proof || wr.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, wr.out.data(), wr.out.size());
+  return SPG_OK;
+}
+
+// R1CSInstance::multi_evaluate (src/r1csinstance.rs:583-596) / evaluate (:632-641):
+// out[3p + m] = M_p(rx, ry) for M in (A, B, C), p < num_instances of the uploaded instance
+extern "C" int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, const uint64_t* rx, size_t rx_len,
+                                       const uint64_t* ry, size_t ry_len, uint64_t* out) {
+  if (!ctx || !inst || !out || (!rx && rx_len) || (!ry && ry_len)) return SPG_E_ARG;
+  if (rx_len > 32 || ry_len > 32 || ((size_t)1 << rx_len) < inst->max_num_cons ||
+      ((size_t)1 << ry_len) < inst->num_vars)
+    return set_err(ctx, SPG_E_ARG, "multi_evaluate: rx / ry shorter than the matrix dimensions");
+  hipStream_t s = ctx->stream;
+  const size_t Pm = inst->num_instances;
+  FqV vx(rx_len), vy(ry_len);
+  for (size_t i = 0; i < rx_len; i++) vx[i] = ld_fq(rx + 4 * i);
+  for (size_t i = 0; i < ry_len; i++) vy[i] = ld_fq(ry + 4 * i);
+  Fq* erx = (Fq*)ws_get(ctx, WS_EV_RX, (sizeof(Fq) << rx_len) + 64);
+  Fq* ery = (Fq*)ws_get(ctx, WS_EV_RY, (sizeof(Fq) << ry_len) + 64);
+  size_t maxrows = 0;
+  for (size_t p = 0; p < Pm; p++) maxrows = std::max(maxrows, inst->num_cons[p]);
+  const unsigned nblk = blocks_for(maxrows);
+  Fq* part = (Fq*)ws_get(ctx, WS_EV_PART, 3 * Pm * nblk * sizeof(Fq) + 64);
+  Fq* dout = (Fq*)ws_get(ctx, WS_EV_OUT, 3 * Pm * sizeof(Fq) + 64);
+  uint8_t* ddesc = (uint8_t*)ws_get(ctx, WS_EV_DESC, Pm * (sizeof(MatDesc) + 4) + 64);
+  if (!erx || !ery || !part || !dout || !ddesc) return set_err(ctx, SPG_E_NOMEM, "multi_evaluate");
+  std::vector<MatDesc> md(Pm);
+  std::vector<uint32_t> nr(Pm);
+  double visits = 0;
+  for (size_t p = 0; p < Pm; p++) {
+    for (int m = 0; m < 3; m++) md[p].rp[m] = inst->rp_off[3 * p + m];
+    md[p].cp = inst->cp_off[p];
+    nr[p] = (uint32_t)inst->num_cons[p];
+    visits += inst->nnz[3 * p] + inst->nnz[3 * p + 1] + inst->nnz[3 * p + 2];
+  }
+  MatDesc* dmd = (MatDesc*)ddesc;
+  uint32_t* dnr = (uint32_t*)(ddesc + Pm * sizeof(MatDesc));
+  SPG_HIP(ctx, hipMemcpyAsync(dmd, md.data(), Pm * sizeof(MatDesc), hipMemcpyHostToDevice, s));
+  SPG_HIP(ctx, hipMemcpyAsync(dnr, nr.data(), Pm * 4, hipMemcpyHostToDevice, s));
+  timer_start(ctx);
+  int rc = eq_table(ctx, vx, erx);
+  if (!rc) rc = eq_table(ctx, vy, ery);
+  if (rc) return rc;
+  {
+    double rows = 0;
+    for (size_t p = 0; p < Pm; p++) rows += 3.0 * inst->num_cons[p];
+    KScope ks(ctx, "sparse_eval", 68.0 * visits + 40.0 * rows);
+    hipLaunchKernelGGL(k_sparse_eval, dim3(nblk, (unsigned)(3 * Pm)), dim3(256), 0, s, dmd, dnr, inst->d_rowptr,
+                       inst->d_col, inst->d_val, erx, ery, part);
+    hipLaunchKernelGGL(k_sum_segments, dim3((unsigned)(3 * Pm)), dim3(256), 0, s, part, (int)nblk, dout);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  timer_stop(ctx);
+  std::vector<Fq> h(3 * Pm);
+  SPG_HIP(ctx, hipMemcpyAsync(h.data(), dout, 3 * Pm * sizeof(Fq), hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  ctx->last_us = ms * 1000.0;
+  for (size_t i = 0; i < 3 * Pm; i++) st_fq(out + 4 * i, h[i]);
   return SPG_OK;
 }

@@ -41,6 +41,36 @@ class SpgError(RuntimeError):
     pass
 
 
+# int (*spg_allgather_fn)(void* user, const void* send, size_t bytes, void* recv)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+def torch_allgather(dist, group=None, device="cpu"):
+    """An spg_allgather_fn over torch.distributed (gloo: device='cpu'; nccl = RCCL: device='cuda:<local>'):
+    the `bytes` of rank k land at recv + k * bytes on every rank."""
+    import torch
+
+    def cb(user, send, nbytes, recv):
+        try:
+            world = dist.get_world_size(group)
+            buf = bytearray(ctypes.string_at(send, nbytes)) if nbytes else bytearray(1)
+            src = torch.frombuffer(buf, dtype=torch.uint8).to(device)
+            outs = [torch.empty_like(src) for _ in range(world)]
+            dist.all_gather(outs, src, group=group)
+            flat = torch.cat(outs).cpu().numpy() if nbytes else None
+            if nbytes:
+                for k in range(world):
+                    ctypes.memmove(recv + k * nbytes, flat[k * len(buf):].ctypes.data, nbytes)
+            return 0
+        except Exception as e:  # noqa: BLE001 - reported through the return code
+            import sys
+
+            print(f"spg allgather callback failed: {e!r}", file=sys.stderr)
+            return 1
+
+    return ALLGATHER_FN(cb)
+
+
 class Context:
     def __init__(self, device=0):
         self._h = ctypes.c_void_p()
@@ -56,6 +86,12 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_comm(self, rank, nranks, allgather_fn=None):
+        """spg_set_comm: shard R1CSProof::prove by instance over nranks processes (one GPU each)."""
+        self._comm = allgather_fn  # keep the ctypes thunk alive
+        fn = allgather_fn if allgather_fn is not None else ctypes.cast(None, ALLGATHER_FN)
+        self.check(lib().spg_set_comm(self._h, ctypes.c_int(rank), ctypes.c_int(nranks), fn, None), "spg_set_comm")
 
     def last_kernel_us(self):
         return lib().spg_last_kernel_us(self._h)
@@ -316,14 +352,30 @@ class R1CSInst:
             pass
 
 
-class R1CSWitness:
-    """Witness sections (Vec<&ProverWitnessSecInfo>) resident in HBM. `secs` is workload.CViews().secs."""
+def r1cs_multi_evaluate(ctx, inst, num_instances, rx, ry):
+    """R1CSInstance::multi_evaluate -> (3 * num_instances, 4) limbs [A_0, B_0, C_0, A_1, ...]"""
+    rx = _scalars(rx)
+    ry = _scalars(ry)
+    out = np.zeros((3 * num_instances, 4), dtype=np.uint64)
+    ctx.check(lib().spg_r1cs_multi_evaluate(ctx.handle, inst.handle, _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
+                                            ctypes.c_size_t(ry.shape[0]), _p(out)), "spg_r1cs_multi_evaluate")
+    return out
 
-    def __init__(self, ctx, secs, nws):
+
+class R1CSWitness:
+    """Witness sections (Vec<&ProverWitnessSecInfo>) resident in HBM. `secs` is workload.CViews().secs.
+    shard=(p0, p1): upload only instances [p0, p1) of the per-instance sections (sharded proving)."""
+
+    def __init__(self, ctx, secs, nws, shard=None):
         self.ctx = ctx
         self._h = ctypes.c_void_p()
-        ctx.check(lib().spg_r1cs_witness_new(ctx.handle, secs, ctypes.c_size_t(nws), ctypes.byref(self._h)),
-                  "spg_r1cs_witness_new")
+        if shard is None:
+            ctx.check(lib().spg_r1cs_witness_new(ctx.handle, secs, ctypes.c_size_t(nws), ctypes.byref(self._h)),
+                      "spg_r1cs_witness_new")
+        else:
+            ctx.check(lib().spg_r1cs_witness_new_shard(ctx.handle, secs, ctypes.c_size_t(nws), ctypes.c_size_t(shard[0]),
+                                                       ctypes.c_size_t(shard[1]), ctypes.byref(self._h)),
+                      "spg_r1cs_witness_new_shard")
 
     @property
     def handle(self):
@@ -357,3 +409,10 @@ def r1cs_prove(ctx, gens, inst, witness, num_instances, max_num_proofs, num_proo
         out.append(ch[o:o + L].copy())
         o += L
     return buf[: ln.value].tobytes(), out
+
+
+def shard_range(num_instances, rank, nranks):
+    """instances [p0, p1) held by `rank` in a sharded R1CSProof (include/spg.h, spg_set_comm)"""
+    per = -(-num_instances // nranks)
+    p0 = min(num_instances, rank * per)
+    return p0, min(num_instances, p0 + per)

@@ -63,3 +63,23 @@ def test_r1cs_proof_is_repeatable(ctx, r1cs_gens):
     b, _ = gpu_prove(ctx, r1cs_gens, wl, workload.tape_seed())
     c, _ = gpu_prove(ctx, r1cs_gens, wl, workload.tape_seed(b"x"))
     assert a == b and a != c
+
+
+@pytest.mark.parametrize("case", ["p3_ragged_3secs", "shared_p2", "p2_x1024_q64"])
+def test_multi_evaluate_matches_oracle(ctx, oracle, case):
+    """R1CSInstance::multi_evaluate on the GPU (k_sparse_eval) vs the oracle at random (rx, ry)."""
+    import spg
+    import workload
+
+    nc, npf, nws, shared = ALL[case]
+    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+    rng = np.random.default_rng(5)
+    nx = (wl.max_num_cons - 1).bit_length()
+    ny = (wl.num_vars - 1).bit_length()
+    r = oracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * (nx + ny), dtype=np.uint8).tobytes())
+    rx, ry = r[:nx], r[nx:]
+    v = workload.CViews(wl)
+    inst = spg.R1CSInst(ctx, v.inst)
+    got = spg.r1cs_multi_evaluate(ctx, inst, len(wl.entries), rx, ry)
+    ref = oracle.r1cs_multi_evaluate(wl, rx, ry)
+    assert np.array_equal(got, ref)
