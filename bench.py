@@ -9,8 +9,12 @@ runs for its blocks (src/r1csproof.rs:210-685, called from src/lib.rs:2259-2490)
 X = 2^10 constraints each, Q = 2^9 executions each -> N = 2^20 constraints, synthetic chain-of-squarings
 circuit (spartan-parallel_amd/workload.py). A step is one full R1CSProof::prove with the instance,
 witness and generators already resident in HBM; the proof bytes are produced in every step.
-Multi-GPU: every rank proves its own 2^20-constraint instance (independent proofs, no collective on the
-data path) -> weak scaling; value = all ranks' constraints / max-over-ranks time.
+Multi-GPU (--mode):
+  replicas (default): every rank proves its own 2^20-constraint R1CS (independent proofs, no collective on
+           the data path) -> weak scaling; value = all ranks' constraints / max-over-ranks time.
+  shard:   ONE proof over 2N instances (2^20 constraints per GPU) sharded by instance across the N ranks;
+           per sumcheck round the ranks allgather 96 B of partial sums (spg_set_comm over torch.distributed:
+           RCCL with --backend nccl) and replicate the transcript -> weak scaling of a single proof.
 
 `roofline` is computed for the kernel with the largest device time among those with an algorithmic
 byte model (libspg's per-launch HIP-event timing on the context stream, spg_prof_read), `cpu_baseline`
@@ -44,6 +48,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="r1cs_2e20", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="replicas", choices=["replicas", "shard"])
+    ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 --pmc (scripts/pmc_traffic.py), if present")
     return ap.parse_args()
@@ -57,26 +63,37 @@ def main():
     import torch
 
     dist = None
+    backend = a.backend or ("nccl" if torch.cuda.is_available() else "gloo")
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend)
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if ndev else local  # ranks share a GPU only when there are fewer GPUs (rehearsals)
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(gpu)
 
     import spg
     import workload
 
     nc, npf, nws = CONFIGS[a.config]
-    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, seed=0x5350415254414E31 + rank)
+    shard = a.mode == "shard" and world > 1
+    ctx = spg.Context(gpu)
+    if shard:
+        nc, npf = nc * world, npf * world  # one proof over world x the per-GPU instances
+        p0, p1 = spg.shard_range(len(nc), rank, world)
+        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, instances=range(p0, p1))
+        dev = f"cuda:{gpu}" if backend == "nccl" else "cpu"
+        ctx.set_comm(rank, world, spg.torch_allgather(dist, device=dev))
+    else:
+        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, seed=0x5350415254414E31 + rank)
     seed = workload.tape_seed()
-    ctx = spg.Context(local)
     gens = spg.R1CSGens(ctx, GENS_LABEL, GENS_NUM_VARS)
     views = workload.CViews(wl)
     inst = spg.R1CSInst(ctx, views.inst)
 
     def upload():
-        return spg.R1CSWitness(ctx, views.secs, wl.nws)
+        return spg.R1CSWitness(ctx, views.secs, wl.nws, shard=(p0, p1) if shard else None)
 
     wit = upload()
 
@@ -119,7 +136,7 @@ def main():
     step()
     t_incl = time.perf_counter() - t1
 
-    N = wl.total_constraints
+    N = wl.total_constraints // world if shard else wl.total_constraints  # per GPU
     value = N * world * a.steps / dt
     ms = dt / a.steps * 1e3
 
@@ -167,7 +184,9 @@ def main():
             "config": {"workload": "R1CSProof::prove, block-sat proof of SNARK::prove (src/r1csproof.rs:210-685)",
                        "num_instances": wl.P, "num_cons": nc, "num_proofs": npf, "witness_sections": nws,
                        "constraints_per_gpu": N, "max_num_inputs": wl.max_num_inputs,
-                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{world}"},
+                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)",
+                       "parallelism": f"instance-sharded single proof x{world} ({backend})" if shard
+                       else f"replicas x{world}"},
             "roofline": roof, "cpu_baseline": cpu, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16], "device_busy_ms_per_step": round(device_ms, 3),
             "value_incl_witness_upload": round(N * world / t_incl, 1), "kernels": kernels,

@@ -50,7 +50,10 @@ class R1CSWorkload:
     """Inputs of R1CSProof::prove (src/r1csproof.rs:210-230) for the synthetic circuit."""
 
     def __init__(self, num_cons, num_proofs, num_sections=1, max_num_inputs=None, seed=0x5350415254414E31,
-                 shared_instance=False):
+                 shared_instance=False, instances=None):
+        """instances: generate witness data only for these instance indices (sharded proving); every
+        instance then draws from its own stream seed ^ (p+1)*0x9E3779B97F4A7C15, so any rank can build its
+        shard alone. None: all instances from one sequential stream (the layout the fixtures pin)."""
         self.P = len(num_cons)
         assert len(num_proofs) == self.P
         for x in list(num_cons) + list(num_proofs):
@@ -92,10 +95,16 @@ class R1CSWorkload:
             self.entries.append(mats)
         # ---- witness sections: w_mat[p] = (num_proofs[p], num_inputs[p]) scalars
         self.sections = []
+        inst_state = {}
         for w in range(num_sections):
             mats = []
             for p in range(self.P):
                 X, Y, Qp = self.num_cons[p], self.num_inputs[p], self.num_proofs[p]
+                if instances is not None:
+                    if p not in instances:
+                        mats.append(None)
+                        continue
+                    state = inst_state.get(p, (seed ^ ((p + 1) * 0x9E3779B97F4A7C15)) & MASK64)
                 if w == 0:
                     half = X // 2 if (num_sections > 1 and X >= 2) else X
                     seeds, state = random_fq(Qp, state)
@@ -111,6 +120,8 @@ class R1CSWorkload:
                 else:
                     vals, state = random_fq(Qp * Y, state)
                     mats.append(to_mont_limbs(vals).reshape(Qp, Y, 4))
+                if instances is not None:
+                    inst_state[p] = state
             self.sections.append(mats)
 
     @property
@@ -166,11 +177,14 @@ class CViews:
             mats = wl.sections[w]
             wp = (ctypes.c_void_p * len(mats))()
             for p, m in enumerate(mats):
+                if m is None:  # held by another rank
+                    wp[p] = None
+                    continue
                 arr = np.ascontiguousarray(m)
                 self.keep.append(arr)
                 wp[p] = arr.ctypes.data
-            npf = _sz([m.shape[0] for m in mats])
-            nin = _sz([m.shape[1] for m in mats])
+            npf = _sz([wl.num_proofs[p] if m is None else m.shape[0] for p, m in enumerate(mats)])
+            nin = _sz([wl.num_inputs[p] if m is None else m.shape[1] for p, m in enumerate(mats)])
             self.sec_keep.append((wp, npf, nin))
             secs[w] = CWitnessSec(len(mats), npf, nin, wp)
         self.secs = secs
