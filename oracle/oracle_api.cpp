@@ -310,3 +310,51 @@ int orc_r1cs_multi_evaluate(const spg_r1cs_instance* ci, const uint64_t* rx, siz
   return 0;
 }
 }
+
+#include "spark.hpp"
+
+extern "C" {
+// SPARK on the matrices of an R1CS instance, batch = [A_0, B_0, C_0, A_1, ...] (R1CSInstance::commit,
+// src/r1csinstance.rs:722-737) with SparseMatPolyCommitmentGens(label, nvx, nvy, gens_nnz, gens_batch)
+// (R1CSCommitmentGens::new passes num_instances*nnz and batch 3, src/r1csinstance.rs:39-56).
+// Proves SparseMatPolyEvalProof at (rx, ry) for evals = multi_evaluate(rx, ry) under a fresh
+// Transcript(label) + RandomTape("proof", seed), writes bincode(commitment) and bincode(proof), then runs
+// the verifier on a fresh transcript. Returns 1 if it verifies, 0 if not, <0 on error.
+int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t gens_nnz, size_t gens_batch,
+                    const uint64_t* rx, size_t rx_len, const uint64_t* ry, size_t ry_len, const char* label,
+                    const uint64_t* tape_seed, uint8_t* comm_out, size_t comm_cap, size_t* comm_len,
+                    uint8_t* proof_out, size_t proof_cap, size_t* proof_len) {
+  try {
+    R1CSInstance inst = inst_from_c(ci);
+    std::vector<const SparseMat*> polys;
+    for (size_t p = 0; p < inst.num_instances; p++) {
+      polys.push_back(&inst.A[p]);
+      polys.push_back(&inst.B[p]);
+      polys.push_back(&inst.C[p]);
+    }
+    FqVec vx, vy;
+    for (size_t i = 0; i < rx_len; i++) vx.push_back(ld(rx + 4 * i));
+    for (size_t i = 0; i < ry_len; i++) vy.push_back(ld(ry + 4 * i));
+    size_t nvx = polys[0]->num_vars_x, nvy = polys[0]->num_vars_y;
+    SparkGens g = SparkGens::create(gens_label, nvx, nvy, gens_nnz, gens_batch);
+    MultiSparseDense dense;
+    SparkCommitment comm = spark_multi_commit(polys, g, &dense);
+    FqVec evals = inst.multi_evaluate(vx, vy);
+    Transcript t(label);
+    RandomTape tape("proof", ld(tape_seed));
+    SparkEvalProof pf = spark_prove(dense, vx, vy, evals, g, t, tape);
+    Ser sc, sp;
+    comm.ser(sc);
+    pf.ser(sp);
+    *comm_len = sc.b.size();
+    *proof_len = sp.b.size();
+    if (sc.b.size() > comm_cap || sp.b.size() > proof_cap) return -1;
+    memcpy(comm_out, sc.b.data(), sc.b.size());
+    memcpy(proof_out, sp.b.data(), sp.b.size());
+    Transcript tv(label);
+    return spark_verify(pf, comm, vx, vy, evals, g, tv) ? 1 : 0;
+  } catch (const std::string& e) {
+    return -2;
+  }
+}
+}

@@ -238,3 +238,27 @@ def r1cs_multi_evaluate(wl, rx, ry):
                                        ctypes.c_size_t(ry.shape[0]), _p(out))
     assert rc == 0
     return out
+
+
+def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=None, gens_batch=3,
+                label=b"spark_test"):
+    """SparseMatPolyEvalProof over [A_0, B_0, C_0, ...] of the workload's instance at (rx, ry):
+    (bincode(commitment), bincode(proof), verified)"""
+    import workload
+
+    v = workload.CViews(wl)
+    rx = u64s(rx).reshape(-1, 4)
+    ry = u64s(ry).reshape(-1, 4)
+    if gens_nnz is None:  # R1CSCommitmentGens::new: num_instances * num_nz_entries (src/r1csinstance.rs:39-56)
+        gens_nnz = len(wl.entries) * max(max(int(m.shape[0]) for m in mats) for mats in wl.entries)
+    cb = np.zeros(1 << 20, dtype=np.uint8)
+    pb = np.zeros(1 << 22, dtype=np.uint8)
+    cl, pl = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    seed = u64s(tape_seed)
+    rc = lib().orc_spark_prove(ctypes.byref(v.inst), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_nnz),
+                               ctypes.c_size_t(gens_batch), _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
+                               ctypes.c_size_t(ry.shape[0]), ctypes.c_char_p(label), _p(seed), _p(cb),
+                               ctypes.c_size_t(len(cb)), ctypes.byref(cl), _p(pb), ctypes.c_size_t(len(pb)),
+                               ctypes.byref(pl))
+    assert rc >= 0, rc
+    return cb[: cl.value].tobytes(), pb[: pl.value].tobytes(), rc == 1

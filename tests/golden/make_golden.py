@@ -178,10 +178,32 @@ def r1cs_fixture():
     return out
 
 
+def spark_fixture():
+    """sha256 of bincode(SparseMatPolyCommitment) and bincode(SparseMatPolyEvalProof) from the oracle, each
+    after its verifier accepted (tests/r1cs_cases.py SPARK_CASES)."""
+    sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import workload
+    from r1cs_cases import SPARK_CASES
+    from test_oracle_spark import spark_inputs
+
+    out = {}
+    for name in sorted(SPARK_CASES):
+        wl, rx, ry = spark_inputs(O, name)
+        comm, proof, ok = O.spark_prove(wl, rx, ry, workload.tape_seed())
+        assert ok, name
+        out[name] = {"comm_sha256": hashlib.sha256(comm).hexdigest(), "proof_sha256": hashlib.sha256(proof).hexdigest(),
+                     "proof_len": len(proof)}
+    return out
+
+
 def main():
     O.build()
     if sys.argv[1:] == ["r1cs"]:
         json.dump(r1cs_fixture(), open(os.path.join(HERE, "r1cs_proofs.json"), "w"), indent=1)
+        return
+    if sys.argv[1:] == ["spark"]:
+        json.dump(spark_fixture(), open(os.path.join(HERE, "spark_proofs.json"), "w"), indent=1)
         return
     rng = np.random.default_rng(0x5350415254414E31)
     lib = sodium()
@@ -193,6 +215,7 @@ def main():
     w("msm_64.json", msm_fixture(lib, rng, b"gens_r1cs_sat", 64))
     w("msm_256.json", msm_fixture(lib, rng, b"spg_bench_msm", 256))
     w("r1cs_proofs.json", r1cs_fixture())
+    w("spark_proofs.json", spark_fixture())
     print("golden fixtures written to", HERE)
 
 

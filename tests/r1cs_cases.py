@@ -15,3 +15,13 @@ GPU_CASES = {
     "p2_x1024_q64": ([1024, 1024], [64, 64], 1, False),
     "p8_x256_q32_shared": ([256] * 8, [32] * 8, 1, True),
 }
+# SPARK (SparseMatPolyEvalProof) cases: the batch is [A_0, B_0, C_0, A_1, ...] of the workload's instance
+SPARK_CASES = {
+    "p1_x16": ([16], [4], 1, False),
+    "p2_x64_2secs": ([64, 64], [8, 8], 2, False),
+    "shared_x32": ([32, 32, 32], [4, 4, 4], 1, True),
+    "p2_x256": ([256, 256], [4, 4], 1, False),
+}
+GPU_SPARK_CASES = {
+    "p2_x4096": ([4096, 4096], [2, 2], 1, False),
+}
