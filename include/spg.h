@@ -170,6 +170,24 @@ int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst*
 int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, const uint64_t* rx, size_t rx_len,
                             const uint64_t* ry, size_t ry_len, uint64_t* out);
 
+/* ---- SPARK: sparse matrix polynomial commitments and evaluation proofs ------------------------------
+ * The batch is the 3P matrices A_0, B_0, C_0, A_1, ... of an R1CS instance (R1CSInstance::multi_commit,
+ * src/r1csinstance.rs:645-700 -> SparseMatPolynomial::multi_commit, src/sparse_mlpoly.rs:566-587).
+ * The dense representation (addresses, timestamps, values, comb_ops / comb_mem) stays in HBM. */
+typedef struct spg_spark spg_spark;
+/* SparseMatPolyCommitmentGens::new(label, nvx, nvy, gens_nnz, gens_batch) (src/sparse_mlpoly.rs:289-317)
+ * + multi_commit. Writes bincode(SparseMatPolyCommitment) into comm (*comm_len = its size). */
+int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* inst, const uint8_t* label, size_t label_len,
+                     size_t gens_nnz, size_t gens_batch, spg_spark** out, uint8_t* comm, size_t comm_cap,
+                     size_t* comm_len);
+/* SparseMatPolyEvalProof::prove(dense, rx, ry, evals, gens, transcript, random_tape)
+ * (src/sparse_mlpoly.rs:1497-1564): evals[3p + m] = M_p(rx, ry) (spg_r1cs_multi_evaluate).
+ * Writes bincode(SparseMatPolyEvalProof) into proof (*proof_len = its size even when it does not fit). */
+int spg_spark_prove(spg_ctx* ctx, spg_spark* s, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                    size_t ry_len, const uint64_t* evals, size_t n_evals, spg_transcript* transcript,
+                    spg_random_tape* tape, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+int spg_spark_free(spg_ctx* ctx, spg_spark* s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -128,3 +128,13 @@ int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars,
                    std::vector<Pt>* out);
 
 }  // namespace spg
+
+// C-ABI handles of the Fiat-Shamir transcript and the prover random tape
+struct spg_transcript {
+  spg::Tr t;
+  explicit spg_transcript(const char* l) : t(l) {}
+};
+struct spg_random_tape {
+  spg::Tape t;
+  spg_random_tape(const char* n, const spg::Fq& s) : t(n, s) {}
+};

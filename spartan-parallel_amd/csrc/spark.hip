@@ -1,0 +1,802 @@
+// spg — SPARK: commitments to and evaluation proofs of batched sparse matrix polynomials on MI355X.
+//
+//   SparseMatPolynomial::multi_commit            src/sparse_mlpoly.rs:368-425, 566-587  spg_spark_commit
+//   SparseMatPolyEvalProof::prove                src/sparse_mlpoly.rs:1497-1564         spg_spark_prove
+//     AddrTimestamps::deref, Derefs::commit      :255-270, :51-67                        k_gather, Hyrax rows
+//     Layers::build_hash_layer, ProductCircuit   :612-736, src/product_tree.rs:36-58    k_hash_*, k_tree_level
+//     ProductLayerProof::prove                   :1118-1263                              batched_prove
+//     ProductCircuitEvalProofBatched::prove      src/product_tree.rs:271-396             k_layer_eval, k_fold_many
+//     SumcheckInstanceProof::prove_cubic_batched src/sumcheck.rs:264-434
+//     HashLayerProof::prove                      :805-918                                k_seg_dot, PolyEvalProofs
+//
+// HBM layout (B = 3 x instances matrices, N = next_pow2(max nnz), cells = 2^max(nvx, nvy)):
+//   addr / read_ts : u32 [2][B][N] (rows, then cols)    audit : u32 [2][cells]
+//   val            : Fq [B][N]
+//   comb_ops (Fq)  : [row addr | row read_ts | col addr | col read_ts | val] (each B x N), zero-padded to 2^k
+//   comb_mem (Fq)  : [row audit | col audit]
+//   product trees  : circuit c at c * 2M; its levels v_0 (the M hashed leaves), v_1, .. v_{L-1} (2 entries)
+//                    back to back at offset 2M - 2(M >> k). Layer k of the circuit is (left, right) = the
+//                    two halves of v_k, and v_{k+1}[i] = v_k[i] * v_k[i + |v_k|/2].
+// All O(N) work stays in HBM; the host runs the transcript and one UniPoly per sumcheck round.
+#include <algorithm>
+
+#include "hostpoly.hpp"
+#include "proto.hpp"
+
+namespace spg {
+
+// ------------------------------------------------------------------------------------ kernels
+__global__ void k_u32_to_fq(const uint32_t* __restrict__ in, Fq* __restrict__ out, size_t n) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = fq_from_u64(in[i]);
+}
+
+// derefs[s][b][i] = mem_s[addr[s][b][i]]  (s = 0: rows with eq(rx), s = 1: cols with eq(ry))
+__global__ void k_gather(const uint32_t* __restrict__ addr, const Fq* __restrict__ mem_rx, const Fq* __restrict__ mem_ry,
+                         size_t BN, Fq* __restrict__ out) {
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * BN) return;
+  out[t] = (t < BN ? mem_rx : mem_ry)[addr[t]];
+}
+
+// hash(addr, val, ts) = ts * r_hash^2 + val * r_hash + addr - r_multiset  (sparse_mlpoly.rs:621-626)
+__device__ __forceinline__ Fq hash3(const Fq& a, const Fq& v, const Fq& ts, const Fq& rh, const Fq& rh2, const Fq& rms) {
+  return fq_sub(fq_add(fq_add(fq_mul(ts, rh2), fq_mul(v, rh)), a), rms);
+}
+// leaves of the 4B ops circuits (row read b, row write b, col read b, col write b), written into the trees
+__global__ void k_hash_ops(const uint32_t* __restrict__ addr, const uint32_t* __restrict__ rts,
+                           const Fq* __restrict__ derefs, size_t B, int logN, Fq rh, Fq rh2, Fq rms,
+                           Fq* __restrict__ tree) {
+  const size_t N = (size_t)1 << logN;
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * B * N) return;
+  size_t sb = t >> logN, i = t & (N - 1);  // sb = side * B + b
+  size_t s = sb >= B, b = sb - s * B;
+  Fq a = fq_from_u64(addr[t]), ts = fq_from_u64(rts[t]), v = derefs[t];
+  tree[((2 * s) * B + b) * 2 * N + i] = hash3(a, v, ts, rh, rh2, rms);
+  tree[((2 * s + 1) * B + b) * 2 * N + i] = hash3(a, v, fq_add(ts, fq_one()), rh, rh2, rms);
+}
+// leaves of the 4 memory circuits (row init, row audit, col init, col audit)
+__global__ void k_hash_mem(const uint32_t* __restrict__ audit, const Fq* __restrict__ mem_rx,
+                           const Fq* __restrict__ mem_ry, int logC, Fq rh, Fq rh2, Fq rms, Fq* __restrict__ tree) {
+  const size_t cells = (size_t)1 << logC;
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * cells) return;
+  size_t s = t >> logC, i = t & (cells - 1);
+  Fq a = fq_from_u64(i), v = (s ? mem_ry : mem_rx)[i];
+  tree[(2 * s) * 2 * cells + i] = hash3(a, v, fq_zero(), rh, rh2, rms);
+  tree[(2 * s + 1) * 2 * cells + i] = hash3(a, v, fq_from_u64(audit[t]), rh, rh2, rms);
+}
+// v_{k+1}[i] = v_k[i] * v_k[i + half] for every circuit (circuit stride 2M)
+__global__ void k_tree_level(Fq* __restrict__ tree, size_t nc, size_t stride, size_t off_k, size_t off_k1, int log_half) {
+  const size_t half = (size_t)1 << log_half;
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= nc * half) return;
+  size_t c = t >> log_half, i = t & (half - 1);
+  Fq* v = tree + c * stride;
+  v[off_k1 + i] = fq_mul(v[off_k + i], v[off_k + i + half]);
+}
+// ProductCircuit::evaluate of every circuit: product of the top level's two entries
+__global__ void k_tops(const Fq* __restrict__ tree, size_t nc, size_t stride, size_t off, Fq* __restrict__ out) {
+  size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (c < nc) out[c] = fq_mul(tree[c * stride + off], tree[c * stride + off + 1]);
+}
+
+struct Triple {
+  Fq *A, *B, *C;
+};
+__device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
+  __shared__ Fq sh[3][256];
+  int t = threadIdx.x;
+  sh[0][t] = v0;
+  sh[1][t] = v1;
+  sh[2][t] = v2;
+  __syncthreads();
+  for (int d = 128; d >= 1; d >>= 1) {
+    if (t < d) {
+      sh[0][t] = fq_add(sh[0][t], sh[0][t + d]);
+      sh[1][t] = fq_add(sh[1][t], sh[1][t + d]);
+      sh[2][t] = fq_add(sh[2][t], sh[2][t + d]);
+    }
+    __syncthreads();
+  }
+  v0 = sh[0][0];
+  v1 = sh[1][0];
+  v2 = sh[2][0];
+  __syncthreads();
+}
+// one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
+// sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367); blocks publish partials
+__global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
+                                                    size_t nt, int log_len, Fq* __restrict__ partials) {
+  const size_t len = (size_t)1 << log_len;
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < nt * len; t += (size_t)gridDim.x * 256) {
+    size_t c = t >> log_len, i = t & (len - 1);
+    const Triple x = tr[c];
+    Fq al = x.A[i], ah = x.A[i + len], bl = x.B[i], bh = x.B[i + len], cl = x.C[i], ch = x.C[i + len];
+    Fq k = coeff[c];
+    Fq v0 = fq_mul(fq_mul(al, bl), cl);
+    Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
+    Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
+    Fq v2 = fq_mul(fq_mul(a2, b2), c2);
+    Fq v3 = fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc));
+    e0 = fq_add(e0, fq_mul(k, v0));
+    e2 = fq_add(e2, fq_mul(k, v2));
+    e3 = fq_add(e3, fq_mul(k, v3));
+  }
+  block_sum3_sp(e0, e2, e3);
+  if (threadIdx.x == 0) {
+    partials[3 * blockIdx.x] = e0;
+    partials[3 * blockIdx.x + 1] = e2;
+    partials[3 * blockIdx.x + 2] = e3;
+  }
+}
+__global__ void __launch_bounds__(256) k_sum3(const Fq* __restrict__ partials, int nb, Fq* __restrict__ out) {
+  Fq a = fq_zero(), b = fq_zero(), c = fq_zero();
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    a = fq_add(a, partials[3 * i]);
+    b = fq_add(b, partials[3 * i + 1]);
+    c = fq_add(c, partials[3 * i + 2]);
+  }
+  block_sum3_sp(a, b, c);
+  if (threadIdx.x == 0) {
+    out[0] = a;
+    out[1] = b;
+    out[2] = c;
+  }
+}
+// DensePolynomial::bound_poly_var_top on nv distinct vectors of length 2 * len (in place)
+__global__ void k_fold_many(Fq* const* __restrict__ v, size_t nv, int log_len, Fq r) {
+  const size_t len = (size_t)1 << log_len;
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= nv * len) return;
+  Fq* p = v[t >> log_len];
+  size_t i = t & (len - 1);
+  Fq lo = p[i];
+  p[i] = fq_add(lo, fq_mul(r, fq_sub(p[i + len], lo)));
+}
+// A[0], B[0], C[0] of every triple (the final claims of a layer)
+__global__ void k_finals(const Triple* __restrict__ tr, size_t nt, Fq* __restrict__ out) {
+  size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= nt) return;
+  out[3 * c] = tr[c].A[0];
+  out[3 * c + 1] = tr[c].B[0];
+  out[3 * c + 2] = tr[c].C[0];
+}
+// DotProductCircuit::evaluate per triple: sum_i A*B*C over n entries (blockIdx.y = triple)
+__global__ void __launch_bounds__(256) k_dot3(const Triple* __restrict__ tr, size_t n, Fq* __restrict__ partials) {
+  const Triple x = tr[blockIdx.y];
+  Fq acc = fq_zero(), z = fq_zero(), z2 = fq_zero();
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    acc = fq_add(acc, fq_mul(fq_mul(x.A[i], x.B[i]), x.C[i]));
+  block_sum3_sp(acc, z, z2);
+  if (threadIdx.x == 0) partials[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = acc;
+}
+// sum_i base[s * seglen + i] * eq[i] for segments s = blockIdx.y (DensePolynomial::evaluate on HBM)
+__global__ void __launch_bounds__(256) k_seg_dot(const Fq* __restrict__ base, size_t seglen, const Fq* __restrict__ eq,
+                                                 size_t n, Fq* __restrict__ partials) {
+  const size_t s = blockIdx.y;
+  Fq acc = fq_zero(), z = fq_zero(), z2 = fq_zero();
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    acc = fq_add(acc, fq_mul(base[s * seglen + i], eq[i]));
+  block_sum3_sp(acc, z, z2);
+  if (threadIdx.x == 0) partials[s * gridDim.x + blockIdx.x] = acc;
+}
+__global__ void __launch_bounds__(256) k_sum_seg(const Fq* __restrict__ partials, int nb, Fq* __restrict__ out) {
+  Fq a = fq_zero(), z = fq_zero(), z2 = fq_zero();
+  for (int i = threadIdx.x; i < nb; i += 256) a = fq_add(a, partials[(size_t)blockIdx.x * nb + i]);
+  block_sum3_sp(a, z, z2);
+  if (threadIdx.x == 0) out[blockIdx.x] = a;
+}
+// DensePolynomial::bound (dense_mlpoly.rs:258-265): out[i] = sum_j L[j] * Z[j * Rs + i], rows split over y
+__global__ void __launch_bounds__(256) k_bound_rows(const Fq* __restrict__ Z, const Fq* __restrict__ L, size_t Ls,
+                                                    size_t Rs, size_t chunk, Fq* __restrict__ part) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= Rs) return;
+  size_t j0 = blockIdx.y * chunk, j1 = j0 + chunk < Ls ? j0 + chunk : Ls;
+  Fq acc = fq_zero();
+  for (size_t j = j0; j < j1; j++) acc = fq_add(acc, fq_mul(L[j], Z[j * Rs + i]));
+  part[(size_t)blockIdx.y * Rs + i] = acc;
+}
+__global__ void k_bound_sum(const Fq* __restrict__ part, size_t S, size_t Rs, Fq* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= Rs) return;
+  Fq acc = fq_zero();
+  for (size_t y = 0; y < S; y++) acc = fq_add(acc, part[y * Rs + i]);
+  out[i] = acc;
+}
+
+}  // namespace spg
+
+using namespace spg;
+
+// ------------------------------------------------------------------------------------ handle
+struct spg_spark {
+  size_t B = 0, N = 0, cells = 0;
+  uint32_t* d_addr = nullptr;   // [2][B][N]
+  uint32_t* d_rts = nullptr;    // [2][B][N]
+  uint32_t* d_audit = nullptr;  // [2][cells]
+  Fq* d_val = nullptr;          // [B][N]
+  Fq* d_comb_ops = nullptr;
+  Fq* d_comb_mem = nullptr;
+  size_t comb_ops_len = 0, comb_mem_len = 0;
+  spg_gens* dev = nullptr;
+  ProverGens g_ops, g_mem, g_der;
+};
+
+namespace spg {
+
+static unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
+// workspace slots of this file
+enum : size_t {
+  kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
+  kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
+  kWsTops
+};
+
+// PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
+static ProverGens gens_view(spg_gens* dev, size_t nv) {
+  ProverGens g;
+  g.dev = dev;
+  g.host.init(dev->compressed, dev->n + 1);
+  size_t n = (size_t)1 << (nv - nv / 2);
+  g.n_pc = n;
+  g.gens_n.G.resize(n);
+  for (size_t i = 0; i < n; i++) g.gens_n.G[i] = i;
+  g.gens_n.h = n + 1;
+  g.gens_1.G = {n};
+  g.gens_1.h = n + 1;
+  return g;
+}
+
+// DensePolynomial::commit without blinds (dense_mlpoly.rs:181-216) of 2^nv device scalars: one MSM per
+// row of R = 2^(nv - nv/2) scalars, in chunks of rows that keep the MSM sort within 32-bit indices
+static int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out) {
+  size_t L = (size_t)1 << (nv / 2), R = (size_t)1 << (nv - nv / 2);
+  if (R != g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: polynomial size does not match its generators");
+  out->resize(L);
+  size_t chunk = std::max<size_t>(1, std::min<size_t>(L, ((size_t)1 << 24) / R));
+  uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsCommit, 32 * chunk + 64);
+  if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit out");
+  for (size_t r0 = 0; r0 < L; r0 += chunk) {
+    size_t nb = std::min(chunk, L - r0);
+    int rc = msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr, (long)(g.n_pc + 1));
+    if (rc) return rc;
+    SPG_HIP(ctx, hipMemcpyAsync(out->data() + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
+    SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
+  }
+  return 0;
+}
+
+static void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c) {
+  t.msg(label, "poly_commitment_begin");
+  for (auto& p : c) t.point("poly_commitment_share", p);
+  t.msg(label, "poly_commitment_end");
+}
+
+// PolyEvalProof::prove without blinds (dense_mlpoly.rs:437-490) of a device polynomial of 2^|r| scalars
+static int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, const Fq& Zr, Tr& t, Tape& tape,
+                           DotProductProofLogP* out) {
+  t.protocol("polynomial evaluation proof");
+  size_t nv = r.size(), ln = nv / 2;
+  FqV rl(r.begin(), r.begin() + ln), rr(r.begin() + ln, r.end());
+  size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
+  if (Rs != g.n_pc) return set_err(ctx, SPG_E_ARG, "poly eval: size does not match the generators");
+  FqV R = eq_evals_host(rr);
+  size_t S = std::min<size_t>(Ls, std::max<size_t>(1, 8192 / nblk(Rs)));  // row splits to fill the chip
+  size_t chunk = (Ls + S - 1) / S;
+  S = (Ls + chunk - 1) / chunk;
+  Fq* dL = (Fq*)ws_get(ctx, kWsL, Ls * sizeof(Fq) + 64);
+  Fq* dpart = (Fq*)ws_get(ctx, kWsBoundPart, S * Rs * sizeof(Fq) + 64);
+  Fq* dout = (Fq*)ws_get(ctx, kWsBound, Rs * sizeof(Fq) + 64);
+  if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "poly_eval_prove");
+  int rc = eq_table(ctx, rl, dL);
+  if (rc) return rc;
+  {
+    KScope ks(ctx, "spark_bound", 32.0 * (double)Ls * Rs + 64.0 * S * Rs);
+    hipLaunchKernelGGL(k_bound_rows, dim3(nblk(Rs), (unsigned)S), dim3(256), 0, ctx->stream, d_Z, dL, Ls, Rs, chunk,
+                       dpart);
+    hipLaunchKernelGGL(k_bound_sum, dim3(nblk(Rs)), dim3(256), 0, ctx->stream, dpart, S, Rs, dout);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  FqV LZ(Rs);
+  rc = d2h_fq(ctx, dout, LZ.data(), Rs);
+  if (rc) return rc;
+  Pt cy;
+  return dotproduct_log_prove(ctx, g, t, tape, LZ, fq_zero(), R, Zr, fq_zero(), out, &cy);
+}
+
+// out[s] = sum_i base[s * seglen + i] * eq[i], i < n, s < nseg
+static int seg_dots(spg_ctx* ctx, const Fq* base, size_t seglen, size_t nseg, const Fq* d_eq, size_t n, FqV* out) {
+  unsigned nb = (unsigned)std::min<size_t>(nblk(n), std::max<size_t>(1, 2048 / nseg));
+  Fq* part = (Fq*)ws_get(ctx, kWsSegPart, nseg * nb * sizeof(Fq) + 64);
+  Fq* dres = (Fq*)ws_get(ctx, kWsSeg, nseg * sizeof(Fq) + 64);
+  if (!part || !dres) return set_err(ctx, SPG_E_NOMEM, "seg_dots");
+  {
+    KScope ks(ctx, "spark_evaluate", 32.0 * n * nseg + 32.0 * n);
+    hipLaunchKernelGGL(k_seg_dot, dim3(nb, (unsigned)nseg), dim3(256), 0, ctx->stream, base, seglen, d_eq, n, part);
+    hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)nseg), dim3(256), 0, ctx->stream, part, (int)nb, dres);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  out->resize(nseg);
+  return d2h_fq(ctx, dres, out->data(), nseg);
+}
+
+// UniPoly::append_to_transcript (unipoly.rs:112-120)
+static void append_unipoly(Tr& t, const FqV& c) {
+  t.msg("poly", "UniPoly_begin");
+  for (auto& x : c) t.scalar("coeff", x);
+  t.msg("poly", "UniPoly_end");
+}
+
+struct LayerProofP {
+  std::vector<FqV> polys;  // CompressedUniPoly per round
+  FqV left, right;
+};
+struct BatchedProofP {  // ProductCircuitEvalProofBatched
+  std::vector<LayerProofP> layers;
+  FqV dotp[3];
+  void ser(Writer& w) const {
+    w.u64(layers.size());
+    for (auto& l : layers) {
+      w.u64(l.polys.size());
+      for (auto& p : l.polys) w.fqs(p);
+      w.fqs(l.left);
+      w.fqs(l.right);
+    }
+    for (int i = 0; i < 3; i++) w.fqs(dotp[i]);
+  }
+};
+
+// ProductCircuitEvalProofBatched::prove (product_tree.rs:271-396) over the nc product circuits of `tree`
+// (M leaves each, claims = their ProductCircuit::evaluate) and, at layer 0, the dot-product circuits
+// `dotp` (three device vectors of M/2 entries each, folded in place) with claims `dotp_claims`.
+static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims, const std::vector<Triple>& dotp,
+                         const FqV& dotp_claims, Tr& t, BatchedProofP* out, FqV* rand_out) {
+  hipStream_t s = ctx->stream;
+  const size_t L = lg2(M), stride = 2 * M;
+  auto off = [&](size_t k) { return 2 * M - 2 * (M >> k); };
+  const size_t nt_max = nc + dotp.size();
+  Fq* dC = (Fq*)ws_get(ctx, kWsC, (M / 2) * sizeof(Fq) + 64);
+  Triple* dtr = (Triple*)ws_get(ctx, kWsTriples, nt_max * sizeof(Triple) + 64);
+  Fq* dcoef = (Fq*)ws_get(ctx, kWsCoeff, nt_max * sizeof(Fq) + 64);
+  Fq** dptr = (Fq**)ws_get(ctx, kWsFoldPtr, (2 * nc + 1 + 3 * dotp.size()) * sizeof(Fq*) + 64);
+  Fq* part = (Fq*)ws_get(ctx, kWsPart, 3 * 1024 * sizeof(Fq) + 64);
+  Fq* d3 = (Fq*)ws_get(ctx, kWs3, 3 * sizeof(Fq) + 64);
+  Fq* dfin = (Fq*)ws_get(ctx, kWsFinals, 3 * nt_max * sizeof(Fq) + 64);
+  if (!dC || !dtr || !dcoef || !dptr || !part || !d3 || !dfin) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
+  FqV rand;
+  for (size_t layer = L; layer-- > 0;) {
+    const size_t half = M >> (layer + 1);  // |left| = |right| = |C|
+    const size_t rounds = lg2(half);
+    int rc = eq_table(ctx, rand, dC);
+    if (rc) return rc;
+    const bool with_dotp = layer == 0 && !dotp.empty();
+    std::vector<Triple> tr;
+    std::vector<Fq*> fold;
+    for (size_t c = 0; c < nc; c++) {
+      Fq* v = tree + c * stride + off(layer);
+      tr.push_back({v, v + half, dC});
+      fold.push_back(v);
+      fold.push_back(v + half);
+    }
+    fold.push_back(dC);
+    if (with_dotp) {
+      claims.insert(claims.end(), dotp_claims.begin(), dotp_claims.end());
+      for (auto& d : dotp) {
+        tr.push_back(d);
+        fold.push_back(d.A);
+        fold.push_back(d.B);
+        fold.push_back(d.C);
+      }
+    }
+    FqV coeffs = t.challenges("rand_coeffs_next_layer", claims.size());
+    Fq e = fq_zero();
+    for (size_t i = 0; i < claims.size(); i++) e = fq_add(e, fq_mul(claims[i], coeffs[i]));
+    SPG_HIP(ctx, hipMemcpyAsync(dtr, tr.data(), tr.size() * sizeof(Triple), hipMemcpyHostToDevice, s));
+    SPG_HIP(ctx, hipMemcpyAsync(dcoef, coeffs.data(), coeffs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
+    SPG_HIP(ctx, hipMemcpyAsync(dptr, fold.data(), fold.size() * sizeof(Fq*), hipMemcpyHostToDevice, s));
+    LayerProofP lp;
+    FqV r_prod;
+    size_t log_len = rounds;
+    for (size_t j = 0; j < rounds; j++) {
+      log_len--;
+      const size_t len = (size_t)1 << log_len;
+      unsigned nb = (unsigned)std::min<size_t>(nblk(tr.size() * len), 1024);
+      {
+        KScope ks(ctx, "spark_layer_eval", 192.0 * tr.size() * len);
+        hipLaunchKernelGGL(k_layer_eval, dim3(nb), dim3(256), 0, s, dtr, dcoef, tr.size(), (int)log_len, part);
+        hipLaunchKernelGGL(k_sum3, dim3(1), dim3(256), 0, s, part, (int)nb, d3);
+      }
+      Fq ev[3];
+      rc = d2h_fq(ctx, d3, ev, 3);
+      if (rc) return rc;
+      Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
+      FqV poly = uni_from_evals3(evals);
+      append_unipoly(t, poly);
+      Fq r_j = t.challenge("challenge_nextround");
+      r_prod.push_back(r_j);
+      {
+        KScope ks(ctx, "spark_fold", 96.0 * fold.size() * len);
+        hipLaunchKernelGGL(k_fold_many, dim3(nblk(fold.size() * len)), dim3(256), 0, s, dptr, fold.size(),
+                           (int)log_len, r_j);
+      }
+      SPG_HIP(ctx, hipGetLastError());
+      e = uni_eval(poly, r_j);
+      lp.polys.push_back({poly[0], poly[2], poly[3]});
+    }
+    // final claims: A[0], B[0] (and C[0] for the dot-product circuits)
+    hipLaunchKernelGGL(k_finals, dim3(nblk(tr.size())), dim3(256), 0, s, dtr, tr.size(), dfin);
+    FqV fin(3 * tr.size());
+    rc = d2h_fq(ctx, dfin, fin.data(), fin.size());
+    if (rc) return rc;
+    for (size_t c = 0; c < nc; c++) {
+      lp.left.push_back(fin[3 * c]);
+      lp.right.push_back(fin[3 * c + 1]);
+    }
+    for (size_t c = 0; c < nc; c++) {
+      t.scalar("claim_prod_left", lp.left[c]);
+      t.scalar("claim_prod_right", lp.right[c]);
+    }
+    if (with_dotp) {
+      for (size_t k = 0; k < dotp.size(); k++)
+        for (int i = 0; i < 3; i++) out->dotp[i].push_back(fin[3 * (nc + k) + i]);
+      for (size_t k = 0; k < dotp.size(); k++) {
+        t.scalar("claim_dotp_left", out->dotp[0][k]);
+        t.scalar("claim_dotp_right", out->dotp[1][k]);
+        t.scalar("claim_dotp_weight", out->dotp[2][k]);
+      }
+    }
+    Fq r_layer = t.challenge("challenge_r_layer");
+    claims.assign(nc, fq_zero());
+    for (size_t c = 0; c < nc; c++) claims[c] = fq_add(lp.left[c], fq_mul(r_layer, fq_sub(lp.right[c], lp.left[c])));
+    rand.assign(1, r_layer);
+    rand.insert(rand.end(), r_prod.begin(), r_prod.end());
+    out->layers.push_back(std::move(lp));
+  }
+  *rand_out = rand;
+  return 0;
+}
+
+// n-to-1 reduction of claimed evaluations (sparse_mlpoly.rs:92-112, 868-883)
+static void combine_evals(const FqV& evals, const FqV& r, const char* label, Tr& t, FqV* r_joint, Fq* eval) {
+  FqV ch = t.challenges(label, lg2(evals.size()));
+  FqV v = evals;
+  for (size_t i = ch.size(); i-- > 0;) {  // bound_poly_var_bot with challenge i
+    size_t n = v.size() / 2;
+    for (size_t k = 0; k < n; k++) v[k] = fq_add(v[2 * k], fq_mul(ch[i], fq_sub(v[2 * k + 1], v[2 * k])));
+    v.resize(n);
+  }
+  *eval = v[0];
+  *r_joint = ch;
+  r_joint->insert(r_joint->end(), r.begin(), r.end());
+}
+
+}  // namespace spg
+
+// ------------------------------------------------------------------------------------ C-ABI
+extern "C" int spg_spark_free(spg_ctx* ctx, spg_spark* S) {
+  if (!S) return SPG_OK;
+  hipFree(S->d_addr);
+  hipFree(S->d_rts);
+  hipFree(S->d_audit);
+  hipFree(S->d_val);
+  hipFree(S->d_comb_ops);
+  hipFree(S->d_comb_mem);
+  spg_gens_free(ctx, S->dev);
+  delete S;
+  return SPG_OK;
+}
+
+extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const uint8_t* label, size_t label_len,
+                                size_t gens_nnz, size_t gens_batch, spg_spark** out, uint8_t* comm, size_t comm_cap,
+                                size_t* comm_len) {
+  if (!ctx || !ci || !label || !out || !comm_len || !ci->num_instances || !ci->nnz || !ci->entries) return SPG_E_ARG;
+  if (!is_pow2(ci->max_num_cons) || !is_pow2(ci->num_vars)) return set_err(ctx, SPG_E_ARG, "sizes must be powers of 2");
+  hipStream_t s = ctx->stream;
+  const size_t B = 3 * ci->num_instances;
+  size_t N = 2;
+  for (size_t k = 0; k < B; k++) N = std::max(N, npow2(ci->nnz[k]));
+  const size_t nvx = lg2(ci->max_num_cons), nvy = lg2(ci->num_vars);
+  const size_t cells = (size_t)1 << std::max<size_t>(std::max(nvx, nvy), 1);
+  if (2 * B * N >= 0xffffffffULL || cells > 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "SPARK batch too large");
+  // SparseMatPolyCommitmentGens::new (sparse_mlpoly.rs:289-317)
+  const size_t nv_ops = lg2(npow2(gens_nnz)) + lg2(npow2(gens_batch * 5));
+  const size_t nv_mem = std::max(nvx, nvy) + 1;
+  const size_t nv_der = lg2(npow2(gens_nnz)) + lg2(npow2(gens_batch * 2));
+  const size_t ops_len = npow2(5 * B * N);
+  if (lg2(ops_len) != nv_ops || lg2(npow2(2 * B * N)) != nv_der)
+    return set_err(ctx, SPG_E_ARG, "SPARK generators (gens_nnz, gens_batch) do not match the batch");
+  // AddrTimestamps::new (sparse_mlpoly.rs:219-253): read / audit timestamps are a sequential scan (host)
+  std::vector<uint32_t> addr(2 * B * N, 0), rts(2 * B * N, 0), audit(2 * cells, 0);
+  std::vector<Fq> val(B * N, fq_zero());
+  for (size_t k = 0; k < B; k++) {
+    const spg_sparse_entry* E = ci->entries[k];
+    if (ci->nnz[k] && !E) return SPG_E_ARG;
+    for (size_t i = 0; i < ci->nnz[k]; i++) {
+      if (E[i].row >= ((uint64_t)1 << nvx) || E[i].col >= ((uint64_t)1 << nvy))
+        return set_err(ctx, SPG_E_ARG, "sparse entry outside the matrix");
+      addr[k * N + i] = (uint32_t)E[i].row;
+      addr[B * N + k * N + i] = (uint32_t)E[i].col;
+      memcpy(val[k * N + i].l, E[i].val, 32);
+    }
+  }
+  for (size_t side = 0; side < 2; side++) {
+    uint32_t* au = audit.data() + side * cells;
+    for (size_t t = side * B * N; t < (side + 1) * B * N; t++) {
+      rts[t] = au[addr[t]];
+      au[addr[t]] = rts[t] + 1;
+    }
+  }
+  spg_spark* S = new spg_spark();
+  S->B = B;
+  S->N = N;
+  S->cells = cells;
+  S->comb_ops_len = ops_len;
+  S->comb_mem_len = 2 * cells;
+  auto up = [&](void** d, const void* h, size_t bytes) -> bool {
+    return hipMalloc(d, bytes + 64) == hipSuccess && hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up((void**)&S->d_addr, addr.data(), addr.size() * 4) || !up((void**)&S->d_rts, rts.data(), rts.size() * 4) ||
+      !up((void**)&S->d_audit, audit.data(), audit.size() * 4) ||
+      !up((void**)&S->d_val, val.data(), val.size() * sizeof(Fq)) ||
+      hipMalloc(&S->d_comb_ops, S->comb_ops_len * sizeof(Fq)) != hipSuccess ||
+      hipMalloc(&S->d_comb_mem, S->comb_mem_len * sizeof(Fq)) != hipSuccess) {
+    spg_spark_free(ctx, S);
+    return set_err(ctx, SPG_E_NOMEM, "spark upload");
+  }
+  // comb_ops = merge(row addr, row read_ts, col addr, col read_ts, val); comb_mem = row audit ++ col audit
+  const size_t BN = B * N;
+  int rc = 0;
+  if (hipMemsetAsync(S->d_comb_ops, 0, S->comb_ops_len * sizeof(Fq), s) != hipSuccess) rc = SPG_E_HIP;
+  hipLaunchKernelGGL(k_u32_to_fq, dim3(nblk(BN)), dim3(256), 0, s, S->d_addr, S->d_comb_ops, BN);
+  hipLaunchKernelGGL(k_u32_to_fq, dim3(nblk(BN)), dim3(256), 0, s, S->d_rts, S->d_comb_ops + BN, BN);
+  hipLaunchKernelGGL(k_u32_to_fq, dim3(nblk(BN)), dim3(256), 0, s, S->d_addr + BN, S->d_comb_ops + 2 * BN, BN);
+  hipLaunchKernelGGL(k_u32_to_fq, dim3(nblk(BN)), dim3(256), 0, s, S->d_rts + BN, S->d_comb_ops + 3 * BN, BN);
+  if (hipMemcpyAsync(S->d_comb_ops + 4 * BN, S->d_val, BN * sizeof(Fq), hipMemcpyDeviceToDevice, s) != hipSuccess)
+    rc = SPG_E_HIP;
+  hipLaunchKernelGGL(k_u32_to_fq, dim3(nblk(2 * cells)), dim3(256), 0, s, S->d_audit, S->d_comb_mem, 2 * cells);
+  if (rc || hipGetLastError() != hipSuccess) {
+    spg_spark_free(ctx, S);
+    return set_err(ctx, SPG_E_HIP, "spark dense representation");
+  }
+  // the three PolyCommitmentGens share one label: prefixes of one derived stream
+  size_t nmax = 0;
+  for (size_t nv : {nv_ops, nv_mem, nv_der}) nmax = std::max(nmax, (size_t)1 << (nv - nv / 2));
+  rc = spg_gens_derive(ctx, label, label_len, nmax + 1, &S->dev);
+  if (rc) {
+    spg_spark_free(ctx, S);
+    return rc;
+  }
+  S->g_ops = gens_view(S->dev, nv_ops);
+  S->g_mem = gens_view(S->dev, nv_mem);
+  S->g_der = gens_view(S->dev, nv_der);
+  std::vector<Pt> comm_ops, comm_mem;
+  rc = commit_dev(ctx, S->g_ops, S->d_comb_ops, nv_ops, &comm_ops);
+  if (!rc) rc = commit_dev(ctx, S->g_mem, S->d_comb_mem, nv_mem, &comm_mem);
+  if (rc) {
+    spg_spark_free(ctx, S);
+    return rc;
+  }
+  Writer w;  // SparseMatPolyCommitment (sparse_mlpoly.rs:319-325)
+  w.u64(B);
+  w.u64(N);
+  w.u64(cells);
+  w.pts(comm_ops);
+  w.pts(comm_mem);
+  *comm_len = w.out.size();
+  *out = S;
+  if (!comm || w.out.size() > comm_cap) return set_err(ctx, SPG_E_ARG, "commitment buffer too small");
+  memcpy(comm, w.out.data(), w.out.size());
+  return SPG_OK;
+}
+
+extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                               size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
+                               spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  if (!ctx || !S || !transcript || !tape_h || !proof_len || (!rx && rx_len) || (!ry && ry_len) || !evals_in)
+    return SPG_E_ARG;
+  if (n_evals != S->B) return set_err(ctx, SPG_E_ARG, "one evaluation per batched matrix");
+  hipStream_t s = ctx->stream;
+  Tr& t = transcript->t;
+  Tape& tape = tape_h->t;
+  const size_t B = S->B, N = S->N, BN = B * N, cells = S->cells, hN = N / 2;
+  FqV ex, ey, evals(n_evals);
+  for (size_t i = 0; i < rx_len; i++) ex.push_back(ld_fq(rx + 4 * i));
+  for (size_t i = 0; i < ry_len; i++) ey.push_back(ld_fq(ry + 4 * i));
+  for (size_t i = 0; i < n_evals; i++) evals[i] = ld_fq(evals_in + 4 * i);
+  if (ex.size() < ey.size()) ex.insert(ex.begin(), ey.size() - ex.size(), fq_zero());
+  if (ey.size() < ex.size()) ey.insert(ey.begin(), ex.size() - ey.size(), fq_zero());
+  if (ex.size() > 40 || ((size_t)1 << ex.size()) != cells)
+    return set_err(ctx, SPG_E_ARG, "rx / ry do not match the memory size");
+  t.protocol("Sparse polynomial evaluation proof");
+  timer_start(ctx);
+  const size_t der_len = npow2(2 * BN);
+  Fq* mem_rx = (Fq*)ws_get(ctx, kWsMemRx, cells * sizeof(Fq) + 64);
+  Fq* mem_ry = (Fq*)ws_get(ctx, kWsMemRy, cells * sizeof(Fq) + 64);
+  Fq* derefs = (Fq*)ws_get(ctx, kWsDerefs, der_len * sizeof(Fq) + 64);
+  Fq* tree_ops = (Fq*)ws_get(ctx, kWsTreeOps, 4 * B * 2 * N * sizeof(Fq) + 64);
+  Fq* tree_mem = (Fq*)ws_get(ctx, kWsTreeMem, 4 * 2 * cells * sizeof(Fq) + 64);
+  Fq* dotbuf = (Fq*)ws_get(ctx, kWsDotp, 2 * B * 3 * hN * sizeof(Fq) + 64);
+  Fq* dtops = (Fq*)ws_get(ctx, kWsTops, 4 * (B + 1) * sizeof(Fq) + 64);
+  Fq* eq_ops = (Fq*)ws_get(ctx, kWsEqOps, N * sizeof(Fq) + 64);
+  Fq* eq_mem = (Fq*)ws_get(ctx, kWsEqMem, cells * sizeof(Fq) + 64);
+  if (!mem_rx || !mem_ry || !derefs || !tree_ops || !tree_mem || !dotbuf || !dtops || !eq_ops || !eq_mem)
+    return set_err(ctx, SPG_E_NOMEM, "spark workspace");
+  int rc = eq_table(ctx, ex, mem_rx);
+  if (!rc) rc = eq_table(ctx, ey, mem_ry);
+  if (rc) return rc;
+  // Derefs (sparse_mlpoly.rs:51-67): comb = row derefs ++ col derefs, zero-padded
+  if (der_len > 2 * BN) SPG_HIP(ctx, hipMemsetAsync(derefs + 2 * BN, 0, (der_len - 2 * BN) * sizeof(Fq), s));
+  {
+    KScope ks(ctx, "spark_deref", (4.0 + 32.0 + 32.0) * 2 * BN);
+    hipLaunchKernelGGL(k_gather, dim3(nblk(2 * BN)), dim3(256), 0, s, S->d_addr, mem_rx, mem_ry, BN, derefs);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  std::vector<Pt> comm_derefs;
+  rc = commit_dev(ctx, S->g_der, derefs, lg2(der_len), &comm_derefs);
+  if (rc) return rc;
+  t.msg("derefs_commitment", "begin_derefs_commitment");
+  append_polycomm(t, "comm_poly_row_col_ops_val", comm_derefs);
+  t.msg("derefs_commitment", "end_derefs_commitment");
+  FqV rmc = t.challenges("challenge_r_hash", 2);
+  const Fq rh = rmc[0], rh2 = fq_mul(rmc[0], rmc[0]), rms = rmc[1];
+  // hash layer leaves straight into the trees, then the product trees (Layers::new)
+  {
+    KScope ks(ctx, "spark_hash_layer", (8.0 + 32.0 + 64.0) * 2 * BN + (4.0 + 32.0 + 64.0) * 2 * cells);
+    hipLaunchKernelGGL(k_hash_ops, dim3(nblk(2 * BN)), dim3(256), 0, s, S->d_addr, S->d_rts, derefs, B, (int)lg2(N),
+                       rh, rh2, rms, tree_ops);
+    hipLaunchKernelGGL(k_hash_mem, dim3(nblk(2 * cells)), dim3(256), 0, s, S->d_audit, mem_rx, mem_ry,
+                       (int)lg2(cells), rh, rh2, rms, tree_mem);
+  }
+  for (int which = 0; which < 2; which++) {  // ProductCircuit::new (product_tree.rs:36-58)
+    Fq* tree = which ? tree_mem : tree_ops;
+    const size_t M = which ? cells : N, nc = which ? 4 : 4 * B;
+    KScope ks(ctx, "spark_product_tree", 96.0 * nc * M / 2);
+    for (size_t k = 0; k + 1 < lg2(M); k++) {
+      size_t ok = 2 * M - 2 * (M >> k), ok1 = 2 * M - 2 * (M >> (k + 1));
+      hipLaunchKernelGGL(k_tree_level, dim3(nblk(nc * (M >> (k + 1)))), dim3(256), 0, s, tree, nc, 2 * M, ok, ok1,
+                         (int)lg2(M >> (k + 1)));
+    }
+    const size_t top = 2 * M - 4;  // v_{L-1}
+    hipLaunchKernelGGL(k_tops, dim3(nblk(nc)), dim3(256), 0, s, tree, nc, 2 * M, top, dtops + (which ? 4 * B : 0));
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  FqV tops(4 * B + 4);
+  rc = d2h_fq(ctx, dtops, tops.data(), tops.size());
+  if (rc) return rc;
+  // ---- PolyEvalNetworkProof -> ProductLayerProof (sparse_mlpoly.rs:1368-1402, 1118-1263)
+  t.protocol("Sparse polynomial evaluation proof");
+  t.protocol("Sparse polynomial product layer proof");
+  const Fq row_init = tops[4 * B], row_audit = tops[4 * B + 1], col_init = tops[4 * B + 2], col_audit = tops[4 * B + 3];
+  FqV row_read(tops.begin(), tops.begin() + B), row_write(tops.begin() + B, tops.begin() + 2 * B),
+      col_read(tops.begin() + 2 * B, tops.begin() + 3 * B), col_write(tops.begin() + 3 * B, tops.begin() + 4 * B);
+  t.scalar("claim_row_eval_init", row_init);
+  t.scalars("claim_row_eval_read", row_read);
+  t.scalars("claim_row_eval_write", row_write);
+  t.scalar("claim_row_eval_audit", row_audit);
+  t.scalar("claim_col_eval_init", col_init);
+  t.scalars("claim_col_eval_read", col_read);
+  t.scalars("claim_col_eval_write", col_write);
+  t.scalar("claim_col_eval_audit", col_audit);
+  // dot-product circuits (row derefs, col derefs, val) split into halves, interleaved (left_b, right_b);
+  // copies, since the layer-0 sumcheck folds them while the hash layer evaluates the originals
+  std::vector<Triple> dotp;
+  for (size_t b = 0; b < B; b++)
+    for (size_t h = 0; h < 2; h++) {
+      Fq* base = dotbuf + (2 * b + h) * 3 * hN;
+      SPG_HIP(ctx, hipMemcpyAsync(base, derefs + b * N + h * hN, hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
+      SPG_HIP(ctx, hipMemcpyAsync(base + hN, derefs + BN + b * N + h * hN, hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
+      SPG_HIP(ctx, hipMemcpyAsync(base + 2 * hN, S->d_val + b * N + h * hN, hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
+      dotp.push_back({base, base + hN, base + 2 * hN});
+    }
+  FqV dotp_claims(2 * B);
+  {
+    Triple* dtr = (Triple*)ws_get(ctx, kWsTriples, 6 * B * sizeof(Triple) + 64);
+    unsigned nb = (unsigned)std::min<size_t>(nblk(hN), std::max<size_t>(1, 2048 / (2 * B)));
+    Fq* part = (Fq*)ws_get(ctx, kWsSegPart, 2 * B * nb * sizeof(Fq) + 64);
+    Fq* dres = (Fq*)ws_get(ctx, kWsSeg, 2 * B * sizeof(Fq) + 64);
+    if (!dtr || !part || !dres) return set_err(ctx, SPG_E_NOMEM, "dotp eval");
+    SPG_HIP(ctx, hipMemcpyAsync(dtr, dotp.data(), dotp.size() * sizeof(Triple), hipMemcpyHostToDevice, s));
+    KScope ks(ctx, "spark_dotp_eval", 96.0 * 2 * B * hN);
+    hipLaunchKernelGGL(k_dot3, dim3(nb, (unsigned)(2 * B)), dim3(256), 0, s, dtr, hN, part);
+    hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)(2 * B)), dim3(256), 0, s, part, (int)nb, dres);
+    SPG_HIP(ctx, hipGetLastError());
+    rc = d2h_fq(ctx, dres, dotp_claims.data(), 2 * B);
+    if (rc) return rc;
+  }
+  FqV dl(B), dr(B);
+  for (size_t b = 0; b < B; b++) {
+    dl[b] = dotp_claims[2 * b];
+    dr[b] = dotp_claims[2 * b + 1];
+    t.scalar("claim_eval_dotp_left", dl[b]);
+    t.scalar("claim_eval_dotp_right", dr[b]);
+  }
+  BatchedProofP proof_ops, proof_mem;
+  FqV rand_ops, rand_mem;
+  rc = batched_prove(ctx, tree_ops, 4 * B, N, FqV(tops.begin(), tops.begin() + 4 * B), dotp, dotp_claims, t,
+                     &proof_ops, &rand_ops);
+  if (!rc)
+    rc = batched_prove(ctx, tree_mem, 4, cells, FqV(tops.begin() + 4 * B, tops.end()), {}, {}, t, &proof_mem, &rand_mem);
+  if (rc) return rc;
+  // ---- HashLayerProof (sparse_mlpoly.rs:805-918)
+  t.protocol("Sparse polynomial hash layer proof");
+  rc = eq_table(ctx, rand_ops, eq_ops);
+  if (!rc) rc = eq_table(ctx, rand_mem, eq_mem);
+  if (rc) return rc;
+  FqV ev_der, ev_ops, ev_mem;
+  rc = seg_dots(ctx, derefs, N, 2 * B, eq_ops, N, &ev_der);
+  if (!rc) rc = seg_dots(ctx, S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops);
+  if (!rc) rc = seg_dots(ctx, S->d_comb_mem, cells, 2, eq_mem, cells, &ev_mem);
+  if (rc) return rc;
+  DotProductProofLogP pf_der, pf_ops, pf_mem;
+  {  // DerefsEvalProof::prove (sparse_mlpoly.rs:80-146)
+    t.protocol("Derefs evaluation proof");
+    FqV ev = ev_der;
+    ev.resize(npow2(ev.size()), fq_zero());
+    t.scalars("evals_ops_val", ev);
+    FqV rj;
+    Fq ej;
+    combine_evals(ev, rand_ops, "challenge_combine_n_to_one", t, &rj, &ej);
+    t.scalar("joint_claim_eval", ej);
+    rc = poly_eval_prove(ctx, S->g_der, derefs, rj, ej, t, tape, &pf_der);
+    if (rc) return rc;
+  }
+  {
+    FqV ev = ev_ops;
+    ev.resize(npow2(ev.size()), fq_zero());
+    t.scalars("claim_evals_ops", ev);
+    FqV rj;
+    Fq ej;
+    combine_evals(ev, rand_ops, "challenge_combine_n_to_one", t, &rj, &ej);
+    t.scalar("joint_claim_eval_ops", ej);
+    rc = poly_eval_prove(ctx, S->g_ops, S->d_comb_ops, rj, ej, t, tape, &pf_ops);
+    if (rc) return rc;
+  }
+  {
+    t.scalars("claim_evals_mem", ev_mem);
+    FqV rj;
+    Fq ej;
+    combine_evals(ev_mem, rand_mem, "challenge_combine_two_to_one", t, &rj, &ej);
+    t.scalar("joint_claim_eval_mem", ej);
+    rc = poly_eval_prove(ctx, S->g_mem, S->d_comb_mem, rj, ej, t, tape, &pf_mem);
+    if (rc) return rc;
+  }
+  timer_stop(ctx);
+  // ---- bincode(SparseMatPolyEvalProof)
+  Writer w;
+  w.pts(comm_derefs);
+  w.fq(row_init);  // ProductLayerProof
+  w.fqs(row_read);
+  w.fqs(row_write);
+  w.fq(row_audit);
+  w.fq(col_init);
+  w.fqs(col_read);
+  w.fqs(col_write);
+  w.fq(col_audit);
+  w.fqs(dl);
+  w.fqs(dr);
+  proof_mem.ser(w);
+  proof_ops.ser(w);
+  auto seg = [&](size_t k) { return FqV(ev_ops.begin() + k * B, ev_ops.begin() + (k + 1) * B); };
+  w.fqs(seg(0));  // HashLayerProof: row addr, row read_ts, row audit, col ..., val, derefs, proofs
+  w.fqs(seg(1));
+  w.fq(ev_mem[0]);
+  w.fqs(seg(2));
+  w.fqs(seg(3));
+  w.fq(ev_mem[1]);
+  w.fqs(seg(4));
+  w.fqs(FqV(ev_der.begin(), ev_der.begin() + B));
+  w.fqs(FqV(ev_der.begin() + B, ev_der.end()));
+  pf_ops.ser(w);
+  pf_mem.ser(w);
+  pf_der.ser(w);
+  *proof_len = w.out.size();
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  ctx->last_us = ms * 1000.0;
+  if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
+  memcpy(proof, w.out.data(), w.out.size());
+  return SPG_OK;
+}

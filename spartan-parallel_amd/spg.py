@@ -416,3 +416,47 @@ def shard_range(num_instances, rank, nranks):
     per = -(-num_instances // nranks)
     p0 = min(num_instances, rank * per)
     return p0, min(num_instances, p0 + per)
+
+
+class SparkCommitment:
+    """SparseMatPolynomial::multi_commit over the 3P matrices of an R1CS instance (src/sparse_mlpoly.rs:566-587)
+    with SparseMatPolyCommitmentGens::new(label, nvx, nvy, gens_nnz, gens_batch). The dense representation
+    stays in HBM for SparkCommitment.prove. `cinst` is a workload.CViews().inst."""
+
+    def __init__(self, ctx, cinst, label, gens_nnz, gens_batch=3, cap=1 << 22):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        if isinstance(label, str):
+            label = label.encode()
+        buf = np.zeros(cap, dtype=np.uint8)
+        ln = ctypes.c_size_t(0)
+        lb = (ctypes.c_uint8 * len(label)).from_buffer_copy(label)
+        ctx.check(lib().spg_spark_commit(ctx.handle, ctypes.byref(cinst), lb, ctypes.c_size_t(len(label)),
+                                         ctypes.c_size_t(gens_nnz), ctypes.c_size_t(gens_batch), ctypes.byref(self._h),
+                                         _p(buf), ctypes.c_size_t(cap), ctypes.byref(ln)), "spg_spark_commit")
+        self.bytes = buf[: ln.value].tobytes()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def prove(self, rx, ry, evals, transcript, tape, cap=1 << 24):
+        """SparseMatPolyEvalProof::prove (src/sparse_mlpoly.rs:1497-1564) -> bincode bytes"""
+        rx = _scalars(rx)
+        ry = _scalars(ry)
+        ev = _scalars(evals)
+        buf = np.zeros(cap, dtype=np.uint8)
+        ln = ctypes.c_size_t(0)
+        self.ctx.check(lib().spg_spark_prove(self.ctx.handle, self._h, _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
+                                             ctypes.c_size_t(ry.shape[0]), _p(ev), ctypes.c_size_t(ev.shape[0]),
+                                             transcript.handle, tape.handle, _p(buf), ctypes.c_size_t(cap),
+                                             ctypes.byref(ln)), "spg_spark_prove")
+        return buf[: ln.value].tobytes()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_spark_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass

@@ -75,3 +75,57 @@ def first_diff(a, b):
         if a[s:e] != b[s:e]:
             return name
     return None
+
+
+def _batched(r, name):  # ProductCircuitEvalProofBatched (src/product_tree.rs:262-269)
+    nl = r.u64(name + ".proof.len")
+    for i in range(nl):
+        p = f"{name}.proof[{i}]"
+        npol = r.u64(p + ".polys.len")
+        for j in range(npol):
+            r.scs(f"{p}.polys[{j}]")
+        r.scs(p + ".claims_prod_left")
+        r.scs(p + ".claims_prod_right")
+    for k in ("left", "right", "weight"):
+        r.scs(f"{name}.claims_dotp.{k}")
+
+
+def _dotlog(r, name):
+    r.pts(name + ".L")
+    r.pts(name + ".R")
+    for f in ("delta", "beta", "z1", "z2"):
+        r.take(name + "." + f, 32)
+
+
+def spark_proof_fields(b):
+    """bincode(SparseMatPolyEvalProof) (src/sparse_mlpoly.rs:1469-1475)"""
+    r = _R(b)
+    r.pts("comm_derefs")
+    for side in ("row", "col"):
+        r.take(f"{side}_init", 32)
+        r.scs(f"{side}_read")
+        r.scs(f"{side}_write")
+        r.take(f"{side}_audit", 32)
+    r.scs("dotp_left")
+    r.scs("dotp_right")
+    _batched(r, "proof_mem")
+    _batched(r, "proof_ops")
+    for side in ("row", "col"):
+        r.scs(f"eval_{side}_addr")
+        r.scs(f"eval_{side}_read_ts")
+        r.take(f"eval_{side}_audit_ts", 32)
+    r.scs("eval_val")
+    r.scs("eval_row_ops_val")
+    r.scs("eval_col_ops_val")
+    _dotlog(r, "proof_ops")
+    _dotlog(r, "proof_mem")
+    _dotlog(r, "proof_derefs")
+    assert r.o == len(b), (r.o, len(b))
+    return r.fields
+
+
+def first_diff_spark(a, b):
+    for name, s, e in spark_proof_fields(a):
+        if a[s:e] != b[s:e]:
+            return name
+    return None
