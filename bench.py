@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="replicas", choices=["replicas", "shard"])
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
+    ap.add_argument("--workload", default="r1cs", choices=["r1cs", "spark"],
+                    help="r1cs: the headline metric (R1CSProof::prove); spark: SURVEY 8d config 5 (SPARK)")
+    ap.add_argument("--log-nnz", type=int, default=24, help="spark: 2^k nonzeros per matrix (x3 matrices)")
+    ap.add_argument("--cpu-log-nnz", type=int, default=15, help="spark: CPU baseline sample size")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 --pmc (scripts/pmc_traffic.py), if present")
     return ap.parse_args()
@@ -57,6 +61,8 @@ def parse():
 
 def main():
     a = parse()
+    if a.workload == "spark":
+        return main_spark(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -192,6 +198,128 @@ def main():
             "value_incl_witness_upload": round(N * world / t_incl, 1), "kernels": kernels,
         }
         print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def roofline_of(prof, traffic_file):
+    """roofline object for the modelled kernel with the largest device time"""
+    modelled = {k: v for k, v in prof.items() if v[2] > 0}
+    dom = max(modelled, key=lambda k: modelled[k][1])
+    launches, us, nbytes = modelled[dom]
+    achieved = (nbytes / launches) / (us / launches * 1e-6) / 1e9
+    traffic = None
+    if traffic_file and os.path.exists(traffic_file):
+        tr = json.load(open(traffic_file))
+        if dom in tr.get("kernels", {}):
+            traffic = tr["kernels"][dom]["hbm_bytes_per_launch"]
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": nbytes / launches, "avg_launch_us": us / launches, "launches": launches}
+
+
+def main_spark(a):
+    """SURVEY 8d config 5: SparseMatPolynomial::multi_evaluate + SparseMatPolyEvalProof::prove over the three
+    2^k-nonzero matrices (A, B, C) with num_vars_x = num_vars_y = k. A step is one multi_evaluate at (rx, ry)
+    plus one full SPARK evaluation proof (derefs, derefs commit, hash layer, product trees, batched layer
+    sumchecks, hash-layer PolyEvalProofs) with the dense representation resident in HBM (multi_commit is the
+    preprocessing step, SNARK::encode, and is timed separately). Multi-GPU: independent replicas."""
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(a.backend or ("nccl" if torch.cuda.is_available() else "gloo"))
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if ndev else local
+    if torch.cuda.is_available():
+        torch.cuda.set_device(gpu)
+    import spg
+    import workload
+
+    k = a.log_nnz
+    ctx = spg.Context(gpu)
+    t0 = time.perf_counter()
+    wl = workload.SparkWorkload(k)
+    views = workload.CViews(wl)
+    t_gen = time.perf_counter() - t0
+    rng = np.random.default_rng(3 + rank)
+    r = rng.integers(0, 1 << 63, size=(2 * k, 4), dtype=np.uint64)
+    r[:, 3] &= np.uint64((1 << 60) - 1)
+    rx, ry = r[:k], r[k:]
+    t0 = time.perf_counter()
+    comm = spg.SparkCommitment(ctx, views.inst, b"gens_r1cs_eval", wl.nnz, 3)
+    t_commit = time.perf_counter() - t0
+    inst = spg.R1CSInst(ctx, views.inst)
+    seed = workload.tape_seed()
+
+    def step():
+        evals = spg.r1cs_multi_evaluate(ctx, inst, 1, rx, ry)
+        return comm.prove(rx, ry, evals, spg.Transcript(b"spark_bench"), spg.RandomTape(b"proof", seed))
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    sync()
+    ctx.prof_enable(True)
+    ctx.prof_read(reset=True)
+    sync()
+    t0 = time.perf_counter()
+    proofs = set()
+    for _ in range(a.steps):
+        proofs.add(hashlib.sha256(step()).hexdigest())
+    sync()
+    dt = time.perf_counter() - t0
+    prof = ctx.prof_read(reset=True)
+    ctx.prof_enable(False)
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    assert len(proofs) == 1, "proof bytes changed between steps"
+    nnz = 3 * wl.nnz
+    value = nnz * world * a.steps / dt
+    top = sorted(prof.items(), key=lambda kv: -kv[1][1])[:10]
+    kernels = {n: {"launches_per_step": v[0] / a.steps, "ms_per_step": round(v[1] / a.steps / 1e3, 3),
+                   "GBps": round(v[2] / (v[1] * 1e-6) / 1e9, 1) if v[2] else None} for n, v in top}
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle  # the checker / CPU baseline only
+
+        pyoracle.build()
+        kc = min(a.cpu_log_nnz, k)
+        wc = workload.SparkWorkload(kc)
+        rc_ = rng.integers(0, 1 << 63, size=(2 * kc, 4), dtype=np.uint64)
+        rc_[:, 3] &= np.uint64((1 << 60) - 1)
+        pyoracle.spark_prove(wc, rc_[:kc], rc_[kc:], seed)
+        tcpu = pyoracle.spark_last_prove_us() * 1e-6
+        cpu = {"value": round(3 * (1 << kc) / tcpu, 1), "unit": "nonzeros/s", "cores": 1, "kind": "port",
+               "sample": f"3 x 2^{kc} nonzeros (same generator), multi_evaluate + SparseMatPolyEvalProof::prove, "
+                         f"{tcpu:.2f} s on 1 host thread"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SPARK nonzeros/sec (sparse_mlpoly multi_evaluate + SparseMatPolyEvalProof::prove)",
+            "value": round(value, 1), "unit": "nonzeros/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255",
+            "data": "synthetic (SURVEY 8d config 5 generator, seed 5)",
+            "config": {"workload": "SparseMatPolyEvalProof::prove, batch 3 (src/sparse_mlpoly.rs:1497-1564)",
+                       "log_nnz": k, "num_vars_x": k, "num_vars_y": k, "parallelism": f"replicas x{world}"},
+            "roofline": roofline_of(prof, None), "cpu_baseline": cpu, "proof_sha256": sorted(proofs)[0][:16],
+            "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
+            "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
+            "kernels": kernels}))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -311,6 +311,8 @@ int orc_r1cs_multi_evaluate(const spg_r1cs_instance* ci, const uint64_t* rx, siz
 }
 }
 
+#include <chrono>
+
 #include "spark.hpp"
 
 extern "C" {
@@ -320,6 +322,10 @@ extern "C" {
 // Proves SparseMatPolyEvalProof at (rx, ry) for evals = multi_evaluate(rx, ry) under a fresh
 // Transcript(label) + RandomTape("proof", seed), writes bincode(commitment) and bincode(proof), then runs
 // the verifier on a fresh transcript. Returns 1 if it verifies, 0 if not, <0 on error.
+static double g_spark_prove_us = 0.0;
+// wall time of the last orc_spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove (CPU baseline)
+double orc_spark_last_prove_us() { return g_spark_prove_us; }
+
 int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t gens_nnz, size_t gens_batch,
                     const uint64_t* rx, size_t rx_len, const uint64_t* ry, size_t ry_len, const char* label,
                     const uint64_t* tape_seed, uint8_t* comm_out, size_t comm_cap, size_t* comm_len,
@@ -339,10 +345,12 @@ int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t 
     SparkGens g = SparkGens::create(gens_label, nvx, nvy, gens_nnz, gens_batch);
     MultiSparseDense dense;
     SparkCommitment comm = spark_multi_commit(polys, g, &dense);
+    auto t0 = std::chrono::steady_clock::now();
     FqVec evals = inst.multi_evaluate(vx, vy);
     Transcript t(label);
     RandomTape tape("proof", ld(tape_seed));
     SparkEvalProof pf = spark_prove(dense, vx, vy, evals, g, t, tape);
+    g_spark_prove_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     Ser sc, sp;
     comm.ser(sc);
     pf.ser(sp);

@@ -262,3 +262,10 @@ def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=No
                                ctypes.byref(pl))
     assert rc >= 0, rc
     return cb[: cl.value].tobytes(), pb[: pl.value].tobytes(), rc == 1
+
+
+def spark_last_prove_us():
+    """wall time (us) of the last spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove on the host"""
+    f = lib().orc_spark_last_prove_us
+    f.restype = ctypes.c_double
+    return f()

@@ -198,3 +198,34 @@ def tape_seed(label=b"spg-tape-seed-0"):
 
     b = hashlib.shake_256(label).digest(64)
     return to_mont_limbs([int.from_bytes(b, "little") % Q])[0]
+
+
+class SparkWorkload:
+    """one SparseMatPolynomial per A, B and C with num_vars_x = num_vars_y = k and
+    2^k entries each: entry i has row = i, col = (i * 0x9E3779B1) mod 2^k, val = a random scalar (seed 5;
+    uniform 252-bit limbs taken as Montgomery representations). Exposed as a one-instance R1CS so the
+    same C views (CViews) carry it to spg_spark_commit / spg_r1cs_multi_evaluate."""
+
+    def __init__(self, log_nnz, seed=5):
+        n = 1 << log_nnz
+        rng = np.random.default_rng(seed)
+        i = np.arange(n, dtype=np.uint64)
+        mats = []
+        for _ in range(3):
+            arr = np.empty((n, 6), dtype=np.uint64)
+            arr[:, 0] = i
+            arr[:, 1] = (i * np.uint64(0x9E3779B1)) & np.uint64(n - 1)
+            arr[:, 2:] = rng.integers(0, 1 << 63, size=(n, 4), dtype=np.uint64, endpoint=False) * np.uint64(2) \
+                + rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
+            arr[:, 5] &= np.uint64((1 << 60) - 1)
+            mats.append(arr)
+        self.entries = [mats]
+        self.P = 1
+        self.num_cons = [n]
+        self.max_num_cons = n
+        self.num_vars = n
+        self.nws = 0
+        self.sections = []
+        self.num_proofs = [1]
+        self.num_inputs = [n]
+        self.nnz = n
