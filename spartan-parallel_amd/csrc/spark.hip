@@ -106,30 +106,27 @@ __device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
   __syncthreads();
 }
 // one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
-// sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367); blocks publish partials
+// sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367). blockIdx.y = triple, so the
+// coefficient multiplies the block's sums once; blocks publish partials (triple-major).
 __global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
-                                                    size_t nt, int log_len, Fq* __restrict__ partials) {
-  const size_t len = (size_t)1 << log_len;
+                                                    size_t len, Fq* __restrict__ partials) {
+  const Triple x = tr[blockIdx.y];
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
-  for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < nt * len; t += (size_t)gridDim.x * 256) {
-    size_t c = t >> log_len, i = t & (len - 1);
-    const Triple x = tr[c];
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (size_t)gridDim.x * 256) {
     Fq al = x.A[i], ah = x.A[i + len], bl = x.B[i], bh = x.B[i + len], cl = x.C[i], ch = x.C[i + len];
-    Fq k = coeff[c];
-    Fq v0 = fq_mul(fq_mul(al, bl), cl);
     Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
     Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
-    Fq v2 = fq_mul(fq_mul(a2, b2), c2);
-    Fq v3 = fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc));
-    e0 = fq_add(e0, fq_mul(k, v0));
-    e2 = fq_add(e2, fq_mul(k, v2));
-    e3 = fq_add(e3, fq_mul(k, v3));
+    e0 = fq_add(e0, fq_mul(fq_mul(al, bl), cl));
+    e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
+    e3 = fq_add(e3, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
   }
   block_sum3_sp(e0, e2, e3);
   if (threadIdx.x == 0) {
-    partials[3 * blockIdx.x] = e0;
-    partials[3 * blockIdx.x + 1] = e2;
-    partials[3 * blockIdx.x + 2] = e3;
+    const Fq k = coeff[blockIdx.y];
+    const size_t o = 3 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
+    partials[o] = fq_mul(k, e0);
+    partials[o + 1] = fq_mul(k, e2);
+    partials[o + 2] = fq_mul(k, e3);
   }
 }
 __global__ void __launch_bounds__(256) k_sum3(const Fq* __restrict__ partials, int nb, Fq* __restrict__ out) {
@@ -362,7 +359,7 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
   Triple* dtr = (Triple*)ws_get(ctx, kWsTriples, nt_max * sizeof(Triple) + 64);
   Fq* dcoef = (Fq*)ws_get(ctx, kWsCoeff, nt_max * sizeof(Fq) + 64);
   Fq** dptr = (Fq**)ws_get(ctx, kWsFoldPtr, (2 * nc + 1 + 3 * dotp.size()) * sizeof(Fq*) + 64);
-  Fq* part = (Fq*)ws_get(ctx, kWsPart, 3 * 1024 * sizeof(Fq) + 64);
+  Fq* part = (Fq*)ws_get(ctx, kWsPart, 3 * std::max<size_t>(2048, nt_max) * sizeof(Fq) + 64);
   Fq* d3 = (Fq*)ws_get(ctx, kWs3, 3 * sizeof(Fq) + 64);
   Fq* dfin = (Fq*)ws_get(ctx, kWsFinals, 3 * nt_max * sizeof(Fq) + 64);
   if (!dC || !dtr || !dcoef || !dptr || !part || !d3 || !dfin) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
@@ -403,11 +400,11 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     for (size_t j = 0; j < rounds; j++) {
       log_len--;
       const size_t len = (size_t)1 << log_len;
-      unsigned nb = (unsigned)std::min<size_t>(nblk(tr.size() * len), 1024);
+      const unsigned nbx = (unsigned)std::min<size_t>(nblk(len), std::max<size_t>(1, 2048 / tr.size()));
       {
         KScope ks(ctx, "spark_layer_eval", 192.0 * tr.size() * len);
-        hipLaunchKernelGGL(k_layer_eval, dim3(nb), dim3(256), 0, s, dtr, dcoef, tr.size(), (int)log_len, part);
-        hipLaunchKernelGGL(k_sum3, dim3(1), dim3(256), 0, s, part, (int)nb, d3);
+        hipLaunchKernelGGL(k_layer_eval, dim3(nbx, (unsigned)tr.size()), dim3(256), 0, s, dtr, dcoef, len, part);
+        hipLaunchKernelGGL(k_sum3, dim3(1), dim3(256), 0, s, part, (int)(nbx * tr.size()), d3);
       }
       Fq ev[3];
       rc = d2h_fq(ctx, d3, ev, 3);

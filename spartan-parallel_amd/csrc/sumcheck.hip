@@ -96,6 +96,14 @@ __global__ void k_eq_table(FqArg32 r, Fq* __restrict__ out, size_t n) {
   out[b] = acc;
 }
 
+// factored form for large tables: out[b] = hi[b >> lo_bits] * lo[b & (2^lo_bits - 1)]
+__global__ void k_eq_combine(const Fq* __restrict__ hi, const Fq* __restrict__ lo, int lo_bits, Fq* __restrict__ out,
+                             size_t n) {
+  size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  out[b] = fq_mul(hi[b >> lo_bits], lo[b & (((size_t)1 << lo_bits) - 1)]);
+}
+
 // bound_poly_var_top on a dense vector of length 2n (in place, first n outputs)
 __global__ void k_fold_top(Fq* __restrict__ v, size_t n, Fq r) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -292,7 +300,25 @@ int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out) {
   for (int i = 0; i < ell; i++) a.v[i] = r[i];
   size_t n = (size_t)1 << ell;
   KScope ks(ctx, "eq_table", 32.0 * n);
-  hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, a, out, n);
+  if (ell <= 12) {
+    hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, a, out, n);
+  } else {  // eq(r) = eq(r_hi) (x) eq(r_lo): two small tables, then one multiplication per entry
+    const int hb = ell / 2, lb = ell - hb;
+    Fq* t = (Fq*)ws_get(ctx, 16, (((size_t)1 << hb) + ((size_t)1 << lb)) * sizeof(Fq) + 64);
+    if (!t) return set_err(ctx, SPG_E_NOMEM, "eq table");
+    Fq* hi = t;
+    Fq* lo = t + ((size_t)1 << hb);
+    FqArg32 ah, al;
+    ah.n = hb;
+    al.n = lb;
+    for (int i = 0; i < hb; i++) ah.v[i] = r[i];
+    for (int i = 0; i < lb; i++) al.v[i] = r[hb + i];
+    hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((((size_t)1 << hb) + 255) / 256)), dim3(256), 0, ctx->stream, ah,
+                       hi, (size_t)1 << hb);
+    hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((((size_t)1 << lb) + 255) / 256)), dim3(256), 0, ctx->stream, al,
+                       lo, (size_t)1 << lb);
+    hipLaunchKernelGGL(k_eq_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, hi, lo, lb, out, n);
+  }
   SPG_HIP(ctx, hipGetLastError());
   return 0;
 }
