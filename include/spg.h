@@ -188,6 +188,45 @@ int spg_spark_prove(spg_ctx* ctx, spg_spark* s, const uint64_t* rx, size_t rx_le
                     spg_random_tape* tape, uint8_t* proof, size_t proof_cap, size_t* proof_len);
 int spg_spark_free(spg_ctx* ctx, spg_spark* s);
 
+/* ---- SNARK::prove (src/lib.rs:971-2746) -------------------------------------------------------------
+ * Public side: each of the three R1CS instances (block, pairwise check, perm root) with the parameters of
+ * the SNARKGens it was encoded with (SNARKGens::new(num_cons, num_vars, num_instances, num_nz_entries),
+ * src/lib.rs:164-185; only its gens_r1cs_eval part is used by SNARK::prove). */
+typedef struct {
+  spg_r1cs_instance inst;  /* unsorted, as generated (src/instance.rs) */
+  size_t gens_num_cons, gens_num_vars, gens_num_instances, gens_num_nz_entries;
+} spg_snark_instance;
+
+/* The run-time arguments of SNARK::prove in declaration order (src/lib.rs:971-1023). Scalars are Montgomery
+ * limbs (4 x u64); witness lists are flattened row-major. */
+typedef struct {
+  size_t input_block_num, output_block_num;
+  const uint8_t* input_liveness; /* [input_len] */
+  size_t input_len;
+  size_t func_input_width, input_offset, output_offset;
+  const uint64_t* input;  /* [input_len][4] */
+  const uint64_t* output; /* [4] */
+  size_t output_exec_num;
+  size_t num_vars, num_ios;
+  size_t max_block_num_phy_ops;
+  const size_t* block_num_phy_ops; /* [block_num_instances_bound] */
+  size_t max_block_num_vir_ops;
+  const size_t* block_num_vir_ops; /* [block_num_instances_bound] */
+  size_t mem_addr_ts_bits_size, num_inputs_unpadded;
+  const size_t* block_num_vars; /* [block_num_instances_bound] */
+  size_t block_num_instances_bound, block_max_num_proofs;
+  const size_t* block_num_proofs; /* [block_num_instances_bound] */
+  size_t consis_num_proofs, total_num_init_phy_mem_accesses, total_num_init_vir_mem_accesses,
+      total_num_phy_mem_accesses, total_num_vir_mem_accesses;
+  const uint64_t* const* block_vars; /* [b] -> block_num_proofs[b] x block_num_vars[b] x 4 */
+  const uint64_t* exec_inputs;       /* consis_num_proofs x num_ios x 4 */
+  const uint64_t* init_phy_mems;     /* total_num_init_phy_mem_accesses x 4 x 4 */
+  const uint64_t* init_vir_mems;     /* total_num_init_vir_mem_accesses x 4 x 4 */
+  const uint64_t* addr_phy_mems;     /* total_num_phy_mem_accesses x 4 x 4 */
+  const uint64_t* addr_vir_mems;     /* total_num_vir_mem_accesses x 8 x 4 */
+  const uint64_t* addr_ts_bits;      /* total_num_vir_mem_accesses x mem_addr_ts_bits_size x 4 */
+} spg_snark_inputs;
+
 #ifdef __cplusplus
 }
 #endif

@@ -366,3 +366,105 @@ int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t 
   }
 }
 }
+
+#include "snark.hpp"
+
+namespace {
+using namespace orc;
+double g_snark_prove_us = 0.0;
+
+SnarkIn snark_in_from_c(const spg_snark_inputs* c) {
+  SnarkIn in;
+  in.input_block_num = c->input_block_num;
+  in.output_block_num = c->output_block_num;
+  for (size_t i = 0; i < c->input_len; i++) {
+    in.input_liveness.push_back(c->input_liveness[i] != 0);
+    in.input.push_back(ld(c->input + 4 * i));
+  }
+  in.func_input_width = c->func_input_width;
+  in.input_offset = c->input_offset;
+  in.output_offset = c->output_offset;
+  in.output = ld(c->output);
+  in.output_exec_num = c->output_exec_num;
+  in.num_vars = c->num_vars;
+  in.num_ios = c->num_ios;
+  in.max_block_num_phy_ops = c->max_block_num_phy_ops;
+  in.max_block_num_vir_ops = c->max_block_num_vir_ops;
+  const size_t B = c->block_num_instances_bound;
+  in.block_num_phy_ops.assign(c->block_num_phy_ops, c->block_num_phy_ops + B);
+  in.block_num_vir_ops.assign(c->block_num_vir_ops, c->block_num_vir_ops + B);
+  in.mem_addr_ts_bits_size = c->mem_addr_ts_bits_size;
+  in.num_inputs_unpadded = c->num_inputs_unpadded;
+  in.block_num_vars.assign(c->block_num_vars, c->block_num_vars + B);
+  in.block_num_instances_bound = B;
+  in.block_max_num_proofs = c->block_max_num_proofs;
+  in.block_num_proofs.assign(c->block_num_proofs, c->block_num_proofs + B);
+  in.consis_num_proofs = c->consis_num_proofs;
+  in.total_num_init_phy_mem_accesses = c->total_num_init_phy_mem_accesses;
+  in.total_num_init_vir_mem_accesses = c->total_num_init_vir_mem_accesses;
+  in.total_num_phy_mem_accesses = c->total_num_phy_mem_accesses;
+  in.total_num_vir_mem_accesses = c->total_num_vir_mem_accesses;
+  auto rows = [](const uint64_t* p, size_t n, size_t w) {
+    std::vector<FqVec> m(n, FqVec(w));
+    for (size_t q = 0; q < n; q++)
+      for (size_t i = 0; i < w; i++) m[q][i] = ld(p + 4 * (q * w + i));
+    return m;
+  };
+  for (size_t b = 0; b < B; b++)
+    in.block_vars_mat.push_back(c->block_num_proofs[b] ? rows(c->block_vars[b], c->block_num_proofs[b], c->block_num_vars[b])
+                                                       : std::vector<FqVec>());
+  in.exec_inputs_list = rows(c->exec_inputs, c->consis_num_proofs, c->num_ios);
+  if (c->total_num_init_phy_mem_accesses)
+    in.init_phy_mems_list = rows(c->init_phy_mems, c->total_num_init_phy_mem_accesses, INIT_PHY_MEM_WIDTH);
+  if (c->total_num_init_vir_mem_accesses)
+    in.init_vir_mems_list = rows(c->init_vir_mems, c->total_num_init_vir_mem_accesses, INIT_VIR_MEM_WIDTH);
+  if (c->total_num_phy_mem_accesses)
+    in.addr_phy_mems_list = rows(c->addr_phy_mems, c->total_num_phy_mem_accesses, PHY_MEM_WIDTH);
+  if (c->total_num_vir_mem_accesses) {
+    in.addr_vir_mems_list = rows(c->addr_vir_mems, c->total_num_vir_mem_accesses, VIR_MEM_WIDTH);
+    in.addr_ts_bits_list = rows(c->addr_ts_bits, c->total_num_vir_mem_accesses, c->mem_addr_ts_bits_size);
+  }
+  return in;
+}
+
+SnarkInst snark_inst_from_c(const spg_snark_instance* c, bool multi) {
+  SnarkInst s;
+  s.inst = inst_from_c(&c->inst);
+  s.gens = snark_eval_gens(c->gens_num_cons, c->gens_num_vars, c->gens_num_instances, c->gens_num_nz_entries);
+  s.multi = multi;
+  s.encode();
+  return s;
+}
+}  // namespace
+
+extern "C" {
+// SNARK::multi_encode(block) / encode(pairwise) / encode(perm_root), then SNARK::prove under a fresh
+// Transcript(label) + RandomTape("proof", seed) with vars_gens = R1CSGens(gens_label, gens_num_vars); writes
+// bincode(SNARK). Returns 0 when the oracle's verifier accepts, >0 = failing verifier stage, <0 on error.
+int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* block_c,
+                    const spg_snark_instance* pairwise_c, const spg_snark_instance* perm_root_c, const char* gens_label,
+                    size_t gens_num_vars, const char* label, const uint64_t* tape_seed, uint8_t* out, size_t cap,
+                    size_t* out_len) {
+  try {
+    SnarkIn in = snark_in_from_c(in_c);
+    SnarkInst block = snark_inst_from_c(block_c, true), pairwise = snark_inst_from_c(pairwise_c, false),
+              perm_root = snark_inst_from_c(perm_root_c, false);
+    R1CSGens vg = R1CSGens::create(gens_label, gens_num_vars);
+    auto t0 = std::chrono::steady_clock::now();
+    Transcript t(label);
+    RandomTape tape("proof", ld(tape_seed));
+    SNARKProof pf = snark_prove(in, block, pairwise, perm_root, vg, t, tape);
+    g_snark_prove_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    Ser s;
+    pf.ser(s);
+    *out_len = s.b.size();
+    if (s.b.size() > cap) return -1;
+    memcpy(out, s.b.data(), s.b.size());
+    Transcript tv(label);
+    return snark_verify(pf, in, block, pairwise, perm_root, vg, tv);
+  } catch (const std::string& e) {
+    return -2;
+  }
+}
+double orc_snark_last_prove_us() { return g_snark_prove_us; }
+}

@@ -269,3 +269,24 @@ def spark_last_prove_us():
     f = lib().orc_spark_last_prove_us
     f.restype = ctypes.c_double
     return f()
+
+
+def snark_prove(wl, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24, label=b"snark_test", cap=1 << 24):
+    """SNARK::prove on a workload.SnarkWorkload -> (bincode(SNARK), verifier status: 0 = accepted)"""
+    import workload
+
+    v = workload.SnarkViews(wl)
+    out = np.zeros(cap, dtype=np.uint8)
+    ln = ctypes.c_size_t(0)
+    seed = u64s(tape_seed)
+    rc = lib().orc_snark_prove(ctypes.byref(v.inputs), ctypes.byref(v.block), ctypes.byref(v.pairwise),
+                               ctypes.byref(v.perm_root), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars),
+                               ctypes.c_char_p(label), _p(seed), _p(out), ctypes.c_size_t(cap), ctypes.byref(ln))
+    assert rc >= 0, rc
+    return out[: ln.value].tobytes(), rc
+
+
+def snark_last_prove_us():
+    f = lib().orc_snark_last_prove_us
+    f.restype = ctypes.c_double
+    return f()

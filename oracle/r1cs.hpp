@@ -402,7 +402,7 @@ struct R1CSProof {
               size_t max_num_inputs, const std::vector<std::vector<size_t>>& ws_num_inputs,
               const std::vector<std::vector<size_t>>& ws_num_proofs,
               const std::vector<std::vector<PolyCommitment>>& ws_comm, size_t num_cons, const R1CSGens& gens,
-              const Fq evals[3], Transcript& t) const {
+              const Fq evals[3], Transcript& t, std::vector<FqVec>* challenges = nullptr) const {
     t.append_protocol_name("R1CS proof");
     size_t nws = ws_comm.size();
     size_t np = log_2(next_pow2(num_instances)), nq = log_2(max_num_proofs), nx = log_2(num_cons),
@@ -482,7 +482,13 @@ struct R1CSProof {
     uint8_t kb[32];
     fq_to_bytes(k, kb);
     CPt expected2 = cpt(ge_scalarmul_bytes(unpack(comm_vars_at_ry), kb));
-    return eq2.verify(gens.gens_1, t, expected2, post2);
+    bool ok = eq2.verify(gens.gens_1, t, expected2, post2);
+    if (challenges) {  // [rp, rq_rev, rx, rw || ry] (r1csproof.rs:953)
+      FqVec rx(rx_rev.rbegin(), rx_rev.rend()), rwry(rw);
+      rwry.insert(rwry.end(), ry.begin(), ry.end());
+      *challenges = {rp, rq_rev, rx, rwry};
+    }
+    return ok;
   }
 };
 

@@ -229,3 +229,342 @@ class SparkWorkload:
         self.num_proofs = [1]
         self.num_inputs = [n]
         self.nnz = n
+
+
+# ---------------------------------------------------------------- SNARK::prove workload
+def _instance_new(num_instances, max_num_cons, num_cons, num_vars, A, B, C):
+    """Instance::new (src/instance.rs:19-146): pads num_cons / max_num_cons / num_vars to powers of two
+    (at least 2 constraints) and turns (row, col, int) triples into (n, 6) uint64 entry arrays."""
+    npow = lambda x: 1 << max(0, (x - 1).bit_length())
+    nvp = npow(num_vars)
+    mnc = max_num_cons if max_num_cons >= 2 else 2
+    if npow(max_num_cons) != max_num_cons:
+        mnc = npow(max_num_cons)
+    ncp = [2 if c <= 1 else npow(c) for c in num_cons]
+    mats = []
+    for b in range(num_instances):
+        one = []
+        for L in (A[b], B[b], C[b]):
+            arr = np.zeros((len(L), 6), dtype=np.uint64)
+            if L:
+                vals = to_mont_limbs([v % Q for _, _, v in L])
+                for k, (r, c, _) in enumerate(L):
+                    assert r < num_cons[b] and c < num_vars
+                    arr[k, 0] = r
+                    arr[k, 1] = c
+                arr[:, 2:] = vals
+            one.append(arr)
+        mats.append(one)
+    return mats, mnc, ncp, nvp
+
+
+class _Constr:
+    """Instance::gen_constr (src/instance.rs:156-192): appends one row of (col, int) terms to A, B, C"""
+
+    def __init__(self):
+        self.A, self.B, self.C = [], [], []
+
+    def add(self, row, a, b, c):
+        self.A += [(row, col, v) for col, v in a]
+        self.B += [(row, col, v) for col, v in b]
+        self.C += [(row, col, v) for col, v in c]
+
+
+def gen_block_inst(num_vars, args, niu, num_phy_ops, num_vir_ops):
+    """Instance::gen_block_inst (src/instance.rs:253-737) -> (block_num_vars, block_max_num_cons,
+    block_num_non_zero_entries, (mats, max_num_cons, num_cons, num_vars))"""
+    io_width = 2 * niu
+    V_valid = V_cnst = 0
+    V_input = lambda i: 2 + i
+    V_output = lambda i: 2 + (niu - 1) + i
+    V_PA = lambda i: io_width + 2 * i
+    V_PD = lambda i: io_width + 2 * i + 1
+    V_VA = lambda b, i: io_width + 2 * num_phy_ops[b] + 4 * i
+    V_VD = lambda b, i: io_width + 2 * num_phy_ops[b] + 4 * i + 1
+    V_VL = lambda b, i: io_width + 2 * num_phy_ops[b] + 4 * i + 2
+    V_VT = lambda b, i: io_width + 2 * num_phy_ops[b] + 4 * i + 3
+    V_tau = num_vars
+    V_r = lambda i: num_vars + i
+    V_in_dp = lambda i: V_input(0) if i == 0 else 2 * num_vars + 2 + i
+    V_out_dp = lambda i: 2 * num_vars + 2 + (niu - 1) + i
+    V_PMR = lambda i: 2 * num_vars + 2 * niu + 2 * i
+    V_PMC = lambda i: 2 * num_vars + 2 * niu + 2 * i + 1
+    V_VMR1 = lambda b, i: 2 * num_vars + 2 * niu + 2 * num_phy_ops[b] + 4 * i
+    V_VMR2 = lambda b, i: 2 * num_vars + 2 * niu + 2 * num_phy_ops[b] + 4 * i + 1
+    V_VMR3 = lambda b, i: 2 * num_vars + 2 * niu + 2 * num_phy_ops[b] + 4 * i + 2
+    V_VMC = lambda b, i: 2 * num_vars + 2 * niu + 2 * num_phy_ops[b] + 4 * i + 3
+    V_v, V_x, V_pi, V_d = 3 * num_vars, 3 * num_vars + 1, 3 * num_vars + 2, 3 * num_vars + 3
+    V_Pp, V_Pd, V_Vp, V_Vd = 3 * num_vars + 4, 3 * num_vars + 5, 3 * num_vars + 6, 3 * num_vars + 7
+    V_sv, V_spi, V_Psp, V_Vsp = 4 * num_vars, 4 * num_vars + 2, 4 * num_vars + 4, 4 * num_vars + 6
+    A_l, B_l, C_l, ncons = [], [], [], []
+    max_nc, nnz = 0, 0
+    for b, arg in enumerate(args):
+        k = _Constr()
+        nA = nB = nC = 0
+        for i, (a, bb, c) in enumerate(arg):
+            nA += len(a); nB += len(bb); nC += len(c)
+            k.add(i, a, bb, c)
+        cnt = len(arg)
+        for i in range(1, niu - 1):
+            k.add(cnt, [(V_input(i), 1)], [(V_r(i), 1)], [(V_in_dp(i), 1)]); cnt += 1
+        for i in range(niu - 1):
+            k.add(cnt, [(V_output(i), 1)], [(V_r(i + niu - 1), 1)], [(V_out_dp(i), 1)]); cnt += 1
+        k.add(cnt, [], [], [(V_valid, 1), (V_v, -1)]); cnt += 1
+        k.add(cnt, [(V_tau, 1)] + [(V_in_dp(i), -1) for i in range(2 * niu - 2)], [(V_cnst, 1)], [(V_x, 1)]); cnt += 1
+        k.add(cnt, [(V_x, 1)], [(V_spi, 1), (V_cnst, 1), (V_sv, -1)], [(V_d, 1)]); cnt += 1
+        k.add(cnt, [(V_v, 1)], [(V_d, 1)], [(V_pi, 1)]); cnt += 1
+        nA += 4 * niu - 2; nB += 2 * niu + 2; nC += 2 * niu + 2
+        for i in range(num_phy_ops[b]):
+            k.add(cnt, [(V_r(1), 1)], [(V_PD(i), 1)], [(V_PMR(i), 1)]); cnt += 1
+            k.add(cnt, [(V_cnst, 1) if i == 0 else (V_PMC(i - 1), 1)], [(V_tau, 1), (V_PA(i), -1), (V_PMR(i), -1)],
+                  [(V_PMC(i), 1)]); cnt += 1
+        cnt += 1
+        k.add(cnt, [(V_cnst, 1) if num_phy_ops[b] == 0 else (V_PMC(num_phy_ops[b] - 1), 1)],
+              [(V_Psp, 1), (V_cnst, 1), (V_sv, -1)], [(V_Pd, 1)]); cnt += 1
+        k.add(cnt, [(V_v, 1)], [(V_Pd, 1)], [(V_Pp, 1)]); cnt += 1
+        nA += 3 * num_phy_ops[b] + 2; nB += 7 * num_phy_ops[b] + 4; nC += 3 * num_phy_ops[b] + 2
+        for i in range(num_vir_ops[b]):
+            k.add(cnt, [(V_r(1), 1)], [(V_VD(b, i), 1)], [(V_VMR1(b, i), 1)]); cnt += 1
+            k.add(cnt, [(V_r(2), 1)], [(V_VL(b, i), 1)], [(V_VMR2(b, i), 1)]); cnt += 1
+            k.add(cnt, [(V_r(3), 1)], [(V_VT(b, i), 1)], [(V_VMR3(b, i), 1)]); cnt += 1
+            k.add(cnt, [(V_cnst, 1) if i == 0 else (V_VMC(b, i - 1), 1)],
+                  [(V_tau, 1), (V_VA(b, i), -1), (V_VMR1(b, i), -1), (V_VMR2(b, i), -1), (V_VMR3(b, i), -1)],
+                  [(V_VMC(b, i), 1)]); cnt += 1
+        cnt += 1
+        k.add(cnt, [(V_cnst, 1) if num_vir_ops[b] == 0 else (V_VMC(b, num_vir_ops[b] - 1), 1)],
+              [(V_Vsp, 1), (V_cnst, 1), (V_sv, -1)], [(V_Vd, 1)]); cnt += 1
+        k.add(cnt, [(V_v, 1)], [(V_Vd, 1)], [(V_Vp, 1)]); cnt += 1
+        nA += 5 * num_vir_ops[b] + 2; nB += 13 * num_vir_ops[b] + 4; nC += 5 * num_vir_ops[b] + 2
+        max_nc = max(max_nc, cnt)
+        ncons.append(cnt)
+        nnz = max(nnz, nA, nB, nC)
+        A_l.append(k.A); B_l.append(k.B); C_l.append(k.C)
+    block_num_vars = 8 * num_vars
+    inst = _instance_new(len(args), max_nc, ncons, block_num_vars, A_l, B_l, C_l)
+    return block_num_vars, max_nc, nnz, inst
+
+
+def gen_pairwise_check_inst(max_ts_width, mem_addr_ts_bits_size):
+    """Instance::gen_pairwise_check_inst (src/instance.rs:740-1073) -> (num_vars, max_num_cons, nnz, inst)"""
+    width = max(8, mem_addr_ts_bits_size)
+    max_nc = 8 + max_ts_width
+    ncons = [2, 4, 8 + max_ts_width]
+    nnz = max(13 + max_ts_width, 5 + 2 * max_ts_width)
+    c0 = _Constr()  # CONSIS_CHECK
+    c0.add(0, [(5, 1), (width + 4, -1)], [(width + 4, 1)], [])
+    c1 = _Constr()  # PHY_MEM_COHERE
+    c1.add(0, [(0, 1), (0, -1)], [(width, 1)], [])
+    c1.add(1, [(width, 1)], [(0, 1), (width + 2, -1), (2, 1)], [(1, 1)])
+    c1.add(2, [(1, 1)], [(width + 2, 1), (2, -1)], [])
+    c1.add(3, [(1, 1)], [(width + 3, 1), (3, -1)], [])
+    c2 = _Constr()  # VIR_MEM_COHERE
+    V_D2, V_EQ = 2 * width, 2 * width + 1
+    V_B = lambda i: 2 * width + 2 + i
+    n = 0
+    c2.add(n, [(0, 1), (0, -1)], [(width, 1)], []); n += 1
+    c2.add(n, [(width, 1)], [(0, 1), (width + 2, -1), (2, 1)], [(1, 1)]); n += 1
+    c2.add(n, [(1, 1)], [(width + 2, 1), (2, -1)], []); n += 1
+    c2.add(n, [(V_EQ, 1)], [(V_EQ, 1)], [(V_EQ, 1)]); n += 1
+    for i in range(max_ts_width):
+        c2.add(n, [(V_B(i), 1)], [(V_B(i), 1)], [(V_B(i), 1)]); n += 1
+    c2.add(n, [(1, 1)], [(width + 5, 1), (5, -1)], [(V_EQ, 1)] + [(V_B(i), 1 << i) for i in range(max_ts_width)]); n += 1
+    c2.add(n, [(1, 1)], [(width + 4, 1)], [(V_D2, 1)]); n += 1
+    c2.add(n, [(V_D2, 1)], [(width + 3, 1), (3, -1)], []); n += 1
+    c2.add(n, [(0, 1), (1, -1)], [(width + 4, 1)], []); n += 1
+    inst = _instance_new(3, max_nc, ncons, 4 * width, [c0.A, c1.A, c2.A], [c0.B, c1.B, c2.B], [c0.C, c1.C, c2.C])
+    return width, max_nc, nnz, inst
+
+
+def gen_perm_root_inst(niu, num_vars):
+    """Instance::gen_perm_root_inst (src/instance.rs:1088-1327) -> (num_cons, nnz, inst)"""
+    V_tau = 0
+    V_r = lambda i: i
+    V_valid = V_cnst = num_vars
+    V_input = lambda i: num_vars + 2 + i
+    V_output = lambda i: num_vars + 2 + (niu - 1) + i
+    V_ZO = 2 * num_vars + 2
+    V_in_dp = lambda i: V_input(0) if i == 0 else 2 * num_vars + 2 + i
+    V_out_dp = lambda i: 2 * num_vars + 2 + (niu - 1) + i
+    V_v, V_x, V_pi, V_d, V_I, V_O = (3 * num_vars + k for k in range(6))
+    V_sv, V_spi = 4 * num_vars, 4 * num_vars + 2
+    k = _Constr()
+    n = 0
+    for i in range(1, niu - 1):
+        k.add(n, [(V_input(i), 1)], [(V_r(i), 1)], [(V_in_dp(i), 1)]); n += 1
+    for i in range(niu - 1):
+        k.add(n, [(V_output(i), 1)], [(V_r(i + niu - 1), 1)], [(V_out_dp(i), 1)]); n += 1
+    k.add(n, [(V_ZO, 1)], [(V_r(niu - 1), 1)], [(V_out_dp(i), 1) for i in range(niu - 1)]); n += 1
+    k.add(n, [(V_valid, 1)], [(V_cnst, 1)] + [(V_in_dp(i), 1) for i in range(niu - 1)], [(V_I, 1)]); n += 1
+    k.add(n, [(V_valid, 1)], [(V_valid, 1), (V_ZO, 1)], [(V_O, 1)]); n += 1
+    k.add(n, [], [], [(V_valid, 1), (V_v, -1)]); n += 1
+    k.add(n, [(V_tau, 1)] + [(V_in_dp(i), -1) for i in range(2 * niu - 2)], [(num_vars, 1)], [(V_x, 1)]); n += 1
+    k.add(n, [(V_x, 1)], [(V_spi, 1), (V_cnst, 1), (V_sv, -1)], [(V_d, 1)]); n += 1
+    k.add(n, [(V_v, 1)], [(V_d, 1)], [(V_pi, 1)]); n += 1
+    num_cons = 2 * niu + 4
+    nnz = 4 * niu + 5
+    inst = _instance_new(1, num_cons, [num_cons], 8 * num_vars, [k.A], [k.B], [k.C])
+    return num_cons, nnz, inst
+
+
+class SnarkWorkload:
+    """Inputs of SNARK::prove (src/lib.rs:971-1026) for a synthetic straight-line program (SURVEY.md 8d
+    configs 1 and 3): `num_blocks` block types executed round-robin, 2^log_proofs executions each, no memory
+    operations. Every execution k of block b = k mod num_blocks reads inputs (i0 = b, i1 = x_k, i2 = y_k) and
+    writes outputs (o0 = next block, o1 = x_k^(2^m), o2 = y_k) through a chain of m squarings in its private
+    variables, so the block, consistency and permutation instances are all satisfied. The instances are
+    built by restatements of Instance::gen_block_inst / gen_pairwise_check_inst / gen_perm_root_inst, and the
+    block constraints fill 2^log_cons rows after the permutation rows are added."""
+
+    NIU = 4  # num_inputs_unpadded: (v, _, i0, i1, i2 | o0, o1, o2) -> num_ios = 8
+
+    def __init__(self, num_blocks=2, log_cons=10, log_proofs=9, num_vars=1024, max_ts_width=2, seed=0x5350415254414E31):
+        niu = self.NIU
+        self.num_blocks = num_blocks
+        self.num_vars = num_vars
+        self.num_inputs_unpadded = niu
+        self.num_ios = 1 << (2 * niu - 1).bit_length()
+        io_width = 2 * niu
+        extra = (niu - 2) + (niu - 1) + 4 + 3 + 3
+        m = (1 << log_cons) - extra - 3
+        assert m >= 1 and io_width + m + 1 <= num_vars, "num_vars too small for the chain"
+        self.chain = m
+        # user constraints of every block (A, B, C lists of (col, int) per row)
+        V_in, V_out = (lambda i: 2 + i), (lambda i: 2 + (niu - 1) + i)
+        rows = [([(V_in(1), 1)], [(0, 1)], [(io_width, 1)])]
+        rows += [([(io_width + j - 1, 1)], [(io_width + j - 1, 1)], [(io_width + j, 1)]) for j in range(1, m + 1)]
+        rows += [([(io_width + m, 1)], [(0, 1)], [(V_out(1), 1)]), ([(V_in(2), 1)], [(0, 1)], [(V_out(2), 1)])]
+        args = [rows for _ in range(num_blocks)]
+        self.block_num_phy_ops = [0] * num_blocks
+        self.block_num_vir_ops = [0] * num_blocks
+        self.block_num_vars, self.block_max_num_cons, self.block_nnz, self.block_inst = gen_block_inst(
+            num_vars, args, niu, self.block_num_phy_ops, self.block_num_vir_ops)
+        self.max_ts_width = max_ts_width
+        self.mem_addr_ts_bits_size = 1 << (2 + max_ts_width - 1).bit_length()
+        (self.pairwise_num_vars, self.pairwise_max_num_cons, self.pairwise_nnz,
+         self.pairwise_inst) = gen_pairwise_check_inst(max_ts_width, self.mem_addr_ts_bits_size)
+        self.perm_root_num_cons, self.perm_root_nnz, self.perm_root_inst = gen_perm_root_inst(niu, self.num_ios)
+        # ---- execution trace
+        E = num_blocks << log_proofs
+        seeds, _ = random_fq(2, seed)
+        x, y = int(seeds[0]), int(seeds[1])
+        self.x0 = x
+        per_block = [[] for _ in range(num_blocks)]
+        exec_rows = []
+        for k in range(E):
+            b = k % num_blocks
+            nb = (k + 1) % num_blocks if k + 1 < E else num_blocks
+            chain = [x]
+            for _ in range(m):
+                chain.append(chain[-1] * chain[-1] % Q)
+            xo = chain[-1]
+            io = [1, 0, b, x, y, nb, xo, y]
+            exec_rows.append(io + [0] * (self.num_ios - len(io)))
+            row = io + chain + [0] * (num_vars - io_width - len(chain))
+            per_block[b].append(row)
+            x = xo
+        self.output = x
+        self.block_num_proofs = [len(r) for r in per_block]
+        self.block_max_num_proofs = max(self.block_num_proofs)
+        self.block_vars = [to_mont_limbs(np.array(r, dtype=object).reshape(-1)).reshape(len(r), num_vars, 4)
+                           for r in per_block]
+        self.consis_num_proofs = E
+        self.exec_inputs = to_mont_limbs(np.array(exec_rows, dtype=object).reshape(-1)).reshape(E, self.num_ios, 4)
+        self.input_block_num = 0
+        self.output_block_num = num_blocks
+        self.input_liveness = [False, False, True]
+        self.func_input_width = 1
+        self.input_offset = 1
+        self.output_offset = 2
+        self.input = to_mont_limbs([0, 0, self.x0])
+        self.output_mont = to_mont_limbs([self.output])[0]
+        self.output_exec_num = E - 1
+
+    @property
+    def total_constraints(self):
+        """N = sum_p Q_p * X_p after padding"""
+        npow = lambda v: 1 << max(0, (v - 1).bit_length())
+        return sum(npow(q) * c for q, c in zip(self.block_num_proofs, self.block_inst[2]))
+
+
+class CSnarkInstance(ctypes.Structure):
+    _fields_ = [("inst", CInstance), ("gens_num_cons", ctypes.c_size_t), ("gens_num_vars", ctypes.c_size_t),
+                ("gens_num_instances", ctypes.c_size_t), ("gens_num_nz_entries", ctypes.c_size_t)]
+
+
+class CSnarkInputs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_size_t) for n in ("input_block_num", "output_block_num")] + [
+        ("input_liveness", ctypes.c_void_p), ("input_len", ctypes.c_size_t)] + [
+        (n, ctypes.c_size_t) for n in ("func_input_width", "input_offset", "output_offset")] + [
+        ("input", ctypes.c_void_p), ("output", ctypes.c_void_p), ("output_exec_num", ctypes.c_size_t),
+        ("num_vars", ctypes.c_size_t), ("num_ios", ctypes.c_size_t), ("max_block_num_phy_ops", ctypes.c_size_t),
+        ("block_num_phy_ops", ctypes.POINTER(ctypes.c_size_t)), ("max_block_num_vir_ops", ctypes.c_size_t),
+        ("block_num_vir_ops", ctypes.POINTER(ctypes.c_size_t)), ("mem_addr_ts_bits_size", ctypes.c_size_t),
+        ("num_inputs_unpadded", ctypes.c_size_t), ("block_num_vars", ctypes.POINTER(ctypes.c_size_t)),
+        ("block_num_instances_bound", ctypes.c_size_t), ("block_max_num_proofs", ctypes.c_size_t),
+        ("block_num_proofs", ctypes.POINTER(ctypes.c_size_t))] + [
+        (n, ctypes.c_size_t) for n in ("consis_num_proofs", "total_num_init_phy_mem_accesses",
+                                       "total_num_init_vir_mem_accesses", "total_num_phy_mem_accesses",
+                                       "total_num_vir_mem_accesses")] + [
+        ("block_vars", ctypes.POINTER(ctypes.c_void_p))] + [
+        (n, ctypes.c_void_p) for n in ("exec_inputs", "init_phy_mems", "init_vir_mems", "addr_phy_mems",
+                                       "addr_vir_mems", "addr_ts_bits")]
+
+
+class SnarkViews:
+    """C views (include/spg.h spg_snark_inputs / spg_snark_instance) of a SnarkWorkload; keeps buffers alive."""
+
+    def __init__(self, wl):
+        self.keep = []
+
+        def arr(a, dt=np.uint64):
+            a = np.ascontiguousarray(a, dtype=dt)
+            self.keep.append(a)
+            return a.ctypes.data
+
+        def sz(v):
+            a = _sz(v)
+            self.keep.append(a)
+            return a
+
+        def inst(mats_tuple, gens):
+            mats, mnc, ncp, nvp = mats_tuple
+            n = len(mats)
+            ptrs = (ctypes.c_void_p * (3 * n))()
+            nnz = []
+            for p, m3 in enumerate(mats):
+                for k in range(3):
+                    ptrs[3 * p + k] = arr(m3[k]) if m3[k].shape[0] else None
+                    nnz.append(m3[k].shape[0])
+            self.keep.append(ptrs)
+            ci = CInstance(n, mnc, nvp, sz(ncp), sz(nnz), ptrs)
+            return CSnarkInstance(ci, *gens)
+
+        B = wl.num_blocks
+        self.block = inst(wl.block_inst, (wl.block_max_num_cons, wl.block_num_vars, B, wl.block_nnz))
+        self.pairwise = inst(wl.pairwise_inst, (wl.pairwise_max_num_cons, 4 * wl.pairwise_num_vars, 3, wl.pairwise_nnz))
+        self.perm_root = inst(wl.perm_root_inst, (wl.perm_root_num_cons, 8 * wl.num_ios, 1, wl.perm_root_nnz))
+        bv = (ctypes.c_void_p * B)(*[arr(v) for v in wl.block_vars])
+        self.keep.append(bv)
+        c = CSnarkInputs()
+        c.input_block_num, c.output_block_num = wl.input_block_num, wl.output_block_num
+        c.input_liveness = arr(np.array(wl.input_liveness, dtype=np.uint8), np.uint8)
+        c.input_len = len(wl.input_liveness)
+        c.func_input_width, c.input_offset, c.output_offset = wl.func_input_width, wl.input_offset, wl.output_offset
+        c.input = arr(wl.input)
+        c.output = arr(wl.output_mont)
+        c.output_exec_num = wl.output_exec_num
+        c.num_vars, c.num_ios = wl.num_vars, wl.num_ios
+        c.max_block_num_phy_ops = max(wl.block_num_phy_ops)
+        c.block_num_phy_ops = sz(wl.block_num_phy_ops)
+        c.max_block_num_vir_ops = max(wl.block_num_vir_ops)
+        c.block_num_vir_ops = sz(wl.block_num_vir_ops)
+        c.mem_addr_ts_bits_size = wl.mem_addr_ts_bits_size
+        c.num_inputs_unpadded = wl.num_inputs_unpadded
+        c.block_num_vars = sz([wl.num_vars] * B)
+        c.block_num_instances_bound = B
+        c.block_max_num_proofs = wl.block_max_num_proofs
+        c.block_num_proofs = sz(wl.block_num_proofs)
+        c.consis_num_proofs = wl.consis_num_proofs
+        c.block_vars = bv
+        c.exec_inputs = arr(wl.exec_inputs)
+        self.inputs = c

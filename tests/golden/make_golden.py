@@ -197,8 +197,28 @@ def spark_fixture():
     return out
 
 
+def snark_fixture():
+    """sha256 of bincode(SNARK) from the oracle's SNARK::prove, each after the oracle's verifier (three
+    R1CSProofs, three R1CSEvalProofs, permutation-product identity) accepted (tests/r1cs_cases.py SNARK_CASES)."""
+    sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import workload
+    from r1cs_cases import SNARK_CASES
+
+    out = {}
+    for name in sorted(SNARK_CASES):
+        wl = workload.SnarkWorkload(**SNARK_CASES[name])
+        proof, rc = O.snark_prove(wl, workload.tape_seed())
+        assert rc == 0, (name, rc)
+        out[name] = {"proof_sha256": hashlib.sha256(proof).hexdigest(), "proof_len": len(proof)}
+    return out
+
+
 def main():
     O.build()
+    if sys.argv[1:] == ["snark"]:
+        json.dump(snark_fixture(), open(os.path.join(HERE, "snark_proofs.json"), "w"), indent=1)
+        return
     if sys.argv[1:] == ["r1cs"]:
         json.dump(r1cs_fixture(), open(os.path.join(HERE, "r1cs_proofs.json"), "w"), indent=1)
         return
@@ -216,6 +236,7 @@ def main():
     w("msm_256.json", msm_fixture(lib, rng, b"spg_bench_msm", 256))
     w("r1cs_proofs.json", r1cs_fixture())
     w("spark_proofs.json", spark_fixture())
+    w("snark_proofs.json", snark_fixture())
     print("golden fixtures written to", HERE)
 
 

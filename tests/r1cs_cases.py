@@ -25,3 +25,14 @@ SPARK_CASES = {
 GPU_SPARK_CASES = {
     "p2_x4096": ([4096, 4096], [2, 2], 1, False),
 }
+
+# SNARK::prove cases (workload.SnarkWorkload kwargs): block types, 2^log_cons rows, 2^log_proofs executions each
+SNARK_CASES = {
+    "b2_x32_q2": dict(num_blocks=2, log_cons=5, log_proofs=1, num_vars=32),
+    "b3_x32_q4": dict(num_blocks=3, log_cons=5, log_proofs=2, num_vars=32),
+    "b2_x64_q8": dict(num_blocks=2, log_cons=6, log_proofs=3, num_vars=64),
+}
+GPU_SNARK_CASES = {
+    "b2_x1024_q8": dict(num_blocks=2, log_cons=10, log_proofs=3, num_vars=1024),
+    "b2_x256_q64": dict(num_blocks=2, log_cons=8, log_proofs=6, num_vars=256),
+}
