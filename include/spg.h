@@ -227,6 +227,25 @@ typedef struct {
   const uint64_t* addr_ts_bits;      /* total_num_vir_mem_accesses x mem_addr_ts_bits_size x 4 */
 } spg_snark_inputs;
 
+typedef struct spg_snark_comp spg_snark_comp; /* ComputationCommitment + ComputationDecommitment */
+typedef struct spg_snark_wit spg_snark_wit;   /* SNARK::prove run-time inputs, resident in HBM */
+
+/* SNARK::multi_encode (multi != 0: matrices grouped by next_power_of_eight(nnz), src/r1csinstance.rs:654-715)
+ * or SNARK::encode (one commitment over all 3P matrices, :717-737) of one instance, with
+ * SNARKGens::new(gens_num_cons, gens_num_vars, gens_num_instances, gens_num_nz_entries).gens_r1cs_eval
+ * (label "gens_r1cs_eval"). The dense representations stay in HBM. */
+int spg_snark_encode(spg_ctx* ctx, const spg_snark_instance* inst, int multi, spg_snark_comp** out);
+int spg_snark_comp_free(spg_ctx* ctx, spg_snark_comp* comp);
+/* Uploads block_vars and exec inputs to HBM (padded to powers of two) and keeps host copies of the parts the
+ * witness recurrences read. Block witness lists must be given in the sorted order (as in the reference). */
+int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* inputs, spg_snark_wit** out);
+int spg_snark_witness_free(spg_ctx* ctx, spg_snark_wit* wit);
+/* SNARK::prove (src/lib.rs:971-2746) with vars_gens (spg_r1cs_gens_new(label "gens_r1cs_sat", bound)).
+ * Writes bincode(SNARK) into proof (*proof_len = its size even when it does not fit). */
+int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_comp* pairwise, spg_snark_comp* perm_root,
+                    const spg_snark_wit* wit, spg_r1cs_gens* vars_gens, spg_transcript* transcript,
+                    spg_random_tape* tape, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -127,6 +127,36 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
 int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars, const std::vector<std::vector<uint32_t>>& idx,
                    std::vector<Pt>* out);
 
+// ---- Hyrax commitments / PolyEvalProof on device polynomials (spark.hip) ----
+// PolyCommitmentGens::new(nv, label) as a view of a derived generator stream
+ProverGens gens_view(spg_gens* dev, size_t nv);
+// DensePolynomial::commit (no blinds) of 2^nv device scalars; rows of 2^(nv - nv/2) <= g.n_pc scalars
+int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out);
+// PolyCommitment::append_to_transcript
+void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c);
+// PolyEvalProof::prove (no blinds) of a device polynomial of 2^|r| scalars
+int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, const Fq& Zr, Tr& t, Tape& tape,
+                    DotProductProofLogP* out);
+
+// ---- SPARK (spark.hip) ----
+struct SparsePoly {
+  const spg_sparse_entry* e;
+  size_t nnz;
+};
+int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_t nvx, size_t nvy,
+                       const uint8_t* label, size_t label_len, size_t gens_nvx, size_t gens_nvy, size_t gens_nnz,
+                       size_t gens_batch, spg_spark** out);
+void spark_comm_ser(const spg_spark* S, Writer& w);
+void spark_comm_append(const spg_spark* S, Tr& t);
+int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w);
+
+// ---- R1CS witness from parts (r1cs.hip) ----
+struct WPart {  // one ProverWitnessSecInfo: per instance (num_proofs x num_inputs) scalars at src (host or device)
+  std::vector<size_t> num_proofs, num_inputs;
+  std::vector<const Fq*> src;
+};
+int witness_from_parts(spg_ctx* ctx, const std::vector<WPart>& secs, spg_r1cs_witness** inout);
+
 }  // namespace spg
 
 // C-ABI handles of the Fiat-Shamir transcript and the prover random tape
@@ -137,4 +167,7 @@ struct spg_transcript {
 struct spg_random_tape {
   spg::Tape t;
   spg_random_tape(const char* n, const spg::Fq& s) : t(n, s) {}
+};
+struct spg_r1cs_gens {  // R1CSGens: one derived stream; gens_pc / gens_1 / gens_4 are views of it
+  spg::ProverGens g;
 };

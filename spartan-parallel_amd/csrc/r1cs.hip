@@ -18,9 +18,6 @@
 #include "proto.hpp"
 #include "sumcheck.hpp"
 
-struct spg_r1cs_gens {
-  spg::ProverGens g;
-};
 
 // R1CSInstance resident in HBM: per matrix instance p, CSR of A_p, B_p, C_p (SpMV) and one merged CSC
 // (rows tagged 0/1/2) for the transposed eq-weighted product.
@@ -1246,6 +1243,54 @@ static int witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, si
   *out = W;
   return SPG_OK;
 }
+namespace spg {
+// witness sections assembled from host or device parts (SNARK::prove's ProverWitnessSecInfo lists); an
+// existing *inout whose total size matches is refilled in place
+int witness_from_parts(spg_ctx* ctx, const std::vector<WPart>& secs, spg_r1cs_witness** inout) {
+  if (secs.empty() || secs.size() > 8) return set_err(ctx, SPG_E_ARG, "1..8 witness sections");
+  size_t total = 0;
+  for (auto& w : secs) {
+    if (w.num_proofs.empty() || w.num_proofs.size() != w.num_inputs.size() || w.src.size() != w.num_proofs.size())
+      return set_err(ctx, SPG_E_ARG, "witness part shape");
+    for (size_t p = 0; p < w.num_proofs.size(); p++) {
+      if (!is_pow2(w.num_proofs[p]) || !is_pow2(w.num_inputs[p]))
+        return set_err(ctx, SPG_E_ARG, "witness section sizes must be powers of two");
+      total += w.num_proofs[p] * w.num_inputs[p];
+    }
+  }
+  spg_r1cs_witness* W = *inout;
+  if (W && W->total < total) {
+    spg_r1cs_witness_free(ctx, W);
+    W = nullptr;
+  }
+  if (!W) {
+    W = new spg_r1cs_witness();
+    if (hipMalloc(&W->d_w, total * sizeof(Fq) + 64) != hipSuccess) {
+      delete W;
+      *inout = nullptr;
+      return set_err(ctx, SPG_E_NOMEM, "witness");
+    }
+    W->total = total;
+  }
+  *inout = W;
+  W->nws = secs.size();
+  W->num_proofs.assign(secs.size(), {});
+  W->num_inputs.assign(secs.size(), {});
+  W->off.assign(secs.size(), {});
+  size_t o = 0;
+  for (size_t w = 0; w < secs.size(); w++)
+    for (size_t p = 0; p < secs[w].num_proofs.size(); p++) {
+      size_t n = secs[w].num_proofs[p] * secs[w].num_inputs[p];
+      W->num_proofs[w].push_back(secs[w].num_proofs[p]);
+      W->num_inputs[w].push_back(secs[w].num_inputs[p]);
+      W->off[w].push_back(o);
+      SPG_HIP(ctx, hipMemcpyAsync(W->d_w + o, secs[w].src[p], n * sizeof(Fq), hipMemcpyDefault, ctx->stream));
+      o += n;
+    }
+  return 0;
+}
+}  // namespace spg
+
 extern "C" int spg_r1cs_witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, spg_r1cs_witness** out) {
   return witness_new(ctx, secs, nws, 0, ~(size_t)0, out);
 }

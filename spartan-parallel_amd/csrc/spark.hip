@@ -220,6 +220,7 @@ struct spg_spark {
   size_t comb_ops_len = 0, comb_mem_len = 0;
   spg_gens* dev = nullptr;
   ProverGens g_ops, g_mem, g_der;
+  std::vector<spg::Pt> comm_ops, comm_mem;  // SparseMatPolyCommitment
 };
 
 namespace spg {
@@ -233,7 +234,7 @@ enum : size_t {
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
-static ProverGens gens_view(spg_gens* dev, size_t nv) {
+ProverGens gens_view(spg_gens* dev, size_t nv) {
   ProverGens g;
   g.dev = dev;
   g.host.init(dev->compressed, dev->n + 1);
@@ -249,9 +250,9 @@ static ProverGens gens_view(spg_gens* dev, size_t nv) {
 
 // DensePolynomial::commit without blinds (dense_mlpoly.rs:181-216) of 2^nv device scalars: one MSM per
 // row of R = 2^(nv - nv/2) scalars, in chunks of rows that keep the MSM sort within 32-bit indices
-static int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out) {
+int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out) {
   size_t L = (size_t)1 << (nv / 2), R = (size_t)1 << (nv - nv / 2);
-  if (R != g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: polynomial size does not match its generators");
+  if (R > g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: polynomial size does not match its generators");
   out->resize(L);
   size_t chunk = std::max<size_t>(1, std::min<size_t>(L, ((size_t)1 << 24) / R));
   uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsCommit, 32 * chunk + 64);
@@ -266,20 +267,20 @@ static int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std
   return 0;
 }
 
-static void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c) {
+void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c) {
   t.msg(label, "poly_commitment_begin");
   for (auto& p : c) t.point("poly_commitment_share", p);
   t.msg(label, "poly_commitment_end");
 }
 
 // PolyEvalProof::prove without blinds (dense_mlpoly.rs:437-490) of a device polynomial of 2^|r| scalars
-static int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, const Fq& Zr, Tr& t, Tape& tape,
+int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, const Fq& Zr, Tr& t, Tape& tape,
                            DotProductProofLogP* out) {
   t.protocol("polynomial evaluation proof");
   size_t nv = r.size(), ln = nv / 2;
   FqV rl(r.begin(), r.begin() + ln), rr(r.begin() + ln, r.end());
   size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
-  if (Rs != g.n_pc) return set_err(ctx, SPG_E_ARG, "poly eval: size does not match the generators");
+  if (Rs > g.n_pc) return set_err(ctx, SPG_E_ARG, "poly eval: polynomial wider than the generators");
   FqV R = eq_evals_host(rr);
   size_t S = std::min<size_t>(Ls, std::max<size_t>(1, 8192 / nblk(Rs)));  // row splits to fill the chip
   size_t chunk = (Ls + S - 1) / S;
@@ -486,32 +487,34 @@ extern "C" int spg_spark_free(spg_ctx* ctx, spg_spark* S) {
   return SPG_OK;
 }
 
-extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const uint8_t* label, size_t label_len,
-                                size_t gens_nnz, size_t gens_batch, spg_spark** out, uint8_t* comm, size_t comm_cap,
-                                size_t* comm_len) {
-  if (!ctx || !ci || !label || !out || !comm_len || !ci->num_instances || !ci->nnz || !ci->entries) return SPG_E_ARG;
-  if (!is_pow2(ci->max_num_cons) || !is_pow2(ci->num_vars)) return set_err(ctx, SPG_E_ARG, "sizes must be powers of 2");
+namespace spg {
+
+// SparseMatPolynomial::multi_commit (sparse_mlpoly.rs:566-587) over `polys` (num_vars_x / num_vars_y of the
+// matrices) with SparseMatPolyCommitmentGens::new(label, gens_nvx, gens_nvy, gens_nnz, gens_batch)
+int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_t nvx, size_t nvy,
+                       const uint8_t* label, size_t label_len, size_t gens_nvx, size_t gens_nvy, size_t gens_nnz,
+                       size_t gens_batch, spg_spark** out) {
+  if (!ctx || polys.empty() || !label || !out) return SPG_E_ARG;
   hipStream_t s = ctx->stream;
-  const size_t B = 3 * ci->num_instances;
+  const size_t B = polys.size();
   size_t N = 2;
-  for (size_t k = 0; k < B; k++) N = std::max(N, npow2(ci->nnz[k]));
-  const size_t nvx = lg2(ci->max_num_cons), nvy = lg2(ci->num_vars);
+  for (auto& p : polys) N = std::max(N, npow2(p.nnz));
   const size_t cells = (size_t)1 << std::max<size_t>(std::max(nvx, nvy), 1);
   if (2 * B * N >= 0xffffffffULL || cells > 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "SPARK batch too large");
   // SparseMatPolyCommitmentGens::new (sparse_mlpoly.rs:289-317)
   const size_t nv_ops = lg2(npow2(gens_nnz)) + lg2(npow2(gens_batch * 5));
-  const size_t nv_mem = std::max(nvx, nvy) + 1;
+  const size_t nv_mem = std::max(gens_nvx, gens_nvy) + 1;
   const size_t nv_der = lg2(npow2(gens_nnz)) + lg2(npow2(gens_batch * 2));
   const size_t ops_len = npow2(5 * B * N);
-  if (lg2(ops_len) != nv_ops || lg2(npow2(2 * B * N)) != nv_der)
-    return set_err(ctx, SPG_E_ARG, "SPARK generators (gens_nnz, gens_batch) do not match the batch");
+  if (lg2(ops_len) > nv_ops || lg2(npow2(2 * B * N)) > nv_der || std::max(nvx, nvy) + 1 > nv_mem)
+    return set_err(ctx, SPG_E_ARG, "SPARK generators (gens_nnz, gens_batch) too small for the batch");
   // AddrTimestamps::new (sparse_mlpoly.rs:219-253): read / audit timestamps are a sequential scan (host)
   std::vector<uint32_t> addr(2 * B * N, 0), rts(2 * B * N, 0), audit(2 * cells, 0);
   std::vector<Fq> val(B * N, fq_zero());
   for (size_t k = 0; k < B; k++) {
-    const spg_sparse_entry* E = ci->entries[k];
-    if (ci->nnz[k] && !E) return SPG_E_ARG;
-    for (size_t i = 0; i < ci->nnz[k]; i++) {
+    const spg_sparse_entry* E = polys[k].e;
+    if (polys[k].nnz && !E) return SPG_E_ARG;
+    for (size_t i = 0; i < polys[k].nnz; i++) {
       if (E[i].row >= ((uint64_t)1 << nvx) || E[i].col >= ((uint64_t)1 << nvy))
         return set_err(ctx, SPG_E_ARG, "sparse entry outside the matrix");
       addr[k * N + i] = (uint32_t)E[i].row;
@@ -576,12 +579,44 @@ extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const
     spg_spark_free(ctx, S);
     return rc;
   }
-  Writer w;  // SparseMatPolyCommitment (sparse_mlpoly.rs:319-325)
-  w.u64(B);
-  w.u64(N);
-  w.u64(cells);
-  w.pts(comm_ops);
-  w.pts(comm_mem);
+  S->comm_ops = comm_ops;
+  S->comm_mem = comm_mem;
+  *out = S;
+  return SPG_OK;
+}
+
+// bincode(SparseMatPolyCommitment) (sparse_mlpoly.rs:319-325)
+void spark_comm_ser(const spg_spark* S, Writer& w) {
+  w.u64(S->B);
+  w.u64(S->N);
+  w.u64(S->cells);
+  w.pts(S->comm_ops);
+  w.pts(S->comm_mem);
+}
+// SparseMatPolyCommitment::append_to_transcript (sparse_mlpoly.rs:327-339)
+void spark_comm_append(const spg_spark* S, Tr& t) {
+  t.u64("batch_size", S->B);
+  t.u64("num_ops", S->N);
+  t.u64("num_mem_cells", S->cells);
+  append_polycomm(t, "comm_comb_ops", S->comm_ops);
+  append_polycomm(t, "comm_comb_mem", S->comm_mem);
+}
+
+}  // namespace spg
+
+extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const uint8_t* label, size_t label_len,
+                                size_t gens_nnz, size_t gens_batch, spg_spark** out, uint8_t* comm, size_t comm_cap,
+                                size_t* comm_len) {
+  if (!ctx || !ci || !label || !out || !comm_len || !ci->num_instances || !ci->nnz || !ci->entries) return SPG_E_ARG;
+  if (!is_pow2(ci->max_num_cons) || !is_pow2(ci->num_vars)) return set_err(ctx, SPG_E_ARG, "sizes must be powers of 2");
+  std::vector<SparsePoly> polys;
+  for (size_t k = 0; k < 3 * ci->num_instances; k++) polys.push_back({ci->entries[k], ci->nnz[k]});
+  const size_t nvx = lg2(ci->max_num_cons), nvy = lg2(ci->num_vars);
+  spg_spark* S = nullptr;
+  int rc = spark_commit_polys(ctx, polys, nvx, nvy, label, label_len, nvx, nvy, gens_nnz, gens_batch, &S);
+  if (rc) return rc;
+  Writer w;
+  spark_comm_ser(S, w);
   *comm_len = w.out.size();
   *out = S;
   if (!comm || w.out.size() > comm_cap) return set_err(ctx, SPG_E_ARG, "commitment buffer too small");
@@ -589,20 +624,13 @@ extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const
   return SPG_OK;
 }
 
-extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
-                               size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
-                               spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
-  if (!ctx || !S || !transcript || !tape_h || !proof_len || (!rx && rx_len) || (!ry && ry_len) || !evals_in)
-    return SPG_E_ARG;
-  if (n_evals != S->B) return set_err(ctx, SPG_E_ARG, "one evaluation per batched matrix");
+namespace spg {
+
+// SparseMatPolyEvalProof::prove (sparse_mlpoly.rs:1497-1564); appends bincode(proof) to w
+int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w) {
+  if (evals.size() != S->B) return set_err(ctx, SPG_E_ARG, "one evaluation per batched matrix");
   hipStream_t s = ctx->stream;
-  Tr& t = transcript->t;
-  Tape& tape = tape_h->t;
   const size_t B = S->B, N = S->N, BN = B * N, cells = S->cells, hN = N / 2;
-  FqV ex, ey, evals(n_evals);
-  for (size_t i = 0; i < rx_len; i++) ex.push_back(ld_fq(rx + 4 * i));
-  for (size_t i = 0; i < ry_len; i++) ey.push_back(ld_fq(ry + 4 * i));
-  for (size_t i = 0; i < n_evals; i++) evals[i] = ld_fq(evals_in + 4 * i);
   if (ex.size() < ey.size()) ex.insert(ex.begin(), ey.size() - ex.size(), fq_zero());
   if (ey.size() < ex.size()) ey.insert(ey.begin(), ex.size() - ey.size(), fq_zero());
   if (ex.size() > 40 || ((size_t)1 << ex.size()) != cells)
@@ -762,7 +790,6 @@ extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, s
   }
   timer_stop(ctx);
   // ---- bincode(SparseMatPolyEvalProof)
-  Writer w;
   w.pts(comm_derefs);
   w.fq(row_init);  // ProductLayerProof
   w.fqs(row_read);
@@ -789,10 +816,27 @@ extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, s
   pf_ops.ser(w);
   pf_mem.ser(w);
   pf_der.ser(w);
-  *proof_len = w.out.size();
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
   ctx->last_us = ms * 1000.0;
+  return SPG_OK;
+}
+
+}  // namespace spg
+
+extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                               size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
+                               spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  if (!ctx || !S || !transcript || !tape_h || !proof_len || (!rx && rx_len) || (!ry && ry_len) || !evals_in)
+    return SPG_E_ARG;
+  FqV ex, ey, evals(n_evals);
+  for (size_t i = 0; i < rx_len; i++) ex.push_back(ld_fq(rx + 4 * i));
+  for (size_t i = 0; i < ry_len; i++) ey.push_back(ld_fq(ry + 4 * i));
+  for (size_t i = 0; i < n_evals; i++) evals[i] = ld_fq(evals_in + 4 * i);
+  Writer w;
+  int rc = spark_prove_core(ctx, S, ex, ey, evals, transcript->t, tape_h->t, w);
+  if (rc) return rc;
+  *proof_len = w.out.size();
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, w.out.data(), w.out.size());
   return SPG_OK;

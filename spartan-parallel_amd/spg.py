@@ -460,3 +460,58 @@ class SparkCommitment:
                 self._h = ctypes.c_void_p()
         except Exception:
             pass
+
+
+class SnarkComp:
+    """SNARK::multi_encode (multi=True) / SNARK::encode of one R1CS instance (src/lib.rs:793-829); `cinst` is a
+    workload.SnarkViews().block / .pairwise / .perm_root (spg_snark_instance)."""
+
+    def __init__(self, ctx, cinst, multi=False):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        ctx.check(lib().spg_snark_encode(ctx.handle, ctypes.byref(cinst), ctypes.c_int(1 if multi else 0),
+                                         ctypes.byref(self._h)), "spg_snark_encode")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_snark_comp_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+class SnarkWitness:
+    """SNARK::prove's run-time inputs with block_vars / exec inputs resident in HBM (workload.SnarkViews().inputs)"""
+
+    def __init__(self, ctx, cinputs):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        ctx.check(lib().spg_snark_witness_new(ctx.handle, ctypes.byref(cinputs), ctypes.byref(self._h)),
+                  "spg_snark_witness_new")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_snark_witness_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+def snark_prove(ctx, block, pairwise, perm_root, witness, vars_gens, transcript, tape, cap=1 << 24):
+    """SNARK::prove (src/lib.rs:971-2746) -> bincode(SNARK)"""
+    buf = np.zeros(cap, dtype=np.uint8)
+    ln = ctypes.c_size_t(0)
+    ctx.check(lib().spg_snark_prove(ctx.handle, block.handle, pairwise.handle, perm_root.handle, witness.handle,
+                                    vars_gens.handle, transcript.handle, tape.handle, _p(buf), ctypes.c_size_t(cap),
+                                    ctypes.byref(ln)), "spg_snark_prove")
+    return buf[: ln.value].tobytes()

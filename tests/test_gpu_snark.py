@@ -1,0 +1,71 @@
+"""SNARK::prove on the GPU (libspg.so: spg_snark_encode / spg_snark_witness_new / spg_snark_prove) vs the CPU
+oracle: identical bincode(SNARK) under the same transcript label and RandomTape seed. Small cases are pinned by
+tests/golden/snark_proofs.json (oracle proofs its verifier accepted); the larger ones run the oracle live."""
+import hashlib
+import json
+import os
+
+import pytest
+
+from r1cs_cases import GPU_SNARK_CASES, SNARK_CASES
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+GENS_LABEL = b"gens_r1cs_sat"
+GENS_NV = 1 << 24
+
+
+@pytest.fixture(scope="module")
+def vars_gens(ctx):
+    import spg
+
+    return spg.R1CSGens(ctx, GENS_LABEL, GENS_NV)
+
+
+def gpu_snark(ctx, vars_gens, wl, seed, label=b"snark_test", repeat=1):
+    import spg
+    import workload
+
+    v = workload.SnarkViews(wl)
+    block = spg.SnarkComp(ctx, v.block, multi=True)
+    pairwise = spg.SnarkComp(ctx, v.pairwise)
+    perm_root = spg.SnarkComp(ctx, v.perm_root)
+    wit = spg.SnarkWitness(ctx, v.inputs)
+    out = []
+    for _ in range(repeat):
+        out.append(spg.snark_prove(ctx, block, pairwise, perm_root, wit, vars_gens, spg.Transcript(label),
+                                   spg.RandomTape(b"proof", seed)))
+    return out
+
+
+def _check(got, ref):
+    if got != ref:
+        from proof_layout import first_diff_snark
+
+        where = first_diff_snark(got, ref) if len(got) == len(ref) else f"length {len(got)} vs {len(ref)}"
+        pytest.fail(f"SNARK bytes differ first at {where}")
+
+
+@pytest.mark.parametrize("case", sorted(SNARK_CASES))
+def test_snark_matches_golden(ctx, oracle, vars_gens, case):
+    import workload
+
+    wl = workload.SnarkWorkload(**SNARK_CASES[case])
+    (proof,) = gpu_snark(ctx, vars_gens, wl, workload.tape_seed())
+    golden = json.load(open(os.path.join(G, "snark_proofs.json")))[case]
+    if hashlib.sha256(proof).hexdigest() != golden["proof_sha256"]:
+        ref, rc = oracle.snark_prove(wl, workload.tape_seed())
+        assert rc == 0
+        _check(proof, ref)
+
+
+@pytest.mark.parametrize("case", sorted(GPU_SNARK_CASES))
+def test_snark_matches_oracle_large(ctx, oracle, vars_gens, case):
+    import workload
+
+    wl = workload.SnarkWorkload(**GPU_SNARK_CASES[case])
+    a, b = gpu_snark(ctx, vars_gens, wl, workload.tape_seed(), repeat=2)
+    assert a == b, "proof not repeatable"
+    ref, rc = oracle.snark_prove(wl, workload.tape_seed())
+    assert rc == 0
+    _check(a, ref)
