@@ -12,6 +12,8 @@
 // plus a verifier of the pieces that carry the argument's soundness (the three R1CSProofs with their
 // R1CSEvalProofs and the permutation-product identity), replaying SNARK::prove's transcript.
 #pragma once
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <map>
 #include <vector>
@@ -395,6 +397,13 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   SnarkIn in = in0;
   SNARKProof pf;
   t.append_protocol_name("Spartan SNARK proof");
+  const bool dbg0 = getenv("SPG_DEBUG_SNARK") != nullptr;
+  auto fp = [&](const char* where) {
+    if (!dbg0) return;
+    Transcript c = t;
+    Fq x = c.challenge_scalar("dbg");
+    fprintf(stderr, "fp %s %08x\n", where, (uint32_t)x.v[0]);
+  };
   const size_t niu = in.num_inputs_unpadded, num_ios = in.num_ios, io_width = 2 * niu;
   const DotGens& gpc = vars_gens.gens_pc;
   Fq input_block_num = fq_from_u64(in.input_block_num), output_block_num = fq_from_u64(in.output_block_num);
@@ -418,11 +427,16 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   app("total_num_vir_mem_accesses", in.total_num_vir_mem_accesses);
   app("block_max_num_proofs", in.block_max_num_proofs);
   for (auto n : in.block_num_proofs) app("block_num_proofs", n);
+  fp("params");
   for (auto& b : block.label_map)
     for (auto l : b) app("block_comm_map", l);
+  fp("map");
   for (auto& c : block.comms) c.append(t);
+  fp("block");
   pairwise.comms[0].append(t);
+  fp("pairwise");
   perm_root.comms[0].append(t);
+  fp("perm_root");
   t.append_scalar("input_block_num", input_block_num);
   t.append_scalar("output_block_num", output_block_num);
   t.append_scalars("input_list", in.input);
@@ -496,6 +510,8 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   // ---- WITNESS GEN: block (lib.rs:1299-1741)
   Fq comb_tau = t.challenge_scalar("challenge_tau");
   Fq comb_r = t.challenge_scalar("challenge_r");
+  const bool dbg = getenv("SPG_DEBUG_SNARK") != nullptr;
+  if (dbg) fprintf(stderr, "snark tau %08x %08x r %08x\n", (uint32_t)comb_tau.v[0], (uint32_t)(comb_tau.v[0] >> 32), (uint32_t)comb_r.v[0]);
   FqVec perm_w0 = {comb_tau};
   {
     Fq rt = comb_r;
@@ -540,6 +556,9 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
     w[2] = fq_mul(w[0], w[3]);
     perm_exec_w3[q] = w;
   }
+  if (dbg)
+    for (size_t q = 0; q < 2; q++)
+      for (size_t i = 0; i < num_ios; i++) fprintf(stderr, "pe_w2[%zu][%zu] %08x\n", q, i, (uint32_t)perm_exec_w2[q][i].v[0]);
   DensePoly perm_exec_poly_w2(flatten(perm_exec_w2)), perm_exec_poly_w3(flatten(perm_exec_w3));
   std::vector<FqVec> perm_exec_w3s = shift_rows(perm_exec_w3, 8);
   DensePoly perm_exec_poly_w3s(flatten(perm_exec_w3s));

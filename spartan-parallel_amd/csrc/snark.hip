@@ -11,6 +11,9 @@
 //     perm product, shift and IO PolyEvalProofs            lib.rs:2534-2693, 187-446    host bound + device Bullet
 // The host side is the transcript, the small witness recurrences and the bincode writer; every O(N) table
 // (block_vars, Az/Bz/Cz, SPARK dense representations) lives in HBM.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "hostpoly.hpp"
@@ -587,6 +590,13 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   const size_t Bb = a.block_num_instances_bound;
   if (2 * niu > num_ios) return set_err(ctx, SPG_E_ARG, "num_ios < 2 * num_inputs_unpadded");
   t.protocol("Spartan SNARK proof");
+  const bool dbg0 = getenv("SPG_DEBUG_SNARK") != nullptr;
+  auto fp = [&](const char* where) {
+    if (!dbg0) return;
+    Tr c = t;
+    Fq x = c.challenge("dbg");
+    fprintf(stderr, "fp %s %08x\n", where, x.l[0]);
+  };
   // ---- INSTANCE COMMITMENTS (lib.rs:1086-1153)
   auto app = [&](const char* l, size_t v) { t.scalar(l, fq_from_u64(v)); };
   app("func_input_width", a.func_input_width);
@@ -607,11 +617,16 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   app("total_num_vir_mem_accesses", a.total_num_vir_mem_accesses);
   app("block_max_num_proofs", a.block_max_num_proofs);
   for (size_t b = 0; b < Bb; b++) app("block_num_proofs", W->nproofs[b]);
+  fp("params");
   for (auto& lm : block->label_map)
     for (auto l : lm) app("block_comm_map", l);
+  fp("map");
   for (size_t gi = 0; gi < block->sparks.size(); gi++) append_r1cs_comm(block, gi, t);
+  fp("block");
   append_r1cs_comm(pairwise, 0, t);
+  fp("pairwise");
   append_r1cs_comm(perm_root, 0, t);
+  fp("perm_root");
   const Fq input_block_num = fq_from_u64(a.input_block_num), output_block_num = fq_from_u64(a.output_block_num);
   t.scalar("input_block_num", input_block_num);
   t.scalar("output_block_num", output_block_num);
@@ -666,6 +681,8 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
 
   // ---- WITNESS GEN: block (lib.rs:1299-1741)
   const Fq tau = t.challenge("challenge_tau"), r = t.challenge("challenge_r");
+  const bool dbg = getenv("SPG_DEBUG_SNARK") != nullptr;
+  if (dbg) fprintf(stderr, "snark tau %08x %08x r %08x\n", tau.l[0], tau.l[1], r.l[0]);
   FqV perm_w0 = {tau};
   {
     Fq rt = r;
@@ -711,6 +728,9 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   std::vector<Rows> pe_w2v = {pe_w2}, pe_w3v = {pe_w3}, pe_w3sv = {shift_rows(pe_w3, 8)};
   std::vector<FqV> pe_p2 = {pad_pow2(flatten(pe_w2))}, pe_p3 = {pad_pow2(flatten(pe_w3))},
                    pe_p3s = {pad_pow2(flatten(pe_w3sv[0]))};
+  if (dbg)
+    for (size_t q = 0; q < 2; q++)
+      for (size_t i = 0; i < num_ios; i++) fprintf(stderr, "pe_w2[%zu][%zu] %08x\n", q, i, pe_w2[q][i].l[0]);
   std::vector<Pt> c_pe2, c_pe3, c_pe3s;
   if ((rc = commit_host(ctx, g, pe_p2[0], &c_pe2))) return rc;
   append_polycomm(t, "poly_commitment", c_pe2);

@@ -573,8 +573,8 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
   S->g_mem = gens_view(S->dev, nv_mem);
   S->g_der = gens_view(S->dev, nv_der);
   std::vector<Pt> comm_ops, comm_mem;
-  rc = commit_dev(ctx, S->g_ops, S->d_comb_ops, nv_ops, &comm_ops);
-  if (!rc) rc = commit_dev(ctx, S->g_mem, S->d_comb_mem, nv_mem, &comm_mem);
+  rc = commit_dev(ctx, S->g_ops, S->d_comb_ops, lg2(S->comb_ops_len), &comm_ops);
+  if (!rc) rc = commit_dev(ctx, S->g_mem, S->d_comb_mem, lg2(S->comb_mem_len), &comm_mem);
   if (rc) {
     spg_spark_free(ctx, S);
     return rc;
