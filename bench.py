@@ -50,8 +50,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="replicas", choices=["replicas", "shard"])
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
-    ap.add_argument("--workload", default="r1cs", choices=["r1cs", "spark"],
-                    help="r1cs: the headline metric (R1CSProof::prove); spark: SURVEY 8d config 5 (SPARK)")
+    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark"],
+                    help="snark: the headline metric (SNARK::prove, SURVEY 8d config 3); r1cs: its block "
+                         "R1CSProof::prove alone; spark: SURVEY 8d config 5 (SPARK)")
+    ap.add_argument("--log-cons", type=int, default=10, help="snark: 2^k constraints per block")
+    ap.add_argument("--log-proofs", type=int, default=9, help="snark: 2^k executions per block")
     ap.add_argument("--log-nnz", type=int, default=24, help="spark: 2^k nonzeros per matrix (x3 matrices)")
     ap.add_argument("--cpu-log-nnz", type=int, default=15, help="spark: CPU baseline sample size")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
@@ -63,6 +66,8 @@ def main():
     a = parse()
     if a.workload == "spark":
         return main_spark(a)
+    if a.workload == "snark":
+        return main_snark(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -216,6 +221,116 @@ def roofline_of(prof, traffic_file):
     return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "algorithmic_bytes_per_launch": nbytes / launches, "avg_launch_us": us / launches, "launches": launches}
+
+
+def main_snark(a):
+    """The headline metric (SURVEY 8d config 3): SNARK::prove (src/lib.rs:971-2746) on the synthetic program of
+    workload.SnarkWorkload: 2 block types x 2^log_proofs executions x 2^log_cons constraints (N = 2^20 by
+    default), no memory operations, vars_gens = R1CSGens(gens_r1cs_sat, 2^24). A step is one full SNARK::prove
+    (witness recurrences, every Hyrax commitment, the block / pairwise / perm-root R1CSProofs with their
+    R1CSEvalProofs, perm-product, shift and IO proofs) with the instances encoded (SNARK::encode, preprocessing)
+    and block_vars / exec inputs resident in HBM. Multi-GPU: independent replicas (one SNARK per rank)."""
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(a.backend or ("nccl" if torch.cuda.is_available() else "gloo"))
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if ndev else local
+    if torch.cuda.is_available():
+        torch.cuda.set_device(gpu)
+    import spg
+    import workload
+
+    ctx = spg.Context(gpu)
+    t0 = time.perf_counter()
+    wl = workload.SnarkWorkload(num_blocks=2, log_cons=a.log_cons, log_proofs=a.log_proofs,
+                                num_vars=1 << a.log_cons, seed=0x5350415254414E31 + rank)
+    views = workload.SnarkViews(wl)
+    t_gen = time.perf_counter() - t0
+    seed = workload.tape_seed()
+    gens = spg.R1CSGens(ctx, GENS_LABEL, GENS_NUM_VARS)
+    t0 = time.perf_counter()
+    block = spg.SnarkComp(ctx, views.block, multi=True)
+    pairwise = spg.SnarkComp(ctx, views.pairwise)
+    perm_root = spg.SnarkComp(ctx, views.perm_root)
+    t_encode = time.perf_counter() - t0
+    wit = spg.SnarkWitness(ctx, views.inputs)
+
+    def step():
+        return spg.snark_prove(ctx, block, pairwise, perm_root, wit, gens, spg.Transcript(b"snark_bench"),
+                               spg.RandomTape(b"proof", seed))
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    sync()
+    ctx.prof_enable(True)
+    ctx.prof_read(reset=True)
+    sync()
+    t0 = time.perf_counter()
+    proofs = set()
+    for _ in range(a.steps):
+        proofs.add(hashlib.sha256(step()).hexdigest())
+    sync()
+    dt = time.perf_counter() - t0
+    prof = ctx.prof_read(reset=True)
+    ctx.prof_enable(False)
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    assert len(proofs) == 1, "proof bytes changed between steps"
+    t1 = time.perf_counter()  # PCIe-inclusive variant: witness upload + prove (reported beside value)
+    wit = spg.SnarkWitness(ctx, views.inputs)
+    step()
+    t_incl = time.perf_counter() - t1
+    N = wl.total_constraints
+    value = N * world * a.steps / dt
+    top = sorted(prof.items(), key=lambda kv: -kv[1][1])[:10]
+    kernels = {n: {"launches_per_step": v[0] / a.steps, "ms_per_step": round(v[1] / a.steps / 1e3, 3),
+                   "GBps": round(v[2] / (v[1] * 1e-6) / 1e9, 1) if v[2] else None} for n, v in top}
+    cpu, bitexact = None, None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle  # the checker / CPU baseline only
+
+        pyoracle.build()
+        ref, rc = pyoracle.snark_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS,
+                                       label=b"snark_bench")
+        tcpu = pyoracle.snark_last_prove_us() * 1e-6
+        cpu = {"value": round(N / tcpu, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
+               "sample": f"full workload ({N} constraints), one SNARK::prove (instances pre-encoded), "
+                         f"{tcpu:.2f} s on 1 host thread; oracle verifier status {rc}"}
+        bitexact = hashlib.sha256(ref).hexdigest() in proofs
+    if rank == 0:
+        print(json.dumps({
+            "metric": "R1CS constraints/sec (SNARK::prove) at 2^20 vars; proof bytes bit-exact",
+            "value": round(value, 1), "unit": "constraints/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255",
+            "data": "synthetic program (2 block types, chain-of-squarings blocks, seeded), random-tape seed fixed",
+            "config": {"workload": "SNARK::prove (src/lib.rs:971-2746)", "block_types": 2,
+                       "constraints_per_block": 1 << a.log_cons, "executions_per_block": 1 << a.log_proofs,
+                       "constraints_per_gpu": N, "num_vars": wl.num_vars, "num_ios": wl.num_ios,
+                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{world}"},
+            "roofline": roofline_of(prof, a.traffic), "cpu_baseline": cpu, "proof_bitexact_vs_cpu": bitexact,
+            "proof_sha256": sorted(proofs)[0][:16], "proof_bytes": None,
+            "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
+            "value_incl_witness_upload": round(N * world / t_incl, 1), "encode_s": round(t_encode, 3),
+            "host_gen_s": round(t_gen, 3), "kernels": kernels}))
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def main_spark(a):
