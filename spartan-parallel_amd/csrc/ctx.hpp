@@ -91,6 +91,10 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
 int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, Ext* d_out, const uint32_t* d_idx, long h_index);
 
+// the latency path for many small rows (Hyrax rows of <= ~1K scalars): compressed outputs, d_out: B x 32 (device)
+int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                         uint8_t* d_out);
+
 // per-kernel profiling scope (no-op unless spg_prof_enable(ctx, 1))
 struct KScope {
   spg_ctx* c;

@@ -1,6 +1,11 @@
 // spg — small host-side helpers shared by the prover drivers (r1cs.hip, spark.hip): sizes, eq tables,
 // round polynomials, scalar (de)serialisation at the C-ABI.
 #pragma once
+#include <chrono>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string>
+#include <vector>
 #include <string.h>
 
 #include <vector>
@@ -91,5 +96,32 @@ inline bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
 inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 inline int eq_table(spg_ctx* ctx, const FqV& r, Fq* out) { return dev_eq_table(ctx, r.data(), (int)r.size(), out); }
+
+struct Laps {  // SPG_TRACE=1: wall-time breakdown of a host orchestration
+  const char* title = "R1CSProof::prove";
+  bool on = getenv("SPG_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::vector<std::pair<std::string, double>> acc;
+  void lap(const char* name) {
+    if (!on) return;
+    auto now = std::chrono::steady_clock::now();
+    double us = std::chrono::duration<double, std::micro>(now - t).count();
+    t = now;
+    for (auto& a : acc)
+      if (a.first == name) {
+        a.second += us;
+        return;
+      }
+    acc.push_back({name, us});
+  }
+  void print() {
+    if (!on) return;
+    double tot = 0;
+    for (auto& a : acc) tot += a.second;
+    fprintf(stderr, "[spg] %s host breakdown (us):", title);
+    for (auto& a : acc) fprintf(stderr, " %s=%.0f", a.first.c_str(), a.second);
+    fprintf(stderr, " total=%.0f\n", tot);
+  }
+};
 
 }  // namespace spg

@@ -262,19 +262,19 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
 // `blinds` must be a valid pointer even when has_blind == 0: blinds[b] has a wave-uniform address, so
 // the compiler issues it as a scalar load inside a divergent branch, and scalar loads are not masked
 // by EXEC when the branch is skipped (a null pointer there faults).
-template <int C>
-__global__ void __launch_bounds__(256) k_smsm_bucket(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
+template <int C, int BS>
+__global__ void __launch_bounds__(BS) k_smsm_bucket(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
                                                      const Fq* __restrict__ blinds, int has_blind, int n, int n1,
                                                      int gen_offset, int h_index, const Niels* __restrict__ tab,
                                                      Ext* __restrict__ buckets) {
   constexpr int W = 253 / C + 1;
   constexpr int NB = 1 << (C - 1);
   constexpr uint32_t MASK = (1u << C) - 1u;
-  __shared__ Ext sh[256];
+  __shared__ Ext sh[BS];
   const int v = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x;
   const int per = n + has_blind;
   Ext acc = ext_identity();
-  for (int i = t; i < per; i += 256) {
+  for (int i = t; i < per; i += BS) {
     Fq s;
     uint32_t gidx;
     if (i < n) {
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(256) k_smsm_bucket(const Fq* __restrict__ scal
       acc = ext_madd(acc, tab[(size_t)(w * C) * n1 + gidx], (neg >> w) & 1);
     }
   }
-  for (int d = 128; d >= 1; d >>= 1) {
+  for (int d = BS / 2; d >= 1; d >>= 1) {
     sh[t] = acc;
     __syncthreads();
     if (t < d) acc = ext_add(acc, sh[t + d]);
@@ -355,9 +355,19 @@ static void launch_small(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const 
                          Ext* bk, Ext* out, int B, hipStream_t s) {
   constexpr int NB = 1 << (C - 1);
   {
+    // threads per block = the scalars of one MSM rounded up (a smaller LDS tree and more resident blocks)
     KScope ks(ctx, "msm_small_bucket");
-    hipLaunchKernelGGL(k_smsm_bucket<C>, dim3(NB, B), dim3(256), 0, s, sc, idx, bl ? bl : sc, bl ? 1 : 0, n, n1, off,
-                       h, tab, bk);
+    const int per = n + (bl ? 1 : 0);
+    const Fq* blp = bl ? bl : sc;
+    if (per <= 64)
+      hipLaunchKernelGGL((k_smsm_bucket<C, 64>), dim3(NB, B), dim3(64), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
+                         tab, bk);
+    else if (per <= 128)
+      hipLaunchKernelGGL((k_smsm_bucket<C, 128>), dim3(NB, B), dim3(128), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off,
+                         h, tab, bk);
+    else
+      hipLaunchKernelGGL((k_smsm_bucket<C, 256>), dim3(NB, B), dim3(256), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off,
+                         h, tab, bk);
   }
   KScope ks(ctx, "msm_small_final");
   hipLaunchKernelGGL(k_smsm_final, dim3(B), dim3(NB), 0, s, bk, NB, out);
@@ -382,6 +392,41 @@ int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
     default: launch_small<9>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, bk, d_out, (int)B, s); break;
   }
   SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+// ext_compress of every point (RFC 9496 ENCODE), one lane per point
+__global__ void k_compress_ext(const Ext* __restrict__ in, size_t n, uint8_t* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) ext_compress(in[i], out + 32 * i);
+}
+
+// B MSMs of n scalars (rows of a Hyrax commitment) through the latency path, compressed on the device
+int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                         uint8_t* d_out) {
+  Ext* d_ext = (Ext*)ws_get(ctx, 15, B * sizeof(Ext) + 64);
+  if (!d_ext) return set_err(ctx, SPG_E_NOMEM, "small msm output");
+  static const bool trace3 = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 3;
+  hipEvent_t e[3];
+  if (trace3) {
+    for (auto& x : e) hipEventCreate(&x);
+    hipEventRecord(e[0], ctx->stream);
+  }
+  int rc = msm_small_device(ctx, g, gen_offset, d_scalars, n, B, nullptr, d_ext, nullptr, -1);
+  if (rc) return rc;
+  if (trace3) hipEventRecord(e[1], ctx->stream);
+  KScope ks(ctx, "msm_compress");
+  hipLaunchKernelGGL(k_compress_ext, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, ctx->stream, d_ext, B, d_out);
+  SPG_HIP(ctx, hipGetLastError());
+  if (trace3) {
+    hipEventRecord(e[2], ctx->stream);
+    hipEventSynchronize(e[2]);
+    float a = 0, b = 0;
+    hipEventElapsedTime(&a, e[0], e[1]);
+    hipEventElapsedTime(&b, e[1], e[2]);
+    fprintf(stderr, "[spg] small msm B=%zu n=%zu: msm %.0f us compress %.0f us\n", B, n, a * 1e3, b * 1e3);
+    for (auto& x : e) hipEventDestroy(x);
+  }
   return 0;
 }
 

@@ -132,6 +132,8 @@ int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars,
 ProverGens gens_view(spg_gens* dev, size_t nv);
 // DensePolynomial::commit (no blinds) of 2^nv device scalars; rows of 2^(nv - nv/2) <= g.n_pc scalars
 int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out);
+// L rows of R consecutive device scalars -> L row commitments (host)
+int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out);
 // PolyCommitment::append_to_transcript
 void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c);
 // PolyEvalProof::prove (no blinds) of a device polynomial of 2^|r| scalars

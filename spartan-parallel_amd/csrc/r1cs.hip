@@ -272,31 +272,6 @@ struct ZKRounds {
 
 
 // host wall-clock breakdown of one prove (printed to stderr when SPG_TRACE is set)
-struct Laps {
-  bool on = getenv("SPG_TRACE") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  std::vector<std::pair<std::string, double>> acc;
-  void lap(const char* name) {
-    if (!on) return;
-    auto now = std::chrono::steady_clock::now();
-    double us = std::chrono::duration<double, std::micro>(now - t).count();
-    t = now;
-    for (auto& a : acc)
-      if (a.first == name) {
-        a.second += us;
-        return;
-      }
-    acc.push_back({name, us});
-  }
-  void print() {
-    if (!on) return;
-    double tot = 0;
-    for (auto& a : acc) tot += a.second;
-    fprintf(stderr, "[spg] R1CSProof::prove host breakdown (us):");
-    for (auto& a : acc) fprintf(stderr, " %s=%.0f", a.first.c_str(), a.second);
-    fprintf(stderr, " total=%.0f\n", tot);
-  }
-};
 
 // device eq table of a host vector (uploads through the kernel argument)
 

@@ -380,12 +380,56 @@ SecInfo host_sec(const std::vector<Rows>& w, const std::vector<FqV>& poly) {
 }
 
 // Hyrax commitment of a host polynomial (uploads into a staging slot, device MSMs)
-int commit_host(spg_ctx* ctx, ProverGens& g, const FqV& Z, std::vector<Pt>* out) {
-  Fq* d = (Fq*)ws_get(ctx, 90, Z.size() * sizeof(Fq) + 64);
-  if (!d) return set_err(ctx, SPG_E_NOMEM, "commit staging");
-  SPG_HIP(ctx, hipMemcpyAsync(d, Z.data(), Z.size() * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
-  return commit_dev(ctx, g, d, lg2(Z.size()), out);
-}
+// Hyrax commitments of the witness polynomials of SNARK::prove, deferred so that all rows of one width go to
+// the device in one MSM launch; flush() appends them to the transcript in the order they were added (every
+// commitment between challenge_r and the block R1CSProof depends only on the witness and tau, r).
+struct CQ {
+  struct Item {
+    const FqV* host;
+    const Fq* dev;
+    size_t len;
+    std::vector<Pt>* out;
+  };
+  std::vector<Item> items;
+  void add(const FqV& v, std::vector<Pt>* out) { items.push_back({&v, nullptr, v.size(), out}); }
+  void add_dev(const Fq* d, size_t len, std::vector<Pt>* out) { items.push_back({nullptr, d, len, out}); }
+  int flush(spg_ctx* ctx, ProverGens& g, Tr& t) {
+    std::vector<size_t> widths;
+    for (auto& it : items) {
+      const size_t nv = lg2(it.len), R = (size_t)1 << (nv - nv / 2);
+      it.out->assign((size_t)1 << (nv / 2), Pt());
+      if (std::find(widths.begin(), widths.end(), R) == widths.end()) widths.push_back(R);
+    }
+    for (size_t R : widths) {
+      size_t total = 0;
+      for (auto& it : items)
+        if (((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) == R) total += it.len;
+      Fq* d = (Fq*)ws_get(ctx, 91, total * sizeof(Fq) + 64);
+      if (!d) return set_err(ctx, SPG_E_NOMEM, "commit staging");
+      size_t o = 0;
+      for (auto& it : items) {
+        if (((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
+        if (it.host)
+          SPG_HIP(ctx, hipMemcpyAsync(d + o, it.host->data(), it.len * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+        else
+          SPG_HIP(ctx, hipMemcpyAsync(d + o, it.dev, it.len * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
+        o += it.len;
+      }
+      std::vector<Pt> rows(total / R);
+      int rc = commit_rows(ctx, g, d, R, total / R, rows.data());
+      if (rc) return rc;
+      o = 0;
+      for (auto& it : items) {
+        if (((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
+        std::copy(rows.begin() + o, rows.begin() + o + it.out->size(), it.out->begin());
+        o += it.out->size();
+      }
+    }
+    for (auto& it : items) append_polycomm(t, "poly_commitment", *it.out);
+    items.clear();
+    return 0;
+  }
+};
 
 }  // namespace
 
@@ -530,8 +574,7 @@ struct MemGen {  // SNARK::mem_gen output (lib.rs:831-968)
   std::vector<Pt> c2, c3, c3s;
   SecInfo s2, s3, s3s;
 };
-int mem_gen(spg_ctx* ctx, ProverGens& g, size_t width, Rows mems, size_t total, const Fq& r, const Fq& tau, bool vir,
-            Tr& t, MemGen* o) {
+int mem_gen(size_t width, Rows mems, size_t total, const Fq& r, const Fq& tau, bool vir, CQ& q, MemGen* o) {
   if (total == 0) return 0;
   Rows w2(total, FqV(width, fq_zero())), w3(total, FqV(W3_WIDTH, fq_zero()));
   const Fq r2 = fq_mul(r, r), r3 = fq_mul(r2, r);
@@ -558,17 +601,9 @@ int mem_gen(spg_ctx* ctx, ProverGens& g, size_t width, Rows mems, size_t total, 
   o->p2 = {pad_pow2(flatten(o->w2[0]))};
   o->p3 = {pad_pow2(flatten(o->w3[0]))};
   o->p3s = {pad_pow2(flatten(o->w3s[0]))};
-  int rc = commit_host(ctx, g, o->p2[0], &o->c2);
-  if (!rc) {
-    append_polycomm(t, "poly_commitment", o->c2);
-    rc = commit_host(ctx, g, o->p3[0], &o->c3);
-  }
-  if (!rc) {
-    append_polycomm(t, "poly_commitment", o->c3);
-    rc = commit_host(ctx, g, o->p3s[0], &o->c3s);
-  }
-  if (rc) return rc;
-  append_polycomm(t, "poly_commitment", o->c3s);
+  q.add(o->p2[0], &o->c2);
+  q.add(o->p3[0], &o->c3);
+  q.add(o->p3s[0], &o->c3s);
   o->s2 = host_sec(o->w2, o->p2);
   o->s3 = host_sec(o->w3, o->p3);
   o->s3s = host_sec(o->w3s, o->p3s);
@@ -589,6 +624,8 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   const size_t niu = a.num_inputs_unpadded, num_ios = a.num_ios, io_width = 2 * niu;
   const size_t Bb = a.block_num_instances_bound;
   if (2 * niu > num_ios) return set_err(ctx, SPG_E_ARG, "num_ios < 2 * num_inputs_unpadded");
+  Laps lp;
+  lp.title = "SNARK::prove";
   t.protocol("Spartan SNARK proof");
   const bool dbg0 = getenv("SPG_DEBUG_SNARK") != nullptr;
   auto fp = [&](const char* where) {
@@ -679,6 +716,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   rc = ensure_sorted(ctx, pairwise, pw_order);
   if (rc) return rc;
 
+  lp.lap("inst_commit+sort");
   // ---- WITNESS GEN: block (lib.rs:1299-1741)
   const Fq tau = t.challenge("challenge_tau"), r = t.challenge("challenge_r");
   const bool dbg = getenv("SPG_DEBUG_SNARK") != nullptr;
@@ -692,10 +730,9 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     }
     perm_w0.resize(num_ios, fq_zero());
   }
+  CQ cq;
   std::vector<Pt> c_w0;
-  rc = commit_host(ctx, g, perm_w0, &c_w0);
-  if (rc) return rc;
-  append_polycomm(t, "poly_commitment", c_w0);
+  cq.add(perm_w0, &c_w0);
   const Rows& exec = W->exec;
   Rows pe_w2(consis), pe_w3(consis);
   for (size_t q = 0; q < consis; q++) {
@@ -731,14 +768,13 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   if (dbg)
     for (size_t q = 0; q < 2; q++)
       for (size_t i = 0; i < num_ios; i++) fprintf(stderr, "pe_w2[%zu][%zu] %08x\n", q, i, pe_w2[q][i].l[0]);
+  lp.lap("perm_exec_witness");
   std::vector<Pt> c_pe2, c_pe3, c_pe3s;
-  if ((rc = commit_host(ctx, g, pe_p2[0], &c_pe2))) return rc;
-  append_polycomm(t, "poly_commitment", c_pe2);
-  if ((rc = commit_host(ctx, g, pe_p3[0], &c_pe3))) return rc;
-  append_polycomm(t, "poly_commitment", c_pe3);
-  if ((rc = commit_host(ctx, g, pe_p3s[0], &c_pe3s))) return rc;
-  append_polycomm(t, "poly_commitment", c_pe3s);
+  cq.add(pe_p2[0], &c_pe2);
+  cq.add(pe_p3[0], &c_pe3);
+  cq.add(pe_p3s[0], &c_pe3s);
 
+  lp.lap("perm_exec_commit");
   std::vector<Rows> b_w2(P), b_w3(P), b_w3s(P);
   const Fq r2 = fq_mul(r, r), r3 = fq_mul(r2, r);
   for (size_t p = 0; p < P; p++) {
@@ -795,69 +831,60 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     }
     b_w3s[p] = shift_rows(b_w3[p], 8);
   }
+  lp.lap("block_witness");
   std::vector<FqV> b_p2(P), b_p3(P), b_p3s(P);
   std::vector<std::vector<Pt>> c_b2(P), c_b3(P), c_b3s(P), c_bv(P);
   for (size_t p = 0; p < P; p++) {
     b_p2[p] = pad_pow2(flatten(b_w2[p]));
-    if ((rc = commit_host(ctx, g, b_p2[p], &c_b2[p]))) return rc;
-    append_polycomm(t, "poly_commitment", c_b2[p]);
+    cq.add(b_p2[p], &c_b2[p]);
   }
   for (size_t p = 0; p < P; p++) {
     b_p3[p] = pad_pow2(flatten(b_w3[p]));
     b_p3s[p] = pad_pow2(flatten(b_w3s[p]));
-    if ((rc = commit_host(ctx, g, b_p3[p], &c_b3[p]))) return rc;
-    append_polycomm(t, "poly_commitment", c_b3[p]);
-    if ((rc = commit_host(ctx, g, b_p3s[p], &c_b3s[p]))) return rc;
-    append_polycomm(t, "poly_commitment", c_b3s[p]);
+    cq.add(b_p3[p], &c_b3[p]);
+    cq.add(b_p3s[p], &c_b3s[p]);
   }
+  lp.lap("block_w_commit");
   // ---- memory witnesses (lib.rs:1742-1955)
   MemGen m_iphy, m_ivir, m_phy, m_vir;
-  if ((rc = mem_gen(ctx, g, INIT_PHY_MEM_WIDTH, init_phy, t_iphy, r, tau, false, t, &m_iphy))) return rc;
-  if ((rc = mem_gen(ctx, g, INIT_VIR_MEM_WIDTH, init_vir, t_ivir, r, tau, false, t, &m_ivir))) return rc;
-  if ((rc = mem_gen(ctx, g, PHY_MEM_WIDTH, addr_phy, t_phy, r, tau, false, t, &m_phy))) return rc;
-  if ((rc = mem_gen(ctx, g, VIR_MEM_WIDTH, addr_vir, t_vir, r, tau, true, t, &m_vir))) return rc;
+  mem_gen(INIT_PHY_MEM_WIDTH, init_phy, t_iphy, r, tau, false, cq, &m_iphy);
+  mem_gen(INIT_VIR_MEM_WIDTH, init_vir, t_ivir, r, tau, false, cq, &m_ivir);
+  mem_gen(PHY_MEM_WIDTH, addr_phy, t_phy, r, tau, false, cq, &m_phy);
+  mem_gen(VIR_MEM_WIDTH, addr_vir, t_vir, r, tau, true, cq, &m_vir);
+  lp.lap("mem_gen");
   // ---- WITNESS COMMITMENTS (lib.rs:1957-2221): block_vars and exec inputs from HBM
-  for (size_t p = 0; p < P; p++) {
-    if ((rc = commit_dev(ctx, g, W->d_block_vars[p], lg2(bnp_pad[p] * bnv[p]), &c_bv[p]))) return rc;
-    append_polycomm(t, "poly_commitment", c_bv[p]);
-  }
+  for (size_t p = 0; p < P; p++) cq.add_dev(W->d_block_vars[p], bnp_pad[p] * bnv[p], &c_bv[p]);
   std::vector<Pt> c_exec;
-  if ((rc = commit_dev(ctx, g, W->d_exec, lg2(consis * num_ios), &c_exec))) return rc;
-  append_polycomm(t, "poly_commitment", c_exec);
+  cq.add_dev(W->d_exec, consis * num_ios, &c_exec);
   std::vector<FqV> p_iphy, p_ivir, p_aphy, p_aphys, p_avir, p_avirs, p_ts;
   std::vector<Rows> r_aphys, r_avirs;
-  std::vector<Pt> c_aphy, c_aphys, c_avir, c_avirs, c_ts, c_unused;
+  std::vector<Pt> c_aphy, c_aphys, c_avir, c_avirs, c_ts, c_iphy_in, c_ivir_in;
   if (t_iphy) {
     p_iphy = {pad_pow2(flatten(init_phy))};
-    if ((rc = commit_host(ctx, g, p_iphy[0], &c_unused))) return rc;
-    append_polycomm(t, "poly_commitment", c_unused);
+    cq.add(p_iphy[0], &c_iphy_in);
   }
   if (t_ivir) {
     p_ivir = {pad_pow2(flatten(init_vir))};
-    if ((rc = commit_host(ctx, g, p_ivir[0], &c_unused))) return rc;
-    append_polycomm(t, "poly_commitment", c_unused);
+    cq.add(p_ivir[0], &c_ivir_in);
   }
   if (t_phy) {
     p_aphy = {pad_pow2(flatten(addr_phy))};
-    if ((rc = commit_host(ctx, g, p_aphy[0], &c_aphy))) return rc;
-    append_polycomm(t, "poly_commitment", c_aphy);
+    cq.add(p_aphy[0], &c_aphy);
     r_aphys = {shift_rows(addr_phy, PHY_MEM_WIDTH)};
     p_aphys = {pad_pow2(flatten(r_aphys[0]))};
-    if ((rc = commit_host(ctx, g, p_aphys[0], &c_aphys))) return rc;
-    append_polycomm(t, "poly_commitment", c_aphys);
+    cq.add(p_aphys[0], &c_aphys);
   }
   if (t_vir) {
     p_avir = {pad_pow2(flatten(addr_vir))};
-    if ((rc = commit_host(ctx, g, p_avir[0], &c_avir))) return rc;
-    append_polycomm(t, "poly_commitment", c_avir);
+    cq.add(p_avir[0], &c_avir);
     r_avirs = {shift_rows(addr_vir, VIR_MEM_WIDTH)};
     p_avirs = {pad_pow2(flatten(r_avirs[0]))};
-    if ((rc = commit_host(ctx, g, p_avirs[0], &c_avirs))) return rc;
-    append_polycomm(t, "poly_commitment", c_avirs);
+    cq.add(p_avirs[0], &c_avirs);
     p_ts = {pad_pow2(flatten(ts_bits))};
-    if ((rc = commit_host(ctx, g, p_ts[0], &c_ts))) return rc;
-    append_polycomm(t, "poly_commitment", c_ts);
+    cq.add(p_ts[0], &c_ts);
   }
+  if ((rc = cq.flush(ctx, g, t))) return rc;
+  lp.lap("input_commit");
   // witness sections
   std::vector<FqV> w0v = {perm_w0};
   SecInfo s_w0 = host_sec({{perm_w0}}, w0v);
@@ -922,6 +949,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   rc = sat_prove(ctx, vars_gens, block->dev_sorted, P, bmax, bnp_pad, a.num_vars, bnv,
                  {wpart(s_bvars), wpart(s_w0), wpart(s_bw2), wpart(s_bw3), wpart(s_bw3s)}, &Wt, transcript, tape_h, &so);
   if (rc) return rc;
+  lp.lap("block_sat");
   w.out.insert(w.out.end(), so.bytes.begin(), so.bytes.end());
   {
     FqV list;
@@ -941,6 +969,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
       if ((rc = spark_prove_core(ctx, block->sparks[gi], so.ch[2], so.ch[3], ev, t, tape, w))) return rc;
     }
   }
+  lp.lap("block_eval");
   // ---- PAIRWISE_CHECK (lib.rs:2311-2424)
   {
     const size_t pairwise_size = std::max({consis, t_phy, t_vir});
@@ -969,6 +998,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     w.fqs(list);
     if ((rc = spark_prove_core(ctx, pairwise->sparks[0], so.ch[2], so.ch[3], list, t, tape, w))) return rc;
   }
+  lp.lap("pairwise");
   // ---- PERM_ROOT (lib.rs:2426-2532)
   {
     const size_t perm_size = std::max({consis, t_iphy, t_ivir, t_phy, t_vir});
@@ -993,6 +1023,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
                                w)))
       return rc;
   }
+  lp.lap("perm_root");
   // ---- PERM_PRODUCT_PROOF (lib.rs:2534-2609)
   {
     std::vector<const SecInfo*> comps = {&s_pe3, &m_iphy.s3, &m_ivir.s3, &m_phy.s3, &m_vir.s3, &s_bw3};
@@ -1019,6 +1050,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     w.fqs(prod);
     if ((rc = prove_batched_instances(ctx, g, pw3.poly, r_list, prod, t, tape, w))) return rc;
   }
+  lp.lap("perm_product");
   // ---- SHIFT_PROOFS (lib.rs:2611-2668)
   {
     std::vector<const FqV*> orig = {&pe_p3[0]}, shifted = {&pe_p3s[0]};
@@ -1102,6 +1134,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     w.u64(n);
     for (auto& o : openings) w.pts(o);
   }
+  lp.lap("shift");
   // ---- IO_PROOFS (lib.rs:194-272)
   {
     const size_t r_len = lg2(consis * num_ios);
@@ -1129,6 +1162,8 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     FqV Z = pad_pow2(flatten(W->exec));
     if ((rc = prove_batched_points(ctx, g, Z, r_list, Zr, t, tape, w))) return rc;
   }
+  lp.lap("io");
+  lp.print();
   *proof_len = w.out.size();
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, w.out.data(), w.out.size());

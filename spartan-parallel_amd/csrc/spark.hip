@@ -226,6 +226,8 @@ struct spg_spark {
 namespace spg {
 
 static unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
+// Hyrax rows up to this many scalars go through the latency MSM path (one block per bucket and row)
+static const size_t kSmallRowMax = 256;
 // workspace slots of this file
 enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
@@ -248,23 +250,38 @@ ProverGens gens_view(spg_gens* dev, size_t nv) {
   return g;
 }
 
-// DensePolynomial::commit without blinds (dense_mlpoly.rs:181-216) of 2^nv device scalars: one MSM per
-// row of R = 2^(nv - nv/2) scalars, in chunks of rows that keep the MSM sort within 32-bit indices
-int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out) {
-  size_t L = (size_t)1 << (nv / 2), R = (size_t)1 << (nv - nv / 2);
-  if (R > g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: polynomial size does not match its generators");
-  out->resize(L);
-  size_t chunk = std::max<size_t>(1, std::min<size_t>(L, ((size_t)1 << 24) / R));
+// L Hyrax rows of R consecutive device scalars each -> L compressed row commitments (host). Rows of up to
+// kSmallRowMax scalars take the latency MSM path (one block per bucket and row), longer rows the sorted batch
+// pipeline in chunks that keep its sort within 32-bit indices.
+int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out) {
+  if (R > g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: rows wider than the generators");
+  const bool small = R <= kSmallRowMax;
+  const size_t chunk = small ? std::min<size_t>(L, 65535)
+                             : std::max<size_t>(1, std::min<size_t>(L, ((size_t)1 << 24) / R));
   uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsCommit, 32 * chunk + 64);
   if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit out");
+  static const bool trace2 = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2;
   for (size_t r0 = 0; r0 < L; r0 += chunk) {
     size_t nb = std::min(chunk, L - r0);
-    int rc = msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr, (long)(g.n_pc + 1));
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = small ? msm_small_compressed(ctx, g.dev, 0, d_Z + r0 * R, R, nb, d_out)
+                   : msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr, (long)(g.n_pc + 1));
     if (rc) return rc;
-    SPG_HIP(ctx, hipMemcpyAsync(out->data() + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
+    SPG_HIP(ctx, hipMemcpyAsync(out + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
     SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
+    if (trace2)
+      fprintf(stderr, "[spg] commit rows=%zu R=%zu %s %.0f us\n", nb, R, small ? "small" : "batch",
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   }
   return 0;
+}
+
+// DensePolynomial::commit without blinds (dense_mlpoly.rs:184-256) of 2^nv device scalars: L = 2^(nv/2)
+// rows of R = 2^(nv - nv/2) scalars against the first R generators
+int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out) {
+  size_t L = (size_t)1 << (nv / 2), R = (size_t)1 << (nv - nv / 2);
+  out->resize(L);
+  return commit_rows(ctx, g, d_Z, R, L, out->data());
 }
 
 void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c) {
