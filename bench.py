@@ -123,9 +123,6 @@ def main():
     for _ in range(a.warmup):
         step()
     sync()
-    ctx.prof_enable(True)
-    ctx.prof_read(reset=True)
-    sync()
     t0 = time.perf_counter()
     proofs = set()
     for _ in range(a.steps):
@@ -133,8 +130,7 @@ def main():
         proofs.add(hashlib.sha256(pf).hexdigest())
     sync()
     dt = time.perf_counter() - t0
-    prof = ctx.prof_read(reset=True)
-    ctx.prof_enable(False)
+    prof = profile_pass(ctx, step, a.steps)
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -207,6 +203,18 @@ def main():
         dist.destroy_process_group()
 
 
+def profile_pass(ctx, step, steps):
+    """per-kernel HIP-event timing (libspg spg_prof_*) of `steps` extra steps run after the timed region, so
+    the events never perturb `value`; returns {kernel: (launches, us, algorithmic bytes)} summed over them"""
+    ctx.prof_enable(True)
+    ctx.prof_read(reset=True)
+    for _ in range(steps):
+        step()
+    prof = ctx.prof_read(reset=True)
+    ctx.prof_enable(False)
+    return prof
+
+
 def roofline_of(prof, traffic_file):
     """roofline object for the modelled kernel with the largest device time"""
     modelled = {k: v for k, v in prof.items() if v[2] > 0}
@@ -275,17 +283,13 @@ def main_snark(a):
     for _ in range(a.warmup):
         step()
     sync()
-    ctx.prof_enable(True)
-    ctx.prof_read(reset=True)
-    sync()
     t0 = time.perf_counter()
     proofs = set()
     for _ in range(a.steps):
         proofs.add(hashlib.sha256(step()).hexdigest())
     sync()
     dt = time.perf_counter() - t0
-    prof = ctx.prof_read(reset=True)
-    ctx.prof_enable(False)
+    prof = profile_pass(ctx, step, a.steps)
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -386,17 +390,13 @@ def main_spark(a):
     for _ in range(a.warmup):
         step()
     sync()
-    ctx.prof_enable(True)
-    ctx.prof_read(reset=True)
-    sync()
     t0 = time.perf_counter()
     proofs = set()
     for _ in range(a.steps):
         proofs.add(hashlib.sha256(step()).hexdigest())
     sync()
     dt = time.perf_counter() - t0
-    prof = ctx.prof_read(reset=True)
-    ctx.prof_enable(False)
+    prof = profile_pass(ctx, step, a.steps)
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

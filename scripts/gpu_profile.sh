@@ -6,7 +6,7 @@ mkdir -p "$R/gpurun_out"
 export TMPDIR=/tmp
 cd /tmp
 BA="--steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o r1cs -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- \
   python3 "$R/bench.py" $BA > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err" || exit $?
 echo "stats done"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o f -- \

@@ -646,6 +646,8 @@ namespace spg {
 // SparseMatPolyEvalProof::prove (sparse_mlpoly.rs:1497-1564); appends bincode(proof) to w
 int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w) {
   if (evals.size() != S->B) return set_err(ctx, SPG_E_ARG, "one evaluation per batched matrix");
+  Laps lp;
+  lp.title = "SparseMatPolyEvalProof::prove";
   hipStream_t s = ctx->stream;
   const size_t B = S->B, N = S->N, BN = B * N, cells = S->cells, hN = N / 2;
   if (ex.size() < ey.size()) ex.insert(ex.begin(), ey.size() - ex.size(), fq_zero());
@@ -676,8 +678,10 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     hipLaunchKernelGGL(k_gather, dim3(nblk(2 * BN)), dim3(256), 0, s, S->d_addr, mem_rx, mem_ry, BN, derefs);
   }
   SPG_HIP(ctx, hipGetLastError());
+  lp.lap("setup+deref");
   std::vector<Pt> comm_derefs;
   rc = commit_dev(ctx, S->g_der, derefs, lg2(der_len), &comm_derefs);
+  lp.lap("derefs_commit");
   if (rc) return rc;
   t.msg("derefs_commitment", "begin_derefs_commitment");
   append_polycomm(t, "comm_poly_row_col_ops_val", comm_derefs);
@@ -707,6 +711,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   SPG_HIP(ctx, hipGetLastError());
   FqV tops(4 * B + 4);
   rc = d2h_fq(ctx, dtops, tops.data(), tops.size());
+  lp.lap("hash+trees");
   if (rc) return rc;
   // ---- PolyEvalNetworkProof -> ProductLayerProof (sparse_mlpoly.rs:1368-1402, 1118-1263)
   t.protocol("Sparse polynomial evaluation proof");
@@ -755,6 +760,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     t.scalar("claim_eval_dotp_left", dl[b]);
     t.scalar("claim_eval_dotp_right", dr[b]);
   }
+  lp.lap("dotp_claims");
   BatchedProofP proof_ops, proof_mem;
   FqV rand_ops, rand_mem;
   rc = batched_prove(ctx, tree_ops, 4 * B, N, FqV(tops.begin(), tops.begin() + 4 * B), dotp, dotp_claims, t,
@@ -762,6 +768,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   if (!rc)
     rc = batched_prove(ctx, tree_mem, 4, cells, FqV(tops.begin() + 4 * B, tops.end()), {}, {}, t, &proof_mem, &rand_mem);
   if (rc) return rc;
+  lp.lap("layer_sumchecks");
   // ---- HashLayerProof (sparse_mlpoly.rs:805-918)
   t.protocol("Sparse polynomial hash layer proof");
   rc = eq_table(ctx, rand_ops, eq_ops);
@@ -772,6 +779,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   if (!rc) rc = seg_dots(ctx, S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops);
   if (!rc) rc = seg_dots(ctx, S->d_comb_mem, cells, 2, eq_mem, cells, &ev_mem);
   if (rc) return rc;
+  lp.lap("hash_evals");
   DotProductProofLogP pf_der, pf_ops, pf_mem;
   {  // DerefsEvalProof::prove (sparse_mlpoly.rs:80-146)
     t.protocol("Derefs evaluation proof");
@@ -805,6 +813,8 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     rc = poly_eval_prove(ctx, S->g_mem, S->d_comb_mem, rj, ej, t, tape, &pf_mem);
     if (rc) return rc;
   }
+  lp.lap("poly_eval_proofs");
+  lp.print();
   timer_stop(ctx);
   // ---- bincode(SparseMatPolyEvalProof)
   w.pts(comm_derefs);
