@@ -91,6 +91,9 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
 int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, Ext* d_out, const uint32_t* d_idx, long h_index);
 
+// bucket stage of the latency path only (d_buckets: B x NB Ext); *nb_out = NB
+int msm_small_buckets(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                      const Fq* d_blinds, const uint32_t* d_idx, long h_index, Ext* d_buckets, int* nb_out);
 // the latency path for many small rows (Hyrax rows of <= ~1K scalars): compressed outputs, d_out: B x 32 (device)
 int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                          uint8_t* d_out);

@@ -23,20 +23,59 @@
 namespace spg {
 
 // ---------------------------------------------------------------- carry helpers
+// On the device these lower to single v_add_co_ci / v_sub_co_ci instructions (carry in VCC); the 64-bit
+// formulation costs ~4 instructions per limb there.
 SPG_HD uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_addc(a, b, cin, &cout);
+#else
   uint64_t s = (uint64_t)a + b + cin;
   cout = (uint32_t)(s >> 32);
   return (uint32_t)s;
+#endif
 }
 SPG_HD uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_subc(a, b, bin, &bout);
+#else
   uint64_t d = (uint64_t)a - b - bin;
   bout = (uint32_t)(d >> 63);
   return (uint32_t)d;
+#endif
 }
 // (hi:lo) = a*b + c + d ; never overflows 64 bits
 SPG_HD uint64_t mad(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return (uint64_t)a * b + c + d;
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc (64 bits) += a * b with the carry out of bit 64 counted in ov: one v_mad_u64_u32 (64-bit addend,
+// carry to an SGPR pair) + one v_addc_co_u32. Product scanning with this keeps a 255-bit product at
+// ~2 instructions per limb product instead of ~5 for the row form with 32-bit addends.
+__device__ __forceinline__ void mac_ov(uint64_t& acc, uint32_t& ov, uint32_t a, uint32_t b) {
+  uint64_t cy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cy) : "v"(a), "v"(b));
+  asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(ov), "=s"(cy) : "s"(cy));
+}
+// t[0..16) = a * b (8 x 32-bit limbs each), product scanning
+__device__ __forceinline__ void mul_8x8(const uint32_t* a, const uint32_t* b, uint32_t* t) {
+  uint64_t acc = 0;
+  uint32_t ov = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      mac_ov(acc, ov, a[i], b[j]);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)ov << 32);
+    ov = 0;
+  }
+  t[15] = (uint32_t)acc;
+}
+#endif
 
 // ================================================================= Fq (Montgomery, R = 2^256)
 struct Fq {
@@ -313,6 +352,11 @@ SPG_HD Fp fp_reduce512(uint32_t t[16]) {
   return r;
 }
 SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t t[16];
+  mul_8x8(a.l, b.l, t);
+  return fp_reduce512(t);
+#else
   uint32_t t[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) t[i] = 0;
@@ -328,8 +372,12 @@ SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
     t[i + 8] = c;
   }
   return fp_reduce512(t);
+#endif
 }
 SPG_HD Fp fp_sqr(const Fp& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fp_mul(a, a);
+#else
   // off-diagonal products once, doubled, plus the diagonal
   uint32_t t[16];
 #pragma unroll
@@ -360,6 +408,7 @@ SPG_HD Fp fp_sqr(const Fp& a) {
     t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(v >> 32), c, c);
   }
   return fp_reduce512(t);
+#endif
 }
 SPG_HD Fp fp_mul_small(const Fp& a, uint32_t k) {
   Fp r;

@@ -373,6 +373,47 @@ static void launch_small(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const 
   hipLaunchKernelGGL(k_smsm_final, dim3(B), dim3(NB), 0, s, bk, NB, out);
 }
 
+template <int C>
+static void launch_buckets(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const Fq* bl, int n, int n1, int off, int h,
+                           const Niels* tab, Ext* bk, int B, hipStream_t s) {
+  constexpr int NB = 1 << (C - 1);
+  KScope ks(ctx, "msm_small_bucket");
+  const int per = n + (bl ? 1 : 0);
+  const Fq* blp = bl ? bl : sc;
+  if (per <= 64)
+    hipLaunchKernelGGL((k_smsm_bucket<C, 64>), dim3(NB, B), dim3(64), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h, tab,
+                       bk);
+  else if (per <= 128)
+    hipLaunchKernelGGL((k_smsm_bucket<C, 128>), dim3(NB, B), dim3(128), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
+                       tab, bk);
+  else
+    hipLaunchKernelGGL((k_smsm_bucket<C, 256>), dim3(NB, B), dim3(256), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
+                       tab, bk);
+}
+
+// the bucket stage of the latency path only: d_buckets[b * NB + v - 1] = B_v of MSM b; returns NB. The caller
+// forms sum_v v * B_v (2 NB dependent additions: ~100 ns each on a host core with radix-2^51 limbs, ~5 us
+// each on one GPU lane).
+int msm_small_buckets(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+                      const Fq* d_blinds, const uint32_t* d_idx, long h_index, Ext* d_buckets, int* nb_out) {
+  hipStream_t s = ctx->stream;
+  const size_t per = n + (d_blinds ? 1 : 0);
+  const int c = pick_small_window(per);
+  SPG_CHECK(ctx, B <= 65535, "msm batch too large for the latency path");
+  const int n1 = (int)(g->n + 1), off = (int)gen_offset, h = h_index < 0 ? (int)g->n : (int)h_index;
+  switch (c) {
+    case 4: launch_buckets<4>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, d_buckets, (int)B, s); break;
+    case 5: launch_buckets<5>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, d_buckets, (int)B, s); break;
+    case 6: launch_buckets<6>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, d_buckets, (int)B, s); break;
+    case 7: launch_buckets<7>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, d_buckets, (int)B, s); break;
+    case 8: launch_buckets<8>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, d_buckets, (int)B, s); break;
+    default: launch_buckets<9>(ctx, d_scalars, d_idx, d_blinds, (int)n, n1, off, h, g->table, d_buckets, (int)B, s); break;
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  *nb_out = 1 << (c - 1);
+  return 0;
+}
+
 int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, Ext* d_out, const uint32_t* d_idx, long h_index) {
   hipStream_t s = ctx->stream;
@@ -396,7 +437,7 @@ int msm_small_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
 }
 
 // ext_compress of every point (RFC 9496 ENCODE), one lane per point
-__global__ void k_compress_ext(const Ext* __restrict__ in, size_t n, uint8_t* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_compress_ext(const Ext* __restrict__ in, size_t n, uint8_t* __restrict__ out) {
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) ext_compress(in[i], out + 32 * i);
 }

@@ -22,6 +22,7 @@
 
 #include "hostpoly.hpp"
 #include "proto.hpp"
+#include "sumcheck.hpp"
 
 namespace spg {
 
@@ -106,10 +107,12 @@ __device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
   __syncthreads();
 }
 // one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
-// sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367). blockIdx.y = triple, so the
-// coefficient multiplies the block's sums once; blocks publish partials (triple-major).
+// sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367). blockIdx.y = triple, so the coefficient
+// multiplies the block's sums once; the last block to finish (ticket on `counter`) adds every block's
+// partials and writes the round's three scalars to out3 (one launch per round).
 __global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
-                                                    size_t len, Fq* __restrict__ partials) {
+                                                    size_t len, Fq* __restrict__ partials,
+                                                    unsigned* __restrict__ counter, Fq* __restrict__ out3) {
   const Triple x = tr[blockIdx.y];
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (size_t)gridDim.x * 256) {
@@ -121,26 +124,36 @@ __global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ t
     e3 = fq_add(e3, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
   }
   block_sum3_sp(e0, e2, e3);
+  __shared__ bool last;
+  const unsigned nblocks = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
   if (threadIdx.x == 0) {
     const Fq k = coeff[blockIdx.y];
-    const size_t o = 3 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
-    partials[o] = fq_mul(k, e0);
-    partials[o + 1] = fq_mul(k, e2);
-    partials[o + 2] = fq_mul(k, e3);
+    partials[3 * bid] = fq_mul(k, e0);
+    partials[3 * bid + 1] = fq_mul(k, e2);
+    partials[3 * bid + 2] = fq_mul(k, e3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
-}
-__global__ void __launch_bounds__(256) k_sum3(const Fq* __restrict__ partials, int nb, Fq* __restrict__ out) {
+  __syncthreads();
+  if (!last) return;
   Fq a = fq_zero(), b = fq_zero(), c = fq_zero();
-  for (int i = threadIdx.x; i < nb; i += 256) {
+  for (unsigned i = threadIdx.x; i < nblocks; i += 256) {
     a = fq_add(a, partials[3 * i]);
     b = fq_add(b, partials[3 * i + 1]);
     c = fq_add(c, partials[3 * i + 2]);
   }
   block_sum3_sp(a, b, c);
   if (threadIdx.x == 0) {
-    out[0] = a;
-    out[1] = b;
-    out[2] = c;
+    out3[0] = a;
+    out3[1] = b;
+    out3[2] = c;
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 // DensePolynomial::bound_poly_var_top on nv distinct vectors of length 2 * len (in place)
@@ -421,11 +434,11 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
       const unsigned nbx = (unsigned)std::min<size_t>(nblk(len), std::max<size_t>(1, 2048 / tr.size()));
       {
         KScope ks(ctx, "spark_layer_eval", 192.0 * tr.size() * len);
-        hipLaunchKernelGGL(k_layer_eval, dim3(nbx, (unsigned)tr.size()), dim3(256), 0, s, dtr, dcoef, len, part);
-        hipLaunchKernelGGL(k_sum3, dim3(1), dim3(256), 0, s, part, (int)(nbx * tr.size()), d3);
+        hipLaunchKernelGGL(k_layer_eval, dim3(nbx, (unsigned)tr.size()), dim3(256), 0, s, dtr, dcoef, len, part,
+                           ctx->d_counter, d3);
       }
       Fq ev[3];
-      rc = d2h_fq(ctx, d3, ev, 3);
+      rc = eval_reduce_finish(ctx, d3, ev);
       if (rc) return rc;
       Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
       FqV poly = uni_from_evals3(evals);

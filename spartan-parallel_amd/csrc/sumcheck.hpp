@@ -36,5 +36,8 @@ int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_h
 // The *_eval calls above return (e0, e2, e3) in out3; with out3 == nullptr they only enqueue the work
 // and eval_wait() later blocks for the values (host work of the round runs in between).
 int eval_wait(spg_ctx* ctx, Fq* out3);
+// copies the three scalars a fused eval kernel left in d_out3 to the pinned staging buffer (and into out3,
+// waiting, unless out3 == nullptr)
+int eval_reduce_finish(spg_ctx* ctx, Fq* d_out3, Fq* out3);
 
 }  // namespace spg
