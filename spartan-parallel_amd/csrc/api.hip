@@ -1,3 +1,5 @@
+#include <chrono>
+#include <string.h>
 // spg — context management for the C-ABI (include/spg.h).
 #include <stdio.h>
 #include <string.h>
@@ -29,6 +31,24 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes) {
   }
   s.bytes = want;
   return s.p;
+}
+
+int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t it = 0;; it++) {
+    if (__atomic_load_n(ctx->mbox, __ATOMIC_ACQUIRE) == seq) break;
+    if ((it & 1023) == 1023) {
+      hipError_t e = hipStreamQuery(ctx->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) return set_err(ctx, SPG_E_HIP, "mailbox: stream failed");
+      if (e == hipSuccess && __atomic_load_n(ctx->mbox, __ATOMIC_ACQUIRE) != seq)
+        return set_err(ctx, SPG_E_HIP, "mailbox: kernel finished without posting");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+        return set_err(ctx, SPG_E_HIP, "mailbox: timed out");
+    }
+  }
+  for (int k = 0; k < n; k++)
+    for (int i = 0; i < 8; i++) out[k].l[i] = ctx->mbox[8 + 8 * k + i];
+  return 0;
 }
 
 void timer_start(spg_ctx* c) { hipEventRecord(c->ev0, c->stream); }
@@ -81,6 +101,14 @@ extern "C" int spg_init(int device, spg_ctx** out) {
     delete c;
     return SPG_E_HIP;
   }
+  void* mb = nullptr;
+  if (hipHostMalloc(&mb, 4096, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->d_mbox, mb, 0) != hipSuccess) {
+    delete c;
+    return SPG_E_HIP;
+  }
+  memset(mb, 0, 4096);
+  c->mbox = (volatile uint32_t*)mb;
   *out = c;
   return SPG_OK;
 }
@@ -92,6 +120,7 @@ extern "C" int spg_free(spg_ctx* c) {
   for (auto& s : c->ws)
     if (s.p) hipFree(s.p);
   if (c->pinned) hipHostFree(c->pinned);
+  if (c->mbox) hipHostFree((void*)c->mbox);
   if (c->d_counter) hipFree(c->d_counter);
   hipEventDestroy(c->ev0);
   hipEventDestroy(c->ev1);

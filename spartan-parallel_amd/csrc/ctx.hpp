@@ -15,6 +15,12 @@ struct spg_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* pinned = nullptr;          // 4 KiB page-locked host staging for per-round device->host scalars
   unsigned* d_counter = nullptr;   // grid-reduction ticket (zero between launches)
+  // mailbox in fine-grained (coherent, mapped) host memory: a kernel's last block posts a round's scalars
+  // and a sequence number with system-scope stores; the host spins on the number instead of a D2H copy +
+  // stream synchronisation (spg::mbox_wait)
+  volatile uint32_t* mbox = nullptr;
+  uint32_t* d_mbox = nullptr;
+  uint32_t mbox_seq = 0;
   // multi-process proving (spg_set_comm): this process' rank and an allgather provided by the caller
   int rank = 0, nranks = 1;
   spg_allgather_fn allgather = nullptr;
@@ -97,6 +103,17 @@ int msm_small_buckets(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const 
 // the latency path for many small rows (Hyrax rows of <= ~1K scalars): compressed outputs, d_out: B x 32 (device)
 int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                          uint8_t* d_out);
+
+// waits (spinning, bounded) until the mailbox carries sequence number `seq`, then copies n scalars out
+int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n);
+
+// device side of the mailbox: the scalars, then (after a system-scope release fence) the sequence number
+__device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* v, int n) {
+  for (int k = 0; k < n; k++)
+    for (int i = 0; i < 8; i++) __hip_atomic_store(mb + 8 + 8 * k + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // per-kernel profiling scope (no-op unless spg_prof_enable(ctx, 1))
 struct KScope {

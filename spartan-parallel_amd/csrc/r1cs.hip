@@ -530,8 +530,7 @@ int Prover::run_inner(Laps& lp) {
 
   lp.lap("setup");
   Fq* partials = (Fq*)ws_get(ctx, WS_PART, 3 * 1024 * sizeof(Fq) + 64);
-  Fq* d_out3 = (Fq*)ws_get(ctx, WS_OUT3, 4 * sizeof(Fq) + 64);
-  if (!partials || !d_out3) return set_err(ctx, SPG_E_NOMEM, "partials");
+  if (!partials) return set_err(ctx, SPG_E_NOMEM, "partials");
 
   // ---- phase 1 (sumcheck.rs:1067-1380)
   FqV rx_all;
@@ -559,14 +558,14 @@ int Prover::run_inner(Laps& lp) {
       if (mode == MODE_P) {
         std::vector<size_t> ones(P, 1);
         return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, ones, ones, Ap, Aq, Ax, T->d, TB, TC,
-                           partials, d_out3, nullptr);
+                           partials, nullptr);
       }
       for (size_t p = 0; p < sc_np.size(); p++) {  // instance_len >= P here: every instance takes part
         if (mode == MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
         if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
       }
       return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap_l, Aq, Ax, T->d, TB,
-                         TC, partials, d_out3, nullptr);
+                         TC, partials, nullptr);
     };
     // before the first instance round: collect every instance's remaining (Az, Bz, Cz) value
     auto to_compact = [&]() -> int {
@@ -734,12 +733,12 @@ int Prover::run_inner(Laps& lp) {
       else instance_len /= 2;
       if (mode == MODE_P) {
         std::vector<size_t> ones(P, 1);
-        return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, ones, eq_p, partials, d_out3,
+        return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, ones, eq_p, partials,
                            nullptr);
       }
       for (size_t p = 0; p < sc_ni.size(); p++)
         if (mode == MODE_X && sc_ni[p] > 1) sc_ni[p] /= 2;
-      return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, sc_ni, eq_l, partials, d_out3,
+      return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, sc_ni, eq_l, partials,
                          nullptr);
     };
     auto to_compact = [&]() -> int {

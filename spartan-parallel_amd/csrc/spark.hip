@@ -109,10 +109,11 @@ __device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
 // one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
 // sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367). blockIdx.y = triple, so the coefficient
 // multiplies the block's sums once; the last block to finish (ticket on `counter`) adds every block's
-// partials and writes the round's three scalars to out3 (one launch per round).
+// partials and posts the round's three scalars to the host mailbox (one launch per round).
 __global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
                                                     size_t len, Fq* __restrict__ partials,
-                                                    unsigned* __restrict__ counter, Fq* __restrict__ out3) {
+                                                    unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
+                                                    uint32_t seq) {
   const Triple x = tr[blockIdx.y];
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (size_t)gridDim.x * 256) {
@@ -150,9 +151,8 @@ __global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ t
   }
   block_sum3_sp(a, b, c);
   if (threadIdx.x == 0) {
-    out3[0] = a;
-    out3[1] = b;
-    out3[2] = c;
+    const Fq r[3] = {a, b, c};
+    mbox_post(mb, seq, r, 3);
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -391,10 +391,11 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
   Fq* dcoef = (Fq*)ws_get(ctx, kWsCoeff, nt_max * sizeof(Fq) + 64);
   Fq** dptr = (Fq**)ws_get(ctx, kWsFoldPtr, (2 * nc + 1 + 3 * dotp.size()) * sizeof(Fq*) + 64);
   Fq* part = (Fq*)ws_get(ctx, kWsPart, 3 * std::max<size_t>(2048, nt_max) * sizeof(Fq) + 64);
-  Fq* d3 = (Fq*)ws_get(ctx, kWs3, 3 * sizeof(Fq) + 64);
   Fq* dfin = (Fq*)ws_get(ctx, kWsFinals, 3 * nt_max * sizeof(Fq) + 64);
-  if (!dC || !dtr || !dcoef || !dptr || !part || !d3 || !dfin) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
+  if (!dC || !dtr || !dcoef || !dptr || !part || !dfin) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
   FqV rand;
+  Laps lp;
+  lp.title = "ProductCircuitEvalProofBatched::prove";
   for (size_t layer = L; layer-- > 0;) {
     const size_t half = M >> (layer + 1);  // |left| = |right| = |C|
     const size_t rounds = lg2(half);
@@ -425,7 +426,8 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     SPG_HIP(ctx, hipMemcpyAsync(dtr, tr.data(), tr.size() * sizeof(Triple), hipMemcpyHostToDevice, s));
     SPG_HIP(ctx, hipMemcpyAsync(dcoef, coeffs.data(), coeffs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
     SPG_HIP(ctx, hipMemcpyAsync(dptr, fold.data(), fold.size() * sizeof(Fq*), hipMemcpyHostToDevice, s));
-    LayerProofP lp;
+    lp.lap("layer_setup");
+    LayerProofP lpf;
     FqV r_prod;
     size_t log_len = rounds;
     for (size_t j = 0; j < rounds; j++) {
@@ -435,16 +437,18 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
       {
         KScope ks(ctx, "spark_layer_eval", 192.0 * tr.size() * len);
         hipLaunchKernelGGL(k_layer_eval, dim3(nbx, (unsigned)tr.size()), dim3(256), 0, s, dtr, dcoef, len, part,
-                           ctx->d_counter, d3);
+                           ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
       }
       Fq ev[3];
-      rc = eval_reduce_finish(ctx, d3, ev);
+      rc = eval_reduce_finish(ctx, ev);
       if (rc) return rc;
+      lp.lap("round_eval_wait");
       Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
       FqV poly = uni_from_evals3(evals);
       append_unipoly(t, poly);
       Fq r_j = t.challenge("challenge_nextround");
       r_prod.push_back(r_j);
+      lp.lap("round_host");
       {
         KScope ks(ctx, "spark_fold", 96.0 * fold.size() * len);
         hipLaunchKernelGGL(k_fold_many, dim3(nblk(fold.size() * len)), dim3(256), 0, s, dptr, fold.size(),
@@ -452,7 +456,8 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
       }
       SPG_HIP(ctx, hipGetLastError());
       e = uni_eval(poly, r_j);
-      lp.polys.push_back({poly[0], poly[2], poly[3]});
+      lpf.polys.push_back({poly[0], poly[2], poly[3]});
+      lp.lap("round_fold_launch");
     }
     // final claims: A[0], B[0] (and C[0] for the dot-product circuits)
     hipLaunchKernelGGL(k_finals, dim3(nblk(tr.size())), dim3(256), 0, s, dtr, tr.size(), dfin);
@@ -460,12 +465,12 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     rc = d2h_fq(ctx, dfin, fin.data(), fin.size());
     if (rc) return rc;
     for (size_t c = 0; c < nc; c++) {
-      lp.left.push_back(fin[3 * c]);
-      lp.right.push_back(fin[3 * c + 1]);
+      lpf.left.push_back(fin[3 * c]);
+      lpf.right.push_back(fin[3 * c + 1]);
     }
     for (size_t c = 0; c < nc; c++) {
-      t.scalar("claim_prod_left", lp.left[c]);
-      t.scalar("claim_prod_right", lp.right[c]);
+      t.scalar("claim_prod_left", lpf.left[c]);
+      t.scalar("claim_prod_right", lpf.right[c]);
     }
     if (with_dotp) {
       for (size_t k = 0; k < dotp.size(); k++)
@@ -478,11 +483,13 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     }
     Fq r_layer = t.challenge("challenge_r_layer");
     claims.assign(nc, fq_zero());
-    for (size_t c = 0; c < nc; c++) claims[c] = fq_add(lp.left[c], fq_mul(r_layer, fq_sub(lp.right[c], lp.left[c])));
+    for (size_t c = 0; c < nc; c++) claims[c] = fq_add(lpf.left[c], fq_mul(r_layer, fq_sub(lpf.right[c], lpf.left[c])));
     rand.assign(1, r_layer);
     rand.insert(rand.end(), r_prod.begin(), r_prod.end());
-    out->layers.push_back(std::move(lp));
+    out->layers.push_back(std::move(lpf));
+    lp.lap("layer_finals");
   }
+  lp.print();
   *rand_out = rand;
   return 0;
 }

@@ -46,11 +46,11 @@ __device__ __forceinline__ void block_sum3(Fq& v0, Fq& v1, Fq& v2) {
 }
 
 // Grid-wide (e0, e2, e3): every block publishes its partial sums; the last block to finish (ticket on
-// `counter`) adds all partials and writes out3, then re-arms the counter. One launch per round.
+// `counter`) adds all partials and posts them to the host mailbox (mbox_post), then re-arms the counter. One launch per round.
 // Cross-XCD hand-off: plain stores + agent-scope release before the ticket, agent-scope acquire in
 // the reducer before plain loads (MI355X L2s are per-XCD and not coherent).
 __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict__ partials,
-                                             unsigned* __restrict__ counter, Fq* __restrict__ out3) {
+                                             unsigned* __restrict__ counter, uint32_t* __restrict__ mb, uint32_t seq) {
   __shared__ bool last;
   block_sum3(v0, v1, v2);
   const int t = threadIdx.x;
@@ -77,9 +77,8 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
   }
   block_sum3(a, b, c);
   if (t == 0) {
-    out3[0] = a;
-    out3[1] = b;
-    out3[2] = c;
+    const Fq r[3] = {a, b, c};
+    mbox_post(mb, seq, r, 3);
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -119,7 +118,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
                                                      const Fq* __restrict__ Ax, const Fq* __restrict__ B,
                                                      const Fq* __restrict__ C, const Fq* __restrict__ D,
                                                      Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                     Fq* __restrict__ out3) {
+                                                     uint32_t* __restrict__ mb, uint32_t seq) {
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(a, t);
@@ -162,7 +161,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
     Fq c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
     e3 = fq_add(e3, fq_mul(a3, fq_sub(fq_mul(b3, c3), d3)));
   }
-  grid_reduce3(e0, e2, e3, partials, counter, out3);
+  grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
 // ---------------------------------------------------------------- phase 2 round evaluation
@@ -188,7 +187,7 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
                                                      bool single, uint32_t instance_len, const Fq* __restrict__ eq,
                                                      const Fq* __restrict__ B, const Fq* __restrict__ C,
                                                      Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                     Fq* __restrict__ out3) {
+                                                     uint32_t* __restrict__ mb, uint32_t seq) {
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(zz, t);
@@ -207,7 +206,7 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
     Fq a3 = fq_sub(fq_add(a2, a_hi), a_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo);
     e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
   }
-  grid_reduce3(e0, e2, e3, partials, counter, out3);
+  grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
 // ---------------------------------------------------------------- Pqx folds (custom_dense_mlpoly.rs:205-289)
@@ -261,7 +260,7 @@ __global__ void k_pqx_fold(PqxArgs a, int mode, uint32_t total, Fq r, Fq* __rest
 // ---------------------------------------------------------------- plain cubic (product trees), A*B*C
 __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, const Fq* __restrict__ B,
                                                     const Fq* __restrict__ C, uint32_t len, Fq* __restrict__ partials,
-                                                    unsigned* __restrict__ counter, Fq* __restrict__ out3) {
+                                                    unsigned* __restrict__ counter, uint32_t* __restrict__ mb, uint32_t seq) {
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < len; i += gridDim.x * 256) {
     Fq al = A[i], ah = A[i + len], bl = B[i], bh = B[i + len], cl = C[i], ch = C[i + len];
@@ -271,7 +270,7 @@ __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, co
     Fq a3 = fq_sub(fq_add(a2, ah), al), b3 = fq_sub(fq_add(b2, bh), bl), c3 = fq_sub(fq_add(c2, ch), cl);
     e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
   }
-  grid_reduce3(e0, e2, e3, partials, counter, out3);
+  grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -281,17 +280,10 @@ static int grid_for(uint32_t total) {
   return nb < 1 ? 1 : nb;
 }
 
-// device -> pinned host copy of the round's three scalars (written by the last block of the eval kernel);
-// out3 == nullptr only enqueues the copy (collect it with eval_wait), so host work can overlap the round
-int eval_reduce_finish(spg_ctx* ctx, Fq* d_out3, Fq* out3) {
-  SPG_HIP(ctx, hipMemcpyAsync(ctx->pinned, d_out3, 3 * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
-  return out3 ? eval_wait(ctx, out3) : 0;
-}
-int eval_wait(spg_ctx* ctx, Fq* out3) {
-  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  memcpy(out3, ctx->pinned, 3 * sizeof(Fq));
-  return 0;
-}
+// the round's three scalars arrive in the host mailbox (posted by the last block of the eval kernel);
+// out3 == nullptr returns at once (collect them with eval_wait), so host work can overlap the round
+int eval_reduce_finish(spg_ctx* ctx, Fq* out3) { return out3 ? eval_wait(ctx, out3) : 0; }
+int eval_wait(spg_ctx* ctx, Fq* out3) { return mbox_wait(ctx, ctx->mbox_seq, out3, 3); }
 
 int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out) {
   if (ell > 32) return set_err(ctx, SPG_E_ARG, "eq table: too many variables");
@@ -352,7 +344,7 @@ void pqx_fill_args(const PqxDev& T, PqxArgs& a) {
 
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
-                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* d_out3, Fq* out3) {
+                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* out3) {
   PqxArgs a;
   pqx_fill_args(T, a);
   size_t P = std::min(instance_len, sc_np.size());
@@ -375,15 +367,15 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
     KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len));
     hipLaunchKernelGGL(k_phase1_eval, dim3(nb), dim3(256), 0, ctx->stream, a, mode, (uint32_t)dom,
                        (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq, Ax, B, C, D,
-                       partials, ctx->d_counter, d_out3);
+                       partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
   }
   SPG_HIP(ctx, hipGetLastError());
-  return eval_reduce_finish(ctx, d_out3, out3);
+  return eval_reduce_finish(ctx, out3);
 }
 
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
-                const Fq* eq, Fq* partials, Fq* d_out3, Fq* out3) {
+                const Fq* eq, Fq* partials, Fq* out3) {
   PqxArgs ab, zz;
   pqx_fill_args(AB, ab);
   pqx_fill_args(Z, zz);
@@ -402,10 +394,10 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
   {
     KScope ks(ctx, "sc_phase2_eval", 128.0 * dom);  // ABC and Z, lo+hi per domain point
     hipLaunchKernelGGL(k_phase2_eval, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, (int)W,
-                       single, (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, d_out3);
+                       single, (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
   }
   SPG_HIP(ctx, hipGetLastError());
-  return eval_reduce_finish(ctx, d_out3, out3);
+  return eval_reduce_finish(ctx, out3);
 }
 
 // DensePolynomialPqx::bound_poly(r, mode) applied to up to three tables of identical shape (T[0] owns shape)
@@ -467,16 +459,16 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode) {
   return 0;
 }
 
-int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials, Fq* d_out3,
+int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials,
                Fq* out3) {
   int nb = grid_for((uint32_t)len_half);
   {
     KScope ks(ctx, "sc_cubic_eval", 192.0 * len_half);
     hipLaunchKernelGGL(k_cubic_eval, dim3(nb), dim3(256), 0, ctx->stream, A, B, C, (uint32_t)len_half, partials,
-                       ctx->d_counter, d_out3);
+                       ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
   }
   SPG_HIP(ctx, hipGetLastError());
-  return eval_reduce_finish(ctx, d_out3, out3);
+  return eval_reduce_finish(ctx, out3);
 }
 
 }  // namespace spg

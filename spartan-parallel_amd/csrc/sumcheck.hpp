@@ -23,21 +23,20 @@ int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r);
 // one phase-1 round: (e0, e2, e3) of eq(p,q,x) * (B*C - D)  (src/sumcheck.rs:1173-1245)
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
-                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* d_out3, Fq* out3);
+                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* out3);
 // one phase-2 round: (e0, e2, e3) of eq(p) * ABC * Z  (src/sumcheck.rs:881-941)
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
-                const Fq* eq, Fq* partials, Fq* d_out3, Fq* out3);
+                const Fq* eq, Fq* partials, Fq* out3);
 // DensePolynomialPqx::bound_poly on T (and d1, d2 sharing T's shape, may be null)
 int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode);
 // SumcheckInstanceProof::prove_cubic round on dense A, B, C of length 2*len_half
-int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials, Fq* d_out3,
+int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials,
                Fq* out3);
 // The *_eval calls above return (e0, e2, e3) in out3; with out3 == nullptr they only enqueue the work
 // and eval_wait() later blocks for the values (host work of the round runs in between).
 int eval_wait(spg_ctx* ctx, Fq* out3);
-// copies the three scalars a fused eval kernel left in d_out3 to the pinned staging buffer (and into out3,
-// waiting, unless out3 == nullptr)
-int eval_reduce_finish(spg_ctx* ctx, Fq* d_out3, Fq* out3);
+// waits for the three scalars the last fused eval kernel posts to the host mailbox (no-op if out3 == nullptr)
+int eval_reduce_finish(spg_ctx* ctx, Fq* out3);
 
 }  // namespace spg
