@@ -7,6 +7,7 @@
 // folded and the group elements produced are identical to the reference's.
 #include <functional>
 
+#include "hostpoly.hpp"
 #include "proto.hpp"
 
 namespace spg {
@@ -138,9 +139,13 @@ DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyVie
 }
 
 // B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
+// SPG_TRACE >= 2: where a Bullet round's time goes (accumulated over a process, printed per DotProductProofLog)
+static Laps g_msm_laps{"DotProductProofLog::prove (cumulative)", getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2};
+
 static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& hs, size_t n, size_t B,
                            const uint32_t* d_idx, std::vector<Pt>* out) {
   hipStream_t s = ctx->stream;
+  g_msm_laps.lap("bullet_host");
   Fq* d_s = (Fq*)ws_get(ctx, 20, hs.size() * sizeof(Fq) + 64);
   Ext* d_o = (Ext*)ws_get(ctx, 22, sizeof(Ext) * B + 64);
   if (!d_s || !d_o) return set_err(ctx, SPG_E_NOMEM, "device_msm");
@@ -156,6 +161,7 @@ static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& h
   std::vector<Ext> bk(B * (size_t)NB);
   SPG_HIP(ctx, hipMemcpyAsync(bk.data(), d_bk, sizeof(Ext) * bk.size(), hipMemcpyDeviceToHost, s));
   SPG_HIP(ctx, hipStreamSynchronize(s));
+  g_msm_laps.lap("msm_device");
   out->resize(B);
   pool().parallel_for((int)B, [&](int b) {
     h::HExt run = h::hext_identity(), acc = h::hext_identity();
@@ -165,6 +171,7 @@ static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& h
     }
     (*out)[b] = compress(acc);
   });
+  g_msm_laps.lap("msm_host_final");
   return 0;
 }
 
@@ -300,6 +307,8 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   out->z1 = fq_add(d, fq_mul(c, y_hat));
   out->z2 = fq_add(fq_mul(a_hat, fq_add(fq_mul(c, blind_fin), r_beta)), r_delta);
   if (Cy_out) *Cy_out = Cy;
+  g_msm_laps.lap("bullet_host");
+  g_msm_laps.print();
   return 0;
 }
 
