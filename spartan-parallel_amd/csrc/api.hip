@@ -1,3 +1,4 @@
+#include <algorithm>
 #include <chrono>
 #include <string.h>
 // spg — context management for the C-ABI (include/spg.h).
@@ -11,6 +12,23 @@ namespace spg {
 int set_err(spg_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
+}
+
+void* pinned_get(spg_ctx* c, size_t bytes) {
+  if (bytes <= c->pinned_bytes) return c->pinned;
+  if (c->pinned) {
+    hipStreamSynchronize(c->stream);  // the old staging may still be the source or target of a copy
+    hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
+  }
+  size_t sz = std::max<size_t>((bytes + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1), 1 << 20);
+  if (hipHostMalloc(&c->pinned, sz) != hipSuccess) {
+    c->pinned = nullptr;
+    return nullptr;
+  }
+  c->pinned_bytes = sz;
+  return c->pinned;
 }
 
 void* ws_get(spg_ctx* c, size_t slot, size_t bytes) {
@@ -96,7 +114,7 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipHostMalloc(&c->pinned, 4096) != hipSuccess || hipMalloc(&c->d_counter, 64) != hipSuccess ||
+      hipMalloc(&c->d_counter, 64) != hipSuccess ||
       hipMemset(c->d_counter, 0, 64) != hipSuccess) {
     delete c;
     return SPG_E_HIP;

@@ -13,7 +13,8 @@ struct spg_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  void* pinned = nullptr;          // 4 KiB page-locked host staging for per-round device->host scalars
+  void* pinned = nullptr;          // page-locked host staging (pinned_get), grown on demand
+  size_t pinned_bytes = 0;
   unsigned* d_counter = nullptr;   // grid-reduction ticket (zero between launches)
   // mailbox in fine-grained (coherent, mapped) host memory: a kernel's last block posts a round's scalars
   // and a sequence number with system-scope stores; the host spins on the number instead of a D2H copy +
@@ -81,6 +82,10 @@ int set_err(spg_ctx* c, int code, const std::string& msg);
 
 // returns a device buffer of at least `bytes` for workspace slot `slot` (contents undefined)
 void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
+
+// page-locked host staging of at least `bytes` (contents undefined; valid until the next larger request,
+// which synchronises the stream before freeing the old buffer)
+void* pinned_get(spg_ctx* c, size_t bytes);
 
 // timing bracket on the context stream
 void timer_start(spg_ctx* c);

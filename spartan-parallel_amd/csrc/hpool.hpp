@@ -92,7 +92,7 @@ inline Pool& pool() {
   static Pool p([] {
     unsigned hw = std::thread::hardware_concurrency();
     int n = hw > 1 ? (int)hw - 1 : 0;
-    return n > 7 ? 7 : n;
+    return n > 15 ? 15 : n;  // the GPU box grants 16 host threads per GPU process
   }());
   return p;
 }

@@ -142,35 +142,65 @@ DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyVie
 // SPG_TRACE >= 2: where a Bullet round's time goes (accumulated over a process, printed per DotProductProofLog)
 static Laps g_msm_laps{"DotProductProofLog::prove (cumulative)", getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2};
 
+static h::HExt hext_small_mul(h::HExt P, unsigned k) {
+  h::HExt r = h::hext_identity();
+  for (; k; k >>= 1) {
+    if (k & 1) r = h::hext_add(r, P);
+    P = h::hext_dbl(P);
+  }
+  return r;
+}
+
+void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out) {
+  // chunk (lo, hi] of a bucket set: run = sum B_v, acc = sum (v - lo) B_v; the set's sum is
+  // sum over chunks of acc + lo * run. Chunks spread one MSM's 2 NB dependent additions over the pool.
+  const int K = NB >= 64 ? 8 : 1, per = NB / K;
+  std::vector<h::HExt> part(B * K);
+  pool().parallel_for((int)(B * K), [&](int task) {
+    const size_t b = task / K;
+    const int lo = (task % K) * per;
+    h::HExt run = h::hext_identity(), acc = h::hext_identity();
+    for (int v = lo + per; v > lo; v--) {
+      run = h::hext_add(run, h::hext_from_dev(bk[b * NB + v - 1]));
+      acc = h::hext_add(acc, run);
+    }
+    part[task] = lo ? h::hext_add(acc, hext_small_mul(run, (unsigned)lo)) : acc;
+  });
+  auto fin = [&](int b) {
+    h::HExt s = part[(size_t)b * K];
+    for (int c = 1; c < K; c++) s = h::hext_add(s, part[(size_t)b * K + c]);
+    out[b] = compress(s);
+  };
+  if (B <= 2)
+    for (int b = 0; b < (int)B; b++) fin(b);
+  else
+    pool().parallel_for((int)B, fin);
+}
+
+// B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
 static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& hs, size_t n, size_t B,
                            const uint32_t* d_idx, std::vector<Pt>* out) {
   hipStream_t s = ctx->stream;
   g_msm_laps.lap("bullet_host");
-  Fq* d_s = (Fq*)ws_get(ctx, 20, hs.size() * sizeof(Fq) + 64);
-  Ext* d_o = (Ext*)ws_get(ctx, 22, sizeof(Ext) * B + 64);
-  if (!d_s || !d_o) return set_err(ctx, SPG_E_NOMEM, "device_msm");
-  SPG_HIP(ctx, hipMemcpyAsync(d_s, hs.data(), hs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
+  const size_t in_bytes = hs.size() * sizeof(Fq), bk_bytes = sizeof(Ext) * B * 256;
+  Fq* d_s = (Fq*)ws_get(ctx, 20, in_bytes + 64);
+  Ext* d_bk = (Ext*)ws_get(ctx, 23, bk_bytes + 64);
+  uint8_t* stage = (uint8_t*)pinned_get(ctx, in_bytes + bk_bytes + 256);
+  if (!d_s || !d_bk || !stage) return set_err(ctx, SPG_E_NOMEM, "device_msm");
+  // scalars up through page-locked staging (a pageable source costs a staging copy + blit per call)
+  memcpy(stage, hs.data(), in_bytes);
+  SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, in_bytes, hipMemcpyHostToDevice, s));
   // bucket sums on the device; sum_v v * B_v and the encoding on host cores (a short dependent chain of
   // additions is ~50x faster there than on one GPU lane)
-  Ext* d_bk = (Ext*)ws_get(ctx, 23, sizeof(Ext) * B * 256 + 64);
-  if (!d_bk) return set_err(ctx, SPG_E_NOMEM, "device_msm buckets");
   int NB = 0;
   int rc = msm_small_buckets(ctx, g.dev, 0, d_s, n, B, nullptr, d_idx, -1, d_bk, &NB);
   if (rc) return rc;
-  (void)d_o;
-  std::vector<Ext> bk(B * (size_t)NB);
-  SPG_HIP(ctx, hipMemcpyAsync(bk.data(), d_bk, sizeof(Ext) * bk.size(), hipMemcpyDeviceToHost, s));
+  Ext* bk = (Ext*)(stage + ((in_bytes + 255) & ~(size_t)255));
+  SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * B * NB, hipMemcpyDeviceToHost, s));
   SPG_HIP(ctx, hipStreamSynchronize(s));
   g_msm_laps.lap("msm_device");
   out->resize(B);
-  pool().parallel_for((int)B, [&](int b) {
-    h::HExt run = h::hext_identity(), acc = h::hext_identity();
-    for (int v = NB; v >= 1; v--) {  // running sum: acc = sum_v v * B_v
-      run = h::hext_add(run, h::hext_from_dev(bk[(size_t)b * NB + v - 1]));
-      acc = h::hext_add(acc, run);
-    }
-    (*out)[b] = compress(acc);
-  });
+  bucket_finals(bk, B, NB, out->data());
   g_msm_laps.lap("msm_host_final");
   return 0;
 }

@@ -241,11 +241,12 @@ namespace spg {
 static unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
 // Hyrax rows up to this many scalars go through the latency MSM path (one block per bucket and row)
 static const size_t kSmallRowMax = 256;
+static const size_t kHostFinalRows = 64;  // latency-path commits of at most this many rows finish on the host
 // workspace slots of this file
 enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
-  kWsTops
+  kWsTops, kWsCommitBk
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -277,11 +278,26 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
   for (size_t r0 = 0; r0 < L; r0 += chunk) {
     size_t nb = std::min(chunk, L - r0);
     auto t0 = std::chrono::steady_clock::now();
-    int rc = small ? msm_small_compressed(ctx, g.dev, 0, d_Z + r0 * R, R, nb, d_out)
-                   : msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr, (long)(g.n_pc + 1));
-    if (rc) return rc;
-    SPG_HIP(ctx, hipMemcpyAsync(out + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
-    SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
+    if (small && nb <= kHostFinalRows) {
+      // few rows: the bucket running sums and encodings are cheaper on host cores than the device's
+      // one-lane-per-row final + compress (~0.25 ms floor)
+      Ext* d_bk = (Ext*)ws_get(ctx, kWsCommitBk, sizeof(Ext) * nb * 256 + 64);
+      Ext* bk = (Ext*)pinned_get(ctx, sizeof(Ext) * nb * 256);
+      if (!d_bk || !bk) return set_err(ctx, SPG_E_NOMEM, "commit buckets");
+      int NB = 0;
+      int rc = msm_small_buckets(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, nullptr, -1, d_bk, &NB);
+      if (rc) return rc;
+      SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * nb * NB, hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      bucket_finals(bk, nb, NB, out + r0);
+    } else {
+      int rc = small ? msm_small_compressed(ctx, g.dev, 0, d_Z + r0 * R, R, nb, d_out)
+                     : msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr,
+                                        (long)(g.n_pc + 1));
+      if (rc) return rc;
+      SPG_HIP(ctx, hipMemcpyAsync(out + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
+    }
     if (trace2)
       fprintf(stderr, "[spg] commit rows=%zu R=%zu %s %.0f us\n", nb, R, small ? "small" : "batch",
               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
