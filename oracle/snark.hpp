@@ -993,15 +993,12 @@ static inline bool check_bound_rp(const FqVec& list, const FqVec& rp, const Fq b
 
 // Replays SNARK::prove's transcript with the verifier's knowledge (public inputs, instance commitments, the
 // proof) and checks the three R1CSProofs, their R1CSEvalProofs and the permutation-product identity
-// (lib.rs:2750-3881, the memory-free parts). Returns 0 when all checks pass, else the failing stage.
+// (lib.rs:2750-3881; shift and IO proofs are not re-checked). Returns 0 when all checks pass, else the failing stage.
 static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const SnarkInst& block,
                                const SnarkInst& pairwise, const SnarkInst& perm_root, const R1CSGens& vars_gens,
                                Transcript& t) {
   const size_t niu = in.num_inputs_unpadded, num_ios = in.num_ios;
   const DotGens& gpc = vars_gens.gens_pc;
-  if (in.total_num_init_phy_mem_accesses || in.total_num_init_vir_mem_accesses || in.total_num_phy_mem_accesses ||
-      in.total_num_vir_mem_accesses)
-    return 100;  // the self-check covers memory-free programs
   t.append_protocol_name("Spartan SNARK proof");
   auto app = [&](const char* l, size_t v) { t.append_scalar(l, fq_from_u64(v)); };
   app("func_input_width", in.func_input_width);
@@ -1016,10 +1013,10 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
   app("block_max_num_proofs", in.block_max_num_proofs);
   for (auto p : in.block_num_phy_ops) app("block_num_phy_ops", p);
   for (auto v : in.block_num_vir_ops) app("block_num_vir_ops", v);
-  app("total_num_init_phy_mem_accesses", 0);
-  app("total_num_init_vir_mem_accesses", 0);
-  app("total_num_phy_mem_accesses", 0);
-  app("total_num_vir_mem_accesses", 0);
+  app("total_num_init_phy_mem_accesses", in.total_num_init_phy_mem_accesses);
+  app("total_num_init_vir_mem_accesses", in.total_num_init_vir_mem_accesses);
+  app("total_num_phy_mem_accesses", in.total_num_phy_mem_accesses);
+  app("total_num_vir_mem_accesses", in.total_num_vir_mem_accesses);
   app("block_max_num_proofs", in.block_max_num_proofs);
   for (auto n : in.block_num_proofs) app("block_num_proofs", n);
   for (auto& b : block.label_map)
@@ -1048,8 +1045,18 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
   R1CSInstance block_sorted = block.inst;
   block_sorted.sort(P, order);
   const size_t bmax = next_pow2(in.block_max_num_proofs), consis = next_pow2(in.consis_num_proofs);
+  // padded memory sizes and the pairwise sort (lib.rs:2951-3009)
+  auto pad0 = [](size_t v) { return v == 0 ? size_t(0) : next_pow2(v); };
+  const size_t t_iphy = pad0(in.total_num_init_phy_mem_accesses), t_ivir = pad0(in.total_num_init_vir_mem_accesses),
+               t_phy = pad0(in.total_num_phy_mem_accesses), t_vir = pad0(in.total_num_vir_mem_accesses);
+  std::vector<std::pair<size_t, size_t>> ps = {{consis, 0}, {t_phy, 1}, {t_vir, 2}};
+  std::stable_sort(ps.begin(), ps.end(), [](const std::pair<size_t, size_t>& a, const std::pair<size_t, size_t>& b) {
+    return a.first > b.first;
+  });
+  std::vector<size_t> pw_index;
+  for (size_t i = 0; i < 1 + (t_phy > 0) + (t_vir > 0); i++) pw_index.push_back(ps[i].second);
   R1CSInstance pairwise_sorted = pairwise.inst;
-  pairwise_sorted.sort(1, {0});
+  pairwise_sorted.sort(pw_index.size(), pw_index);
   // commitments, in the prover's order
   Fq tau = t.challenge_scalar("challenge_tau"), r = t.challenge_scalar("challenge_r");
   FqVec perm_w0 = {tau};
@@ -1073,8 +1080,60 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
     append_polycomm(t, "poly_commitment", pf.block_comm_w3_list[p]);
     append_polycomm(t, "poly_commitment", pf.block_comm_w3_list_shifted[p]);
   }
+  // memory (w2, w3, w3_shifted) triples (lib.rs:3100-3240)
+  auto mem_vsecs = [&](size_t total, size_t width, const PolyCommitment& c2, const PolyCommitment& c3,
+                       const PolyCommitment& c3s, VSec* w2, VSec* w3, VSec* w3s) {
+    if (total == 0) return;
+    append_polycomm(t, "poly_commitment", c2);
+    append_polycomm(t, "poly_commitment", c3);
+    append_polycomm(t, "poly_commitment", c3s);
+    *w2 = vsec({width}, {total}, {c2});
+    *w3 = vsec({8}, {total}, {c3});
+    *w3s = vsec({8}, {total}, {c3s});
+  };
+  VSec ip2, ip3, ip3s, iv2, iv3, iv3s, pa2, pa3, pa3s, va2, va3, va3s;
+  mem_vsecs(t_iphy, INIT_PHY_MEM_WIDTH, pf.init_phy_mem_comm_w2, pf.init_phy_mem_comm_w3,
+            pf.init_phy_mem_comm_w3_shifted, &ip2, &ip3, &ip3s);
+  mem_vsecs(t_ivir, INIT_VIR_MEM_WIDTH, pf.init_vir_mem_comm_w2, pf.init_vir_mem_comm_w3,
+            pf.init_vir_mem_comm_w3_shifted, &iv2, &iv3, &iv3s);
+  mem_vsecs(t_phy, PHY_MEM_WIDTH, pf.phy_mem_addr_comm_w2, pf.phy_mem_addr_comm_w3, pf.phy_mem_addr_comm_w3_shifted,
+            &pa2, &pa3, &pa3s);
+  mem_vsecs(t_vir, VIR_MEM_WIDTH, pf.vir_mem_addr_comm_w2, pf.vir_mem_addr_comm_w3, pf.vir_mem_addr_comm_w3_shifted,
+            &va2, &va3, &va3s);
   for (auto& c : pf.block_comm_vars_list) append_polycomm(t, "poly_commitment", c);
   append_polycomm(t, "poly_commitment", pf.exec_comm_inputs[0]);
+  // the verifier rebuilds the init lists from the public input stack / input memory (lib.rs:3274-3333):
+  // entry i = (1, 0, i, value_i), zero-padded to the power of two
+  auto init_vsec = [&](size_t total, size_t n, const std::vector<FqVec>& lst, size_t width) {
+    VSec v;
+    if (n == 0) return v;
+    FqVec flat(total * width, fq_zero());
+    for (size_t i = 0; i < n; i++) {
+      flat[i * width] = fq_one();
+      flat[i * width + 2] = fq_from_u64(i);
+      flat[i * width + 3] = lst[i][3];
+    }
+    PolyCommitment c = poly_commit(DensePoly(flat), gpc);
+    append_polycomm(t, "poly_commitment", c);
+    return vsec({width}, {total}, {c});
+  };
+  VSec init_phy_v = init_vsec(t_iphy, in.total_num_init_phy_mem_accesses, in.init_phy_mems_list, INIT_PHY_MEM_WIDTH);
+  VSec init_vir_v = init_vsec(t_ivir, in.total_num_init_vir_mem_accesses, in.init_vir_mems_list, INIT_VIR_MEM_WIDTH);
+  VSec addr_phy_v, addr_phy_sv, addr_vir_v, addr_vir_sv, ts_bits_v;
+  if (t_phy > 0) {
+    append_polycomm(t, "poly_commitment", pf.addr_comm_phy_mems);
+    append_polycomm(t, "poly_commitment", pf.addr_comm_phy_mems_shifted);
+    addr_phy_v = vsec({PHY_MEM_WIDTH}, {t_phy}, {pf.addr_comm_phy_mems});
+    addr_phy_sv = vsec({PHY_MEM_WIDTH}, {t_phy}, {pf.addr_comm_phy_mems_shifted});
+  }
+  if (t_vir > 0) {
+    append_polycomm(t, "poly_commitment", pf.addr_comm_vir_mems);
+    append_polycomm(t, "poly_commitment", pf.addr_comm_vir_mems_shifted);
+    append_polycomm(t, "poly_commitment", pf.addr_comm_ts_bits);
+    addr_vir_v = vsec({VIR_MEM_WIDTH}, {t_vir}, {pf.addr_comm_vir_mems});
+    addr_vir_sv = vsec({VIR_MEM_WIDTH}, {t_vir}, {pf.addr_comm_vir_mems_shifted});
+    ts_bits_v = vsec({in.mem_addr_ts_bits_size}, {t_vir}, {pf.addr_comm_ts_bits});
+  }
   // BLOCK_CORRECTNESS_EXTRACT
   std::vector<size_t> w2sz;
   for (size_t p = 0; p < P; p++)
@@ -1102,15 +1161,28 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
         return 4;
     }
   }
-  // PAIRWISE_CHECK (consistency only)
+  // PAIRWISE_CHECK (lib.rs:3474-3568): CONSIS_CHECK, PHY_MEM_COHERE, VIR_MEM_COHERE
   VSec pe3 = vsec({8}, {consis}, {pf.perm_exec_comm_w3_list}), pe3s = vsec({8}, {consis}, {pf.perm_exec_comm_w3_shifted});
   const size_t pw_nv = std::max<size_t>(8, in.mem_addr_ts_bits_size);
-  if (!r1cs_verify(pf.pairwise_check_r1cs_sat_proof, 1, consis, {consis}, pw_nv, {&pe3, &pe3s, &w0},
-                   pairwise_sorted.max_num_cons, vars_gens, pf.pairwise_check_inst_evals_bound_rp, t, &ch))
+  std::vector<size_t> pw_map, pw_map2;
+  VSec pw = VSec::merge({&pe3, &addr_phy_v, &addr_vir_v}, &pw_map);
+  VSec pws = VSec::merge({&pe3s, &addr_phy_sv, &addr_vir_sv}, &pw_map2);
+  VSec pwb;
+  {
+    std::vector<const VSec*> comps(pw_map.size(), &w0);
+    for (size_t i = 0; i < pw_map.size(); i++)
+      if (pw_map[i] == 2) comps[i] = &ts_bits_v;
+    pwb = VSec::concat(comps);
+  }
+  const size_t pairwise_size = std::max({consis, t_phy, t_vir});
+  if (!r1cs_verify(pf.pairwise_check_r1cs_sat_proof, pw.num_proofs.size(), pairwise_size, pw.num_proofs, pw_nv,
+                   {&pw, &pws, &pwb}, pairwise_sorted.max_num_cons, vars_gens, pf.pairwise_check_inst_evals_bound_rp,
+                   t, &ch))
     return 5;
   {
     const FqVec &rp = ch[0], &rx = ch[2], &ry = ch[3];
-    if (!check_bound_rp(pf.pairwise_check_inst_evals_list, rp, pf.pairwise_check_inst_evals_bound_rp, {0})) return 6;
+    if (!check_bound_rp(pf.pairwise_check_inst_evals_list, rp, pf.pairwise_check_inst_evals_bound_rp, pw_index))
+      return 6;
     for (auto& e : pf.pairwise_check_inst_evals_list) t.append_scalar("ABCr_claim", e);
     t.challenge_scalar("challenge_c0");
     t.challenge_scalar("challenge_c1");
@@ -1119,10 +1191,16 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
                       pf.pairwise_check_inst_evals_list, pairwise.gens.gens, t))
       return 7;
   }
-  // PERM_ROOT
-  VSec w1 = vsec({num_ios}, {consis}, {pf.exec_comm_inputs[0]}), pw2 = vsec({num_ios}, {consis}, {pf.perm_exec_comm_w2_list});
-  if (!r1cs_verify(pf.perm_root_r1cs_sat_proof, 1, consis, {consis}, num_ios, {&w0, &w1, &pw2, &pe3, &pe3s},
-                   perm_root.inst.max_num_cons, vars_gens, pf.perm_root_inst_evals, t, &ch))
+  // PERM_EXEC_ROOT, MEM_ADDR_ROOT (lib.rs:3569-3650)
+  VSec ex1 = vsec({num_ios}, {consis}, {pf.exec_comm_inputs[0]}), pw2 = vsec({num_ios}, {consis}, {pf.perm_exec_comm_w2_list});
+  std::vector<size_t> mm;
+  VSec r1 = VSec::merge({&ex1, &init_phy_v, &init_vir_v, &addr_phy_v, &addr_vir_v}, &mm);
+  VSec r2 = VSec::merge({&pw2, &ip2, &iv2, &pa2, &va2}, &mm);
+  VSec r3 = VSec::merge({&pe3, &ip3, &iv3, &pa3, &va3}, &mm);
+  VSec r3s = VSec::merge({&pe3s, &ip3s, &iv3s, &pa3s, &va3s}, &mm);
+  const size_t perm_size = std::max({consis, t_iphy, t_ivir, t_phy, t_vir});
+  if (!r1cs_verify(pf.perm_root_r1cs_sat_proof, r1.num_proofs.size(), perm_size, r1.num_proofs, num_ios,
+                   {&w0, &r1, &r2, &r3, &r3s}, perm_root.inst.max_num_cons, vars_gens, pf.perm_root_inst_evals, t, &ch))
     return 8;
   {
     const FqVec &rx = ch[2], &ry = ch[3];
@@ -1133,18 +1211,34 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
     if (!spark_verify(pf.perm_root_r1cs_eval_proof, perm_root.comms[0].comm, rx, ry, e, perm_root.gens.gens, t))
       return 9;
   }
-  // PERM_PRODUCT identity (lib.rs:3712-3770): exec side product == block side product
+  // PERM_PRODUCT identities (lib.rs:3652-3772): exec == block, phy block == phy addr, vir block == vir addr
   {
-    VSec bw3c = bw3;
+    std::vector<const VSec*> comps = {&pe3, &ip3, &iv3, &pa3, &va3, &bw3};
+    if (in.max_block_num_phy_ops > 0) comps.push_back(&bw3);
+    if (in.max_block_num_vir_ops > 0) comps.push_back(&bw3);
     std::vector<size_t> im;
-    VSec m = VSec::merge({&pe3, &bw3c}, &im);  // components 0 (perm_exec) and 5 (perm_block) of the reference
+    VSec m = VSec::merge(comps, &im);
     if (pf.perm_poly_poly_list.size() != m.num_proofs.size()) return 10;
-    Fq pe = fq_one(), pb = fq_one();
+    Fq pe = fq_one(), pb = fq_one(), pmb = fq_one(), pma = fq_one(), vmb = fq_one(), vma = fq_one();
     for (size_t i = 0; i < im.size(); i++) {
-      if (im[i] == 0) pe = fq_mul(pe, pf.perm_poly_poly_list[i]);
-      else pb = fq_mul(pb, pf.perm_poly_poly_list[i]);
+      const Fq& v = pf.perm_poly_poly_list[i];
+      switch (im[i]) {
+        case 0: pe = fq_mul(pe, v); break;
+        case 1: pmb = fq_mul(pmb, v); break;
+        case 2: vmb = fq_mul(vmb, v); break;
+        case 3: pma = fq_mul(pma, v); break;
+        case 4: vma = fq_mul(vma, v); break;
+        case 5: pb = fq_mul(pb, v); break;
+        case 6:
+          if (in.max_block_num_phy_ops > 0) pmb = fq_mul(pmb, v);
+          else vmb = fq_mul(vmb, v);
+          break;
+        case 7: vmb = fq_mul(vmb, v); break;
+      }
     }
     if (!(pe == pb)) return 11;
+    if (!(pmb == pma)) return 12;
+    if (!(vmb == vma)) return 13;
   }
   return 0;
 }

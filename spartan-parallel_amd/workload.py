@@ -415,27 +415,35 @@ class SnarkWorkload:
     built by restatements of Instance::gen_block_inst / gen_pairwise_check_inst / gen_perm_root_inst, and the
     block constraints fill 2^log_cons rows after the permutation rows are added."""
 
-    NIU = 4  # num_inputs_unpadded: (v, _, i0, i1, i2 | o0, o1, o2) -> num_ios = 8
+    NIU = 4  # default num_inputs_unpadded: (v, _, i0, i1, i2 | o0, o1, o2) -> num_ios = 8
 
-    def __init__(self, num_blocks=2, log_cons=10, log_proofs=9, num_vars=1024, max_ts_width=2, seed=0x5350415254414E31):
-        niu = self.NIU
+    def __init__(self, num_blocks=2, log_cons=10, log_proofs=9, num_vars=1024, max_ts_width=2, seed=0x5350415254414E31,
+                 phy_ops=0, vir_ops=0, init_phy=0, init_vir=0, niu=None):
+        # niu >= 5 is needed for virtual memory: a VIR entry's timestamp (column 5) must fall on an input slot of
+        # the perm-root instance, whose output slots must be zero for memory entries (ZO = 0)
+        niu = niu or self.NIU
         self.num_blocks = num_blocks
         self.num_vars = num_vars
         self.num_inputs_unpadded = niu
         self.num_ios = 1 << (2 * niu - 1).bit_length()
         io_width = 2 * niu
-        extra = (niu - 2) + (niu - 1) + 4 + 3 + 3
+        assert vir_ops in (0, 2), "virtual memory: each execution stores then loads one cell (2 ops)"
+        # memory-op variables (PA, PD)*phy_ops then (VA, VD, VL, VT)*vir_ops follow the io block
+        # (Instance::gen_block_inst layout, src/instance.rs:268-283); the squaring chain follows them
+        base = io_width + 2 * phy_ops + 4 * vir_ops
+        extra = (niu - 2) + (niu - 1) + 4 + 3 + 3 + 2 * phy_ops + 4 * vir_ops
         m = (1 << log_cons) - extra - 3
-        assert m >= 1 and io_width + m + 1 <= num_vars, "num_vars too small for the chain"
+        assert m >= 1 and base + m + 1 <= num_vars, "num_vars too small for the chain"
         self.chain = m
+        self.chain_base = base
         # user constraints of every block (A, B, C lists of (col, int) per row)
         V_in, V_out = (lambda i: 2 + i), (lambda i: 2 + (niu - 1) + i)
-        rows = [([(V_in(1), 1)], [(0, 1)], [(io_width, 1)])]
-        rows += [([(io_width + j - 1, 1)], [(io_width + j - 1, 1)], [(io_width + j, 1)]) for j in range(1, m + 1)]
-        rows += [([(io_width + m, 1)], [(0, 1)], [(V_out(1), 1)]), ([(V_in(2), 1)], [(0, 1)], [(V_out(2), 1)])]
+        rows = [([(V_in(1), 1)], [(0, 1)], [(base, 1)])]
+        rows += [([(base + j - 1, 1)], [(base + j - 1, 1)], [(base + j, 1)]) for j in range(1, m + 1)]
+        rows += [([(base + m, 1)], [(0, 1)], [(V_out(1), 1)]), ([(V_in(2), 1)], [(0, 1)], [(V_out(2), 1)])]
         args = [rows for _ in range(num_blocks)]
-        self.block_num_phy_ops = [0] * num_blocks
-        self.block_num_vir_ops = [0] * num_blocks
+        self.block_num_phy_ops = [phy_ops] * num_blocks
+        self.block_num_vir_ops = [vir_ops] * num_blocks
         self.block_num_vars, self.block_max_num_cons, self.block_nnz, self.block_inst = gen_block_inst(
             num_vars, args, niu, self.block_num_phy_ops, self.block_num_vir_ops)
         self.max_ts_width = max_ts_width
@@ -445,9 +453,25 @@ class SnarkWorkload:
         self.perm_root_num_cons, self.perm_root_nnz, self.perm_root_inst = gen_perm_root_inst(niu, self.num_ios)
         # ---- execution trace
         E = num_blocks << log_proofs
-        seeds, _ = random_fq(2, seed)
+        seeds, st = random_fq(2, seed)
         x, y = int(seeds[0]), int(seeds[1])
         self.x0 = x
+        # Memory trace, consistent with the verifier's memory checks (src/lib.rs:3275-3330 init lists,
+        # :3474-3568 PHY/VIR_MEM_COHERE, :3652-3772 permutation products):
+        #  * physical: the input stack init_phy_mems = (1, 0, a, stack[a]) for a < init_phy; execution k, op i
+        #    reads cell (k * phy_ops + i) mod init_phy;
+        #  * virtual: input memory init_vir_mems = (1, 0, a, mem[a]) for a < init_vir (ls = ts = 0); execution
+        #    k stores a fresh value into cell k mod init_vir and loads it back, both at timestamp k // init_vir + 1.
+        #  The address-sorted lists hold the init entries and every block access.
+        assert not phy_ops or init_phy > 0, "physical ops read the input stack"
+        assert not vir_ops or init_vir > 0, "virtual ops need an input memory"
+        stack, st = random_fq(max(init_phy, 1), st)
+        imem, st = random_fq(max(init_vir, 1), st)
+        vir_data, st = random_fq(max(E, 1), st)
+        self.input_stack = [int(v) for v in stack[:init_phy]]
+        self.input_mem = [int(v) for v in imem[:init_vir]]
+        phy_acc = [(a, self.input_stack[a]) for a in range(init_phy)]
+        vir_acc = [(a, self.input_mem[a], 0, 0) for a in range(init_vir)]
         per_block = [[] for _ in range(num_blocks)]
         exec_rows = []
         for k in range(E):
@@ -457,9 +481,18 @@ class SnarkWorkload:
             for _ in range(m):
                 chain.append(chain[-1] * chain[-1] % Q)
             xo = chain[-1]
-            io = [1, 0, b, x, y, nb, xo, y]
+            io = [1, 0, b, x, y] + [0] * (niu - 4) + [nb, xo, y] + [0] * (niu - 4)
             exec_rows.append(io + [0] * (self.num_ios - len(io)))
-            row = io + chain + [0] * (num_vars - io_width - len(chain))
+            memv = []
+            for i in range(phy_ops):
+                a = (k * phy_ops + i) % init_phy
+                memv += [a, self.input_stack[a]]
+                phy_acc.append((a, self.input_stack[a]))
+            if vir_ops:
+                a, d, ts = k % init_vir, int(vir_data[k]), k // init_vir + 1
+                memv += [a, d, 0, ts, a, d, 1, ts]
+                vir_acc += [(a, d, 0, ts), (a, d, 1, ts)]
+            row = io + memv + chain + [0] * (num_vars - base - len(chain))
             per_block[b].append(row)
             x = xo
         self.output = x
@@ -469,6 +502,29 @@ class SnarkWorkload:
                            for r in per_block]
         self.consis_num_proofs = E
         self.exec_inputs = to_mont_limbs(np.array(exec_rows, dtype=object).reshape(-1)).reshape(E, self.num_ios, 4)
+
+        # D = v_next * (v + addr - addr_next) (gen_pairwise_check_inst, src/instance.rs:815-1060)
+        def mems(acc, width):
+            out = []
+            for j, e in enumerate(acc):
+                D = 0 if j + 1 == len(acc) else (1 + e[0] - acc[j + 1][0]) % Q
+                out.append([1, D] + list(e) + [0] * (width - 2 - len(e)))
+            return out
+        phy_acc.sort(key=lambda e: e[0])  # stable: the init entry of a cell precedes its reads
+        vir_acc.sort(key=lambda e: (e[0], e[3], e[2]))
+        self.init_phy_mems = [[1, 0, a, v] for a, v in enumerate(self.input_stack)]
+        self.init_vir_mems = [[1, 0, a, v] for a, v in enumerate(self.input_mem)]
+        self.addr_phy_mems = mems(phy_acc, 4) if phy_ops else []
+        self.addr_vir_mems = mems(vir_acc, 8) if vir_ops else []
+        # timestamp aux row (D2, EQ, B_0..): D2 = D1 * ls_next, D1 * (ts_next - ts) = EQ + sum 2^i B_i
+        self.addr_ts_bits = []
+        for j, e in enumerate(self.addr_vir_mems):
+            nxt = self.addr_vir_mems[j + 1] if j + 1 < len(self.addr_vir_mems) else [0] * 8
+            diff = (nxt[5] - e[5]) % Q if e[1] else 0
+            assert diff < (1 << max_ts_width)
+            bits = [(diff >> i) & 1 for i in range(max_ts_width)]
+            row = [e[1] * nxt[4] % Q, 0] + bits
+            self.addr_ts_bits.append(row + [0] * (self.mem_addr_ts_bits_size - len(row)))
         self.input_block_num = 0
         self.output_block_num = num_blocks
         self.input_liveness = [False, False, True]
@@ -567,4 +623,14 @@ class SnarkViews:
         c.consis_num_proofs = wl.consis_num_proofs
         c.block_vars = bv
         c.exec_inputs = arr(wl.exec_inputs)
+
+        def mem_list(rows):
+            if not rows:
+                return 0, None
+            return len(rows), arr(to_mont_limbs(np.array(rows, dtype=object).reshape(-1)))
+        c.total_num_init_phy_mem_accesses, c.init_phy_mems = mem_list(getattr(wl, "init_phy_mems", []))
+        c.total_num_init_vir_mem_accesses, c.init_vir_mems = mem_list(getattr(wl, "init_vir_mems", []))
+        c.total_num_phy_mem_accesses, c.addr_phy_mems = mem_list(getattr(wl, "addr_phy_mems", []))
+        c.total_num_vir_mem_accesses, c.addr_vir_mems = mem_list(getattr(wl, "addr_vir_mems", []))
+        _, c.addr_ts_bits = mem_list(getattr(wl, "addr_ts_bits", []))
         self.inputs = c

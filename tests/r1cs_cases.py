@@ -31,8 +31,15 @@ SNARK_CASES = {
     "b2_x32_q2": dict(num_blocks=2, log_cons=5, log_proofs=1, num_vars=32),
     "b3_x32_q4": dict(num_blocks=3, log_cons=5, log_proofs=2, num_vars=32),
     "b2_x64_q8": dict(num_blocks=2, log_cons=6, log_proofs=3, num_vars=64),
+    # memory programs: physical reads of the input stack, virtual store/load pairs (needs niu >= 5), both
+    "mem_phy_b2_x64_q4": dict(num_blocks=2, log_cons=6, log_proofs=2, num_vars=64, phy_ops=2, init_phy=5),
+    "mem_vir_b2_x64_q4": dict(num_blocks=2, log_cons=6, log_proofs=2, num_vars=64, vir_ops=2, init_vir=3, niu=5),
+    "mem_both_b3_x64_q2": dict(num_blocks=3, log_cons=6, log_proofs=1, num_vars=64, phy_ops=1, vir_ops=2, init_phy=3,
+                               init_vir=5, niu=5),
 }
 GPU_SNARK_CASES = {
     "b2_x1024_q8": dict(num_blocks=2, log_cons=10, log_proofs=3, num_vars=1024),
     "b2_x256_q64": dict(num_blocks=2, log_cons=8, log_proofs=6, num_vars=256),
+    "mem_both_b2_x256_q32": dict(num_blocks=2, log_cons=8, log_proofs=5, num_vars=256, phy_ops=3, vir_ops=2,
+                                 init_phy=20, init_vir=7, niu=5),
 }

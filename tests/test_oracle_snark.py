@@ -50,3 +50,21 @@ def test_snark_workload_is_satisfied():
                 acc += val(e) * z[int(e[1])]
             s.append(acc % Q)
         assert s[0] * s[1] % Q == s[2], row
+
+
+@pytest.mark.parametrize("what", ["phy_data", "vir_data", "ts_bits"])
+def test_snark_memory_trace_is_checked(oracle, what):
+    """the oracle verifier rejects a memory trace whose address-sorted list disagrees with the block accesses
+    (permutation identities, lib.rs:3652-3772) or breaks the coherence rows (PHY/VIR_MEM_COHERE)"""
+    import workload
+
+    wl = workload.SnarkWorkload(num_blocks=2, log_cons=6, log_proofs=1, num_vars=64, phy_ops=1, vir_ops=2,
+                                init_phy=2, init_vir=2, niu=5)
+    if what == "phy_data":
+        wl.addr_phy_mems[-1][3] += 1
+    elif what == "vir_data":
+        wl.addr_vir_mems[-1][3] += 1
+    else:
+        wl.addr_ts_bits[0][2] ^= 1
+    _, rc = oracle.snark_prove(wl, workload.tape_seed())
+    assert rc != 0
