@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="replicas", choices=["replicas", "shard"])
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
-    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark"],
+    ap.add_argument("--log-msm", type=int, default=16, help="msm: 2^k (scalar, generator) pairs")
+    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark", "msm"],
                     help="snark: the headline metric (SNARK::prove, SURVEY 8d config 3); r1cs: its block "
                          "R1CSProof::prove alone; spark: SURVEY 8d config 5 (SPARK)")
     ap.add_argument("--log-cons", type=int, default=10, help="snark: 2^k constraints per block")
@@ -68,6 +69,8 @@ def main():
         return main_spark(a)
     if a.workload == "snark":
         return main_snark(a)
+    if a.workload == "msm":
+        return main_msm(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -333,6 +336,125 @@ def main_snark(a):
             "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
             "value_incl_witness_upload": round(N * world / t_incl, 1), "encode_s": round(t_encode, 3),
             "host_gen_s": round(t_gen, 3), "kernels": kernels}))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def msm_scalars(n):
+    """SURVEY 8d config 2 scalars: uniform Fq (splitmix64 seed 1) with edge cases 0, 1, 2, q-1, q-2, 2^252,
+    2^252 - 1, 2^251 in the first 8 slots; Montgomery limbs (n x 4 u64)"""
+    import workload
+
+    v, _ = workload.random_fq(n, 1)
+    v = [int(x) for x in v]
+    Q = workload.Q
+    edge = [0, 1, 2, Q - 1, Q - 2, 1 << 252, (1 << 252) - 1, 1 << 251]
+    v[: min(8, n)] = edge[: min(8, n)]
+    return workload.to_mont_limbs(v)
+
+
+def main_msm(a):
+    """SURVEY 8d config 2: one 2^k-point MSM (GroupElement::vartime_multiscalar_mul, src/group.rs:98-116) against
+    MultiCommitGens::new(2^k, b"spg_bench_msm").G, resident in HBM. With N ranks the MSM is split into
+    contiguous chunks: each rank computes an uncompressed partial sum (spg_msm_partial), the
+    128-byte partials are allgathered over RCCL and added exactly on the host (shard.py) -> strong scaling.
+    A step is one whole MSM ending in the 32-byte compressed result on every rank."""
+    import torch
+
+    import shard
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = a.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(backend)
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if ndev else local
+    if torch.cuda.is_available():
+        torch.cuda.set_device(gpu)
+    import spg
+
+    ctx = spg.Context(gpu)
+    n = 1 << a.log_msm
+    gens = spg.Gens(ctx, n, b"spg_bench_msm")
+    sc = msm_scalars(n)
+    partial = shard.gpu_partial(gens, sc)
+    dev = f"cuda:{gpu}" if backend == "nccl" else None
+
+    def step():
+        if dist is None:
+            return spg.points_sum_compress([partial(0, n)])
+        return shard.sharded_msm(dist, partial, n, dev)[0]
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    outs = set()
+    for _ in range(a.steps):
+        outs.add(step())
+    sync()
+    dt = time.perf_counter() - t0
+    prof = profile_pass(ctx, step, a.steps)
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    assert len(outs) == 1, "MSM result changed between steps"
+    lo, hi = shard.chunk(n, rank, world)
+    dev_us = sum(v[1] for v in prof.values()) / a.steps
+    # algorithmic bytes per point (SURVEY 8d config 2): 32 B scalar + 64 B affine point; the launch sequence of one
+    # partial MSM is the unit (the MSM is VALU-bound: mixed additions, reported beside the HBM figure)
+    alg = (hi - lo) * 96 + 32
+    achieved = alg / (dev_us * 1e-6) / 1e9
+    c_win = 16 if hi - lo > 16384 else 8
+    madds = (hi - lo) * (253 // c_win + 1)
+    roof = {"bound": "hbm", "kernel": "msm (all launches of one partial MSM)", "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(dev_us, 1), "launches": a.steps,
+            "valu": {"mixed_adds_per_msm": madds, "mixed_adds_per_s": round(madds / (dev_us * 1e-6), 1),
+                     "note": "fixed-base signed windows: one 7M mixed addition per nonzero digit"}}
+    cpu, bitexact = None, None
+    if rank == 0 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import numpy as np
+
+        import pyoracle  # the checker / CPU baseline only
+
+        pyoracle.build()
+        pts = gens.compressed()
+        ref_pts = pyoracle.gens_stream(b"spg_bench_msm", n + 1)
+        tc = time.perf_counter()
+        ref = pyoracle.msm(ref_pts[:n], sc)
+        tcpu = time.perf_counter() - tc
+        bitexact = bool(np.array_equal(pts, ref_pts) and ref in outs)
+        if world == 1:
+            cpu = {"value": round(n / tcpu, 1), "unit": "points/s", "cores": 1, "kind": "port",
+                   "sample": f"the whole MSM ({n} pairs) by the oracle's vartime Pippenger restatement incl. point "
+                             f"decompression, {tcpu:.2f} s on 1 host thread"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "MSM points/sec (GroupElement::vartime_multiscalar_mul, 2^%d points); result bit-exact" % a.log_msm,
+            "value": round(n * a.steps / dt, 1), "unit": "points/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "ristretto255 / fq252",
+            "data": "synthetic scalars (splitmix64 seed 1 + edge cases), generators MultiCommitGens(2^k, spg_bench_msm)",
+            "config": {"workload": "single MSM, SURVEY 8d config 2", "points": n,
+                       "parallelism": f"contiguous shards x{world}, allgather of partials ({backend})"},
+            "roofline": roof, "cpu_baseline": cpu, "result_bitexact_vs_cpu": bitexact,
+            "result": sorted(outs)[0].hex(), "device_us_per_partial": round(dev_us, 1),
+            "kernels": {k: {"launches_per_step": v[0] / a.steps, "us_per_step": round(v[1] / a.steps, 1)}
+                        for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1])}}))
     if dist is not None:
         dist.destroy_process_group()
 

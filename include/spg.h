@@ -85,6 +85,15 @@ int spg_msm(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* 
  * the `random_tape = None` case every SNARK::prove commit uses). Z is L*R scalars, row-major. */
 int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* Z_mont, size_t L, size_t R,
                     const uint64_t* blinds_mont, uint8_t* out);
+/* One shard of an MSM split over devices ("split points and scalars into contiguous chunks; each
+ * GPU produces a partial sum in extended coordinates"): out_ext = sum_i s_i * G[gen_offset + i] as X, Y, Z, T,
+ * each 32 little-endian bytes (a representative < 2^256 of the coordinate mod 2^255 - 19). Not compressed,
+ * so the partials of all ranks add exactly. Same group.rs:98-116 semantics as spg_msm without the blind. */
+int spg_msm_partial(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont, size_t n,
+                    uint8_t out_ext[128]);
+/* Host only, needs no device or context: the sum of k partial points (k x 128 bytes, spg_msm_partial layout)
+ * encoded as a 32-byte CompressedRistretto (RFC 9496 ENCODE). */
+int spg_points_sum_compress(const uint8_t* parts, size_t k, uint8_t out[32]);
 
 /* ---- R1CS data-parallel satisfiability proof --------------------------------------------------
  * Flat C views of the reference's R1CSInstance (src/r1csinstance.rs:19-31) and

@@ -125,6 +125,21 @@ int orc_msm(const uint8_t* bases, const uint64_t* scalars, size_t n, uint8_t* ou
   ge_compress(vartime_msm(s.data(), P.data(), n), out);
   return 1;
 }
+// one shard of a sharded MSM: the uncompressed partial sum as extended coordinates
+// X, Y, Z, T, each 32 canonical little-endian bytes (test reference for spg_msm_partial / spg_points_sum_compress)
+int orc_msm_partial(const uint8_t* bases, const uint64_t* scalars, size_t n, uint8_t* out_ext) {
+  std::vector<Ge> P(n);
+  for (size_t i = 0; i < n; i++)
+    if (!ge_decompress(bases + 32 * i, &P[i])) return 0;
+  std::vector<Fq> s(n);
+  for (size_t i = 0; i < n; i++) s[i] = ld(scalars + 4 * i);
+  Ge r = vartime_msm(s.data(), P.data(), n);
+  fe_to_bytes(r.X, out_ext);
+  fe_to_bytes(r.Y, out_ext + 32);
+  fe_to_bytes(r.Z, out_ext + 64);
+  fe_to_bytes(r.T, out_ext + 96);
+  return 1;
+}
 // Hyrax rows (src/dense_mlpoly.rs:200-212): for i < L: C_i = MSM(Z[R i .. R(i+1)], G[0..R]) + blind_i * h
 // bases: (>= R) compressed G followed by h at index nb. blinds may be NULL (zeros).
 int orc_commit_rows(const uint8_t* bases, size_t nb, const uint8_t* h, const uint64_t* Z, size_t L, size_t R,

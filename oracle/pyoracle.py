@@ -175,6 +175,16 @@ def msm(bases, scalars):
     return out.tobytes()
 
 
+def msm_partial(bases, scalars):
+    """uncompressed MSM result (X, Y, Z, T as 4 x 32 LE bytes) of one shard"""
+    bases = np.ascontiguousarray(bases, dtype=np.uint8).reshape(-1, 32)
+    s = u64s(scalars).reshape(-1, 4)
+    assert bases.shape[0] == s.shape[0]
+    out = np.zeros(128, dtype=np.uint8)
+    assert lib().orc_msm_partial(_p(bases), _p(s), ctypes.c_size_t(s.shape[0]), _p(out))
+    return out.tobytes()
+
+
 def commit_rows(bases, h, Z, L, R, blinds=None):
     bases = np.ascontiguousarray(bases, dtype=np.uint8).reshape(-1, 32)
     hh = np.frombuffer(bytes(h), dtype=np.uint8).copy()

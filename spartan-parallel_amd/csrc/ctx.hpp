@@ -95,7 +95,7 @@ void timer_stop(spg_ctx* c);
 // generator d_idx[b*n+i] when d_idx is given, else gen_offset + i; d_blinds (B) multiply generator
 // h_index (-1: g->n). d_out: B x 32 compressed bytes (device). Stream-ordered, no host sync.
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
-                     const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index);
+                     const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext = nullptr);
 
 // latency path for small batches (B * n up to a few thousand): same inputs, results left in extended
 // coordinates in d_out (B x Ext, device); the caller encodes them (host).

@@ -1,14 +1,18 @@
 // spg — a small persistent host worker pool for the prover's sequential-protocol work.
 // Between two Fiat-Shamir challenges the prover computes a handful of independent fixed-base
 // commitments and point encodings (tens of microseconds each); running them on several host cores
-// shortens every sumcheck round. Workers park on a condition variable between bursts.
+// shortens every sumcheck round. Bursts come every few tens of microseconds inside a proof, so a worker
+// spins on the burst generation for a while (SPG_POOL_SPIN_US, default 300) before it parks on the
+// condition variable: a futex wake-up costs 10-30 us per burst, a spinning worker picks the burst up at once.
 //
 // Task indices are claimed with a CAS on one 64-bit word holding (burst generation, next index), and
 // every worker works from a snapshot (generation, function, count) taken under the mutex, so a worker
 // that wakes late can never run a task of a newer burst with an older function or vice versa.
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -19,12 +23,15 @@ namespace spg {
 class Pool {
  public:
   explicit Pool(int nthreads) {
+    const char* e = getenv("SPG_POOL_SPIN_US");
+    spin_ = std::chrono::microseconds(e ? atoi(e) : 300);
     for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
   }
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       quit_ = true;
+      quit_pub_.store(true);
     }
     cv_.notify_all();
     for (auto& t : threads_) t.join();
@@ -37,6 +44,7 @@ class Pool {
     }
     std::lock_guard<std::mutex> call(call_mu_);  // one burst at a time
     uint32_t g;
+    bool wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
       g = ++gen_;
@@ -44,8 +52,10 @@ class Pool {
       n_ = n;
       remaining_.store(n);
       next_.store((uint64_t)g << 32);
+      gen_pub_.store(g, std::memory_order_release);
+      wake = sleepers_ > 0;
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
     work(g, &f, n);
     while (remaining_.load() > 0) std::this_thread::yield();
   }
@@ -66,9 +76,19 @@ class Pool {
       uint32_t g;
       const std::function<void(int)>* f;
       int n;
+      // spin phase: pick up the next burst without a futex wake-up
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned k = 0; gen_pub_.load(std::memory_order_acquire) == seen && !quit_pub_.load(); k++) {
+        if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > spin_) break;
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
       {
         std::unique_lock<std::mutex> lk(mu_);
+        sleepers_++;
         cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        sleepers_--;
         if (quit_) return;
         seen = g = gen_;
         f = fn_;
@@ -86,6 +106,10 @@ class Pool {
   std::atomic<uint64_t> next_{0};
   std::atomic<int> remaining_{0};
   bool quit_ = false;
+  int sleepers_ = 0;
+  std::atomic<uint32_t> gen_pub_{0};
+  std::atomic<bool> quit_pub_{false};
+  std::chrono::microseconds spin_{300};
 };
 
 inline Pool& pool() {

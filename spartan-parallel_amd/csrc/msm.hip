@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ it
 //   value_t = sum T_j + m * sum_j (j - t*g) S_j      and      V_t = sum S_j,
 // leaving sum_t value_t + (g*m) * sum_t t*V_t, done with an LDS suffix scan of V plus a tree sum.
 __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, const Ext* __restrict__ segS,
-                                               uint8_t* __restrict__ out, int S, int log2m) {
+                                               uint8_t* __restrict__ out, int S, int log2m, Ext* __restrict__ ext_out) {
   __shared__ Ext sh[256];
   const int b = blockIdx.x, t = threadIdx.x;
   const int g = S >= 256 ? S / 256 : 1;
@@ -244,7 +244,8 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
     if (t < d) val = ext_add(val, sh[t + d]);
     __syncthreads();
   }
-  if (t == 0) {
+  if (t == 0 && ext_out) ext_out[b] = val;
+  if (t == 0 && out) {
     uint8_t c[32];
     ext_compress(val, c);
     for (int k = 0; k < 32; k++) out[32 * (size_t)b + k] = c[k];
@@ -512,7 +513,7 @@ static void dispatch_digits(int c, const MsmArgs& a, bool count, hipStream_t s) 
 
 // B MSMs of n scalars each (device pointers), out_dev: B x 32 bytes (device)
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
-                     const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index) {
+                     const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext) {
   hipStream_t s = ctx->stream;
   const int c = pick_window(n + (d_blinds ? 1 : 0));
   const int NB = 1 << (c - 1);
@@ -593,7 +594,7 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   }
   {
     KScope ks(ctx, "msm_final");
-    hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(256), 0, s, segT, segS, d_out, S, log2m);
+    hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(256), 0, s, segT, segS, d_out, S, log2m, d_ext);
   }
   SPG_HIP(ctx, hipGetLastError());
   return 0;
@@ -757,6 +758,52 @@ static int msm_host(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const ui
 extern "C" int spg_msm(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont, size_t n,
                        const uint64_t* blind_mont, uint8_t out[32]) {
   return msm_host(ctx, g, gen_offset, scalars_mont, n, 1, blind_mont, out);
+}
+
+// one shard of an MSM that is split over devices: the sum stays uncompressed so that the partials
+// of all ranks add exactly; spg_points_sum_compress adds and encodes them on the host
+extern "C" int spg_msm_partial(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont,
+                               size_t n, uint8_t out_ext[128]) {
+  if (!ctx || !g || !out_ext || (!scalars_mont && n)) return SPG_E_ARG;
+  if (gen_offset + n > g->n) return set_err(ctx, SPG_E_ARG, "MSM longer than the generator set");
+  if (n == 0) {
+    const Ext id = ext_identity();
+    memcpy(out_ext, &id, sizeof(Ext));
+    return SPG_OK;
+  }
+  hipStream_t s = ctx->stream;
+  Fq* d_s = (Fq*)ws_get(ctx, 0, n * sizeof(Fq) + sizeof(Ext) + 64);
+  if (!d_s) return set_err(ctx, SPG_E_NOMEM, "scalar upload");
+  Ext* d_ext = (Ext*)(d_s + n);
+  SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars_mont, n * sizeof(Fq), hipMemcpyHostToDevice, s));
+  timer_start(ctx);
+  int rc = n <= kSmallMaxN ? msm_small_device(ctx, g, gen_offset, d_s, n, 1, nullptr, d_ext, nullptr, -1)
+                           : msm_batch_device(ctx, g, gen_offset, d_s, n, 1, nullptr, nullptr, nullptr, -1, d_ext);
+  if (rc) return rc;
+  timer_stop(ctx);
+  Ext r;
+  SPG_HIP(ctx, hipMemcpyAsync(&r, d_ext, sizeof(Ext), hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  static_assert(sizeof(Ext) == 128, "Ext is X, Y, Z, T of 32 bytes");
+  memcpy(out_ext, &r, sizeof(Ext));
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  ctx->last_us = ms * 1000.0;
+  return SPG_OK;
+}
+
+// host only (no device): sum of k partial points (X, Y, Z, T; 32 little-endian bytes each, any representative
+// below 2^256 of the coordinate mod 2^255 - 19) and its RFC 9496 encoding
+extern "C" int spg_points_sum_compress(const uint8_t* parts, size_t k, uint8_t out[32]) {
+  if (!out || (!parts && k)) return SPG_E_ARG;
+  h::HExt acc = h::hext_identity();
+  for (size_t i = 0; i < k; i++) {
+    Ext e;
+    memcpy(&e, parts + 128 * i, sizeof(Ext));
+    acc = h::hext_add(acc, h::hext_from_dev(e));
+  }
+  h::hext_compress(acc, out);
+  return SPG_OK;
 }
 
 extern "C" int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* Z_mont, size_t L, size_t R,

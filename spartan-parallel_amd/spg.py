@@ -200,6 +200,15 @@ class Gens:
         self.ctx.check(rc, "spg_msm")
         return out.tobytes()
 
+    def msm_partial(self, scalars, gen_offset=0):
+        """spg_msm_partial: uncompressed (X, Y, Z, T) partial sum of one shard, 128 bytes"""
+        s = _scalars(scalars)
+        out = np.zeros(128, dtype=np.uint8)
+        rc = lib().spg_msm_partial(self.ctx.handle, self._h, ctypes.c_size_t(gen_offset), _p(s),
+                                   ctypes.c_size_t(s.shape[0]), _p(out))
+        self.ctx.check(rc, "spg_msm_partial")
+        return out.tobytes()
+
     def commit_rows(self, Z, L, R, blinds=None):
         z = _scalars(Z)
         assert z.shape[0] == L * R
@@ -515,3 +524,12 @@ def snark_prove(ctx, block, pairwise, perm_root, witness, vars_gens, transcript,
                                     vars_gens.handle, transcript.handle, tape.handle, _p(buf), ctypes.c_size_t(cap),
                                     ctypes.byref(ln)), "spg_snark_prove")
     return buf[: ln.value].tobytes()
+
+
+def points_sum_compress(parts):
+    """spg_points_sum_compress (host only): encoding of the sum of 128-byte partial points"""
+    buf = np.frombuffer(b"".join(parts), dtype=np.uint8).copy() if parts else np.zeros(1, np.uint8)
+    out = np.zeros(32, dtype=np.uint8)
+    rc = lib().spg_points_sum_compress(_p(buf), ctypes.c_size_t(len(parts)), _p(out))
+    assert rc == 0, rc
+    return out.tobytes()

@@ -66,3 +66,57 @@ def test_allgather_sum_two_ranks(oracle):
         assert rc == 0 and rc2 == 0
         assert np.array_equal(np.array(out, dtype=np.uint64), expect)
         assert raw == [1] * 8 + [2] * 8
+
+
+def _msm_worker(rank, world, port, q):
+    import sys
+
+    sys.path[:0] = [os.path.join(ROOT, "spartan-parallel_amd"), os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+
+    import pyoracle
+    import shard
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 37  # ragged split over the ranks
+        pts = pyoracle.gens_stream(b"spg_bench_msm", n + 1)[:n]
+        rng = np.random.default_rng(7)
+        Z = pyoracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * n, dtype=np.uint8).tobytes())
+        got, _ = shard.sharded_msm(dist, lambda lo, hi: pyoracle.msm_partial(pts[lo:hi], Z[lo:hi]), n)
+        q.put((rank, got, pyoracle.msm(pts, Z)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_msm_matches_single(oracle, world):
+    """contiguous shards, one allgather of uncompressed partials, exact host sum == the
+    unsharded MSM (partials from the CPU oracle; tests/test_gpu_dist.py runs the device partials)"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_msm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, got, ref in res:
+        assert got == ref, rank
+
+
+def test_shard_chunks_cover():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))
+    import shard
+
+    for n in (0, 1, 7, 64, 65537):
+        for w in (1, 2, 3, 8):
+            cs = [shard.chunk(n, r, w) for r in range(w)]
+            assert cs[0][0] == 0 and cs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(cs, cs[1:]))
+            assert max(h - l for l, h in cs) - min(h - l for l, h in cs) <= 1

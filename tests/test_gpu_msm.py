@@ -117,3 +117,22 @@ def test_large_msm_2e16_property(ctx, oracle):
     s = rand_fq(oracle, rng, n)
     got = g.msm(s)
     assert got == oracle.msm(pts[:n], s)
+
+
+@pytest.mark.parametrize("n,world", [(1000, 3), (4099, 8), (1 << 16, 8), (20000, 1)])
+def test_msm_partial_shards(ctx, oracle, n, world):
+    """per-rank uncompressed partials (spg_msm_partial, both the latency path and the batch
+    pipeline) add on the host (spg_points_sum_compress) to the unsharded MSM, and each partial equals the
+    oracle's partial point"""
+    import shard
+    import spg
+
+    g = spg.Gens(ctx, n, b"spg_bench_msm")
+    pts = g.compressed()
+    s = rand_fq(oracle, np.random.default_rng(n), n)
+    parts = [g.msm_partial(s[lo:hi], gen_offset=lo) for lo, hi in (shard.chunk(n, r, world) for r in range(world))]
+    assert spg.points_sum_compress(parts) == g.msm(s) == oracle.msm(pts[:n], s)
+    lo, hi = shard.chunk(n, world - 1, world)
+    ref = oracle.msm_partial(pts[lo:hi], s[lo:hi])
+    # same point, possibly different projective representative: compare encodings
+    assert spg.points_sum_compress([parts[-1]]) == spg.points_sum_compress([ref])
