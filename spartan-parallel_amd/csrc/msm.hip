@@ -26,6 +26,7 @@
 #include "ctx.hpp"
 #include "hcurve.hpp"
 #include "keccak.hpp"
+#include "lds.hpp"
 
 namespace spg {
 
@@ -207,7 +208,7 @@ __global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ it
 // leaving sum_t value_t + (g*m) * sum_t t*V_t, done with an LDS suffix scan of V plus a tree sum.
 __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, const Ext* __restrict__ segS,
                                                uint8_t* __restrict__ out, int S, int log2m, Ext* __restrict__ ext_out) {
-  __shared__ Ext sh[256];
+  __shared__ uint32_t sh[soa_words<Ext, 256>()];
   const int b = blockIdx.x, t = threadIdx.x;
   const int g = S >= 256 ? S / 256 : 1;
   int log2g = 0;
@@ -229,9 +230,9 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
   // inclusive suffix scan of V over threads
   Ext suf = V;
   for (int d = 1; d < 256; d <<= 1) {
-    sh[t] = suf;
+    soa_put<256>(sh, t, suf);
     __syncthreads();
-    if (t + d < 256) suf = ext_add(suf, sh[t + d]);
+    if (t + d < 256) suf = ext_add(suf, soa_get<256, Ext>(sh, t + d));
     __syncthreads();
   }
   if (t >= 1) {
@@ -239,9 +240,9 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
     val = ext_add(val, suf);
   }
   for (int d = 128; d >= 1; d >>= 1) {
-    sh[t] = val;
+    soa_put<256>(sh, t, val);
     __syncthreads();
-    if (t < d) val = ext_add(val, sh[t + d]);
+    if (t < d) val = ext_add(val, soa_get<256, Ext>(sh, t + d));
     __syncthreads();
   }
   if (t == 0 && ext_out) ext_out[b] = val;
@@ -271,7 +272,7 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket(const Fq* __restrict__ scala
   constexpr int W = 253 / C + 1;
   constexpr int NB = 1 << (C - 1);
   constexpr uint32_t MASK = (1u << C) - 1u;
-  __shared__ Ext sh[BS];
+  __shared__ uint32_t sh[soa_words<Ext, BS>()];
   const int v = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x;
   const int per = n + has_blind;
   Ext acc = ext_identity();
@@ -313,9 +314,9 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket(const Fq* __restrict__ scala
     }
   }
   for (int d = BS / 2; d >= 1; d >>= 1) {
-    sh[t] = acc;
+    soa_put<BS>(sh, t, acc);
     __syncthreads();
-    if (t < d) acc = ext_add(acc, sh[t + d]);
+    if (t < d) acc = ext_add(acc, soa_get<BS, Ext>(sh, t + d));
     __syncthreads();
   }
   if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
@@ -323,19 +324,19 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket(const Fq* __restrict__ scala
 
 // one block of NB threads per MSM: sum_v v * B_v = sum_t (sum_{u >= t} B_u)
 __global__ void __launch_bounds__(256) k_smsm_final(const Ext* __restrict__ buckets, int NB, Ext* __restrict__ out) {
-  __shared__ Ext sh[256];
+  __shared__ uint32_t sh[soa_words<Ext, 256>()];
   const int b = blockIdx.x, t = threadIdx.x;
   Ext suf = buckets[(size_t)b * NB + t];
   for (int d = 1; d < NB; d <<= 1) {
-    sh[t] = suf;
+    soa_put<256>(sh, t, suf);
     __syncthreads();
-    if (t + d < NB) suf = ext_add(suf, sh[t + d]);
+    if (t + d < NB) suf = ext_add(suf, soa_get<256, Ext>(sh, t + d));
     __syncthreads();
   }
   for (int d = NB / 2; d >= 1; d >>= 1) {
-    sh[t] = suf;
+    soa_put<256>(sh, t, suf);
     __syncthreads();
-    if (t < d) suf = ext_add(suf, sh[t + d]);
+    if (t < d) suf = ext_add(suf, soa_get<256, Ext>(sh, t + d));
     __syncthreads();
   }
   if (t == 0) out[b] = suf;

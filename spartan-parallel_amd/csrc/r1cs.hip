@@ -16,6 +16,7 @@
 
 #include "hostpoly.hpp"
 #include "proto.hpp"
+#include "lds.hpp"
 #include "sumcheck.hpp"
 
 
@@ -178,15 +179,17 @@ __global__ void k_sum_cols(const Fq* __restrict__ part, uint32_t S, uint32_t Rs,
 // instance at once: segment s = 3p + m (A, B, C of matrix instance p); one thread per CSR row computes
 // eq_rx[row] * sum_e val_e * eq_ry[col_e]; blocks publish partial sums, k_sum_segments adds them.
 __device__ __forceinline__ Fq block_sum1(Fq v) {
-  __shared__ Fq sh[256];
+  __shared__ uint32_t sh[soa_words<Fq, 256>()];  // component-major: no bank conflicts
   int t = threadIdx.x;
-  sh[t] = v;
-  __syncthreads();
   for (int d = 128; d >= 1; d >>= 1) {
-    if (t < d) sh[t] = fq_add(sh[t], sh[t + d]);
+    if (t >= d && t < 2 * d) soa_put<256>(sh, t - d, v);
+    __syncthreads();
+    if (t < d) v = fq_add(v, soa_get<256, Fq>(sh, t));
     __syncthreads();
   }
-  Fq r = sh[0];
+  if (t == 0) soa_put<256>(sh, 0, v);
+  __syncthreads();
+  Fq r = soa_get<256, Fq>(sh, 0);
   __syncthreads();
   return r;
 }

@@ -22,6 +22,7 @@
 
 #include "hostpoly.hpp"
 #include "proto.hpp"
+#include "lds.hpp"
 #include "sumcheck.hpp"
 
 namespace spg {
@@ -87,23 +88,32 @@ struct Triple {
   Fq *A, *B, *C;
 };
 __device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
-  __shared__ Fq sh[3][256];
+  __shared__ uint32_t sh[3][soa_words<Fq, 256>()];  // component-major: no bank conflicts
   int t = threadIdx.x;
-  sh[0][t] = v0;
-  sh[1][t] = v1;
-  sh[2][t] = v2;
-  __syncthreads();
   for (int d = 128; d >= 1; d >>= 1) {
+    if (t >= d && t < 2 * d) {
+      soa_put<256>(sh[0], t - d, v0);
+      soa_put<256>(sh[1], t - d, v1);
+      soa_put<256>(sh[2], t - d, v2);
+    }
+    __syncthreads();
     if (t < d) {
-      sh[0][t] = fq_add(sh[0][t], sh[0][t + d]);
-      sh[1][t] = fq_add(sh[1][t], sh[1][t + d]);
-      sh[2][t] = fq_add(sh[2][t], sh[2][t + d]);
+      v0 = fq_add(v0, soa_get<256, Fq>(sh[0], t));
+      v1 = fq_add(v1, soa_get<256, Fq>(sh[1], t));
+      v2 = fq_add(v2, soa_get<256, Fq>(sh[2], t));
     }
     __syncthreads();
   }
-  v0 = sh[0][0];
-  v1 = sh[1][0];
-  v2 = sh[2][0];
+  // broadcast thread 0's sums
+  if (t == 0) {
+    soa_put<256>(sh[0], 0, v0);
+    soa_put<256>(sh[1], 0, v1);
+    soa_put<256>(sh[2], 0, v2);
+  }
+  __syncthreads();
+  v0 = soa_get<256, Fq>(sh[0], 0);
+  v1 = soa_get<256, Fq>(sh[1], 0);
+  v2 = soa_get<256, Fq>(sh[2], 0);
   __syncthreads();
 }
 // one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
