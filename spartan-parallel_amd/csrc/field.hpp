@@ -275,8 +275,73 @@ SPG_HD Fq fq_from_u64(uint64_t x) {
   t.l[1] = (uint32_t)(x >> 32);
   return fq_to_mont(t);
 }
-// x^(q-2) by 4-bit fixed windows over the exponent
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host inverse by the binary extended Euclidean algorithm on 4 x 64-bit limbs: ~5x faster than the
+// Fermat chain below on a CPU. Variable time, which is fine here: the prover only inverts public
+// Fiat-Shamir challenges (BulletReductionProof's u, src/nizk/bullet.rs:100). Same value as Scalar::invert
+// (src/scalar/ristretto255.rs:541-595); 0 maps to 0 like the Fermat chain.
+inline Fq fq_inv_host(const Fq& am) {
+  typedef unsigned __int128 u128;
+  static const uint64_t q[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0ULL, 0x1000000000000000ULL};
+  const Fq c = fq_from_mont(am);
+  uint64_t u[4], v[4] = {q[0], q[1], q[2], q[3]}, x1[4] = {1, 0, 0, 0}, x2[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) u[i] = (uint64_t)c.l[2 * i] | ((uint64_t)c.l[2 * i + 1] << 32);
+  if ((u[0] | u[1] | u[2] | u[3]) == 0) return fq_zero();
+  auto is_one = [](const uint64_t* a) { return a[0] == 1 && (a[1] | a[2] | a[3]) == 0; };
+  auto geq = [](const uint64_t* a, const uint64_t* b) {
+    for (int i = 3; i >= 0; i--)
+      if (a[i] != b[i]) return a[i] > b[i];
+    return true;
+  };
+  auto sub = [](uint64_t* a, const uint64_t* b) {  // a -= b (no underflow by construction)
+    uint64_t bw = 0;
+    for (int i = 0; i < 4; i++) {
+      u128 d = (u128)a[i] - b[i] - bw;
+      a[i] = (uint64_t)d;
+      bw = (uint64_t)(d >> 64) & 1;
+    }
+  };
+  auto add = [](uint64_t* a, const uint64_t* b) {  // a += b (sum < 2^256)
+    u128 cy = 0;
+    for (int i = 0; i < 4; i++) {
+      cy += (u128)a[i] + b[i];
+      a[i] = (uint64_t)cy;
+      cy >>= 64;
+    }
+  };
+  auto shr1 = [](uint64_t* a) {
+    for (int i = 0; i < 3; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 63);
+    a[3] >>= 1;
+  };
+  auto half_mod = [&](uint64_t* x) {  // x / 2 mod q (x < q < 2^253, so x + q does not overflow)
+    if (x[0] & 1) add(x, q);
+    shr1(x);
+  };
+  auto sub_mod = [&](uint64_t* a, const uint64_t* b) {  // a = a - b mod q (a, b < q)
+    if (!geq(a, b)) add(a, q);
+    sub(a, b);
+  };
+  while (!is_one(u) && !is_one(v)) {
+    while (!(u[0] & 1)) { shr1(u); half_mod(x1); }
+    while (!(v[0] & 1)) { shr1(v); half_mod(x2); }
+    if (geq(u, v)) { sub(u, v); sub_mod(x1, x2); }
+    else { sub(v, u); sub_mod(x2, x1); }
+  }
+  const uint64_t* r = is_one(u) ? x1 : x2;
+  Fq out;
+  for (int i = 0; i < 4; i++) {
+    out.l[2 * i] = (uint32_t)r[i];
+    out.l[2 * i + 1] = (uint32_t)(r[i] >> 32);
+  }
+  return fq_to_mont(out);
+}
+#endif
+
+// x^(q-2) by 4-bit fixed windows over the exponent (device; the host uses fq_inv_host)
 SPG_HD Fq fq_inv(const Fq& a) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return fq_inv_host(a);
+#endif
   // q - 2 limbs (little-endian u32)
   const uint32_t E[8] = {SPG_Q0 - 2u, SPG_Q1, SPG_Q2, SPG_Q3, 0u, 0u, 0u, SPG_Q7};
   Fq tab[16];

@@ -70,7 +70,26 @@ inline Fe fe_mul(const Fe& a, const Fe& b) {
   c = r.v[0] >> 51; r.v[0] &= M51; r.v[1] += c;
   return r;
 }
-inline Fe fe_sqr(const Fe& a) { return fe_mul(a, a); }
+// 15 limb products instead of 25 (the cross terms doubled); the inversion / square-root chains of every
+// point encoding are ~250 squarings
+inline Fe fe_sqr(const Fe& a) {
+  const uint64_t a0_2 = a.v[0] * 2, a1_2 = a.v[1] * 2;
+  const uint64_t a3_19 = a.v[3] * 19, a4_19 = a.v[4] * 19;
+  const u128 t0 = (u128)a.v[0] * a.v[0] + (u128)a1_2 * a4_19 + (u128)(a.v[2] * 2) * a3_19;
+  u128 t1 = (u128)a0_2 * a.v[1] + (u128)(a.v[2] * 2) * a4_19 + (u128)a.v[3] * a3_19;
+  u128 t2 = (u128)a0_2 * a.v[2] + (u128)a.v[1] * a.v[1] + (u128)(a.v[3] * 2) * a4_19;
+  u128 t3 = (u128)a0_2 * a.v[3] + (u128)a1_2 * a.v[2] + (u128)a.v[4] * a4_19;
+  u128 t4 = (u128)a0_2 * a.v[4] + (u128)a1_2 * a.v[3] + (u128)a.v[2] * a.v[2];
+  Fe r;
+  t1 += (uint64_t)(t0 >> 51); r.v[0] = (uint64_t)t0 & M51;
+  t2 += (uint64_t)(t1 >> 51); r.v[1] = (uint64_t)t1 & M51;
+  t3 += (uint64_t)(t2 >> 51); r.v[2] = (uint64_t)t2 & M51;
+  t4 += (uint64_t)(t3 >> 51); r.v[3] = (uint64_t)t3 & M51;
+  uint64_t c = (uint64_t)(t4 >> 51); r.v[4] = (uint64_t)t4 & M51;
+  r.v[0] += c * 19;
+  c = r.v[0] >> 51; r.v[0] &= M51; r.v[1] += c;
+  return r;
+}
 inline Fe fe_sqrn(Fe a, int n) {
   for (int i = 0; i < n; i++) a = fe_sqr(a);
   return a;

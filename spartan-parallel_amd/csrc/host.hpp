@@ -126,10 +126,12 @@ struct FixedBase {
     h::hext_batch_to_niels(ext, tab);
   }
   // acc += k * P   (k Montgomery)
-  void mul_add(h::HExt& acc, const Fq& k) const {
+  void mul_add(h::HExt& acc, const Fq& k) const { mul_add_windows(acc, k, 0, 32); }
+  // acc += (sum over byte windows w0 <= w < w1 of k_w 2^(8w)) * P: one share of k * P
+  void mul_add_windows(h::HExt& acc, const Fq& k, int w0, int w1) const {
     uint8_t b[32];
     fq_le_bytes(k, b);
-    for (int w = 0; w < 32; w++)
+    for (int w = w0; w < w1; w++)
       if (b[w]) acc = h::hext_madd(acc, tab[w * 256 + b[w]]);
   }
 };
@@ -157,8 +159,11 @@ struct HostGens {
     for (size_t i = 0; i < idx.size(); i++) get(idx[i]).mul_add(acc, s[i]);
     return acc;
   }
-  // several independent commitments (index list, scalars) at once on the host pool, encoded
+  // several independent commitments (index list, scalars) at once on the host pool, encoded. Every
+  // scalar multiple is split into kShares window ranges, so even a 2-term commitment keeps several cores
+  // busy: the pool's workers spin between the bursts of a sumcheck round, so a burst costs ~1 us to start.
   std::vector<Pt> commit_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs) {
+    static const int kShares = 4;  // 8 byte-windows (<= 8 mixed additions) per task
     std::vector<std::pair<size_t, size_t>> terms;  // (job, term)
     for (size_t j = 0; j < jobs.size(); j++) {
       for (size_t i = 0; i < jobs[j].first.size(); i++) {
@@ -166,23 +171,20 @@ struct HostGens {
         terms.push_back({j, i});
       }
     }
-    // the pool only pays for larger bursts: waking workers costs about as much as one scalar multiple
-    const bool par = terms.size() > 16;
-    std::vector<h::HExt> part(terms.size());
-    auto run = [&](int n, const std::function<void(int)>& f) {
-      if (par) pool().parallel_for(n, f);
-      else for (int i = 0; i < n; i++) f(i);
-    };
-    run((int)terms.size(), [&](int k) {
-      const auto& jb = jobs[terms[k].first];
+    const int ntask = (int)terms.size() * kShares;
+    std::vector<h::HExt> part(ntask);
+    pool().parallel_for(ntask, [&](int k) {
+      const auto& tm = terms[k / kShares];
+      const auto& jb = jobs[tm.first];
+      const int w0 = (k % kShares) * (32 / kShares);
       h::HExt acc = h::hext_identity();
-      fb.find(jb.first[terms[k].second])->second.mul_add(acc, jb.second[terms[k].second]);
+      fb.find(jb.first[tm.second])->second.mul_add_windows(acc, jb.second[tm.second], w0, w0 + 32 / kShares);
       part[k] = acc;
     });
     std::vector<h::HExt> sum(jobs.size(), h::hext_identity());
-    for (size_t k = 0; k < terms.size(); k++) sum[terms[k].first] = h::hext_add(sum[terms[k].first], part[k]);
+    for (int k = 0; k < ntask; k++) sum[terms[k / kShares].first] = h::hext_add(sum[terms[k / kShares].first], part[k]);
     std::vector<Pt> out(jobs.size());
-    run((int)jobs.size(), [&](int j) { out[j] = compress(sum[j]); });
+    pool().parallel_for((int)jobs.size(), [&](int j) { out[j] = compress(sum[j]); });
     return out;
   }
 };

@@ -114,9 +114,13 @@ class Pool {
 
 inline Pool& pool() {
   static Pool p([] {
+    const char* e = getenv("SPG_POOL_THREADS");  // workers besides the calling thread
+    if (e) return atoi(e);
     unsigned hw = std::thread::hardware_concurrency();
     int n = hw > 1 ? (int)hw - 1 : 0;
-    return n > 15 ? 15 : n;  // the GPU box grants 16 host threads per GPU process
+    // 7 workers + the caller: measured best on the GPU box (16-CPU quota per process; 15 workers were
+    // 2-5 ms slower per SNARK::prove, scripts/pool_sweep.sh), and it leaves room for HIP's own threads
+    return n > 7 ? 7 : n;
   }());
   return p;
 }
