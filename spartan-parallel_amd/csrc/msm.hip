@@ -322,6 +322,150 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket(const Fq* __restrict__ scala
   if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
 }
 
+// ---- quad-cooperative point arithmetic for the latency path --------------------------------------
+// The four lanes of a quad hold the same point and split each addition's field products between them:
+// product round 1 gives lane r one of A, B, C', D of add-2008-hwcd-3, round 2 scales C' by 2d (lane 2),
+// round 3 gives lane r one of X3, Y3, T3, Z3; DPP quad broadcasts exchange the products. The dependent chain
+// of an addition drops from 10 (mixed: 7) field multiplications to 3 (2); every formula and value is the one
+// ext_add / ext_madd compute, so the group element (and its encoding) is identical.
+template <int K>
+__device__ __forceinline__ Fp fp_qbcast(const Fp& a) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ Fp fp_sel(bool c, const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+// lane q holds product q of (A, B, C, D); returns the sum point on every lane of the quad
+__device__ __forceinline__ Ext quad_finish(const Fp& p, int q) {
+  const Fp A = fp_qbcast<0>(p), B = fp_qbcast<1>(p), C = fp_qbcast<2>(p), D = fp_qbcast<3>(p);
+  const Fp E = fp_sub(B, A), F = fp_sub(D, C), G = fp_add(D, C), H = fp_add(B, A);
+  // X3 = E F (lane 0), Y3 = G H (1), T3 = E H (2), Z3 = F G (3)
+  const Fp u = fp_sel(q == 0 || q == 2, E, fp_sel(q == 1, G, F));
+  const Fp v = fp_sel(q == 0, F, fp_sel(q == 3, G, H));
+  const Fp w = fp_mul(u, v);
+  Ext r;
+  r.X = fp_qbcast<0>(w);
+  r.Y = fp_qbcast<1>(w);
+  r.T = fp_qbcast<2>(w);
+  r.Z = fp_qbcast<3>(w);
+  return r;
+}
+// P + (+-Niels); qv is this lane's Niels coordinate: lane 0 the "minus" one (neg ? ypx : ymx), lane 1 the
+// "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it)
+__device__ __forceinline__ Ext quad_madd(const Ext& P, const Fp& qv, bool neg, int q) {
+  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
+  const Fp y = fp_sel(q == 3, fp_small(2), qv);
+  Fp p = fp_mul(x, y);
+  p = fp_sel(neg && q == 2, fp_neg(p), p);
+  return quad_finish(p, q);
+}
+__device__ __forceinline__ Ext quad_add(const Ext& P, const Ext& Q, int q) {
+  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
+  const Fp y = fp_sel(q == 0, fp_sub(Q.Y, Q.X), fp_sel(q == 1, fp_add(Q.Y, Q.X), fp_sel(q == 2, Q.T, Q.Z)));
+  Fp p = fp_mul(x, y);
+  const Fp pd = fp_mul(p, c_d2());  // C = 2d T1 T2 (lane 2)
+  p = fp_sel(q == 2, pd, fp_sel(q == 3, fp_add(p, p), p));  // D = 2 Z1 Z2 (lane 3)
+  return quad_finish(p, q);
+}
+
+// Latency-path bucket kernel, quad form: one workgroup per (bucket v, MSM b) as k_smsm_bucket, but the
+// table entries of bucket v are first collected in LDS (one round of BS scalars at a time) and dealt out
+// evenly to the BS/4 quads, which add them with the quad-split arithmetic; the quads' sums then meet in an
+// LDS tree (component-major, each lane of a giving quad stores one coordinate).
+template <int C, int BS>
+__global__ void __launch_bounds__(BS) k_smsm_bucket_q(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
+                                                       const Fq* __restrict__ blinds, int has_blind, int n, int n1,
+                                                       int gen_offset, int h_index, const Niels* __restrict__ tab,
+                                                       Ext* __restrict__ buckets) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  constexpr int S = BS / 4;  // quads
+  __shared__ uint32_t list[BS * W];  // bucket entries of one round: table index | neg << 31
+  __shared__ uint32_t pts[soa_words<Ext, S>()];
+  __shared__ uint32_t cnt;
+  const int v = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int per = n + has_blind;
+  Ext acc = ext_identity();
+  if (t == 0) cnt = 0;
+  __syncthreads();
+  for (int base = 0; base < per; base += BS) {
+    const int i = base + t;
+    if (i < per) {
+      Fq s;
+      uint32_t gidx;
+      if (i < n) {
+        s = scalars[(size_t)b * n + i];
+        gidx = idx ? idx[(size_t)b * n + i] : (uint32_t)(gen_offset + i);
+      } else {
+        s = blinds[b];
+        gidx = (uint32_t)h_index;
+      }
+      Fq k = fq_from_mont(s);
+      int carry = 0;
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        const int bit = w * C;
+        const int li = bit >> 5, of = bit & 31;
+        uint32_t x = k.l[li] >> of;
+        if (of + C > 32 && li + 1 < 8) x |= k.l[li + 1] << (32 - of);
+        int d = (int)(x & MASK) + carry;
+        carry = d > NB ? 1 : 0;
+        d -= carry << C;
+        if (d == v || d == -v) {
+          const uint32_t pos = atomicAdd(&cnt, 1u);
+          list[pos] = (uint32_t)((size_t)(w * C) * n1 + gidx) | (d < 0 ? 0x80000000u : 0u);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t m = cnt;
+    for (uint32_t e = slot; e < m; e += S) {
+      const uint32_t ent = list[e];
+      const bool neg = ent >> 31;
+      const Niels* np = tab + (ent & 0x7fffffffu);
+      // Niels field order: ypx, ymx, t2d
+      const int which = q >= 2 ? 2 : ((q == 0) != neg ? 1 : 0);
+      const Fp qv = which == 0 ? np->ypx : (which == 1 ? np->ymx : np->t2d);
+      acc = quad_madd(acc, qv, neg, q);
+    }
+    __syncthreads();
+    if (t == 0) cnt = 0;
+    __syncthreads();
+  }
+  for (int d = S / 2; d >= 1; d >>= 1) {
+    if (slot >= d && slot < 2 * d) {
+      const Fp c = fp_sel(q == 0, acc.X, fp_sel(q == 1, acc.Y, fp_sel(q == 2, acc.Z, acc.T)));
+#pragma unroll
+      for (int i = 0; i < 8; i++) pts[(q * 8 + i) * S + (slot - d)] = c.l[i];
+    }
+    __syncthreads();
+    if (slot < d) acc = quad_add(acc, soa_get<S, Ext>(pts, slot), q);
+    __syncthreads();
+  }
+  if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
+}
+
+static bool use_quad() {
+  static const bool on = !getenv("SPG_SMSM_QUAD") || atoi(getenv("SPG_SMSM_QUAD")) != 0;
+  return on;
+}
+
+// the latency-path bucket kernel, quad form unless SPG_SMSM_QUAD=0
+#define SMSM_LAUNCH(BSZ, ...)                                                                   \
+  do {                                                                                          \
+    if (use_quad())                                                                             \
+      hipLaunchKernelGGL((k_smsm_bucket_q<C, BSZ>), dim3(NB, B), dim3(BSZ), 0, s, __VA_ARGS__); \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_smsm_bucket<C, BSZ>), dim3(NB, B), dim3(BSZ), 0, s, __VA_ARGS__);   \
+  } while (0)
+
 // one block of NB threads per MSM: sum_v v * B_v = sum_t (sum_{u >= t} B_u)
 __global__ void __launch_bounds__(256) k_smsm_final(const Ext* __restrict__ buckets, int NB, Ext* __restrict__ out) {
   __shared__ uint32_t sh[soa_words<Ext, 256>()];
@@ -362,13 +506,13 @@ static void launch_small(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const 
     const int per = n + (bl ? 1 : 0);
     const Fq* blp = bl ? bl : sc;
     if (per <= 64)
-      hipLaunchKernelGGL((k_smsm_bucket<C, 64>), dim3(NB, B), dim3(64), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
+      SMSM_LAUNCH(64, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
                          tab, bk);
     else if (per <= 128)
-      hipLaunchKernelGGL((k_smsm_bucket<C, 128>), dim3(NB, B), dim3(128), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off,
+      SMSM_LAUNCH(128, sc, idx, blp, bl ? 1 : 0, n, n1, off,
                          h, tab, bk);
     else
-      hipLaunchKernelGGL((k_smsm_bucket<C, 256>), dim3(NB, B), dim3(256), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off,
+      SMSM_LAUNCH(256, sc, idx, blp, bl ? 1 : 0, n, n1, off,
                          h, tab, bk);
   }
   KScope ks(ctx, "msm_small_final");
@@ -383,13 +527,13 @@ static void launch_buckets(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, cons
   const int per = n + (bl ? 1 : 0);
   const Fq* blp = bl ? bl : sc;
   if (per <= 64)
-    hipLaunchKernelGGL((k_smsm_bucket<C, 64>), dim3(NB, B), dim3(64), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h, tab,
+    SMSM_LAUNCH(64, sc, idx, blp, bl ? 1 : 0, n, n1, off, h, tab,
                        bk);
   else if (per <= 128)
-    hipLaunchKernelGGL((k_smsm_bucket<C, 128>), dim3(NB, B), dim3(128), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
+    SMSM_LAUNCH(128, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
                        tab, bk);
   else
-    hipLaunchKernelGGL((k_smsm_bucket<C, 256>), dim3(NB, B), dim3(256), 0, s, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
+    SMSM_LAUNCH(256, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
                        tab, bk);
 }
 
