@@ -202,6 +202,82 @@ __global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ it
   segS[t] = run;
 }
 
+// ---- quad-cooperative point arithmetic for the latency path --------------------------------------
+// The four lanes of a quad hold the same point and split each addition's field products between them:
+// product round 1 gives lane r one of A, B, C', D of add-2008-hwcd-3, round 2 scales C' by 2d (lane 2),
+// round 3 gives lane r one of X3, Y3, T3, Z3; DPP quad broadcasts exchange the products. The dependent chain
+// of an addition drops from 10 (mixed: 7) field multiplications to 3 (2); every formula and value is the one
+// ext_add / ext_madd compute, so the group element (and its encoding) is identical.
+template <int K>
+__device__ __forceinline__ Fp fp_qbcast(const Fp& a) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ Fp fp_sel(bool c, const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+// lane q holds product q of (A, B, C, D); returns the sum point on every lane of the quad
+// X3 = E F (lane 0), Y3 = G H (1), T3 = E H (2), Z3 = F G (3), broadcast to the quad
+__device__ __forceinline__ Ext quad_out(const Fp& E, const Fp& F, const Fp& G, const Fp& H, int q) {
+  const Fp u = fp_sel(q == 0 || q == 2, E, fp_sel(q == 1, G, F));
+  const Fp v = fp_sel(q == 0, F, fp_sel(q == 3, G, H));
+  const Fp w = fp_mul(u, v);
+  Ext r;
+  r.X = fp_qbcast<0>(w);
+  r.Y = fp_qbcast<1>(w);
+  r.T = fp_qbcast<2>(w);
+  r.Z = fp_qbcast<3>(w);
+  return r;
+}
+__device__ __forceinline__ Ext quad_finish(const Fp& p, int q) {
+  const Fp A = fp_qbcast<0>(p), B = fp_qbcast<1>(p), C = fp_qbcast<2>(p), D = fp_qbcast<3>(p);
+  return quad_out(fp_sub(B, A), fp_sub(D, C), fp_add(D, C), fp_add(B, A), q);
+}
+// P + (+-Niels); qv is this lane's Niels coordinate: lane 0 the "minus" one (neg ? ypx : ymx), lane 1 the
+// "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it)
+__device__ __forceinline__ Ext quad_madd(const Ext& P, const Fp& qv, bool neg, int q) {
+  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
+  const Fp y = fp_sel(q == 3, fp_small(2), qv);
+  Fp p = fp_mul(x, y);
+  p = fp_sel(neg && q == 2, fp_neg(p), p);
+  return quad_finish(p, q);
+}
+__device__ __forceinline__ Ext quad_add(const Ext& P, const Ext& Q, int q) {
+  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
+  const Fp y = fp_sel(q == 0, fp_sub(Q.Y, Q.X), fp_sel(q == 1, fp_add(Q.Y, Q.X), fp_sel(q == 2, Q.T, Q.Z)));
+  Fp p = fp_mul(x, y);
+  const Fp pd = fp_mul(p, c_d2());  // C = 2d T1 T2 (lane 2)
+  p = fp_sel(q == 2, pd, fp_sel(q == 3, fp_add(p, p), p));  // D = 2 Z1 Z2 (lane 3)
+  return quad_finish(p, q);
+}
+
+// 2P (dbl-2008-hwcd as ext_dbl): lane q squares X, Y, Z, X + Y
+__device__ __forceinline__ Ext quad_dbl(const Ext& P, int q) {
+  const Fp x = fp_sel(q == 0, P.X, fp_sel(q == 1, P.Y, fp_sel(q == 2, P.Z, fp_add(P.X, P.Y))));
+  const Fp p = fp_mul(x, x);
+  const Fp A = fp_qbcast<0>(p), B = fp_qbcast<1>(p), ZZ = fp_qbcast<2>(p), SS = fp_qbcast<3>(p);
+  const Fp C = fp_add(ZZ, ZZ);
+  const Fp E = fp_sub(fp_sub(SS, A), B), G = fp_sub(B, A);
+  return quad_out(E, fp_sub(G, C), G, fp_neg(fp_add(A, B)), q);
+}
+// a quad's point into a component-major LDS slot (lane q stores coordinate q: X, Y, Z, T)
+template <int SL>
+__device__ __forceinline__ void quad_put(uint32_t* sh, int slot, const Ext& P, int q) {
+  const Fp c = fp_sel(q == 0, P.X, fp_sel(q == 1, P.Y, fp_sel(q == 2, P.Z, P.T)));
+#pragma unroll
+  for (int i = 0; i < 8; i++) sh[(q * 8 + i) * SL + slot] = c.l[i];
+}
+
+static bool use_quad() {
+  static const bool on = !getenv("SPG_SMSM_QUAD") || atoi(getenv("SPG_SMSM_QUAD")) != 0;
+  return on;
+}
+
 // one 256-thread block per MSM. Segment j (bucket values j*m+1 .. j*m+m) contributes
 // T_j + j*m*S_j. Thread t folds the g = S/256 consecutive segments [t*g, t*g+g) into
 //   value_t = sum T_j + m * sum_j (j - t*g) S_j      and      V_t = sum S_j,
@@ -243,6 +319,56 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
     soa_put<256>(sh, t, val);
     __syncthreads();
     if (t < d) val = ext_add(val, soa_get<256, Ext>(sh, t + d));
+    __syncthreads();
+  }
+  if (t == 0 && ext_out) ext_out[b] = val;
+  if (t == 0 && out) {
+    uint8_t c[32];
+    ext_compress(val, c);
+    for (int k = 0; k < 32; k++) out[32 * (size_t)b + k] = c[k];
+  }
+}
+
+// k_final with quads: SL slots of 4 lanes (4 SL threads; SL = 128 keeps it under 256 VGPRs), slot plays
+// k_final's thread with SL in place of 256, every point operation
+// split over the quad (quad_add / quad_dbl)
+template <int SL>
+__global__ void __launch_bounds__(4 * SL) k_final_q(const Ext* __restrict__ segT, const Ext* __restrict__ segS,
+                                                 uint8_t* __restrict__ out, int S, int log2m, Ext* __restrict__ ext_out) {
+  __shared__ uint32_t sh[soa_words<Ext, SL>()];
+  const int b = blockIdx.x, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int g = S >= SL ? S / SL : 1;
+  int log2g = 0;
+  while ((1 << log2g) < g) log2g++;
+  const int lo = slot * g, hi = lo + g < S ? lo + g : S;
+  const Ext* T = segT + (size_t)b * S;
+  const Ext* Sv = segS + (size_t)b * S;
+  Ext U = ext_identity(), V = ext_identity(), acc = ext_identity(), tot = ext_identity();
+  for (int j = hi - 1; j >= lo; j--) {
+    U = quad_add(U, T[j], q);
+    V = quad_add(V, Sv[j], q);
+    if (j > lo) {
+      acc = quad_add(acc, Sv[j], q);
+      tot = quad_add(tot, acc, q);
+    }
+  }
+  for (int k = 0; k < log2m; k++) tot = quad_dbl(tot, q);
+  Ext val = quad_add(U, tot, q);
+  Ext suf = V;
+  for (int d = 1; d < SL; d <<= 1) {
+    quad_put<SL>(sh, slot, suf, q);
+    __syncthreads();
+    if (slot + d < SL) suf = quad_add(suf, soa_get<SL, Ext>(sh, slot + d), q);
+    __syncthreads();
+  }
+  if (slot >= 1) {
+    for (int k = 0; k < log2g + log2m; k++) suf = quad_dbl(suf, q);
+    val = quad_add(val, suf, q);
+  }
+  for (int d = SL / 2; d >= 1; d >>= 1) {
+    quad_put<SL>(sh, slot, val, q);
+    __syncthreads();
+    if (slot < d) val = quad_add(val, soa_get<SL, Ext>(sh, slot + d), q);
     __syncthreads();
   }
   if (t == 0 && ext_out) ext_out[b] = val;
@@ -322,58 +448,6 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket(const Fq* __restrict__ scala
   if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
 }
 
-// ---- quad-cooperative point arithmetic for the latency path --------------------------------------
-// The four lanes of a quad hold the same point and split each addition's field products between them:
-// product round 1 gives lane r one of A, B, C', D of add-2008-hwcd-3, round 2 scales C' by 2d (lane 2),
-// round 3 gives lane r one of X3, Y3, T3, Z3; DPP quad broadcasts exchange the products. The dependent chain
-// of an addition drops from 10 (mixed: 7) field multiplications to 3 (2); every formula and value is the one
-// ext_add / ext_madd compute, so the group element (and its encoding) is identical.
-template <int K>
-__device__ __forceinline__ Fp fp_qbcast(const Fp& a) {
-  Fp r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
-  return r;
-}
-__device__ __forceinline__ Fp fp_sel(bool c, const Fp& a, const Fp& b) {
-  Fp r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.l[i] = c ? a.l[i] : b.l[i];
-  return r;
-}
-// lane q holds product q of (A, B, C, D); returns the sum point on every lane of the quad
-__device__ __forceinline__ Ext quad_finish(const Fp& p, int q) {
-  const Fp A = fp_qbcast<0>(p), B = fp_qbcast<1>(p), C = fp_qbcast<2>(p), D = fp_qbcast<3>(p);
-  const Fp E = fp_sub(B, A), F = fp_sub(D, C), G = fp_add(D, C), H = fp_add(B, A);
-  // X3 = E F (lane 0), Y3 = G H (1), T3 = E H (2), Z3 = F G (3)
-  const Fp u = fp_sel(q == 0 || q == 2, E, fp_sel(q == 1, G, F));
-  const Fp v = fp_sel(q == 0, F, fp_sel(q == 3, G, H));
-  const Fp w = fp_mul(u, v);
-  Ext r;
-  r.X = fp_qbcast<0>(w);
-  r.Y = fp_qbcast<1>(w);
-  r.T = fp_qbcast<2>(w);
-  r.Z = fp_qbcast<3>(w);
-  return r;
-}
-// P + (+-Niels); qv is this lane's Niels coordinate: lane 0 the "minus" one (neg ? ypx : ymx), lane 1 the
-// "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it)
-__device__ __forceinline__ Ext quad_madd(const Ext& P, const Fp& qv, bool neg, int q) {
-  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
-  const Fp y = fp_sel(q == 3, fp_small(2), qv);
-  Fp p = fp_mul(x, y);
-  p = fp_sel(neg && q == 2, fp_neg(p), p);
-  return quad_finish(p, q);
-}
-__device__ __forceinline__ Ext quad_add(const Ext& P, const Ext& Q, int q) {
-  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
-  const Fp y = fp_sel(q == 0, fp_sub(Q.Y, Q.X), fp_sel(q == 1, fp_add(Q.Y, Q.X), fp_sel(q == 2, Q.T, Q.Z)));
-  Fp p = fp_mul(x, y);
-  const Fp pd = fp_mul(p, c_d2());  // C = 2d T1 T2 (lane 2)
-  p = fp_sel(q == 2, pd, fp_sel(q == 3, fp_add(p, p), p));  // D = 2 Z1 Z2 (lane 3)
-  return quad_finish(p, q);
-}
-
 // Latency-path bucket kernel, quad form: one workgroup per (bucket v, MSM b) as k_smsm_bucket, but the
 // table entries of bucket v are first collected in LDS (one round of BS scalars at a time) and dealt out
 // evenly to the BS/4 quads, which add them with the quad-split arithmetic; the quads' sums then meet in an
@@ -440,11 +514,7 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket_q(const Fq* __restrict__ sca
     __syncthreads();
   }
   for (int d = S / 2; d >= 1; d >>= 1) {
-    if (slot >= d && slot < 2 * d) {
-      const Fp c = fp_sel(q == 0, acc.X, fp_sel(q == 1, acc.Y, fp_sel(q == 2, acc.Z, acc.T)));
-#pragma unroll
-      for (int i = 0; i < 8; i++) pts[(q * 8 + i) * S + (slot - d)] = c.l[i];
-    }
+    if (slot >= d && slot < 2 * d) quad_put<S>(pts, slot - d, acc, q);
     __syncthreads();
     if (slot < d) acc = quad_add(acc, soa_get<S, Ext>(pts, slot), q);
     __syncthreads();
@@ -452,10 +522,6 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket_q(const Fq* __restrict__ sca
   if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
 }
 
-static bool use_quad() {
-  static const bool on = !getenv("SPG_SMSM_QUAD") || atoi(getenv("SPG_SMSM_QUAD")) != 0;
-  return on;
-}
 
 // the latency-path bucket kernel, quad form unless SPG_SMSM_QUAD=0
 #define SMSM_LAUNCH(BSZ, ...)                                                                   \
@@ -481,6 +547,26 @@ __global__ void __launch_bounds__(256) k_smsm_final(const Ext* __restrict__ buck
     soa_put<256>(sh, t, suf);
     __syncthreads();
     if (t < d) suf = ext_add(suf, soa_get<256, Ext>(sh, t + d));
+    __syncthreads();
+  }
+  if (t == 0) out[b] = suf;
+}
+
+// k_smsm_final with quads: 4 NB threads (NB <= 256), slot = thread / 4 plays bucket slot's thread
+__global__ void __launch_bounds__(1024) k_smsm_final_q(const Ext* __restrict__ buckets, int NB, Ext* __restrict__ out) {
+  __shared__ uint32_t sh[soa_words<Ext, 256>()];
+  const int b = blockIdx.x, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  Ext suf = buckets[(size_t)b * NB + slot];
+  for (int d = 1; d < NB; d <<= 1) {
+    quad_put<256>(sh, slot, suf, q);
+    __syncthreads();
+    if (slot + d < NB) suf = quad_add(suf, soa_get<256, Ext>(sh, slot + d), q);
+    __syncthreads();
+  }
+  for (int d = NB / 2; d >= 1; d >>= 1) {
+    quad_put<256>(sh, slot, suf, q);
+    __syncthreads();
+    if (slot < d) suf = quad_add(suf, soa_get<256, Ext>(sh, slot + d), q);
     __syncthreads();
   }
   if (t == 0) out[b] = suf;
@@ -516,7 +602,10 @@ static void launch_small(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const 
                          h, tab, bk);
   }
   KScope ks(ctx, "msm_small_final");
-  hipLaunchKernelGGL(k_smsm_final, dim3(B), dim3(NB), 0, s, bk, NB, out);
+  if (use_quad())
+    hipLaunchKernelGGL(k_smsm_final_q, dim3(B), dim3(4 * NB), 0, s, bk, NB, out);
+  else
+    hipLaunchKernelGGL(k_smsm_final, dim3(B), dim3(NB), 0, s, bk, NB, out);
 }
 
 template <int C>
@@ -739,7 +828,10 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   }
   {
     KScope ks(ctx, "msm_final");
-    hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(256), 0, s, segT, segS, d_out, S, log2m, d_ext);
+    if (use_quad())
+      hipLaunchKernelGGL(k_final_q<128>, dim3((unsigned)B), dim3(512), 0, s, segT, segS, d_out, S, log2m, d_ext);
+    else
+      hipLaunchKernelGGL(k_final, dim3((unsigned)B), dim3(256), 0, s, segT, segS, d_out, S, log2m, d_ext);
   }
   SPG_HIP(ctx, hipGetLastError());
   return 0;
