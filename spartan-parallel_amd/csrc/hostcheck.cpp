@@ -16,7 +16,7 @@ static void stq(uint64_t* p, const Fq& a) { memcpy(p, a.l, 32); }
 
 extern "C" {
 
-// op: 0 add, 1 sub, 2 mul, 3 neg, 4 square, 5 invert, 6 from_mont, 7 to_mont
+// op: 0 add, 1 sub, 2 mul, 3 neg, 4 square, 5 invert, 6 from_mont, 7 to_mont, 8 mul_ps, 9 mul32
 void spgh_fq_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n) {
   for (size_t i = 0; i < n; i++) {
     Fq x = ldq(a + 4 * i), y = b ? ldq(b + 4 * i) : fq_zero(), r;
@@ -28,6 +28,8 @@ void spgh_fq_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, siz
       case 4: r = fq_sqr(x); break;
       case 5: r = fq_inv(x); break;
       case 6: r = fq_from_mont(x); break;
+      case 8: r = fq_mul_ps(x, y); break;  // the device's product-scanning Montgomery product
+      case 9: r = fq_mul32(x, y); break;   // the CIOS form
       default: r = fq_to_mont(x); break;
     }
     stq(out + 4 * i, r);

@@ -30,7 +30,8 @@ def rand_fq(oracle, rng, n):
     return oracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * n, dtype=np.uint8).tobytes())
 
 
-@pytest.mark.parametrize("op,code", [("add", 0), ("sub", 1), ("mul", 2), ("neg", 3), ("square", 4), ("invert", 5)])
+@pytest.mark.parametrize("op,code", [("add", 0), ("sub", 1), ("mul", 2), ("neg", 3), ("square", 4), ("invert", 5),
+                                     ("mul", 8), ("mul", 9)])  # 8, 9: the device's product-scanning and CIOS forms
 def test_fq_ops(oracle, hc, op, code):
     rng = np.random.default_rng(code)
     n = 4000 if code != 5 else 200
@@ -38,6 +39,7 @@ def test_fq_ops(oracle, hc, op, code):
     a[0] = 0
     a[1] = oracle.fq_from_u64(1)
     b[2] = oracle.fq_op("neg", oracle.fq_from_u64(1))[0]
+    a[3] = b[3] = oracle.fq_op("neg", oracle.fq_from_u64(1))[0]  # (q-1)^2
     if code == 5:
         a[0] = oracle.fq_from_u64(3)
     out = np.zeros_like(a)
