@@ -1,25 +1,23 @@
 #!/usr/bin/env python3
-"""Benchmark: R1CS constraints/sec of the GPU-resident R1CSProof::prove (libspg.so) on MI355X.
+"""Benchmark for the MI355X Spartan prover (libspg.so), one JSON line on rank 0.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched under
-torch.distributed.run, one rank per GPU. Prints ONE JSON line on rank 0.
+torch.distributed.run, one rank per GPU.
 
-Workload (SURVEY.md 8d, config 3 shape): the data-parallel R1CS satisfiability proof that SNARK::prove
-runs for its blocks (src/r1csproof.rs:210-685, called from src/lib.rs:2259-2490): P = 2 block instances,
-X = 2^10 constraints each, Q = 2^9 executions each -> N = 2^20 constraints, synthetic chain-of-squarings
-circuit (spartan-parallel_amd/workload.py). A step is one full R1CSProof::prove with the instance,
-witness and generators already resident in HBM; the proof bytes are produced in every step.
-Multi-GPU (--mode):
-  replicas (default): every rank proves its own 2^20-constraint R1CS (independent proofs, no collective on
-           the data path) -> weak scaling; value = all ranks' constraints / max-over-ranks time.
-  shard:   ONE proof over 2N instances (2^20 constraints per GPU) sharded by instance across the N ranks;
-           per sumcheck round the ranks allgather 96 B of partial sums (spg_set_comm over torch.distributed:
-           RCCL with --backend nccl) and replicate the transcript -> weak scaling of a single proof.
+--workload snark (default, the headline metric): SNARK::prove (src/lib.rs:971-2746)
+    on a synthetic 2^20-constraint program (2 block types x 2^9 executions x 2^10 constraints), instances
+    encoded and witness resident in HBM before the timed region; every step produces the full bincode(SNARK),
+    compared byte-for-byte with the CPU oracle's. Multi-GPU: independent replicas (weak scaling).
+--workload r1cs: the block R1CSProof::prove alone (src/r1csproof.rs:210-685); --mode shard splits ONE proof
+    over the ranks by instance with a per-round allgather (spg_set_comm).
+--workload spark: SURVEY 8d config 5, multi_evaluate + SparseMatPolyEvalProof::prove at 3 x 2^k nonzeros.
+--workload msm: SURVEY 8d config 2, one 2^16-point MSM split over the ranks (spg_msm_partial + allgather +
+    spg_points_sum_compress, strong scaling).
 
-`roofline` is computed for the kernel with the largest device time among those with an algorithmic
-byte model (libspg's per-launch HIP-event timing on the context stream, spg_prof_read), `cpu_baseline`
-is the C++ CPU restatement of the reference (oracle/, 1 thread) on rank 0 at N = 1, which also checks
-that the GPU proof bytes equal the CPU proof bytes on the same workload and seed.
+`roofline` is computed for the kernel with the largest device time among those with an algorithmic byte
+model (libspg's per-launch HIP-event timing on its context stream, spg_prof_read, taken in a separate pass
+after the timed steps); `traffic` comes from the committed PMC summary (profiles/r01_pmc_traffic.json).
+`cpu_baseline` is the C++ CPU restatement of the reference (oracle/, 1 thread) on rank 0 at N = 1.
 """
 import argparse
 import hashlib
