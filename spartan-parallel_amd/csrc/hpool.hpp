@@ -45,17 +45,17 @@ class Pool {
     std::lock_guard<std::mutex> call(call_mu_);  // one burst at a time
     uint32_t g;
     bool wake;
-    {
+    g = ++gen_;
+    fn_.store(&f);
+    n_.store(n);
+    remaining_.store(n);
+    next_.store((uint64_t)g << 32);
+    gen_pub_.store(g);  // seq_cst: pairs with a parking worker's sleepers_ increment (no lost wake-up)
+    wake = sleepers_.load() > 0;
+    if (wake) {
       std::lock_guard<std::mutex> lk(mu_);
-      g = ++gen_;
-      fn_ = &f;
-      n_ = n;
-      remaining_.store(n);
-      next_.store((uint64_t)g << 32);
-      gen_pub_.store(g, std::memory_order_release);
-      wake = sleepers_ > 0;
+      cv_.notify_all();
     }
-    if (wake) cv_.notify_all();
     work(g, &f, n);
     while (remaining_.load() > 0) std::this_thread::yield();
   }
@@ -84,29 +84,31 @@ class Pool {
         __builtin_ia32_pause();
 #endif
       }
-      {
+      if (gen_pub_.load() == seen) {  // park until the next burst
         std::unique_lock<std::mutex> lk(mu_);
         sleepers_++;
-        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        cv_.wait(lk, [&] { return quit_pub_.load() || gen_pub_.load() != seen; });
         sleepers_--;
-        if (quit_) return;
-        seen = g = gen_;
-        f = fn_;
-        n = n_;
       }
+      if (quit_pub_.load()) return;
+      // lock-free snapshot: f and n are at least as new as g; if a newer burst already replaced them, the
+      // generation check in work() finds next_ tagged with another generation and returns at once
+      seen = g = gen_pub_.load();
+      f = fn_.load();
+      n = n_.load();
       work(g, f, n);
     }
   }
   std::vector<std::thread> threads_;
   std::mutex mu_, call_mu_;
   std::condition_variable cv_;
-  const std::function<void(int)>* fn_ = nullptr;
-  int n_ = 0;
-  uint32_t gen_ = 0;
+  std::atomic<const std::function<void(int)>*> fn_{nullptr};
+  std::atomic<int> n_{0};
+  uint32_t gen_ = 0;  // written by the (serialised) caller only
   std::atomic<uint64_t> next_{0};
   std::atomic<int> remaining_{0};
   bool quit_ = false;
-  int sleepers_ = 0;
+  std::atomic<int> sleepers_{0};
   std::atomic<uint32_t> gen_pub_{0};
   std::atomic<bool> quit_pub_{false};
   std::chrono::microseconds spin_{300};
