@@ -391,6 +391,42 @@ struct CQ {
     std::vector<Pt>* out;
   };
   std::vector<Item> items;
+  // Early group: device-resident polynomials (the block witnesses) whose rows are committed by one batch MSM
+  // launched before the host builds the permutation witnesses, so the device works while the host does;
+  // flush() only downloads those rows. Their commitments depend on the witness alone, never on the
+  // transcript, and they are recomputed in every prove.
+  std::vector<const Fq*> early_dev;
+  size_t early_R = 0, early_L = 0;
+  uint8_t* early_out = nullptr;
+  int launch_early(spg_ctx* ctx, ProverGens& g, const std::vector<std::pair<const Fq*, size_t>>& its) {
+    size_t R = 0, total = 0;
+    for (auto& it : its) {
+      const size_t nv = lg2(it.second), r = (size_t)1 << (nv - nv / 2);
+      if (R && r != R) return 0;  // one width only; otherwise flush() groups them as usual
+      R = r;
+      total += it.second;
+    }
+    // the one-launch batch path of commit_rows only (rows wider than the latency path, one chunk)
+    if (its.empty() || R <= 256 || R > g.n_pc || total / R > ((size_t)1 << 24) / R) return 0;
+    Fq* d = (Fq*)ws_get(ctx, 92, total * sizeof(Fq) + 64);
+    uint8_t* out = (uint8_t*)ws_get(ctx, 93, 32 * (total / R) + 64);
+    if (!d || !out) return set_err(ctx, SPG_E_NOMEM, "early commit staging");
+    size_t o = 0;
+    for (auto& it : its) {
+      SPG_HIP(ctx, hipMemcpyAsync(d + o, it.first, it.second * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
+      o += it.second;
+    }
+    int rc = msm_batch_device(ctx, g.dev, 0, d, R, total / R, nullptr, out, nullptr, (long)(g.n_pc + 1));
+    if (rc) return rc;
+    for (auto& it : its) early_dev.push_back(it.first);
+    early_R = R;
+    early_L = total / R;
+    early_out = out;
+    return 0;
+  }
+  bool is_early(const Item& it) const {
+    return it.dev && std::find(early_dev.begin(), early_dev.end(), it.dev) != early_dev.end();
+  }
   void add(const FqV& v, std::vector<Pt>* out) { items.push_back({&v, nullptr, v.size(), out}); }
   void add_dev(const Fq* d, size_t len, std::vector<Pt>* out) { items.push_back({nullptr, d, len, out}); }
   int flush(spg_ctx* ctx, ProverGens& g, Tr& t) {
@@ -398,17 +434,17 @@ struct CQ {
     for (auto& it : items) {
       const size_t nv = lg2(it.len), R = (size_t)1 << (nv - nv / 2);
       it.out->assign((size_t)1 << (nv / 2), Pt());
-      if (std::find(widths.begin(), widths.end(), R) == widths.end()) widths.push_back(R);
+      if (!is_early(it) && std::find(widths.begin(), widths.end(), R) == widths.end()) widths.push_back(R);
     }
     for (size_t R : widths) {
       size_t total = 0;
       for (auto& it : items)
-        if (((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) == R) total += it.len;
+        if (!is_early(it) && ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) == R) total += it.len;
       Fq* d = (Fq*)ws_get(ctx, 91, total * sizeof(Fq) + 64);
       if (!d) return set_err(ctx, SPG_E_NOMEM, "commit staging");
       size_t o = 0;
       for (auto& it : items) {
-        if (((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
+        if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
         if (it.host)
           SPG_HIP(ctx, hipMemcpyAsync(d + o, it.host->data(), it.len * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
         else
@@ -420,10 +456,24 @@ struct CQ {
       if (rc) return rc;
       o = 0;
       for (auto& it : items) {
-        if (((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
+        if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
         std::copy(rows.begin() + o, rows.begin() + o + it.out->size(), it.out->begin());
         o += it.out->size();
       }
+    }
+    if (early_L) {
+      std::vector<Pt> rows(early_L);
+      SPG_HIP(ctx, hipMemcpyAsync(rows.data(), early_out, 32 * early_L, hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      size_t o = 0;
+      for (const Fq* d : early_dev)  // rows in launch order
+        for (auto& it : items)
+          if (it.dev == d) {
+            std::copy(rows.begin() + o, rows.begin() + o + it.out->size(), it.out->begin());
+            o += it.out->size();
+          }
+      early_dev.clear();
+      early_L = 0;
     }
     for (auto& it : items) append_polycomm(t, "poly_commitment", *it.out);
     items.clear();
@@ -717,6 +767,12 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   if (rc) return rc;
 
   lp.lap("inst_commit+sort");
+  CQ cq;
+  {  // block_vars commitments: on the device now, read back when the queue is flushed
+    std::vector<std::pair<const Fq*, size_t>> bv;
+    for (size_t p = 0; p < P; p++) bv.push_back({W->d_block_vars[p], bnp_pad[p] * bnv[p]});
+    if ((rc = cq.launch_early(ctx, g, bv))) return rc;
+  }
   // ---- WITNESS GEN: block (lib.rs:1299-1741)
   const Fq tau = t.challenge("challenge_tau"), r = t.challenge("challenge_r");
   const bool dbg = getenv("SPG_DEBUG_SNARK") != nullptr;
@@ -730,7 +786,6 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     }
     perm_w0.resize(num_ios, fq_zero());
   }
-  CQ cq;
   std::vector<Pt> c_w0;
   cq.add(perm_w0, &c_w0);
   const Rows& exec = W->exec;
