@@ -116,6 +116,63 @@ __device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
   v2 = soa_get<256, Fq>(sh[2], 0);
   __syncthreads();
 }
+// block-wide sums of three Fq values over BS threads; the result is valid in thread 0
+template <int BS>
+__device__ __forceinline__ void block_sum3_t0(Fq& v0, Fq& v1, Fq& v2) {
+  __shared__ uint32_t sh[3][soa_words<Fq, BS / 2>()];
+  const int t = threadIdx.x;
+  for (int d = BS / 2; d >= 1; d >>= 1) {
+    if (t >= d && t < 2 * d) {
+      soa_put<BS / 2>(sh[0], t - d, v0);
+      soa_put<BS / 2>(sh[1], t - d, v1);
+      soa_put<BS / 2>(sh[2], t - d, v2);
+    }
+    __syncthreads();
+    if (t < d) {
+      v0 = fq_add(v0, soa_get<BS / 2, Fq>(sh[0], t));
+      v1 = fq_add(v1, soa_get<BS / 2, Fq>(sh[1], t));
+      v2 = fq_add(v2, soa_get<BS / 2, Fq>(sh[2], t));
+    }
+    __syncthreads();
+  }
+}
+// A whole round of a small layer in one workgroup of 1024 threads (nt * len <= 1024): first the previous
+// round's bound_poly_var_top of every layer vector (when do_fold; vectors of 2 flen -> flen, one pass,
+// __syncthreads), then the round's (e0, e2, e3) with each triple's coefficient applied per element, a block
+// reduction and the mailbox post. No grid-wide ticket and one launch instead of fold + eval.
+__global__ void __launch_bounds__(1024) k_layer_tiny(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
+                                                     int nt, int log_len, Fq* const* __restrict__ fv, int nv,
+                                                     int do_fold, Fq r, uint32_t* __restrict__ mb, uint32_t seq) {
+  const int t = threadIdx.x;
+  const int len = 1 << log_len;
+  if (do_fold) {
+    const int flen = 2 * len;  // folded length
+    for (int k = t; k < nv * flen; k += 1024) {
+      Fq* p = fv[k / flen];
+      const int i = k % flen;
+      const Fq lo = p[i];
+      p[i] = fq_add(lo, fq_mul(r, fq_sub(p[i + flen], lo)));
+    }
+    __syncthreads();
+  }
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  if (t < nt * len) {
+    const Triple x = tr[t >> log_len];
+    const Fq k = coeff[t >> log_len];
+    const int i = t & (len - 1);
+    Fq al = x.A[i], ah = x.A[i + len], bl = x.B[i], bh = x.B[i + len], cl = x.C[i], ch = x.C[i + len];
+    Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
+    Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
+    e0 = fq_mul(k, fq_mul(fq_mul(al, bl), cl));
+    e2 = fq_mul(k, fq_mul(fq_mul(a2, b2), c2));
+    e3 = fq_mul(k, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
+  }
+  block_sum3_t0<1024>(e0, e2, e3);
+  if (t == 0) {
+    const Fq rr[3] = {e0, e2, e3};
+    mbox_post(mb, seq, rr, 3);
+  }
+}
 // one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
 // sum_c coeff_c * sum_i A*B*C at X = 0, 2, 3 (sumcheck.rs:300-367). blockIdx.y = triple, so the coefficient
 // multiplies the block's sums once; the last block to finish (ticket on `counter`) adds every block's
@@ -456,11 +513,26 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     LayerProofP lpf;
     FqV r_prod;
     size_t log_len = rounds;
+    bool pending = false;  // a bound_poly_var_top with r_pend not yet launched
+    Fq r_pend = fq_zero();
+    static const bool tiny_ok = !getenv("SPG_SPARK_TINY") || atoi(getenv("SPG_SPARK_TINY")) != 0;
     for (size_t j = 0; j < rounds; j++) {
       log_len--;
       const size_t len = (size_t)1 << log_len;
       const unsigned nbx = (unsigned)std::min<size_t>(nblk(len), std::max<size_t>(1, 2048 / tr.size()));
-      {
+      const bool tiny = tiny_ok && tr.size() * len <= 1024;
+      if (pending && !tiny) {
+        KScope ks(ctx, "spark_fold", 96.0 * fold.size() * (2 * len));
+        hipLaunchKernelGGL(k_fold_many, dim3(nblk(fold.size() * 2 * len)), dim3(256), 0, s, dptr, fold.size(),
+                           (int)log_len + 1, r_pend);
+        pending = false;
+      }
+      if (tiny) {  // the pending fold and this round's evaluations in one workgroup
+        KScope ks(ctx, "spark_layer_tiny", 192.0 * tr.size() * len + (pending ? 192.0 * fold.size() * len : 0.0));
+        hipLaunchKernelGGL(k_layer_tiny, dim3(1), dim3(1024), 0, s, dtr, dcoef, (int)tr.size(), (int)log_len, dptr,
+                           (int)fold.size(), pending ? 1 : 0, r_pend, ctx->d_mbox, ++ctx->mbox_seq);
+        pending = false;
+      } else {
         KScope ks(ctx, "spark_layer_eval", 192.0 * tr.size() * len);
         hipLaunchKernelGGL(k_layer_eval, dim3(nbx, (unsigned)tr.size()), dim3(256), 0, s, dtr, dcoef, len, part,
                            ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
@@ -475,15 +547,17 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
       Fq r_j = t.challenge("challenge_nextround");
       r_prod.push_back(r_j);
       lp.lap("round_host");
-      {
-        KScope ks(ctx, "spark_fold", 96.0 * fold.size() * len);
-        hipLaunchKernelGGL(k_fold_many, dim3(nblk(fold.size() * len)), dim3(256), 0, s, dptr, fold.size(),
-                           (int)log_len, r_j);
-      }
+      pending = true;  // bound_poly_var_top with r_j: launched with (or before) the next round's evaluation
+      r_pend = r_j;
       SPG_HIP(ctx, hipGetLastError());
       e = uni_eval(poly, r_j);
       lpf.polys.push_back({poly[0], poly[2], poly[3]});
       lp.lap("round_fold_launch");
+    }
+    if (pending) {  // the last round's fold
+      KScope ks(ctx, "spark_fold", 96.0 * fold.size());
+      hipLaunchKernelGGL(k_fold_many, dim3(nblk(fold.size())), dim3(256), 0, s, dptr, fold.size(), 0, r_pend);
+      pending = false;
     }
     // final claims: A[0], B[0] (and C[0] for the dot-product circuits)
     hipLaunchKernelGGL(k_finals, dim3(nblk(tr.size())), dim3(256), 0, s, dtr, tr.size(), dfin);
