@@ -833,7 +833,7 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
       // encodings one lane per MSM (k_compress_ext) instead of on one lane of each k_final block: the
       // ~250 dependent squarings of an encoding would otherwise serialise behind every block's tree
       Ext* ext = d_ext;
-      if (!ext && d_out) ext = (Ext*)ws_get(ctx, 16, B * sizeof(Ext) + 64);
+      if (!ext && d_out) ext = (Ext*)ws_get(ctx, 17, B * sizeof(Ext) + 64);
       if (!ext) return set_err(ctx, SPG_E_NOMEM, "msm final points");
       hipLaunchKernelGGL(k_final_q<128>, dim3((unsigned)B), dim3(512), 0, s, segT, segS, nullptr, S, log2m, ext);
       if (d_out)

@@ -64,6 +64,13 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
   __shared__ bool last;
   block_sum3(v0, v1, v2);
   const int t = threadIdx.x;
+  if (gridDim.x == 1) {  // a one-block round posts directly: no partials, ticket or second reduction
+    if (t == 0) {
+      const Fq r[3] = {v0, v1, v2};
+      mbox_post(mb, seq, r, 3);
+    }
+    return;
+  }
   if (t == 0) {
     partials[3 * blockIdx.x] = v0;
     partials[3 * blockIdx.x + 1] = v1;
