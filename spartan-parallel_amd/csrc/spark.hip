@@ -136,7 +136,7 @@ __device__ __forceinline__ void block_sum3_t0(Fq& v0, Fq& v1, Fq& v2) {
     __syncthreads();
   }
 }
-// A whole round of a small layer in one workgroup of 1024 threads (nt * len <= 1024): first the previous
+// A whole round of a small layer in one workgroup of 1024 threads (nt * len up to a few thousand): first the previous
 // round's bound_poly_var_top of every layer vector (when do_fold; vectors of 2 flen -> flen, one pass,
 // __syncthreads), then the round's (e0, e2, e3) with each triple's coefficient applied per element, a block
 // reduction and the mailbox post. No grid-wide ticket and one launch instead of fold + eval.
@@ -156,16 +156,16 @@ __global__ void __launch_bounds__(1024) k_layer_tiny(const Triple* __restrict__ 
     __syncthreads();
   }
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
-  if (t < nt * len) {
-    const Triple x = tr[t >> log_len];
-    const Fq k = coeff[t >> log_len];
-    const int i = t & (len - 1);
+  for (int u = t; u < nt * len; u += 1024) {
+    const Triple x = tr[u >> log_len];
+    const Fq k = coeff[u >> log_len];
+    const int i = u & (len - 1);
     Fq al = x.A[i], ah = x.A[i + len], bl = x.B[i], bh = x.B[i + len], cl = x.C[i], ch = x.C[i + len];
     Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
     Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
-    e0 = fq_mul(k, fq_mul(fq_mul(al, bl), cl));
-    e2 = fq_mul(k, fq_mul(fq_mul(a2, b2), c2));
-    e3 = fq_mul(k, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
+    e0 = fq_add(e0, fq_mul(k, fq_mul(fq_mul(al, bl), cl)));
+    e2 = fq_add(e2, fq_mul(k, fq_mul(fq_mul(a2, b2), c2)));
+    e3 = fq_add(e3, fq_mul(k, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc))));
   }
   block_sum3_t0<1024>(e0, e2, e3);
   if (t == 0) {
@@ -516,11 +516,12 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     bool pending = false;  // a bound_poly_var_top with r_pend not yet launched
     Fq r_pend = fq_zero();
     static const bool tiny_ok = !getenv("SPG_SPARK_TINY") || atoi(getenv("SPG_SPARK_TINY")) != 0;
+    static const size_t tiny_max = getenv("SPG_SPARK_TINY_MAX") ? (size_t)atoi(getenv("SPG_SPARK_TINY_MAX")) : 2048;
     for (size_t j = 0; j < rounds; j++) {
       log_len--;
       const size_t len = (size_t)1 << log_len;
       const unsigned nbx = (unsigned)std::min<size_t>(nblk(len), std::max<size_t>(1, 2048 / tr.size()));
-      const bool tiny = tiny_ok && tr.size() * len <= 1024;
+      const bool tiny = tiny_ok && tr.size() * len <= tiny_max;
       if (pending && !tiny) {
         KScope ks(ctx, "spark_fold", 96.0 * fold.size() * (2 * len));
         hipLaunchKernelGGL(k_fold_many, dim3(nblk(fold.size() * 2 * len)), dim3(256), 0, s, dptr, fold.size(),
