@@ -5,9 +5,11 @@
 // per-generator weights cw that are products of u / u^-1. So every L, R (and the final g_hat) is a
 // fixed-base MSM over the generator table already resident in HBM (msm.hip); no curve point is ever
 // folded and the group elements produced are identical to the reference's.
+#include <chrono>
 #include <functional>
 
 #include "hostpoly.hpp"
+
 #include "proto.hpp"
 
 namespace spg {
@@ -27,7 +29,22 @@ h::HExt commit_host(ProverGens& g, const KeyView& k, const FqV& x, const Fq& bli
 }
 
 // independent commitments computed together on the host pool (Commitments::commit, src/commitments.rs:69-92)
+// SPG_TRACE >= 2: cumulative host time and count of the sigma-protocol commitments (printed by SNARK::prove)
+CommitStats g_commit_stats;
 std::vector<Pt> commit_batch(ProverGens& g, const std::vector<CJob>& jobs) {
+  static const bool tr2 = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2;
+  const auto t0 = tr2 ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+  struct Done {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    size_t n;
+    ~Done() {
+      if (!on) return;
+      g_commit_stats.us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      g_commit_stats.calls++;
+      g_commit_stats.points += n;
+    }
+  } done{tr2, t0, jobs.size()};
   std::vector<std::pair<std::vector<size_t>, FqV>> j2;
   for (auto& j : jobs) {
     std::vector<size_t> idx;

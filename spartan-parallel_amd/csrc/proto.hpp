@@ -111,6 +111,11 @@ struct CJob {
   CJob(const KeyView& kv, const FqV& xx, const Fq& b) : k(&kv), h(kv.h), x(xx), blind(b) {}
   CJob(size_t h_index, const Fq& b) : k(nullptr), h(h_index), blind(b) {}
 };
+struct CommitStats {
+  double us = 0;
+  size_t calls = 0, points = 0;
+};
+extern CommitStats g_commit_stats;  // SPG_TRACE >= 2
 std::vector<Pt> commit_batch(ProverGens& g, const std::vector<CJob>& jobs);
 KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C);
 EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& v1, const Fq& s1,

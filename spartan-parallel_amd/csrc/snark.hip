@@ -1219,6 +1219,11 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   }
   lp.lap("io");
   lp.print();
+  if (getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2) {
+    fprintf(stderr, "[spg] sigma-protocol commitments: %zu calls, %zu commitments, %.0f us on the host\n",
+                    g_commit_stats.calls, g_commit_stats.points, g_commit_stats.us);
+    g_commit_stats = CommitStats();
+  }
   *proof_len = w.out.size();
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, w.out.data(), w.out.size());
