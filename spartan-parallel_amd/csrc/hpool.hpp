@@ -2,7 +2,7 @@
 // Between two Fiat-Shamir challenges the prover computes a handful of independent fixed-base
 // commitments and point encodings (tens of microseconds each); running them on several host cores
 // shortens every sumcheck round. Bursts come every few tens of microseconds inside a proof, so a worker
-// spins on the burst generation for a while (SPG_POOL_SPIN_US, default 300) before it parks on the
+// spins on the burst generation for a while (SPG_POOL_SPIN_US, default 20 ms) before it parks on the
 // condition variable: a futex wake-up costs 10-30 us per burst, a spinning worker picks the burst up at once.
 //
 // Task indices are claimed with a CAS on one 64-bit word holding (burst generation, next index), and
@@ -24,7 +24,7 @@ class Pool {
  public:
   explicit Pool(int nthreads) {
     const char* e = getenv("SPG_POOL_SPIN_US");
-    spin_ = std::chrono::microseconds(e ? atoi(e) : 300);
+    spin_ = std::chrono::microseconds(e ? atoi(e) : 20000);
     for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
   }
   ~Pool() {
@@ -111,7 +111,7 @@ class Pool {
   std::atomic<int> sleepers_{0};
   std::atomic<uint32_t> gen_pub_{0};
   std::atomic<bool> quit_pub_{false};
-  std::chrono::microseconds spin_{300};
+  std::chrono::microseconds spin_{20000};
 };
 
 inline Pool& pool() {
