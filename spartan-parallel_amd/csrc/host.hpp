@@ -10,7 +10,9 @@
 #include <string.h>
 
 #include <functional>
+#include <atomic>
 #include <map>
+#include <memory>
 #include <vector>
 
 #include "curve.hpp"
@@ -173,6 +175,13 @@ struct HostGens {
     }
     const int ntask = (int)terms.size() * kShares;
     std::vector<h::HExt> part(ntask);
+    // one burst: the last share of a job to finish (per-job countdown) adds the job's shares and encodes it
+    std::vector<int> first(jobs.size() + 1, 0);
+    for (size_t k = 0; k < terms.size(); k++) first[terms[k].first + 1] = (int)(k + 1) * kShares;
+    for (size_t j = 1; j <= jobs.size(); j++) first[j] = std::max(first[j], first[j - 1]);
+    std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[jobs.size()]);
+    for (size_t j = 0; j < jobs.size(); j++) left[j].store(first[j + 1] - first[j]);
+    std::vector<Pt> out(jobs.size());
     pool().parallel_for(ntask, [&](int k) {
       const auto& tm = terms[k / kShares];
       const auto& jb = jobs[tm.first];
@@ -180,11 +189,12 @@ struct HostGens {
       h::HExt acc = h::hext_identity();
       fb.find(jb.first[tm.second])->second.mul_add_windows(acc, jb.second[tm.second], w0, w0 + 32 / kShares);
       part[k] = acc;
+      if (left[tm.first].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        h::HExt sum = part[first[tm.first]];
+        for (int i = first[tm.first] + 1; i < first[tm.first + 1]; i++) sum = h::hext_add(sum, part[i]);
+        out[tm.first] = compress(sum);
+      }
     });
-    std::vector<h::HExt> sum(jobs.size(), h::hext_identity());
-    for (int k = 0; k < ntask; k++) sum[terms[k / kShares].first] = h::hext_add(sum[terms[k / kShares].first], part[k]);
-    std::vector<Pt> out(jobs.size());
-    pool().parallel_for((int)jobs.size(), [&](int j) { out[j] = compress(sum[j]); });
     return out;
   }
 };

@@ -5,8 +5,10 @@
 // per-generator weights cw that are products of u / u^-1. So every L, R (and the final g_hat) is a
 // fixed-base MSM over the generator table already resident in HBM (msm.hip); no curve point is ever
 // folded and the group elements produced are identical to the reference's.
+#include <atomic>
 #include <chrono>
 #include <functional>
+#include <memory>
 
 #include "hostpoly.hpp"
 
@@ -170,9 +172,12 @@ static h::HExt hext_small_mul(h::HExt P, unsigned k) {
 
 void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out) {
   // chunk (lo, hi] of a bucket set: run = sum B_v, acc = sum (v - lo) B_v; the set's sum is
-  // sum over chunks of acc + lo * run. Chunks spread one MSM's 2 NB dependent additions over the pool.
+  // sum over chunks of acc + lo * run. Chunks spread one MSM's 2 NB dependent additions over the pool;
+  // the last chunk of an MSM to finish (countdown) adds the chunks and encodes, all in one burst.
   const int K = NB >= 64 ? 8 : 1, per = NB / K;
   std::vector<h::HExt> part(B * K);
+  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[B]);
+  for (size_t b = 0; b < B; b++) left[b].store(K);
   pool().parallel_for((int)(B * K), [&](int task) {
     const size_t b = task / K;
     const int lo = (task % K) * per;
@@ -182,16 +187,12 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out) {
       acc = h::hext_add(acc, run);
     }
     part[task] = lo ? h::hext_add(acc, hext_small_mul(run, (unsigned)lo)) : acc;
+    if (left[b].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+      h::HExt s = part[b * K];
+      for (int c = 1; c < K; c++) s = h::hext_add(s, part[b * K + c]);
+      out[b] = compress(s);
+    }
   });
-  auto fin = [&](int b) {
-    h::HExt s = part[(size_t)b * K];
-    for (int c = 1; c < K; c++) s = h::hext_add(s, part[(size_t)b * K + c]);
-    out[b] = compress(s);
-  };
-  if (B <= 2)
-    for (int b = 0; b < (int)B; b++) fin(b);
-  else
-    pool().parallel_for((int)B, fin);
 }
 
 // B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
