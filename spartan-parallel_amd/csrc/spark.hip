@@ -506,9 +506,18 @@ static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims
     FqV coeffs = t.challenges("rand_coeffs_next_layer", claims.size());
     Fq e = fq_zero();
     for (size_t i = 0; i < claims.size(); i++) e = fq_add(e, fq_mul(claims[i], coeffs[i]));
-    SPG_HIP(ctx, hipMemcpyAsync(dtr, tr.data(), tr.size() * sizeof(Triple), hipMemcpyHostToDevice, s));
-    SPG_HIP(ctx, hipMemcpyAsync(dcoef, coeffs.data(), coeffs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
-    SPG_HIP(ctx, hipMemcpyAsync(dptr, fold.data(), fold.size() * sizeof(Fq*), hipMemcpyHostToDevice, s));
+    {  // descriptors up through page-locked staging (a pageable source blocks the host for a staging blit);
+       // the staging is free again here: the previous layer ended with a synchronising download
+      const size_t b1 = tr.size() * sizeof(Triple), b2 = coeffs.size() * sizeof(Fq), b3 = fold.size() * sizeof(Fq*);
+      uint8_t* st = (uint8_t*)pinned_get(ctx, b1 + b2 + b3 + 64);
+      if (!st) return set_err(ctx, SPG_E_NOMEM, "layer staging");
+      memcpy(st, tr.data(), b1);
+      memcpy(st + b1, coeffs.data(), b2);
+      memcpy(st + b1 + b2, fold.data(), b3);
+      SPG_HIP(ctx, hipMemcpyAsync(dtr, st, b1, hipMemcpyHostToDevice, s));
+      SPG_HIP(ctx, hipMemcpyAsync(dcoef, st + b1, b2, hipMemcpyHostToDevice, s));
+      SPG_HIP(ctx, hipMemcpyAsync(dptr, st + b1 + b2, b3, hipMemcpyHostToDevice, s));
+    }
     lp.lap("layer_setup");
     LayerProofP lpf;
     FqV r_prod;
