@@ -19,7 +19,7 @@ NAMES = {
     "k_spmv": "spmv_block", "k_z_fill": "z_fill", "k_abc": "eval_table_abc", "k_bound_part": "poly_bound",
     "k_fold_top": "fold_dense", "k_eq_table": "eq_table", "k_cubic_eval": "sc_cubic_eval",
     "k_final": "msm_final", "k_segments": "msm_segments", "k_items": "msm_bucket_items",
-    "k_layer_eval": "spark_layer_eval", "k_fold_many": "spark_fold", "k_seg_dot": "spark_evaluate",
+    "k_layer_eval": "spark_layer_eval", "k_layer_tiny": "spark_layer_tiny", "k_fold_many": "spark_fold", "k_seg_dot": "spark_evaluate",
     "k_gather": "spark_deref", "k_bound_rows": "spark_bound", "k_dot3": "spark_dotp_eval",
     "k_tree_level": "spark_product_tree", "k_hash_ops": "spark_hash_layer",
 }
