@@ -329,6 +329,61 @@ __global__ void __launch_bounds__(256) k_final(const Ext* __restrict__ segT, con
   }
 }
 
+// k_segments with quads (4 lanes per segment, quad_add): for few MSMs, where the segment sums are a short
+// latency-bound phase rather than a throughput-bound one
+__global__ void __launch_bounds__(256) k_segments_q(const uint32_t* __restrict__ item_off,
+                                                    const Ext* __restrict__ partial, Ext* __restrict__ segT,
+                                                    Ext* __restrict__ segS, int B, int NB, int m) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x, q = t & 3, sid = t >> 2;
+  const int S = NB / m;
+  if (sid >= B * S) return;  // whole quads exit together (4 | blockDim)
+  const int b = sid / S, j = sid % S;
+  const int lo = j * m + 1, hi = j * m + m;
+  Ext run = ext_identity(), T = ext_identity();
+  bool any = false;
+  for (int v = hi; v >= lo; v--) {
+    const uint32_t key = (uint32_t)b * NB + (v - 1);
+    for (uint32_t it = item_off[key]; it < item_off[key + 1]; it++) {
+      run = any ? quad_add(run, partial[it], q) : partial[it];
+      any = true;
+    }
+    if (any) T = quad_add(T, run, q);
+  }
+  if (q == 0) {
+    segT[sid] = T;
+    segS[sid] = run;
+  }
+}
+// Regrouping for few MSMs with many segments: group c of G folds the g consecutive segments
+// [c g, c g + g) into T'_c = sum T_j + m sum_j (j - c g) S_j and S'_c = sum S_j (k_final's per-slot fold),
+// so the set becomes G segments of m' = m g buckets and k_final_q needs fewer sequential steps per slot.
+__global__ void __launch_bounds__(256) k_regroup_q(const Ext* __restrict__ segT, const Ext* __restrict__ segS, int B,
+                                                   int S, int log2g, int log2m, Ext* __restrict__ outT,
+                                                   Ext* __restrict__ outS) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x, q = t & 3, gid = t >> 2;
+  const int g = 1 << log2g, G = S >> log2g;
+  if (gid >= B * G) return;
+  const int b = gid / G, c = gid % G;
+  const Ext* T = segT + (size_t)b * S;
+  const Ext* Sv = segS + (size_t)b * S;
+  const int lo = c * g, hi = lo + g;
+  Ext U = ext_identity(), V = ext_identity(), acc = ext_identity(), tot = ext_identity();
+  for (int j = hi - 1; j >= lo; j--) {
+    U = quad_add(U, T[j], q);
+    V = quad_add(V, Sv[j], q);
+    if (j > lo) {
+      acc = quad_add(acc, Sv[j], q);
+      tot = quad_add(tot, acc, q);
+    }
+  }
+  for (int k = 0; k < log2m; k++) tot = quad_dbl(tot, q);
+  const Ext val = quad_add(U, tot, q);
+  if (q == 0) {
+    outT[gid] = val;
+    outS[gid] = V;
+  }
+}
+
 // k_final with quads: SL slots of 4 lanes (4 SL threads; SL = 128 keeps it under 256 VGPRs), slot plays
 // k_final's thread with SL in place of 256, every point operation
 // split over the quad (quad_add / quad_dbl)
@@ -823,8 +878,12 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   }
   {
     KScope ks(ctx, "msm_segments");
-    hipLaunchKernelGGL(k_segments, dim3((unsigned)((B * S + 63) / 64)), dim3(64), 0, s, item_off, partial, segT,
-                       segS, (int)B, NB, m);
+    if (use_quad() && B * (size_t)S <= 16384)
+      hipLaunchKernelGGL(k_segments_q, dim3((unsigned)((4 * B * S + 255) / 256)), dim3(256), 0, s, item_off, partial,
+                         segT, segS, (int)B, NB, m);
+    else
+      hipLaunchKernelGGL(k_segments, dim3((unsigned)((B * S + 63) / 64)), dim3(64), 0, s, item_off, partial, segT,
+                         segS, (int)B, NB, m);
   }
   {
     KScope ks(ctx, "msm_final");
@@ -835,7 +894,21 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
       Ext* ext = d_ext;
       if (!ext && d_out) ext = (Ext*)ws_get(ctx, 17, B * sizeof(Ext) + 64);
       if (!ext) return set_err(ctx, SPG_E_NOMEM, "msm final points");
-      hipLaunchKernelGGL(k_final_q<128>, dim3((unsigned)B), dim3(512), 0, s, segT, segS, nullptr, S, log2m, ext);
+      const Ext *fT = segT, *fS = segS;
+      int fSn = S, flog2m = log2m;
+      if (B <= 16 && S > 1024) {  // few MSMs with many segments: regroup 8 segments per group first
+        const int lg = 3, G = S >> lg;
+        Ext* rT = (Ext*)ws_get(ctx, 18, 2 * B * (size_t)G * sizeof(Ext) + 64);
+        if (!rT) return set_err(ctx, SPG_E_NOMEM, "msm regroup");
+        Ext* rS = rT + B * (size_t)G;
+        hipLaunchKernelGGL(k_regroup_q, dim3((unsigned)((4 * B * (size_t)G + 255) / 256)), dim3(256), 0, s, segT,
+                           segS, (int)B, S, lg, log2m, rT, rS);
+        fT = rT;
+        fS = rS;
+        fSn = G;
+        flog2m = log2m + lg;
+      }
+      hipLaunchKernelGGL(k_final_q<128>, dim3((unsigned)B), dim3(512), 0, s, fT, fS, nullptr, fSn, flog2m, ext);
       if (d_out)
         hipLaunchKernelGGL(k_compress_ext, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, ext, B, d_out);
     }
