@@ -251,6 +251,7 @@ static void par_range(size_t n, const std::function<void(size_t, size_t)>& f) {
 // src/nizk/mod.rs:439-523 + src/nizk/bullet.rs:32-132
 int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const FqV& x, const Fq& blind_x, const FqV& a,
                          const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy_out) {
+  g_msm_laps.lap("outside_bullet");
   t.protocol("dot product proof (log)");
   size_t n = x.size();
   size_t lg = 0;
@@ -285,16 +286,21 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   }
   Pt Cx = pts[0];
   t.point("Cx", Cx);
+  g_msm_laps.lap("bp_cx");
   Pt Cy = commit_batch(g, {CJob(g.gens_1, {y}, blind_y)})[0];
+  g_msm_laps.lap("bp_cy");
   t.point("Cy", Cy);
   t.scalars("a", a);
+  g_msm_laps.lap("bp_tr");
   Fq r = t.challenge("r");
   Fq blind_fin = fq_add(blind_x, fq_mul(r, blind_y));
   FqV aa(x), bb(a), cw(n, fq_one());
   size_t nk = n, k = 0;
+  g_msm_laps.lap("bullet_prep");
   while (nk != 1) {
     size_t nh = nk / 2;
     Fq cL = dot(aa, bb, 0, nh, nh), cR = dot(aa, bb, nh, 0, nh);
+    g_msm_laps.lap("bullet_dot");
     Fq blind_L = v1[k], blind_R = v2[k];
     // L scalars in hs[0 .. n2), R scalars in hs[n2 .. 2 n2)
     par_range(n, [&](size_t lo, size_t hi) {
@@ -313,6 +319,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     hs[n + 1] = blind_L;
     hs[n2 + n] = fq_mul(cR, r);
     hs[n2 + n + 1] = blind_R;
+    g_msm_laps.lap("bullet_scalars");
     int rc = device_msm_flat(ctx, g, hs, n2, 2, d_idx, &pts);
     if (rc) return rc;
     t.point("L", pts[0]);
@@ -329,6 +336,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
       for (size_t j = lo; j < hi; j++) cw[j] = fq_mul(cw[j], (j % nk) < nh ? uinv : u);
     });
     blind_fin = fq_add(fq_add(blind_fin, fq_mul(fq_mul(blind_L, u), u)), fq_mul(fq_mul(blind_R, uinv), uinv));
+    g_msm_laps.lap("bullet_fold");
     out->L.push_back(pts[0]);
     out->R.push_back(pts[1]);
     nk = nh;
