@@ -82,6 +82,7 @@ struct MsmArgs {
   const uint32_t* idx;  // optional: explicit generator index per scalar (B x n), overrides gen_offset
   uint32_t* hist;     // B*NB
   const uint32_t* off;
+  uint32_t* off_out;  // k_digits_rows: writes the bucket offsets itself
   uint32_t* cursor;
   uint32_t* entries;
 };
@@ -134,6 +135,86 @@ __global__ void k_digits(MsmArgs a, bool count) {
     gidx = (uint32_t)a.h_index;
   }
   emit_digits<C>(s, b, gidx, a.n1, a, count);
+}
+
+// Row-local counting sort for batches of many MSMs (one workgroup per MSM b): the bucket histogram and the
+// cursors live in LDS, so the 24 digit atomics per scalar are LDS atomics instead of L2 atomics on a
+// B*NB-key global histogram, and the entries of MSM b land in its own region [b*per*W, (b+1)*per*W) of
+// the entries array (off[key] points into it; k_items only reads off[key] and hist[key]). The bucket order
+// of entries differs from k_digits', the bucket sums (group elements) do not.
+template <int C>
+__global__ void __launch_bounds__(256) k_digits_rows(MsmArgs a) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  constexpr int PT = (NB + 255) / 256;  // keys per thread in the scan
+  __shared__ uint32_t cnt[NB], part[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int per = a.n + (a.blinds ? 1 : 0);
+  const uint32_t rowbase = (uint32_t)b * (uint32_t)per * (uint32_t)W;
+  for (int k = tid; k < NB; k += 256) cnt[k] = 0;
+  __syncthreads();
+  for (int pass = 0; pass < 2; pass++) {
+    for (int i = tid; i < per; i += 256) {
+      Fq sm;
+      uint32_t gidx;
+      if (i < a.n) {
+        sm = a.scalars[(size_t)b * a.n + i];
+        gidx = a.idx ? a.idx[(size_t)b * a.n + i] : (uint32_t)(a.gen_offset + i);
+      } else {
+        sm = a.blinds[b];
+        gidx = (uint32_t)a.h_index;
+      }
+      const Fq k = fq_from_mont(sm);
+      int carry = 0;
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        const int bit = w * C;
+        const int li = bit >> 5, of = bit & 31;
+        uint32_t v = k.l[li] >> of;
+        if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+        int d = (int)(v & MASK) + carry;
+        carry = d > NB ? 1 : 0;
+        d -= carry << C;
+        if (d != 0) {
+          const uint32_t mag = (uint32_t)(d < 0 ? -d : d);
+          const uint32_t slot = atomicAdd(&cnt[mag - 1], 1u);
+          if (pass)
+            a.entries[rowbase + slot] = ((uint32_t)bit * (uint32_t)a.n1 + gidx) | (d < 0 ? 0x80000000u : 0u);
+        }
+      }
+    }
+    __syncthreads();
+    if (pass) break;
+    // counts -> global hist; exclusive scan -> off (global) and the LDS cursors
+    uint32_t loc[PT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+      const int k = tid * PT + j;
+      loc[j] = k < NB ? cnt[k] : 0u;
+      sum += loc[j];
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int st = 1; st < 256; st <<= 1) {  // Hillis-Steele inclusive scan of the 256 partial sums
+      const uint32_t x = tid >= st ? part[tid - st] : 0u;
+      __syncthreads();
+      part[tid] += x;
+      __syncthreads();
+    }
+    uint32_t run = part[tid] - sum;
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+      const int k = tid * PT + j;
+      if (k < NB) {
+        a.hist[(size_t)b * NB + k] = loc[j];
+        a.off_out[(size_t)b * NB + k] = rowbase + run;
+        cnt[k] = run;
+      }
+      run += loc[j];
+    }
+    __syncthreads();
+  }
 }
 
 __global__ void k_item_counts(const uint32_t* __restrict__ hist, uint32_t* __restrict__ items, int nkeys) {
@@ -800,6 +881,22 @@ static void dispatch_digits(int c, const MsmArgs& a, bool count, hipStream_t s) 
   }
 }
 
+static void dispatch_digits_rows(int c, const MsmArgs& a, hipStream_t s) {
+  const dim3 g((unsigned)a.B), t(256);
+  switch (c) {
+    case 4: hipLaunchKernelGGL(k_digits_rows<4>, g, t, 0, s, a); break;
+    case 5: hipLaunchKernelGGL(k_digits_rows<5>, g, t, 0, s, a); break;
+    case 6: hipLaunchKernelGGL(k_digits_rows<6>, g, t, 0, s, a); break;
+    case 7: hipLaunchKernelGGL(k_digits_rows<7>, g, t, 0, s, a); break;
+    case 8: hipLaunchKernelGGL(k_digits_rows<8>, g, t, 0, s, a); break;
+    case 9: hipLaunchKernelGGL(k_digits_rows<9>, g, t, 0, s, a); break;
+    case 10: hipLaunchKernelGGL(k_digits_rows<10>, g, t, 0, s, a); break;
+    case 11: hipLaunchKernelGGL(k_digits_rows<11>, g, t, 0, s, a); break;
+    case 12: hipLaunchKernelGGL(k_digits_rows<12>, g, t, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_digits_rows<13>, g, t, 0, s, a); break;
+  }
+}
+
 // B MSMs of n scalars each (device pointers), out_dev: B x 32 bytes (device)
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext) {
@@ -831,8 +928,14 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   if (!hist || !off || !cursor || !items || !item_off || !entries || !item_key || !partial || !segT || !segS)
     return set_err(ctx, SPG_E_NOMEM, "msm workspace allocation failed");
 
-  SPG_HIP(ctx, hipMemsetAsync(hist, 0, (nkeys + 1) * 4, s));
-  SPG_HIP(ctx, hipMemsetAsync(cursor, 0, (nkeys + 1) * 4, s));
+  // many MSMs of moderate length: one workgroup per MSM sorts its digits in LDS (k_digits_rows)
+  const bool rows = B >= 64 && c <= 13;
+  if (rows) {
+    SPG_HIP(ctx, hipMemsetAsync(hist + nkeys, 0, 4, s));
+  } else {
+    SPG_HIP(ctx, hipMemsetAsync(hist, 0, (nkeys + 1) * 4, s));
+    SPG_HIP(ctx, hipMemsetAsync(cursor, 0, (nkeys + 1) * 4, s));
+  }
 
   MsmArgs a;
   a.scalars = d_scalars;
@@ -845,26 +948,30 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   a.idx = d_idx;
   a.hist = hist;
   a.off = off;
+  a.off_out = off;
   a.cursor = cursor;
   a.entries = entries;
 
-  {
+  size_t tmp_bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, hist, off, (int)(nkeys + 1), s);
+  void* tmp = ws_get(ctx, 11, tmp_bytes + 16);
+  if (!tmp) return set_err(ctx, SPG_E_NOMEM, "scan workspace");
+  if (rows) {
+    KScope ks(ctx, "msm_digits_rows");
+    dispatch_digits_rows(c, a, s);
+  } else {
     KScope ks(ctx, "msm_count");
     dispatch_digits(c, a, true, s);
   }
   SPG_HIP(ctx, hipGetLastError());
 
   // scans over nkeys+1 entries (hist[nkeys] == 0 so off[nkeys] = total entries)
-  size_t tmp_bytes = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, hist, off, (int)(nkeys + 1), s);
-  void* tmp = ws_get(ctx, 11, tmp_bytes + 16);
-  if (!tmp) return set_err(ctx, SPG_E_NOMEM, "scan workspace");
-  SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hist, off, (int)(nkeys + 1), s));
+  if (!rows) SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hist, off, (int)(nkeys + 1), s));
   hipLaunchKernelGGL(k_item_counts, dim3((unsigned)((nkeys + 1 + 255) / 256)), dim3(256), 0, s, hist, items,
                      (int)nkeys);
   SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, items, item_off, (int)(nkeys + 1), s));
 
-  {
+  if (!rows) {
     KScope ks(ctx, "msm_scatter");
     dispatch_digits(c, a, false, s);
   }

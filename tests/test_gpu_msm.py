@@ -94,12 +94,15 @@ def test_msm_blind_and_offset(ctx, oracle, gens64):
     assert gens64.msm(s, gen_offset=10) == oracle.msm(pts[10:60], s)
 
 
-@pytest.mark.parametrize("L,R", [(1, 1), (4, 2), (8, 32), (64, 128), (16, 1024)])
+# (128, 512) and (64, 1024): >= 64 rows wider than the latency path take the LDS row sort (k_digits_rows)
+@pytest.mark.parametrize("L,R", [(1, 1), (4, 2), (8, 32), (64, 128), (16, 1024), (128, 512), (64, 1024)])
 def test_commit_rows(ctx, oracle, gens64, L, R):
     rng = np.random.default_rng(L * 1000 + R)
     pts = gens64.compressed()
     Z = rand_fq(oracle, rng, L * R)
     Z[: min(L * R, 5)] = 0
+    if L >= 64:
+        Z[3 * R: 4 * R] = 0  # an all-zero row: empty histogram
     assert np.array_equal(gens64.commit_rows(Z, L, R), oracle.commit_rows(pts[:R], pts[1024].tobytes(), Z, L, R))
     bl = rand_fq(oracle, rng, L)
     assert np.array_equal(gens64.commit_rows(Z, L, R, bl),
