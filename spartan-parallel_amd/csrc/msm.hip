@@ -985,7 +985,8 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   }
   {
     KScope ks(ctx, "msm_segments");
-    if (use_quad() && B * (size_t)S <= 16384)
+    static const size_t seg_quad_max = getenv("SPG_SEG_QUAD_MAX") ? atol(getenv("SPG_SEG_QUAD_MAX")) : 16384;
+    if (use_quad() && B * (size_t)S <= seg_quad_max)
       hipLaunchKernelGGL(k_segments_q, dim3((unsigned)((4 * B * S + 255) / 256)), dim3(256), 0, s, item_off, partial,
                          segT, segS, (int)B, NB, m);
     else
@@ -1015,7 +1016,16 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
         fSn = G;
         flog2m = log2m + lg;
       }
-      hipLaunchKernelGGL(k_final_q<128>, dim3((unsigned)B), dim3(512), 0, s, fT, fS, nullptr, fSn, flog2m, ext);
+      // many MSMs fill the chip with blocks: fewer slots per MSM do less redundant scan work (the Hillis-Steele
+      // scan costs SL log SL additions), few MSMs need the shortest dependent chain
+      static const int sl_env = getenv("SPG_FINAL_SL") ? atoi(getenv("SPG_FINAL_SL")) : 0;
+      const int sl = sl_env ? sl_env : (B >= 256 ? 32 : 128);  // B = 1024 rows: 414 -> 155 us (MI355X)
+      if (sl == 32)
+        hipLaunchKernelGGL(k_final_q<32>, dim3((unsigned)B), dim3(128), 0, s, fT, fS, nullptr, fSn, flog2m, ext);
+      else if (sl == 64)
+        hipLaunchKernelGGL(k_final_q<64>, dim3((unsigned)B), dim3(256), 0, s, fT, fS, nullptr, fSn, flog2m, ext);
+      else
+        hipLaunchKernelGGL(k_final_q<128>, dim3((unsigned)B), dim3(512), 0, s, fT, fS, nullptr, fSn, flog2m, ext);
       if (d_out)
         hipLaunchKernelGGL(k_compress_ext, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, ext, B, d_out);
     }
