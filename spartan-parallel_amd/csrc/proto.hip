@@ -196,17 +196,23 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out) {
 }
 
 // B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
+// h_idx (optional, host, B x n): generator indices uploaded with the scalars in the same copy, d_idx unused
 static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& hs, size_t n, size_t B,
-                           const uint32_t* d_idx, std::vector<Pt>* out) {
+                           const uint32_t* d_idx, std::vector<Pt>* out, const std::vector<uint32_t>* h_idx = nullptr) {
   hipStream_t s = ctx->stream;
   g_msm_laps.lap("bullet_host");
-  const size_t in_bytes = hs.size() * sizeof(Fq), bk_bytes = sizeof(Ext) * B * 256;
+  const size_t sc_bytes = hs.size() * sizeof(Fq), ix_bytes = h_idx ? h_idx->size() * 4 : 0;
+  const size_t in_bytes = sc_bytes + ix_bytes, bk_bytes = sizeof(Ext) * B * 256;
   Fq* d_s = (Fq*)ws_get(ctx, 20, in_bytes + 64);
   Ext* d_bk = (Ext*)ws_get(ctx, 23, bk_bytes + 64);
   uint8_t* stage = (uint8_t*)pinned_get(ctx, in_bytes + bk_bytes + 256);
   if (!d_s || !d_bk || !stage) return set_err(ctx, SPG_E_NOMEM, "device_msm");
-  // scalars up through page-locked staging (a pageable source costs a staging copy + blit per call)
-  memcpy(stage, hs.data(), in_bytes);
+  // scalars (and indices) up through page-locked staging (a pageable source costs a staging copy + blit per call)
+  memcpy(stage, hs.data(), sc_bytes);
+  if (h_idx) {
+    memcpy(stage + sc_bytes, h_idx->data(), ix_bytes);
+    d_idx = (const uint32_t*)((const uint8_t*)d_s + sc_bytes);
+  }
   SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, in_bytes, hipMemcpyHostToDevice, s));
   // bucket sums on the device; sum_v v * B_v and the encoding on host cores (a short dependent chain of
   // additions is ~50x faster there than on one GPU lane)
@@ -295,6 +301,14 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   Fq r = t.challenge("r");
   Fq blind_fin = fq_add(blind_x, fq_mul(r, blind_y));
   FqV aa(x), bb(a), cw(n, fq_one());
+  // per-round L / R MSM inputs: hn = n/2 + 2 scalars and generator indices each (G_1 and h last)
+  const size_t hn = n / 2 + 2;
+  std::vector<Fq> hc(2 * hn);
+  std::vector<uint32_t> ic(2 * hn);
+  for (size_t b = 0; b < 2; b++) {
+    ic[b * hn + n / 2] = G1;
+    ic[b * hn + n / 2 + 1] = H;
+  }
   size_t nk = n, k = 0;
   g_msm_laps.lap("bullet_prep");
   while (nk != 1) {
@@ -302,25 +316,24 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     Fq cL = dot(aa, bb, 0, nh, nh), cR = dot(aa, bb, nh, 0, nh);
     g_msm_laps.lap("bullet_dot");
     Fq blind_L = v1[k], blind_R = v2[k];
-    // L scalars in hs[0 .. n2), R scalars in hs[n2 .. 2 n2)
-    par_range(n, [&](size_t lo, size_t hi) {
-      for (size_t j = lo; j < hi; j++) {
-        size_t m = j % nk;
-        if (m >= nh) {
-          hs[j] = fq_mul(aa[m - nh], cw[j]);
-          hs[n2 + j] = fq_zero();
-        } else {
-          hs[j] = fq_zero();
-          hs[n2 + j] = fq_mul(aa[m + nh], cw[j]);
-        }
+    // L = sum over the n/2 generators j with (j mod nk) >= nh of a[j mod nk - nh] cw_j G_j (+ cL r G_1 +
+    // blind_L h), R over the other half; each MSM carries only its own half (hc = n/2 + 2 scalars, explicit
+    // generator indices uploaded with them), so the bucket kernel extracts digits of half as many scalars
+    par_range(n / 2, [&](size_t lo, size_t hi) {
+      for (size_t p = lo; p < hi; p++) {
+        const size_t blk = p / nh, off = p % nh, jl = blk * nk + nh + off, jr = blk * nk + off;
+        hc[p] = fq_mul(aa[off], cw[jl]);
+        ic[p] = (uint32_t)kn.G[jl];
+        hc[hn + p] = fq_mul(aa[off + nh], cw[jr]);
+        ic[hn + p] = (uint32_t)kn.G[jr];
       }
     });
-    hs[n] = fq_mul(cL, r);
-    hs[n + 1] = blind_L;
-    hs[n2 + n] = fq_mul(cR, r);
-    hs[n2 + n + 1] = blind_R;
+    hc[n / 2] = fq_mul(cL, r);
+    hc[n / 2 + 1] = blind_L;
+    hc[hn + n / 2] = fq_mul(cR, r);
+    hc[hn + n / 2 + 1] = blind_R;
     g_msm_laps.lap("bullet_scalars");
-    int rc = device_msm_flat(ctx, g, hs, n2, 2, d_idx, &pts);
+    int rc = device_msm_flat(ctx, g, hc, hn, 2, nullptr, &pts, &ic);
     if (rc) return rc;
     t.point("L", pts[0]);
     t.point("R", pts[1]);
