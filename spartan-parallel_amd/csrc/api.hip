@@ -31,6 +31,30 @@ void* pinned_get(spg_ctx* c, size_t bytes) {
   return c->pinned;
 }
 
+void* mapped_get(spg_ctx* c, size_t bytes, void** dev) {
+  static const bool on = !getenv("SPG_MAPPED_BUCKETS") || atoi(getenv("SPG_MAPPED_BUCKETS")) != 0;
+  if (!on) return nullptr;
+  if (bytes > c->mapped_bytes) {
+    if (c->mapped) {
+      hipStreamSynchronize(c->stream);
+      hipHostFree(c->mapped);
+      c->mapped = c->d_mapped = nullptr;
+      c->mapped_bytes = 0;
+    }
+    size_t sz = std::max<size_t>((bytes + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1), 1 << 20);
+    void* h = nullptr;
+    if (hipHostMalloc(&h, sz, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+    if (hipHostGetDevicePointer(&c->d_mapped, h, 0) != hipSuccess) {
+      hipHostFree(h);
+      return nullptr;
+    }
+    c->mapped = h;
+    c->mapped_bytes = sz;
+  }
+  *dev = c->d_mapped;
+  return c->mapped;
+}
+
 void* ws_get(spg_ctx* c, size_t slot, size_t bytes) {
   if (c->ws.size() <= slot) c->ws.resize(slot + 1);
   spg_ctx::Slot& s = c->ws[slot];
@@ -138,6 +162,7 @@ extern "C" int spg_free(spg_ctx* c) {
   for (auto& s : c->ws)
     if (s.p) hipFree(s.p);
   if (c->pinned) hipHostFree(c->pinned);
+  if (c->mapped) hipHostFree(c->mapped);
   if (c->mbox) hipHostFree((void*)c->mbox);
   if (c->d_counter) hipFree(c->d_counter);
   hipEventDestroy(c->ev0);

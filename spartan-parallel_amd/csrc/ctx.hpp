@@ -15,6 +15,11 @@ struct spg_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* pinned = nullptr;          // page-locked host staging (pinned_get), grown on demand
   size_t pinned_bytes = 0;
+  // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into
+  // directly (mapped_get): the host reads them after the stream synchronisation, no D2H copy launch
+  void* mapped = nullptr;
+  void* d_mapped = nullptr;
+  size_t mapped_bytes = 0;
   unsigned* d_counter = nullptr;   // grid-reduction ticket (zero between launches)
   // mailbox in fine-grained (coherent, mapped) host memory: a kernel's last block posts a round's scalars
   // and a sequence number with system-scope stores; the host spins on the number instead of a D2H copy +
@@ -86,6 +91,11 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
 // page-locked host staging of at least `bytes` (contents undefined; valid until the next larger request,
 // which synchronises the stream before freeing the old buffer)
 void* pinned_get(spg_ctx* c, size_t bytes);
+
+// coherent mapped host memory of at least `bytes`: host pointer returned, device alias in *dev (contents
+// undefined; a larger request synchronises the stream before freeing the old buffer). Null when
+// SPG_MAPPED_BUCKETS=0 or on failure: callers then take the device buffer + copy path.
+void* mapped_get(spg_ctx* c, size_t bytes, void** dev);
 
 // timing bracket on the context stream
 void timer_start(spg_ctx* c);

@@ -217,10 +217,12 @@ static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& h
   // bucket sums on the device; sum_v v * B_v and the encoding on host cores (a short dependent chain of
   // additions is ~50x faster there than on one GPU lane)
   int NB = 0;
-  int rc = msm_small_buckets(ctx, g.dev, 0, d_s, n, B, nullptr, d_idx, -1, d_bk, &NB);
+  void* d_map = nullptr;
+  Ext* mbk = (Ext*)mapped_get(ctx, bk_bytes, &d_map);  // buckets straight into host memory
+  int rc = msm_small_buckets(ctx, g.dev, 0, d_s, n, B, nullptr, d_idx, -1, mbk ? (Ext*)d_map : d_bk, &NB);
   if (rc) return rc;
-  Ext* bk = (Ext*)(stage + ((in_bytes + 255) & ~(size_t)255));
-  SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * B * NB, hipMemcpyDeviceToHost, s));
+  Ext* bk = mbk ? mbk : (Ext*)(stage + ((in_bytes + 255) & ~(size_t)255));
+  if (!mbk) SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * B * NB, hipMemcpyDeviceToHost, s));
   SPG_HIP(ctx, hipStreamSynchronize(s));
   g_msm_laps.lap("msm_device");
   out->resize(B);

@@ -348,13 +348,16 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
     if (small && nb <= kHostFinalRows) {
       // few rows: the bucket running sums and encodings are cheaper on host cores than the device's
       // one-lane-per-row final + compress (~0.25 ms floor)
-      Ext* d_bk = (Ext*)ws_get(ctx, kWsCommitBk, sizeof(Ext) * nb * 256 + 64);
-      Ext* bk = (Ext*)pinned_get(ctx, sizeof(Ext) * nb * 256);
+      void* d_map = nullptr;
+      Ext* mbk = (Ext*)mapped_get(ctx, sizeof(Ext) * nb * 256, &d_map);  // buckets straight into host memory
+      Ext* d_bk = mbk ? (Ext*)d_map : (Ext*)ws_get(ctx, kWsCommitBk, sizeof(Ext) * nb * 256 + 64);
+      Ext* bk = mbk ? mbk : (Ext*)pinned_get(ctx, sizeof(Ext) * nb * 256);
       if (!d_bk || !bk) return set_err(ctx, SPG_E_NOMEM, "commit buckets");
       int NB = 0;
       int rc = msm_small_buckets(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, nullptr, -1, d_bk, &NB);
       if (rc) return rc;
-      SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * nb * NB, hipMemcpyDeviceToHost, ctx->stream));
+      if (!mbk)
+        SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * nb * NB, hipMemcpyDeviceToHost, ctx->stream));
       SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
       bucket_finals(bk, nb, NB, out + r0);
     } else {
