@@ -307,6 +307,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   const size_t hn = n / 2 + 2;
   std::vector<Fq> hc(2 * hn);
   std::vector<uint32_t> ic(2 * hn);
+  FqV fa(n / 2), fb(n / 2);  // fold products that need u only
   for (size_t b = 0; b < 2; b++) {
     ic[b * hn + n / 2] = G1;
     ic[b * hn + n / 2 + 1] = H;
@@ -340,16 +341,41 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     t.point("L", pts[0]);
     t.point("R", pts[1]);
     Fq u = t.challenge("u");
-    Fq uinv = fq_inv(u);
-    par_range(nh, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; i++) {
+    Fq uinv;
+    static const bool overlap = !getenv("SPG_BULLET_OVERLAP") || atoi(getenv("SPG_BULLET_OVERLAP")) != 0;
+    if (n < 256 || !overlap) {
+      uinv = fq_inv(u);
+      for (size_t i = 0; i < nh; i++) {
         aa[i] = fq_add(fq_mul(aa[i], u), fq_mul(uinv, aa[i + nh]));
         bb[i] = fq_add(fq_mul(bb[i], uinv), fq_mul(u, bb[i + nh]));
       }
-    });
-    par_range(n, [&](size_t lo, size_t hi) {
-      for (size_t j = lo; j < hi; j++) cw[j] = fq_mul(cw[j], (j % nk) < nh ? uinv : u);
-    });
+      for (size_t j = 0; j < n; j++) cw[j] = fq_mul(cw[j], (j % nk) < nh ? uinv : u);
+    } else {
+      // two bursts: the inversion of u (a ~5 us binary GCD) runs as task 0 of the first, beside the
+      // products that need u only; the second finishes every fold with u^-1 (same field values)
+      const int C = 8;
+      pool().parallel_for(C + 1, [&](int task) {
+        if (task == 0) {
+          uinv = fq_inv(u);
+          return;
+        }
+        const int c = task - 1;
+        for (size_t i = nh * c / C; i < nh * (c + 1) / C; i++) {
+          fa[i] = fq_mul(aa[i], u);
+          fb[i] = fq_mul(u, bb[i + nh]);
+        }
+        for (size_t j = n * c / C; j < n * (c + 1) / C; j++)
+          if ((j % nk) >= nh) cw[j] = fq_mul(cw[j], u);
+      });
+      pool().parallel_for(C, [&](int c) {
+        for (size_t i = nh * c / C; i < nh * (c + 1) / C; i++) {
+          aa[i] = fq_add(fa[i], fq_mul(uinv, aa[i + nh]));
+          bb[i] = fq_add(fq_mul(bb[i], uinv), fb[i]);
+        }
+        for (size_t j = n * c / C; j < n * (c + 1) / C; j++)
+          if ((j % nk) < nh) cw[j] = fq_mul(cw[j], uinv);
+      });
+    }
     blind_fin = fq_add(fq_add(blind_fin, fq_mul(fq_mul(blind_L, u), u)), fq_mul(fq_mul(blind_R, uinv), uinv));
     g_msm_laps.lap("bullet_fold");
     out->L.push_back(pts[0]);
