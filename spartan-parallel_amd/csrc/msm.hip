@@ -714,8 +714,10 @@ static int pick_small_window(size_t per) {
     int c = atoi(e);
     if (c >= 4 && c <= 9) return c;
   }
-  // measured on MI355X (scripts/perf_small_msm.py): n = 130 -> c = 7, n = 1028 and 4098 -> c = 8
-  return per <= 512 ? 7 : 8;
+  // measured on MI355X (scripts/perf_small_msm.py): n = 130 -> c = 7, n = 4098 -> c = 8; the compacted
+  // Bullet MSMs (n/2 + 2 = 514 scalars) finish on the host, where 64 buckets per MSM are cheaper than 128
+  // (scripts/ab_env.sh SPG_SMSM_C "7 0": 39.7 vs 39.9-40.9 ms per SNARK::prove)
+  return per <= 1024 ? 7 : 8;
 }
 
 template <int C>
