@@ -160,12 +160,14 @@ __global__ void __launch_bounds__(1024) k_layer_tiny(const Triple* __restrict__ 
     const Triple x = tr[u >> log_len];
     const Fq k = coeff[u >> log_len];
     const int i = u & (len - 1);
-    Fq al = x.A[i], ah = x.A[i + len], bl = x.B[i], bh = x.B[i + len], cl = x.C[i], ch = x.C[i + len];
+    // the coefficient scales the A factor (k A is linear in X), 8 multiplications per element instead of 9
+    const Fq al = fq_mul(k, x.A[i]), ah = fq_mul(k, x.A[i + len]);
+    const Fq bl = x.B[i], bh = x.B[i + len], cl = x.C[i], ch = x.C[i + len];
     Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
     Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
-    e0 = fq_add(e0, fq_mul(k, fq_mul(fq_mul(al, bl), cl)));
-    e2 = fq_add(e2, fq_mul(k, fq_mul(fq_mul(a2, b2), c2)));
-    e3 = fq_add(e3, fq_mul(k, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc))));
+    e0 = fq_add(e0, fq_mul(fq_mul(al, bl), cl));
+    e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
+    e3 = fq_add(e3, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
   }
   block_sum3_t0<1024>(e0, e2, e3);
   if (t == 0) {
