@@ -83,6 +83,36 @@ __device__ __forceinline__ void mul_8x8(const uint32_t* a, const uint32_t* b, ui
   }
   t[15] = (uint32_t)acc;
 }
+// t[0..16) = a^2: the 28 off-diagonal products once (product scanning), doubled, plus the 8 squares
+__device__ __forceinline__ void sqr_8(const uint32_t* a, uint32_t* t) {
+  uint64_t acc = 0;
+  uint32_t ov = 0;
+  t[0] = 0;
+#pragma unroll
+  for (int k = 1; k < 14; k++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j <= i || j > 7) continue;
+      mac_ov(acc, ov, a[i], a[j]);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)ov << 32);
+    ov = 0;
+  }
+  t[14] = (uint32_t)acc;
+  t[15] = (uint32_t)(acc >> 32);
+#pragma unroll
+  for (int i = 15; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
+  t[0] <<= 1;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t v = (uint64_t)a[i] * a[i];
+    t[2 * i] = addc(t[2 * i], (uint32_t)v, c, c);
+    t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(v >> 32), c, c);
+  }
+}
 #endif
 
 // ================================================================= Fq (Montgomery, R = 2^256)
@@ -489,7 +519,9 @@ SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
 }
 SPG_HD Fp fp_sqr(const Fp& a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return fp_mul(a, a);
+  uint32_t t[16];
+  sqr_8(a.l, t);
+  return fp_reduce512(t);
 #else
   // off-diagonal products once, doubled, plus the diagonal
   uint32_t t[16];
