@@ -42,8 +42,10 @@ const char* spg_last_error(const spg_ctx* ctx);
 double spg_last_kernel_us(const spg_ctx* ctx);
 
 /* Multi-process proving: one process (and context) per GPU. R1CSProof::prove is then sharded by instance
- * p: rank r holds instances [r*ceil(P/n), (r+1)*ceil(P/n)) and every rank runs the same Fiat-Shamir
- * transcript. fn(user, send, bytes, recv) must place the `bytes` sent by rank k at recv + k*bytes on every
+ * p: rank r holds instances [b(r), b(r+1)) with b(r) = r*floor(P/n) + min(r, P mod n) (the first P mod n
+ * ranks hold one more; spg.shard_range) and every rank runs the same Fiat-Shamir transcript. A sharded
+ * spg_r1cs_prove first allgathers every rank's argument check, so a bad argument on one rank fails all of
+ * them (SPG_E_ARG) rather than leaving the others blocked. fn(user, send, bytes, recv) must place the `bytes` sent by rank k at recv + k*bytes on every
  * rank (an allgather, e.g. RCCL / torch.distributed); it returns 0 on success. nranks == 1 clears it. */
 typedef int (*spg_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
 int spg_set_comm(spg_ctx* ctx, int rank, int nranks, spg_allgather_fn fn, void* user);

@@ -65,8 +65,11 @@ __device__ __forceinline__ void mac_ov(uint64_t& acc, uint32_t& ov, uint32_t a, 
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cy) : "v"(a), "v"(b));
   asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(ov), "=s"(cy) : "s"(cy));
 }
+#endif
+// The device's product-scanning forms, compiled for the host too (through the host mac_ov above), so
+// tests/test_product_host.py checks them against the oracle without a GPU (fp ops 6 and 7 of hostcheck).
 // t[0..16) = a * b (8 x 32-bit limbs each), product scanning
-__device__ __forceinline__ void mul_8x8(const uint32_t* a, const uint32_t* b, uint32_t* t) {
+SPG_HD void mul_8x8(const uint32_t* a, const uint32_t* b, uint32_t* t) {
   uint64_t acc = 0;
   uint32_t ov = 0;
 #pragma unroll
@@ -84,7 +87,7 @@ __device__ __forceinline__ void mul_8x8(const uint32_t* a, const uint32_t* b, ui
   t[15] = (uint32_t)acc;
 }
 // t[0..16) = a^2: the 28 off-diagonal products once (product scanning), doubled, plus the 8 squares
-__device__ __forceinline__ void sqr_8(const uint32_t* a, uint32_t* t) {
+SPG_HD void sqr_8(const uint32_t* a, uint32_t* t) {
   uint64_t acc = 0;
   uint32_t ov = 0;
   t[0] = 0;
@@ -113,7 +116,6 @@ __device__ __forceinline__ void sqr_8(const uint32_t* a, uint32_t* t) {
     t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(v >> 32), c, c);
   }
 }
-#endif
 
 // ================================================================= Fq (Montgomery, R = 2^256)
 struct Fq {
@@ -494,11 +496,20 @@ SPG_HD Fp fp_reduce512(uint32_t t[16]) {
   fp_fold38(r.l, c);
   return r;
 }
-SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+// the device forms (product scanning), callable on the host for testing
+SPG_HD Fp fp_mul_ps(const Fp& a, const Fp& b) {
   uint32_t t[16];
   mul_8x8(a.l, b.l, t);
   return fp_reduce512(t);
+}
+SPG_HD Fp fp_sqr_ps(const Fp& a) {
+  uint32_t t[16];
+  sqr_8(a.l, t);
+  return fp_reduce512(t);
+}
+SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fp_mul_ps(a, b);
 #else
   uint32_t t[16];
 #pragma unroll
@@ -519,9 +530,7 @@ SPG_HD Fp fp_mul(const Fp& a, const Fp& b) {
 }
 SPG_HD Fp fp_sqr(const Fp& a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t t[16];
-  sqr_8(a.l, t);
-  return fp_reduce512(t);
+  return fp_sqr_ps(a);
 #else
   // off-diagonal products once, doubled, plus the diagonal
   uint32_t t[16];

@@ -5,7 +5,12 @@
 
 #include <vector>
 
+#include <atomic>
+#include <memory>
+#include <random>
+
 #include "curve.hpp"
+#include "hpool.hpp"
 #include "hcurve.hpp"
 #include "keccak.hpp"
 
@@ -36,7 +41,8 @@ void spgh_fq_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, siz
   }
 }
 
-// op: 0 add, 1 sub, 2 mul, 3 sqr, 4 inv, 5 canon ; inputs/outputs as 8 x u32 (loose allowed)
+// op: 0 add, 1 sub, 2 mul, 3 sqr, 4 inv, 5 canon, 6 mul (device product scanning), 7 sqr (device);
+// inputs/outputs as 8 x u32 (loose allowed)
 void spgh_fp_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
   for (size_t i = 0; i < n; i++) {
     Fp x, y, r;
@@ -48,6 +54,8 @@ void spgh_fp_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, siz
       case 2: r = fp_mul(x, y); break;
       case 3: r = fp_sqr(x); break;
       case 4: r = fp_inv(x); break;
+      case 6: r = fp_mul_ps(x, y); break;
+      case 7: r = fp_sqr_ps(x); break;
       default: r = x; break;
     }
     r = fp_canon(r);
@@ -162,6 +170,35 @@ int spgh_allgather_sum(int (*fn)(void*, const void*, size_t, void*), void* user,
     memcpy(out + 4 * k, acc.l, 32);
   }
   return 0;
+}
+
+// The host pool (hpool.hpp) under stress: `bursts` parallel_for calls of random size 1..max_n on a fresh
+// pool of `workers` threads whose workers sleep `delay_us` between their generation and function loads
+// and whose caller sleeps `delay_us` between publishing a burst's function/count and opening it (the two
+// sides of the stale-snapshot race window). Every task bumps its own counter; right after each call
+// returns, every counter must be exactly 1 and no task may still be running. Returns the number of
+// violations (0 = pass).
+long spgh_pool_stress(int workers, int bursts, int max_n, int delay_us, unsigned seed) {
+  spg::Pool pool(workers, delay_us, delay_us);
+  std::mt19937 rng(seed);
+  std::atomic<long> bad{0};
+  std::atomic<int> running{0};
+  for (int b = 0; b < bursts; b++) {
+    const int n = 1 + (int)(rng() % (unsigned)max_n);
+    std::unique_ptr<std::atomic<int>[]> cnt(new std::atomic<int>[n]);
+    for (int i = 0; i < n; i++) cnt[i].store(0);
+    const int tag = b;
+    pool.parallel_for(n, [&, tag](int i) {
+      running.fetch_add(1);
+      if (i < 0 || i >= n || tag != b) bad.fetch_add(1);
+      else cnt[i].fetch_add(1);
+      if ((i & 7) == 0) std::this_thread::yield();
+      running.fetch_sub(1);
+    });
+    if (running.load() != 0) bad.fetch_add(1);
+    for (int i = 0; i < n; i++) bad.fetch_add(cnt[i].load() != 1);
+  }
+  return bad.load();
 }
 
 }  // extern "C"

@@ -5,9 +5,16 @@
 // spins on the burst generation for a while (SPG_POOL_SPIN_US, default 20 ms) before it parks on the
 // condition variable: a futex wake-up costs 10-30 us per burst, a spinning worker picks the burst up at once.
 //
-// Task indices are claimed with a CAS on one 64-bit word holding (burst generation, next index), and
-// every worker works from a snapshot (generation, function, count) taken under the mutex, so a worker
-// that wakes late can never run a task of a newer burst with an older function or vice versa.
+// Task indices are claimed with a CAS on one 64-bit word next_ = (burst generation, next index). A worker
+// snapshots (generation, function, count) without a lock, so the caller publishes a burst in this order
+// (all seq_cst): next_ = (g, CLOSED) -> fn_, n_, remaining_ -> next_ = (g, 0) -> gen_pub_ = g. Then
+//  * a worker whose snapshot mixes generation G with the function/count of a newer burst G' read fn_ after
+//    next_ was tagged G' (closed), so every later load of next_ carries a tag >= G' and its claim fails;
+//  * a worker that read gen_pub_ = g reads fn_ / n_ of burst g or newer (never older);
+//  * a successful claim (CAS on a (g, i < n_g) value) means burst g is still open, so its function is alive
+//    and remaining_ still counts it: the caller returns only after every claimed task has finished.
+// tests/test_product_host.py::test_pool_bursts runs bursts of varying size with a worker delayed between its
+// snapshot loads (spgh_pool_stress) and checks that every task runs exactly once before parallel_for returns.
 #pragma once
 #include <atomic>
 #include <chrono>
@@ -22,7 +29,10 @@ namespace spg {
 
 class Pool {
  public:
-  explicit Pool(int nthreads) {
+  // test hooks: a worker sleeps snapshot_delay_us between its generation and function loads, the caller
+  // sleeps publish_delay_us between storing a burst's function/count and opening it
+  explicit Pool(int nthreads, int snapshot_delay_us = 0, int publish_delay_us = 0)
+      : delay_us_(snapshot_delay_us), pub_delay_us_(publish_delay_us) {
     const char* e = getenv("SPG_POOL_SPIN_US");
     spin_ = std::chrono::microseconds(e ? atoi(e) : 20000);
     for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
@@ -46,10 +56,12 @@ class Pool {
     uint32_t g;
     bool wake;
     g = ++gen_;
+    next_.store(((uint64_t)g << 32) | kClosed);  // tag first: stale snapshots can no longer claim
     fn_.store(&f);
     n_.store(n);
     remaining_.store(n);
-    next_.store((uint64_t)g << 32);
+    if (pub_delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(pub_delay_us_));
+    next_.store((uint64_t)g << 32);  // open
     gen_pub_.store(g);  // seq_cst: pairs with a parking worker's sleepers_ increment (no lost wake-up)
     wake = sleepers_.load() > 0;
     if (wake) {
@@ -64,7 +76,7 @@ class Pool {
   void work(uint32_t g, const std::function<void(int)>* f, int n) {
     for (;;) {
       uint64_t v = next_.load();
-      if ((uint32_t)(v >> 32) != g || (int)(uint32_t)v >= n) return;
+      if ((uint32_t)(v >> 32) != g || (uint32_t)v >= (uint32_t)n) return;  // kClosed >= any n
       if (!next_.compare_exchange_weak(v, v + 1)) continue;
       (*f)((int)(uint32_t)v);
       remaining_.fetch_sub(1);
@@ -91,14 +103,17 @@ class Pool {
         sleepers_--;
       }
       if (quit_pub_.load()) return;
-      // lock-free snapshot: f and n are at least as new as g; if a newer burst already replaced them, the
-      // generation check in work() finds next_ tagged with another generation and returns at once
+      // lock-free snapshot: f and n are at least as new as g; if a newer burst already replaced them, next_
+      // was tagged with that newer generation before fn_ changed, so work() returns at once (header comment)
       seen = g = gen_pub_.load();
+      if (delay_us_) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
       f = fn_.load();
       n = n_.load();
       work(g, f, n);
     }
   }
+  static constexpr uint32_t kClosed = 0xffffffffu;
+  int delay_us_ = 0, pub_delay_us_ = 0;
   std::vector<std::thread> threads_;
   std::mutex mu_, call_mu_;
   std::condition_variable cv_;

@@ -315,8 +315,17 @@ struct Prover {
     return 0;
   }
 
-  // instance shard of this rank (R1CSProof sharded by instance p over nranks processes)
+  // instance shard of this rank (R1CSProof sharded by instance p over nranks processes): balanced split,
+  // the first P % nranks ranks hold one instance more, so every rank holds one when nranks <= P
   size_t rank = 0, nranks = 1, p0 = 0, p1 = 0;
+  static size_t shard_begin(size_t P, size_t nranks, size_t r) {
+    return r * (P / nranks) + std::min(r, P % nranks);
+  }
+  size_t owner_of(size_t p) const {
+    size_t r = 0;
+    while (r + 1 < nranks && shard_begin(P, nranks, r + 1) <= p) r++;
+    return r;
+  }
   int allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv);
   int sum_ranks(Fq e[3]);
   int gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full);
@@ -360,7 +369,7 @@ int Prover::sum_ranks(Fq e[3]) {
 }
 // per local instance p, the element (p, 0, 0, 0) of each table -> the same for all P instances, on the host
 int Prover::gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full) {
-  const size_t k = tabs.size(), PL = (P + nranks - 1) / nranks;
+  const size_t k = tabs.size(), PL = (P + nranks - 1) / nranks;  // the largest shard; slots per rank
   std::vector<Fq> mine(PL * k, fq_zero());
   for (size_t i = 0; i < k; i++) {
     const PqxDev& T = *tabs[i];
@@ -376,7 +385,8 @@ int Prover::gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std
   full.assign(k, std::vector<Fq>(P, fq_zero()));
   for (size_t q = 0; q < nranks; q++)
     for (size_t i = 0; i < k; i++)
-      for (size_t p = 0; p < PL && q * PL + p < P; p++) full[i][q * PL + p] = v[q * PL * k + i * PL + p];
+      for (size_t b = shard_begin(P, nranks, q), p = 0; b + p < shard_begin(P, nranks, q + 1); p++)
+        full[i][b + p] = v[q * PL * k + i * PL + p];
   return 0;
 }
 // a table of n instances holding one element each (what remains of a Pqx table when only the instance
@@ -872,7 +882,7 @@ int Prover::run_inner(Laps& lp) {
     size_t o = 0;
     for (auto& pr : polys) {
       size_t owner = 0;
-      if (wit.num_proofs[pr.w].size() != 1) owner = pr.p / ((P + nranks - 1) / nranks);
+      if (wit.num_proofs[pr.w].size() != 1) owner = owner_of(pr.p);
       pr.LZ.assign(v + owner * lz_total + o, v + owner * lz_total + o + pr.Rs);
       o += pr.Rs;
     }
@@ -1283,13 +1293,10 @@ extern "C" int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* W) {
   return SPG_OK;
 }
 
-extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst,
-                              size_t num_instances, size_t max_num_proofs, const size_t* num_proofs,
-                              size_t max_num_inputs, const size_t* num_inputs, const spg_r1cs_witness* wit,
-                              spg_transcript* transcript, spg_random_tape* tape, uint8_t* proof, size_t proof_cap,
-                              size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
-  if (!ctx || !gens || !inst || !num_proofs || !num_inputs || !wit || !transcript || !tape || !proof_len)
-    return SPG_E_ARG;
+// argument check of spg_r1cs_prove; also derives this rank's instance shard [p0, p1)
+static int check_prove_args(spg_ctx* ctx, const spg_r1cs_inst* inst, size_t num_instances, size_t max_num_proofs,
+                            const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
+                            const spg_r1cs_witness* wit, size_t rank, size_t nranks, size_t* p0, size_t* p1) {
   if (!num_instances || !is_pow2(max_num_proofs) || !is_pow2(max_num_inputs))
     return set_err(ctx, SPG_E_ARG, "bad sizes");
   if (inst->num_instances != 1 && inst->num_instances != num_instances)
@@ -1311,16 +1318,41 @@ extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg
       if (wit->num_proofs[w][pw] > max_num_proofs) return set_err(ctx, SPG_E_ARG, "witness section too tall");
     }
   }
+  if (nranks > num_instances) return set_err(ctx, SPG_E_ARG, "more ranks than instances");
+  *p0 = Prover::shard_begin(num_instances, nranks, rank);
+  *p1 = Prover::shard_begin(num_instances, nranks, rank + 1);
+  for (size_t w = 0; w < wit->nws; w++) {
+    if (wit->num_proofs[w].size() == 1) continue;
+    for (size_t p = *p0; p < *p1; p++)
+      if (wit->off[w][p] == kNotResident) return set_err(ctx, SPG_E_ARG, "witness shard does not hold instance");
+  }
+  return SPG_OK;
+}
+
+extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst,
+                              size_t num_instances, size_t max_num_proofs, const size_t* num_proofs,
+                              size_t max_num_inputs, const size_t* num_inputs, const spg_r1cs_witness* wit,
+                              spg_transcript* transcript, spg_random_tape* tape, uint8_t* proof, size_t proof_cap,
+                              size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  if (!ctx || !gens || !inst || !num_proofs || !num_inputs || !wit || !transcript || !tape || !proof_len)
+    return SPG_E_ARG;
   Prover pr(ctx, const_cast<spg_r1cs_gens*>(gens)->g, *inst, *wit, transcript->t, tape->t);
   pr.rank = (size_t)ctx->rank;
   pr.nranks = (size_t)ctx->nranks;
-  if (pr.nranks > num_instances) return set_err(ctx, SPG_E_ARG, "more ranks than instances");
-  {
-    size_t PL = (num_instances + pr.nranks - 1) / pr.nranks;
-    pr.p0 = std::min(num_instances, pr.rank * PL);
-    pr.p1 = std::min(num_instances, pr.p0 + PL);
-    if (pr.p0 >= pr.p1) return set_err(ctx, SPG_E_ARG, "rank holds no instance (use fewer ranks)");
+  int rc_args = check_prove_args(ctx, inst, num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs,
+                                 wit, pr.rank, pr.nranks, &pr.p0, &pr.p1);
+  if (pr.nranks > 1) {
+    // a sharded prove starts with every rank agreeing on the argument check, so a rank-local failure
+    // (e.g. a witness shard that does not hold this rank's instances) fails every rank alike instead of
+    // leaving the others blocked in the first round's allgather
+    int32_t mine = rc_args;
+    std::vector<uint8_t> all;
+    int rc = pr.allgather(&mine, sizeof(mine), all);
+    if (rc) return rc;
+    for (size_t q = 0; q < pr.nranks && !rc_args; q++)
+      if (((const int32_t*)all.data())[q]) rc_args = set_err(ctx, SPG_E_ARG, "a peer rank rejected its arguments");
   }
+  if (rc_args) return rc_args;
   pr.P = num_instances;
   pr.max_np = max_num_proofs;
   pr.Y = max_num_inputs;

@@ -421,10 +421,11 @@ def r1cs_prove(ctx, gens, inst, witness, num_instances, max_num_proofs, num_proo
 
 
 def shard_range(num_instances, rank, nranks):
-    """instances [p0, p1) held by `rank` in a sharded R1CSProof (include/spg.h, spg_set_comm)"""
-    per = -(-num_instances // nranks)
-    p0 = min(num_instances, rank * per)
-    return p0, min(num_instances, p0 + per)
+    """instances [p0, p1) held by `rank` in a sharded R1CSProof (include/spg.h, spg_set_comm): balanced split,
+    the first num_instances % nranks ranks hold one instance more (same rule as r1cs.hip Prover::shard_begin)"""
+    def begin(r):
+        return r * (num_instances // nranks) + min(r, num_instances % nranks)
+    return begin(rank), begin(rank + 1)
 
 
 class SparkCommitment:

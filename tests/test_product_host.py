@@ -81,6 +81,40 @@ def test_fp_ops_against_bigint(hc):
         assert toint(out[i]) == pow(a, P - 2, P)
 
 
+def test_fp_device_forms_boundary(hc):
+    """the device's product-scanning Fp multiply and squaring (field.hpp mul_8x8 / sqr_8) on the host, on
+    random and boundary inputs (all-ones limbs, p, 2^256 - 1, 0) against Python big-int"""
+    rng = np.random.default_rng(19)
+    n = 3000
+    A = rng.integers(0, 2**32, size=(n, 8), dtype=np.uint64).astype(np.uint32)
+    B = rng.integers(0, 2**32, size=(n, 8), dtype=np.uint64).astype(np.uint32)
+    edge = [np.full(8, 0xFFFFFFFF, np.uint32), np.zeros(8, np.uint32),
+            np.array([0xFFFFFFED] + [0xFFFFFFFF] * 6 + [0x7FFFFFFF], dtype=np.uint32),
+            np.array([0xFFFFFFEC] + [0xFFFFFFFF] * 6 + [0x7FFFFFFF], dtype=np.uint32),
+            np.array([1, 0, 0, 0, 0, 0, 0, 0], dtype=np.uint32),
+            np.array([0xFFFFFFFF] * 4 + [0] * 4, dtype=np.uint32), np.array([0] * 4 + [0xFFFFFFFF] * 4, np.uint32)]
+    for i, e in enumerate(edge):
+        for j, f in enumerate(edge):
+            A[i * len(edge) + j] = e
+            B[i * len(edge) + j] = f
+    toint = lambda r: sum(int(x) << (32 * i) for i, x in enumerate(r))
+    for code, f in [(6, lambda a, b: a * b % P), (7, lambda a, b: a * a % P)]:
+        out = np.zeros_like(A)
+        hc.spgh_fp_op(code, _p(A), _p(B), _p(out), ctypes.c_size_t(n))
+        for i in range(n):
+            assert toint(out[i]) == f(toint(A[i]), toint(B[i])), (code, i)
+
+
+@pytest.mark.parametrize("workers,delay_us", [(7, 0), (7, 50), (3, 200)])
+def test_pool_bursts(hc, workers, delay_us):
+    """hpool.hpp: bursts of growing / varying size with workers delayed inside their lock-free snapshot;
+    every task must run exactly once and be finished when parallel_for returns (stale-snapshot
+    race)"""
+    hc.spgh_pool_stress.restype = ctypes.c_long
+    bad = hc.spgh_pool_stress(workers, 3000 if delay_us == 0 else 400, 64, delay_us, 1234 + delay_us)
+    assert bad == 0
+
+
 def test_curve_ops(oracle, hc):
     rng = np.random.default_rng(12)
     u = rng.integers(0, 256, 64 * 64, dtype=np.uint8)
