@@ -1,0 +1,134 @@
+// spg — the device Bullet round kernel (one launch per round of BulletReductionProof::prove); msm.hip
+// launches it, scripts/micro/bullet_phases.hip times its phases.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ctx.hpp"
+#include "lds.hpp"
+#include "quad.hpp"
+
+namespace spg {
+
+// ---- one Bullet round on the device (BulletReductionProof::prove, src/nizk/bullet.rs:32-132) ----------
+// Round k of a DotProductProofLog of size n holds a^(k) (nk = n >> k entries, Montgomery) and the generator
+// weights cw (n entries, kept as plain integers so that a Montgomery product with them is already the
+// canonical scalar). Its L and R are fixed-base MSMs over n/2 ORIGINAL generators each (proto.hip):
+//   L: p -> a^(k)[p mod nh] * cw[(p / nh) nk + nh + p mod nh],   R: p -> a^(k)[nh + p mod nh] * cw[(p / nh) nk + p mod nh]
+// with nh = nk / 2. For k >= 1 the kernel first applies round k-1's fold with (u, u^-1) from the kernel
+// arguments: a^(k)[i] = u a[i] + u^-1 a[i + nk], cw[j] *= (j mod 2nk < nk ? u^-1 : u). Every workgroup
+// (bucket v, MSM b) recomputes the scalars of its MSM; the v = 1 workgroups also write the folded state
+// (double-buffered: in and out never alias) for the next round. So a round needs no host-computed
+// scalars, no host-to-device copy and one launch: the host sends (u, u^-1) and reads back NB bucket sums
+// per MSM (coherent mapped memory), whose completion the last workgroup posts to the mailbox.
+struct BulletArgs {
+  const Fq* aa_in;
+  const Fq* cw_in;
+  Fq* aa_out;
+  Fq* cw_out;
+  const uint32_t* gidx;  // generator index of weight j (n entries)
+  Fq u, uinv;
+  int k, n, nk, n1;
+  const Niels* tab;
+  Ext* buckets;  // B = 2 bucket sets of NB (mapped host memory)
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq;
+  unsigned long long* probe;  // optional phase timestamps (scripts/micro/bullet_phases.hip), null in the product
+};
+
+template <int C, int BS>
+__global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  constexpr int S = BS / 4;  // quads
+  __shared__ uint32_t list[BS * W];
+  __shared__ uint32_t pts[soa_words<Ext, S>()];
+  __shared__ uint32_t cnt;
+  __shared__ bool last;
+  const int v = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int P = a.n / 2, nk = a.nk, nh = nk / 2;
+  const bool writer = blockIdx.x == 0;
+  Ext acc = ext_identity();
+  if (t == 0) cnt = 0;
+  unsigned long long* pr = a.probe ? a.probe + 8 * (blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
+  __syncthreads();
+  for (int base = 0; base < P; base += BS) {
+    const int p = base + t;
+    if (p < P) {
+      const int blk = p / nh, off = p - blk * nh;
+      const int ia = b ? off + nh : off;
+      const int j = blk * nk + (b ? 0 : nh) + off;
+      Fq av, cv;
+      if (a.k == 0) {
+        av = a.aa_in[ia];
+        cv = fq_zero();
+        cv.l[0] = 1u;
+      } else {
+        av = fq_add(fq_mul(a.aa_in[ia], a.u), fq_mul(a.uinv, a.aa_in[ia + nk]));
+        cv = fq_mul(a.cw_in[j], (j & (2 * nk - 1)) < nk ? a.uinv : a.u);
+      }
+      if (writer) {
+        if (blk == 0) a.aa_out[ia] = av;
+        a.cw_out[j] = cv;
+      }
+      const Fq k = fq_mul(av, cv);  // canonical scalar (cw is a plain integer)
+      const uint32_t gi = a.gidx[j];
+      int carry = 0;
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        const int bit = w * C;
+        const int li = bit >> 5, of = bit & 31;
+        uint32_t x = k.l[li] >> of;
+        if (of + C > 32 && li + 1 < 8) x |= k.l[li + 1] << (32 - of);
+        int d = (int)(x & MASK) + carry;
+        carry = d > NB ? 1 : 0;
+        d -= carry << C;
+        if (d == v || d == -v) {
+          const uint32_t pos = atomicAdd(&cnt, 1u);
+          list[pos] = (uint32_t)((size_t)(w * C) * a.n1 + gi) | (d < 0 ? 0x80000000u : 0u);
+        }
+      }
+    }
+    __syncthreads();
+    if (pr && t == 0 && base == 0) pr[1] = wall_clock64();
+    const uint32_t m = cnt;
+    for (uint32_t e = slot; e < m; e += S) {
+      const uint32_t ent = list[e];
+      const bool neg = ent >> 31;
+      const Niels* np = a.tab + (ent & 0x7fffffffu);
+      const int which = q >= 2 ? 2 : ((q == 0) != neg ? 1 : 0);
+      const Fp qv = which == 0 ? np->ypx : (which == 1 ? np->ymx : np->t2d);
+      acc = quad_madd(acc, qv, neg, q);
+    }
+    __syncthreads();
+    if (t == 0) cnt = 0;
+    __syncthreads();
+  }
+  if (pr && t == 0) pr[2] = wall_clock64();
+  for (int d = S / 2; d >= 1; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put<S>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add(acc, soa_get<S, Ext>(pts, slot), q);
+    __syncthreads();
+  }
+  if (pr && t == 0) pr[3] = wall_clock64();
+  if (t == 0) {
+    a.buckets[(size_t)b * NB + (v - 1)] = acc;
+    // the bucket (mapped host memory) and the folded state (HBM) before the ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.x * gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mbox_post(a.mb, a.seq, nullptr, 0);
+    }
+    if (pr) pr[4] = wall_clock64();
+  }
+}
+
+}  // namespace spg

@@ -461,7 +461,7 @@ SPG_HD Fp fp_add(const Fp& a, const Fp& b) {
 #pragma unroll
   for (int i = 0; i < 8; i++) r.l[i] = addc(a.l[i], b.l[i], c, c);
   c = fp_fold38(r.l, c);
-  fp_fold38(r.l, c);
+  r.l[0] += c * 38u;  // a second wrap leaves r < 38: no carry past limb 0
   return r;
 }
 SPG_HD Fp fp_sub(const Fp& a, const Fp& b) {
@@ -474,11 +474,8 @@ SPG_HD Fp fp_sub(const Fp& a, const Fp& b) {
   r.l[0] = subb(r.l[0], s, 0, b2);
 #pragma unroll
   for (int i = 1; i < 8; i++) r.l[i] = subb(r.l[i], 0, b2, b2);
-  s = b2 * 38u;
-  uint32_t b3 = 0;
-  r.l[0] = subb(r.l[0], s, 0, b3);
-#pragma unroll
-  for (int i = 1; i < 8; i++) r.l[i] = subb(r.l[i], 0, b3, b3);
+  // a second wrap leaves r >= 2^256 - 38 (limb 0 >= 2^32 - 38): no borrow past limb 0
+  r.l[0] -= b2 * 38u;
   return r;
 }
 SPG_HD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
@@ -493,7 +490,7 @@ SPG_HD Fp fp_reduce512(uint32_t t[16]) {
     c = (uint32_t)(v >> 32);
   }
   c = fp_fold38(r.l, c);
-  fp_fold38(r.l, c);
+  r.l[0] += c * 38u;  // c <= 38 above, so a second wrap leaves r < 38 * 38: no carry past limb 0
   return r;
 }
 // the device forms (product scanning), callable on the host for testing
@@ -563,19 +560,6 @@ SPG_HD Fp fp_sqr(const Fp& a) {
   }
   return fp_reduce512(t);
 #endif
-}
-SPG_HD Fp fp_mul_small(const Fp& a, uint32_t k) {
-  Fp r;
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t v = mad(a.l[i], k, c, 0);
-    r.l[i] = (uint32_t)v;
-    c = (uint32_t)(v >> 32);
-  }
-  c = fp_fold38(r.l, c);
-  fp_fold38(r.l, c);
-  return r;
 }
 // canonical representative in [0, p)
 SPG_HD Fp fp_canon(const Fp& a) {

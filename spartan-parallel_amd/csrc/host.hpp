@@ -165,6 +165,22 @@ struct HostGens {
   // scalar multiple is split into kShares window ranges, so even a 2-term commitment keeps several cores
   // busy: the pool's workers spin between the bursts of a sumcheck round, so a burst costs ~1 us to start.
   std::vector<Pt> commit_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs) {
+    std::vector<Pt> out(jobs.size());
+    run_many(jobs, [&](size_t j, const h::HExt& sum) { out[j] = compress(sum); });
+    return out;
+  }
+  // the same sums left uncompressed (terms a caller adds to a device result before encoding it)
+  std::vector<h::HExt> sum_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs) {
+    std::vector<h::HExt> out(jobs.size());
+    run_many(jobs, [&](size_t j, const h::HExt& sum) { out[j] = sum; });
+    return out;
+  }
+
+ private:
+  // one pool burst over every (job, term, window share); the last share of a job to finish (per-job
+  // countdown) adds the job's shares and hands the sum to done(job, sum)
+  template <class Done>
+  void run_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs, const Done& done) {
     static const int kShares = 4;  // 8 byte-windows (<= 8 mixed additions) per task
     std::vector<std::pair<size_t, size_t>> terms;  // (job, term)
     for (size_t j = 0; j < jobs.size(); j++) {
@@ -175,13 +191,14 @@ struct HostGens {
     }
     const int ntask = (int)terms.size() * kShares;
     std::vector<h::HExt> part(ntask);
-    // one burst: the last share of a job to finish (per-job countdown) adds the job's shares and encodes it
     std::vector<int> first(jobs.size() + 1, 0);
     for (size_t k = 0; k < terms.size(); k++) first[terms[k].first + 1] = (int)(k + 1) * kShares;
     for (size_t j = 1; j <= jobs.size(); j++) first[j] = std::max(first[j], first[j - 1]);
     std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[jobs.size()]);
-    for (size_t j = 0; j < jobs.size(); j++) left[j].store(first[j + 1] - first[j]);
-    std::vector<Pt> out(jobs.size());
+    for (size_t j = 0; j < jobs.size(); j++) {
+      left[j].store(first[j + 1] - first[j]);
+      if (first[j + 1] == first[j]) done(j, h::hext_identity());
+    }
     pool().parallel_for(ntask, [&](int k) {
       const auto& tm = terms[k / kShares];
       const auto& jb = jobs[tm.first];
@@ -192,10 +209,9 @@ struct HostGens {
       if (left[tm.first].fetch_sub(1, std::memory_order_acq_rel) == 1) {
         h::HExt sum = part[first[tm.first]];
         for (int i = first[tm.first] + 1; i < first[tm.first + 1]; i++) sum = h::hext_add(sum, part[i]);
-        out[tm.first] = compress(sum);
+        done(tm.first, sum);
       }
     });
-    return out;
   }
 };
 

@@ -170,7 +170,7 @@ static h::HExt hext_small_mul(h::HExt P, unsigned k) {
   return r;
 }
 
-void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out) {
+void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extra) {
   // chunk (lo, hi] of a bucket set: run = sum B_v, acc = sum (v - lo) B_v; the set's sum is
   // sum over chunks of acc + lo * run. Chunks spread one MSM's 2 NB dependent additions over the pool;
   // the last chunk of an MSM to finish (countdown) adds the chunks and encodes, all in one burst.
@@ -190,6 +190,7 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out) {
     if (left[b].fetch_sub(1, std::memory_order_acq_rel) == 1) {
       h::HExt s = part[b * K];
       for (int c = 1; c < K; c++) s = h::hext_add(s, part[b * K + c]);
+      if (extra) s = h::hext_add(s, extra[b]);
       out[b] = compress(s);
     }
   });
@@ -256,6 +257,95 @@ static void par_range(size_t n, const std::function<void(size_t, size_t)>& f) {
   pool().parallel_for((int)chunks, [&](int c) { f(n * c / chunks, n * (c + 1) / chunks); });
 }
 
+// Folds of one Bullet round on host copies (a, b for the next c_L / c_R, cw for the final g_hat) with u and
+// u^-1 of the round that took the size from 2 nn to nn (when fold), plus the next round's cross products
+// c_L = <a_L, b_R>, c_R = <a_R, b_L> over the halves of nn / 2 entries, in one pool burst.
+static void host_fold_dots(FqV& aa, FqV& bb, FqV& cw, size_t n, size_t nn, bool fold, const Fq& u, const Fq& uinv,
+                           Fq* cL, Fq* cR) {
+  const size_t nh = nn / 2;  // nn: size after the fold (2 nn before it)
+  const int C = nh >= 64 ? 8 : 1;
+  Fq pl[8], pr[8];
+  pool().parallel_for(C, [&](int c) {
+    Fq sl = fq_zero(), sr = fq_zero();
+    for (size_t i = nh * c / C; i < nh * (c + 1) / C; i++) {
+      if (fold) {
+        for (size_t i2 : {i, i + nh}) {
+          aa[i2] = fq_add(fq_mul(aa[i2], u), fq_mul(uinv, aa[i2 + nn]));
+          bb[i2] = fq_add(fq_mul(bb[i2], uinv), fq_mul(u, bb[i2 + nn]));
+        }
+      }
+      sl = fq_add(sl, fq_mul(aa[i], bb[i + nh]));
+      sr = fq_add(sr, fq_mul(aa[i + nh], bb[i]));
+    }
+    if (fold)
+      for (size_t j = n * c / C; j < n * (c + 1) / C; j++) cw[j] = fq_mul(cw[j], (j % (2 * nn)) < nn ? uinv : u);
+    pl[c] = sl;
+    pr[c] = sr;
+  });
+  *cL = pl[0];
+  *cR = pr[0];
+  for (int c = 1; c < C; c++) {
+    *cL = fq_add(*cL, pl[c]);
+    *cR = fq_add(*cR, pr[c]);
+  }
+}
+
+// Every Bullet round of one DotProductProofLog with the round's fold and MSM scalars computed on the device
+// (bullet_round_device): per round the host launches one kernel with (u, u^-1), then - while it runs - folds
+// its own copies of a, b, cw and computes c_L, c_R and the G_1 / h terms of L and R, waits for the bucket
+// sums (mailbox), finishes L and R on the pool and draws the next challenge. Same transcript, same points.
+static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x, const FqV& a, const Fq& r,
+                                const FqV& v1, const FqV& v2, const uint32_t* d_idx, Ext* mbk, Ext* d_bk, FqV* aa,
+                                FqV* bb, FqV* cw, Fq* blind_fin, DotProductProofLogP* out) {
+  const size_t n = x.size();
+  const size_t G1 = g.gens_1.G[0], H = g.gens_n.h;
+  Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
+  if (!st) return set_err(ctx, SPG_E_NOMEM, "bullet state");
+  Fq* d_aa[2] = {st, st + n};
+  Fq* d_cw[2] = {st + 2 * n, st + 3 * n};
+  uint8_t* stage = (uint8_t*)pinned_get(ctx, n * sizeof(Fq));
+  if (!stage) return set_err(ctx, SPG_E_NOMEM, "bullet staging");
+  memcpy(stage, x.data(), n * sizeof(Fq));
+  SPG_HIP(ctx, hipMemcpyAsync(d_aa[0], stage, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+  Fq u = fq_zero(), uinv = fq_zero();
+  size_t nk = n;
+  for (int k = 0; nk != 1; k++) {
+    uint32_t seq = 0;
+    int rc = bullet_round_device(ctx, g.dev, d_aa[k & 1], d_cw[k & 1], d_aa[(k + 1) & 1], d_cw[(k + 1) & 1], d_idx, u,
+                                 uinv, k, (int)n, (int)nk, d_bk, &seq);
+    if (rc) return rc;
+    g_msm_laps.lap("bullet_launch");
+    Fq cL, cR;
+    host_fold_dots(*aa, *bb, *cw, n, nk, k > 0, u, uinv, &cL, &cR);
+    const Fq blind_L = v1[k], blind_R = v2[k];
+    std::vector<h::HExt> ex = g.host.sum_many({{{G1, H}, {fq_mul(cL, r), blind_L}}, {{G1, H}, {fq_mul(cR, r), blind_R}}});
+    g_msm_laps.lap("bullet_host_overlap");
+    rc = mbox_wait(ctx, seq, nullptr, 0);
+    if (rc) return rc;
+    g_msm_laps.lap("msm_device");
+    Pt LR[2];
+    bucket_finals(mbk, 2, kBulletNB, LR, ex.data());
+    g_msm_laps.lap("msm_host_final");
+    t.point("L", LR[0]);
+    t.point("R", LR[1]);
+    u = t.challenge("u");
+    uinv = fq_inv(u);
+    *blind_fin = fq_add(fq_add(*blind_fin, fq_mul(fq_mul(blind_L, u), u)), fq_mul(fq_mul(blind_R, uinv), uinv));
+    out->L.push_back(LR[0]);
+    out->R.push_back(LR[1]);
+    g_msm_laps.lap("bullet_challenge");
+    nk /= 2;
+  }
+  // the last round's fold of the host copies (a_hat, b_hat and the final generator weights)
+  (*aa)[0] = fq_add(fq_mul((*aa)[0], u), fq_mul(uinv, (*aa)[1]));
+  (*bb)[0] = fq_add(fq_mul((*bb)[0], uinv), fq_mul(u, (*bb)[1]));
+  par_range(n, [&](size_t lo, size_t hi) {
+    for (size_t j = lo; j < hi; j++) (*cw)[j] = fq_mul((*cw)[j], (j & 1) ? u : uinv);
+  });
+  g_msm_laps.lap("bullet_fold");
+  return 0;
+}
+
 // src/nizk/mod.rs:439-523 + src/nizk/bullet.rs:32-132
 int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const FqV& x, const Fq& blind_x, const FqV& a,
                          const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy_out) {
@@ -314,6 +404,16 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   }
   size_t nk = n, k = 0;
   g_msm_laps.lap("bullet_prep");
+  static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
+  void* d_map = nullptr;
+  Ext* mbk = (dev_rounds && n >= 2 && (n & (n - 1)) == 0)
+                 ? (Ext*)mapped_get(ctx, sizeof(Ext) * 2 * kBulletNB + 64, &d_map)
+                 : nullptr;
+  if (mbk) {
+    int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, mbk, (Ext*)d_map, &aa, &bb, &cw, &blind_fin, out);
+    if (rc) return rc;
+    nk = 1;
+  }
   while (nk != 1) {
     size_t nh = nk / 2;
     Fq cL = dot(aa, bb, 0, nh, nh), cR = dot(aa, bb, nh, 0, nh);

@@ -105,6 +105,21 @@ def test_fp_device_forms_boundary(hc):
             assert toint(out[i]) == f(toint(A[i]), toint(B[i])), (code, i)
 
 
+def test_fp_add_sub_double_wrap(hc):
+    """fp_add / fp_sub fold a second wrap by 2^256 into limb 0 alone (field.hpp): inputs whose sums or
+    differences wrap twice (limbs near 2^32 - 1, values near 2^256 and 0) against Python big-int"""
+    vals = [0, 1, 37, 38, 75, 2**255 - 19, 2**255 - 20, 2**256 - 1, 2**256 - 38, 2**256 - 39, 2**256 - 75, 2**128 - 1]
+    pairs = [(a, b) for a in vals for b in vals]
+    A = np.array([[(a >> (32 * i)) & 0xFFFFFFFF for i in range(8)] for a, _ in pairs], dtype=np.uint32)
+    B = np.array([[(b >> (32 * i)) & 0xFFFFFFFF for i in range(8)] for _, b in pairs], dtype=np.uint32)
+    toint = lambda r: sum(int(x) << (32 * i) for i, x in enumerate(r))
+    for code, f in [(0, lambda a, b: (a + b) % P), (1, lambda a, b: (a - b) % P)]:
+        out = np.zeros_like(A)
+        hc.spgh_fp_op(code, _p(A), _p(B), _p(out), ctypes.c_size_t(len(pairs)))
+        for i, (a, b) in enumerate(pairs):
+            assert toint(out[i]) % P == f(a, b), (code, a, b)
+
+
 @pytest.mark.parametrize("workers,delay_us", [(7, 0), (7, 50), (3, 200)])
 def test_pool_bursts(hc, workers, delay_us):
     """hpool.hpp: bursts of growing / varying size with workers delayed inside their lock-free snapshot;
