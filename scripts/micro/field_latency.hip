@@ -4,6 +4,7 @@
 #include <stdio.h>
 
 #include "../../spartan-parallel_amd/csrc/curve.hpp"
+#include "../../spartan-parallel_amd/csrc/quad.hpp"
 
 using namespace spg;
 
@@ -26,6 +27,10 @@ __global__ void __launch_bounds__(64) k_lat(const Fp* in, Fp* out, long long* cy
     if (W == 4) qa = fq_mul(qa, qb);
     if (W == 5) a = fp_add(a, b);
     if (W == 6) qa = fq_add(qa, qb);
+    if (W == 7) P = quad_add(P, P, threadIdx.x & 3);
+    if (W == 8) P = quad_madd(P, b, (i & 1) != 0, threadIdx.x & 3);
+    if (W == 9) P = quad_dbl(P, threadIdx.x & 3);
+    if (W == 10) a = fp_sub(a, b);
   }
   long long t1 = clock64();
   Fp q{{qa.l[0], qa.l[1], qa.l[2], qa.l[3], qa.l[4], qa.l[5], qa.l[6], qa.l[7]}};
@@ -57,6 +62,10 @@ int main() {
   printf("fq_mul   %lld\n", run<4>(in, out, cyc));
   printf("fp_add   %lld\n", run<5>(in, out, cyc));
   printf("fq_add   %lld\n", run<6>(in, out, cyc));
+  printf("quad_add %lld\n", run<7>(in, out, cyc));
+  printf("quad_madd %lld\n", run<8>(in, out, cyc));
+  printf("quad_dbl %lld\n", run<9>(in, out, cyc));
+  printf("fp_sub   %lld\n", run<10>(in, out, cyc));
   printf("(cycles per dependent op, one wave)\n");
   return 0;
 }

@@ -479,6 +479,39 @@ SPG_HD Fp fp_sub(const Fp& a, const Fp& b) {
   return r;
 }
 SPG_HD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
+// a + b (neg false) or a - b (neg true) in one carry pass, for lanes that need different ones: a + (b ^ m) + neg,
+// then the wrap folded as in fp_add / fp_sub (the same representative as theirs)
+SPG_HD Fp fp_addsub(const Fp& a, const Fp& b, bool neg) {
+  const uint32_t m = neg ? 0xffffffffu : 0u;
+  Fp r;
+  uint32_t c = neg ? 1u : 0u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = addc(a.l[i], b.l[i] ^ m, c, c);
+  // add: carry -> r + 38 ; sub: no carry (a < b, r = a - b + 2^256) -> r - 38, as + (2^256 - 38)
+  const bool t = (c != 0) != neg;
+  const uint32_t k0 = t ? (neg ? 0u - 38u : 38u) : 0u, kh = (t && neg) ? 0xffffffffu : 0u;
+  uint32_t c2 = 0;
+  r.l[0] = addc(r.l[0], k0, 0u, c2);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.l[i] = addc(r.l[i], kh, c2, c2);
+  // a second wrap (add: r < 38 now; sub: r >= 2^256 - 76 now) touches limb 0 alone
+  if (t) r.l[0] += neg ? (c2 ? 0u : 0u - 38u) : (c2 ? 38u : 0u);
+  return r;
+}
+// a * k for a small k (< 2^18): 8 limb products and one 38-fold
+SPG_HD Fp fp_mul_k(const Fp& a, uint32_t k) {
+  Fp r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t v = mad(a.l[i], k, c, 0);
+    r.l[i] = (uint32_t)v;
+    c = (uint32_t)(v >> 32);
+  }
+  c = fp_fold38(r.l, c);  // c < 2^18: c * 38 + r[0] carries at most 1
+  r.l[0] += c * 38u;      // a second wrap leaves r < 38 * 2^18: no carry past limb 0
+  return r;
+}
 
 SPG_HD Fp fp_reduce512(uint32_t t[16]) {
   Fp r;

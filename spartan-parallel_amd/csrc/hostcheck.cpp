@@ -41,7 +41,8 @@ void spgh_fq_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, siz
   }
 }
 
-// op: 0 add, 1 sub, 2 mul, 3 sqr, 4 inv, 5 canon, 6 mul (device product scanning), 7 sqr (device);
+// op: 0 add, 1 sub, 2 mul, 3 sqr, 4 inv, 5 canon, 6 mul (device product scanning), 7 sqr (device),
+// 12 mul_k (k = b's low 18 bits); raw (not canonicalised) outputs: 8 addsub(+), 9 addsub(-), 10 add, 11 sub;
 // inputs/outputs as 8 x u32 (loose allowed)
 void spgh_fp_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
   for (size_t i = 0; i < n; i++) {
@@ -56,9 +57,14 @@ void spgh_fp_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, siz
       case 4: r = fp_inv(x); break;
       case 6: r = fp_mul_ps(x, y); break;
       case 7: r = fp_sqr_ps(x); break;
+      case 8: r = fp_addsub(x, y, false); break;
+      case 9: r = fp_addsub(x, y, true); break;
+      case 10: r = fp_add(x, y); break;
+      case 11: r = fp_sub(x, y); break;
+      case 12: r = fp_mul_k(x, y.l[0] & 0x3ffffu); break;
       default: r = x; break;
     }
-    r = fp_canon(r);
+    if (op < 8 || op > 11) r = fp_canon(r);
     memcpy(out + 8 * i, r.l, 32);
   }
 }

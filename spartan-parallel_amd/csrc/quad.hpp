@@ -9,10 +9,10 @@ namespace spg {
 
 // ---- quad-cooperative point arithmetic for the latency path --------------------------------------
 // The four lanes of a quad hold the same point and split each addition's field products between them:
-// product round 1 gives lane r one of A, B, C', D of add-2008-hwcd-3, round 2 scales C' by 2d (lane 2),
-// round 3 gives lane r one of X3, Y3, T3, Z3; DPP quad broadcasts exchange the products. The dependent chain
-// of an addition drops from 10 (mixed: 7) field multiplications to 3 (2); every formula and value is the one
-// ext_add / ext_madd compute, so the group element (and its encoding) is identical.
+// product round 1 gives lane r one of A, B, C, D of add-2008-hwcd-3 (for P + Q scaled by a small constant,
+// see quad_add), round 2 gives lane r one of X3, Y3, T3, Z3; DPP quad permutations exchange the products.
+// The dependent chain of an addition drops from 10 (mixed: 7) field multiplications to 2 plus a small-constant
+// product (mixed: 2). The group element, so its encoding, is the one ext_add / ext_madd compute.
 template <int K>
 __device__ __forceinline__ Fp fp_qbcast(const Fp& a) {
   Fp r;
@@ -39,26 +39,48 @@ __device__ __forceinline__ Ext quad_out(const Fp& E, const Fp& F, const Fp& G, c
   r.Z = fp_qbcast<3>(w);
   return r;
 }
-__device__ __forceinline__ Ext quad_finish(const Fp& p, int q) {
-  const Fp A = fp_qbcast<0>(p), B = fp_qbcast<1>(p), C = fp_qbcast<2>(p), D = fp_qbcast<3>(p);
-  return quad_out(fp_sub(B, A), fp_sub(D, C), fp_add(D, C), fp_add(B, A), q);
+// DPP quad permutation: lane r of each quad reads lane (CTRL >> 2r) & 3 of its quad
+template <int CTRL>
+__device__ __forceinline__ Fp fp_qperm(const Fp& a) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], CTRL, 0xf, 0xf, false);
+  return r;
+}
+// second product round of add-2008-hwcd-3: lane r holds p_r in (A, B, C, D) (cneg: the true C is -p_2).
+// E = B - A, F = D - C, G = D + C, H = B + A; lane 0 forms X3 = E F, 1 Y3 = G H, 2 T3 = E H, 3 Z3 = F G, so
+// every lane needs two of them: u in (E, G, E, F) and v in (F, H, H, G), each one add-or-subtract of two
+// gathered products (quad_perm [1,3,1,3] / [0,2,0,2] and [3,1,1,3] / [2,0,0,2]).
+__device__ __forceinline__ Ext quad_finish(const Fp& p, int q, bool cneg) {
+  const Fp uA = fp_qperm<0xDD>(p), uB = fp_qperm<0x88>(p);
+  const Fp vA = fp_qperm<0xD7>(p), vB = fp_qperm<0x82>(p);
+  const bool usub = q == 1 ? cneg : (q == 3 ? !cneg : true);
+  const bool vsub = q == 0 ? !cneg : (q == 3 ? cneg : false);
+  const Fp w = fp_mul(fp_addsub(uA, uB, usub), fp_addsub(vA, vB, vsub));
+  Ext r;
+  r.X = fp_qbcast<0>(w);
+  r.Y = fp_qbcast<1>(w);
+  r.T = fp_qbcast<2>(w);
+  r.Z = fp_qbcast<3>(w);
+  return r;
+}
+// lane q's first-round operand of P: Y - X, Y + X, T, Z
+__device__ __forceinline__ Fp quad_operand(const Ext& P, int q) {
+  return q < 2 ? fp_addsub(P.Y, P.X, q == 0) : (q == 2 ? P.T : P.Z);
 }
 // P + (+-Niels); qv is this lane's Niels coordinate: lane 0 the "minus" one (neg ? ypx : ymx), lane 1 the
-// "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it)
+// "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it); -Q has C negated (cneg)
 __device__ __forceinline__ Ext quad_madd(const Ext& P, const Fp& qv, bool neg, int q) {
-  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
-  const Fp y = fp_sel(q == 3, fp_small(2), qv);
-  Fp p = fp_mul(x, y);
-  p = fp_sel(neg && q == 2, fp_neg(p), p);
-  return quad_finish(p, q);
+  const Fp y = q == 3 ? fp_small(2) : qv;
+  return quad_finish(fp_mul(quad_operand(P, q), y), q, neg);
 }
+// P + Q with A, B, C, D all scaled by 121666 (so E..H scale alike and the sum is the same projective point,
+// its coordinates 121666^2 times ext_add's): C = 2d T1 T2 becomes -243330 T1 T2 since 2d = -2 * 121665 / 121666,
+// a small constant like 121666 (A, B) and 243332 (D = 2 Z1 Z2): one full product round fewer than 2d T1 T2.
 __device__ __forceinline__ Ext quad_add(const Ext& P, const Ext& Q, int q) {
-  const Fp x = fp_sel(q == 0, fp_sub(P.Y, P.X), fp_sel(q == 1, fp_add(P.Y, P.X), fp_sel(q == 2, P.T, P.Z)));
-  const Fp y = fp_sel(q == 0, fp_sub(Q.Y, Q.X), fp_sel(q == 1, fp_add(Q.Y, Q.X), fp_sel(q == 2, Q.T, Q.Z)));
-  Fp p = fp_mul(x, y);
-  const Fp pd = fp_mul(p, c_d2());  // C = 2d T1 T2 (lane 2)
-  p = fp_sel(q == 2, pd, fp_sel(q == 3, fp_add(p, p), p));  // D = 2 Z1 Z2 (lane 3)
-  return quad_finish(p, q);
+  const Fp p = fp_mul(quad_operand(P, q), quad_operand(Q, q));
+  const uint32_t k = q == 2 ? 243330u : (q == 3 ? 243332u : 121666u);
+  return quad_finish(fp_mul_k(p, k), q, true);
 }
 
 // 2P (dbl-2008-hwcd as ext_dbl): lane q squares X, Y, Z, X + Y

@@ -120,6 +120,35 @@ def test_fp_add_sub_double_wrap(hc):
             assert toint(out[i]) % P == f(a, b), (code, a, b)
 
 
+def test_fp_addsub_and_mul_k(hc):
+    """fp_addsub (one carry pass for lane-dependent add / sub in the quad point arithmetic) returns the same
+    representative as fp_add / fp_sub; fp_mul_k (small constants of the scaled quad addition) against big-int"""
+    rng = np.random.default_rng(23)
+    vals = [0, 1, 37, 38, 75, 2**255 - 19, 2**256 - 1, 2**256 - 38, 2**256 - 39, 2**256 - 75, 2**256 - 76]
+    pairs = [(a, b) for a in vals for b in vals]
+    n = len(pairs) + 2000
+    A = rng.integers(0, 2**32, size=(n, 8), dtype=np.uint64).astype(np.uint32)
+    B = rng.integers(0, 2**32, size=(n, 8), dtype=np.uint64).astype(np.uint32)
+    for i, (a, b) in enumerate(pairs):
+        A[i] = [(a >> (32 * k)) & 0xFFFFFFFF for k in range(8)]
+        B[i] = [(b >> (32 * k)) & 0xFFFFFFFF for k in range(8)]
+    toint = lambda r: sum(int(x) << (32 * i) for i, x in enumerate(r))
+    raw = {}
+    for code in (8, 9, 10, 11):
+        raw[code] = np.zeros_like(A)
+        hc.spgh_fp_op(code, _p(A), _p(B), _p(raw[code]), ctypes.c_size_t(n))
+    assert np.array_equal(raw[8], raw[10]) and np.array_equal(raw[9], raw[11])
+    for i in range(n):
+        a, b = toint(A[i]), toint(B[i])
+        assert toint(raw[8][i]) % P == (a + b) % P and toint(raw[9][i]) % P == (a - b) % P
+    B[:, 0] = rng.integers(0, 2**18, size=n, dtype=np.uint64).astype(np.uint32)
+    B[:4, 0] = [0, 1, 243330, 2**18 - 1]
+    out = np.zeros_like(A)
+    hc.spgh_fp_op(12, _p(A), _p(B), _p(out), ctypes.c_size_t(n))
+    for i in range(n):
+        assert toint(out[i]) == toint(A[i]) * int(B[i, 0]) % P, i
+
+
 @pytest.mark.parametrize("workers,delay_us", [(7, 0), (7, 50), (3, 200)])
 def test_pool_bursts(hc, workers, delay_us):
     """hpool.hpp: bursts of growing / varying size with workers delayed inside their lock-free snapshot;
