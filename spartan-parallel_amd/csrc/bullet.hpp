@@ -94,13 +94,20 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
     __syncthreads();
     if (pr && t == 0 && base == 0) pr[1] = wall_clock64();
     const uint32_t m = cnt;
-    for (uint32_t e = slot; e < m; e += S) {
-      const uint32_t ent = list[e];
-      const bool neg = ent >> 31;
-      const Niels* np = a.tab + (ent & 0x7fffffffu);
-      const int which = q >= 2 ? 2 : ((q == 0) != neg ? 1 : 0);
-      const Fp qv = which == 0 ? np->ypx : (which == 1 ? np->ymx : np->t2d);
+    // software-pipelined: the table coordinate of entry e + S is loaded while entry e is added
+    uint32_t e = slot;
+    Fp qv;
+    bool neg = false;
+    if (e < m) qv = niels_coord(a.tab, list[e], q, &neg);
+    while (e < m) {
+      const uint32_t e2 = e + S;
+      Fp qn;
+      bool nn = false;
+      if (e2 < m) qn = niels_coord(a.tab, list[e2], q, &nn);
       acc = quad_madd(acc, qv, neg, q);
+      qv = qn;
+      neg = nn;
+      e = e2;
     }
     __syncthreads();
     if (t == 0) cnt = 0;
@@ -108,9 +115,9 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
   }
   if (pr && t == 0) pr[2] = wall_clock64();
   for (int d = S / 2; d >= 1; d >>= 1) {
-    if (slot >= d && slot < 2 * d) quad_put<S>(pts, slot - d, acc, q);
+    if (slot >= d && slot < 2 * d) quad_put_op<S>(pts, slot - d, acc, q);
     __syncthreads();
-    if (slot < d) acc = quad_add(acc, soa_get<S, Ext>(pts, slot), q);
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<S>(pts, slot, q), q);
     __syncthreads();
   }
   if (pr && t == 0) pr[3] = wall_clock64();

@@ -423,9 +423,9 @@ __global__ void __launch_bounds__(4 * SL) k_final_q(const Ext* __restrict__ segT
   Ext val = quad_add(U, tot, q);
   Ext suf = V;
   for (int d = 1; d < SL; d <<= 1) {
-    quad_put<SL>(sh, slot, suf, q);
+    quad_put_op<SL>(sh, slot, suf, q);
     __syncthreads();
-    if (slot + d < SL) suf = quad_add(suf, soa_get<SL, Ext>(sh, slot + d), q);
+    if (slot + d < SL) suf = quad_add_op(suf, quad_get_op<SL>(sh, slot + d, q), q);
     __syncthreads();
   }
   if (slot >= 1) {
@@ -433,9 +433,9 @@ __global__ void __launch_bounds__(4 * SL) k_final_q(const Ext* __restrict__ segT
     val = quad_add(val, suf, q);
   }
   for (int d = SL / 2; d >= 1; d >>= 1) {
-    quad_put<SL>(sh, slot, val, q);
+    quad_put_op<SL>(sh, slot, val, q);
     __syncthreads();
-    if (slot < d) val = quad_add(val, soa_get<SL, Ext>(sh, slot + d), q);
+    if (slot < d) val = quad_add_op(val, quad_get_op<SL>(sh, slot + d, q), q);
     __syncthreads();
   }
   if (t == 0 && ext_out) ext_out[b] = val;
@@ -567,23 +567,29 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket_q(const Fq* __restrict__ sca
     }
     __syncthreads();
     const uint32_t m = cnt;
-    for (uint32_t e = slot; e < m; e += S) {
-      const uint32_t ent = list[e];
-      const bool neg = ent >> 31;
-      const Niels* np = tab + (ent & 0x7fffffffu);
-      // Niels field order: ypx, ymx, t2d
-      const int which = q >= 2 ? 2 : ((q == 0) != neg ? 1 : 0);
-      const Fp qv = which == 0 ? np->ypx : (which == 1 ? np->ymx : np->t2d);
+    // software-pipelined: the table coordinate of entry e + S is loaded while entry e is added
+    uint32_t e = slot;
+    Fp qv;
+    bool neg = false;
+    if (e < m) qv = niels_coord(tab, list[e], q, &neg);
+    while (e < m) {
+      const uint32_t e2 = e + S;
+      Fp qn;
+      bool nn = false;
+      if (e2 < m) qn = niels_coord(tab, list[e2], q, &nn);
       acc = quad_madd(acc, qv, neg, q);
+      qv = qn;
+      neg = nn;
+      e = e2;
     }
     __syncthreads();
     if (t == 0) cnt = 0;
     __syncthreads();
   }
   for (int d = S / 2; d >= 1; d >>= 1) {
-    if (slot >= d && slot < 2 * d) quad_put<S>(pts, slot - d, acc, q);
+    if (slot >= d && slot < 2 * d) quad_put_op<S>(pts, slot - d, acc, q);
     __syncthreads();
-    if (slot < d) acc = quad_add(acc, soa_get<S, Ext>(pts, slot), q);
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<S>(pts, slot, q), q);
     __syncthreads();
   }
   if (t == 0) buckets[(size_t)b * NB + (v - 1)] = acc;
@@ -643,15 +649,15 @@ __global__ void __launch_bounds__(1024) k_smsm_final_q(const Ext* __restrict__ b
   const int b = blockIdx.x, t = threadIdx.x, q = t & 3, slot = t >> 2;
   Ext suf = buckets[(size_t)b * NB + slot];
   for (int d = 1; d < NB; d <<= 1) {
-    quad_put<256>(sh, slot, suf, q);
+    quad_put_op<256>(sh, slot, suf, q);
     __syncthreads();
-    if (slot + d < NB) suf = quad_add(suf, soa_get<256, Ext>(sh, slot + d), q);
+    if (slot + d < NB) suf = quad_add_op(suf, quad_get_op<256>(sh, slot + d, q), q);
     __syncthreads();
   }
   for (int d = NB / 2; d >= 1; d >>= 1) {
-    quad_put<256>(sh, slot, suf, q);
+    quad_put_op<256>(sh, slot, suf, q);
     __syncthreads();
-    if (slot < d) suf = quad_add(suf, soa_get<256, Ext>(sh, slot + d), q);
+    if (slot < d) suf = quad_add_op(suf, quad_get_op<256>(sh, slot + d, q), q);
     __syncthreads();
   }
   if (t == 0) out[b] = suf;

@@ -68,11 +68,24 @@ __device__ __forceinline__ Ext quad_finish(const Fp& p, int q, bool cneg) {
 __device__ __forceinline__ Fp quad_operand(const Ext& P, int q) {
   return q < 2 ? fp_addsub(P.Y, P.X, q == 0) : (q == 2 ? P.T : P.Z);
 }
+// the Niels coordinate lane q of a quad needs for table entry ent (index | neg << 31): lane 0 the "minus" one
+// (neg ? ypx : ymx), lane 1 the "plus" one, lanes 2, 3 t2d; one 32-byte load per lane
+__device__ __forceinline__ Fp niels_coord(const Niels* __restrict__ tab, uint32_t ent, int q, bool* neg) {
+  *neg = ent >> 31;
+  const int which = q >= 2 ? 2 : ((q == 0) != *neg ? 1 : 0);  // Niels field order: ypx, ymx, t2d
+  return reinterpret_cast<const Fp*>(tab + (ent & 0x7fffffffu))[which];
+}
 // P + (+-Niels); qv is this lane's Niels coordinate: lane 0 the "minus" one (neg ? ypx : ymx), lane 1 the
 // "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it); -Q has C negated (cneg)
 __device__ __forceinline__ Ext quad_madd(const Ext& P, const Fp& qv, bool neg, int q) {
   const Fp y = q == 3 ? fp_small(2) : qv;
   return quad_finish(fp_mul(quad_operand(P, q), y), q, neg);
+}
+// P + Q given lane q's first-round operand of Q (quad_operand(Q, q)), scaled as quad_add below
+__device__ __forceinline__ Ext quad_add_op(const Ext& P, const Fp& qop, int q) {
+  const Fp p = fp_mul(quad_operand(P, q), qop);
+  const uint32_t k = q == 2 ? 243330u : (q == 3 ? 243332u : 121666u);
+  return quad_finish(fp_mul_k(p, k), q, true);
 }
 // P + Q with A, B, C, D all scaled by 121666 (so E..H scale alike and the sum is the same projective point,
 // its coordinates 121666^2 times ext_add's): C = 2d T1 T2 becomes -243330 T1 T2 since 2d = -2 * 121665 / 121666,
@@ -98,6 +111,22 @@ __device__ __forceinline__ void quad_put(uint32_t* sh, int slot, const Ext& P, i
   const Fp c = fp_sel(q == 0, P.X, fp_sel(q == 1, P.Y, fp_sel(q == 2, P.Z, P.T)));
 #pragma unroll
   for (int i = 0; i < 8; i++) sh[(q * 8 + i) * SL + slot] = c.l[i];
+}
+
+// tree / scan hand-offs through LDS carry first-round operands: the giving quad's lane q stores
+// quad_operand(P, q) (component-major slot), the receiving quad's lane q reads only its own 8 words
+template <int SL>
+__device__ __forceinline__ void quad_put_op(uint32_t* sh, int slot, const Ext& P, int q) {
+  const Fp c = quad_operand(P, q);
+#pragma unroll
+  for (int i = 0; i < 8; i++) sh[(q * 8 + i) * SL + slot] = c.l[i];
+}
+template <int SL>
+__device__ __forceinline__ Fp quad_get_op(const uint32_t* sh, int slot, int q) {
+  Fp c;
+#pragma unroll
+  for (int i = 0; i < 8; i++) c.l[i] = sh[(q * 8 + i) * SL + slot];
+  return c;
 }
 
 }  // namespace spg
