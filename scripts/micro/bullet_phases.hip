@@ -7,6 +7,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include "../../spartan-parallel_amd/csrc/bullet.hpp"
@@ -71,6 +73,52 @@ static void run(int n, int k, Niels* tab, int n1, Fq* st, uint32_t* gidx, unsign
          n, k, BS, ms * 1000 / R, skew, ph[0], mx[0], ph[1], mx[1], ph[2], mx[2], ph[3], mx[3], (tend - t0) * 0.01);
 }
 
+__global__ void k_clock(unsigned long long* out, int iters) {
+  unsigned long long w0 = wall_clock64(), c0 = clock64();
+  float x = threadIdx.x;
+  for (int i = 0; i < iters; i++) x = x * 0.999f + 1.0f;
+  unsigned long long w1 = wall_clock64(), c1 = clock64();
+  if (threadIdx.x == 0) {
+    out[0] = w1 - w0;
+    out[1] = c1 - c0;
+    out[2] = (unsigned long long)x;
+  }
+}
+
+// per-launch time of one Bullet round when launches are separated by host idle gaps (the prover's pattern)
+template <int BS>
+static void run_gaps(int n, Niels* tab, int n1, Fq* st, uint32_t* gidx, unsigned* ctr, uint32_t* mb, Ext* bk,
+                     int gap_us, unsigned long long* clk) {
+  const int NB = 64;
+  Fq u, ui;
+  for (int i = 0; i < 8; i++) u.l[i] = ui.l[i] = 0x01234567u * (i + 1);
+  u.l[7] = ui.l[7] = 0x01000000u;
+  BulletArgs a{st, st + 2 * (size_t)n, st + (size_t)n, st + 3 * (size_t)n, gidx, u, ui, 1, n, n >> 1, n1, tab, bk,
+               ctr, mb, 1u, nullptr};
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  double tot = 0;
+  const int R = 30;
+  for (int r = 0; r < R + 3; r++) {
+    std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
+    hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB, 2), dim3(BS), 0, 0, a);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (r >= 3) tot += ms;
+  }
+  // shader clock after the same gap
+  std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
+  hipLaunchKernelGGL(k_clock, dim3(1), dim3(64), 0, 0, clk, 20000);
+  unsigned long long h[3];
+  hipMemcpy(h, clk, 24, hipMemcpyDeviceToHost);
+  printf("gap %5d us: n=%d round %.1f us/launch; shader clock %.0f MHz (single-wave loop after the gap)\n", gap_us, n,
+         tot * 1000 / R, h[1] * 100.0 / h[0]);
+}
+
 int main() {
   const int n1 = 4098, rows = 254;
   Niels* tab;
@@ -119,6 +167,10 @@ int main() {
     hipEventElapsedTime(&ms, e0, e1);
     printf("null kernel (64 x 2 blocks): %.1f us/launch\n", ms * 1000 / 20);
   }
+  unsigned long long* clk;
+  hipMalloc(&clk, 64);
+  for (int gap : {0, 20, 100, 1000})
+    run_gaps<256>(512, tab, n1, st, gidx, ctr, mb, bk, gap, clk);
   for (int k = 0; k < 2; k++) {
     run<64>(128, k, tab, n1, st, gidx, ctr, mb, bk, probe);
     run<128>(256, k, tab, n1, st, gidx, ctr, mb, bk, probe);

@@ -144,12 +144,12 @@ extern "C" int spg_init(int device, spg_ctx** out) {
     return SPG_E_HIP;
   }
   void* mb = nullptr;
-  if (hipHostMalloc(&mb, 4096, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+  if (hipHostMalloc(&mb, spg::kMboxBytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mbox, mb, 0) != hipSuccess) {
     delete c;
     return SPG_E_HIP;
   }
-  memset(mb, 0, 4096);
+  memset(mb, 0, spg::kMboxBytes);
   c->mbox = (volatile uint32_t*)mb;
   *out = c;
   return SPG_OK;

@@ -127,6 +127,9 @@ int bullet_round_device(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const 
                         uint32_t* seq_out);
 static const int kBulletNB = 64;  // buckets per MSM of bullet_round_device (c = 7)
 
+// the mailbox page: sequence number (word 0), then up to kMboxScalars scalars from word 8
+static const size_t kMboxBytes = 65536;
+static const size_t kMboxScalars = (kMboxBytes - 32) / 32;
 // waits (spinning, bounded) until the mailbox carries sequence number `seq`, then copies n scalars out
 int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n);
 

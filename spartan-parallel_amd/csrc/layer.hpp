@@ -1,0 +1,313 @@
+// spg — SPARK layer-sumcheck kernels (ProductCircuitEvalProofBatched rounds, product_tree.rs:271-396);
+// spark.hip launches them, scripts/micro/layer_phases.hip times their phases.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ctx.hpp"
+#include "lds.hpp"
+
+namespace spg {
+
+struct Triple {
+  Fq *A, *B, *C;
+};
+__device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
+  __shared__ uint32_t sh[3][soa_words<Fq, 256>()];  // component-major: no bank conflicts
+  int t = threadIdx.x;
+  for (int d = 128; d >= 1; d >>= 1) {
+    if (t >= d && t < 2 * d) {
+      soa_put<256>(sh[0], t - d, v0);
+      soa_put<256>(sh[1], t - d, v1);
+      soa_put<256>(sh[2], t - d, v2);
+    }
+    __syncthreads();
+    if (t < d) {
+      v0 = fq_add(v0, soa_get<256, Fq>(sh[0], t));
+      v1 = fq_add(v1, soa_get<256, Fq>(sh[1], t));
+      v2 = fq_add(v2, soa_get<256, Fq>(sh[2], t));
+    }
+    __syncthreads();
+  }
+  // broadcast thread 0's sums
+  if (t == 0) {
+    soa_put<256>(sh[0], 0, v0);
+    soa_put<256>(sh[1], 0, v1);
+    soa_put<256>(sh[2], 0, v2);
+  }
+  __syncthreads();
+  v0 = soa_get<256, Fq>(sh[0], 0);
+  v1 = soa_get<256, Fq>(sh[1], 0);
+  v2 = soa_get<256, Fq>(sh[2], 0);
+  __syncthreads();
+}
+// block-wide sums of three Fq values over BS threads; the result is valid in thread 0
+template <int BS>
+__device__ __forceinline__ void block_sum3_t0(Fq& v0, Fq& v1, Fq& v2) {
+  __shared__ uint32_t sh[3][soa_words<Fq, BS / 2>()];
+  const int t = threadIdx.x;
+  for (int d = BS / 2; d >= 1; d >>= 1) {
+    if (t >= d && t < 2 * d) {
+      soa_put<BS / 2>(sh[0], t - d, v0);
+      soa_put<BS / 2>(sh[1], t - d, v1);
+      soa_put<BS / 2>(sh[2], t - d, v2);
+    }
+    __syncthreads();
+    if (t < d) {
+      v0 = fq_add(v0, soa_get<BS / 2, Fq>(sh[0], t));
+      v1 = fq_add(v1, soa_get<BS / 2, Fq>(sh[1], t));
+      v2 = fq_add(v2, soa_get<BS / 2, Fq>(sh[2], t));
+    }
+    __syncthreads();
+  }
+}
+// ---- fused layer rounds (ProductCircuitEvalProofBatched, product_tree.rs:271-396) -------------------------
+// One launch per round: element (c, i) of the nt x len domain first applies the previous round's pending
+// bound_poly_var_top to the four entries it reads of each of its triple's vectors (X[k] + r (X[k + 2 len] - X[k])
+// at k = i and i + len) and writes those two folded entries back, then evaluates the round. Every folded
+// entry is read and written by exactly one element, so any number of workgroups fold in place without a
+// grid barrier; only the eq vector C, shared by the product circuits (Triple.C == null), is read by every
+// circuit's element i and therefore ping-pongs between two buffers (cin -> cout, written by circuit 0).
+// One workgroup posts the round's (e0, e2, e3) directly; more add their partials through a ticket.
+__device__ __forceinline__ Fq fold_at(const Fq* __restrict__ p, int k, int fl, const Fq& r) {
+  const Fq lo = p[k];
+  return fq_add(lo, fq_mul(r, fq_sub(p[k + fl], lo)));
+}
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_round(const Triple* __restrict__ tr, const Fq* __restrict__ coeff, int nt,
+                                                    int log_len, int do_fold, Fq r, const Fq* __restrict__ cin,
+                                                    Fq* __restrict__ cout, Fq* __restrict__ partials,
+                                                    unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
+                                                    uint32_t seq, unsigned long long* probe) {
+  const int t = threadIdx.x, len = 1 << log_len;
+  unsigned long long* pr = probe ? probe + 8 * blockIdx.x : nullptr;  // phase timestamps (scripts/micro)
+  if (pr && t == 0) pr[0] = wall_clock64();
+  const long total = (long)nt << log_len;
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  for (long u = (long)blockIdx.x * BS + t; u < total; u += (long)gridDim.x * BS) {
+    const int c = (int)(u >> log_len), i = (int)(u & (len - 1));
+    const Triple x = tr[c];
+    const Fq k = coeff[c];
+    const Fq* Cp = x.C ? x.C : cin;
+    Fq al, ah, bl, bh, cl, ch;
+    if (do_fold) {
+      const int fl = 2 * len;
+      al = fold_at(x.A, i, fl, r);
+      ah = fold_at(x.A, i + len, fl, r);
+      bl = fold_at(x.B, i, fl, r);
+      bh = fold_at(x.B, i + len, fl, r);
+      cl = fold_at(Cp, i, fl, r);
+      ch = fold_at(Cp, i + len, fl, r);
+      x.A[i] = al;
+      x.A[i + len] = ah;
+      x.B[i] = bl;
+      x.B[i + len] = bh;
+      Fq* Cw = x.C ? x.C : (c == 0 ? cout : nullptr);
+      if (Cw) {
+        Cw[i] = cl;
+        Cw[i + len] = ch;
+      }
+    } else {
+      al = x.A[i];
+      ah = x.A[i + len];
+      bl = x.B[i];
+      bh = x.B[i + len];
+      cl = Cp[i];
+      ch = Cp[i + len];
+    }
+    // the coefficient scales the A factor (k A is linear in X)
+    al = fq_mul(k, al);
+    ah = fq_mul(k, ah);
+    const Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
+    const Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
+    e0 = fq_add(e0, fq_mul(fq_mul(al, bl), cl));
+    e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
+    e3 = fq_add(e3, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
+  }
+  if (pr && t == 0) pr[1] = wall_clock64();
+  block_sum3_t0<BS>(e0, e2, e3);
+  if (pr && t == 0) pr[2] = wall_clock64();
+  if (gridDim.x == 1) {
+    if (t == 0) {
+      const Fq rr[3] = {e0, e2, e3};
+      mbox_post(mb, seq, rr, 3);
+      if (pr) pr[3] = wall_clock64();
+    }
+    return;
+  }
+  __shared__ bool last;
+  if (t == 0) {
+    partials[3 * blockIdx.x] = e0;
+    partials[3 * blockIdx.x + 1] = e2;
+    partials[3 * blockIdx.x + 2] = e3;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  Fq a = fq_zero(), b = fq_zero(), cc = fq_zero();
+  for (unsigned j = t; j < gridDim.x; j += BS) {
+    a = fq_add(a, partials[3 * j]);
+    b = fq_add(b, partials[3 * j + 1]);
+    cc = fq_add(cc, partials[3 * j + 2]);
+  }
+  block_sum3_t0<BS>(a, b, cc);
+  if (t == 0) {
+    const Fq rr[3] = {a, b, cc};
+    mbox_post(mb, seq, rr, 3);
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// end of a layer: the last round's fold (length 2 -> 1) of every triple's vectors and the layer's final claims
+// A[0], B[0], C[0] per triple, written straight into the mailbox (3 nt scalars, then the sequence number)
+__global__ void __launch_bounds__(256) k_layer_close(const Triple* __restrict__ tr, int nt, Fq r,
+                                                     const Fq* __restrict__ cin, uint32_t* __restrict__ mb,
+                                                     uint32_t seq) {
+  for (int c = threadIdx.x; c < nt; c += 256) {
+    const Triple x = tr[c];
+    const Fq v[3] = {fold_at(x.A, 0, 1, r), fold_at(x.B, 0, 1, r), fold_at(x.C ? x.C : cin, 0, 1, r)};
+    for (int k = 0; k < 3; k++)
+      for (int i = 0; i < 8; i++)
+        __hip_atomic_store(mb + 8 + 8 * (3 * c + k) + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---- the same round with a quad (4 lanes) per element --------------------------------------------------
+// A wave issues one instruction at a time, so an element's ~14 field products cost ~14 product times even when
+// independent; spread over a quad they take 5: round 1 folds (lane 0: A lo/hi, 1: B, 2: C), the quad exchanges
+// the six values (DPP), then lane p in {0, 1, 2} forms the cubic at X = 0, 2, 3 as ((a_X b_X) c_X) k.
+// Lane 3 mirrors lane 0's work (SIMT) and is ignored. The sums meet by cross-quad shuffles inside the wave,
+// then across waves in LDS.
+template <int K>
+__device__ __forceinline__ Fq fq_qbcast(const Fq& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ Fq fq_shfl_xor(const Fq& a, int m) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__shfl_xor((int)a.l[i], m);
+  return r;
+}
+// value at X = 0, 2, 3 (p = 0, 1, 2) of the line through (0, lo), (1, hi)
+__device__ __forceinline__ Fq line_at(const Fq& lo, const Fq& hi, int p) {
+  const Fq d = fq_sub(hi, lo), x2 = fq_add(hi, d);
+  return p == 0 ? lo : (p == 1 ? x2 : fq_add(x2, d));
+}
+// sums of the values of lanes with equal (thread & 3) over a block of BS threads: quads of a wave by
+// cross-quad shuffles, then waves through LDS; the sum for q is left in thread q (q < 3)
+template <int BS>
+__device__ __forceinline__ void quad_block_sum(Fq& e) {
+  constexpr int NW = BS / 64;
+  __shared__ uint32_t wsum[NW > 1 ? NW : 1][3][8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int m = 4; m < 64; m <<= 1) e = fq_add(e, fq_shfl_xor(e, m));
+  if (NW > 1) {
+    if (lane < 3)
+      for (int j = 0; j < 8; j++) wsum[w][lane][j] = e.l[j];
+    __syncthreads();
+    if (w == 0 && lane < 3)
+      for (int v = 1; v < NW; v++) {
+        Fq o;
+        for (int j = 0; j < 8; j++) o.l[j] = wsum[v][lane][j];
+        e = fq_add(e, o);
+      }
+    __syncthreads();
+  }
+}
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
+                                                      int nt, int log_len, int do_fold, Fq r, const Fq* __restrict__ cin,
+                                                      Fq* __restrict__ cout, Fq* __restrict__ partials,
+                                                      unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
+                                                      uint32_t seq, unsigned long long* probe) {
+  __shared__ bool last;
+  const int t = threadIdx.x, q = t & 3, len = 1 << log_len;
+  const int pt = q < 3 ? q : 0;  // the evaluation point (and round-1 vector) this lane works on
+  unsigned long long* pr = probe ? probe + 8 * blockIdx.x : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
+  const long total = (long)nt << log_len;
+  Fq e = fq_zero();
+  for (long u = ((long)blockIdx.x * BS + t) >> 2; u < total; u += (long)gridDim.x * (BS / 4)) {
+    const int c = (int)(u >> log_len), i = (int)(u & (len - 1));
+    const Triple x = tr[c];
+    const Fq* Cp = x.C ? x.C : cin;
+    const Fq* src = pt == 0 ? x.A : (pt == 1 ? x.B : Cp);
+    Fq lo, hi;
+    if (do_fold) {
+      const int fl = 2 * len;
+      lo = fold_at(src, i, fl, r);
+      hi = fold_at(src, i + len, fl, r);
+      Fq* dst = q == 0 ? x.A : (q == 1 ? x.B : (q == 2 ? (x.C ? x.C : (c == 0 ? cout : nullptr)) : nullptr));
+      if (dst) {
+        dst[i] = lo;
+        dst[i + len] = hi;
+      }
+    } else {
+      lo = src[i];
+      hi = src[i + len];
+    }
+    const Fq al = fq_qbcast<0>(lo), ah = fq_qbcast<0>(hi), bl = fq_qbcast<1>(lo), bh = fq_qbcast<1>(hi);
+    const Fq cl = fq_qbcast<2>(lo), ch = fq_qbcast<2>(hi);
+    const Fq k = coeff[c];
+    e = fq_add(e, fq_mul(fq_mul(fq_mul(line_at(al, ah, pt), line_at(bl, bh, pt)), line_at(cl, ch, pt)), k));
+  }
+  if (pr && t == 0) pr[1] = wall_clock64();
+  quad_block_sum<BS>(e);
+  if (pr && t == 0) pr[2] = wall_clock64();
+  if (gridDim.x == 1) {  // lanes 0..2 of wave 0 post e0, e2, e3, then lane 0 the sequence number
+    if (t < 3) {
+      for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+    if (t == 0) {
+      __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (pr) pr[3] = wall_clock64();
+    }
+    return;
+  }
+  // cross-workgroup hand-off without L2 write-back (the in-place folds leave many dirty lines, which an agent
+  // release would flush): the partials go out as sc1 stores (agent-scope relaxed atomics), the storing wave
+  // waits for them, then one lane adds to the ticket; the last workgroup reads them with sc1 loads
+  // (MI355X_MICROARCH hand-off table, row 1)
+  if (t < 3)
+    for (int j = 0; j < 8; j++)
+      __hip_atomic_store(&partials[3 * blockIdx.x + t].l[j], e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  // the last workgroup: thread 4 m + p (p < 3) adds point p's partials of blocks m, m + BS / 4, ...
+  Fq a = fq_zero();
+  if (q < 3)
+    for (unsigned j = t >> 2; j < gridDim.x; j += BS / 4) {
+      Fq o;
+      for (int k = 0; k < 8; k++)
+        o.l[k] = __hip_atomic_load(&partials[3 * j + q].l[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a = fq_add(a, o);
+    }
+  quad_block_sum<BS>(a);
+  if (t < 3) {
+    for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  if (t == 0) {
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+}  // namespace spg

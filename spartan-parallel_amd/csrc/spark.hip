@@ -22,6 +22,7 @@
 
 #include "hostpoly.hpp"
 #include "proto.hpp"
+#include "layer.hpp"
 #include "lds.hpp"
 #include "sumcheck.hpp"
 
@@ -84,58 +85,6 @@ __global__ void k_tops(const Fq* __restrict__ tree, size_t nc, size_t stride, si
   if (c < nc) out[c] = fq_mul(tree[c * stride + off], tree[c * stride + off + 1]);
 }
 
-struct Triple {
-  Fq *A, *B, *C;
-};
-__device__ __forceinline__ void block_sum3_sp(Fq& v0, Fq& v1, Fq& v2) {
-  __shared__ uint32_t sh[3][soa_words<Fq, 256>()];  // component-major: no bank conflicts
-  int t = threadIdx.x;
-  for (int d = 128; d >= 1; d >>= 1) {
-    if (t >= d && t < 2 * d) {
-      soa_put<256>(sh[0], t - d, v0);
-      soa_put<256>(sh[1], t - d, v1);
-      soa_put<256>(sh[2], t - d, v2);
-    }
-    __syncthreads();
-    if (t < d) {
-      v0 = fq_add(v0, soa_get<256, Fq>(sh[0], t));
-      v1 = fq_add(v1, soa_get<256, Fq>(sh[1], t));
-      v2 = fq_add(v2, soa_get<256, Fq>(sh[2], t));
-    }
-    __syncthreads();
-  }
-  // broadcast thread 0's sums
-  if (t == 0) {
-    soa_put<256>(sh[0], 0, v0);
-    soa_put<256>(sh[1], 0, v1);
-    soa_put<256>(sh[2], 0, v2);
-  }
-  __syncthreads();
-  v0 = soa_get<256, Fq>(sh[0], 0);
-  v1 = soa_get<256, Fq>(sh[1], 0);
-  v2 = soa_get<256, Fq>(sh[2], 0);
-  __syncthreads();
-}
-// block-wide sums of three Fq values over BS threads; the result is valid in thread 0
-template <int BS>
-__device__ __forceinline__ void block_sum3_t0(Fq& v0, Fq& v1, Fq& v2) {
-  __shared__ uint32_t sh[3][soa_words<Fq, BS / 2>()];
-  const int t = threadIdx.x;
-  for (int d = BS / 2; d >= 1; d >>= 1) {
-    if (t >= d && t < 2 * d) {
-      soa_put<BS / 2>(sh[0], t - d, v0);
-      soa_put<BS / 2>(sh[1], t - d, v1);
-      soa_put<BS / 2>(sh[2], t - d, v2);
-    }
-    __syncthreads();
-    if (t < d) {
-      v0 = fq_add(v0, soa_get<BS / 2, Fq>(sh[0], t));
-      v1 = fq_add(v1, soa_get<BS / 2, Fq>(sh[1], t));
-      v2 = fq_add(v2, soa_get<BS / 2, Fq>(sh[2], t));
-    }
-    __syncthreads();
-  }
-}
 // A whole round of a small layer in one workgroup of 1024 threads (nt * len up to a few thousand): first the previous
 // round's bound_poly_var_top of every layer vector (when do_fold; vectors of 2 flen -> flen, one pass,
 // __syncthreads), then the round's (e0, e2, e3) with each triple's coefficient applied per element, a block
@@ -315,7 +264,7 @@ static const size_t kHostFinalRows = 64;  // latency-path commits of at most thi
 enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
-  kWsTops, kWsCommitBk
+  kWsTops, kWsCommitBk, kWsC2
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -465,11 +414,171 @@ struct BatchedProofP {  // ProductCircuitEvalProofBatched
   }
 };
 
+// workgroups and block size of a fused layer round over W = nt * len elements: one workgroup up to kOneWgMax
+// elements (no ticket), else about kEltPerThread elements per thread over 256-thread workgroups
+static void layer_grid(size_t W, unsigned* K, int* BS) {
+  static const size_t one_wg = getenv("SPG_LAYER_ONEWG") ? (size_t)atoi(getenv("SPG_LAYER_ONEWG")) : 512;
+  static const size_t ept = getenv("SPG_LAYER_EPT") ? (size_t)std::max(1, atoi(getenv("SPG_LAYER_EPT"))) : 2;
+  if (W <= 64) {
+    *K = 1;
+    *BS = 64;
+  } else if (W <= one_wg) {
+    *K = 1;
+    *BS = 256;
+  } else {
+    *BS = 256;
+    *K = (unsigned)std::min<size_t>((W + 256 * ept - 1) / (256 * ept), 2048);
+  }
+}
+
+// ProductCircuitEvalProofBatched::prove with fused layer rounds (k_layer_round / k_layer_close above); same
+// transcript and proof as batched_prove below
+static int batched_prove_fused(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims, const std::vector<Triple>& dotp,
+                               const FqV& dotp_claims, Tr& t, BatchedProofP* out, FqV* rand_out) {
+  hipStream_t s = ctx->stream;
+  const size_t L = lg2(M), stride = 2 * M;
+  auto off = [&](size_t k) { return 2 * M - 2 * (M >> k); };
+  const size_t nt_max = nc + dotp.size();
+  if (3 * nt_max + 1 > kMboxScalars) return set_err(ctx, SPG_E_ARG, "batched_prove: too many circuits for the mailbox");
+  Fq* cbuf[2] = {(Fq*)ws_get(ctx, kWsC, (M / 2) * sizeof(Fq) + 64), (Fq*)ws_get(ctx, kWsC2, (M / 2) * sizeof(Fq) + 64)};
+  // triples, then their coefficients, in one buffer (one upload per layer)
+  const size_t tr_bytes = (nt_max * sizeof(Triple) + 63) & ~(size_t)63;
+  uint8_t* ddesc = (uint8_t*)ws_get(ctx, kWsTriples, tr_bytes + nt_max * sizeof(Fq) + 64);
+  Fq* part = (Fq*)ws_get(ctx, kWsPart, 3 * 2048 * sizeof(Fq) + 64);  // K <= 2048 workgroups per round
+  if (!cbuf[0] || !cbuf[1] || !ddesc || !part) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
+  const Triple* dtr = (const Triple*)ddesc;
+  const Fq* dcoef = (const Fq*)(ddesc + tr_bytes);
+  FqV rand;
+  Laps lp;
+  lp.title = "ProductCircuitEvalProofBatched::prove";
+  for (size_t layer = L; layer-- > 0;) {
+    const size_t half = M >> (layer + 1);  // |left| = |right| = |C|
+    const size_t rounds = lg2(half);
+    int cur = 0;  // the buffer holding the shared eq vector C
+    int rc = eq_table(ctx, rand, cbuf[0]);
+    if (rc) return rc;
+    const bool with_dotp = layer == 0 && !dotp.empty();
+    std::vector<Triple> tr;
+    for (size_t c = 0; c < nc; c++) {
+      Fq* v = tree + c * stride + off(layer);
+      tr.push_back({v, v + half, nullptr});  // C: the shared eq vector
+    }
+    if (with_dotp) {
+      claims.insert(claims.end(), dotp_claims.begin(), dotp_claims.end());
+      for (auto& d : dotp) tr.push_back(d);
+    }
+    FqV coeffs = t.challenges("rand_coeffs_next_layer", claims.size());
+    Fq e = fq_zero();
+    for (size_t i = 0; i < claims.size(); i++) e = fq_add(e, fq_mul(claims[i], coeffs[i]));
+    {  // descriptors up through page-locked staging; free again here (the previous layer ended with a mailbox wait
+       // after its last launch)
+      uint8_t* st = (uint8_t*)pinned_get(ctx, tr_bytes + coeffs.size() * sizeof(Fq) + 64);
+      if (!st) return set_err(ctx, SPG_E_NOMEM, "layer staging");
+      memcpy(st, tr.data(), tr.size() * sizeof(Triple));
+      memcpy(st + tr_bytes, coeffs.data(), coeffs.size() * sizeof(Fq));
+      SPG_HIP(ctx, hipMemcpyAsync(ddesc, st, tr_bytes + coeffs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
+    }
+    lp.lap("layer_setup");
+    LayerProofP lpf;
+    FqV r_prod;
+    size_t log_len = rounds;
+    bool pending = false;  // a bound_poly_var_top with r_pend not yet applied
+    Fq r_pend = fq_zero();
+    for (size_t j = 0; j < rounds; j++) {
+      log_len--;
+      const size_t len = (size_t)1 << log_len;
+      unsigned K;
+      int BS;
+      static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
+      if (quad) {  // a quad per element, about one element per quad
+        const size_t W = tr.size() * len;
+        BS = W <= 16 ? 64 : 256;
+        K = (unsigned)std::min<size_t>((W * 4 + BS - 1) / BS, 2048);
+      } else {
+        layer_grid(tr.size() * len, &K, &BS);
+      }
+      {
+        KScope ks(ctx, "spark_layer_round", 192.0 * tr.size() * len * (pending ? 2.0 : 1.0));
+        const int nt = (int)tr.size(), lg = (int)log_len, df = pending ? 1 : 0;
+        const uint32_t seq = ++ctx->mbox_seq;
+        if (quad && BS == 64)
+          hipLaunchKernelGGL(k_layer_round_q<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+        else if (quad)
+          hipLaunchKernelGGL(k_layer_round_q<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+        else if (BS == 64)
+          hipLaunchKernelGGL(k_layer_round<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+        else
+          hipLaunchKernelGGL(k_layer_round<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+      }
+      if (pending) cur ^= 1;
+      SPG_HIP(ctx, hipGetLastError());
+      Fq ev[3];
+      rc = eval_reduce_finish(ctx, ev);
+      if (rc) return rc;
+      lp.lap("round_eval_wait");
+      Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
+      FqV poly = uni_from_evals3(evals);
+      append_unipoly(t, poly);
+      Fq r_j = t.challenge("challenge_nextround");
+      r_prod.push_back(r_j);
+      pending = true;
+      r_pend = r_j;
+      e = uni_eval(poly, r_j);
+      lpf.polys.push_back({poly[0], poly[2], poly[3]});
+      lp.lap("round_host");
+    }
+    // the last round's fold and the final claims A[0], B[0] (C[0] for the dot-product circuits), by mailbox
+    FqV fin(3 * tr.size());
+    {
+      KScope ks(ctx, "spark_layer_close");
+      const uint32_t seq = ++ctx->mbox_seq;
+      hipLaunchKernelGGL(k_layer_close, dim3(1), dim3(256), 0, s, dtr, (int)tr.size(), r_pend, cbuf[cur], ctx->d_mbox,
+                         seq);
+      SPG_HIP(ctx, hipGetLastError());
+      rc = mbox_wait(ctx, seq, fin.data(), (int)fin.size());
+      if (rc) return rc;
+    }
+    for (size_t c = 0; c < nc; c++) {
+      lpf.left.push_back(fin[3 * c]);
+      lpf.right.push_back(fin[3 * c + 1]);
+    }
+    for (size_t c = 0; c < nc; c++) {
+      t.scalar("claim_prod_left", lpf.left[c]);
+      t.scalar("claim_prod_right", lpf.right[c]);
+    }
+    if (with_dotp) {
+      for (size_t k = 0; k < dotp.size(); k++)
+        for (int i = 0; i < 3; i++) out->dotp[i].push_back(fin[3 * (nc + k) + i]);
+      for (size_t k = 0; k < dotp.size(); k++) {
+        t.scalar("claim_dotp_left", out->dotp[0][k]);
+        t.scalar("claim_dotp_right", out->dotp[1][k]);
+        t.scalar("claim_dotp_weight", out->dotp[2][k]);
+      }
+    }
+    Fq r_layer = t.challenge("challenge_r_layer");
+    claims.assign(nc, fq_zero());
+    for (size_t c = 0; c < nc; c++) claims[c] = fq_add(lpf.left[c], fq_mul(r_layer, fq_sub(lpf.right[c], lpf.left[c])));
+    rand.assign(1, r_layer);
+    rand.insert(rand.end(), r_prod.begin(), r_prod.end());
+    out->layers.push_back(std::move(lpf));
+    lp.lap("layer_finals");
+  }
+  lp.print();
+  *rand_out = rand;
+  return 0;
+}
+
 // ProductCircuitEvalProofBatched::prove (product_tree.rs:271-396) over the nc product circuits of `tree`
 // (M leaves each, claims = their ProductCircuit::evaluate) and, at layer 0, the dot-product circuits
 // `dotp` (three device vectors of M/2 entries each, folded in place) with claims `dotp_claims`.
 static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims, const std::vector<Triple>& dotp,
                          const FqV& dotp_claims, Tr& t, BatchedProofP* out, FqV* rand_out) {
+  static const bool fused = !getenv("SPG_LAYER_FUSED") || atoi(getenv("SPG_LAYER_FUSED")) != 0;
+  if (fused) return batched_prove_fused(ctx, tree, nc, M, claims, dotp, dotp_claims, t, out, rand_out);
   hipStream_t s = ctx->stream;
   const size_t L = lg2(M), stride = 2 * M;
   auto off = [&](size_t k) { return 2 * M - 2 * (M >> k); };
