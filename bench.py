@@ -16,7 +16,7 @@ torch.distributed.run, one rank per GPU.
 
 `roofline` is computed for the kernel with the largest device time among those with an algorithmic byte
 model (libspg's per-launch HIP-event timing on its context stream, spg_prof_read, taken in a separate pass
-after the timed steps); `traffic` comes from the committed PMC summary (profiles/r01_pmc_traffic.json).
+after the timed steps); `traffic` comes from the committed PMC summary (profiles/r02_pmc_traffic.json).
 `cpu_baseline` is the C++ CPU restatement of the reference (oracle/, 1 thread) on rank 0 at N = 1.
 """
 import argparse
@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--log-proofs", type=int, default=9, help="snark: 2^k executions per block")
     ap.add_argument("--log-nnz", type=int, default=24, help="spark: 2^k nonzeros per matrix (x3 matrices)")
     ap.add_argument("--cpu-log-nnz", type=int, default=15, help="spark: CPU baseline sample size")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 --pmc (scripts/pmc_traffic.py), if present")
     return ap.parse_args()
 
