@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="r1cs_2e20", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "shard"])
+    ap.add_argument("--mode", default=None, choices=["replicas", "shard"],
+                    help="N > 1: replicas (independent proofs per rank) or shard (one proof split over the ranks); "
+                         "default: shard for --workload spark / msm, replicas otherwise")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--log-msm", type=int, default=16, help="msm: 2^k (scalar, generator) pairs")
     ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark", "msm"],
@@ -89,7 +91,7 @@ def main():
     import workload
 
     nc, npf, nws = CONFIGS[a.config]
-    shard = a.mode == "shard" and world > 1
+    shard = (a.mode or "replicas") == "shard" and world > 1
     ctx = spg.Context(gpu)
     if shard:
         nc, npf = nc * world, npf * world  # one proof over world x the per-GPU instances
@@ -462,18 +464,22 @@ def main_spark(a):
     2^k-nonzero matrices (A, B, C) with num_vars_x = num_vars_y = k. A step is one multi_evaluate at (rx, ry)
     plus one full SPARK evaluation proof (derefs, derefs commit, hash layer, product trees, batched layer
     sumchecks, hash-layer PolyEvalProofs) with the dense representation resident in HBM (multi_commit is the
-    preprocessing step, SNARK::encode, and is timed separately). Multi-GPU: independent replicas."""
+    preprocessing step, SNARK::encode, and is timed separately). Multi-GPU (default --mode shard): ONE proof split
+    over the ranks (spg_set_comm; SURVEY 8e: Hyrax rows, interleaved product trees, per-round (e0, e2, e3)
+    allgathers over RCCL) -> strong scaling; --mode replicas: an independent proof per rank (weak)."""
     import numpy as np
     import torch
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = a.backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    shard = world > 1 and (a.mode or "shard") == "shard"
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group(a.backend or ("nccl" if torch.cuda.is_available() else "gloo"))
+        dist.init_process_group(backend)
     ndev = torch.cuda.device_count()
     gpu = local % ndev if ndev else local
     if torch.cuda.is_available():
@@ -483,11 +489,13 @@ def main_spark(a):
 
     k = a.log_nnz
     ctx = spg.Context(gpu)
+    if shard:
+        ctx.set_comm(rank, world, spg.torch_allgather(dist, device=f"cuda:{gpu}" if backend == "nccl" else "cpu"))
     t0 = time.perf_counter()
     wl = workload.SparkWorkload(k)
     views = workload.CViews(wl)
     t_gen = time.perf_counter() - t0
-    rng = np.random.default_rng(3 + rank)
+    rng = np.random.default_rng(3 + (0 if shard else rank))
     r = rng.integers(0, 1 << 63, size=(2 * k, 4), dtype=np.uint64)
     r[:, 3] &= np.uint64((1 << 60) - 1)
     rx, ry = r[:k], r[k:]
@@ -517,13 +525,18 @@ def main_spark(a):
     sync()
     dt = time.perf_counter() - t0
     prof = profile_pass(ctx, step, a.steps)
+    same = None
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+        if shard:  # every rank of one sharded proof must hold the same bytes
+            hs = [None] * world
+            dist.all_gather_object(hs, sorted(proofs))
+            same = all(h == hs[0] for h in hs)
     assert len(proofs) == 1, "proof bytes changed between steps"
     nnz = 3 * wl.nnz
-    value = nnz * world * a.steps / dt
+    value = nnz * (1 if shard else world) * a.steps / dt
     top = sorted(prof.items(), key=lambda kv: -kv[1][1])[:10]
     kernels = {n: {"launches_per_step": v[0] / a.steps, "ms_per_step": round(v[1] / a.steps / 1e3, 3),
                    "GBps": round(v[2] / (v[1] * 1e-6) / 1e9, 1) if v[2] else None} for n, v in top}
@@ -546,13 +559,15 @@ def main_spark(a):
         print(json.dumps({
             "metric": "SPARK nonzeros/sec (sparse_mlpoly multi_evaluate + SparseMatPolyEvalProof::prove)",
             "value": round(value, 1), "unit": "nonzeros/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None, "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255",
             "data": "synthetic (SURVEY 8d config 5 generator, seed 5)",
             "config": {"workload": "SparseMatPolyEvalProof::prove, batch 3 (src/sparse_mlpoly.rs:1497-1564)",
-                       "log_nnz": k, "num_vars_x": k, "num_vars_y": k, "parallelism": f"replicas x{world}"},
+                       "log_nnz": k, "num_vars_x": k, "num_vars_y": k,
+                       "parallelism": f"one proof sharded x{world} ({backend})" if shard else f"replicas x{world}"},
             "roofline": roofline_of(prof, None), "cpu_baseline": cpu, "proof_sha256": sorted(proofs)[0][:16],
-            "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
+            "ranks_agree": same, "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
             "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
             "kernels": kernels}))
     if dist is not None:

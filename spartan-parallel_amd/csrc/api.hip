@@ -185,6 +185,49 @@ extern "C" int spg_set_comm(spg_ctx* c, int rank, int nranks, spg_allgather_fn f
   return SPG_OK;
 }
 
+namespace spg {
+
+int comm_allgather(spg_ctx* c, const Shard& sh, int status, const void* send, size_t bytes, std::vector<uint8_t>& recv) {
+  if (sh.n == 1) {
+    recv.assign((const uint8_t*)send, (const uint8_t*)send + bytes);
+    return status;
+  }
+  if (!c->allgather) return set_err(c, SPG_E_ARG, "no communicator set (spg_set_comm)");
+  // [status (8 bytes) | payload] per rank
+  const size_t rec = 8 + bytes;
+  std::vector<uint8_t> mine(rec, 0), all(rec * sh.n);
+  int64_t st = status;
+  memcpy(mine.data(), &st, 8);
+  if (bytes) memcpy(mine.data() + 8, send, bytes);
+  if (c->allgather(c->comm_user, mine.data(), rec, all.data()) != 0)
+    return set_err(c, SPG_E_HIP, "allgather callback failed");
+  recv.resize(bytes * sh.n);
+  int first = status;
+  for (int q = 0; q < sh.n; q++) {
+    int64_t s;
+    memcpy(&s, all.data() + q * rec, 8);
+    if (!first && s) first = set_err(c, (int)s, "a peer rank failed (status " + std::to_string(s) + ")");
+    if (bytes) memcpy(recv.data() + q * bytes, all.data() + q * rec + 8, bytes);
+  }
+  return first;
+}
+
+int comm_sum_fq(spg_ctx* c, const Shard& sh, int status, Fq* v, size_t n) {
+  if (sh.n == 1) return status;
+  std::vector<uint8_t> r;
+  int rc = comm_allgather(c, sh, status, v, n * sizeof(Fq), r);
+  if (rc) return rc;
+  const Fq* a = (const Fq*)r.data();
+  for (size_t i = 0; i < n; i++) {
+    Fq acc = a[i];
+    for (int q = 1; q < sh.n; q++) acc = fq_add(acc, a[q * n + i]);
+    v[i] = acc;
+  }
+  return 0;
+}
+
+}  // namespace spg
+
 extern "C" int spg_prof_enable(spg_ctx* c, int on) {
   if (!c) return SPG_E_ARG;
   c->prof_on = on != 0;

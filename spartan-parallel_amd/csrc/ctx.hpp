@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -140,6 +141,24 @@ __device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* 
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+// ---- multi-process collectives (spg_set_comm) -----------------------------------------------------------
+// One shard of an SPMD call: rank `rank` of `n` processes (n == 1: this process alone, no communication).
+struct Shard {
+  int rank = 0, n = 1;
+};
+inline Shard ctx_shard(const spg_ctx* c) { return Shard{c->rank, c->nranks}; }
+// balanced split of [0, n) into `parts`: part r is [shard_begin(n, parts, r), shard_begin(n, parts, r + 1)),
+// the first n % parts parts one longer
+inline size_t shard_begin(size_t n, int parts, int r) {
+  return (size_t)r * (n / (size_t)parts) + std::min((size_t)r, n % (size_t)parts);
+}
+// allgather through the context's callback, carrying every rank's status: recv holds rank 0's `bytes`, then
+// rank 1's, ...; returns 0 only when every rank's status is 0 (a failure on any rank fails all of them alike,
+// so no rank is left blocked in a later collective). sh.n == 1: a local copy.
+int comm_allgather(spg_ctx* c, const Shard& sh, int status, const void* send, size_t bytes, std::vector<uint8_t>& recv);
+// v[0..n) summed mod q over the ranks (in place), with the same status rule
+int comm_sum_fq(spg_ctx* c, const Shard& sh, int status, Fq* v, size_t n);
 
 // per-kernel profiling scope (no-op unless spg_prof_enable(ctx, 1))
 struct KScope {

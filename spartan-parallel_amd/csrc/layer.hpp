@@ -164,13 +164,16 @@ __global__ void __launch_bounds__(BS) k_layer_round(const Triple* __restrict__ t
   }
 }
 // end of a layer: the last round's fold (length 2 -> 1) of every triple's vectors and the layer's final claims
-// A[0], B[0], C[0] per triple, written straight into the mailbox (3 nt scalars, then the sequence number)
-__global__ void __launch_bounds__(256) k_layer_close(const Triple* __restrict__ tr, int nt, Fq r,
+// A[0], B[0], C[0] per triple, written straight into the mailbox (3 nt scalars, then the sequence number).
+// do_fold == 0 posts the entries as they are (a sharded layer whose local vectors already have length 1).
+__global__ void __launch_bounds__(256) k_layer_close(const Triple* __restrict__ tr, int nt, int do_fold, Fq r,
                                                      const Fq* __restrict__ cin, uint32_t* __restrict__ mb,
                                                      uint32_t seq) {
   for (int c = threadIdx.x; c < nt; c += 256) {
     const Triple x = tr[c];
-    const Fq v[3] = {fold_at(x.A, 0, 1, r), fold_at(x.B, 0, 1, r), fold_at(x.C ? x.C : cin, 0, 1, r)};
+    const Fq* Cp = x.C ? x.C : cin;
+    const Fq v[3] = {do_fold ? fold_at(x.A, 0, 1, r) : x.A[0], do_fold ? fold_at(x.B, 0, 1, r) : x.B[0],
+                     do_fold ? fold_at(Cp, 0, 1, r) : Cp[0]};
     for (int k = 0; k < 3; k++)
       for (int i = 0; i < 8; i++)
         __hip_atomic_store(mb + 8 + 8 * (3 * c + k) + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -850,7 +850,10 @@ static void dispatch_digits_rows(int c, const MsmArgs& a, hipStream_t s) {
     case 10: hipLaunchKernelGGL(k_digits_rows<10>, g, t, 0, s, a); break;
     case 11: hipLaunchKernelGGL(k_digits_rows<11>, g, t, 0, s, a); break;
     case 12: hipLaunchKernelGGL(k_digits_rows<12>, g, t, 0, s, a); break;
-    default: hipLaunchKernelGGL(k_digits_rows<13>, g, t, 0, s, a); break;
+    case 13: hipLaunchKernelGGL(k_digits_rows<13>, g, t, 0, s, a); break;
+    case 14: hipLaunchKernelGGL(k_digits_rows<14>, g, t, 0, s, a); break;
+    case 15: hipLaunchKernelGGL(k_digits_rows<15>, g, t, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_digits_rows<16>, g, t, 0, s, a); break;
   }
 }
 
@@ -885,8 +888,10 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   if (!hist || !off || !cursor || !items || !item_off || !entries || !item_key || !partial || !segT || !segS)
     return set_err(ctx, SPG_E_NOMEM, "msm workspace allocation failed");
 
-  // many MSMs of moderate length: one workgroup per MSM sorts its digits in LDS (k_digits_rows)
-  const bool rows = B >= 64 && c <= 13;
+  // many MSMs: one workgroup per MSM sorts its digits in LDS (k_digits_rows; up to 2^15 bucket counters,
+  // 128 KiB of the 160 KiB LDS, at c = 16)
+  static const int rows_cmax = getenv("SPG_ROWS_CMAX") ? atoi(getenv("SPG_ROWS_CMAX")) : 16;
+  const bool rows = B >= 64 && c <= rows_cmax;
   if (rows) {
     SPG_HIP(ctx, hipMemsetAsync(hist + nkeys, 0, 4, s));
   } else {

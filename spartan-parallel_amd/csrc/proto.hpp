@@ -138,15 +138,19 @@ int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars,
 // ---- Hyrax commitments / PolyEvalProof on device polynomials (spark.hip) ----
 // PolyCommitmentGens::new(nv, label) as a view of a derived generator stream
 ProverGens gens_view(spg_gens* dev, size_t nv);
-// DensePolynomial::commit (no blinds) of 2^nv device scalars; rows of 2^(nv - nv/2) <= g.n_pc scalars
-int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out);
+// DensePolynomial::commit (no blinds) of 2^nv device scalars; rows of 2^(nv - nv/2) <= g.n_pc scalars. With
+// sh.n > 1 an SPMD collective: rank r commits its balanced share of the rows, the encodings are allgathered.
+int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out, const Shard& sh = Shard());
 // L rows of R consecutive device scalars -> L row commitments (host)
 int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out);
+// the same split over the ranks of sh (every rank returns all L commitments)
+int commit_rows_sh(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out, const Shard& sh);
 // PolyCommitment::append_to_transcript
 void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c);
 // PolyEvalProof::prove (no blinds) of a device polynomial of 2^|r| scalars
+// (sh.n > 1: the L.Z rows are split over the ranks and the partial vectors summed; the Bullet rounds are replicated)
 int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, const Fq& Zr, Tr& t, Tape& tape,
-                    DotProductProofLogP* out);
+                    DotProductProofLogP* out, const Shard& sh = Shard());
 
 // ---- SPARK (spark.hip) ----
 struct SparsePoly {
@@ -155,10 +159,13 @@ struct SparsePoly {
 };
 int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_t nvx, size_t nvy,
                        const uint8_t* label, size_t label_len, size_t gens_nvx, size_t gens_nvy, size_t gens_nnz,
-                       size_t gens_batch, spg_spark** out);
+                       size_t gens_batch, spg_spark** out, const Shard& sh = Shard());
 void spark_comm_ser(const spg_spark* S, Writer& w);
 void spark_comm_append(const spg_spark* S, Tr& t);
-int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w);
+// sh.n > 1: one proof as an SPMD collective over the ranks of sh (every rank holds the whole dense representation
+// and returns the same bytes); see spark.hip "sharded proof"
+int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w,
+                     const Shard& sh = Shard());
 
 // ---- R1CS witness from parts (r1cs.hip) ----
 struct WPart {  // one ProverWitnessSecInfo: per instance (num_proofs x num_inputs) scalars at src (host or device)

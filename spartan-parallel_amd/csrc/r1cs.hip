@@ -193,14 +193,15 @@ __device__ __forceinline__ Fq block_sum1(Fq v) {
   __syncthreads();
   return r;
 }
-__global__ void __launch_bounds__(256) k_sparse_eval(const MatDesc* __restrict__ md, const uint32_t* __restrict__ nrows,
+__global__ void __launch_bounds__(256) k_sparse_eval(const MatDesc* __restrict__ md, const uint32_t* __restrict__ rows,
                                                      const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
                                                      const Fq* __restrict__ val, const Fq* __restrict__ eq_rx,
                                                      const Fq* __restrict__ eq_ry, Fq* __restrict__ partials) {
+  // rows[2p], rows[2p + 1]: the row range [r0, r1) of instance p evaluated here (a rank's share when sharded)
   const int seg = blockIdx.y, p = seg / 3, m = seg % 3;
-  const uint32_t row = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t row = rows[2 * p] + blockIdx.x * 256 + threadIdx.x;
   Fq acc = fq_zero();
-  if (row < nrows[p]) {
+  if (row < rows[2 * p + 1]) {
     const uint32_t* rp = rowptr + md[p].rp[m];
     Fq sr = fq_zero();
     for (uint32_t e = rp[row]; e < rp[row + 1]; e++) sr = fq_add(sr, fq_mul(val[e], eq_ry[col[e]]));
@@ -1388,40 +1389,47 @@ extern "C" int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, 
     return set_err(ctx, SPG_E_ARG, "multi_evaluate: rx / ry shorter than the matrix dimensions");
   hipStream_t s = ctx->stream;
   const size_t Pm = inst->num_instances;
+  // sharded over the ranks of spg_set_comm: every matrix's rows split (balanced), the 3 Pm partial sums added
+  const Shard sh = ctx_shard(ctx);
   FqV vx(rx_len), vy(ry_len);
   for (size_t i = 0; i < rx_len; i++) vx[i] = ld_fq(rx + 4 * i);
   for (size_t i = 0; i < ry_len; i++) vy[i] = ld_fq(ry + 4 * i);
   Fq* erx = (Fq*)ws_get(ctx, WS_EV_RX, (sizeof(Fq) << rx_len) + 64);
   Fq* ery = (Fq*)ws_get(ctx, WS_EV_RY, (sizeof(Fq) << ry_len) + 64);
-  size_t maxrows = 0;
-  for (size_t p = 0; p < Pm; p++) maxrows = std::max(maxrows, inst->num_cons[p]);
-  const unsigned nblk = blocks_for(maxrows);
-  Fq* part = (Fq*)ws_get(ctx, WS_EV_PART, 3 * Pm * nblk * sizeof(Fq) + 64);
-  Fq* dout = (Fq*)ws_get(ctx, WS_EV_OUT, 3 * Pm * sizeof(Fq) + 64);
-  uint8_t* ddesc = (uint8_t*)ws_get(ctx, WS_EV_DESC, Pm * (sizeof(MatDesc) + 4) + 64);
-  if (!erx || !ery || !part || !dout || !ddesc) return set_err(ctx, SPG_E_NOMEM, "multi_evaluate");
   std::vector<MatDesc> md(Pm);
-  std::vector<uint32_t> nr(Pm);
-  double visits = 0;
+  std::vector<uint32_t> rr(2 * Pm);
+  size_t maxrows = 1;
+  double visits = 0, rows = 0;
   for (size_t p = 0; p < Pm; p++) {
     for (int m = 0; m < 3; m++) md[p].rp[m] = inst->rp_off[3 * p + m];
     md[p].cp = inst->cp_off[p];
-    nr[p] = (uint32_t)inst->num_cons[p];
-    visits += inst->nnz[3 * p] + inst->nnz[3 * p + 1] + inst->nnz[3 * p + 2];
+    rr[2 * p] = (uint32_t)shard_begin(inst->num_cons[p], sh.n, sh.rank);
+    rr[2 * p + 1] = (uint32_t)shard_begin(inst->num_cons[p], sh.n, sh.rank + 1);
+    maxrows = std::max<size_t>(maxrows, rr[2 * p + 1] - rr[2 * p]);
+    const double frac = (double)(rr[2 * p + 1] - rr[2 * p]) / (double)std::max<size_t>(1, inst->num_cons[p]);
+    visits += frac * (inst->nnz[3 * p] + inst->nnz[3 * p + 1] + inst->nnz[3 * p + 2]);
+    rows += 3.0 * (rr[2 * p + 1] - rr[2 * p]);
+  }
+  const unsigned nblk = blocks_for(maxrows);
+  Fq* part = (Fq*)ws_get(ctx, WS_EV_PART, 3 * Pm * nblk * sizeof(Fq) + 64);
+  Fq* dout = (Fq*)ws_get(ctx, WS_EV_OUT, 3 * Pm * sizeof(Fq) + 64);
+  uint8_t* ddesc = (uint8_t*)ws_get(ctx, WS_EV_DESC, Pm * (sizeof(MatDesc) + 8) + 64);
+  if (!erx || !ery || !part || !dout || !ddesc) {
+    int rc = set_err(ctx, SPG_E_NOMEM, "multi_evaluate");
+    FqV none(3 * Pm);
+    return comm_sum_fq(ctx, sh, rc, none.data(), 3 * Pm);
   }
   MatDesc* dmd = (MatDesc*)ddesc;
-  uint32_t* dnr = (uint32_t*)(ddesc + Pm * sizeof(MatDesc));
+  uint32_t* drr = (uint32_t*)(ddesc + Pm * sizeof(MatDesc));
   SPG_HIP(ctx, hipMemcpyAsync(dmd, md.data(), Pm * sizeof(MatDesc), hipMemcpyHostToDevice, s));
-  SPG_HIP(ctx, hipMemcpyAsync(dnr, nr.data(), Pm * 4, hipMemcpyHostToDevice, s));
+  SPG_HIP(ctx, hipMemcpyAsync(drr, rr.data(), 2 * Pm * 4, hipMemcpyHostToDevice, s));
   timer_start(ctx);
   int rc = eq_table(ctx, vx, erx);
   if (!rc) rc = eq_table(ctx, vy, ery);
   if (rc) return rc;
   {
-    double rows = 0;
-    for (size_t p = 0; p < Pm; p++) rows += 3.0 * inst->num_cons[p];
     KScope ks(ctx, "sparse_eval", 68.0 * visits + 40.0 * rows);
-    hipLaunchKernelGGL(k_sparse_eval, dim3(nblk, (unsigned)(3 * Pm)), dim3(256), 0, s, dmd, dnr, inst->d_rowptr,
+    hipLaunchKernelGGL(k_sparse_eval, dim3(nblk, (unsigned)(3 * Pm)), dim3(256), 0, s, dmd, drr, inst->d_rowptr,
                        inst->d_col, inst->d_val, erx, ery, part);
     hipLaunchKernelGGL(k_sum_segments, dim3((unsigned)(3 * Pm)), dim3(256), 0, s, part, (int)nblk, dout);
   }
@@ -1433,6 +1441,8 @@ extern "C" int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, 
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
   ctx->last_us = ms * 1000.0;
+  rc = comm_sum_fq(ctx, sh, 0, h.data(), 3 * Pm);
+  if (rc) return rc;
   for (size_t i = 0; i < 3 * Pm; i++) st_fq(out + 4 * i, h[i]);
   return SPG_OK;
 }

@@ -46,29 +46,40 @@ __global__ void k_gather(const uint32_t* __restrict__ addr, const Fq* __restrict
 __device__ __forceinline__ Fq hash3(const Fq& a, const Fq& v, const Fq& ts, const Fq& rh, const Fq& rh2, const Fq& rms) {
   return fq_sub(fq_add(fq_add(fq_mul(ts, rh2), fq_mul(v, rh)), a), rms);
 }
-// leaves of the 4B ops circuits (row read b, row write b, col read b, col write b), written into the trees
+// leaves of the 4B ops circuits (row read b, row write b, col read b, col write b), written into the trees.
+// Sharded proofs (W ranks) keep the leaves i = W i' + r of rank r: local leaf i' of m = N / W (W = 1: all)
 __global__ void k_hash_ops(const uint32_t* __restrict__ addr, const uint32_t* __restrict__ rts,
-                           const Fq* __restrict__ derefs, size_t B, int logN, Fq rh, Fq rh2, Fq rms,
-                           Fq* __restrict__ tree) {
-  const size_t N = (size_t)1 << logN;
+                           const Fq* __restrict__ derefs, size_t B, int logN, int logm, uint32_t W, uint32_t r, Fq rh,
+                           Fq rh2, Fq rms, Fq* __restrict__ tree) {
+  const size_t N = (size_t)1 << logN, m = (size_t)1 << logm;
   size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= 2 * B * N) return;
-  size_t sb = t >> logN, i = t & (N - 1);  // sb = side * B + b
-  size_t s = sb >= B, b = sb - s * B;
-  Fq a = fq_from_u64(addr[t]), ts = fq_from_u64(rts[t]), v = derefs[t];
-  tree[((2 * s) * B + b) * 2 * N + i] = hash3(a, v, ts, rh, rh2, rms);
-  tree[((2 * s + 1) * B + b) * 2 * N + i] = hash3(a, v, fq_add(ts, fq_one()), rh, rh2, rms);
+  if (t >= 2 * B * m) return;
+  size_t sb = t >> logm, il = t & (m - 1);  // sb = side * B + b
+  size_t s = sb >= B, b = sb - s * B, g = sb * N + il * W + r;
+  Fq a = fq_from_u64(addr[g]), ts = fq_from_u64(rts[g]), v = derefs[g];
+  tree[((2 * s) * B + b) * 2 * m + il] = hash3(a, v, ts, rh, rh2, rms);
+  tree[((2 * s + 1) * B + b) * 2 * m + il] = hash3(a, v, fq_add(ts, fq_one()), rh, rh2, rms);
 }
-// leaves of the 4 memory circuits (row init, row audit, col init, col audit)
+// leaves of the 4 memory circuits (row init, row audit, col init, col audit); cell i = W i' + r as above
 __global__ void k_hash_mem(const uint32_t* __restrict__ audit, const Fq* __restrict__ mem_rx,
-                           const Fq* __restrict__ mem_ry, int logC, Fq rh, Fq rh2, Fq rms, Fq* __restrict__ tree) {
-  const size_t cells = (size_t)1 << logC;
+                           const Fq* __restrict__ mem_ry, int logC, int logm, uint32_t W, uint32_t r, Fq rh, Fq rh2,
+                           Fq rms, Fq* __restrict__ tree) {
+  const size_t cells = (size_t)1 << logC, m = (size_t)1 << logm;
   size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= 2 * cells) return;
-  size_t s = t >> logC, i = t & (cells - 1);
+  if (t >= 2 * m) return;
+  size_t s = t >> logm, il = t & (m - 1), i = il * W + r;
   Fq a = fq_from_u64(i), v = (s ? mem_ry : mem_rx)[i];
-  tree[(2 * s) * 2 * cells + i] = hash3(a, v, fq_zero(), rh, rh2, rms);
-  tree[(2 * s + 1) * 2 * cells + i] = hash3(a, v, fq_from_u64(audit[t]), rh, rh2, rms);
+  tree[(2 * s) * 2 * m + il] = hash3(a, v, fq_zero(), rh, rh2, rms);
+  tree[(2 * s + 1) * 2 * m + il] = hash3(a, v, fq_from_u64(audit[s * cells + i]), rh, rh2, rms);
+}
+// dst[i] = src[i W + r], i < n (a rank's interleaved share of a vector)
+__global__ void k_strided(Fq* __restrict__ dst, const Fq* __restrict__ src, size_t n, uint32_t W, uint32_t r) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = src[i * W + r];
+}
+__global__ void k_scale(Fq* __restrict__ v, size_t n, Fq s) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = fq_mul(v[i], s);
 }
 // v_{k+1}[i] = v_k[i] * v_k[i + half] for every circuit (circuit stride 2M)
 __global__ void k_tree_level(Fq* __restrict__ tree, size_t nc, size_t stride, size_t off_k, size_t off_k1, int log_half) {
@@ -264,7 +275,7 @@ static const size_t kHostFinalRows = 64;  // latency-path commits of at most thi
 enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
-  kWsTops, kWsCommitBk, kWsC2
+  kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -326,12 +337,30 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
   return 0;
 }
 
+// Hyrax rows split over the ranks of sh (SURVEY 8e "Hyrax commits: rows per GPU, allgather of the 32-byte
+// rows"): rank r commits rows [b(r), b(r+1)) of the balanced split, then every rank receives all L encodings
+int commit_rows_sh(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out, const Shard& sh) {
+  if (sh.n == 1) return commit_rows(ctx, g, d_Z, R, L, out);
+  const size_t r0 = shard_begin(L, sh.n, sh.rank), r1 = shard_begin(L, sh.n, sh.rank + 1);
+  const size_t per = (L + sh.n - 1) / sh.n;  // slots per rank in the gather
+  std::vector<Pt> mine(per);
+  int rc = r1 > r0 ? commit_rows(ctx, g, d_Z + r0 * R, R, r1 - r0, mine.data()) : 0;
+  std::vector<uint8_t> all;
+  rc = comm_allgather(ctx, sh, rc, mine.data(), per * sizeof(Pt), all);
+  if (rc) return rc;
+  for (int q = 0; q < sh.n; q++) {
+    const size_t b0 = shard_begin(L, sh.n, q), b1 = shard_begin(L, sh.n, q + 1);
+    memcpy(out + b0, all.data() + (size_t)q * per * sizeof(Pt), (b1 - b0) * sizeof(Pt));
+  }
+  return 0;
+}
+
 // DensePolynomial::commit without blinds (dense_mlpoly.rs:184-256) of 2^nv device scalars: L = 2^(nv/2)
 // rows of R = 2^(nv - nv/2) scalars against the first R generators
-int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out) {
+int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out, const Shard& sh) {
   size_t L = (size_t)1 << (nv / 2), R = (size_t)1 << (nv - nv / 2);
   out->resize(L);
-  return commit_rows(ctx, g, d_Z, R, L, out->data());
+  return commit_rows_sh(ctx, g, d_Z, R, L, out->data(), sh);
 }
 
 void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c) {
@@ -340,52 +369,65 @@ void append_polycomm(Tr& t, const char* label, const std::vector<Pt>& c) {
   t.msg(label, "poly_commitment_end");
 }
 
-// PolyEvalProof::prove without blinds (dense_mlpoly.rs:437-490) of a device polynomial of 2^|r| scalars
+// PolyEvalProof::prove without blinds (dense_mlpoly.rs:437-490) of a device polynomial of 2^|r| scalars.
+// Sharded (sh.n > 1): rank r binds its balanced share of the Ls rows, the partial L.Z vectors are summed over the
+// ranks, and every rank runs the same (replicated) Bullet rounds.
 int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, const Fq& Zr, Tr& t, Tape& tape,
-                           DotProductProofLogP* out) {
+                    DotProductProofLogP* out, const Shard& sh) {
   t.protocol("polynomial evaluation proof");
   size_t nv = r.size(), ln = nv / 2;
   FqV rl(r.begin(), r.begin() + ln), rr(r.begin() + ln, r.end());
   size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
   if (Rs > g.n_pc) return set_err(ctx, SPG_E_ARG, "poly eval: polynomial wider than the generators");
   FqV R = eq_evals_host(rr);
-  size_t S = std::min<size_t>(Ls, std::max<size_t>(1, 8192 / nblk(Rs)));  // row splits to fill the chip
-  size_t chunk = (Ls + S - 1) / S;
-  S = (Ls + chunk - 1) / chunk;
-  Fq* dL = (Fq*)ws_get(ctx, kWsL, Ls * sizeof(Fq) + 64);
-  Fq* dpart = (Fq*)ws_get(ctx, kWsBoundPart, S * Rs * sizeof(Fq) + 64);
-  Fq* dout = (Fq*)ws_get(ctx, kWsBound, Rs * sizeof(Fq) + 64);
-  if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "poly_eval_prove");
-  int rc = eq_table(ctx, rl, dL);
-  if (rc) return rc;
-  {
-    KScope ks(ctx, "spark_bound", 32.0 * (double)Ls * Rs + 64.0 * S * Rs);
-    hipLaunchKernelGGL(k_bound_rows, dim3(nblk(Rs), (unsigned)S), dim3(256), 0, ctx->stream, d_Z, dL, Ls, Rs, chunk,
-                       dpart);
-    hipLaunchKernelGGL(k_bound_sum, dim3(nblk(Rs)), dim3(256), 0, ctx->stream, dpart, S, Rs, dout);
+  const size_t j0 = shard_begin(Ls, sh.n, sh.rank), j1 = shard_begin(Ls, sh.n, sh.rank + 1), Lm = j1 - j0;
+  FqV LZ(Rs, fq_zero());
+  int rc = 0;
+  if (Lm) {
+    size_t S = std::min<size_t>(Lm, std::max<size_t>(1, 8192 / nblk(Rs)));  // row splits to fill the chip
+    size_t chunk = (Lm + S - 1) / S;
+    S = (Lm + chunk - 1) / chunk;
+    Fq* dL = (Fq*)ws_get(ctx, kWsL, Ls * sizeof(Fq) + 64);
+    Fq* dpart = (Fq*)ws_get(ctx, kWsBoundPart, S * Rs * sizeof(Fq) + 64);
+    Fq* dout = (Fq*)ws_get(ctx, kWsBound, Rs * sizeof(Fq) + 64);
+    if (!dL || !dpart || !dout) rc = set_err(ctx, SPG_E_NOMEM, "poly_eval_prove");
+    if (!rc) rc = eq_table(ctx, rl, dL);
+    if (!rc) {
+      KScope ks(ctx, "spark_bound", 32.0 * (double)Lm * Rs + 64.0 * S * Rs);
+      hipLaunchKernelGGL(k_bound_rows, dim3(nblk(Rs), (unsigned)S), dim3(256), 0, ctx->stream, d_Z + j0 * Rs, dL + j0,
+                         Lm, Rs, chunk, dpart);
+      hipLaunchKernelGGL(k_bound_sum, dim3(nblk(Rs)), dim3(256), 0, ctx->stream, dpart, S, Rs, dout);
+      if (hipGetLastError() != hipSuccess) rc = set_err(ctx, SPG_E_HIP, "poly_eval_prove launch");
+    }
+    if (!rc) rc = d2h_fq(ctx, dout, LZ.data(), Rs);
   }
-  SPG_HIP(ctx, hipGetLastError());
-  FqV LZ(Rs);
-  rc = d2h_fq(ctx, dout, LZ.data(), Rs);
+  rc = comm_sum_fq(ctx, sh, rc, LZ.data(), Rs);
   if (rc) return rc;
   Pt cy;
   return dotproduct_log_prove(ctx, g, t, tape, LZ, fq_zero(), R, Zr, fq_zero(), out, &cy);
 }
 
-// out[s] = sum_i base[s * seglen + i] * eq[i], i < n, s < nseg
-static int seg_dots(spg_ctx* ctx, const Fq* base, size_t seglen, size_t nseg, const Fq* d_eq, size_t n, FqV* out) {
-  unsigned nb = (unsigned)std::min<size_t>(nblk(n), std::max<size_t>(1, 2048 / nseg));
-  Fq* part = (Fq*)ws_get(ctx, kWsSegPart, nseg * nb * sizeof(Fq) + 64);
-  Fq* dres = (Fq*)ws_get(ctx, kWsSeg, nseg * sizeof(Fq) + 64);
-  if (!part || !dres) return set_err(ctx, SPG_E_NOMEM, "seg_dots");
-  {
-    KScope ks(ctx, "spark_evaluate", 32.0 * n * nseg + 32.0 * n);
-    hipLaunchKernelGGL(k_seg_dot, dim3(nb, (unsigned)nseg), dim3(256), 0, ctx->stream, base, seglen, d_eq, n, part);
-    hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)nseg), dim3(256), 0, ctx->stream, part, (int)nb, dres);
+// out[s] = sum_i base[s * seglen + i] * eq[i], i < n, s < nseg; sharded: rank r sums its balanced share of i
+static int seg_dots(spg_ctx* ctx, const Fq* base, size_t seglen, size_t nseg, const Fq* d_eq, size_t n, FqV* out,
+                    const Shard& sh = Shard()) {
+  const size_t i0 = shard_begin(n, sh.n, sh.rank), i1 = shard_begin(n, sh.n, sh.rank + 1), nm = i1 - i0;
+  out->assign(nseg, fq_zero());
+  int rc = 0;
+  if (nm) {
+    unsigned nb = (unsigned)std::min<size_t>(nblk(nm), std::max<size_t>(1, 2048 / nseg));
+    Fq* part = (Fq*)ws_get(ctx, kWsSegPart, nseg * nb * sizeof(Fq) + 64);
+    Fq* dres = (Fq*)ws_get(ctx, kWsSeg, nseg * sizeof(Fq) + 64);
+    if (!part || !dres) rc = set_err(ctx, SPG_E_NOMEM, "seg_dots");
+    if (!rc) {
+      KScope ks(ctx, "spark_evaluate", 32.0 * nm * nseg + 32.0 * nm);
+      hipLaunchKernelGGL(k_seg_dot, dim3(nb, (unsigned)nseg), dim3(256), 0, ctx->stream, base + i0, seglen, d_eq + i0, nm,
+                         part);
+      hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)nseg), dim3(256), 0, ctx->stream, part, (int)nb, dres);
+      if (hipGetLastError() != hipSuccess) rc = set_err(ctx, SPG_E_HIP, "seg_dots launch");
+    }
+    if (!rc) rc = d2h_fq(ctx, dres, out->data(), nseg);
   }
-  SPG_HIP(ctx, hipGetLastError());
-  out->resize(nseg);
-  return d2h_fq(ctx, dres, out->data(), nseg);
+  return comm_sum_fq(ctx, sh, rc, out->data(), nseg);
 }
 
 // UniPoly::append_to_transcript (unipoly.rs:112-120)
@@ -431,37 +473,68 @@ static void layer_grid(size_t W, unsigned* K, int* BS) {
   }
 }
 
+// A set of nc product circuits (M leaves each), possibly sharded over the W ranks of a proof (see "sharded
+// proof" at spark_prove_core): rank r holds leaves i = W i' + r as a local tree of m = M / W leaves (levels of
+// >= 2 entries at loc + c 2m, the usual back-to-back layout), and every rank holds the global levels of <= W
+// entries as a replicated "top" tree (circuit c at top + c 2W, W entries first). W == 1: loc is the whole tree.
+struct TreeSh {
+  Fq* loc = nullptr;
+  size_t m = 0;
+  Fq* top = nullptr;
+  int W = 1, r = 0;
+};
+
 // ProductCircuitEvalProofBatched::prove with fused layer rounds (k_layer_round / k_layer_close above); same
-// transcript and proof as batched_prove below
-static int batched_prove_fused(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims, const std::vector<Triple>& dotp,
-                               const FqV& dotp_claims, Tr& t, BatchedProofP* out, FqV* rand_out) {
+// transcript and proof as batched_prove below.
+// A layer whose vectors are sharded (global half length >= W) runs its first lg(half / W) rounds on the local
+// shares (pairs (i, i + len) stay on one rank while W | len; the round's (e0, e2, e3) are summed over the ranks),
+// then gathers the W remaining entries of every vector (k_layer_close without the fold when no round ran) and
+// runs the last lg W rounds replicated, exactly like an unsharded layer of that length.
+static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t M, FqV claims,
+                               const std::vector<Triple>& dotp, const FqV& dotp_claims, Tr& t, BatchedProofP* out,
+                               FqV* rand_out, const Shard& sh) {
   hipStream_t s = ctx->stream;
-  const size_t L = lg2(M), stride = 2 * M;
-  auto off = [&](size_t k) { return 2 * M - 2 * (M >> k); };
+  const size_t L = lg2(M), W = (size_t)ts.W, lgW = lg2(W), m = ts.m, lgm = lg2(m);
+  auto off = [](size_t MM, size_t k) { return 2 * MM - 2 * (MM >> k); };
   const size_t nt_max = nc + dotp.size();
   if (3 * nt_max + 1 > kMboxScalars) return set_err(ctx, SPG_E_ARG, "batched_prove: too many circuits for the mailbox");
-  Fq* cbuf[2] = {(Fq*)ws_get(ctx, kWsC, (M / 2) * sizeof(Fq) + 64), (Fq*)ws_get(ctx, kWsC2, (M / 2) * sizeof(Fq) + 64)};
+  const size_t half_max = std::max<size_t>(M / 2 / W, 1);  // the longest eq vector held here
+  Fq* cbuf[2] = {(Fq*)ws_get(ctx, kWsC, std::max(half_max, W) * sizeof(Fq) + 64),
+                 (Fq*)ws_get(ctx, kWsC2, std::max(half_max, W) * sizeof(Fq) + 64)};
   // triples, then their coefficients, in one buffer (one upload per layer)
   const size_t tr_bytes = (nt_max * sizeof(Triple) + 63) & ~(size_t)63;
   uint8_t* ddesc = (uint8_t*)ws_get(ctx, kWsTriples, tr_bytes + nt_max * sizeof(Fq) + 64);
   Fq* part = (Fq*)ws_get(ctx, kWsPart, 3 * 2048 * sizeof(Fq) + 64);  // K <= 2048 workgroups per round
-  if (!cbuf[0] || !cbuf[1] || !ddesc || !part) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
+  Fq* gbuf = W > 1 ? (Fq*)ws_get(ctx, kWsGather, 3 * nt_max * W * sizeof(Fq) + 64) : nullptr;
+  if (!cbuf[0] || !cbuf[1] || !ddesc || !part || (W > 1 && !gbuf)) return set_err(ctx, SPG_E_NOMEM, "batched_prove");
   const Triple* dtr = (const Triple*)ddesc;
   const Fq* dcoef = (const Fq*)(ddesc + tr_bytes);
   FqV rand;
   Laps lp;
   lp.title = "ProductCircuitEvalProofBatched::prove";
   for (size_t layer = L; layer-- > 0;) {
-    const size_t half = M >> (layer + 1);  // |left| = |right| = |C|
-    const size_t rounds = lg2(half);
-    int cur = 0;  // the buffer holding the shared eq vector C
-    int rc = eq_table(ctx, rand, cbuf[0]);
+    const size_t half = M >> (layer + 1);  // |left| = |right| = |C| (global)
+    // where this layer's vectors live: local shares (sharded), the replicated top tree, or the whole tree
+    const bool sharded = W > 1 && layer < lgm;
+    const size_t hl = sharded ? half / W : half;  // entries of each vector held here
+    int rc = 0;
+    if (sharded) {  // local eq share: eq(rand)[W i' + r] = eq(rand_hi)[i'] * eq(rand_lo)[r]
+      const size_t nh = rand.size() - lgW;
+      rc = eq_table(ctx, FqV(rand.begin(), rand.begin() + nh), cbuf[0]);
+      Fq sc = fq_one();
+      for (size_t k = 0; k < lgW; k++)
+        sc = fq_mul(sc, ((ts.r >> (lgW - 1 - k)) & 1) ? rand[nh + k] : fq_sub(fq_one(), rand[nh + k]));
+      if (!rc) hipLaunchKernelGGL(k_scale, dim3(nblk(hl)), dim3(256), 0, s, cbuf[0], hl, sc);
+    } else {
+      rc = eq_table(ctx, rand, cbuf[0]);
+    }
     if (rc) return rc;
+    int cur = 0;  // the buffer holding the shared eq vector C
     const bool with_dotp = layer == 0 && !dotp.empty();
     std::vector<Triple> tr;
     for (size_t c = 0; c < nc; c++) {
-      Fq* v = tree + c * stride + off(layer);
-      tr.push_back({v, v + half, nullptr});  // C: the shared eq vector
+      Fq* v = sharded || W == 1 ? ts.loc + c * 2 * m + off(m, layer) : ts.top + c * 2 * W + off(W, layer - lgm);
+      tr.push_back({v, v + hl, nullptr});  // C: the shared eq vector
     }
     if (with_dotp) {
       claims.insert(claims.end(), dotp_claims.begin(), dotp_claims.end());
@@ -481,67 +554,104 @@ static int batched_prove_fused(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV 
     lp.lap("layer_setup");
     LayerProofP lpf;
     FqV r_prod;
-    size_t log_len = rounds;
     bool pending = false;  // a bound_poly_var_top with r_pend not yet applied
     Fq r_pend = fq_zero();
-    for (size_t j = 0; j < rounds; j++) {
-      log_len--;
-      const size_t len = (size_t)1 << log_len;
-      unsigned K;
-      int BS;
-      static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
-      if (quad) {  // a quad per element, about one element per quad
-        const size_t W = tr.size() * len;
-        BS = W <= 16 ? 64 : 256;
-        K = (unsigned)std::min<size_t>((W * 4 + BS - 1) / BS, 2048);
-      } else {
-        layer_grid(tr.size() * len, &K, &BS);
+    // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks
+    auto run_rounds = [&](size_t log_len, bool local) -> int {
+      while (log_len-- > 0) {
+        const size_t len = (size_t)1 << log_len;
+        unsigned K;
+        int BS;
+        static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
+        if (quad) {  // a quad per element, about one element per quad
+          const size_t Wd = tr.size() * len;
+          BS = Wd <= 16 ? 64 : 256;
+          K = (unsigned)std::min<size_t>((Wd * 4 + BS - 1) / BS, 2048);
+        } else {
+          layer_grid(tr.size() * len, &K, &BS);
+        }
+        {
+          KScope ks(ctx, "spark_layer_round", 192.0 * tr.size() * len * (pending ? 2.0 : 1.0));
+          const int nt = (int)tr.size(), lg = (int)log_len, df = pending ? 1 : 0;
+          const uint32_t seq = ++ctx->mbox_seq;
+          if (quad && BS == 64)
+            hipLaunchKernelGGL(k_layer_round_q<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                               cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+          else if (quad)
+            hipLaunchKernelGGL(k_layer_round_q<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend,
+                               cbuf[cur], cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+          else if (BS == 64)
+            hipLaunchKernelGGL(k_layer_round<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                               cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+          else
+            hipLaunchKernelGGL(k_layer_round<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
+                               cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+        }
+        if (pending) cur ^= 1;
+        SPG_HIP(ctx, hipGetLastError());
+        Fq ev[3];
+        int rc2 = eval_reduce_finish(ctx, ev);
+        if (local) rc2 = comm_sum_fq(ctx, sh, rc2, ev, 3);
+        if (rc2) return rc2;
+        lp.lap("round_eval_wait");
+        Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
+        FqV poly = uni_from_evals3(evals);
+        append_unipoly(t, poly);
+        Fq r_j = t.challenge("challenge_nextround");
+        r_prod.push_back(r_j);
+        pending = true;
+        r_pend = r_j;
+        e = uni_eval(poly, r_j);
+        lpf.polys.push_back({poly[0], poly[2], poly[3]});
+        lp.lap("round_host");
       }
-      {
-        KScope ks(ctx, "spark_layer_round", 192.0 * tr.size() * len * (pending ? 2.0 : 1.0));
-        const int nt = (int)tr.size(), lg = (int)log_len, df = pending ? 1 : 0;
-        const uint32_t seq = ++ctx->mbox_seq;
-        if (quad && BS == 64)
-          hipLaunchKernelGGL(k_layer_round_q<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
-                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
-        else if (quad)
-          hipLaunchKernelGGL(k_layer_round_q<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
-                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
-        else if (BS == 64)
-          hipLaunchKernelGGL(k_layer_round<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
-                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
-        else
-          hipLaunchKernelGGL(k_layer_round<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
-                             cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
-      }
-      if (pending) cur ^= 1;
-      SPG_HIP(ctx, hipGetLastError());
-      Fq ev[3];
-      rc = eval_reduce_finish(ctx, ev);
-      if (rc) return rc;
-      lp.lap("round_eval_wait");
-      Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
-      FqV poly = uni_from_evals3(evals);
-      append_unipoly(t, poly);
-      Fq r_j = t.challenge("challenge_nextround");
-      r_prod.push_back(r_j);
-      pending = true;
-      r_pend = r_j;
-      e = uni_eval(poly, r_j);
-      lpf.polys.push_back({poly[0], poly[2], poly[3]});
-      lp.lap("round_host");
-    }
-    // the last round's fold and the final claims A[0], B[0] (C[0] for the dot-product circuits), by mailbox
-    FqV fin(3 * tr.size());
-    {
+      return 0;
+    };
+    // A[0], B[0], C[0] of every triple (after the pending fold, if any), by mailbox
+    auto close = [&](FqV& fin) -> int {
+      fin.resize(3 * tr.size());
       KScope ks(ctx, "spark_layer_close");
       const uint32_t seq = ++ctx->mbox_seq;
-      hipLaunchKernelGGL(k_layer_close, dim3(1), dim3(256), 0, s, dtr, (int)tr.size(), r_pend, cbuf[cur], ctx->d_mbox,
-                         seq);
+      hipLaunchKernelGGL(k_layer_close, dim3(1), dim3(256), 0, s, dtr, (int)tr.size(), pending ? 1 : 0, r_pend,
+                         cbuf[cur], ctx->d_mbox, seq);
       SPG_HIP(ctx, hipGetLastError());
-      rc = mbox_wait(ctx, seq, fin.data(), (int)fin.size());
+      pending = false;
+      return mbox_wait(ctx, seq, fin.data(), (int)fin.size());
+    };
+    if (sharded) {
+      rc = run_rounds(lg2(hl), true);
+      // gather: every vector has one entry per rank left; rank q's entry is global index q
+      FqV mine;
+      if (!rc) rc = close(mine);
+      std::vector<uint8_t> all;
+      rc = comm_allgather(ctx, sh, rc, mine.data(), mine.size() * sizeof(Fq), all);
       if (rc) return rc;
+      const Fq* g = (const Fq*)all.data();
+      const size_t nt = tr.size();
+      uint8_t* st = (uint8_t*)pinned_get(ctx, 3 * nt * W * sizeof(Fq) + tr_bytes + 64);
+      if (!st) return set_err(ctx, SPG_E_NOMEM, "gather staging");
+      Fq* hv = (Fq*)(st + tr_bytes);
+      for (size_t c = 0; c < nt; c++)
+        for (size_t k = 0; k < 3; k++)
+          for (size_t q = 0; q < W; q++) hv[(3 * c + k) * W + q] = g[q * 3 * nt + 3 * c + k];
+      for (size_t c = 0; c < nt; c++) {
+        const bool own_c = tr[c].C != nullptr;
+        tr[c] = {gbuf + 3 * c * W, gbuf + (3 * c + 1) * W, own_c ? gbuf + (3 * c + 2) * W : nullptr};
+      }
+      memcpy(st, tr.data(), nt * sizeof(Triple));
+      SPG_HIP(ctx, hipMemcpyAsync(ddesc, st, nt * sizeof(Triple), hipMemcpyHostToDevice, s));
+      SPG_HIP(ctx, hipMemcpyAsync(gbuf, hv, 3 * nt * W * sizeof(Fq), hipMemcpyHostToDevice, s));
+      if (nc)  // the product circuits' shared eq vector (every product triple gathered the same entries)
+        SPG_HIP(ctx, hipMemcpyAsync(cbuf[cur], gbuf + 2 * W, W * sizeof(Fq), hipMemcpyDeviceToDevice, s));
+      rc = run_rounds(lgW, false);
+    } else {
+      rc = run_rounds(lg2(hl), false);
     }
+    if (rc) return rc;
+    // the last round's fold and the final claims A[0], B[0] (C[0] for the dot-product circuits), by mailbox
+    FqV fin;
+    rc = close(fin);
+    if (rc) return rc;
     for (size_t c = 0; c < nc; c++) {
       lpf.left.push_back(fin[3 * c]);
       lpf.right.push_back(fin[3 * c + 1]);
@@ -575,10 +685,12 @@ static int batched_prove_fused(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV 
 // ProductCircuitEvalProofBatched::prove (product_tree.rs:271-396) over the nc product circuits of `tree`
 // (M leaves each, claims = their ProductCircuit::evaluate) and, at layer 0, the dot-product circuits
 // `dotp` (three device vectors of M/2 entries each, folded in place) with claims `dotp_claims`.
-static int batched_prove(spg_ctx* ctx, Fq* tree, size_t nc, size_t M, FqV claims, const std::vector<Triple>& dotp,
-                         const FqV& dotp_claims, Tr& t, BatchedProofP* out, FqV* rand_out) {
+static int batched_prove(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t M, FqV claims,
+                         const std::vector<Triple>& dotp, const FqV& dotp_claims, Tr& t, BatchedProofP* out,
+                         FqV* rand_out, const Shard& sh) {
   static const bool fused = !getenv("SPG_LAYER_FUSED") || atoi(getenv("SPG_LAYER_FUSED")) != 0;
-  if (fused) return batched_prove_fused(ctx, tree, nc, M, claims, dotp, dotp_claims, t, out, rand_out);
+  if (fused || ts.W > 1) return batched_prove_fused(ctx, ts, nc, M, claims, dotp, dotp_claims, t, out, rand_out, sh);
+  Fq* tree = ts.loc;
   hipStream_t s = ctx->stream;
   const size_t L = lg2(M), stride = 2 * M;
   auto off = [&](size_t k) { return 2 * M - 2 * (M >> k); };
@@ -754,7 +866,7 @@ namespace spg {
 // matrices) with SparseMatPolyCommitmentGens::new(label, gens_nvx, gens_nvy, gens_nnz, gens_batch)
 int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_t nvx, size_t nvy,
                        const uint8_t* label, size_t label_len, size_t gens_nvx, size_t gens_nvy, size_t gens_nnz,
-                       size_t gens_batch, spg_spark** out) {
+                       size_t gens_batch, spg_spark** out, const Shard& sh) {
   if (!ctx || polys.empty() || !label || !out) return SPG_E_ARG;
   hipStream_t s = ctx->stream;
   const size_t B = polys.size();
@@ -834,8 +946,8 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
   S->g_mem = gens_view(S->dev, nv_mem);
   S->g_der = gens_view(S->dev, nv_der);
   std::vector<Pt> comm_ops, comm_mem;
-  rc = commit_dev(ctx, S->g_ops, S->d_comb_ops, lg2(S->comb_ops_len), &comm_ops);
-  if (!rc) rc = commit_dev(ctx, S->g_mem, S->d_comb_mem, lg2(S->comb_mem_len), &comm_mem);
+  rc = commit_dev(ctx, S->g_ops, S->d_comb_ops, lg2(S->comb_ops_len), &comm_ops, sh);
+  if (!rc) rc = commit_dev(ctx, S->g_mem, S->d_comb_mem, lg2(S->comb_mem_len), &comm_mem, sh);
   if (rc) {
     spg_spark_free(ctx, S);
     return rc;
@@ -874,7 +986,8 @@ extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const
   for (size_t k = 0; k < 3 * ci->num_instances; k++) polys.push_back({ci->entries[k], ci->nnz[k]});
   const size_t nvx = lg2(ci->max_num_cons), nvy = lg2(ci->num_vars);
   spg_spark* S = nullptr;
-  int rc = spark_commit_polys(ctx, polys, nvx, nvy, label, label_len, nvx, nvy, gens_nnz, gens_batch, &S);
+  int rc = spark_commit_polys(ctx, polys, nvx, nvy, label, label_len, nvx, nvy, gens_nnz, gens_batch, &S,
+                              ctx_shard(ctx));
   if (rc) return rc;
   Writer w;
   spark_comm_ser(S, w);
@@ -887,8 +1000,22 @@ extern "C" int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* ci, const
 
 namespace spg {
 
-// SparseMatPolyEvalProof::prove (sparse_mlpoly.rs:1497-1564); appends bincode(proof) to w
-int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w) {
+// SparseMatPolyEvalProof::prove (sparse_mlpoly.rs:1497-1564); appends bincode(proof) to w.
+//
+// Sharded proof (sh.n = W > 1 processes, one GPU each; SURVEY 8e "SPARK product trees: shard by the low index
+// bits"): every rank holds the whole dense representation and runs the same transcript. The O(N) work splits:
+//   derefs commitment  Hyrax rows split over the ranks, 32-byte rows allgathered (commit_rows_sh)
+//   hash layer, trees  rank r hashes leaves i = W i' + r of each circuit of >= 2W leaves and builds its local
+//                      product tree; ProductCircuit::compute_layer pairs i with i + len/2, which keeps the low
+//                      lg W bits, so every level stays local down to one entry per rank; those W entries are
+//                      allgathered and the top lg W levels built on every rank (TreeSh)
+//   layer sumchecks    batched_prove_fused: local rounds with (e0, e2, e3) summed over the ranks, then a gather
+//   hash-layer evals   contiguous shares of each dot product, summed (seg_dots)
+//   PolyEvalProofs     L.Z rows split, partial vectors summed; Bullet replicated (poly_eval_prove)
+// A circuit set of fewer than 2W leaves (or W not a power of two) stays whole on every rank. Every collective
+// carries the rank's status.
+int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& evals, Tr& t, Tape& tape, Writer& w,
+                     const Shard& sh) {
   if (evals.size() != S->B) return set_err(ctx, SPG_E_ARG, "one evaluation per batched matrix");
   Laps lp;
   lp.title = "SparseMatPolyEvalProof::prove";
@@ -898,21 +1025,41 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   if (ey.size() < ex.size()) ey.insert(ey.begin(), ex.size() - ey.size(), fq_zero());
   if (ex.size() > 40 || ((size_t)1 << ex.size()) != cells)
     return set_err(ctx, SPG_E_ARG, "rx / ry do not match the memory size");
+  // interleaved shards of the two circuit sets (W = 1: whole)
+  const size_t Wr = (size_t)sh.n;
+  TreeSh tso, tsm;
+  const bool pow2 = Wr > 1 && (Wr & (Wr - 1)) == 0;  // interleaving needs W | M (other world sizes: whole trees)
+  tso.W = (pow2 && N >= 2 * Wr) ? (int)Wr : 1;
+  tsm.W = (pow2 && cells >= 2 * Wr) ? (int)Wr : 1;
+  tso.r = tso.W > 1 ? sh.rank : 0;
+  tsm.r = tsm.W > 1 ? sh.rank : 0;
+  tso.m = N / tso.W;
+  tsm.m = cells / tsm.W;
+  const size_t mo = tso.m, mm = tsm.m, hNl = hN / tso.W;
   t.protocol("Sparse polynomial evaluation proof");
   timer_start(ctx);
   const size_t der_len = npow2(2 * BN);
   Fq* mem_rx = (Fq*)ws_get(ctx, kWsMemRx, cells * sizeof(Fq) + 64);
   Fq* mem_ry = (Fq*)ws_get(ctx, kWsMemRy, cells * sizeof(Fq) + 64);
   Fq* derefs = (Fq*)ws_get(ctx, kWsDerefs, der_len * sizeof(Fq) + 64);
-  Fq* tree_ops = (Fq*)ws_get(ctx, kWsTreeOps, 4 * B * 2 * N * sizeof(Fq) + 64);
-  Fq* tree_mem = (Fq*)ws_get(ctx, kWsTreeMem, 4 * 2 * cells * sizeof(Fq) + 64);
-  Fq* dotbuf = (Fq*)ws_get(ctx, kWsDotp, 2 * B * 3 * hN * sizeof(Fq) + 64);
+  tso.loc = (Fq*)ws_get(ctx, kWsTreeOps, 4 * B * 2 * mo * sizeof(Fq) + 64);
+  tsm.loc = (Fq*)ws_get(ctx, kWsTreeMem, 4 * 2 * mm * sizeof(Fq) + 64);
+  tso.top = tso.W > 1 ? (Fq*)ws_get(ctx, kWsTopOps, 4 * B * 2 * Wr * sizeof(Fq) + 64) : nullptr;
+  tsm.top = tsm.W > 1 ? (Fq*)ws_get(ctx, kWsTopMem, 4 * 2 * Wr * sizeof(Fq) + 64) : nullptr;
+  Fq* dotbuf = (Fq*)ws_get(ctx, kWsDotp, 2 * B * 3 * hNl * sizeof(Fq) + 64);
   Fq* dtops = (Fq*)ws_get(ctx, kWsTops, 4 * (B + 1) * sizeof(Fq) + 64);
   Fq* eq_ops = (Fq*)ws_get(ctx, kWsEqOps, N * sizeof(Fq) + 64);
   Fq* eq_mem = (Fq*)ws_get(ctx, kWsEqMem, cells * sizeof(Fq) + 64);
-  if (!mem_rx || !mem_ry || !derefs || !tree_ops || !tree_mem || !dotbuf || !dtops || !eq_ops || !eq_mem)
-    return set_err(ctx, SPG_E_NOMEM, "spark workspace");
-  int rc = eq_table(ctx, ex, mem_rx);
+  int rc = 0;
+  if (!mem_rx || !mem_ry || !derefs || !tso.loc || !tsm.loc || (tso.W > 1 && !tso.top) || (tsm.W > 1 && !tsm.top) ||
+      !dotbuf || !dtops || !eq_ops || !eq_mem)
+    rc = set_err(ctx, SPG_E_NOMEM, "spark workspace");
+  if (sh.n > 1) {  // every rank enters the proof's collectives only if every rank has its workspace
+    std::vector<uint8_t> none;
+    rc = comm_allgather(ctx, sh, rc, nullptr, 0, none);
+  }
+  if (rc) return rc;
+  rc = eq_table(ctx, ex, mem_rx);
   if (!rc) rc = eq_table(ctx, ey, mem_ry);
   if (rc) return rc;
   // Derefs (sparse_mlpoly.rs:51-67): comb = row derefs ++ col derefs, zero-padded
@@ -924,7 +1071,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   SPG_HIP(ctx, hipGetLastError());
   lp.lap("setup+deref");
   std::vector<Pt> comm_derefs;
-  rc = commit_dev(ctx, S->g_der, derefs, lg2(der_len), &comm_derefs);
+  rc = commit_dev(ctx, S->g_der, derefs, lg2(der_len), &comm_derefs, sh);
   lp.lap("derefs_commit");
   if (rc) return rc;
   t.msg("derefs_commitment", "begin_derefs_commitment");
@@ -932,17 +1079,17 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   t.msg("derefs_commitment", "end_derefs_commitment");
   FqV rmc = t.challenges("challenge_r_hash", 2);
   const Fq rh = rmc[0], rh2 = fq_mul(rmc[0], rmc[0]), rms = rmc[1];
-  // hash layer leaves straight into the trees, then the product trees (Layers::new)
+  // hash layer leaves straight into the (local) trees, then the product trees (Layers::new)
   {
-    KScope ks(ctx, "spark_hash_layer", (8.0 + 32.0 + 64.0) * 2 * BN + (4.0 + 32.0 + 64.0) * 2 * cells);
-    hipLaunchKernelGGL(k_hash_ops, dim3(nblk(2 * BN)), dim3(256), 0, s, S->d_addr, S->d_rts, derefs, B, (int)lg2(N),
-                       rh, rh2, rms, tree_ops);
-    hipLaunchKernelGGL(k_hash_mem, dim3(nblk(2 * cells)), dim3(256), 0, s, S->d_audit, mem_rx, mem_ry,
-                       (int)lg2(cells), rh, rh2, rms, tree_mem);
+    KScope ks(ctx, "spark_hash_layer", (8.0 + 32.0 + 64.0) * 2 * B * mo + (4.0 + 32.0 + 64.0) * 2 * mm);
+    hipLaunchKernelGGL(k_hash_ops, dim3(nblk(2 * B * mo)), dim3(256), 0, s, S->d_addr, S->d_rts, derefs, B, (int)lg2(N),
+                       (int)lg2(mo), (uint32_t)tso.W, (uint32_t)tso.r, rh, rh2, rms, tso.loc);
+    hipLaunchKernelGGL(k_hash_mem, dim3(nblk(2 * mm)), dim3(256), 0, s, S->d_audit, mem_rx, mem_ry, (int)lg2(cells),
+                       (int)lg2(mm), (uint32_t)tsm.W, (uint32_t)tsm.r, rh, rh2, rms, tsm.loc);
   }
-  for (int which = 0; which < 2; which++) {  // ProductCircuit::new (product_tree.rs:36-58)
-    Fq* tree = which ? tree_mem : tree_ops;
-    const size_t M = which ? cells : N, nc = which ? 4 : 4 * B;
+  for (int which = 0; which < 2; which++) {  // ProductCircuit::new (product_tree.rs:36-58), local trees
+    Fq* tree = which ? tsm.loc : tso.loc;
+    const size_t M = which ? mm : mo, nc = which ? 4 : 4 * B;
     KScope ks(ctx, "spark_product_tree", 96.0 * nc * M / 2);
     for (size_t k = 0; k + 1 < lg2(M); k++) {
       size_t ok = 2 * M - 2 * (M >> k), ok1 = 2 * M - 2 * (M >> (k + 1));
@@ -955,6 +1102,32 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   SPG_HIP(ctx, hipGetLastError());
   FqV tops(4 * B + 4);
   rc = d2h_fq(ctx, dtops, tops.data(), tops.size());
+  if (tso.W > 1 || tsm.W > 1) {
+    // sharded sets: the product of a local tree is the rank's entry of the global level with W entries; gather
+    // them, build the top lg W levels (ProductCircuit::compute_layer) on every rank, and the circuits' claims
+    std::vector<uint8_t> all;
+    rc = comm_allgather(ctx, sh, rc, tops.data(), tops.size() * sizeof(Fq), all);
+    if (rc) return rc;
+    const Fq* g = (const Fq*)all.data();
+    for (int which = 0; which < 2; which++) {
+      const TreeSh& ts = which ? tsm : tso;
+      if (ts.W == 1) continue;
+      const size_t nc = which ? 4 : 4 * B, base = which ? 4 * B : 0;
+      std::vector<Fq> ht(nc * 2 * Wr, fq_zero());
+      for (size_t c = 0; c < nc; c++) {
+        Fq* v = ht.data() + c * 2 * Wr;
+        for (size_t q = 0; q < Wr; q++) v[q] = g[q * tops.size() + base + c];
+        size_t o = 0;
+        for (size_t len = Wr; len > 2; len /= 2) {
+          for (size_t i = 0; i < len / 2; i++) v[o + len + i] = fq_mul(v[o + i], v[o + i + len / 2]);
+          o += len;
+        }
+        tops[base + c] = fq_mul(v[o], v[o + 1]);
+      }
+      SPG_HIP(ctx, hipMemcpyAsync(ts.top, ht.data(), ht.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
+    }
+    SPG_HIP(ctx, hipStreamSynchronize(s));  // ht is a host temporary
+  }
   lp.lap("hash+trees");
   if (rc) return rc;
   // ---- PolyEvalNetworkProof -> ProductLayerProof (sparse_mlpoly.rs:1368-1402, 1118-1263)
@@ -972,29 +1145,39 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   t.scalars("claim_col_eval_write", col_write);
   t.scalar("claim_col_eval_audit", col_audit);
   // dot-product circuits (row derefs, col derefs, val) split into halves, interleaved (left_b, right_b);
-  // copies, since the layer-0 sumcheck folds them while the hash layer evaluates the originals
+  // copies (this rank's interleaved shares when the ops set is sharded), since the layer-0 sumcheck folds them
+  // while the hash layer evaluates the originals
   std::vector<Triple> dotp;
   for (size_t b = 0; b < B; b++)
     for (size_t h = 0; h < 2; h++) {
-      Fq* base = dotbuf + (2 * b + h) * 3 * hN;
-      SPG_HIP(ctx, hipMemcpyAsync(base, derefs + b * N + h * hN, hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
-      SPG_HIP(ctx, hipMemcpyAsync(base + hN, derefs + BN + b * N + h * hN, hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
-      SPG_HIP(ctx, hipMemcpyAsync(base + 2 * hN, S->d_val + b * N + h * hN, hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
-      dotp.push_back({base, base + hN, base + 2 * hN});
+      Fq* base = dotbuf + (2 * b + h) * 3 * hNl;
+      const Fq* src[3] = {derefs + b * N + h * hN, derefs + BN + b * N + h * hN, S->d_val + b * N + h * hN};
+      for (int k = 0; k < 3; k++) {
+        if (tso.W == 1)
+          SPG_HIP(ctx, hipMemcpyAsync(base + k * hNl, src[k], hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
+        else
+          hipLaunchKernelGGL(k_strided, dim3(nblk(hNl)), dim3(256), 0, s, base + k * hNl, src[k], hNl,
+                             (uint32_t)tso.W, (uint32_t)tso.r);
+      }
+      dotp.push_back({base, base + hNl, base + 2 * hNl});
     }
+  SPG_HIP(ctx, hipGetLastError());
   FqV dotp_claims(2 * B);
   {
     Triple* dtr = (Triple*)ws_get(ctx, kWsTriples, 6 * B * sizeof(Triple) + 64);
-    unsigned nb = (unsigned)std::min<size_t>(nblk(hN), std::max<size_t>(1, 2048 / (2 * B)));
+    unsigned nb = (unsigned)std::min<size_t>(nblk(hNl), std::max<size_t>(1, 2048 / (2 * B)));
     Fq* part = (Fq*)ws_get(ctx, kWsSegPart, 2 * B * nb * sizeof(Fq) + 64);
     Fq* dres = (Fq*)ws_get(ctx, kWsSeg, 2 * B * sizeof(Fq) + 64);
-    if (!dtr || !part || !dres) return set_err(ctx, SPG_E_NOMEM, "dotp eval");
-    SPG_HIP(ctx, hipMemcpyAsync(dtr, dotp.data(), dotp.size() * sizeof(Triple), hipMemcpyHostToDevice, s));
-    KScope ks(ctx, "spark_dotp_eval", 96.0 * 2 * B * hN);
-    hipLaunchKernelGGL(k_dot3, dim3(nb, (unsigned)(2 * B)), dim3(256), 0, s, dtr, hN, part);
-    hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)(2 * B)), dim3(256), 0, s, part, (int)nb, dres);
-    SPG_HIP(ctx, hipGetLastError());
-    rc = d2h_fq(ctx, dres, dotp_claims.data(), 2 * B);
+    if (!dtr || !part || !dres) rc = set_err(ctx, SPG_E_NOMEM, "dotp eval");
+    if (!rc) {
+      SPG_HIP(ctx, hipMemcpyAsync(dtr, dotp.data(), dotp.size() * sizeof(Triple), hipMemcpyHostToDevice, s));
+      KScope ks(ctx, "spark_dotp_eval", 96.0 * 2 * B * hNl);
+      hipLaunchKernelGGL(k_dot3, dim3(nb, (unsigned)(2 * B)), dim3(256), 0, s, dtr, hNl, part);
+      hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)(2 * B)), dim3(256), 0, s, part, (int)nb, dres);
+      SPG_HIP(ctx, hipGetLastError());
+      rc = d2h_fq(ctx, dres, dotp_claims.data(), 2 * B);
+    }
+    if (tso.W > 1) rc = comm_sum_fq(ctx, sh, rc, dotp_claims.data(), 2 * B);
     if (rc) return rc;
   }
   FqV dl(B), dr(B);
@@ -1007,10 +1190,10 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   lp.lap("dotp_claims");
   BatchedProofP proof_ops, proof_mem;
   FqV rand_ops, rand_mem;
-  rc = batched_prove(ctx, tree_ops, 4 * B, N, FqV(tops.begin(), tops.begin() + 4 * B), dotp, dotp_claims, t,
-                     &proof_ops, &rand_ops);
+  rc = batched_prove(ctx, tso, 4 * B, N, FqV(tops.begin(), tops.begin() + 4 * B), dotp, dotp_claims, t, &proof_ops,
+                     &rand_ops, sh);
   if (!rc)
-    rc = batched_prove(ctx, tree_mem, 4, cells, FqV(tops.begin() + 4 * B, tops.end()), {}, {}, t, &proof_mem, &rand_mem);
+    rc = batched_prove(ctx, tsm, 4, cells, FqV(tops.begin() + 4 * B, tops.end()), {}, {}, t, &proof_mem, &rand_mem, sh);
   if (rc) return rc;
   lp.lap("layer_sumchecks");
   // ---- HashLayerProof (sparse_mlpoly.rs:805-918)
@@ -1019,9 +1202,9 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   if (!rc) rc = eq_table(ctx, rand_mem, eq_mem);
   if (rc) return rc;
   FqV ev_der, ev_ops, ev_mem;
-  rc = seg_dots(ctx, derefs, N, 2 * B, eq_ops, N, &ev_der);
-  if (!rc) rc = seg_dots(ctx, S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops);
-  if (!rc) rc = seg_dots(ctx, S->d_comb_mem, cells, 2, eq_mem, cells, &ev_mem);
+  rc = seg_dots(ctx, derefs, N, 2 * B, eq_ops, N, &ev_der, sh);
+  if (!rc) rc = seg_dots(ctx, S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops, sh);
+  if (!rc) rc = seg_dots(ctx, S->d_comb_mem, cells, 2, eq_mem, cells, &ev_mem, sh);
   if (rc) return rc;
   lp.lap("hash_evals");
   DotProductProofLogP pf_der, pf_ops, pf_mem;
@@ -1034,7 +1217,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     Fq ej;
     combine_evals(ev, rand_ops, "challenge_combine_n_to_one", t, &rj, &ej);
     t.scalar("joint_claim_eval", ej);
-    rc = poly_eval_prove(ctx, S->g_der, derefs, rj, ej, t, tape, &pf_der);
+    rc = poly_eval_prove(ctx, S->g_der, derefs, rj, ej, t, tape, &pf_der, sh);
     if (rc) return rc;
   }
   {
@@ -1045,7 +1228,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     Fq ej;
     combine_evals(ev, rand_ops, "challenge_combine_n_to_one", t, &rj, &ej);
     t.scalar("joint_claim_eval_ops", ej);
-    rc = poly_eval_prove(ctx, S->g_ops, S->d_comb_ops, rj, ej, t, tape, &pf_ops);
+    rc = poly_eval_prove(ctx, S->g_ops, S->d_comb_ops, rj, ej, t, tape, &pf_ops, sh);
     if (rc) return rc;
   }
   {
@@ -1054,7 +1237,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     Fq ej;
     combine_evals(ev_mem, rand_mem, "challenge_combine_two_to_one", t, &rj, &ej);
     t.scalar("joint_claim_eval_mem", ej);
-    rc = poly_eval_prove(ctx, S->g_mem, S->d_comb_mem, rj, ej, t, tape, &pf_mem);
+    rc = poly_eval_prove(ctx, S->g_mem, S->d_comb_mem, rj, ej, t, tape, &pf_mem, sh);
     if (rc) return rc;
   }
   lp.lap("poly_eval_proofs");
@@ -1105,7 +1288,7 @@ extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, s
   for (size_t i = 0; i < ry_len; i++) ey.push_back(ld_fq(ry + 4 * i));
   for (size_t i = 0; i < n_evals; i++) evals[i] = ld_fq(evals_in + 4 * i);
   Writer w;
-  int rc = spark_prove_core(ctx, S, ex, ey, evals, transcript->t, tape_h->t, w);
+  int rc = spark_prove_core(ctx, S, ex, ey, evals, transcript->t, tape_h->t, w, ctx_shard(ctx));
   if (rc) return rc;
   *proof_len = w.out.size();
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");

@@ -89,3 +89,86 @@ def test_sharded_proof_matches_oracle(oracle, case):
 def test_sharded_bad_shard_fails_every_rank():
     res = _run("p3_uneven", 2, bad_shard=True)
     assert all(pf is None and err for _, pf, err in res), res
+
+
+# ---- sharded SPARK (SparseMatPolyEvalProof over W processes; multi_evaluate rows split) ----------
+SPARK_SHARD_CASES = {  # (R1CS shape as in r1cs_cases, world sizes)
+    "p2_x64_2secs": [2, 4, 3],
+    "p2_x256": [2, 4],
+    "p1_x16": [8],
+}
+
+
+def _spark_worker(rank, world, port, case, q):
+    import sys
+
+    sys.path[:0] = [os.path.join(ROOT, "spartan-parallel_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+
+    import numpy as np
+
+    import spg
+    import workload
+    from r1cs_cases import GPU_SPARK_CASES, SPARK_CASES
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cases = dict(SPARK_CASES, **GPU_SPARK_CASES)
+        nc, npf, nws, shared = cases[case]
+        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+        nx = (wl.max_num_cons - 1).bit_length()
+        ny = (wl.num_vars - 1).bit_length()
+        rx, ry = _spark_point(nx, ny)
+        ctx = spg.Context(0)
+        ctx.set_comm(rank, world, spg.torch_allgather(dist))
+        v = workload.CViews(wl)
+        gens_nnz = len(wl.entries) * max(max(int(m.shape[0]) for m in mats) for mats in wl.entries)
+        comm = spg.SparkCommitment(ctx, v.inst, b"gens_r1cs_eval", gens_nnz, 3)
+        inst = spg.R1CSInst(ctx, v.inst)
+        evals = spg.r1cs_multi_evaluate(ctx, inst, len(wl.entries), rx, ry)
+        proof = comm.prove(rx, ry, evals, spg.Transcript(b"spark_test"), spg.RandomTape(b"proof", workload.tape_seed()))
+        q.put((rank, comm.bytes, np.asarray(evals).tobytes(), proof, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spark_point(nx, ny):
+    import numpy as np
+
+    import pyoracle
+
+    rng = np.random.default_rng(3)
+    r = pyoracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * (nx + ny), dtype=np.uint8).tobytes())
+    return r[:nx], r[nx:]
+
+
+@pytest.mark.parametrize("case,world", [(c, w) for c, ws in sorted(SPARK_SHARD_CASES.items()) for w in ws])
+def test_sharded_spark_matches_oracle(oracle, case, world):
+    """every rank of a W-process SPARK proof emits the single-process oracle's commitment, evaluations and proof"""
+    import numpy as np
+
+    import workload
+    from test_oracle_spark import spark_inputs
+
+    wl, rx, ry = spark_inputs(oracle, case)
+    rcomm, ref, ok = oracle.spark_prove(wl, rx, ry, workload.tape_seed())
+    assert ok
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_spark_worker, args=(r, world, port, case, qq)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([qq.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    evs = {r[2] for r in res}
+    assert len(evs) == 1, "ranks disagree on multi_evaluate"
+    for rank, cm, _, pf, err in res:
+        assert err is None, err
+        assert cm == rcomm, f"rank {rank} commitment differs"
+        assert pf == ref, f"rank {rank} proof differs"

@@ -139,3 +139,16 @@ def test_msm_partial_shards(ctx, oracle, n, world):
     ref = oracle.msm_partial(pts[lo:hi], s[lo:hi])
     # same point, possibly different projective representative: compare encodings
     assert spg.points_sum_compress([parts[-1]]) == spg.points_sum_compress([ref])
+
+
+def test_commit_rows_wide(ctx, oracle):
+    """Hyrax rows of 2^14 scalars (window c = 14, 2^13 bucket counters) in batches of >= 64 rows take the LDS row
+    sort too (the SPARK derefs / comb_ops commitments at 2^24 nonzeros have such rows)"""
+    import spg
+
+    L, R = 64, 1 << 14
+    g = spg.Gens(ctx, R, b"spg_wide_rows")
+    pts = g.compressed()
+    Z = rand_fq(oracle, np.random.default_rng(14), L * R)
+    Z[5 * R: 6 * R] = 0
+    assert np.array_equal(g.commit_rows(Z, L, R), oracle.commit_rows(pts[:R], pts[R].tobytes(), Z, L, R))
