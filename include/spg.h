@@ -41,12 +41,17 @@ const char* spg_last_error(const spg_ctx* ctx);
 /* device-side wall time of the most recent compute call, in microseconds (HIP events on the stream) */
 double spg_last_kernel_us(const spg_ctx* ctx);
 
-/* Multi-process proving: one process (and context) per GPU. R1CSProof::prove is then sharded by instance
- * p: rank r holds instances [b(r), b(r+1)) with b(r) = r*floor(P/n) + min(r, P mod n) (the first P mod n
- * ranks hold one more; spg.shard_range) and every rank runs the same Fiat-Shamir transcript. A sharded
- * spg_r1cs_prove first allgathers every rank's argument check, so a bad argument on one rank fails all of
- * them (SPG_E_ARG) rather than leaving the others blocked. fn(user, send, bytes, recv) must place the `bytes` sent by rank k at recv + k*bytes on every
- * rank (an allgather, e.g. RCCL / torch.distributed); it returns 0 on success. nranks == 1 clears it. */
+/* Multi-process proving: one process (and context) per GPU; with nranks > 1 the calls below become SPMD
+ * collectives (every rank makes the same call with the same public arguments and runs the same Fiat-Shamir
+ * transcript; every exchange carries each rank's status, so a failure on one rank fails all of them):
+ *  - spg_r1cs_prove is sharded by instance p: rank r holds instances [b(r), b(r+1)) with
+ *    b(r) = r*floor(P/n) + min(r, P mod n) (spg.shard_range); the argument check is allgathered first.
+ *  - spg_spark_commit / spg_spark_prove (every rank holds the whole dense representation): Hyrax rows are
+ *    split, product trees are interleaved by the low lg n index bits (n a power of two; otherwise they stay
+ *    whole), layer rounds and hash-layer evaluations sum partials; every rank returns the same bytes.
+ *  - spg_r1cs_multi_evaluate splits every matrix's rows and sums the 3P partial evaluations.
+ * fn(user, send, bytes, recv) must place the `bytes` sent by rank k at recv + k*bytes on every rank (an
+ * allgather, e.g. RCCL / torch.distributed); it returns 0 on success. nranks == 1 clears it. */
 typedef int (*spg_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
 int spg_set_comm(spg_ctx* ctx, int rank, int nranks, spg_allgather_fn fn, void* user);
 

@@ -37,6 +37,27 @@ int main() {
   printf("transcript append point %.3f us\n", us_per(20000, [&](int) { t.point("comm", Pt{}); }));
   printf("transcript challenge    %.3f us\n", us_per(20000, [&](int) { a = fq_add(a, t.challenge("c")); }));
   printf("pool burst (16 x no-op) %.3f us\n", us_per(2000, [&](int) { pool().parallel_for(16, [](int) {}); }));
+  // sigma-protocol commitment bursts as the ZK sumcheck rounds issue them (HostGens::commit_many)
+  std::vector<uint8_t> comp;
+  h::HExt Q = P;
+  for (int i = 0; i < 8; i++) {
+    Pt c = compress(Q);
+    comp.insert(comp.end(), c.b, c.b + 32);
+    Q = h::hext_add(Q, P);
+  }
+  HostGens hg;
+  hg.init(comp.data(), 8);
+  FqV x(5);
+  for (int i = 0; i < 5; i++) x[i] = fq_add(k, fq_from_u64(i + 1));
+  using Job = std::pair<std::vector<size_t>, FqV>;
+  std::vector<Job> one5 = {{{0, 1, 2, 3, 7}, x}};
+  std::vector<Job> one2 = {{{4, 7}, {x[0], x[1]}}};
+  std::vector<Job> three = {{{4, 7}, {x[0], x[1]}}, {{0, 1, 2, 3, 7}, x}, {{4, 7}, {x[2], x[3]}}};
+  hg.commit_many(three);  // tables
+  printf("commit_many 1 x 5 terms  %.3f us\n", us_per(2000, [&](int) { sink ^= hg.commit_many(one5)[0].b[0]; }));
+  printf("commit_many 1 x 2 terms  %.3f us\n", us_per(2000, [&](int) { sink ^= hg.commit_many(one2)[0].b[0]; }));
+  printf("commit_many 3 jobs (2,5,2) %.3f us\n", us_per(2000, [&](int) { sink ^= hg.commit_many(three)[0].b[0]; }));
+  printf("sum_many 1 x 5 terms (no encoding) %.3f us\n", us_per(2000, [&](int) { acc = hg.sum_many(one5)[0]; }));
   printf("(sink %d %u)\n", (int)sink, a.l[0]);
   return 0;
 }

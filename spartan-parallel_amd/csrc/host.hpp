@@ -161,55 +161,93 @@ struct HostGens {
     for (size_t i = 0; i < idx.size(); i++) get(idx[i]).mul_add(acc, s[i]);
     return acc;
   }
-  // several independent commitments (index list, scalars) at once on the host pool, encoded. Every
-  // scalar multiple is split into kShares window ranges, so even a 2-term commitment keeps several cores
-  // busy: the pool's workers spin between the bursts of a sumcheck round, so a burst costs ~1 us to start.
+  // several independent commitments (index list, scalars) at once on the host pool, encoded
   std::vector<Pt> commit_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs) {
     std::vector<Pt> out(jobs.size());
-    run_many(jobs, [&](size_t j, const h::HExt& sum) { out[j] = compress(sum); });
+    run(jobs, nullptr, [&](size_t j, const h::HExt& sum) { out[j] = compress(sum); });
+    return out;
+  }
+  // the same with a precomputed point extra[j] added to commitment j before it is encoded
+  std::vector<Pt> commit_many_plus(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs, const h::HExt* extra) {
+    std::vector<Pt> out(jobs.size());
+    run(jobs, extra, [&](size_t j, const h::HExt& sum) { out[j] = compress(sum); });
     return out;
   }
   // the same sums left uncompressed (terms a caller adds to a device result before encoding it)
   std::vector<h::HExt> sum_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs) {
     std::vector<h::HExt> out(jobs.size());
-    run_many(jobs, [&](size_t j, const h::HExt& sum) { out[j] = sum; });
+    run(jobs, nullptr, [&](size_t j, const h::HExt& sum) { out[j] = sum; });
     return out;
   }
 
- private:
-  // one pool burst over every (job, term, window share); the last share of a job to finish (per-job
-  // countdown) adds the job's shares and hands the sum to done(job, sum)
+  // One pool burst over every (job, term, byte window) unit: the units are cut into at most one contiguous
+  // slice per pool thread (>= 8 windows each); a slice adds its units per job, and the last slice of a job to
+  // finish (per-job countdown) adds that job's slice sums (+ extra[j]) and hands them to done(job, sum), which
+  // may encode on that thread. A sumcheck round's few commitments thus keep every core busy for ~ (terms x 32
+  // / threads) mixed additions instead of queueing whole scalar multiples.
   template <class Done>
-  void run_many(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs, const Done& done) {
-    static const int kShares = 4;  // 8 byte-windows (<= 8 mixed additions) per task
-    std::vector<std::pair<size_t, size_t>> terms;  // (job, term)
-    for (size_t j = 0; j < jobs.size(); j++) {
+  void run(const std::vector<std::pair<std::vector<size_t>, FqV>>& jobs, const h::HExt* extra, const Done& done) {
+    const size_t J = jobs.size();
+    struct Term {
+      const FixedBase* fb;
+      uint8_t b[32];
+    };
+    std::vector<Term> terms;
+    std::vector<size_t> tfirst(J + 1, 0);  // terms of job j: [tfirst[j], tfirst[j + 1])
+    for (size_t j = 0; j < J; j++) {
       for (size_t i = 0; i < jobs[j].first.size(); i++) {
-        get(jobs[j].first[i]);  // build tables on this thread (map insertion is not thread-safe)
-        terms.push_back({j, i});
+        Term tm;
+        tm.fb = &get(jobs[j].first[i]);  // build tables on this thread (map insertion is not thread-safe)
+        fq_le_bytes(jobs[j].second[i], tm.b);
+        terms.push_back(tm);
       }
+      tfirst[j + 1] = terms.size();
     }
-    const int ntask = (int)terms.size() * kShares;
-    std::vector<h::HExt> part(ntask);
-    std::vector<int> first(jobs.size() + 1, 0);
-    for (size_t k = 0; k < terms.size(); k++) first[terms[k].first + 1] = (int)(k + 1) * kShares;
-    for (size_t j = 1; j <= jobs.size(); j++) first[j] = std::max(first[j], first[j - 1]);
-    std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[jobs.size()]);
-    for (size_t j = 0; j < jobs.size(); j++) {
-      left[j].store(first[j + 1] - first[j]);
-      if (first[j + 1] == first[j]) done(j, h::hext_identity());
+    const size_t U = 32 * terms.size();
+    const size_t threads = (size_t)pool().size() + 1;
+    const size_t S = std::max<size_t>(1, std::min(threads, U / 8));
+    auto slice_lo = [&](size_t s) { return U * s / S; };
+    // slices touching job j: [sfirst[j], slast[j]]
+    std::vector<size_t> sfirst(J), slast(J);
+    std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[J]);
+    for (size_t j = 0; j < J; j++) {
+      if (tfirst[j + 1] == tfirst[j]) {  // no terms: the extra point alone
+        done(j, extra ? extra[j] : h::hext_identity());
+        left[j].store(0);
+        continue;
+      }
+      const size_t u0 = 32 * tfirst[j], u1 = 32 * tfirst[j + 1] - 1;
+      size_t s0 = 0;
+      while (s0 + 1 < S && slice_lo(s0 + 1) <= u0) s0++;
+      size_t s1 = s0;
+      while (s1 + 1 < S && slice_lo(s1 + 1) <= u1) s1++;
+      sfirst[j] = s0;
+      slast[j] = s1;
+      left[j].store((int)(s1 - s0 + 1));
     }
-    pool().parallel_for(ntask, [&](int k) {
-      const auto& tm = terms[k / kShares];
-      const auto& jb = jobs[tm.first];
-      const int w0 = (k % kShares) * (32 / kShares);
-      h::HExt acc = h::hext_identity();
-      fb.find(jb.first[tm.second])->second.mul_add_windows(acc, jb.second[tm.second], w0, w0 + 32 / kShares);
-      part[k] = acc;
-      if (left[tm.first].fetch_sub(1, std::memory_order_acq_rel) == 1) {
-        h::HExt sum = part[first[tm.first]];
-        for (int i = first[tm.first] + 1; i < first[tm.first + 1]; i++) sum = h::hext_add(sum, part[i]);
-        done(tm.first, sum);
+    std::vector<h::HExt> part(S * std::max<size_t>(J, 1));
+    // the job of unit u
+    std::vector<size_t> tjob(terms.size());
+    for (size_t j = 0; j < J; j++)
+      for (size_t k = tfirst[j]; k < tfirst[j + 1]; k++) tjob[k] = j;
+    pool().parallel_for((int)S, [&](int si) {
+      const size_t s = (size_t)si, u0 = slice_lo(s), u1 = slice_lo(s + 1);
+      size_t u = u0;
+      while (u < u1) {
+        const size_t j = tjob[u / 32], ue = std::min(u1, 32 * tfirst[j + 1]);
+        h::HExt acc = h::hext_identity();
+        for (; u < ue; u++) {
+          const Term& tm = terms[u / 32];
+          const int w = (int)(u % 32);
+          if (tm.b[w]) acc = h::hext_madd(acc, tm.fb->tab[w * 256 + tm.b[w]]);
+        }
+        part[s * J + j] = acc;
+        if (left[j].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+          h::HExt sum = part[sfirst[j] * J + j];
+          for (size_t q = sfirst[j] + 1; q <= slast[j]; q++) sum = h::hext_add(sum, part[q * J + j]);
+          if (extra) sum = h::hext_add(sum, extra[j]);
+          done(j, sum);
+        }
       }
     });
   }

@@ -46,6 +46,7 @@ class Pool {
     cv_.notify_all();
     for (auto& t : threads_) t.join();
   }
+  int size() const { return (int)threads_.size(); }  // workers besides the calling thread
   // runs f(0) .. f(n-1) on the pool and the calling thread; returns when all are done
   void parallel_for(int n, const std::function<void(int)>& f) {
     if (n <= 1 || threads_.empty()) {

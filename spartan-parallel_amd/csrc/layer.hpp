@@ -229,20 +229,15 @@ __device__ __forceinline__ void quad_block_sum(Fq& e) {
     __syncthreads();
   }
 }
-template <int BS>
-__global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
-                                                      int nt, int log_len, int do_fold, Fq r, const Fq* __restrict__ cin,
-                                                      Fq* __restrict__ cout, Fq* __restrict__ partials,
-                                                      unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
-                                                      uint32_t seq, unsigned long long* probe) {
-  __shared__ bool last;
-  const int t = threadIdx.x, q = t & 3, len = 1 << log_len;
+// the elements u = u0, u0 + ustride, ... of one round (a quad per element): this lane's share of its point's sum
+__device__ __forceinline__ Fq layer_round_elems(const Triple* __restrict__ tr, const Fq* __restrict__ coeff, int nt,
+                                                int log_len, int do_fold, const Fq& r, const Fq* __restrict__ cin,
+                                                Fq* __restrict__ cout, long u0, long ustride) {
+  const int q = threadIdx.x & 3, len = 1 << log_len;
   const int pt = q < 3 ? q : 0;  // the evaluation point (and round-1 vector) this lane works on
-  unsigned long long* pr = probe ? probe + 8 * blockIdx.x : nullptr;
-  if (pr && t == 0) pr[0] = wall_clock64();
   const long total = (long)nt << log_len;
   Fq e = fq_zero();
-  for (long u = ((long)blockIdx.x * BS + t) >> 2; u < total; u += (long)gridDim.x * (BS / 4)) {
+  for (long u = u0; u < total; u += ustride) {
     const int c = (int)(u >> log_len), i = (int)(u & (len - 1));
     const Triple x = tr[c];
     const Fq* Cp = x.C ? x.C : cin;
@@ -266,6 +261,20 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
     const Fq k = coeff[c];
     e = fq_add(e, fq_mul(fq_mul(fq_mul(line_at(al, ah, pt), line_at(bl, bh, pt)), line_at(cl, ch, pt)), k));
   }
+  return e;
+}
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
+                                                      int nt, int log_len, int do_fold, Fq r, const Fq* __restrict__ cin,
+                                                      Fq* __restrict__ cout, Fq* __restrict__ partials,
+                                                      unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
+                                                      uint32_t seq, unsigned long long* probe) {
+  __shared__ bool last;
+  const int t = threadIdx.x, q = t & 3;
+  unsigned long long* pr = probe ? probe + 8 * blockIdx.x : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
+  Fq e = layer_round_elems(tr, coeff, nt, log_len, do_fold, r, cin, cout, ((long)blockIdx.x * BS + t) >> 2,
+                           (long)gridDim.x * (BS / 4));
   if (pr && t == 0) pr[1] = wall_clock64();
   quad_block_sum<BS>(e);
   if (pr && t == 0) pr[2] = wall_clock64();

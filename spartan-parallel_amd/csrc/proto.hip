@@ -129,25 +129,46 @@ ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, 
 }
 
 // src/nizk/mod.rs:306-370 (n = 4 in every sumcheck round). Cx_known: the caller already holds
-// x.commit(blind_x, gens_n) (the sumcheck round's comm_poly is exactly that commitment).
+// x.commit(blind_x, gens_n) (the sumcheck round's comm_poly is exactly that commitment). pre: the randomness
+// and its points were drawn / computed ahead (the tape is then not touched here; the caller advances it).
 DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyView& kn, Tr& t, Tape& tape, const FqV& x,
-                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y, const Pt* Cx_known) {
+                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y, const Pt* Cx_known,
+                                  const DotPre* pre) {
   t.protocol("dot product proof");
   size_t n = x.size();
-  FqV d = tape.vec("d_vec", n);
-  Fq r_delta = tape.scalar("r_delta"), r_beta = tape.scalar("r_beta");
-  Fq ad = dot(a, d, 0, 0, n);
-  std::vector<CJob> jobs = {CJob(k1, {y}, blind_y), CJob(kn, d, r_delta), CJob(k1, {ad}, r_beta)};
-  if (!Cx_known) jobs.push_back(CJob(kn, x, blind_x));
-  std::vector<Pt> c = commit_batch(g, jobs);
-  Pt Cx = Cx_known ? *Cx_known : c[3];
-  t.point("Cx", Cx);
-  t.point("Cy", c[0]);
-  t.scalars("a", a);
   DotProductProofP p;
-  p.delta = c[1];
+  Pt Cx, Cy;
+  FqV d;
+  Fq r_delta, r_beta;
+  if (pre && Cx_known) {
+    d = pre->d;
+    r_delta = pre->r_delta;
+    r_beta = pre->r_beta;
+    Fq ad = dot(a, d, 0, 0, n);
+    // Cy = y G_1 + blind_y h; beta = <a, d> G_1 + (r_beta h, precomputed)
+    const h::HExt ex[2] = {h::hext_identity(), pre->rbh};
+    std::vector<Pt> c = g.host.commit_many_plus({{{k1.G[0], k1.h}, {y, blind_y}}, {{k1.G[0]}, {ad}}}, ex);
+    Cx = *Cx_known;
+    Cy = c[0];
+    p.delta = pre->delta;
+    p.beta = c[1];
+  } else {
+    d = tape.vec("d_vec", n);
+    r_delta = tape.scalar("r_delta");
+    r_beta = tape.scalar("r_beta");
+    Fq ad = dot(a, d, 0, 0, n);
+    std::vector<CJob> jobs = {CJob(k1, {y}, blind_y), CJob(kn, d, r_delta), CJob(k1, {ad}, r_beta)};
+    if (!Cx_known) jobs.push_back(CJob(kn, x, blind_x));
+    std::vector<Pt> c = commit_batch(g, jobs);
+    Cx = Cx_known ? *Cx_known : c[3];
+    Cy = c[0];
+    p.delta = c[1];
+    p.beta = c[2];
+  }
+  t.point("Cx", Cx);
+  t.point("Cy", Cy);
+  t.scalars("a", a);
   t.point("delta", p.delta);
-  p.beta = c[2];
   t.point("beta", p.beta);
   Fq ch = t.challenge("c");
   p.z.resize(n);

@@ -122,9 +122,18 @@ EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape
                               const Fq& v2, const Fq& s2);
 ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& rX, const Fq& y,
                             const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z);
+// the prover randomness of one DotProductProof drawn ahead of time (d_vec, r_delta, r_beta from a fork of the
+// RandomTape at the same position) with its randomness-only points: delta = d.commit(r_delta, gens_n) and
+// r_beta * h of gens_1
+struct DotPre {
+  FqV d;
+  Fq r_delta, r_beta;
+  Pt delta;
+  h::HExt rbh;
+};
 DotProductProofP dotproduct_prove(ProverGens& g, const KeyView& k1, const KeyView& kn, Tr& t, Tape& tape, const FqV& x,
-                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y,
-                                  const Pt* Cx_known = nullptr);
+                                  const Fq& blind_x, const FqV& a, const Fq& y, const Fq& blind_y, const Pt* Cx_known,
+                                  const DotPre* pre = nullptr);
 // ---- DotProductProofLog with all MSMs on the GPU over the original generators ----
 int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const FqV& x, const Fq& blind_x, const FqV& a,
                          const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy);

@@ -224,7 +224,13 @@ __global__ void __launch_bounds__(256) k_sum_segments(const Fq* __restrict__ par
 
 // UniPoly::from_evals for degree 3 (unipoly.rs:23-54) and evaluate (:72-80)
 
-// ZK sumcheck round bookkeeping shared by phase 1 and phase 2 (sumcheck.rs:1247-1370)
+// ZK sumcheck round bookkeeping shared by phase 1 and phase 2 (sumcheck.rs:1247-1370).
+// The RandomTape is a transcript that only ever absorbs labels, so the values a round draws do not depend on
+// the proof: init() draws blinds_poly / blinds_evals as the reference does, then reads every round's
+// DotProductProof randomness (d_vec, r_delta, r_beta) from a copy of the tape at that position and computes,
+// in one host burst, the points that depend on randomness alone (blind * h terms, delta). The rounds then
+// commit only their data-dependent terms, and the tape continues from the copy's final state after the last
+// round (no other draw happens between the rounds), so proofs are byte-identical.
 struct ZKRounds {
   FqV blinds_poly, blinds_evals;
   Fq claim, blind_claim;
@@ -232,25 +238,73 @@ struct ZKRounds {
   ZKSumcheckP out;
   FqV poly;
   Pt comm_poly;
+  std::vector<DotPre> pre;
+  std::vector<h::HExt> hp, he;  // blinds_poly[j] * h (gens_4), blinds_evals[j] * h (gens_1)
+  Tape tape_end{"", fq_zero()};
+  bool ahead = false;
   void init(ProverGens& g, Tape& tape, size_t rounds, const Fq& c, const Fq& b) {
     blinds_poly = tape.vec("blinds_poly", rounds);
     blinds_evals = tape.vec("blinds_evals", rounds);
     claim = c;
     blind_claim = b;
-    comm_claim = commit_batch(g, {CJob(g.gens_1, {c}, b)})[0];
+    static const bool on = !getenv("SPG_TAPE_AHEAD") || atoi(getenv("SPG_TAPE_AHEAD")) != 0;
+    ahead = on && rounds > 0 && g.gens_4.G.size() == 4;
+    if (!ahead) {
+      comm_claim = commit_batch(g, {CJob(g.gens_1, {c}, b)})[0];
+      return;
+    }
+    tape_end = tape;
+    pre.resize(rounds);
+    for (size_t j = 0; j < rounds; j++) {
+      pre[j].d = tape_end.vec("d_vec", 4);
+      pre[j].r_delta = tape_end.scalar("r_delta");
+      pre[j].r_beta = tape_end.scalar("r_beta");
+    }
+    hp.resize(rounds);
+    he.resize(rounds);
+    // jobs: comm_claim, then per round blinds_poly h4, blinds_evals h1, r_beta h1, delta (d G4 + r_delta h4)
+    std::vector<std::pair<std::vector<size_t>, FqV>> jobs;
+    jobs.push_back({{g.gens_1.G[0], g.gens_1.h}, {c, b}});
+    for (size_t j = 0; j < rounds; j++) {
+      jobs.push_back({{g.gens_4.h}, {blinds_poly[j]}});
+      jobs.push_back({{g.gens_1.h}, {blinds_evals[j]}});
+      jobs.push_back({{g.gens_1.h}, {pre[j].r_beta}});
+      std::vector<size_t> idx(g.gens_4.G.begin(), g.gens_4.G.end());
+      idx.push_back(g.gens_4.h);
+      FqV sc = pre[j].d;
+      sc.push_back(pre[j].r_delta);
+      jobs.push_back({idx, sc});
+    }
+    g.host.run(jobs, nullptr, [&](size_t k, const h::HExt& sum) {
+      if (k == 0) {
+        comm_claim = compress(sum);
+        return;
+      }
+      const size_t j = (k - 1) / 4;
+      switch ((k - 1) % 4) {
+        case 0: hp[j] = sum; break;
+        case 1: he[j] = sum; break;
+        case 2: pre[j].rbh = sum; break;
+        default: pre[j].delta = compress(sum);
+      }
+    });
   }
   // commit the round polynomial and draw r_j
   Fq begin(ProverGens& g, Tr& t, size_t j, const Fq e[3]) {
     Fq ev[4] = {e[0], fq_sub(claim, e[0]), e[1], e[2]};
     poly = uni_from_evals3(ev);
-    comm_poly = commit_batch(g, {CJob(g.gens_4, poly, blinds_poly[j])})[0];
+    if (ahead)
+      comm_poly = g.host.commit_many_plus({{g.gens_4.G, poly}}, &hp[j])[0];
+    else
+      comm_poly = commit_batch(g, {CJob(g.gens_4, poly, blinds_poly[j])})[0];
     t.point("comm_poly", comm_poly);
     out.comm_polys.push_back(comm_poly);
     return t.challenge("challenge_nextround");
   }
   void finish(ProverGens& g, Tr& t, Tape& tape, size_t j, const Fq& r_j) {
     Fq eval = uni_eval(poly, r_j);
-    Pt comm_eval = commit_batch(g, {CJob(g.gens_1, {eval}, blinds_evals[j])})[0];
+    Pt comm_eval = ahead ? g.host.commit_many_plus({{{g.gens_1.G[0]}, {eval}}}, &he[j])[0]
+                         : commit_batch(g, {CJob(g.gens_1, {eval}, blinds_evals[j])})[0];
     t.point("comm_claim_per_round", comm_claim);
     t.point("comm_eval", comm_eval);
     FqV w = t.challenges("combine_two_claims_to_one", 2);
@@ -265,15 +319,14 @@ struct ZKRounds {
       a[k] = fq_add(fq_mul(w[0], a_sc), fq_mul(w[1], pw));
       pw = fq_mul(pw, r_j);
     }
-    out.proofs.push_back(
-        dotproduct_prove(g, g.gens_1, g.gens_4, t, tape, poly, blinds_poly[j], a, target, blind, &comm_poly));
+    out.proofs.push_back(dotproduct_prove(g, g.gens_1, g.gens_4, t, tape, poly, blinds_poly[j], a, target, blind,
+                                          &comm_poly, ahead ? &pre[j] : nullptr));
+    if (ahead && j + 1 == pre.size()) tape = tape_end;  // past every round's draws
     claim = eval;
     comm_claim = comm_eval;
     out.comm_evals.push_back(comm_eval);
   }
 };
-
-
 
 // host wall-clock breakdown of one prove (printed to stderr when SPG_TRACE is set)
 
@@ -553,7 +606,6 @@ int Prover::run_inner(Laps& lp) {
   {
     size_t rounds = nx + nq + np;
     ZKRounds zk;
-    zk.init(g, tape, rounds, fq_zero(), fq_zero());
     size_t cons_len = (size_t)1 << nx, proof_len = (size_t)1 << nq, instance_len = (size_t)1 << np;
     size_t lenP = instance_len, lenQ = proof_len, lenX = cons_len;
     std::vector<size_t> sc_np = l_proofs, sc_nc = l_cons;  // local; P rounds use all-ones of length P
@@ -605,6 +657,7 @@ int Prover::run_inner(Laps& lp) {
     if (rounds && nx + nq == 0) rc = to_compact();
     if (!rc && rounds) rc = launch_eval(0);
     if (rc) return rc;
+    zk.init(g, tape, rounds, fq_zero(), fq_zero());  // host precomputation while round 0 evaluates
     for (size_t j = 0; j < rounds; j++) {
       int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       Fq e[3];
@@ -733,7 +786,6 @@ int Prover::run_inner(Laps& lp) {
   {
     size_t rounds = ny + nw + np;
     ZKRounds zk;
-    zk.init(g, tape, rounds, claim2, blind2);
     size_t inputs_len = (size_t)1 << ny, ws_len = (size_t)1 << nw, instance_len = (size_t)1 << np;
     size_t lenP = instance_len;
     std::vector<size_t> sc_ni = l_inputs;
@@ -777,6 +829,7 @@ int Prover::run_inner(Laps& lp) {
     if (rounds && ny + nw == 0) rc = to_compact();
     if (!rc && rounds) rc = launch_eval(0);
     if (rc) return rc;
+    zk.init(g, tape, rounds, claim2, blind2);  // host precomputation while round 0 evaluates
     for (size_t j = 0; j < rounds; j++) {
       int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       Fq e[3];

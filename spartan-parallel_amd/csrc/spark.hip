@@ -556,9 +556,33 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     FqV r_prod;
     bool pending = false;  // a bound_poly_var_top with r_pend not yet applied
     Fq r_pend = fq_zero();
-    // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks
-    auto run_rounds = [&](size_t log_len, bool local) -> int {
-      while (log_len-- > 0) {
+    // A[0], B[0], C[0] of every triple (after the pending fold, if any), by mailbox
+    auto close = [&](FqV& fin) -> int {
+      fin.resize(3 * tr.size());
+      KScope ks(ctx, "spark_layer_close");
+      const uint32_t seq = ++ctx->mbox_seq;
+      hipLaunchKernelGGL(k_layer_close, dim3(1), dim3(256), 0, s, dtr, (int)tr.size(), pending ? 1 : 0, r_pend,
+                         cbuf[cur], ctx->d_mbox, seq);
+      SPG_HIP(ctx, hipGetLastError());
+      pending = false;
+      return mbox_wait(ctx, seq, fin.data(), (int)fin.size());
+    };
+    // the host half of a round: UniPoly from (e0, e2, e3), transcript, r_j
+    auto host_round = [&](const Fq ev[3]) -> Fq {
+      Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
+      FqV poly = uni_from_evals3(evals);
+      append_unipoly(t, poly);
+      Fq r_j = t.challenge("challenge_nextround");
+      r_prod.push_back(r_j);
+      e = uni_eval(poly, r_j);
+      lpf.polys.push_back({poly[0], poly[2], poly[3]});
+      return r_j;
+    };
+    // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks; with
+    // close_after the layer's (or the shard's) final entries follow in `fin`
+    auto run_rounds = [&](size_t log_len, bool local, bool close_after, FqV* fin) -> int {
+      while (log_len > 0) {
+        log_len--;
         const size_t len = (size_t)1 << log_len;
         unsigned K;
         int BS;
@@ -594,37 +618,20 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         if (local) rc2 = comm_sum_fq(ctx, sh, rc2, ev, 3);
         if (rc2) return rc2;
         lp.lap("round_eval_wait");
-        Fq evals[4] = {ev[0], fq_sub(e, ev[0]), ev[1], ev[2]};
-        FqV poly = uni_from_evals3(evals);
-        append_unipoly(t, poly);
-        Fq r_j = t.challenge("challenge_nextround");
-        r_prod.push_back(r_j);
+        r_pend = host_round(ev);
         pending = true;
-        r_pend = r_j;
-        e = uni_eval(poly, r_j);
-        lpf.polys.push_back({poly[0], poly[2], poly[3]});
         lp.lap("round_host");
       }
-      return 0;
+      return close_after ? close(*fin) : 0;
     };
-    // A[0], B[0], C[0] of every triple (after the pending fold, if any), by mailbox
-    auto close = [&](FqV& fin) -> int {
-      fin.resize(3 * tr.size());
-      KScope ks(ctx, "spark_layer_close");
-      const uint32_t seq = ++ctx->mbox_seq;
-      hipLaunchKernelGGL(k_layer_close, dim3(1), dim3(256), 0, s, dtr, (int)tr.size(), pending ? 1 : 0, r_pend,
-                         cbuf[cur], ctx->d_mbox, seq);
-      SPG_HIP(ctx, hipGetLastError());
-      pending = false;
-      return mbox_wait(ctx, seq, fin.data(), (int)fin.size());
-    };
+    FqV fin;
     if (sharded) {
-      rc = run_rounds(lg2(hl), true);
       // gather: every vector has one entry per rank left; rank q's entry is global index q
       FqV mine;
-      if (!rc) rc = close(mine);
+      rc = run_rounds(lg2(hl), true, true, &mine);
+      mine.resize(3 * tr.size(), fq_zero());
       std::vector<uint8_t> all;
-      rc = comm_allgather(ctx, sh, rc, mine.data(), mine.size() * sizeof(Fq), all);
+      rc = comm_allgather(ctx, sh, rc, mine.data(), 3 * tr.size() * sizeof(Fq), all);
       if (rc) return rc;
       const Fq* g = (const Fq*)all.data();
       const size_t nt = tr.size();
@@ -643,14 +650,10 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       SPG_HIP(ctx, hipMemcpyAsync(gbuf, hv, 3 * nt * W * sizeof(Fq), hipMemcpyHostToDevice, s));
       if (nc)  // the product circuits' shared eq vector (every product triple gathered the same entries)
         SPG_HIP(ctx, hipMemcpyAsync(cbuf[cur], gbuf + 2 * W, W * sizeof(Fq), hipMemcpyDeviceToDevice, s));
-      rc = run_rounds(lgW, false);
+      rc = run_rounds(lgW, false, true, &fin);
     } else {
-      rc = run_rounds(lg2(hl), false);
+      rc = run_rounds(lg2(hl), false, true, &fin);
     }
-    if (rc) return rc;
-    // the last round's fold and the final claims A[0], B[0] (C[0] for the dot-product circuits), by mailbox
-    FqV fin;
-    rc = close(fin);
     if (rc) return rc;
     for (size_t c = 0; c < nc; c++) {
       lpf.left.push_back(fin[3 * c]);

@@ -120,3 +120,118 @@ def test_shard_chunks_cover():
             assert cs[0][0] == 0 and cs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(cs, cs[1:]))
             assert max(h - l for l, h in cs) - min(h - l for l, h in cs) <= 1
+
+
+# ---- sharded SPARK layout (spark.hip "sharded proof"), restated with Python integers mod q on gloo ranks -----
+Qmod = 2**252 + 27742317777372353535851937790883648493
+
+
+def _eq(r, n):
+    """EqPolynomial::evals (src/dense_mlpoly.rs:76-92), r[0] the most significant bit"""
+    out = []
+    for b in range(1 << n):
+        acc = 1
+        for j in range(n):
+            acc = acc * (r[j] if (b >> (n - 1 - j)) & 1 else 1 - r[j]) % Qmod
+        out.append(acc)
+    return out
+
+
+def _layer_rounds(A, B, C, rs, W=1, sum_fn=None):
+    """prove_cubic_batched rounds (src/sumcheck.rs:264-434) of one (A, B, C) triple, binding the top variable;
+    returns [(e0, e2, e3)] per round (summed over ranks by sum_fn) and the folded vectors"""
+    evs = []
+    for r in rs:
+        ln = len(A) // 2
+        e = [0, 0, 0]
+        for i in range(ln):
+            for k, x in enumerate((0, 2, 3)):
+                a = A[i] + x * (A[i + ln] - A[i])
+                b = B[i] + x * (B[i + ln] - B[i])
+                c = C[i] + x * (C[i + ln] - C[i])
+                e[k] = (e[k] + a * b * c) % Qmod
+        if sum_fn:
+            e = sum_fn(e)
+        evs.append(tuple(e))
+        A = [(A[i] + r * (A[i + ln] - A[i])) % Qmod for i in range(ln)]
+        B = [(B[i] + r * (B[i + ln] - B[i])) % Qmod for i in range(ln)]
+        C = [(C[i] + r * (C[i + ln] - C[i])) % Qmod for i in range(ln)]
+    return evs, (A, B, C)
+
+
+def _tree_worker(rank, world, port, q):
+    import random
+
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rnd = random.Random(11)
+        M = 32
+        leaves = [rnd.randrange(Qmod) for _ in range(M)]
+        # local product tree over leaves i = W i' + r (ProductCircuit::compute_layer keeps the low bits)
+        v = leaves[rank::world]
+        while len(v) > 1:
+            h = len(v) // 2
+            v = [v[i] * v[i + h] % Qmod for i in range(h)]
+        level = [None] * world
+        dist.all_gather_object(level, v[0])  # the global level of W entries, index = rank
+
+        def allsum(e):
+            parts = [None] * world
+            dist.all_gather_object(parts, e)
+            return [sum(p[k] for p in parts) % Qmod for k in range(3)]
+
+        # layer 0 of the circuit: left / right halves of the leaves, eq over lg(M/2) variables
+        half = M // 2
+        lgh, lgw = half.bit_length() - 1, world.bit_length() - 1
+        rand = [rnd.randrange(Qmod) for _ in range(lgh)]
+        rs = [rnd.randrange(Qmod) for _ in range(lgh)]
+        left, right = leaves[:half], leaves[half:]
+        # local shares: left/right keep i = W i' + r; eq share = eq(rand_hi) * eq(rand_lo)[r]
+        sc = _eq(rand[lgh - lgw:], lgw)[rank]
+        Cl = [x * sc % Qmod for x in _eq(rand[:lgh - lgw], lgh - lgw)]
+        nloc = lgh - lgw
+        ev_loc, (Af, Bf, Cf) = _layer_rounds(left[rank::world], right[rank::world], Cl, rs[:nloc], sum_fn=allsum)
+        g = [None] * world
+        dist.all_gather_object(g, (Af[0], Bf[0], Cf[0]))  # the gather: one entry per rank, index = rank
+        ev_rep, fin = _layer_rounds([x[0] for x in g], [x[1] for x in g], [x[2] for x in g], rs[nloc:])
+        q.put((rank, level, ev_loc + ev_rep, [f[0] for f in fin]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_interleaved_product_tree_shards(world):
+    """the sharded SPARK layout (spark.hip spark_prove_core / batched_prove_fused): interleaved local product
+    trees meet the global tree's W-entry level, and local layer rounds summed over gloo ranks + gathered tail
+    rounds give the unsharded round polynomials and final claims"""
+    import random
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_tree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    rnd = random.Random(11)
+    M = 32
+    leaves = [rnd.randrange(Qmod) for _ in range(M)]
+    v = leaves
+    while len(v) > world:
+        h = len(v) // 2
+        v = [v[i] * v[i + h] % Qmod for i in range(h)]
+    half = M // 2
+    lgh = half.bit_length() - 1
+    rand = [rnd.randrange(Qmod) for _ in range(lgh)]
+    rs = [rnd.randrange(Qmod) for _ in range(lgh)]
+    ev, fin = _layer_rounds(leaves[:half], leaves[half:], _eq(rand, lgh), rs)
+    for rank, level, evs, f in res:
+        assert level == v, rank
+        assert evs == ev, rank
+        assert f == [x[0] for x in fin], rank
