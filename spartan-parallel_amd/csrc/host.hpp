@@ -205,7 +205,8 @@ struct HostGens {
     }
     const size_t U = 32 * terms.size();
     const size_t threads = (size_t)pool().size() + 1;
-    const size_t S = std::max<size_t>(1, std::min(threads, U / 8));
+    static const size_t min_slice = getenv("SPG_SLICE_MIN") ? (size_t)atol(getenv("SPG_SLICE_MIN")) : 8;
+    const size_t S = std::max<size_t>(1, std::min(threads, U / min_slice));
     auto slice_lo = [&](size_t s) { return U * s / S; };
     // slices touching job j: [sfirst[j], slast[j]]
     std::vector<size_t> sfirst(J), slast(J);

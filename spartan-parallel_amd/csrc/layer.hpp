@@ -322,4 +322,105 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   }
 }
 
+// ---- big rounds: one thread per index i over every product circuit (throughput form) -----------------------------
+// Triples 0 .. np-1 share the eq vector C (cin -> cout); since e_X = sum_i C_i(X) sum_c k_c A_c(X) B_c(X), the
+// thread for index i folds C once, then per circuit folds A and B, scales A's two entries by k_c and adds the three
+// products A(X) B(X) (X = 0, 2, 3); C(X) multiplies the sums once. Triples np .. nt-1 (dot-product circuits, own C)
+// take one thread per (triple, i). About 9 products per circuit and index instead of the quad form's 20 lane
+// products, for rounds large enough to fill the chip; the reduction (block sums, ticket, mailbox) is k_layer_round's.
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_round_wide(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
+                                                         int np, int nt, int log_len, int do_fold, Fq r,
+                                                         const Fq* __restrict__ cin, Fq* __restrict__ cout,
+                                                         Fq* __restrict__ partials, unsigned* __restrict__ counter,
+                                                         uint32_t* __restrict__ mb, uint32_t seq) {
+  const int t = threadIdx.x, len = 1 << log_len;
+  const int ng = (np > 0 ? 1 : 0) + (nt - np);
+  const long total = (long)ng << log_len;
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  auto load2 = [&](const Fq* p, Fq* w, int i, Fq& lo, Fq& hi) {
+    if (do_fold) {
+      lo = fold_at(p, i, 2 * len, r);
+      hi = fold_at(p, i + len, 2 * len, r);
+      if (w) {
+        w[i] = lo;
+        w[i + len] = hi;
+      }
+    } else {
+      lo = p[i];
+      hi = p[i + len];
+    }
+  };
+  for (long u = (long)blockIdx.x * BS + t; u < total; u += (long)gridDim.x * BS) {
+    const int g = (int)(u >> log_len), i = (int)(u & (len - 1));
+    if (np > 0 && g == 0) {
+      Fq cl, ch;
+      load2(cin, cout, i, cl, ch);
+      Fq s0 = fq_zero(), s2 = fq_zero(), s3 = fq_zero();
+      for (int c = 0; c < np; c++) {
+        const Triple x = tr[c];
+        const Fq k = coeff[c];
+        Fq al, ah, bl, bh;
+        load2(x.A, x.A, i, al, ah);
+        load2(x.B, x.B, i, bl, bh);
+        al = fq_mul(k, al);
+        ah = fq_mul(k, ah);
+        const Fq da = fq_sub(ah, al), db = fq_sub(bh, bl);
+        const Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db);
+        s0 = fq_add(s0, fq_mul(al, bl));
+        s2 = fq_add(s2, fq_mul(a2, b2));
+        s3 = fq_add(s3, fq_mul(fq_add(a2, da), fq_add(b2, db)));
+      }
+      const Fq dc = fq_sub(ch, cl), c2 = fq_add(ch, dc);
+      e0 = fq_add(e0, fq_mul(s0, cl));
+      e2 = fq_add(e2, fq_mul(s2, c2));
+      e3 = fq_add(e3, fq_mul(s3, fq_add(c2, dc)));
+    } else {
+      const int c = np + g - (np > 0 ? 1 : 0);
+      const Triple x = tr[c];
+      const Fq k = coeff[c];
+      Fq al, ah, bl, bh, cl, ch;
+      load2(x.A, x.A, i, al, ah);
+      load2(x.B, x.B, i, bl, bh);
+      load2(x.C, x.C, i, cl, ch);
+      al = fq_mul(k, al);
+      ah = fq_mul(k, ah);
+      const Fq da = fq_sub(ah, al), db = fq_sub(bh, bl), dc = fq_sub(ch, cl);
+      const Fq a2 = fq_add(ah, da), b2 = fq_add(bh, db), c2 = fq_add(ch, dc);
+      e0 = fq_add(e0, fq_mul(fq_mul(al, bl), cl));
+      e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
+      e3 = fq_add(e3, fq_mul(fq_mul(fq_add(a2, da), fq_add(b2, db)), fq_add(c2, dc)));
+    }
+  }
+  block_sum3_t0<BS>(e0, e2, e3);
+  __shared__ bool last;
+  if (t == 0) {
+    partials[3 * blockIdx.x] = e0;
+    partials[3 * blockIdx.x + 1] = e2;
+    partials[3 * blockIdx.x + 2] = e3;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  Fq a = fq_zero(), b = fq_zero(), cc = fq_zero();
+  for (unsigned j = t; j < gridDim.x; j += BS) {
+    a = fq_add(a, partials[3 * j]);
+    b = fq_add(b, partials[3 * j + 1]);
+    cc = fq_add(cc, partials[3 * j + 2]);
+  }
+  block_sum3_t0<BS>(a, b, cc);
+  if (t == 0) {
+    const Fq rr[3] = {a, b, cc};
+    mbox_post(mb, seq, rr, 3);
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 }  // namespace spg

@@ -587,15 +587,26 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         unsigned K;
         int BS;
         static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
-        if (quad) {  // a quad per element, about one element per quad
+        static const size_t wide_min = getenv("SPG_WIDE_MIN") ? (size_t)atol(getenv("SPG_WIDE_MIN")) : ((size_t)1 << 19);
+        const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
+        // algorithmic HBM bytes of the round: per distinct vector (A, B of every triple; the shared C once; each
+        // dot-product circuit's own C) and index, 2 entries read, or with the pending fold 4 read + 2 written
+        const double layer_bytes = (pending ? 192.0 : 64.0) * (double)len * (double)(2 * tr.size() + ngroups);
+        if (ngroups * len >= wide_min) {  // throughput form for rounds that fill the chip
+          K = (unsigned)std::min<size_t>((ngroups * len + 255) / 256, 2048);
+          KScope ks(ctx, "spark_layer_round", layer_bytes);
+          hipLaunchKernelGGL(k_layer_round_wide<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, (int)nc, (int)tr.size(),
+                             (int)log_len, pending ? 1 : 0, r_pend, cbuf[cur], cbuf[cur ^ 1], part, ctx->d_counter,
+                             ctx->d_mbox, ++ctx->mbox_seq);
+        } else if (quad) {  // a quad per element, about one element per quad
           const size_t Wd = tr.size() * len;
           BS = Wd <= 16 ? 64 : 256;
           K = (unsigned)std::min<size_t>((Wd * 4 + BS - 1) / BS, 2048);
         } else {
           layer_grid(tr.size() * len, &K, &BS);
         }
-        {
-          KScope ks(ctx, "spark_layer_round", 192.0 * tr.size() * len * (pending ? 2.0 : 1.0));
+        if (ngroups * len < wide_min) {
+          KScope ks(ctx, "spark_layer_round", layer_bytes);
           const int nt = (int)tr.size(), lg = (int)log_len, df = pending ? 1 : 0;
           const uint32_t seq = ++ctx->mbox_seq;
           if (quad && BS == 64)

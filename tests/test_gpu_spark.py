@@ -71,3 +71,32 @@ def test_spark_repeatable(ctx, oracle):
     a = gpu_spark(ctx, wl, rx, ry, workload.tape_seed())
     b = gpu_spark(ctx, wl, rx, ry, workload.tape_seed())
     assert a == b
+
+
+@pytest.mark.parametrize("env", [{"SPG_WIDE_MIN": "1"}, {"SPG_LAYER_QUAD": "0", "SPG_WIDE_MIN": "1000000000000"}])
+def test_spark_round_kernel_forms(oracle, env):
+    """every layer round through the throughput form (k_layer_round_wide, normally only for rounds that fill the
+    chip) or through the one-lane form: same proof bytes as the oracle (a fresh process reads the switches)"""
+    import subprocess
+    import sys
+
+    import workload
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, hashlib; sys.path[:0] = [%r, %r, %r]\n"
+        "import spg, workload\n"
+        "from test_oracle_spark import spark_inputs\n"
+        "from test_gpu_spark import gpu_spark\n"
+        "import pyoracle\n"
+        "wl, rx, ry = spark_inputs(pyoracle, 'p2_x64_2secs')\n"
+        "ctx = spg.Context(0)\n"
+        "c, p = gpu_spark(ctx, wl, rx, ry, workload.tape_seed())\n"
+        "print(hashlib.sha256(p).hexdigest())\n"
+    ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "tests"), os.path.join(root, "oracle"))
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    wl, rx, ry = spark_inputs(oracle, "p2_x64_2secs")
+    _, ref, ok = oracle.spark_prove(wl, rx, ry, workload.tape_seed())
+    assert ok and out.stdout.split()[-1] == hashlib.sha256(ref).hexdigest()
