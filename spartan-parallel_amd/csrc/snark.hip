@@ -790,7 +790,15 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   cq.add(perm_w0, &c_w0);
   const Rows& exec = W->exec;
   Rows pe_w2(consis), pe_w3(consis);
-  for (size_t q = 0; q < consis; q++) {
+  // rows are independent except the reverse-q recurrence of w3[3] (and w3[2]): the per-row work runs on the
+  // host pool in chunks, the recurrence (2 products per row) afterwards in order
+  auto par_rows = [](size_t n, const std::function<void(size_t)>& f) {
+    const int C = n >= 64 ? 8 : 1;
+    pool().parallel_for(C, [&](int c) {
+      for (size_t q = n * c / C; q < n * (c + 1) / C; q++) f(q);
+    });
+  };
+  par_rows(consis, [&](size_t q) {
     FqV v(3, fq_zero());
     for (size_t j = 1; j < 2 * niu - 2; j++) v.push_back(fq_mul(perm_w0[j], exec[q][j + 2]));
     v.resize(num_ios, fq_zero());
@@ -803,19 +811,20 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     }
     v[0] = fq_mul(v[0], exec[q][0]);
     v[1] = fq_mul(fq_add(v[1], v[2]), exec[q][0]);
-    pe_w2[q] = v;
-  }
-  for (size_t q = consis; q-- > 0;) {
     FqV w(8, fq_zero());
     w[0] = exec[q][0];
     Fq sacc = fq_zero();
-    for (size_t k = 3; k < pe_w2[q].size(); k++) sacc = fq_add(sacc, pe_w2[q][k]);
+    for (size_t k = 3; k < v.size(); k++) sacc = fq_add(sacc, v[k]);
     w[1] = fq_mul(w[0], fq_sub(fq_sub(tau, sacc), exec[q][2]));
-    w[4] = pe_w2[q][0];
-    w[5] = pe_w2[q][1];
+    w[4] = v[0];
+    w[5] = v[1];
+    pe_w2[q] = std::move(v);
+    pe_w3[q] = std::move(w);
+  });
+  for (size_t q = consis; q-- > 0;) {
+    FqV& w = pe_w3[q];
     w[3] = q != consis - 1 ? fq_mul(w[1], fq_sub(fq_add(pe_w3[q + 1][2], fq_one()), pe_w3[q + 1][0])) : w[1];
     w[2] = fq_mul(w[0], w[3]);
-    pe_w3[q] = w;
   }
   std::vector<Rows> pe_w2v = {pe_w2}, pe_w3v = {pe_w3}, pe_w3sv = {shift_rows(pe_w3, 8)};
   std::vector<FqV> pe_p2 = {pad_pow2(flatten(pe_w2))}, pe_p3 = {pad_pow2(flatten(pe_w3))},
@@ -840,7 +849,8 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     b_w2[p].assign(Q, FqV());
     b_w3[p].assign(Q, FqV());
     FqV zero_row(keep, fq_zero());
-    for (size_t q = Q; q-- > 0;) {
+    std::vector<Fq> pxs(Q), vxs(Q);  // the chain ends read by the reverse-q recurrences
+    par_rows(Q, [&](size_t q) {  // everything of row q that does not depend on row q + 1
       const FqV& bv = q < bio.size() ? bio[q] : zero_row;
       const Fq V_CNST = bv[0];
       FqV w2(w2_size, fq_zero());
@@ -859,17 +869,13 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
       Fq sacc = fq_zero();
       for (size_t k = 3; k < w2.size(); k++) sacc = fq_add(sacc, w2[k]);
       w3[1] = fq_mul(w3[0], fq_sub(fq_sub(tau, sacc), bv[2]));
-      w3[3] = q != Q - 1 ? fq_mul(w3[1], fq_sub(fq_add(b_w3[p][q + 1][2], fq_one()), b_w3[p][q + 1][0])) : w3[1];
-      w3[2] = fq_mul(w3[0], w3[3]);
       for (size_t i = 0; i < np_; i++) {
         const size_t PMR = 2 * niu + 2 * i, PMC = PMR + 1;
         w2[PMR] = fq_mul(r, bv[io_width + 2 * i + 1]);
         const Fq tt = i == 0 ? V_CNST : w2[PMC - 2];
         w2[PMC] = fq_mul(tt, fq_sub(fq_sub(tau, bv[io_width + 2 * i]), w2[PMR]));
       }
-      const Fq px = np_ == 0 ? V_CNST : w2[2 * niu + 2 * (np_ - 1) + 1];
-      w3[5] = q != Q - 1 ? fq_mul(px, fq_sub(fq_add(b_w3[p][q + 1][4], fq_one()), b_w3[p][q + 1][0])) : px;
-      w3[4] = fq_mul(V_CNST, w3[5]);
+      pxs[q] = np_ == 0 ? V_CNST : w2[2 * niu + 2 * (np_ - 1) + 1];
       for (size_t i = 0; i < nv_; i++) {
         const size_t base = 2 * niu + 2 * np_ + 4 * i, vb = io_width + 2 * np_ + 4 * i;
         w2[base] = fq_mul(r, bv[vb + 1]);
@@ -878,11 +884,20 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
         const Fq tt = i == 0 ? V_CNST : w2[base - 1];
         w2[base + 3] = fq_mul(tt, fq_sub(fq_sub(fq_sub(fq_sub(tau, bv[vb]), w2[base]), w2[base + 1]), w2[base + 2]));
       }
-      const Fq vx = nv_ == 0 ? V_CNST : w2[2 * niu + 2 * np_ + 4 * (nv_ - 1) + 3];
-      w3[7] = q != Q - 1 ? fq_mul(vx, fq_sub(fq_add(b_w3[p][q + 1][6], fq_one()), b_w3[p][q + 1][0])) : vx;
+      vxs[q] = nv_ == 0 ? V_CNST : w2[2 * niu + 2 * np_ + 4 * (nv_ - 1) + 3];
+      b_w2[p][q] = std::move(w2);
+      b_w3[p][q] = std::move(w3);
+    });
+    for (size_t q = Q; q-- > 0;) {  // the reverse-q recurrences (src/lib.rs:1539-1611)
+      FqV& w3 = b_w3[p][q];
+      const Fq V_CNST = w3[0];
+      const FqV* nx = q != Q - 1 ? &b_w3[p][q + 1] : nullptr;
+      w3[3] = nx ? fq_mul(w3[1], fq_sub(fq_add((*nx)[2], fq_one()), (*nx)[0])) : w3[1];
+      w3[2] = fq_mul(w3[0], w3[3]);
+      w3[5] = nx ? fq_mul(pxs[q], fq_sub(fq_add((*nx)[4], fq_one()), (*nx)[0])) : pxs[q];
+      w3[4] = fq_mul(V_CNST, w3[5]);
+      w3[7] = nx ? fq_mul(vxs[q], fq_sub(fq_add((*nx)[6], fq_one()), (*nx)[0])) : vxs[q];
       w3[6] = fq_mul(V_CNST, w3[7]);
-      b_w2[p][q] = w2;
-      b_w3[p][q] = w3;
     }
     b_w3s[p] = shift_rows(b_w3[p], 8);
   }
