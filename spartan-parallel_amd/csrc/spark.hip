@@ -20,6 +20,8 @@
 // All O(N) work stays in HBM; the host runs the transcript and one UniPoly per sumcheck round.
 #include <algorithm>
 
+#include <hipcub/hipcub.hpp>
+
 #include "hostpoly.hpp"
 #include "proto.hpp"
 #include "layer.hpp"
@@ -72,6 +74,24 @@ __global__ void k_hash_mem(const uint32_t* __restrict__ audit, const Fq* __restr
   tree[(2 * s) * 2 * m + il] = hash3(a, v, fq_zero(), rh, rh2, rms);
   tree[(2 * s + 1) * 2 * m + il] = hash3(a, v, fq_from_u64(audit[s * cells + i]), rh, rh2, rms);
 }
+// AddrTimestamps::new (sparse_mlpoly.rs:219-253) on the device: read_ts[t] = #{t' < t : addr[t'] = addr[t]} and
+// audit[a] = #{t : addr[t] = a} over the ops in batch order. counts -> exclusive scan = each address's first
+// rank; a stable radix sort of (addr, t) lists every address's ops in order, so sorted position j holds op t with
+// read_ts = j - start[addr].
+__global__ void k_ts_count(const uint32_t* __restrict__ addr, size_t n, uint32_t* __restrict__ cnt) {
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n) atomicAdd(&cnt[addr[t]], 1u);
+}
+__global__ void k_iota(uint32_t* __restrict__ v, size_t n) {
+  size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n) v[t] = (uint32_t)t;
+}
+__global__ void k_ts_rank(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ ops,
+                          const uint32_t* __restrict__ start, size_t n, uint32_t* __restrict__ rts) {
+  size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < n) rts[ops[j]] = (uint32_t)j - start[keys[j]];
+}
+
 // dst[i] = src[i W + r], i < n (a rank's interleaved share of a vector)
 __global__ void k_strided(Fq* __restrict__ dst, const Fq* __restrict__ src, size_t n, uint32_t W, uint32_t r) {
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -275,7 +295,7 @@ static const size_t kHostFinalRows = 64;  // latency-path commits of at most thi
 enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
-  kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage
+  kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -895,8 +915,9 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
   const size_t ops_len = npow2(5 * B * N);
   if (lg2(ops_len) > nv_ops || lg2(npow2(2 * B * N)) > nv_der || std::max(nvx, nvy) + 1 > nv_mem)
     return set_err(ctx, SPG_E_ARG, "SPARK generators (gens_nnz, gens_batch) too small for the batch");
-  // AddrTimestamps::new (sparse_mlpoly.rs:219-253): read / audit timestamps are a sequential scan (host)
-  std::vector<uint32_t> addr(2 * B * N, 0), rts(2 * B * N, 0), audit(2 * cells, 0);
+  // the dense representation's addresses (multi_sparse_to_dense_rep, sparse_mlpoly.rs:368-425); padding ops read
+  // address 0
+  std::vector<uint32_t> addr(2 * B * N, 0);
   std::vector<Fq> val(B * N, fq_zero());
   for (size_t k = 0; k < B; k++) {
     const spg_sparse_entry* E = polys[k].e;
@@ -909,13 +930,6 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
       memcpy(val[k * N + i].l, E[i].val, 32);
     }
   }
-  for (size_t side = 0; side < 2; side++) {
-    uint32_t* au = audit.data() + side * cells;
-    for (size_t t = side * B * N; t < (side + 1) * B * N; t++) {
-      rts[t] = au[addr[t]];
-      au[addr[t]] = rts[t] + 1;
-    }
-  }
   spg_spark* S = new spg_spark();
   S->B = B;
   S->N = N;
@@ -925,13 +939,45 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
   auto up = [&](void** d, const void* h, size_t bytes) -> bool {
     return hipMalloc(d, bytes + 64) == hipSuccess && hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice) == hipSuccess;
   };
-  if (!up((void**)&S->d_addr, addr.data(), addr.size() * 4) || !up((void**)&S->d_rts, rts.data(), rts.size() * 4) ||
-      !up((void**)&S->d_audit, audit.data(), audit.size() * 4) ||
+  if (!up((void**)&S->d_addr, addr.data(), addr.size() * 4) || hipMalloc(&S->d_rts, addr.size() * 4 + 64) != hipSuccess ||
+      hipMalloc(&S->d_audit, 2 * cells * 4 + 64) != hipSuccess ||
       !up((void**)&S->d_val, val.data(), val.size() * sizeof(Fq)) ||
       hipMalloc(&S->d_comb_ops, S->comb_ops_len * sizeof(Fq)) != hipSuccess ||
       hipMalloc(&S->d_comb_mem, S->comb_mem_len * sizeof(Fq)) != hipSuccess) {
     spg_spark_free(ctx, S);
     return set_err(ctx, SPG_E_NOMEM, "spark upload");
+  }
+  {  // AddrTimestamps::new (sparse_mlpoly.rs:219-253) for the row and the column side, on the device
+    const size_t BN = B * N;
+    int bits = 1;
+    while (((size_t)1 << bits) < cells) bits++;
+    uint32_t* tmpk = (uint32_t*)ws_get(ctx, kWsTsKeys, 3 * BN * 4 + 4 * (cells + 1) + 64);
+    size_t sort_bytes = 0, scan_bytes = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)BN, 0, bits, s);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cells, s);
+    void* tmps = ws_get(ctx, kWsTsTemp, std::max(sort_bytes, scan_bytes) + 64);
+    if (!tmpk || !tmps) {
+      spg_spark_free(ctx, S);
+      return set_err(ctx, SPG_E_NOMEM, "timestamps workspace");
+    }
+    uint32_t *keys = tmpk, *ops_in = tmpk + BN, *ops = tmpk + 2 * BN, *start = tmpk + 3 * BN;
+    int rc2 = 0;
+    for (size_t side = 0; side < 2 && !rc2; side++) {
+      const uint32_t* ad = S->d_addr + side * BN;
+      uint32_t* au = S->d_audit + side * cells;
+      if (hipMemsetAsync(au, 0, cells * 4, s) != hipSuccess) rc2 = SPG_E_HIP;
+      hipLaunchKernelGGL(k_ts_count, dim3(nblk(BN)), dim3(256), 0, s, ad, BN, au);
+      if (hipcub::DeviceScan::ExclusiveSum(tmps, scan_bytes, au, start, (int)cells, s) != hipSuccess) rc2 = SPG_E_HIP;
+      hipLaunchKernelGGL(k_iota, dim3(nblk(BN)), dim3(256), 0, s, ops_in, BN);
+      if (hipcub::DeviceRadixSort::SortPairs(tmps, sort_bytes, ad, keys, ops_in, ops, (int)BN, 0, bits, s) != hipSuccess)
+        rc2 = SPG_E_HIP;
+      hipLaunchKernelGGL(k_ts_rank, dim3(nblk(BN)), dim3(256), 0, s, keys, ops, start, BN, S->d_rts + side * BN);
+    }
+    if (rc2 || hipGetLastError() != hipSuccess) {
+      spg_spark_free(ctx, S);
+      return set_err(ctx, SPG_E_HIP, "spark timestamps");
+    }
   }
   // comb_ops = merge(row addr, row read_ts, col addr, col read_ts, val); comb_mem = row audit ++ col audit
   const size_t BN = B * N;
