@@ -475,6 +475,14 @@ int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* bloc
     *out_len = s.b.size();
     if (s.b.size() > cap) return -1;
     memcpy(out, s.b.data(), s.b.size());
+    // negative tests (tests/test_oracle_snark.py): ORC_TAMPER corrupts what the verifier sees
+    const char* tamper = getenv("ORC_TAMPER");
+    if (tamper && std::string(tamper) == "io_proof" && pf.io_proof.proofs.size() > 1)
+      std::swap(pf.io_proof.proofs[0], pf.io_proof.proofs[1]);
+    if (tamper && std::string(tamper) == "shift_eval" && pf.shift_proof.C_orig_evals.size() > 1)
+      std::swap(pf.shift_proof.C_orig_evals[0], pf.shift_proof.C_orig_evals[1]);
+    if (tamper && std::string(tamper) == "perm_opening" && !pf.proof_eval_perm_poly_prod_list.empty())
+      std::swap(pf.proof_eval_perm_poly_prod_list[0], pf.proof_eval_perm_poly_prod_list.back());
     Transcript tv(label);
     return snark_verify(pf, in, block, pairwise, perm_root, vg, tv);
   } catch (const std::string& e) {

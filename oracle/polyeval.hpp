@@ -306,6 +306,153 @@ struct PolyEvalProof {
   }
 };
 
+// c * P for a scalar c (Montgomery) and a point P
+static inline Ge ge_mul_fq(const Ge& P, const Fq& c) {
+  uint8_t cb[32];
+  fq_to_bytes(c, cb);
+  return ge_scalarmul_bytes(P, cb);
+}
+
+// PolyEvalProof::verify_plain_batched_points (src/dense_mlpoly.rs:624-680): one proof per distinct L (left half
+// of r), the R vectors and claimed values of equal-L points combined with powers of challenge_c
+static inline bool verify_plain_batched_points(const std::vector<PolyEvalProof>& proofs, const DotGens& g,
+                                               Transcript& t, const std::vector<FqVec>& r_list, const FqVec& Zr_list,
+                                               const PolyCommitment& comm) {
+  t.append_protocol_name("polynomial evaluation proof");
+  size_t ln, rn;
+  eq_factored_lens(r_list[0].size(), &ln, &rn);
+  std::vector<FqVec> keys, L_list, R_list;
+  FqVec Zc;
+  Fq c_base = t.challenge_scalar("challenge_c");
+  Fq c = fq_one();
+  for (size_t i = 0; i < r_list.size(); i++) {
+    FqVec Li, Ri;
+    eq_factored_evals(r_list[i], &Li, &Ri);
+    FqVec key(r_list[i].begin(), r_list[i].begin() + ln);
+    size_t idx = keys.size();
+    for (size_t k = 0; k < keys.size(); k++)
+      if (keys[k] == key) { idx = k; break; }
+    if (idx < keys.size()) {
+      c = fq_mul(c, c_base);
+      for (size_t j = 0; j < Ri.size(); j++) R_list[idx][j] = fq_add(R_list[idx][j], fq_mul(c, Ri[j]));
+      Zc[idx] = fq_add(Zc[idx], fq_mul(c, Zr_list[i]));
+    } else {
+      keys.push_back(key);
+      L_list.push_back(Li);
+      R_list.push_back(Ri);
+      Zc.push_back(Zr_list[i]);
+    }
+  }
+  if (L_list.size() != proofs.size()) return false;
+  std::vector<Ge> C;
+  for (auto& p : comm) C.push_back(unpack(p));
+  for (size_t i = 0; i < L_list.size(); i++) {
+    CPt C_Zc = cpt(commit1(Zc[i], fq_zero(), g.gens_1));
+    CPt C_LZ = cpt(msm_pts(L_list[i], C));
+    if (!proofs[i].proof.verify(R_list[i].size(), g, t, R_list[i], C_LZ, C_Zc)) return false;
+  }
+  return true;
+}
+
+// PolyEvalProof::verify_plain_batched_instances (src/dense_mlpoly.rs:782-858): one proof per (num_vars, R);
+// the L.C of equal keys and their claimed values combined with powers of challenge_c
+static inline bool verify_plain_batched_instances(const std::vector<PolyEvalProof>& proofs, const DotGens& g,
+                                                  Transcript& t, const std::vector<FqVec>& r_list,
+                                                  const FqVec& Zr_list, const std::vector<PolyCommitment>& comm_list,
+                                                  const std::vector<size_t>& num_vars_list) {
+  t.append_protocol_name("polynomial evaluation proof");
+  if (comm_list.size() != r_list.size()) return false;
+  std::vector<std::pair<size_t, FqVec>> keys;
+  std::vector<Ge> LZ_list;
+  FqVec Zc;
+  std::vector<FqVec> R_list;
+  Fq c_base = t.challenge_scalar("challenge_c");
+  Fq c = fq_one();
+  for (size_t i = 0; i < comm_list.size(); i++) {
+    std::vector<Ge> C;
+    for (auto& p : comm_list[i]) C.push_back(unpack(p));
+    const size_t nv = num_vars_list[i];
+    FqVec r;
+    if (nv >= r_list[i].size()) {
+      r.assign(nv - r_list[i].size(), fq_zero());
+      r.insert(r.end(), r_list[i].begin(), r_list[i].end());
+    } else {
+      r.assign(r_list[i].end() - nv, r_list[i].end());
+    }
+    FqVec L, R;
+    eq_factored_evals(r, &L, &R);
+    std::pair<size_t, FqVec> key = {nv, R};
+    size_t idx = keys.size();
+    for (size_t k = 0; k < keys.size(); k++)
+      if (keys[k] == key) { idx = k; break; }
+    if (idx < keys.size()) {
+      c = fq_mul(c, c_base);
+      LZ_list[idx] = ge_add(LZ_list[idx], ge_mul_fq(msm_pts(L, C), c));
+      Zc[idx] = fq_add(Zc[idx], fq_mul(c, Zr_list[i]));
+    } else {
+      keys.push_back(key);
+      Zc.push_back(Zr_list[i]);
+      LZ_list.push_back(msm_pts(L, C));
+      R_list.push_back(R);
+    }
+  }
+  if (LZ_list.size() != proofs.size()) return false;
+  for (size_t i = 0; i < LZ_list.size(); i++) {
+    CPt C_Zc = cpt(commit1(Zc[i], fq_zero(), g.gens_1));
+    if (!proofs[i].proof.verify(R_list[i].size(), g, t, R_list[i], cpt(LZ_list[i]), C_Zc)) return false;
+  }
+  return true;
+}
+
+// PolyEvalProof::verify_uni_batched_instances (src/dense_mlpoly.rs:1132-1205): R = (1, r, r^2, ...), per num_vars
+// L = (1, r^k, r^2k, ...) with k = |R_i|; L.C and the claimed-value commitments combined with powers of c
+static inline bool verify_uni_batched_instances(const PolyEvalProof& pf, const DotGens& g, Transcript& t, const Fq& r,
+                                                const std::vector<Ge>& C_Zr,
+                                                const std::vector<const PolyCommitment*>& comm_list,
+                                                const std::vector<size_t>& poly_size) {
+  t.append_protocol_name("polynomial evaluation proof");
+  size_t max_size = 0;
+  for (auto s : poly_size) max_size = std::max(max_size, s);
+  size_t ln, rn;
+  eq_factored_lens(log_2(next_pow2(max_size)), &ln, &rn);
+  FqVec R;
+  Fq rb = fq_one();
+  for (size_t i = 0; i < pow2(rn); i++) {
+    R.push_back(rb);
+    rb = fq_mul(rb, r);
+  }
+  std::vector<std::pair<size_t, FqVec>> Lmap;
+  Fq c_base = t.challenge_scalar("challenge_c");
+  Fq c = fq_one();
+  Ge LZc = commit1(fq_zero(), fq_zero(), g.gens_1), Zrc = LZc;
+  for (size_t i = 0; i < comm_list.size(); i++) {
+    const size_t nv = log_2(next_pow2(poly_size[i]));
+    const FqVec* L = nullptr;
+    for (auto& kv : Lmap)
+      if (kv.first == nv) L = &kv.second;
+    if (!L) {
+      size_t l2, r2;
+      eq_factored_lens(nv, &l2, &r2);
+      Fq r_base = fq_one();
+      for (size_t k = 0; k < pow2(r2); k++) r_base = fq_mul(r_base, r);
+      FqVec Lv;
+      Fq lb = fq_one();
+      for (size_t k = 0; k < pow2(l2); k++) {
+        Lv.push_back(lb);
+        lb = fq_mul(lb, r_base);
+      }
+      Lmap.push_back({nv, Lv});
+      L = &Lmap.back().second;
+    }
+    std::vector<Ge> C;
+    for (auto& p : *comm_list[i]) C.push_back(unpack(p));
+    LZc = ge_add(LZc, ge_mul_fq(msm_pts(*L, C), c));
+    Zrc = ge_add(Zrc, ge_mul_fq(C_Zr[i], c));
+    c = fq_mul(c, c_base);
+  }
+  return pf.proof.verify(R.size(), g, t, R, cpt(LZc), cpt(Zrc));
+}
+
 static inline void ser_proofs(Ser& s, const std::vector<PolyEvalProof>& v) {
   s.u64(v.size());
   for (auto& p : v) p.ser(s);

@@ -992,8 +992,8 @@ static inline bool check_bound_rp(const FqVec& list, const FqVec& rp, const Fq b
 }
 
 // Replays SNARK::prove's transcript with the verifier's knowledge (public inputs, instance commitments, the
-// proof) and checks the three R1CSProofs, their R1CSEvalProofs and the permutation-product identity
-// (lib.rs:2750-3881; shift and IO proofs are not re-checked). Returns 0 when all checks pass, else the failing stage.
+// proof) and checks the three R1CSProofs, their R1CSEvalProofs, the permutation-product openings and identities,
+// the shift proofs and the IO proofs (lib.rs:2750-3881). Returns 0 when all checks pass, else the failing stage.
 static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const SnarkInst& block,
                                const SnarkInst& pairwise, const SnarkInst& perm_root, const R1CSGens& vars_gens,
                                Transcript& t) {
@@ -1219,6 +1219,19 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
     std::vector<size_t> im;
     VSec m = VSec::merge(comps, &im);
     if (pf.perm_poly_poly_list.size() != m.num_proofs.size()) return 10;
+    // the openings of every w3 instance at (1, 0), (1, 0, 0) or (1, 1, 0) (lib.rs:3679-3713)
+    const size_t pm_bl_id = 6, vm_bl_id = in.max_block_num_phy_ops > 0 ? 7 : 6;
+    std::vector<FqVec> r_list;
+    std::vector<size_t> nv_list;
+    for (size_t i = 0; i < im.size(); i++) {
+      if (im[i] == vm_bl_id) r_list.push_back({fq_one(), fq_one(), fq_zero()});
+      else if (im[i] == pm_bl_id) r_list.push_back({fq_one(), fq_zero(), fq_zero()});
+      else r_list.push_back({fq_one(), fq_zero()});
+      nv_list.push_back(log_2(m.num_proofs[i] * 8));
+    }
+    if (!verify_plain_batched_instances(pf.proof_eval_perm_poly_prod_list, gpc, t, r_list, pf.perm_poly_poly_list,
+                                        m.comm_w, nv_list))
+      return 14;
     Fq pe = fq_one(), pb = fq_one(), pmb = fq_one(), pma = fq_one(), vmb = fq_one(), vma = fq_one();
     for (size_t i = 0; i < im.size(); i++) {
       const Fq& v = pf.perm_poly_poly_list[i];
@@ -1239,6 +1252,72 @@ static inline int snark_verify(const SNARKProof& pf, const SnarkIn& in, const Sn
     if (!(pe == pb)) return 11;
     if (!(pmb == pma)) return 12;
     if (!(vmb == vma)) return 13;
+  }
+  // SHIFT_PROOFS (lib.rs:3772-3853 -> ShiftProofs::verify, :449-506)
+  {
+    std::vector<const PolyCommitment*> orig = {&pf.perm_exec_comm_w3_list}, shifted = {&pf.perm_exec_comm_w3_shifted};
+    std::vector<size_t> sizes = {8 * consis}, hl = {6};
+    for (size_t p = 0; p < P; p++) {
+      orig.push_back(&pf.block_comm_w3_list[p]);
+      shifted.push_back(&pf.block_comm_w3_list_shifted[p]);
+      sizes.push_back(8 * bnp[p]);
+      hl.push_back(8);
+    }
+    auto add = [&](const PolyCommitment& o, const PolyCommitment& sh, size_t size, size_t h) {
+      orig.push_back(&o);
+      shifted.push_back(&sh);
+      sizes.push_back(size);
+      hl.push_back(h);
+    };
+    if (t_iphy > 0) add(pf.init_phy_mem_comm_w3, pf.init_phy_mem_comm_w3_shifted, 8 * t_iphy, 6);
+    if (t_ivir > 0) add(pf.init_vir_mem_comm_w3, pf.init_vir_mem_comm_w3_shifted, 8 * t_ivir, 6);
+    if (t_phy > 0) {
+      add(pf.addr_comm_phy_mems, pf.addr_comm_phy_mems_shifted, 4 * t_phy, 4);
+      add(pf.phy_mem_addr_comm_w3, pf.phy_mem_addr_comm_w3_shifted, 8 * t_phy, 6);
+    }
+    if (t_vir > 0) {
+      add(pf.addr_comm_vir_mems, pf.addr_comm_vir_mems_shifted, 8 * t_vir, 6);
+      add(pf.vir_mem_addr_comm_w3, pf.vir_mem_addr_comm_w3_shifted, 8 * t_vir, 6);
+    }
+    const ShiftProofs& sp = pf.shift_proof;
+    if (sp.openings.size() != orig.size() || sp.C_orig_evals.size() != orig.size() ||
+        sp.C_shifted_evals.size() != orig.size())
+      return 15;
+    for (size_t p = 0; p < hl.size(); p++) {
+      if (sp.openings[p].size() < hl[p]) return 15;
+      for (size_t i = 0; i < hl[p]; i++) t.append_point("shift_header_entry", sp.openings[p][i].v);
+    }
+    const Fq c = t.challenge_scalar("challenge_c");
+    std::vector<Ge> evals;
+    for (auto& e : sp.C_orig_evals) evals.push_back(unpack(e));
+    for (auto& e : sp.C_shifted_evals) evals.push_back(unpack(e));
+    std::vector<const PolyCommitment*> comms(orig);
+    comms.insert(comms.end(), shifted.begin(), shifted.end());
+    std::vector<size_t> sz2(sizes);
+    sz2.insert(sz2.end(), sizes.begin(), sizes.end());
+    if (!verify_uni_batched_instances(sp.proof, gpc, t, c, evals, comms, sz2)) return 15;
+  }
+  // IO_PROOFS (lib.rs:3855-3873 -> IOProofs::verify, :283-359)
+  {
+    const size_t r_len = log_2(consis * num_ios);
+    std::vector<size_t> idx;
+    for (size_t i = 0; i + 2 < in.input_liveness.size(); i++) idx.push_back(2 + in.input_offset + i);
+    if (in.input_liveness[1]) idx.insert(idx.begin(), 5);
+    if (in.input_liveness[0]) idx.insert(idx.begin(), 6);
+    FqVec live;
+    for (size_t i = 0; i < in.input_liveness.size(); i++)
+      if (in.input_liveness[i]) live.push_back(in.input[i]);
+    idx.resize(live.size());
+    const size_t oe = in.output_exec_num * num_ios;
+    std::vector<size_t> pts = {0, oe, 2, oe + 2 + (niu - 1), oe + 2 + (niu - 1) + in.output_offset - 1};
+    pts.insert(pts.end(), idx.begin(), idx.end());
+    std::vector<FqVec> r_list;
+    for (size_t p : pts) r_list.push_back(to_bin_array(p, r_len));
+    FqVec Zr = {fq_one(), fq_one(), fq_from_u64(in.input_block_num), fq_from_u64(in.output_block_num), in.output};
+    Zr.insert(Zr.end(), live.begin(), live.end());
+    if (pf.exec_comm_inputs.empty() ||
+        !verify_plain_batched_points(pf.io_proof.proofs, gpc, t, r_list, Zr, pf.exec_comm_inputs[0]))
+      return 16;
   }
   return 0;
 }

@@ -68,3 +68,16 @@ def test_snark_memory_trace_is_checked(oracle, what):
         wl.addr_ts_bits[0][2] ^= 1
     _, rc = oracle.snark_prove(wl, workload.tape_seed())
     assert rc != 0
+
+
+@pytest.mark.parametrize("tamper,stage", [("io_proof", 16), ("shift_eval", 15), ("perm_opening", 14)])
+def test_snark_verifier_checks_openings(oracle, tamper, stage, monkeypatch):
+    """the oracle verifier re-checks the perm-product openings (PolyEvalProof::verify_plain_batched_instances),
+    the shift proofs (ShiftProofs::verify) and the IO proofs (IOProofs::verify): a verifier that sees swapped IO
+    opening proofs, swapped shift evaluations or misplaced perm-product opening proofs rejects at that stage"""
+    import workload
+
+    wl = workload.SnarkWorkload(num_blocks=2, log_cons=5, log_proofs=1, num_vars=32)
+    monkeypatch.setenv("ORC_TAMPER", tamper)
+    _, rc = oracle.snark_prove(wl, workload.tape_seed())
+    assert rc == stage
