@@ -1,11 +1,15 @@
+#include <map>
+#include <thread>
 #include <algorithm>
 #include <chrono>
 #include <string.h>
 // spg — context management for the C-ABI (include/spg.h).
+#include <ctype.h>
 #include <stdio.h>
 #include <string.h>
 
 #include "ctx.hpp"
+#include "hpool.hpp"
 
 namespace spg {
 
@@ -93,6 +97,90 @@ int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n) {
   return 0;
 }
 
+
+// ---- host thread placement -------------------------------------------------------------------------------------
+static std::vector<int> parse_cpulist(const std::string& path) {
+  std::vector<int> out;
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return out;
+  char line[8192] = {0};
+  if (fgets(line, sizeof(line), f)) {
+    char* save = nullptr;
+    for (char* tok = strtok_r(line, ",\n", &save); tok; tok = strtok_r(nullptr, ",\n", &save)) {
+      int x = 0, y = 0;
+      if (sscanf(tok, "%d-%d", &x, &y) == 2)
+        for (int k = x; k <= y; k++) out.push_back(k);
+      else if (sscanf(tok, "%d", &x) == 1)
+        out.push_back(x);
+    }
+  }
+  fclose(f);
+  return out;
+}
+// busy jiffies per CPU from /proc/stat
+static std::map<int, unsigned long long> cpu_busy() {
+  std::map<int, unsigned long long> m;
+  FILE* f = fopen("/proc/stat", "r");
+  if (!f) return m;
+  char line[512];
+  while (fgets(line, sizeof(line), f)) {
+    int cpu;
+    unsigned long long u, n, sy, id, io, irq, sirq, st;
+    if (sscanf(line, "cpu%d %llu %llu %llu %llu %llu %llu %llu %llu", &cpu, &u, &n, &sy, &id, &io, &irq, &sirq, &st) == 9)
+      m[cpu] = u + n + sy + irq + sirq + st;
+  }
+  fclose(f);
+  return m;
+}
+// The prover's host side is a chain of short bursts between Fiat-Shamir challenges: the calling thread, the pool
+// workers and the mailbox spin exchange cache lines every few microseconds. Unplaced, those threads land on any
+// of the machine's CPUs (two sockets, 16 L3 domains on the MI355X hosts), and every hand-off crosses dies. This
+// picks the physical cores of one L3 domain on the GPU's NUMA node — the least busy one over a 20 ms sample — so
+// the caller and the workers share an L3 next to the GPU's PCIe root.
+std::vector<int> choose_pool_cpus(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return {};
+  for (char* q = bus; *q; q++) *q = (char)tolower(*q);
+  std::vector<int> local = parse_cpulist(std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist");
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return {};
+  // L3 domains of the allowed, GPU-local physical cores (first SMT sibling only)
+  std::map<std::string, std::vector<int>> doms;
+  for (int c : local) {
+    if (c < 0 || c >= CPU_SETSIZE || !CPU_ISSET(c, &allowed)) continue;
+    const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c);
+    std::vector<int> sib = parse_cpulist(base + "/topology/thread_siblings_list");
+    if (!sib.empty() && sib[0] != c) continue;
+    std::vector<int> l3 = parse_cpulist(base + "/cache/index3/shared_cpu_list");
+    std::string key;
+    for (int x : l3) key += std::to_string(x) + ",";
+    doms[key].push_back(c);
+  }
+  const size_t want = (size_t)pool_threads() + 1;  // the caller and the workers (the pool is not started yet)
+  std::map<int, unsigned long long> b0 = cpu_busy();
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  std::map<int, unsigned long long> b1 = cpu_busy();
+  std::vector<std::pair<double, std::vector<int>>> cand;  // (busy jiffies, cores) per domain
+  for (auto& kv : doms) {
+    if (kv.second.size() < want) continue;
+    double load = 0;
+    for (int c : kv.second) {
+      const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c);
+      for (int x : parse_cpulist(base + "/topology/thread_siblings_list")) load += (double)(b1[x] - b0[x]);
+    }
+    cand.push_back({load, std::vector<int>(kv.second.begin(), kv.second.begin() + want)});
+  }
+  if (cand.empty()) return {};
+  // least busy first; processes of one node that start together (one per GPU) see the same loads, so each
+  // takes the entry at its local rank (else its device ordinal) and they land on different domains
+  std::stable_sort(cand.begin(), cand.end(), [](const std::pair<double, std::vector<int>>& a,
+                                                const std::pair<double, std::vector<int>>& b) { return a.first < b.first; });
+  const char* lr = getenv("LOCAL_RANK");  // torchrun: one process per GPU, or several sharing one in rehearsals
+  const size_t slot = lr ? (size_t)atoi(lr) : (size_t)device;
+  return cand[slot % cand.size()].second;
+}
+
 void timer_start(spg_ctx* c) { hipEventRecord(c->ev0, c->stream); }
 void timer_stop(spg_ctx* c) { hipEventRecord(c->ev1, c->stream); }
 
@@ -151,6 +239,16 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   }
   memset(mb, 0, spg::kMboxBytes);
   c->mbox = (volatile uint32_t*)mb;
+  // SPG_PIN (default on): the host pool (created on first use) and this thread on one L3 domain (CCD) local to the
+  // GPU, the least busy one (spg::choose_pool_cpus)
+  const char* pin = getenv("SPG_PIN");
+  if ((!pin || atoi(pin) != 0) && spg::pool_cpus().empty()) {
+    std::vector<int> cpus = spg::choose_pool_cpus(device);
+    if (!cpus.empty()) {
+      spg::pool_cpus() = cpus;
+      spg::pin_thread(cpus);
+    }
+  }
   *out = c;
   return SPG_OK;
 }

@@ -25,7 +25,24 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
 namespace spg {
+
+// CPUs the pool should live on (set by spg_init from the GPU's NUMA-local CPU list when SPG_PIN=1): the caller
+// thread and the workers then share one CCD's L3, so a burst's hand-offs stay on-die instead of crossing sockets.
+inline std::vector<int>& pool_cpus() {
+  static std::vector<int> v;
+  return v;
+}
+inline void pin_thread(const std::vector<int>& cpus) {
+  if (cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus) CPU_SET(c, &set);
+  pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
 
 class Pool {
  public:
@@ -35,7 +52,12 @@ class Pool {
       : delay_us_(snapshot_delay_us), pub_delay_us_(publish_delay_us) {
     const char* e = getenv("SPG_POOL_SPIN_US");
     spin_ = std::chrono::microseconds(e ? atoi(e) : 20000);
-    for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
+    const std::vector<int> cpus = pool_cpus();
+    for (int i = 0; i < nthreads; i++)
+      threads_.emplace_back([this, cpus, i] {
+        if (!cpus.empty()) pin_thread({cpus[(size_t)(i + 1) % cpus.size()]});
+        worker();
+      });
   }
   ~Pool() {
     {
@@ -130,16 +152,18 @@ class Pool {
   std::chrono::microseconds spin_{20000};
 };
 
+// workers besides the calling thread
+inline int pool_threads() {
+  const char* e = getenv("SPG_POOL_THREADS");
+  if (e) return atoi(e);
+  unsigned hw = std::thread::hardware_concurrency();
+  int n = hw > 1 ? (int)hw - 1 : 0;
+  // 7 workers + the caller: measured best on the GPU box (16-CPU quota per process; 15 workers were
+  // 2-5 ms slower per SNARK::prove, scripts/pool_sweep.sh), and it leaves room for HIP's own threads
+  return n > 7 ? 7 : n;
+}
 inline Pool& pool() {
-  static Pool p([] {
-    const char* e = getenv("SPG_POOL_THREADS");  // workers besides the calling thread
-    if (e) return atoi(e);
-    unsigned hw = std::thread::hardware_concurrency();
-    int n = hw > 1 ? (int)hw - 1 : 0;
-    // 7 workers + the caller: measured best on the GPU box (16-CPU quota per process; 15 workers were
-    // 2-5 ms slower per SNARK::prove, scripts/pool_sweep.sh), and it leaves room for HIP's own threads
-    return n > 7 ? 7 : n;
-  }());
+  static Pool p(pool_threads());
   return p;
 }
 

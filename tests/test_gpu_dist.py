@@ -39,6 +39,7 @@ def _worker(rank, world, port, case, q, bad_shard=False):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["SPG_PIN"] = "0"  # several ranks share the test box's GPU (and would pick the same CPU domain)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         nc, npf, nws, shared = CASES[case]
@@ -113,6 +114,7 @@ def _spark_worker(rank, world, port, case, q):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["SPG_PIN"] = "0"  # several ranks share the test box's GPU (and would pick the same CPU domain)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cases = dict(SPARK_CASES, **GPU_SPARK_CASES)
