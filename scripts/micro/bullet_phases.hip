@@ -42,28 +42,28 @@ static void run(int n, int k, Niels* tab, int n1, Fq* st, uint32_t* gidx, unsign
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int w = 0; w < 3; w++) hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB, 2), dim3(BS), 0, 0, a);
+  for (int w = 0; w < 3; w++) hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB + 1, 2), dim3(BS), 0, 0, a);
   const int R = 20;
   hipEventRecord(e0, 0);
-  for (int r = 0; r < R; r++) hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB, 2), dim3(BS), 0, 0, a);
+  for (int r = 0; r < R; r++) hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB + 1, 2), dim3(BS), 0, 0, a);
   hipEventRecord(e1, 0);
   hipEventSynchronize(e1);
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
   a.probe = probe;
-  hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB, 2), dim3(BS), 0, 0, a);
+  hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB + 1, 2), dim3(BS), 0, 0, a);
   hipDeviceSynchronize();
-  std::vector<unsigned long long> p(8 * 2 * NB);
+  std::vector<unsigned long long> p(8 * 2 * (NB + 1));
   hipMemcpy(p.data(), probe, p.size() * 8, hipMemcpyDeviceToHost);
   unsigned long long t0 = ~0ull, tend = 0;
   double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, skew = 0;
-  for (int b = 0; b < 2 * NB; b++) t0 = std::min(t0, p[8 * b]);
-  for (int b = 0; b < 2 * NB; b++) {
+  for (int b = 0; b < 2 * (NB + 1); b++) t0 = std::min(t0, p[8 * b]);
+  for (int b = 0; b < 2 * (NB + 1); b++) {
     const unsigned long long* q = &p[8 * b];
     skew = std::max(skew, (q[0] - t0) * 0.01);
     for (int i = 0; i < 4; i++) {
       const double d = (q[i + 1] - q[i]) * 0.01;
-      ph[i] += d / (2 * NB);
+      ph[i] += d / (2 * (NB + 1));
       mx[i] = std::max(mx[i], d);
     }
     tend = std::max(tend, q[4]);
@@ -103,7 +103,7 @@ static void run_gaps(int n, Niels* tab, int n1, Fq* st, uint32_t* gidx, unsigned
   for (int r = 0; r < R + 3; r++) {
     std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
     hipEventRecord(e0, 0);
-    hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB, 2), dim3(BS), 0, 0, a);
+    hipLaunchKernelGGL((k_bullet_round_q<7, BS>), dim3(NB + 1, 2), dim3(BS), 0, 0, a);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     float ms;
@@ -152,8 +152,8 @@ int main() {
   hipMalloc(&ctr, 64);
   hipMemset(ctr, 0, 64);
   hipMalloc(&mb, 4096);
-  hipMalloc(&bk, 2 * 64 * sizeof(Ext));
-  hipMalloc(&probe, 8 * 2 * 64 * 8);
+  hipMalloc(&bk, 2 * 65 * sizeof(Ext));
+  hipMalloc(&probe, 8 * 2 * 65 * 8);
   {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);

@@ -222,6 +222,17 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SPG_E_NODEVICE;
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return SPG_E_NODEVICE;
   if (hipSetDevice(device) != hipSuccess) return SPG_E_HIP;
+  // (before the host buffers below are first touched, so they live on that NUMA node)
+  // SPG_PIN (default on): the host pool (created on first use) and this thread on one L3 domain (CCD) local to the
+  // GPU, the least busy one (spg::choose_pool_cpus)
+  const char* pin = getenv("SPG_PIN");
+  if ((!pin || atoi(pin) != 0) && spg::pool_cpus().empty()) {
+    std::vector<int> cpus = spg::choose_pool_cpus(device);
+    if (!cpus.empty()) {
+      spg::pool_cpus() = cpus;
+      spg::pin_thread(cpus);
+    }
+  }
   spg_ctx* c = new spg_ctx();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -239,16 +250,6 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   }
   memset(mb, 0, spg::kMboxBytes);
   c->mbox = (volatile uint32_t*)mb;
-  // SPG_PIN (default on): the host pool (created on first use) and this thread on one L3 domain (CCD) local to the
-  // GPU, the least busy one (spg::choose_pool_cpus)
-  const char* pin = getenv("SPG_PIN");
-  if ((!pin || atoi(pin) != 0) && spg::pool_cpus().empty()) {
-    std::vector<int> cpus = spg::choose_pool_cpus(device);
-    if (!cpus.empty()) {
-      spg::pool_cpus() = cpus;
-      spg::pin_thread(cpus);
-    }
-  }
   *out = c;
   return SPG_OK;
 }

@@ -29,7 +29,7 @@ struct BulletArgs {
   Fq u, uinv;
   int k, n, nk, n1;
   const Niels* tab;
-  Ext* buckets;  // B = 2 bucket sets of NB (mapped host memory)
+  Ext* buckets;  // B = 2 bucket sets of NB + 1 (the last: top-window carries; mapped host memory)
   unsigned* counter;
   uint32_t* mb;
   uint32_t seq;
@@ -46,7 +46,11 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
   __shared__ uint32_t pts[soa_words<Ext, S>()];
   __shared__ uint32_t cnt;
   __shared__ bool last;
+  // v = 1 .. NB: bucket v; v = NB + 1: the top window's digits of magnitude 1 (the final carries of the signed
+  // recoding: about every second scalar, which would nearly double bucket 1's entries and with it the kernel's
+  // critical path), summed apart and added with weight 1 on the host
   const int v = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const bool carry_wg = v == NB + 1;
   const int P = a.n / 2, nk = a.nk, nh = nk / 2;
   const bool writer = blockIdx.x == 0;
   Ext acc = ext_identity();
@@ -85,7 +89,8 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
         int d = (int)(x & MASK) + carry;
         carry = d > NB ? 1 : 0;
         d -= carry << C;
-        if (d == v || d == -v) {
+        const bool top1 = w == W - 1 && (d == 1 || d == -1);
+        if (carry_wg ? top1 : ((d == v || d == -v) && !top1)) {
           const uint32_t pos = atomicAdd(&cnt, 1u);
           list[pos] = (uint32_t)((size_t)(w * C) * a.n1 + gi) | (d < 0 ? 0x80000000u : 0u);
         }
@@ -122,7 +127,7 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
   }
   if (pr && t == 0) pr[3] = wall_clock64();
   if (t == 0) {
-    a.buckets[(size_t)b * NB + (v - 1)] = acc;
+    a.buckets[(size_t)b * (NB + 1) + (v - 1)] = acc;
     // the bucket (mapped host memory) and the folded state (HBM) before the ticket
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");

@@ -122,7 +122,8 @@ int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, con
 
 // one Bullet round (msm.hip k_bullet_round_q): applies round k-1's fold with (u, uinv) to the device state
 // (aa: Montgomery, cw: plain integers; in -> out, double-buffered), then the bucket sums of the round's L and
-// R MSMs (2 x 64 Ext) into d_buckets; completion is posted to the mailbox with *seq_out
+// R MSMs (2 x (64 + 1) Ext: buckets 1..64, then the top window's carries) into d_buckets; completion is
+// posted to the mailbox with *seq_out
 int bullet_round_device(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
                         const uint32_t* gidx, const Fq& u, const Fq& uinv, int k, int n, int nk, Ext* d_buckets,
                         uint32_t* seq_out);

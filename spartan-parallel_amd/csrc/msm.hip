@@ -605,11 +605,11 @@ int bullet_round_device(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const 
   constexpr int C = 7, NB = 1 << (C - 1);
   KScope ks(ctx, "msm_bullet_round");
   if (n / 2 <= 64)
-    hipLaunchKernelGGL((k_bullet_round_q<C, 64>), dim3(NB, 2), dim3(64), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_bullet_round_q<C, 64>), dim3(NB + 1, 2), dim3(64), 0, ctx->stream, a);
   else if (n / 2 <= 128)
-    hipLaunchKernelGGL((k_bullet_round_q<C, 128>), dim3(NB, 2), dim3(128), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_bullet_round_q<C, 128>), dim3(NB + 1, 2), dim3(128), 0, ctx->stream, a);
   else
-    hipLaunchKernelGGL((k_bullet_round_q<C, 256>), dim3(NB, 2), dim3(256), 0, ctx->stream, a);
+    hipLaunchKernelGGL((k_bullet_round_q<C, 256>), dim3(NB + 1, 2), dim3(256), 0, ctx->stream, a);
   SPG_HIP(ctx, hipGetLastError());
   return 0;
 }

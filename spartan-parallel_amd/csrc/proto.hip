@@ -191,11 +191,11 @@ static h::HExt hext_small_mul(h::HExt P, unsigned k) {
   return r;
 }
 
-void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extra) {
+void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extra, bool carry) {
   // chunk (lo, hi] of a bucket set: run = sum B_v, acc = sum (v - lo) B_v; the set's sum is
   // sum over chunks of acc + lo * run. Chunks spread one MSM's 2 NB dependent additions over the pool;
   // the last chunk of an MSM to finish (countdown) adds the chunks and encodes, all in one burst.
-  const int K = NB >= 64 ? 8 : 1, per = NB / K;
+  const int K = NB >= 64 ? 8 : 1, per = NB / K, stride = NB + (carry ? 1 : 0);
   std::vector<h::HExt> part(B * K);
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[B]);
   for (size_t b = 0; b < B; b++) left[b].store(K);
@@ -204,13 +204,14 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extr
     const int lo = (task % K) * per;
     h::HExt run = h::hext_identity(), acc = h::hext_identity();
     for (int v = lo + per; v > lo; v--) {
-      run = h::hext_add(run, h::hext_from_dev(bk[b * NB + v - 1]));
+      run = h::hext_add(run, h::hext_from_dev(bk[b * stride + v - 1]));
       acc = h::hext_add(acc, run);
     }
     part[task] = lo ? h::hext_add(acc, hext_small_mul(run, (unsigned)lo)) : acc;
     if (left[b].fetch_sub(1, std::memory_order_acq_rel) == 1) {
       h::HExt s = part[b * K];
       for (int c = 1; c < K; c++) s = h::hext_add(s, part[b * K + c]);
+      if (carry) s = h::hext_add(s, h::hext_from_dev(bk[b * stride + NB]));
       if (extra) s = h::hext_add(s, extra[b]);
       out[b] = compress(s);
     }
@@ -345,7 +346,7 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
     if (rc) return rc;
     g_msm_laps.lap("msm_device");
     Pt LR[2];
-    bucket_finals(mbk, 2, kBulletNB, LR, ex.data());
+    bucket_finals(mbk, 2, kBulletNB, LR, ex.data(), true);
     g_msm_laps.lap("msm_host_final");
     t.point("L", LR[0]);
     t.point("R", LR[1]);
@@ -428,7 +429,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
   void* d_map = nullptr;
   Ext* mbk = (dev_rounds && n >= 2 && (n & (n - 1)) == 0)
-                 ? (Ext*)mapped_get(ctx, sizeof(Ext) * 2 * kBulletNB + 64, &d_map)
+                 ? (Ext*)mapped_get(ctx, sizeof(Ext) * 2 * (kBulletNB + 1) + 64, &d_map)
                  : nullptr;
   if (mbk) {
     int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, mbk, (Ext*)d_map, &aa, &bb, &cw, &blind_fin, out);

@@ -139,7 +139,8 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
                          const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy);
 // sum_v v * B_v of B bucket sets (bk: B x NB extended points, bucket v at index v - 1), encoded, on host cores
 // (plus extra[b] when given)
-void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extra = nullptr);
+// carry: every set holds NB + 1 points, the last one added with weight 1 (k_bullet_round_q's top-window carries)
+void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extra = nullptr, bool carry = false);
 // device MSMs of B x n scalars over explicit generator indices (host buffers), outputs B points
 int device_msm_idx(spg_ctx* ctx, ProverGens& g, const std::vector<FqV>& scalars, const std::vector<std::vector<uint32_t>>& idx,
                    std::vector<Pt>* out);
