@@ -1,5 +1,6 @@
 #include <map>
 #include <thread>
+#include <mutex>
 #include <algorithm>
 #include <chrono>
 #include <string.h>
@@ -97,6 +98,53 @@ int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n) {
   return 0;
 }
 
+struct SegArgs {
+  const Fq* p[kSegMax];
+  uint32_t off[kSegMax + 1];
+  int k;
+};
+
+// thread i copies scalar i of the concatenated ranges into the result page (plain stores to coherent host memory;
+// the stream synchronisation after the launch makes them visible)
+__global__ void __launch_bounds__(256) k_gather_res(SegArgs a, Fq* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.off[a.k]) return;
+  int j = 0;
+  while (i >= a.off[j + 1]) j++;
+  const uint4* src = (const uint4*)(a.p[j] + (i - a.off[j]));
+  uint4* dst = (uint4*)(out + i);
+  dst[0] = src[0];
+  dst[1] = src[1];
+}
+
+int d2h_multi(spg_ctx* ctx, const FqSeg* segs, int k, Fq* h) {
+  size_t total = 0;
+  for (int j = 0; j < k; j++) total += segs[j].n;
+  if (total == 0) return 0;
+  if (k > kSegMax || total > kResScalars) {  // larger downloads: one copy per range through pinned staging
+    for (int j = 0; j < k; j++) {
+      Fq* st = (Fq*)pinned_get(ctx, segs[j].n * sizeof(Fq));
+      if (!st) return set_err(ctx, SPG_E_NOMEM, "download staging");
+      SPG_HIP(ctx, hipMemcpyAsync(st, segs[j].d, segs[j].n * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      memcpy(h, st, segs[j].n * sizeof(Fq));
+      h += segs[j].n;
+    }
+    return 0;
+  }
+  SegArgs a;
+  a.k = k;
+  a.off[0] = 0;
+  for (int j = 0; j < k; j++) {
+    a.p[j] = segs[j].d;
+    a.off[j + 1] = a.off[j] + (uint32_t)segs[j].n;
+  }
+  hipLaunchKernelGGL(k_gather_res, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, ctx->stream, a, ctx->d_res);
+  SPG_HIP(ctx, hipGetLastError());
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(h, ctx->res, total * sizeof(Fq));
+  return 0;
+}
 
 // ---- host thread placement -------------------------------------------------------------------------------------
 static std::vector<int> parse_cpulist(const std::string& path) {
@@ -181,6 +229,31 @@ std::vector<int> choose_pool_cpus(int device) {
   return cand[slot % cand.size()].second;
 }
 
+static std::map<std::string, long>& copy_counts() {
+  static std::map<std::string, long> m;
+  return m;
+}
+void print_copy_counts() {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  std::vector<std::pair<long, std::string>> v;
+  for (auto& kv : copy_counts()) v.push_back({kv.second, kv.first});
+  std::sort(v.rbegin(), v.rend());
+  for (auto& p : v) fprintf(stderr, "[spg] copies %8ld  %s\n", p.first, p.second.c_str());
+  copy_counts().clear();
+}
+hipError_t memcpy_traced(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s, const char* file,
+                         int line) {
+  static const bool on = getenv("SPG_COPY_TRACE") && atoi(getenv("SPG_COPY_TRACE")) != 0;
+  if (on) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    const char* f = strrchr(file, '/');
+    copy_counts()[std::string(f ? f + 1 : file) + ":" + std::to_string(line)]++;
+  }
+  return (hipMemcpyAsync)(dst, src, n, k, s);
+}
+
 void timer_start(spg_ctx* c) { hipEventRecord(c->ev0, c->stream); }
 void timer_stop(spg_ctx* c) { hipEventRecord(c->ev1, c->stream); }
 
@@ -243,13 +316,15 @@ extern "C" int spg_init(int device, spg_ctx** out) {
     return SPG_E_HIP;
   }
   void* mb = nullptr;
-  if (hipHostMalloc(&mb, spg::kMboxBytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+  if (hipHostMalloc(&mb, 2 * spg::kMboxBytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mbox, mb, 0) != hipSuccess) {
     delete c;
     return SPG_E_HIP;
   }
-  memset(mb, 0, spg::kMboxBytes);
+  memset(mb, 0, 2 * spg::kMboxBytes);
   c->mbox = (volatile uint32_t*)mb;
+  c->res = (spg::Fq*)((uint8_t*)mb + spg::kMboxBytes);
+  c->d_res = (spg::Fq*)((uint8_t*)c->d_mbox + spg::kMboxBytes);
   *out = c;
   return SPG_OK;
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <map>
 #include <string>
 #include <vector>
@@ -28,6 +29,10 @@ struct spg_ctx {
   volatile uint32_t* mbox = nullptr;
   uint32_t* d_mbox = nullptr;
   uint32_t mbox_seq = 0;
+  // result page (coherent, mapped host memory next to the mailbox): d2h_multi's gather kernel writes the
+  // scalars the host needs there, so a download is one small kernel + a stream synchronisation, no blit copy
+  spg::Fq* res = nullptr;
+  spg::Fq* d_res = nullptr;
   // multi-process proving (spg_set_comm): this process' rank and an allgather provided by the caller
   int rank = 0, nranks = 1;
   spg_allgather_fn allgather = nullptr;
@@ -69,6 +74,11 @@ struct spg_gens {
 };
 
 namespace spg {
+
+// SPG_COPY_TRACE=1: count hipMemcpyAsync calls per source line (printed at exit); every async copy is a blit
+// kernel on the stream, so the per-round ones cost a dispatch each
+hipError_t memcpy_traced(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s, const char* file, int line);
+void print_copy_counts();  // and reset
 
 static const int kTableRows = 254;  // bit offsets 0..253 cover every window of a 253-bit scalar
 
@@ -132,6 +142,17 @@ static const int kBulletNB = 64;  // buckets per MSM of bullet_round_device (c =
 // the mailbox page: sequence number (word 0), then up to kMboxScalars scalars from word 8
 static const size_t kMboxBytes = 65536;
 static const size_t kMboxScalars = (kMboxBytes - 32) / 32;
+static const size_t kResScalars = kMboxBytes / sizeof(Fq);
+// a few device scalar ranges downloaded at once: one gather launch into the result page, one synchronisation
+struct FqSeg {
+  const Fq* d;
+  size_t n;
+};
+static const int kSegMax = 16;
+int d2h_multi(spg_ctx* ctx, const FqSeg* segs, int k, Fq* h);
+inline int d2h_multi(spg_ctx* ctx, std::initializer_list<FqSeg> segs, Fq* h) {
+  return d2h_multi(ctx, segs.begin(), (int)segs.size(), h);
+}
 // waits (spinning, bounded) until the mailbox carries sequence number `seq`, then copies n scalars out
 int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n);
 
@@ -170,3 +191,7 @@ struct KScope {
 };
 
 }  // namespace spg
+
+#ifndef SPG_NO_COPY_TRACE
+#define hipMemcpyAsync(d, src, n, k, st) spg::memcpy_traced(d, src, n, k, st, __FILE__, __LINE__)
+#endif

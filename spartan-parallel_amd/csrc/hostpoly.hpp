@@ -72,15 +72,8 @@ inline Fq uni_eval(const FqV& c, const Fq& r) {
   return ev;
 }
 
-// through the context's page-locked staging (stream order keeps it clear of earlier uploads from it)
-inline int d2h_fq(spg_ctx* ctx, const Fq* d, Fq* h, size_t n = 1) {
-  Fq* st = (Fq*)pinned_get(ctx, n * sizeof(Fq));
-  if (!st) return set_err(ctx, SPG_E_NOMEM, "download staging");
-  SPG_HIP(ctx, hipMemcpyAsync(st, d, n * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
-  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  memcpy(h, st, n * sizeof(Fq));
-  return 0;
-}
+// n device scalars to the host (d2h_multi: the result page, or page-locked staging for long ranges)
+inline int d2h_fq(spg_ctx* ctx, const Fq* d, Fq* h, size_t n = 1) { return d2h_multi(ctx, {{d, n}}, h); }
 
 inline Fq ld_fq(const uint64_t* v) {
   Fq a;

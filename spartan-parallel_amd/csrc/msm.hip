@@ -559,9 +559,19 @@ __global__ void __launch_bounds__(BS) k_smsm_bucket_q(const Fq* __restrict__ sca
         int d = (int)(x & MASK) + carry;
         carry = d > NB ? 1 : 0;
         d -= carry << C;
+        // the top window holds little more than the final carry (scalars < 2^253), a digit of magnitude 1 for
+        // about every second scalar, which would pile onto bucket 1 and set the kernel's critical path: such an
+        // entry 2^{(W-1)C} P is taken as 2^s * (2^{(W-1)C - s} P) instead, s = 1 .. C-1 by generator, spreading
+        // those entries over buckets 2, 4, .., 2^{C-1} (same point, table row (W-1)C - s)
+        int bo = w * C;
+        if (w == W - 1 && (d == 1 || d == -1)) {
+          const int sh = 1 + (int)(gidx % (uint32_t)(C - 1));
+          d <<= sh;
+          bo -= sh;
+        }
         if (d == v || d == -v) {
           const uint32_t pos = atomicAdd(&cnt, 1u);
-          list[pos] = (uint32_t)((size_t)(w * C) * n1 + gidx) | (d < 0 ? 0x80000000u : 0u);
+          list[pos] = (uint32_t)((size_t)bo * n1 + gidx) | (d < 0 ? 0x80000000u : 0u);
         }
       }
     }

@@ -425,12 +425,29 @@ int Prover::sum_ranks(Fq e[3]) {
 int Prover::gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full) {
   const size_t k = tabs.size(), PL = (P + nranks - 1) / nranks;  // the largest shard; slots per rank
   std::vector<Fq> mine(PL * k, fq_zero());
-  for (size_t i = 0; i < k; i++) {
-    const PqxDev& T = *tabs[i];
-    for (size_t p = 0; p < T.zlen; p++) {
-      int rc = d2h_fq(ctx, T.d + T.off[p], &mine[i * PL + p]);
-      if (rc) return rc;
+  {  // one gather per kSegMax elements
+    std::vector<FqSeg> segs;
+    std::vector<Fq*> dst;
+    std::vector<Fq> got;
+    auto flush = [&]() -> int {
+      got.resize(segs.size());
+      int rc = d2h_multi(ctx, segs.data(), (int)segs.size(), got.data());
+      for (size_t j = 0; j < segs.size(); j++) *dst[j] = got[j];
+      segs.clear();
+      dst.clear();
+      return rc;
+    };
+    for (size_t i = 0; i < k; i++) {
+      const PqxDev& T = *tabs[i];
+      for (size_t p = 0; p < T.zlen; p++) {
+        segs.push_back({T.d + T.off[p], 1});
+        dst.push_back(&mine[i * PL + p]);
+        if (segs.size() == (size_t)kSegMax)
+          if (int rc = flush()) return rc;
+      }
     }
+    if (!segs.empty())
+      if (int rc = flush()) return rc;
   }
   std::vector<uint8_t> r;
   int rc = allgather(mine.data(), mine.size() * sizeof(Fq), r);
@@ -679,21 +696,13 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p1_host");
       rx_all.push_back(r_j);
     }
-    Fq a[3];
-    rc = d2h_fq(ctx, Ap, &a[0]);
-    if (!rc) rc = d2h_fq(ctx, Aq, &a[1]);
-    if (!rc) rc = d2h_fq(ctx, Ax, &a[2]);
+    Fq a[6];  // eq factors, then Az, Bz, Cz (a single instance: it sits on this (only) rank's local tables)
+    rc = np == 0 ? d2h_multi(ctx, {{Ap, 1}, {Aq, 1}, {Ax, 1}, {Az.d, 1}, {Bz, 1}, {Cz, 1}}, a)
+                 : d2h_multi(ctx, {{Ap, 1}, {Aq, 1}, {Ax, 1}, {T->d, 1}, {TB, 1}, {TC, 1}}, a);
     if (rc) return rc;
-    if (np == 0) {  // a single instance: it sits on this (only) rank's local tables
-      rc = d2h_fq(ctx, Az.d, &claims1[1]);
-      if (!rc) rc = d2h_fq(ctx, Bz, &claims1[2]);
-      if (!rc) rc = d2h_fq(ctx, Cz, &claims1[3]);
-    } else {
-      rc = d2h_fq(ctx, T->d, &claims1[1]);
-      if (!rc) rc = d2h_fq(ctx, TB, &claims1[2]);
-      if (!rc) rc = d2h_fq(ctx, TC, &claims1[3]);
-    }
-    if (rc) return rc;
+    claims1[1] = a[3];
+    claims1[2] = a[4];
+    claims1[3] = a[5];
     claims1[0] = fq_mul(fq_mul(a[0], a[1]), a[2]);
     blind_post1 = zk.blinds_evals[rounds - 1];
     pf.sc1 = std::move(zk.out);
@@ -850,9 +859,7 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p2_host");
       ry_all.push_back(r_j);
     }
-    rc = d2h_fq(ctx, eq_p, &claims2[0]);
-    if (!rc) rc = d2h_fq(ctx, TA->d, &claims2[1]);
-    if (!rc) rc = d2h_fq(ctx, TZ->d, &claims2[2]);
+    rc = d2h_multi(ctx, {{eq_p, 1}, {TA->d, 1}, {TZ->d, 1}}, claims2);
     if (rc) return rc;
     blind_post2 = zk.blinds_evals[rounds - 1];
     pf.sc2 = std::move(zk.out);

@@ -1239,6 +1239,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
                     g_commit_stats.calls, g_commit_stats.points, g_commit_stats.us);
     g_commit_stats = CommitStats();
   }
+  if (getenv("SPG_COPY_TRACE") && atoi(getenv("SPG_COPY_TRACE"))) print_copy_counts();
   *proof_len = w.out.size();
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, w.out.data(), w.out.size());

@@ -97,6 +97,16 @@ __global__ void k_strided(Fq* __restrict__ dst, const Fq* __restrict__ src, size
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) dst[i] = src[i * W + r];
 }
+// the dot-product circuits' inputs in one launch: circuit piece j = (2b + h) * 3 + k of length nl is this rank's
+// interleaved share (i * W + r) of half h of instance b's row derefs (k = 0), col derefs (k = 1) or values (k = 2)
+__global__ void k_dotp_gather(Fq* __restrict__ dst, const Fq* __restrict__ derefs, const Fq* __restrict__ val,
+                              size_t BN, size_t N, size_t hN, size_t nl, uint32_t W, uint32_t r) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nl) return;
+  const uint32_t j = blockIdx.y, k = j % 3, h = (j / 3) & 1, b = j / 6;
+  const Fq* src = (k < 2 ? derefs + k * BN : val) + b * N + h * hN;
+  dst[(size_t)j * nl + i] = src[i * W + r];
+}
 __global__ void k_scale(Fq* __restrict__ v, size_t n, Fq s) {
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) v[i] = fq_mul(v[i], s);
@@ -1208,19 +1218,12 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   // copies (this rank's interleaved shares when the ops set is sharded), since the layer-0 sumcheck folds them
   // while the hash layer evaluates the originals
   std::vector<Triple> dotp;
-  for (size_t b = 0; b < B; b++)
-    for (size_t h = 0; h < 2; h++) {
-      Fq* base = dotbuf + (2 * b + h) * 3 * hNl;
-      const Fq* src[3] = {derefs + b * N + h * hN, derefs + BN + b * N + h * hN, S->d_val + b * N + h * hN};
-      for (int k = 0; k < 3; k++) {
-        if (tso.W == 1)
-          SPG_HIP(ctx, hipMemcpyAsync(base + k * hNl, src[k], hN * sizeof(Fq), hipMemcpyDeviceToDevice, s));
-        else
-          hipLaunchKernelGGL(k_strided, dim3(nblk(hNl)), dim3(256), 0, s, base + k * hNl, src[k], hNl,
-                             (uint32_t)tso.W, (uint32_t)tso.r);
-      }
-      dotp.push_back({base, base + hNl, base + 2 * hNl});
-    }
+  for (size_t j = 0; j < 2 * B; j++) {
+    Fq* base = dotbuf + j * 3 * hNl;
+    dotp.push_back({base, base + hNl, base + 2 * hNl});
+  }
+  hipLaunchKernelGGL(k_dotp_gather, dim3(nblk(hNl), (unsigned)(6 * B)), dim3(256), 0, s, dotbuf, derefs, S->d_val,
+                     BN, N, hN, hNl, (uint32_t)tso.W, (uint32_t)tso.r);
   SPG_HIP(ctx, hipGetLastError());
   FqV dotp_claims(2 * B);
   {
