@@ -234,7 +234,10 @@ typedef struct {
   const size_t* block_num_proofs; /* [block_num_instances_bound] */
   size_t consis_num_proofs, total_num_init_phy_mem_accesses, total_num_init_vir_mem_accesses,
       total_num_phy_mem_accesses, total_num_vir_mem_accesses;
-  const uint64_t* const* block_vars; /* [b] -> block_num_proofs[b] x block_num_vars[b] x 4 */
+  /* [i] -> the witness list of the i-th block in the prover's sort order (block_num_proofs descending, ties in
+   * block order; src/lib.rs:1155-1178 pairs block_vars_mat[i] with sorted instance i): block_num_proofs[o_i] rows of
+   * block_num_vars[o_i] x 4 limbs, o_i = that block's index; NULL for a block without executions */
+  const uint64_t* const* block_vars;
   const uint64_t* exec_inputs;       /* consis_num_proofs x num_ios x 4 */
   const uint64_t* init_phy_mems;     /* total_num_init_phy_mem_accesses x 4 x 4 */
   const uint64_t* init_vir_mems;     /* total_num_init_vir_mem_accesses x 4 x 4 */
@@ -253,7 +256,7 @@ typedef struct spg_snark_wit spg_snark_wit;   /* SNARK::prove run-time inputs, r
 int spg_snark_encode(spg_ctx* ctx, const spg_snark_instance* inst, int multi, spg_snark_comp** out);
 int spg_snark_comp_free(spg_ctx* ctx, spg_snark_comp* comp);
 /* Uploads block_vars and exec inputs to HBM (padded to powers of two) and keeps host copies of the parts the
- * witness recurrences read. Block witness lists must be given in the sorted order (as in the reference). */
+ * witness recurrences read. Block witness lists are given in the sorted order (as in the reference). */
 int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* inputs, spg_snark_wit** out);
 int spg_snark_witness_free(spg_ctx* ctx, spg_snark_wit* wit);
 /* SNARK::prove (src/lib.rs:971-2746) with vars_gens (spg_r1cs_gens_new(label "gens_r1cs_sat", bound)).

@@ -425,9 +425,18 @@ SnarkIn snark_in_from_c(const spg_snark_inputs* c) {
       for (size_t i = 0; i < w; i++) m[q][i] = ld(p + 4 * (q * w + i));
     return m;
   };
-  for (size_t b = 0; b < B; b++)
-    in.block_vars_mat.push_back(c->block_num_proofs[b] ? rows(c->block_vars[b], c->block_num_proofs[b], c->block_num_vars[b])
-                                                       : std::vector<FqVec>());
+  // block_vars[i]: the witness list of the i-th instance in the prover's sort order (lib.rs:1155-1178 pairs
+  // block_vars_mat[i] with sorted instance i), sized by that instance's num_proofs and num_vars
+  std::vector<size_t> order(B);
+  for (size_t i = 0; i < B; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](size_t x, size_t y) { return c->block_num_proofs[x] > c->block_num_proofs[y]; });
+  // (blocks that never execute sort last and have no list: the reference's block_vars_mat holds the executed
+  // blocks only, ProverWitnessSecInfo::new reads every list's first row, lib.rs:520-526)
+  for (size_t i = 0; i < B; i++) {
+    const size_t b = order[i];
+    if (c->block_num_proofs[b]) in.block_vars_mat.push_back(rows(c->block_vars[i], c->block_num_proofs[b], c->block_num_vars[b]));
+  }
   in.exec_inputs_list = rows(c->exec_inputs, c->consis_num_proofs, c->num_ios);
   if (c->total_num_init_phy_mem_accesses)
     in.init_phy_mems_list = rows(c->init_phy_mems, c->total_num_init_phy_mem_accesses, INIT_PHY_MEM_WIDTH);

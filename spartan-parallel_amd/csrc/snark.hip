@@ -569,19 +569,25 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
     delete W;
     return set_err(ctx, rc, msg);
   };
-  for (size_t b = 0; b < B; b++) {
-    const size_t n = W->nproofs[b], w = W->nvars[b];
-    if (n && !a->block_vars[b]) return fail(SPG_E_ARG, "missing block_vars");
+  // block_vars[i] is the witness list of the i-th instance in the prover's sort order (num_proofs descending,
+  // ties in block order; lib.rs:1155-1178): the reference pairs block_vars_mat[i] with sorted instance i, so list
+  // i holds num_proofs[order[i]] rows of num_vars[order[i]] entries
+  std::vector<size_t> order(B);
+  for (size_t i = 0; i < B; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return W->nproofs[x] > W->nproofs[y]; });
+  for (size_t i = 0; i < B; i++) {
+    const size_t b = order[i], n = W->nproofs[b], w = W->nvars[b];
+    if (n && !a->block_vars[i]) return fail(SPG_E_ARG, "missing block_vars");
     // the io part of every row (and the memory-op part the w2 recurrences read)
     const size_t keep = std::min(w, io + 2 * W->phy_ops[b] + 4 * W->vir_ops[b]);
-    W->block_io.push_back(n ? rows(a->block_vars[b], n, w, keep) : Rows());
+    W->block_io.push_back(n ? rows(a->block_vars[i], n, w, keep) : Rows());
     // resident copy, padded to next_pow2(num_proofs) rows of zeros (lib.rs:1209-1216)
     Fq* d = nullptr;
     const size_t rows_p = npow2(std::max<size_t>(n, 1));
     if (hipMalloc(&d, rows_p * w * sizeof(Fq) + 64) != hipSuccess) return fail(SPG_E_NOMEM, "block_vars");
     W->d_block_vars.push_back(d);
     if (hipMemsetAsync(d, 0, rows_p * w * sizeof(Fq), ctx->stream) != hipSuccess ||
-        (n && hipMemcpyAsync(d, a->block_vars[b], n * w * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
+        (n && hipMemcpyAsync(d, a->block_vars[i], n * w * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
       return fail(SPG_E_HIP, "block_vars upload");
   }
   const size_t ce = npow2(a->consis_num_proofs);
@@ -736,9 +742,6 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     bphy[i] = W->phy_ops[order[i]];
     bvir[i] = W->vir_ops[order[i]];
   }
-  for (size_t i = 0; i < P; i++)
-    if (W->nvars[i] != bnv[i] || W->nproofs[i] != bnp[i])
-      return set_err(ctx, SPG_E_ARG, "block witness lists must be given in sorted order");
   const size_t bmax = npow2(a.block_max_num_proofs);
   std::vector<size_t> bnp_pad(P);
   for (size_t i = 0; i < P; i++) bnp_pad[i] = npow2(bnp[i]);

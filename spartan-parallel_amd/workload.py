@@ -125,6 +125,17 @@ class R1CSWorkload:
             self.sections.append(mats)
 
     @property
+    def num_vars_per_block(self):
+        return list(self._vars_width)
+
+    @property
+    def block_vars_sorted(self):
+        """block_vars in the prover's instance order (num_proofs descending, stable): the reference pairs
+        block_vars_mat[i] with sorted instance i (src/lib.rs:1155-1178)"""
+        order = sorted(range(self.num_blocks), key=lambda b: -self.block_num_proofs[b])
+        return [self.block_vars[b] for b in order]
+
+    @property
     def total_constraints(self):
         return sum(x * q for x, q in zip(self.num_cons, self.num_proofs))
 
@@ -418,7 +429,11 @@ class SnarkWorkload:
     NIU = 4  # default num_inputs_unpadded: (v, _, i0, i1, i2 | o0, o1, o2) -> num_ios = 8
 
     def __init__(self, num_blocks=2, log_cons=10, log_proofs=9, num_vars=1024, max_ts_width=2, seed=0x5350415254414E31,
-                 phy_ops=0, vir_ops=0, init_phy=0, init_vir=0, niu=None):
+                 phy_ops=0, vir_ops=0, init_phy=0, init_vir=0, niu=None, schedule=None, vars_width=None):
+        # schedule: the block of every execution (default round robin, num_blocks << log_proofs executions); uneven
+        # schedules give unsorted block_num_proofs and blocks that never run. vars_width: per-block witness widths
+        # (num_vars_per_block, powers of two <= num_vars; default num_vars): block b's rows keep their first
+        # vars_width[b] entries, which must hold the whole chain
         # niu >= 5 is needed for virtual memory: a VIR entry's timestamp (column 5) must fall on an input slot of
         # the perm-root instance, whose output slots must be zero for memory entries (ZO = 0)
         niu = niu or self.NIU
@@ -435,6 +450,9 @@ class SnarkWorkload:
         m = (1 << log_cons) - extra - 3
         assert m >= 1 and base + m + 1 <= num_vars, "num_vars too small for the chain"
         self.chain = m
+        self._vars_width = list(vars_width) if vars_width else [num_vars] * num_blocks
+        assert len(self._vars_width) == num_blocks and all(
+            base + m + 1 <= w <= num_vars and not w & (w - 1) for w in self._vars_width), "vars_width"
         self.chain_base = base
         # user constraints of every block (A, B, C lists of (col, int) per row)
         V_in, V_out = (lambda i: 2 + i), (lambda i: 2 + (niu - 1) + i)
@@ -442,6 +460,7 @@ class SnarkWorkload:
         rows += [([(base + j - 1, 1)], [(base + j - 1, 1)], [(base + j, 1)]) for j in range(1, m + 1)]
         rows += [([(base + m, 1)], [(0, 1)], [(V_out(1), 1)]), ([(V_in(2), 1)], [(0, 1)], [(V_out(2), 1)])]
         args = [rows for _ in range(num_blocks)]
+        self.args = args  # CompileTimeKnowledge.args (examples/interface.rs:47-71), as (col, int) terms
         self.block_num_phy_ops = [phy_ops] * num_blocks
         self.block_num_vir_ops = [vir_ops] * num_blocks
         self.block_num_vars, self.block_max_num_cons, self.block_nnz, self.block_inst = gen_block_inst(
@@ -452,7 +471,10 @@ class SnarkWorkload:
          self.pairwise_inst) = gen_pairwise_check_inst(max_ts_width, self.mem_addr_ts_bits_size)
         self.perm_root_num_cons, self.perm_root_nnz, self.perm_root_inst = gen_perm_root_inst(niu, self.num_ios)
         # ---- execution trace
-        E = num_blocks << log_proofs
+        if schedule is None:
+            schedule = [k % num_blocks for k in range(num_blocks << log_proofs)]
+        assert schedule and all(0 <= b < num_blocks for b in schedule)
+        E = len(schedule)
         seeds, st = random_fq(2, seed)
         x, y = int(seeds[0]), int(seeds[1])
         self.x0 = x
@@ -475,8 +497,8 @@ class SnarkWorkload:
         per_block = [[] for _ in range(num_blocks)]
         exec_rows = []
         for k in range(E):
-            b = k % num_blocks
-            nb = (k + 1) % num_blocks if k + 1 < E else num_blocks
+            b = schedule[k]
+            nb = schedule[k + 1] if k + 1 < E else num_blocks
             chain = [x]
             for _ in range(m):
                 chain.append(chain[-1] * chain[-1] % Q)
@@ -498,8 +520,8 @@ class SnarkWorkload:
         self.output = x
         self.block_num_proofs = [len(r) for r in per_block]
         self.block_max_num_proofs = max(self.block_num_proofs)
-        self.block_vars = [to_mont_limbs(np.array(r, dtype=object).reshape(-1)).reshape(len(r), num_vars, 4)
-                           for r in per_block]
+        self.block_vars = [to_mont_limbs(np.array([row[:w] for row in r], dtype=object).reshape(-1)).reshape(len(r), w, 4)
+                           for r, w in zip(per_block, self._vars_width)]
         self.consis_num_proofs = E
         self.exec_inputs = to_mont_limbs(np.array(exec_rows, dtype=object).reshape(-1)).reshape(E, self.num_ios, 4)
 
@@ -525,7 +547,7 @@ class SnarkWorkload:
             bits = [(diff >> i) & 1 for i in range(max_ts_width)]
             row = [e[1] * nxt[4] % Q, 0] + bits
             self.addr_ts_bits.append(row + [0] * (self.mem_addr_ts_bits_size - len(row)))
-        self.input_block_num = 0
+        self.input_block_num = schedule[0]
         self.output_block_num = num_blocks
         self.input_liveness = [False, False, True]
         self.func_input_width = 1
@@ -534,6 +556,17 @@ class SnarkWorkload:
         self.input = to_mont_limbs([0, 0, self.x0])
         self.output_mont = to_mont_limbs([self.output])[0]
         self.output_exec_num = E - 1
+
+    @property
+    def num_vars_per_block(self):
+        return list(self._vars_width)
+
+    @property
+    def block_vars_sorted(self):
+        """block_vars in the prover's instance order (num_proofs descending, stable): the reference pairs
+        block_vars_mat[i] with sorted instance i (src/lib.rs:1155-1178)"""
+        order = sorted(range(self.num_blocks), key=lambda b: -self.block_num_proofs[b])
+        return [self.block_vars[b] for b in order]
 
     @property
     def total_constraints(self):
@@ -599,7 +632,7 @@ class SnarkViews:
         self.block = inst(wl.block_inst, (wl.block_max_num_cons, wl.block_num_vars, B, wl.block_nnz))
         self.pairwise = inst(wl.pairwise_inst, (wl.pairwise_max_num_cons, 4 * wl.pairwise_num_vars, 3, wl.pairwise_nnz))
         self.perm_root = inst(wl.perm_root_inst, (wl.perm_root_num_cons, 8 * wl.num_ios, 1, wl.perm_root_nnz))
-        bv = (ctypes.c_void_p * B)(*[arr(v) for v in wl.block_vars])
+        bv = (ctypes.c_void_p * B)(*[arr(v) if len(v) else None for v in wl.block_vars_sorted])
         self.keep.append(bv)
         c = CSnarkInputs()
         c.input_block_num, c.output_block_num = wl.input_block_num, wl.output_block_num
@@ -616,7 +649,7 @@ class SnarkViews:
         c.block_num_vir_ops = sz(wl.block_num_vir_ops)
         c.mem_addr_ts_bits_size = wl.mem_addr_ts_bits_size
         c.num_inputs_unpadded = wl.num_inputs_unpadded
-        c.block_num_vars = sz([wl.num_vars] * B)
+        c.block_num_vars = sz(wl.num_vars_per_block)
         c.block_num_instances_bound = B
         c.block_max_num_proofs = wl.block_max_num_proofs
         c.block_num_proofs = sz(wl.block_num_proofs)
@@ -624,9 +657,11 @@ class SnarkViews:
         c.block_vars = bv
         c.exec_inputs = arr(wl.exec_inputs)
 
-        def mem_list(rows):
-            if not rows:
+        def mem_list(rows):  # int rows, or an (n, width, 4) uint64 array already in Montgomery limbs
+            if len(rows) == 0:
                 return 0, None
+            if isinstance(rows, np.ndarray) and rows.dtype == np.uint64:
+                return rows.shape[0], arr(rows)
             return len(rows), arr(to_mont_limbs(np.array(rows, dtype=object).reshape(-1)))
         c.total_num_init_phy_mem_accesses, c.init_phy_mems = mem_list(getattr(wl, "init_phy_mems", []))
         c.total_num_init_vir_mem_accesses, c.init_vir_mems = mem_list(getattr(wl, "init_vir_mems", []))

@@ -36,6 +36,13 @@ SNARK_CASES = {
     "mem_vir_b2_x64_q4": dict(num_blocks=2, log_cons=6, log_proofs=2, num_vars=64, vir_ops=2, init_vir=3, niu=5),
     "mem_both_b3_x64_q2": dict(num_blocks=3, log_cons=6, log_proofs=1, num_vars=64, phy_ops=1, vir_ops=2, init_phy=3,
                                init_vir=5, niu=5),
+    # uneven traces: block_num_proofs not sorted ([2, 4, 0]), a block that never runs, num_proofs = 1, per-block
+    # witness widths (num_vars_per_block) below num_vars
+    "uneven_b3_x32": dict(num_blocks=3, log_cons=5, log_proofs=1, num_vars=32, schedule=[0, 1, 1, 1, 0, 1]),
+    "widths_b3_x64": dict(num_blocks=3, log_cons=5, log_proofs=1, num_vars=64, vars_width=[64, 32, 32],
+                          schedule=[0, 1, 1, 2, 1]),
+    "mem_uneven_b3_x64": dict(num_blocks=3, log_cons=6, log_proofs=1, num_vars=64, phy_ops=1, vir_ops=2, init_phy=3,
+                              init_vir=5, niu=5, schedule=[2, 0, 2, 2, 0, 2]),
 }
 GPU_SNARK_CASES = {
     "b2_x1024_q8": dict(num_blocks=2, log_cons=10, log_proofs=3, num_vars=1024),

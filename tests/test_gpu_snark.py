@@ -69,3 +69,19 @@ def test_snark_matches_oracle_large(ctx, oracle, vars_gens, case):
     ref, rc = oracle.snark_prove(wl, workload.tape_seed())
     assert rc == 0
     _check(a, ref)
+
+
+@pytest.mark.parametrize("case", ["mem_uneven_b3_x64", "widths_b3_x64"])
+def test_circ_program_on_gpu(ctx, vars_gens, tmp_path, case):
+    """a program read back from CirC's .ctk/.rtk files (circ.CircProgram, examples/interface.rs) proves on the GPU
+    to the golden bytes of the program it was exported from"""
+    import circ
+    import workload
+
+    ctk, rtk = circ.export_workload(workload.SnarkWorkload(**SNARK_CASES[case]))
+    cp, rp = tmp_path / "p_bin.ctk", tmp_path / "p_bin.rtk"
+    cp.write_bytes(ctk.to_bytes())
+    rp.write_bytes(rtk.to_bytes())
+    proof = circ.prove(ctx, circ.CircProgram.load(str(cp), str(rp)), label=b"snark_test", vars_gens=vars_gens)
+    golden = json.load(open(os.path.join(G, "snark_proofs.json")))[case]
+    assert hashlib.sha256(proof).hexdigest() == golden["proof_sha256"]
