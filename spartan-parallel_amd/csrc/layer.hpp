@@ -230,9 +230,12 @@ __device__ __forceinline__ void quad_block_sum(Fq& e) {
   }
 }
 // the elements u = u0, u0 + ustride, ... of one round (a quad per element): this lane's share of its point's sum
+// ends (a layer's last round, one workgroup): lane p < 3 also writes its vector's two entries (lo, hi) to mailbox
+// scalars 3 + 6 c + 2 p, + 1, so the host folds the final claims itself once it has drawn the round's challenge
 __device__ __forceinline__ Fq layer_round_elems(const Triple* __restrict__ tr, const Fq* __restrict__ coeff, int nt,
                                                 int log_len, int do_fold, const Fq& r, const Fq* __restrict__ cin,
-                                                Fq* __restrict__ cout, long u0, long ustride) {
+                                                Fq* __restrict__ cout, long u0, long ustride,
+                                                uint32_t* __restrict__ ends = nullptr) {
   const int q = threadIdx.x & 3, len = 1 << log_len;
   const int pt = q < 3 ? q : 0;  // the evaluation point (and round-1 vector) this lane works on
   const long total = (long)nt << log_len;
@@ -256,6 +259,13 @@ __device__ __forceinline__ Fq layer_round_elems(const Triple* __restrict__ tr, c
       lo = src[i];
       hi = src[i + len];
     }
+    if (ends && q < 3) {
+      uint32_t* d = ends + 8 + 8 * (3 + 6 * c + 2 * q);
+      for (int j = 0; j < 8; j++) {
+        __hip_atomic_store(d + j, lo.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(d + 8 + j, hi.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
     const Fq al = fq_qbcast<0>(lo), ah = fq_qbcast<0>(hi), bl = fq_qbcast<1>(lo), bh = fq_qbcast<1>(hi);
     const Fq cl = fq_qbcast<2>(lo), ch = fq_qbcast<2>(hi);
     const Fq k = coeff[c];
@@ -268,17 +278,21 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
                                                       int nt, int log_len, int do_fold, Fq r, const Fq* __restrict__ cin,
                                                       Fq* __restrict__ cout, Fq* __restrict__ partials,
                                                       unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
-                                                      uint32_t seq, unsigned long long* probe) {
+                                                      uint32_t seq, unsigned long long* probe, int ends = 0) {
   __shared__ bool last;
   const int t = threadIdx.x, q = t & 3;
   unsigned long long* pr = probe ? probe + 8 * blockIdx.x : nullptr;
   if (pr && t == 0) pr[0] = wall_clock64();
+  // ends: only with one workgroup (the host launches it so), whose barrier below orders every wave's entry stores
+  // before the sequence number
   Fq e = layer_round_elems(tr, coeff, nt, log_len, do_fold, r, cin, cout, ((long)blockIdx.x * BS + t) >> 2,
-                           (long)gridDim.x * (BS / 4));
+                           (long)gridDim.x * (BS / 4), ends && gridDim.x == 1 ? mb : nullptr);
+  if (ends) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (pr && t == 0) pr[1] = wall_clock64();
   quad_block_sum<BS>(e);
   if (pr && t == 0) pr[2] = wall_clock64();
   if (gridDim.x == 1) {  // lanes 0..2 of wave 0 post e0, e2, e3, then lane 0 the sequence number
+    if (ends) __syncthreads();
     if (t < 3) {
       for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");

@@ -610,6 +610,7 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     };
     // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks; with
     // close_after the layer's (or the shard's) final entries follow in `fin`
+    static const bool ends_on = !getenv("SPG_LAYER_ENDS") || atoi(getenv("SPG_LAYER_ENDS")) != 0;
     auto run_rounds = [&](size_t log_len, bool local, bool close_after, FqV* fin) -> int {
       while (log_len > 0) {
         log_len--;
@@ -635,16 +636,20 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         } else {
           layer_grid(tr.size() * len, &K, &BS);
         }
+        // the layer's last round in one workgroup also posts every vector's two entries: the host then folds the
+        // final claims with the round's challenge, and no close launch (another round trip) follows
+        const bool ends = close_after && log_len == 0 && quad && K == 1 && 3 + 6 * tr.size() <= kMboxScalars &&
+                          ngroups * len < wide_min && ends_on;
         if (ngroups * len < wide_min) {
           KScope ks(ctx, "spark_layer_round", layer_bytes);
           const int nt = (int)tr.size(), lg = (int)log_len, df = pending ? 1 : 0;
           const uint32_t seq = ++ctx->mbox_seq;
           if (quad && BS == 64)
             hipLaunchKernelGGL(k_layer_round_q<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
-                               cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+                               cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr, ends ? 1 : 0);
           else if (quad)
             hipLaunchKernelGGL(k_layer_round_q<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, nt, lg, df, r_pend,
-                               cbuf[cur], cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
+                               cbuf[cur], cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr, ends ? 1 : 0);
           else if (BS == 64)
             hipLaunchKernelGGL(k_layer_round<64>, dim3(K), dim3(64), 0, s, dtr, dcoef, nt, lg, df, r_pend, cbuf[cur],
                                cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
@@ -654,14 +659,23 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         }
         if (pending) cur ^= 1;
         SPG_HIP(ctx, hipGetLastError());
-        Fq ev[3];
-        int rc2 = eval_reduce_finish(ctx, ev);
-        if (local) rc2 = comm_sum_fq(ctx, sh, rc2, ev, 3);
+        FqV ev(ends ? 3 + 6 * tr.size() : 3);
+        int rc2 = mbox_wait(ctx, ctx->mbox_seq, ev.data(), (int)ev.size());
+        if (local) rc2 = comm_sum_fq(ctx, sh, rc2, ev.data(), 3);
         if (rc2) return rc2;
         lp.lap("round_eval_wait");
-        r_pend = host_round(ev);
+        r_pend = host_round(ev.data());
         pending = true;
         lp.lap("round_host");
+        if (ends) {  // bound_poly_var_top of the length-2 vectors, on the host
+          fin->resize(3 * tr.size());
+          for (size_t c = 0; c < 3 * tr.size(); c++) {
+            const Fq lo = ev[3 + 2 * c], hi = ev[4 + 2 * c];
+            (*fin)[c] = fq_add(lo, fq_mul(r_pend, fq_sub(hi, lo)));
+          }
+          pending = false;
+          return 0;
+        }
       }
       return close_after ? close(*fin) : 0;
     };
