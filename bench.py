@@ -300,8 +300,15 @@ def main_snark(a):
     assert len(proofs) == 1, "proof bytes changed between steps"
     t1 = time.perf_counter()  # PCIe-inclusive variant: witness upload + prove (reported beside value)
     wit = spg.SnarkWitness(ctx, views.inputs)
-    step()
+    proof = step()
     t_incl = time.perf_counter() - t1
+    # SNARK::verify of the same proof on the product path (not part of value; reported beside it)
+    ok, why = spg.snark_verify(ctx, block, pairwise, perm_root, views.inputs, gens, spg.Transcript(b"snark_bench"), proof)
+    assert ok, why
+    t1 = time.perf_counter()
+    for _ in range(3):
+        spg.snark_verify(ctx, block, pairwise, perm_root, views.inputs, gens, spg.Transcript(b"snark_bench"), proof)
+    t_verify = (time.perf_counter() - t1) / 3
     N = wl.total_constraints
     value = N * world * a.steps / dt
     top = sorted(prof.items(), key=lambda kv: -kv[1][1])[:10]
@@ -334,7 +341,8 @@ def main_snark(a):
             "roofline": roofline_of(prof, a.traffic), "cpu_baseline": cpu, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16], "proof_bytes": None,
             "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
-            "value_incl_witness_upload": round(N * world / t_incl, 1), "encode_s": round(t_encode, 3),
+            "value_incl_witness_upload": round(N * world / t_incl, 1), "verify_ms": round(t_verify * 1e3, 2),
+            "encode_s": round(t_encode, 3),
             "host_gen_s": round(t_gen, 3), "kernels": kernels}))
     if dist is not None:
         dist.destroy_process_group()

@@ -30,6 +30,7 @@ extern "C" {
 #define SPG_E_HIP -3       /* HIP runtime error */
 #define SPG_E_POINT -4     /* invalid compressed point (ProofVerifyError::DecompressionError) */
 #define SPG_E_NODEVICE -5  /* no usable gfx950 device */
+#define SPG_E_VERIFY -6    /* a proof did not verify (spg_last_error names the failed check) */
 
 typedef struct spg_ctx spg_ctx;
 typedef struct spg_gens spg_gens;
@@ -264,6 +265,15 @@ int spg_snark_witness_free(spg_ctx* ctx, spg_snark_wit* wit);
 int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_comp* pairwise, spg_snark_comp* perm_root,
                     const spg_snark_wit* wit, spg_r1cs_gens* vars_gens, spg_transcript* transcript,
                     spg_random_tape* tape, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+
+/* SNARK::verify (src/lib.rs:2750-3881): replays the transcript from the public inputs (the spg_snark_inputs sizes,
+ * input / output / liveness and the init memory lists; block_vars, exec_inputs and the address lists are not
+ * read), the three encoded instances (their SPARK commitments) and the proof bytes, and runs every check of the
+ * reference verifier. transcript must be a fresh one with the prover's label. Returns 0 when the proof verifies,
+ * SPG_E_VERIFY when it does not (malformed bytes included), another negative code on bad arguments. */
+int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
+                     const spg_snark_comp* perm_root, const spg_snark_inputs* inputs, spg_r1cs_gens* vars_gens,
+                     spg_transcript* transcript, const uint8_t* proof, size_t proof_len);
 
 #ifdef __cplusplus
 }

@@ -198,3 +198,26 @@ struct spg_random_tape {
 struct spg_r1cs_gens {  // R1CSGens: one derived stream; gens_pc / gens_1 / gens_4 are views of it
   spg::ProverGens g;
 };
+// SPARK dense representation in HBM (spark.hip) with its commitment and generators (the verifier reads the latter)
+struct spg_spark {
+  size_t B = 0, N = 0, cells = 0;
+  uint32_t* d_addr = nullptr;   // [2][B][N]
+  uint32_t* d_rts = nullptr;    // [2][B][N]
+  uint32_t* d_audit = nullptr;  // [2][cells]
+  spg::Fq* d_val = nullptr;     // [B][N]
+  spg::Fq* d_comb_ops = nullptr;
+  spg::Fq* d_comb_mem = nullptr;
+  size_t comb_ops_len = 0, comb_mem_len = 0;
+  spg_gens* dev = nullptr;
+  spg::ProverGens g_ops, g_mem, g_der;
+  std::vector<spg::Pt> comm_ops, comm_mem;  // SparseMatPolyCommitment
+};
+namespace spg {
+// what SNARK::verify reads of an encoded instance (snark.hip fills it, verify.hip reads it)
+struct SnarkCompView {
+  size_t num_instances, max_num_cons, num_vars;
+  const std::vector<std::vector<size_t>>* label_map;
+  const std::vector<spg_spark*>* sparks;
+};
+int snark_comp_view(const spg_snark_comp* C, SnarkCompView* v);
+}  // namespace spg

@@ -546,6 +546,7 @@ int Prover::run_inner(Laps& lp) {
   FqV tau_p = t.challenges("challenge_tau_p", np);
   FqV tau_q = t.challenges("challenge_tau_q", nq);
   FqV tau_x = t.challenges("challenge_tau_x", nx);
+  if (getenv("SPG_DEBUG_TR")) fprintf(stderr, "[prove] r1cs P=%zu np=%zu nq=%zu nx=%zu tau_x0 %08x\n", (size_t)P, (size_t)np, (size_t)nq, (size_t)nx, tau_x[0].l[0]);
   Fq* Ap = (Fq*)ws_get(ctx, WS_TP, (sizeof(Fq) << np) + 64);
   Fq* Aq = (Fq*)ws_get(ctx, WS_TQ, (sizeof(Fq) << nq) + 64);
   Fq* Ax = (Fq*)ws_get(ctx, WS_TX, (sizeof(Fq) << nx) + 64);

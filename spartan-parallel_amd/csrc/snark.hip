@@ -545,6 +545,19 @@ extern "C" int spg_snark_encode(spg_ctx* ctx, const spg_snark_instance* si, int 
 }
 extern "C" int spg_snark_comp_free(spg_ctx* ctx, spg_snark_comp* C) { return snark_comp_free(ctx, C); }
 
+namespace spg {
+// what SNARK::verify reads of an encoded instance (verify.hip)
+int snark_comp_view(const spg_snark_comp* C, SnarkCompView* v) {
+  if (!C || C->sparks.empty() || C->label_map.size() != C->sparks.size()) return SPG_E_ARG;
+  v->num_instances = C->num_instances;
+  v->max_num_cons = C->max_num_cons;
+  v->num_vars = C->num_vars;
+  v->label_map = &C->label_map;
+  v->sparks = &C->sparks;
+  return 0;
+}
+}  // namespace spg
+
 extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, spg_snark_wit** out) {
   if (!ctx || !a || !out || !a->block_num_instances_bound || !a->num_inputs_unpadded || !a->num_ios) return SPG_E_ARG;
   spg_snark_wit* W = new spg_snark_wit();
@@ -778,6 +791,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   }
   // ---- WITNESS GEN: block (lib.rs:1299-1741)
   const Fq tau = t.challenge("challenge_tau"), r = t.challenge("challenge_r");
+  if (getenv("SPG_DEBUG_TR")) fprintf(stderr, "[prove] tau %08x r %08x\n", tau.l[0], r.l[0]);
   const bool dbg = getenv("SPG_DEBUG_SNARK") != nullptr;
   if (dbg) fprintf(stderr, "snark tau %08x %08x r %08x\n", tau.l[0], tau.l[1], r.l[0]);
   FqV perm_w0 = {tau};

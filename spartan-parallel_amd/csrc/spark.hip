@@ -281,19 +281,6 @@ __global__ void k_bound_sum(const Fq* __restrict__ part, size_t S, size_t Rs, Fq
 using namespace spg;
 
 // ------------------------------------------------------------------------------------ handle
-struct spg_spark {
-  size_t B = 0, N = 0, cells = 0;
-  uint32_t* d_addr = nullptr;   // [2][B][N]
-  uint32_t* d_rts = nullptr;    // [2][B][N]
-  uint32_t* d_audit = nullptr;  // [2][cells]
-  Fq* d_val = nullptr;          // [B][N]
-  Fq* d_comb_ops = nullptr;
-  Fq* d_comb_mem = nullptr;
-  size_t comb_ops_len = 0, comb_mem_len = 0;
-  spg_gens* dev = nullptr;
-  ProverGens g_ops, g_mem, g_der;
-  std::vector<spg::Pt> comm_ops, comm_mem;  // SparseMatPolyCommitment
-};
 
 namespace spg {
 

@@ -16,7 +16,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPG_LIB") or os.path.join(_HERE, "lib", "libspg.so")
 
-SPG_ERRORS = {-1: "SPG_E_ARG", -2: "SPG_E_NOMEM", -3: "SPG_E_HIP", -4: "SPG_E_POINT", -5: "SPG_E_NODEVICE"}
+SPG_ERRORS = {-1: "SPG_E_ARG", -2: "SPG_E_NOMEM", -3: "SPG_E_HIP", -4: "SPG_E_POINT", -5: "SPG_E_NODEVICE",
+              -6: "SPG_E_VERIFY"}
 
 _lib = None
 
@@ -525,6 +526,22 @@ def snark_prove(ctx, block, pairwise, perm_root, witness, vars_gens, transcript,
                                     vars_gens.handle, transcript.handle, tape.handle, _p(buf), ctypes.c_size_t(cap),
                                     ctypes.byref(ln)), "spg_snark_prove")
     return buf[: ln.value].tobytes()
+
+
+SPG_E_VERIFY = -6
+
+
+def snark_verify(ctx, block, pairwise, perm_root, inputs, vars_gens, transcript, proof):
+    """SNARK::verify (src/lib.rs:2750-3881) of bincode(SNARK) bytes against the encoded instances and the public
+    inputs (`inputs`: workload.SnarkViews().inputs; only its sizes, input / output and init memory lists are read).
+    Returns (True, "") when the proof verifies, (False, reason) when it does not; raises on bad arguments."""
+    buf = np.frombuffer(bytes(proof), dtype=np.uint8).copy() if len(proof) else np.zeros(1, np.uint8)
+    rc = lib().spg_snark_verify(ctx.handle, block.handle, pairwise.handle, perm_root.handle, ctypes.byref(inputs),
+                                vars_gens.handle, transcript.handle, _p(buf), ctypes.c_size_t(len(proof)))
+    if rc == SPG_E_VERIFY:
+        return False, lib().spg_last_error(ctx.handle).decode(errors="replace")
+    ctx.check(rc, "spg_snark_verify")
+    return True, ""
 
 
 def points_sum_compress(parts):
