@@ -203,6 +203,11 @@ int spg_spark_commit(spg_ctx* ctx, const spg_r1cs_instance* inst, const uint8_t*
 int spg_spark_prove(spg_ctx* ctx, spg_spark* s, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
                     size_t ry_len, const uint64_t* evals, size_t n_evals, spg_transcript* transcript,
                     spg_random_tape* tape, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+/* SparseMatPolyEvalProof::verify (src/sparse_mlpoly.rs:1566-1610) of proof bytes against s's commitment: 0 when
+ * it verifies, SPG_E_VERIFY when it does not (spg_last_error names the failed check). */
+int spg_spark_verify(spg_ctx* ctx, spg_spark* s, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                     size_t ry_len, const uint64_t* evals, size_t n_evals, spg_transcript* transcript,
+                     const uint8_t* proof, size_t proof_len);
 int spg_spark_free(spg_ctx* ctx, spg_spark* s);
 
 /* ---- SNARK::prove (src/lib.rs:971-2746) -------------------------------------------------------------

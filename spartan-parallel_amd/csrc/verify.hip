@@ -1386,3 +1386,30 @@ extern "C" int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const
   if (!ok) return set_err(ctx, SPG_E_VERIFY, std::string("snark verify: ") + (v.failed ? v.failed : "rejected"));
   return SPG_OK;
 }
+
+/* SparseMatPolyEvalProof::verify (src/sparse_mlpoly.rs:1566-1610) against the commitment held by s */
+extern "C" int spg_spark_verify(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                                size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
+                                const uint8_t* proof, size_t proof_len) {
+  if (!ctx || !S || !transcript || (!rx && rx_len) || (!ry && ry_len) || (!evals_in && n_evals) || (!proof && proof_len))
+    return SPG_E_ARG;
+  if (n_evals != S->B) return set_err(ctx, SPG_E_ARG, "spark verify: one evaluation per matrix");
+  FqV ex, ey, evals(n_evals);
+  for (size_t i = 0; i < rx_len; i++) ex.push_back(ld_fq(rx + 4 * i));
+  for (size_t i = 0; i < ry_len; i++) ey.push_back(ld_fq(ry + 4 * i));
+  for (size_t i = 0; i < n_evals; i++) evals[i] = ld_fq(evals_in + 4 * i);
+  SPG_HIP(ctx, hipSetDevice(ctx->device));
+  SparkV pf;
+  Rd r(proof, proof_len);
+  rd(r, pf);
+  if (r.bad || r.o != r.n) return set_err(ctx, SPG_E_VERIFY, "spark verify: malformed proof bytes");
+  SnarkVerifier v(ctx, transcript->t);
+  bool ok = false;
+  try {
+    ok = v.spark(S, pf, ex, ey, evals);
+  } catch (const Fail& f) {
+    v.fail(f.what);
+  }
+  if (!ok) return set_err(ctx, SPG_E_VERIFY, std::string("spark verify: ") + (v.failed ? v.failed : "rejected"));
+  return SPG_OK;
+}

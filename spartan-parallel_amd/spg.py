@@ -464,6 +464,18 @@ class SparkCommitment:
                                              ctypes.byref(ln)), "spg_spark_prove")
         return buf[: ln.value].tobytes()
 
+    def verify(self, rx, ry, evals, transcript, proof):
+        """SparseMatPolyEvalProof::verify (src/sparse_mlpoly.rs:1566-1610) -> (ok, reason)"""
+        rx, ry, ev = _scalars(rx), _scalars(ry), _scalars(evals)
+        buf = np.frombuffer(bytes(proof), dtype=np.uint8).copy() if len(proof) else np.zeros(1, np.uint8)
+        rc = lib().spg_spark_verify(self.ctx.handle, self._h, _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
+                                    ctypes.c_size_t(ry.shape[0]), _p(ev), ctypes.c_size_t(ev.shape[0]),
+                                    transcript.handle, _p(buf), ctypes.c_size_t(len(proof)))
+        if rc == SPG_E_VERIFY:
+            return False, lib().spg_last_error(self.ctx.handle).decode(errors="replace")
+        self.ctx.check(rc, "spg_spark_verify")
+        return True, ""
+
     def __del__(self):
         try:
             if self._h:

@@ -100,3 +100,35 @@ def test_spark_round_kernel_forms(oracle, env):
     wl, rx, ry = spark_inputs(oracle, "p2_x64_2secs")
     _, ref, ok = oracle.spark_prove(wl, rx, ry, workload.tape_seed())
     assert ok and out.stdout.split()[-1] == hashlib.sha256(ref).hexdigest()
+
+
+@pytest.mark.parametrize("case", sorted(SPARK_CASES))
+def test_spark_verify(ctx, oracle, case):
+    """spg_spark_verify (SparseMatPolyEvalProof::verify) accepts the GPU proof (the oracle's bytes) and rejects it
+    with a field altered, other evaluations or another transcript label"""
+    import spg
+    import workload
+    from proof_layout import spark_proof_fields
+
+    wl, rx, ry = spark_inputs(oracle, case)
+    v = workload.CViews(wl)
+    gens_nnz = len(wl.entries) * max(max(int(m.shape[0]) for m in mats) for mats in wl.entries)
+    comm = spg.SparkCommitment(ctx, v.inst, GENS_LABEL, gens_nnz, 3)
+    evals = spg.r1cs_multi_evaluate(ctx, spg.R1CSInst(ctx, v.inst), len(wl.entries), rx, ry)
+    proof = comm.prove(rx, ry, evals, spg.Transcript(b"spark_test"), spg.RandomTape(b"proof", workload.tape_seed()))
+    ok, why = comm.verify(rx, ry, evals, spg.Transcript(b"spark_test"), proof)
+    assert ok, why
+    ok, _ = comm.verify(rx, ry, evals, spg.Transcript(b"spark_other"), proof)
+    assert not ok
+    bad_evals = evals.copy()
+    bad_evals[0] = workload.to_mont_limbs([1])[0]
+    if (bad_evals == evals).all():
+        bad_evals[0] = workload.to_mont_limbs([2])[0]
+    ok, _ = comm.verify(rx, ry, bad_evals, spg.Transcript(b"spark_test"), proof)
+    assert not ok
+    fields = spark_proof_fields(proof)
+    for name, s, e in fields[:: max(1, len(fields) // 24)]:
+        bad = bytearray(proof)
+        bad[s + (e - s) // 2] ^= 0x04
+        ok, _ = comm.verify(rx, ry, evals, spg.Transcript(b"spark_test"), bytes(bad))
+        assert not ok, f"accepted with {name} altered"

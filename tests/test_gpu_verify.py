@@ -82,3 +82,27 @@ def test_verify_rejects_other_transcript_or_inputs(ctx, vars_gens):
     prog.v.inputs.output = out.ctypes.data_as(ctypes.c_void_p).value
     ok, why = prog.verify()
     assert not ok, "accepted a wrong output"
+
+
+@pytest.mark.parametrize("a,b", [("io_proof.proofs[0]", "io_proof.proofs[1]"),
+                                 ("shift_proof.C_orig_evals[0]", "shift_proof.C_orig_evals[1]"),
+                                 ("block_r1cs_eval_proof_list[0].dotp_left[0]", "block_r1cs_eval_proof_list[0].dotp_right[0]")])
+def test_verify_rejects_swapped_parts(ctx, vars_gens, a, b):
+    """well-formed proofs with two parts exchanged (the oracle's ORC_TAMPER cases io_proof / shift_eval, whose
+    verifier rejects them at IOProofs / ShiftProofs, tests/test_oracle_snark.py): the product verifier rejects too"""
+    from proof_layout import snark_proof_fields
+
+    prog = Program(ctx, vars_gens, "b2_x32_q2")
+    spans = {}
+    for name, s, e in snark_proof_fields(prog.proof):
+        for want in (a, b):
+            if name == want or name.startswith(want + "."):
+                lo, hi = spans.get(want, (s, e))
+                spans[want] = (min(lo, s), max(hi, e))
+    (sa, ea), (sb, eb) = spans[a], spans[b]
+    assert ea - sa == eb - sb and ea <= sb
+    p = prog.proof
+    swapped = p[:sa] + p[sb:eb] + p[ea:sb] + p[sa:ea] + p[eb:]
+    assert swapped != p
+    ok, why = prog.verify(swapped)
+    assert not ok, f"accepted with {a} and {b} exchanged"
