@@ -180,6 +180,28 @@ int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst*
                    const spg_r1cs_witness* witness, spg_transcript* transcript, spg_random_tape* tape,
                    uint8_t* proof, size_t proof_cap, size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens);
 
+/* DensePolynomial::commit without blinds (src/dense_mlpoly.rs:184-256) of n scalars (zero-padded to a power of
+ * two 2^k) with gens.gens_pc: L = 2^(k/2) Hyrax row commitments of 2^(k - k/2) scalars into out (32 bytes each,
+ * out_cap bytes; *L_out = L). The commitments spg_r1cs_verify takes for every witness section instance. */
+int spg_r1cs_gens_commit(spg_ctx* ctx, const spg_r1cs_gens* gens, const uint64_t* Z, size_t n, uint8_t* out,
+                         size_t out_cap, size_t* L_out);
+/* the verifier's view of one witness section (VerifierWitnessSecInfo, src/lib.rs:606-698) */
+typedef struct {
+  size_t num_instances;      /* 1 (single) or P                                               */
+  const size_t* num_proofs;  /* [num_instances]                                               */
+  const size_t* num_inputs;  /* [num_instances]                                               */
+  const size_t* comm_len;    /* [num_instances]: Hyrax rows of each instance's commitment       */
+  const uint8_t* comms;      /* the row commitments of instance 0, then 1, ... (32 bytes each)   */
+} spg_witness_comm;
+/* R1CSProof::verify (src/r1csproof.rs:687-954) of bincode(R1CSProof) bytes: evals = the claimed (A, B, C)(rx, ry)
+ * bound with eq(rp) (multi_evaluate_bound_rp), num_cons = the instance's max_num_cons. 0 when the proof verifies
+ * (and, when challenges_out != NULL, rp | rq_rev | rx | rw||ry with their lengths in ch_lens[4], as
+ * spg_r1cs_prove returns them), SPG_E_VERIFY when it does not. */
+int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t num_instances, size_t max_num_proofs,
+                    const size_t* num_proofs, size_t max_num_inputs, const spg_witness_comm* secs, size_t nws,
+                    size_t num_cons, const uint64_t* evals, spg_transcript* transcript, const uint8_t* proof,
+                    size_t proof_len, uint64_t* challenges_out, size_t* ch_lens);
+
 /* R1CSInstance::multi_evaluate (src/r1csinstance.rs:583-596) via SparseMatPolynomial::evaluate_with_tables
  * (src/sparse_mlpoly.rs:427-450): out[3p + m] = M_p(rx, ry), M in (A, B, C), for every matrix instance p
  * of the uploaded instance; 2^rx_len >= max_num_cons, 2^ry_len >= num_vars. (With one instance this is

@@ -1413,3 +1413,72 @@ extern "C" int spg_spark_verify(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, 
   if (!ok) return set_err(ctx, SPG_E_VERIFY, std::string("spark verify: ") + (v.failed ? v.failed : "rejected"));
   return SPG_OK;
 }
+
+extern "C" int spg_r1cs_gens_commit(spg_ctx* ctx, const spg_r1cs_gens* gens, const uint64_t* Z, size_t n, uint8_t* out,
+                                    size_t out_cap, size_t* L_out) {
+  if (!ctx || !gens || (!Z && n) || !L_out) return SPG_E_ARG;
+  SPG_HIP(ctx, hipSetDevice(ctx->device));
+  FqV z(n);
+  for (size_t i = 0; i < n; i++) z[i] = ld_fq(Z + 4 * i);
+  PolyComm c;
+  try {
+    c = commit_vec(ctx, const_cast<ProverGens&>(gens->g), z);
+  } catch (const Fail& f) {
+    return set_err(ctx, SPG_E_HIP, std::string("r1cs gens commit: ") + f.what);
+  }
+  *L_out = c.size();
+  if (!out || 32 * c.size() > out_cap) return set_err(ctx, SPG_E_ARG, "r1cs gens commit: output buffer too small");
+  for (size_t i = 0; i < c.size(); i++) memcpy(out + 32 * i, c[i].b, 32);
+  return SPG_OK;
+}
+
+extern "C" int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t num_instances, size_t max_num_proofs,
+                               const size_t* num_proofs, size_t max_num_inputs, const spg_witness_comm* secs, size_t nws,
+                               size_t num_cons, const uint64_t* evals, spg_transcript* transcript, const uint8_t* proof,
+                               size_t proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  if (!ctx || !gens || !num_instances || !num_proofs || !secs || !nws || !evals || !transcript || (!proof && proof_len))
+    return SPG_E_ARG;
+  if (!is_pow2(max_num_proofs) || !is_pow2(max_num_inputs) || !is_pow2(num_cons) || nws > 8)
+    return set_err(ctx, SPG_E_ARG, "r1cs verify: sizes");
+  std::vector<VSec> vs(nws);
+  std::vector<const VSec*> ws;
+  for (size_t i = 0; i < nws; i++) {
+    const spg_witness_comm& c = secs[i];
+    if (!c.num_instances || !c.num_proofs || !c.num_inputs || !c.comm_len) return set_err(ctx, SPG_E_ARG, "r1cs verify: section");
+    size_t o = 0;
+    for (size_t p = 0; p < c.num_instances; p++) {
+      vs[i].num_proofs.push_back(c.num_proofs[p]);
+      vs[i].num_inputs.push_back(c.num_inputs[p]);
+      PolyComm pc(c.comm_len[p]);
+      for (size_t k = 0; k < c.comm_len[p]; k++) memcpy(pc[k].b, c.comms + 32 * (o + k), 32);
+      o += c.comm_len[p];
+      vs[i].comm_w.push_back(pc);
+    }
+    ws.push_back(&vs[i]);
+  }
+  const std::vector<size_t> np(num_proofs, num_proofs + num_instances);
+  const Fq ev[3] = {ld_fq(evals), ld_fq(evals + 4), ld_fq(evals + 8)};
+  SPG_HIP(ctx, hipSetDevice(ctx->device));
+  R1CSProofP pf;
+  Rd r(proof, proof_len);
+  rd(r, pf);
+  if (r.bad || r.o != r.n) return set_err(ctx, SPG_E_VERIFY, "r1cs verify: malformed proof bytes");
+  SnarkVerifier v(ctx, transcript->t);
+  std::vector<FqV> ch;
+  bool ok = false;
+  try {
+    ok = v.r1cs(const_cast<ProverGens&>(gens->g), pf, num_instances, max_num_proofs, np, max_num_inputs, ws, num_cons,
+                ev, &ch);
+  } catch (const Fail& f) {
+    v.fail(f.what);
+  }
+  if (!ok) return set_err(ctx, SPG_E_VERIFY, std::string("r1cs verify: ") + (v.failed ? v.failed : "rejected"));
+  if (challenges_out && ch_lens) {
+    size_t o = 0;
+    for (int k = 0; k < 4; k++) {
+      ch_lens[k] = ch[k].size();
+      for (auto& x : ch[k]) st_fq(challenges_out + 4 * o++, x);
+    }
+  }
+  return SPG_OK;
+}

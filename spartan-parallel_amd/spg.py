@@ -421,6 +421,53 @@ def r1cs_prove(ctx, gens, inst, witness, num_instances, max_num_proofs, num_proo
     return buf[: ln.value].tobytes(), out
 
 
+class CWitnessComm(ctypes.Structure):
+    _fields_ = [("num_instances", ctypes.c_size_t), ("num_proofs", ctypes.POINTER(ctypes.c_size_t)),
+                ("num_inputs", ctypes.POINTER(ctypes.c_size_t)), ("comm_len", ctypes.POINTER(ctypes.c_size_t)),
+                ("comms", ctypes.c_void_p)]
+
+
+def r1cs_gens_commit(ctx, gens, Z):
+    """DensePolynomial::commit (no blinds) with gens.gens_pc -> list of 32-byte Hyrax row commitments"""
+    z = _scalars(Z)
+    out = np.zeros(32 * 4096, dtype=np.uint8)
+    L = ctypes.c_size_t(0)
+    ctx.check(lib().spg_r1cs_gens_commit(ctx.handle, gens.handle, _p(z), ctypes.c_size_t(z.shape[0]), _p(out),
+                                         ctypes.c_size_t(out.shape[0]), ctypes.byref(L)), "spg_r1cs_gens_commit")
+    return [out[32 * i: 32 * i + 32].tobytes() for i in range(L.value)]
+
+
+def r1cs_verify(ctx, gens, num_instances, max_num_proofs, num_proofs, max_num_inputs, sections, num_cons, evals,
+                transcript, proof):
+    """R1CSProof::verify (src/r1csproof.rs:687-954). sections: per witness section (num_proofs, num_inputs, comms)
+    with one entry per instance (comms: lists of 32-byte row commitments). Returns (ok, reason, challenges)."""
+    keep = []
+    secs = (CWitnessComm * len(sections))()
+    for i, (npf, nin, comms) in enumerate(sections):
+        a, b = (ctypes.c_size_t * len(npf))(*npf), (ctypes.c_size_t * len(nin))(*nin)
+        cl = (ctypes.c_size_t * len(comms))(*[len(c) for c in comms])
+        blob = np.frombuffer(b"".join(b"".join(c) for c in comms) or b"\0", dtype=np.uint8).copy()
+        keep += [a, b, cl, blob]
+        secs[i] = CWitnessComm(len(npf), a, b, cl, blob.ctypes.data)
+    ev = _scalars(evals)
+    buf = np.frombuffer(bytes(proof), dtype=np.uint8).copy() if len(proof) else np.zeros(1, np.uint8)
+    ch = np.zeros((4096, 4), dtype=np.uint64)
+    chl = (ctypes.c_size_t * 4)()
+    npf = (ctypes.c_size_t * num_instances)(*num_proofs)
+    rc = lib().spg_r1cs_verify(ctx.handle, gens.handle, ctypes.c_size_t(num_instances), ctypes.c_size_t(max_num_proofs),
+                               npf, ctypes.c_size_t(max_num_inputs), secs, ctypes.c_size_t(len(sections)),
+                               ctypes.c_size_t(num_cons), _p(ev), transcript.handle, _p(buf), ctypes.c_size_t(len(proof)),
+                               _p(ch), chl)
+    if rc == SPG_E_VERIFY:
+        return False, lib().spg_last_error(ctx.handle).decode(errors="replace"), None
+    ctx.check(rc, "spg_r1cs_verify")
+    out, o = [], 0
+    for L in list(chl):
+        out.append(ch[o:o + L].copy())
+        o += L
+    return True, "", out
+
+
 def shard_range(num_instances, rank, nranks):
     """instances [p0, p1) held by `rank` in a sharded R1CSProof (include/spg.h, spg_set_comm): balanced split,
     the first num_instances % nranks ranks hold one instance more (same rule as r1cs.hip Prover::shard_begin)"""

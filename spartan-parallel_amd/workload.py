@@ -125,17 +125,6 @@ class R1CSWorkload:
             self.sections.append(mats)
 
     @property
-    def num_vars_per_block(self):
-        return list(self._vars_width)
-
-    @property
-    def block_vars_sorted(self):
-        """block_vars in the prover's instance order (num_proofs descending, stable): the reference pairs
-        block_vars_mat[i] with sorted instance i (src/lib.rs:1155-1178)"""
-        order = sorted(range(self.num_blocks), key=lambda b: -self.block_num_proofs[b])
-        return [self.block_vars[b] for b in order]
-
-    @property
     def total_constraints(self):
         return sum(x * q for x, q in zip(self.num_cons, self.num_proofs))
 

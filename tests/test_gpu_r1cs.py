@@ -83,3 +83,60 @@ def test_multi_evaluate_matches_oracle(ctx, oracle, case):
     got = spg.r1cs_multi_evaluate(ctx, inst, len(wl.entries), rx, ry)
     ref = oracle.r1cs_multi_evaluate(wl, rx, ry)
     assert np.array_equal(got, ref)
+
+
+def _int(m):
+    import workload
+
+    v = sum(int(m[i]) << (64 * i) for i in range(4))
+    return v * pow(workload.R, -1, workload.Q) % workload.Q
+
+
+def _eq_table(r):
+    import workload
+
+    t = [1]
+    for x in r:
+        t = [v * (1 - x) % workload.Q for v in t] + [v * x % workload.Q for v in t]
+        t = [t[i // 2 + (i % 2) * (len(t) // 2)] for i in range(len(t))]
+    return t
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_r1cs_verify(ctx, r1cs_gens, case):
+    """spg_r1cs_verify (R1CSProof::verify) accepts the GPU proof with the witness commitments and the rp-bound
+    evaluations (multi_evaluate_bound_rp), returns the prover's challenges, and rejects altered claims"""
+    import spg
+    import workload
+
+    nc, npf, nws, shared = CASES[case]
+    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+    proof, ch = gpu_prove(ctx, r1cs_gens, wl, workload.tape_seed())
+    rp, rx, rwry = ch[0], ch[2], ch[3]
+    v = workload.CViews(wl)
+    ev = spg.r1cs_multi_evaluate(ctx, spg.R1CSInst(ctx, v.inst), len(wl.entries), rx, rwry)
+    eq = _eq_table([_int(x) for x in rp])
+    if len(wl.entries) == 1:
+        bound = [_int(ev[k]) for k in range(3)]
+    else:
+        bound = [sum(eq[p] * _int(ev[3 * p + k]) for p in range(wl.P)) % workload.Q for k in range(3)]
+    sections = []
+    for w in range(wl.nws):
+        mats = wl.sections[w]
+        sections.append(([m.shape[0] for m in mats], [m.shape[1] for m in mats],
+                         [spg.r1cs_gens_commit(ctx, r1cs_gens, m.reshape(-1, 4)) for m in mats]))
+    args = (ctx, r1cs_gens, wl.P, wl.max_num_proofs, wl.num_proofs, wl.max_num_inputs, sections, wl.max_num_cons)
+    ok, why, vch = spg.r1cs_verify(*args, workload.to_mont_limbs(bound), spg.Transcript(b"r1cs_test"), proof)
+    assert ok, why
+    for a, b in zip(vch, ch):
+        assert np.array_equal(a, b)
+    bad = list(bound)
+    bad[1] = (bad[1] + 1) % workload.Q
+    ok, _, _ = spg.r1cs_verify(*args, workload.to_mont_limbs(bad), spg.Transcript(b"r1cs_test"), proof)
+    assert not ok
+    other = list(sections)
+    other[0] = (other[0][0], other[0][1], [list(reversed(c)) if len(c) > 1 else c for c in other[0][2]])
+    if other[0][2] != sections[0][2]:
+        ok, _, _ = spg.r1cs_verify(*args[:6], other, wl.max_num_cons, workload.to_mont_limbs(bound),
+                                   spg.Transcript(b"r1cs_test"), proof)
+        assert not ok
