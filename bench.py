@@ -314,7 +314,7 @@ def main_snark(a):
     top = sorted(prof.items(), key=lambda kv: -kv[1][1])[:10]
     kernels = {n: {"launches_per_step": v[0] / a.steps, "ms_per_step": round(v[1] / a.steps / 1e3, 3),
                    "GBps": round(v[2] / (v[1] * 1e-6) / 1e9, 1) if v[2] else None} for n, v in top}
-    cpu, bitexact = None, None
+    cpu, bitexact, cpu_verify_ms = None, None, None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle  # the checker / CPU baseline only
@@ -323,6 +323,7 @@ def main_snark(a):
         ref, rc = pyoracle.snark_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS,
                                        label=b"snark_bench")
         tcpu = pyoracle.snark_last_prove_us() * 1e-6
+        cpu_verify_ms = pyoracle.snark_last_verify_us() * 1e-3
         cpu = {"value": round(N / tcpu, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
                "sample": f"full workload ({N} constraints), one SNARK::prove (instances pre-encoded), "
                          f"{tcpu:.2f} s on 1 host thread; oracle verifier status {rc}"}
@@ -342,7 +343,7 @@ def main_snark(a):
             "proof_sha256": sorted(proofs)[0][:16], "proof_bytes": None,
             "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
             "value_incl_witness_upload": round(N * world / t_incl, 1), "verify_ms": round(t_verify * 1e3, 2),
-            "verify_ok": verify_ok,
+            "verify_ok": verify_ok, "cpu_verify_ms_1thread": None if cpu_verify_ms is None else round(cpu_verify_ms, 1),
             "encode_s": round(t_encode, 3),
             "host_gen_s": round(t_gen, 3), "kernels": kernels}))
     if dist is not None:
@@ -433,7 +434,7 @@ def main_msm(a):
             "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(dev_us, 1), "launches": a.steps,
             "valu": {"mixed_adds_per_msm": madds, "mixed_adds_per_s": round(madds / (dev_us * 1e-6), 1),
                      "note": "fixed-base signed windows: one 7M mixed addition per nonzero digit"}}
-    cpu, bitexact = None, None
+    cpu, bitexact, cpu_verify_ms = None, None, None
     if rank == 0 and not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import numpy as np

@@ -386,6 +386,7 @@ int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t 
 
 namespace {
 using namespace orc;
+double g_snark_verify_us = 0;
 double g_snark_prove_us = 0.0;
 
 SnarkIn snark_in_from_c(const spg_snark_inputs* c) {
@@ -493,10 +494,14 @@ int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* bloc
     if (tamper && std::string(tamper) == "perm_opening" && !pf.proof_eval_perm_poly_prod_list.empty())
       std::swap(pf.proof_eval_perm_poly_prod_list[0], pf.proof_eval_perm_poly_prod_list.back());
     Transcript tv(label);
-    return snark_verify(pf, in, block, pairwise, perm_root, vg, tv);
+    auto t1 = std::chrono::steady_clock::now();
+    const int rc = snark_verify(pf, in, block, pairwise, perm_root, vg, tv);
+    g_snark_verify_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
+    return rc;
   } catch (const std::string& e) {
     return -2;
   }
 }
 double orc_snark_last_prove_us() { return g_snark_prove_us; }
+double orc_snark_last_verify_us() { return g_snark_verify_us; }
 }

@@ -300,3 +300,9 @@ def snark_last_prove_us():
     f = lib().orc_snark_last_prove_us
     f.restype = ctypes.c_double
     return f()
+
+
+def snark_last_verify_us():
+    f = lib().orc_snark_last_verify_us
+    f.restype = ctypes.c_double
+    return f()
