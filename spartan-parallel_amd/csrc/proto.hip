@@ -195,7 +195,12 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extr
   // chunk (lo, hi] of a bucket set: run = sum B_v, acc = sum (v - lo) B_v; the set's sum is
   // sum over chunks of acc + lo * run. Chunks spread one MSM's 2 NB dependent additions over the pool;
   // the last chunk of an MSM to finish (countdown) adds the chunks and encodes, all in one burst.
-  const int K = NB >= 64 ? 8 : 1, per = NB / K, stride = NB + (carry ? 1 : 0);
+  // chunks per set: one burst wave over the pool (B sets x K chunks ~ threads; at least 2 buckets per chunk)
+  static const int kmax = getenv("SPG_FINALS_K") ? std::max(1, atoi(getenv("SPG_FINALS_K"))) : 8;
+  const int threads = pool().size() + 1;
+  int K = NB >= 64 ? std::max(1, std::min(kmax, threads / (int)std::max<size_t>(B, 1))) : 1;
+  while (NB % K) K--;
+  const int per = NB / K, stride = NB + (carry ? 1 : 0);
   std::vector<h::HExt> part(B * K);
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[B]);
   for (size_t b = 0; b < B; b++) left[b].store(K);
