@@ -220,10 +220,16 @@ std::vector<int> choose_pool_cpus(int device) {
     cand.push_back({load, std::vector<int>(kv.second.begin(), kv.second.begin() + want)});
   }
   if (cand.empty()) return {};
-  // least busy first; processes of one node that start together (one per GPU) see the same loads, so each
-  // takes the entry at its local rank (else its device ordinal) and they land on different domains
-  std::stable_sort(cand.begin(), cand.end(), [](const std::pair<double, std::vector<int>>& a,
-                                                const std::pair<double, std::vector<int>>& b) { return a.first < b.first; });
+  // one process alone: the least busy domain first. Several processes of one node started together (torchrun,
+  // LOCAL_WORLD_SIZE > 1) would sample each other's start-up load, so they order the domains by core number
+  // instead, which every process sees alike, and each takes the entry at its local rank: distinct domains
+  const char* lws = getenv("LOCAL_WORLD_SIZE");
+  if (lws && atoi(lws) > 1)
+    std::stable_sort(cand.begin(), cand.end(), [](const std::pair<double, std::vector<int>>& a,
+                                                  const std::pair<double, std::vector<int>>& b) { return a.second[0] < b.second[0]; });
+  else
+    std::stable_sort(cand.begin(), cand.end(), [](const std::pair<double, std::vector<int>>& a,
+                                                  const std::pair<double, std::vector<int>>& b) { return a.first < b.first; });
   const char* lr = getenv("LOCAL_RANK");  // torchrun: one process per GPU, or several sharing one in rehearsals
   const size_t slot = lr ? (size_t)atoi(lr) : (size_t)device;
   return cand[slot % cand.size()].second;
