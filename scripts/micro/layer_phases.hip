@@ -29,12 +29,12 @@ static void run(int nt, int log_len, int fold, unsigned K, Fq* vec, Fq* cin, Fq*
   uint32_t seq = 1000;
   for (int w = 0; w < 3; w++)
     hipLaunchKernelGGL((Q ? k_layer_round_q<BS> : k_layer_round<BS>), dim3(K), dim3(BS), 0, 0, dtr, dcoef, nt, log_len, fold, r, cin, cout, part,
-                       ctr, mb_dev, ++seq, nullptr);
+                       ctr, mb_dev, ++seq, nullptr, 0);
   const int R = 20;
   hipEventRecord(e0, 0);
   for (int i = 0; i < R; i++)
     hipLaunchKernelGGL((Q ? k_layer_round_q<BS> : k_layer_round<BS>), dim3(K), dim3(BS), 0, 0, dtr, dcoef, nt, log_len, fold, r, cin, cout, part,
-                       ctr, mb_dev, ++seq, nullptr);
+                       ctr, mb_dev, ++seq, nullptr, 0);
   hipEventRecord(e1, 0);
   hipEventSynchronize(e1);
   float ms;
@@ -44,14 +44,14 @@ static void run(int nt, int log_len, int fold, unsigned K, Fq* vec, Fq* cin, Fq*
   for (int i = 0; i < R; i++) {
     const uint32_t s = ++seq;
     hipLaunchKernelGGL((Q ? k_layer_round_q<BS> : k_layer_round<BS>), dim3(K), dim3(BS), 0, 0, dtr, dcoef, nt, log_len, fold, r, cin, cout, part,
-                       ctr, mb_dev, s, nullptr);
+                       ctr, mb_dev, s, nullptr, 0);
     while (__atomic_load_n(mb_host, __ATOMIC_ACQUIRE) != s) {
     }
   }
   const double rt = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
   hipDeviceSynchronize();
   hipLaunchKernelGGL((Q ? k_layer_round_q<BS> : k_layer_round<BS>), dim3(K), dim3(BS), 0, 0, dtr, dcoef, nt, log_len, fold, r, cin, cout, part, ctr,
-                     mb_dev, ++seq, probe);
+                     mb_dev, ++seq, probe, 0);
   hipDeviceSynchronize();
   unsigned long long p[8];
   hipMemcpy(p, probe, 64, hipMemcpyDeviceToHost);

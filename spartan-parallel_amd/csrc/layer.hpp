@@ -77,7 +77,8 @@ __global__ void __launch_bounds__(BS) k_layer_round(const Triple* __restrict__ t
                                                     int log_len, int do_fold, Fq r, const Fq* __restrict__ cin,
                                                     Fq* __restrict__ cout, Fq* __restrict__ partials,
                                                     unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
-                                                    uint32_t seq, unsigned long long* probe) {
+                                                    uint32_t seq, unsigned long long* probe, int ends = 0) {
+  (void)ends;  // the one-lane form never posts the layer's entries (the host closes the layer with k_layer_close)
   const int t = threadIdx.x, len = 1 << log_len;
   unsigned long long* pr = probe ? probe + 8 * blockIdx.x : nullptr;  // phase timestamps (scripts/micro)
   if (pr && t == 0) pr[0] = wall_clock64();
