@@ -69,6 +69,7 @@ class Pool {
     for (auto& t : threads_) t.join();
   }
   int size() const { return (int)threads_.size(); }  // workers besides the calling thread
+  uint64_t bursts() const { return bursts_; }         // bursts so far (SPG_TRACE=2 counter)
   // runs f(0) .. f(n-1) on the pool and the calling thread; returns when all are done
   void parallel_for(int n, const std::function<void(int)>& f) {
     if (n <= 1 || threads_.empty()) {
@@ -79,6 +80,7 @@ class Pool {
     uint32_t g;
     bool wake;
     g = ++gen_;
+    bursts_++;
     next_.store(((uint64_t)g << 32) | kClosed);  // tag first: stale snapshots can no longer claim
     fn_.store(&f);
     n_.store(n);
@@ -143,6 +145,7 @@ class Pool {
   std::atomic<const std::function<void(int)>*> fn_{nullptr};
   std::atomic<int> n_{0};
   uint32_t gen_ = 0;  // written by the (serialised) caller only
+  uint64_t bursts_ = 0;
   std::atomic<uint64_t> next_{0};
   std::atomic<int> remaining_{0};
   bool quit_ = false;

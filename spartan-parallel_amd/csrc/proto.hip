@@ -389,24 +389,38 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   FqV v2 = tape.vec("blinds_vec_2", 2 * lg);
   const KeyView& kn = g.gens_n;
   const uint32_t G1 = (uint32_t)g.gens_1.G[0], H = (uint32_t)kn.h;
+  // Small proofs (n <= SPG_BULLET_HOST_MAX, default 32) run every MSM on the host pool against fixed-base
+  // tables of their n generators: a round's two MSMs are then 32 n byte-window additions spread over the pool
+  // (~15 us at n = 32) instead of a device round trip (launch, bucket kernel, bucket finals: ~40 us).
+  static const size_t host_max = getenv("SPG_BULLET_HOST_MAX") ? (size_t)atol(getenv("SPG_BULLET_HOST_MAX")) : 32;
+  const bool on_host = n <= host_max;
   // generator indices G_0..G_{n-1}, G_1, h for B = 2 MSMs, uploaded once for all rounds
   const size_t n2 = n + 2;
-  std::vector<uint32_t> idx2(2 * n2);
-  for (size_t b = 0; b < 2; b++) {
-    for (size_t j = 0; j < n; j++) idx2[b * n2 + j] = (uint32_t)kn.G[j];
-    idx2[b * n2 + n] = G1;
-    idx2[b * n2 + n + 1] = H;
+  uint32_t* d_idx = nullptr;
+  if (!on_host) {
+    std::vector<uint32_t> idx2(2 * n2);
+    for (size_t b = 0; b < 2; b++) {
+      for (size_t j = 0; j < n; j++) idx2[b * n2 + j] = (uint32_t)kn.G[j];
+      idx2[b * n2 + n] = G1;
+      idx2[b * n2 + n + 1] = H;
+    }
+    d_idx = (uint32_t*)ws_get(ctx, 21, idx2.size() * 4 + 64);
+    if (!d_idx) return set_err(ctx, SPG_E_NOMEM, "bullet indices");
+    SPG_HIP(ctx, hipMemcpyAsync(d_idx, idx2.data(), idx2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   }
-  uint32_t* d_idx = (uint32_t*)ws_get(ctx, 21, idx2.size() * 4 + 64);
-  if (!d_idx) return set_err(ctx, SPG_E_NOMEM, "bullet indices");
-  SPG_HIP(ctx, hipMemcpyAsync(d_idx, idx2.data(), idx2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  using HostJob = std::pair<std::vector<size_t>, FqV>;
   // Cx = x.commit(blind_x, gens_n)
   std::vector<Pt> pts;
-  std::vector<Fq> hs(2 * n2, fq_zero());
-  {
+  if (on_host) {
+    HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), x};
+    j.first.push_back(kn.h);
+    j.second.push_back(blind_x);
+    pts = g.host.commit_many({j});
+  } else {
+    std::vector<Fq> hs(n2, fq_zero());
     std::copy(x.begin(), x.end(), hs.begin());
     hs[n + 1] = blind_x;
-    int rc = device_msm_flat(ctx, g, std::vector<Fq>(hs.begin(), hs.begin() + n2), n2, 1, d_idx, &pts);
+    int rc = device_msm_flat(ctx, g, hs, n2, 1, d_idx, &pts);
     if (rc) return rc;
   }
   Pt Cx = pts[0];
@@ -433,7 +447,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   g_msm_laps.lap("bullet_prep");
   static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
   void* d_map = nullptr;
-  Ext* mbk = (dev_rounds && n >= 2 && (n & (n - 1)) == 0)
+  Ext* mbk = (dev_rounds && !on_host && n >= 2 && (n & (n - 1)) == 0)
                  ? (Ext*)mapped_get(ctx, sizeof(Ext) * 2 * (kBulletNB + 1) + 64, &d_map)
                  : nullptr;
   if (mbk) {
@@ -463,8 +477,17 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     hc[hn + n / 2] = fq_mul(cR, r);
     hc[hn + n / 2 + 1] = blind_R;
     g_msm_laps.lap("bullet_scalars");
-    int rc = device_msm_flat(ctx, g, hc, hn, 2, nullptr, &pts, &ic);
-    if (rc) return rc;
+    if (on_host) {
+      std::vector<HostJob> jobs(2);
+      for (size_t b = 0; b < 2; b++) {
+        jobs[b].first.assign(ic.begin() + b * hn, ic.begin() + (b + 1) * hn);
+        jobs[b].second.assign(hc.begin() + b * hn, hc.begin() + (b + 1) * hn);
+      }
+      pts = g.host.commit_many(jobs);
+    } else {
+      int rc = device_msm_flat(ctx, g, hc, hn, 2, nullptr, &pts, &ic);
+      if (rc) return rc;
+    }
     t.point("L", pts[0]);
     t.point("R", pts[1]);
     Fq u = t.challenge("u");
@@ -514,7 +537,13 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   Fq x_hat = aa[0], a_hat = bb[0];
   Fq y_hat = fq_mul(x_hat, a_hat);
   // delta = d * g_hat + r_delta * h with g_hat = sum_j cw[j] G_j
-  {
+  if (on_host) {
+    HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), FqV(n)};
+    for (size_t i = 0; i < n; i++) j.second[i] = fq_mul(d, cw[i]);
+    j.first.push_back(kn.h);
+    j.second.push_back(r_delta);
+    pts = g.host.commit_many({j});
+  } else {
     std::vector<Fq> s(n2, fq_zero());
     par_range(n, [&](size_t lo, size_t hi) {
       for (size_t j = lo; j < hi; j++) s[j] = fq_mul(d, cw[j]);

@@ -1255,6 +1255,9 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
     fprintf(stderr, "[spg] sigma-protocol commitments: %zu calls, %zu commitments, %.0f us on the host\n",
                     g_commit_stats.calls, g_commit_stats.points, g_commit_stats.us);
     g_commit_stats = CommitStats();
+    static uint64_t bursts0 = 0;
+    fprintf(stderr, "[spg] host pool bursts: %llu\n", (unsigned long long)(pool().bursts() - bursts0));
+    bursts0 = pool().bursts();
   }
   if (getenv("SPG_COPY_TRACE") && atoi(getenv("SPG_COPY_TRACE"))) print_copy_counts();
   *proof_len = w.out.size();
