@@ -288,8 +288,11 @@ def main_snark(a):
     sync()
     t0 = time.perf_counter()
     proofs = set()
+    laps = []  # per-prove wall times (a prove returns its bytes, so each step is synchronous)
     for _ in range(a.steps):
+        t1 = time.perf_counter()
         proofs.add(hashlib.sha256(step()).hexdigest())
+        laps.append(time.perf_counter() - t1)
     sync()
     dt = time.perf_counter() - t0
     prof = profile_pass(ctx, step, a.steps)
@@ -342,7 +345,8 @@ def main_snark(a):
             "roofline": roofline_of(prof, a.traffic), "cpu_baseline": cpu, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16], "proof_bytes": None,
             "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
-            "value_incl_witness_upload": round(N * world / t_incl, 1), "verify_ms": round(t_verify * 1e3, 2),
+            "value_incl_witness_upload": round(N * world / t_incl, 1), "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
+            "ms_per_step_min": round(min(laps) * 1e3, 3), "verify_ms": round(t_verify * 1e3, 2),
             "verify_ok": verify_ok, "cpu_verify_ms_1thread": None if cpu_verify_ms is None else round(cpu_verify_ms, 1),
             "encode_s": round(t_encode, 3),
             "host_gen_s": round(t_gen, 3), "kernels": kernels}))

@@ -535,17 +535,6 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     const bool sharded = W > 1 && layer < lgm;
     const size_t hl = sharded ? half / W : half;  // entries of each vector held here
     int rc = 0;
-    if (sharded) {  // local eq share: eq(rand)[W i' + r] = eq(rand_hi)[i'] * eq(rand_lo)[r]
-      const size_t nh = rand.size() - lgW;
-      rc = eq_table(ctx, FqV(rand.begin(), rand.begin() + nh), cbuf[0]);
-      Fq sc = fq_one();
-      for (size_t k = 0; k < lgW; k++)
-        sc = fq_mul(sc, ((ts.r >> (lgW - 1 - k)) & 1) ? rand[nh + k] : fq_sub(fq_one(), rand[nh + k]));
-      if (!rc) hipLaunchKernelGGL(k_scale, dim3(nblk(hl)), dim3(256), 0, s, cbuf[0], hl, sc);
-    } else {
-      rc = eq_table(ctx, rand, cbuf[0]);
-    }
-    if (rc) return rc;
     int cur = 0;  // the buffer holding the shared eq vector C
     const bool with_dotp = layer == 0 && !dotp.empty();
     std::vector<Triple> tr;
@@ -560,14 +549,35 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     FqV coeffs = t.challenges("rand_coeffs_next_layer", claims.size());
     Fq e = fq_zero();
     for (size_t i = 0; i < claims.size(); i++) e = fq_add(e, fq_mul(claims[i], coeffs[i]));
-    {  // descriptors up through page-locked staging; free again here (the previous layer ended with a mailbox wait
-       // after its last launch)
-      uint8_t* st = (uint8_t*)pinned_get(ctx, tr_bytes + coeffs.size() * sizeof(Fq) + 64);
+    // the layer's descriptors and coefficients ride in the eq-table launch's arguments when they fit (no copy
+    // command on the stream), through page-locked staging otherwise
+    KBlob blob;  // 2.3 KB on the stack (contexts on other threads prove concurrently)
+    const size_t blob_bytes = tr_bytes + coeffs.size() * sizeof(Fq);
+    const bool in_args = blob_bytes <= sizeof(blob.w) && !getenv("SPG_LAYER_DESC_COPY");
+    if (in_args) {
+      memset(blob.w, 0, tr_bytes);
+      memcpy(blob.w, tr.data(), tr.size() * sizeof(Triple));
+      memcpy((uint8_t*)blob.w + tr_bytes, coeffs.data(), coeffs.size() * sizeof(Fq));
+      blob.nwords = (int)(blob_bytes / 4);
+    } else {  // free again here (the previous layer ended with a mailbox wait after its last launch)
+      uint8_t* st = (uint8_t*)pinned_get(ctx, blob_bytes + 64);
       if (!st) return set_err(ctx, SPG_E_NOMEM, "layer staging");
       memcpy(st, tr.data(), tr.size() * sizeof(Triple));
       memcpy(st + tr_bytes, coeffs.data(), coeffs.size() * sizeof(Fq));
-      SPG_HIP(ctx, hipMemcpyAsync(ddesc, st, tr_bytes + coeffs.size() * sizeof(Fq), hipMemcpyHostToDevice, s));
+      SPG_HIP(ctx, hipMemcpyAsync(ddesc, st, blob_bytes, hipMemcpyHostToDevice, s));
     }
+    const KBlob* bp = in_args ? &blob : nullptr;
+    if (sharded) {  // local eq share: eq(rand)[W i' + r] = eq(rand_hi)[i'] * eq(rand_lo)[r]
+      const size_t nh = rand.size() - lgW;
+      rc = dev_eq_table(ctx, rand.data(), (int)nh, cbuf[0], bp, ddesc);
+      Fq sc = fq_one();
+      for (size_t k = 0; k < lgW; k++)
+        sc = fq_mul(sc, ((ts.r >> (lgW - 1 - k)) & 1) ? rand[nh + k] : fq_sub(fq_one(), rand[nh + k]));
+      if (!rc) hipLaunchKernelGGL(k_scale, dim3(nblk(hl)), dim3(256), 0, s, cbuf[0], hl, sc);
+    } else {
+      rc = dev_eq_table(ctx, rand.data(), (int)rand.size(), cbuf[0], bp, ddesc);
+    }
+    if (rc) return rc;
     lp.lap("layer_setup");
     LayerProofP lpf;
     FqV r_prod;

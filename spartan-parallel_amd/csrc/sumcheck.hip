@@ -101,8 +101,11 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
 }
 
 // EqPolynomial::evals (src/dense_mlpoly.rs:76-92): out[b] = prod_j (bit_{ell-1-j}(b) ? r_j : 1 - r_j)
-__global__ void k_eq_table(FqArg32 r, Fq* __restrict__ out, size_t n) {
+template <bool BLOB>
+__global__ void k_eq_table(FqArg32 r, Fq* __restrict__ out, size_t n, KBlob blob, uint32_t* __restrict__ blob_dst) {
   size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (BLOB && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < blob.nwords; i += blockDim.x) blob_dst[i] = blob.w[i];
   if (b >= n) return;
   // factors in groups of four: each group's product is independent of the running product, so the
   // dependent chain is ell/4 + 2 multiplications instead of ell
@@ -316,15 +319,28 @@ static int grid_for(uint32_t total) {
 int eval_reduce_finish(spg_ctx* ctx, Fq* out3) { return out3 ? eval_wait(ctx, out3) : 0; }
 int eval_wait(spg_ctx* ctx, Fq* out3) { return mbox_wait(ctx, ctx->mbox_seq, out3, 3); }
 
-int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out) {
+int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out, const KBlob* blob, void* blob_dst) {
   if (ell > 32) return set_err(ctx, SPG_E_ARG, "eq table: too many variables");
+  if (blob && (blob->nwords < 0 || blob->nwords > KBlob::kWords || !blob_dst))
+    return set_err(ctx, SPG_E_ARG, "eq table: bad blob");
   FqArg32 a;
   a.n = ell;
   for (int i = 0; i < ell; i++) a.v[i] = r[i];
   size_t n = (size_t)1 << ell;
   KScope ks(ctx, "eq_table", 32.0 * n);
+  // the first launch carries the blob (an empty one when there is none: the kernel is the <false> form)
+  static KBlob none{};
+  const KBlob& bl = blob ? *blob : none;
+  uint32_t* bd = (uint32_t*)blob_dst;
+  auto launch = [&](const FqArg32& ra, Fq* o, size_t cnt, bool with_blob) {
+    const dim3 g((unsigned)((cnt + 255) / 256));
+    if (with_blob)
+      hipLaunchKernelGGL(k_eq_table<true>, g, dim3(256), 0, ctx->stream, ra, o, cnt, bl, bd);
+    else
+      hipLaunchKernelGGL(k_eq_table<false>, g, dim3(256), 0, ctx->stream, ra, o, cnt, none, nullptr);
+  };
   if (ell <= 12) {
-    hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, a, out, n);
+    launch(a, out, n, blob != nullptr);
   } else {  // eq(r) = eq(r_hi) (x) eq(r_lo): two small tables, then one multiplication per entry
     const int hb = ell / 2, lb = ell - hb;
     Fq* t = (Fq*)ws_get(ctx, 16, (((size_t)1 << hb) + ((size_t)1 << lb)) * sizeof(Fq) + 64);
@@ -336,10 +352,8 @@ int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out) {
     al.n = lb;
     for (int i = 0; i < hb; i++) ah.v[i] = r[i];
     for (int i = 0; i < lb; i++) al.v[i] = r[hb + i];
-    hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((((size_t)1 << hb) + 255) / 256)), dim3(256), 0, ctx->stream, ah,
-                       hi, (size_t)1 << hb);
-    hipLaunchKernelGGL(k_eq_table, dim3((unsigned)((((size_t)1 << lb) + 255) / 256)), dim3(256), 0, ctx->stream, al,
-                       lo, (size_t)1 << lb);
+    launch(ah, hi, (size_t)1 << hb, blob != nullptr);
+    launch(al, lo, (size_t)1 << lb, false);
     hipLaunchKernelGGL(k_eq_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, hi, lo, lb, out, n);
   }
   SPG_HIP(ctx, hipGetLastError());

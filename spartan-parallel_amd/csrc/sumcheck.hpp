@@ -15,8 +15,15 @@ struct FqArg32 {
   int n;
 };
 
-// EqPolynomial::evals(r[0..ell]) into out[2^ell] (device)
-int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out);
+// A small host blob that rides in an eq-table launch's kernel arguments and is written to device memory by it,
+// instead of a separate host-to-device copy on the stream (the SPARK layers' descriptors and coefficients).
+struct KBlob {
+  static constexpr int kWords = 576;  // 2304 B: with FqArg32 the arguments stay well under 4 KB
+  uint32_t w[kWords];
+  int nwords;
+};
+// EqPolynomial::evals(r[0..ell]) into out[2^ell] (device); with blob, also blob->w[0..nwords) -> blob_dst
+int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out, const KBlob* blob = nullptr, void* blob_dst = nullptr);
 // DensePolynomial::bound_poly_var_top on a device vector of length len
 int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r);
 

@@ -73,10 +73,12 @@ def test_spark_repeatable(ctx, oracle):
     assert a == b
 
 
-@pytest.mark.parametrize("env", [{"SPG_WIDE_MIN": "1"}, {"SPG_LAYER_QUAD": "0", "SPG_WIDE_MIN": "1000000000000"}])
+@pytest.mark.parametrize("env", [{"SPG_WIDE_MIN": "1"}, {"SPG_LAYER_QUAD": "0", "SPG_WIDE_MIN": "1000000000000"},
+                                 {"SPG_LAYER_DESC_COPY": "1"}])
 def test_spark_round_kernel_forms(oracle, env):
     """every layer round through the throughput form (k_layer_round_wide, normally only for rounds that fill the
-    chip) or through the one-lane form: same proof bytes as the oracle (a fresh process reads the switches)"""
+    chip) or through the one-lane form, or the layer descriptors uploaded by a copy instead of riding in the
+    eq-table launch: same proof bytes as the oracle (a fresh process reads the switches)"""
     import subprocess
     import sys
 
