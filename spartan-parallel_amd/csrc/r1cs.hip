@@ -685,10 +685,11 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p1_eval");
       Fq r_j = zk.begin(g, t, j, e);
       lp.lap("p1_host");
-      if (mode == MODE_P) { rc = dev_fold_top(ctx, Ap, lenP, r_j); lenP /= 2; }
-      else if (mode == MODE_Q) { rc = dev_fold_top(ctx, Aq, lenQ, r_j); lenQ /= 2; }
-      else { rc = dev_fold_top(ctx, Ax, lenX, r_j); lenX /= 2; }
-      if (!rc) rc = pqx_bound(ctx, *T, TB, TC, r_j, mode);
+      // the round's eq factor is bound in the same launch as Az, Bz, Cz
+      Fq* side = mode == MODE_P ? Ap : (mode == MODE_Q ? Aq : Ax);
+      size_t& side_len = mode == MODE_P ? lenP : (mode == MODE_Q ? lenQ : lenX);
+      rc = pqx_bound(ctx, *T, TB, TC, r_j, mode, side, side_len);
+      side_len /= 2;
       if (!rc && j + 1 == nx + nq && np > 0) rc = to_compact();
       if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
       if (rc) return rc;
@@ -850,8 +851,8 @@ int Prover::run_inner(Laps& lp) {
       Fq r_j = zk.begin(g, t, j, e);
       lp.lap("p2_host");
       if (mode == MODE_P) { rc = dev_fold_top(ctx, eq_p, lenP, r_j); lenP /= 2; }
-      if (!rc && (mode != MODE_P || !single)) rc = pqx_bound(ctx, *TA, nullptr, nullptr, r_j, mode);
-      if (!rc) rc = pqx_bound(ctx, *TZ, nullptr, nullptr, r_j, mode);
+      if (!rc && (mode != MODE_P || !single)) rc = pqx_bound2(ctx, *TA, *TZ, r_j, mode);
+      else if (!rc) rc = pqx_bound(ctx, *TZ, nullptr, nullptr, r_j, mode);
       if (!rc && j + 1 == ny + nw && np > 0) rc = to_compact();
       if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
       if (rc) return rc;

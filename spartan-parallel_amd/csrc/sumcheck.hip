@@ -246,10 +246,9 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
 // ---------------------------------------------------------------- Pqx folds (custom_dense_mlpoly.rs:205-289)
 // domain per instance: np_cur[p] (rows to fold) x nw_cur x n_cols, flattened with dom_off.
 // sc_np = rows, sc_ni = columns written, step_q = nw (sections visited)
-__global__ void k_pqx_fold(PqxArgs a, int mode, uint32_t total, Fq r, Fq* __restrict__ T0, Fq* __restrict__ T1,
-                           Fq* __restrict__ T2) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total) return;
+// entry t of a Pqx table's fold (bound_poly_var_{p,q,w,x}) for up to three tables of one shape
+__device__ __forceinline__ void pqx_fold_at(const PqxArgs& a, int mode, uint32_t t, Fq r, Fq* __restrict__ T0,
+                                            Fq* __restrict__ T1, Fq* __restrict__ T2) {
   int p = find_inst(a, t);
   const PqxInst& d = a.in[p];
   uint32_t loc = t - d.dom_off;
@@ -289,6 +288,25 @@ __global__ void k_pqx_fold(PqxArgs a, int mode, uint32_t total, Fq r, Fq* __rest
       T[base] = fq_add(lo, fq_mul(r, fq_sub(h, lo)));
     }
   }
+}
+
+
+__global__ void k_pqx_fold(PqxArgs a, int mode, uint32_t total, Fq r, Fq* __restrict__ T0, Fq* __restrict__ T1,
+                           Fq* __restrict__ T2, Fq* __restrict__ side, uint32_t side_half) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < side_half) {  // the side vector's bound_poly_var_top (k_fold_top)
+    const Fq lo = side[t];
+    side[t] = fq_add(lo, fq_mul(r, fq_sub(side[t + side_half], lo)));
+  }
+  if (t < total) pqx_fold_at(a, mode, t, r, T0, T1, T2);
+}
+
+// two tables of different shapes bound by the same r in one launch (phase 2: ABC and Z)
+__global__ void k_pqx_fold2(PqxArgs a, uint32_t total_a, Fq* __restrict__ A, PqxArgs b, uint32_t total_b,
+                            Fq* __restrict__ B, int mode, Fq r) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < total_a) pqx_fold_at(a, mode, t, r, A, nullptr, nullptr);
+  else if (t - total_a < total_b) pqx_fold_at(b, mode, t - total_a, r, B, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------- plain cubic (product trees), A*B*C
@@ -446,8 +464,8 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
 }
 
 // DensePolynomialPqx::bound_poly(r, mode) applied to up to three tables of identical shape (T[0] owns shape)
-int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode) {
-  PqxArgs a;
+// host bookkeeping of one Pqx fold (the reference's field updates) and the kernel arguments; dom = entries
+static int pqx_prepare(spg_ctx* ctx, PqxDev& T, int mode, PqxArgs& a, size_t& dom) {
   size_t P = std::min(T.num_instances, T.zlen);
   // host-side size bookkeeping first (mirrors the reference's field updates)
   if (mode == MODE_P) {
@@ -463,7 +481,7 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode) {
   pqx_fill_args(T, a);  // a.ninst / a.nws are the *new* values
   if (P > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
   a.P = (int)P;
-  size_t dom = 0;
+  dom = 0;
   std::vector<size_t> np_after(T.num_proofs), ni_after(T.num_inputs);
   for (size_t p = 0; p < P; p++) {
     PqxInst& d = a.in[p];
@@ -492,15 +510,40 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode) {
     d.step_q = (uint32_t)nw;
     dom += rows * nw * cols;
   }
-  if (dom) {
-    double nt = 1.0 + (d1 ? 1.0 : 0.0) + (d2 ? 1.0 : 0.0);
-    KScope ks(ctx, "sc_fold", 96.0 * nt * dom);  // read lo+hi, write lo, per table
-    hipLaunchKernelGGL(k_pqx_fold, dim3((unsigned)((dom + 255) / 256)), dim3(256), 0, ctx->stream, a, mode,
-                       (uint32_t)dom, r, T.d, d1, d2);
-    SPG_HIP(ctx, hipGetLastError());
-  }
   T.num_proofs = np_after;
   T.num_inputs = ni_after;
+  return 0;
+}
+
+int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq* side, size_t side_len) {
+  PqxArgs a;
+  size_t dom = 0;
+  int rc = pqx_prepare(ctx, T, mode, a, dom);
+  if (rc) return rc;
+  const size_t side_half = side ? side_len / 2 : 0;
+  if (dom || side_half) {
+    double nt = 1.0 + (d1 ? 1.0 : 0.0) + (d2 ? 1.0 : 0.0);
+    KScope ks(ctx, "sc_fold", 96.0 * (nt * dom + side_half));  // read lo+hi, write lo, per table
+    const size_t n = std::max(dom, side_half);
+    hipLaunchKernelGGL(k_pqx_fold, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, a, mode,
+                       (uint32_t)dom, r, T.d, d1, d2, side, (uint32_t)side_half);
+    SPG_HIP(ctx, hipGetLastError());
+  }
+  return 0;
+}
+
+int pqx_bound2(spg_ctx* ctx, PqxDev& TA, PqxDev& TB, const Fq& r, int mode) {
+  PqxArgs a, b;
+  size_t da = 0, db = 0;
+  int rc = pqx_prepare(ctx, TA, mode, a, da);
+  if (!rc) rc = pqx_prepare(ctx, TB, mode, b, db);
+  if (rc) return rc;
+  if (da + db) {
+    KScope ks(ctx, "sc_fold", 96.0 * (double)(da + db));
+    hipLaunchKernelGGL(k_pqx_fold2, dim3((unsigned)((da + db + 255) / 256)), dim3(256), 0, ctx->stream, a,
+                       (uint32_t)da, TA.d, b, (uint32_t)db, TB.d, mode, r);
+    SPG_HIP(ctx, hipGetLastError());
+  }
   return 0;
 }
 

@@ -36,7 +36,11 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
                 const Fq* eq, Fq* partials, Fq* out3);
 // DensePolynomialPqx::bound_poly on T (and d1, d2 sharing T's shape, may be null)
-int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode);
+// side (optional): a dense vector of side_len entries bound by the same r in the same launch
+// (DensePolynomial::bound_poly_var_top, as dev_fold_top) - the round's eq factor in phase 1
+int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq* side = nullptr, size_t side_len = 0);
+// two single-table folds of different shapes with the same r in one launch
+int pqx_bound2(spg_ctx* ctx, PqxDev& TA, PqxDev& TB, const Fq& r, int mode);
 // SumcheckInstanceProof::prove_cubic round on dense A, B, C of length 2*len_half
 int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials,
                Fq* out3);
