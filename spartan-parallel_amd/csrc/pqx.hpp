@@ -12,7 +12,8 @@
 
 namespace spg {
 
-static const int kMaxP = 32;  // instances per table per launch (keeps two PqxArgs under the 4 KiB kernarg budget)
+static const int kMaxP = 32;  // instances whose descriptors ride in the kernel arguments (two PqxArgs stay under
+                              // the 4 KiB kernarg budget); more go to device memory (PqxArgs::ext)
 
 // per-instance view passed by value to kernels
 struct PqxInst {
@@ -29,8 +30,11 @@ struct PqxArgs {
   int zlen;       // Z.len()
   int ninst;      // Pqx.num_instances (current, power of two)
   int nws;        // Pqx.num_witness_secs (current, power of two)
+  const PqxInst* ext;  // more than kMaxP instances: every descriptor in device memory (else null, `in` holds them)
   PqxInst in[kMaxP];
 };
+// descriptor of instance p (kernel argument or device copy)
+__host__ __device__ inline const PqxInst& pinst(const PqxArgs& a, int p) { return a.ext ? a.ext[p] : a.in[p]; }
 
 __host__ __device__ inline size_t pqx_off(const PqxInst& d) { return ((size_t)d.off_hi << 32) | d.off_lo; }
 

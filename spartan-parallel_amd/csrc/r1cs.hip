@@ -1364,7 +1364,6 @@ static int check_prove_args(spg_ctx* ctx, const spg_r1cs_inst* inst, size_t num_
     return set_err(ctx, SPG_E_ARG, "bad sizes");
   if (inst->num_instances != 1 && inst->num_instances != num_instances)
     return set_err(ctx, SPG_E_ARG, "instance count mismatch");
-  if (num_instances > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances for one launch");
   if (wit->nws * max_num_inputs > inst->num_vars) return set_err(ctx, SPG_E_ARG, "witness wider than num_vars");
   for (size_t p = 0; p < num_instances; p++) {
     if (!is_pow2(num_proofs[p]) || num_proofs[p] > max_num_proofs || !is_pow2(num_inputs[p]) ||

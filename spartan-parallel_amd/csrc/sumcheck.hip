@@ -20,7 +20,7 @@ namespace spg {
 __device__ __forceinline__ int find_inst(const PqxArgs& a, uint32_t t) {
   int p = 0;
   for (int k = 1; k < a.P; k++)
-    if (a.in[k].dom_off <= t) p = k;
+    if (pinst(a, k).dom_off <= t) p = k;
   return p;
 }
 
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(a, t);
-    const PqxInst& d = a.in[p];
+    const PqxInst& d = pinst(a, p);
     uint32_t loc = t - d.dom_off;
     uint32_t q = loc / d.sc_ni, x = loc % d.sc_ni;
     Fq apq = fq_mul(Ap[p], Aq[q * d.step_q]);
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
     } else {
       int ph = p + a.ninst / 2;
       zero_hi = ph >= a.zlen;
-      hi = zero_hi ? 0 : pqx_off(a.in[ph]) + (size_t)q * a.in[ph].anw * a.in[ph].ani + x;
+      hi = zero_hi ? 0 : pqx_off(pinst(a, ph)) + (size_t)q * pinst(a, ph).anw * pinst(a, ph).ani + x;
     }
     if (zero_hi) {
       b_hi = fq_zero(); c_hi = fq_zero(); d_hi = fq_zero();
@@ -202,19 +202,19 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
 // domain: p < Pd, w < W, y < sc_ni[p] ; B = ABC table (instance pi = single ? 0 : p), C = Z table
 __device__ __forceinline__ Fq pqx_get(const PqxArgs& a, const Fq* T, int p, uint32_t w, uint32_t y) {
   if (p >= a.zlen) return fq_zero();
-  const PqxInst& d = a.in[p];
+  const PqxInst& d = pinst(a, p);
   if (w >= d.anw || y >= d.ani) return fq_zero();
   return T[pqx_off(d) + (size_t)w * d.ani + y];
 }
 __device__ __forceinline__ Fq pqx_get_high(const PqxArgs& a, const Fq* T, int p, uint32_t w, uint32_t y, int mode) {
-  const PqxInst& d = a.in[p];
+  const PqxInst& d = pinst(a, p);
   if (mode == MODE_X) return d.ni == 1 ? fq_zero() : T[pqx_off(d) + (size_t)w * d.ani + y + d.ni / 2];
   if (mode == MODE_W) {
     uint32_t wh = w + a.nws / 2;
     return wh < d.anw ? T[pqx_off(d) + (size_t)wh * d.ani + y] : fq_zero();
   }
   int ph = p + a.ninst / 2;
-  return ph < a.zlen ? T[pqx_off(a.in[ph]) + (size_t)w * a.in[ph].ani + y] : fq_zero();
+  return ph < a.zlen ? T[pqx_off(pinst(a, ph)) + (size_t)w * pinst(a, ph).ani + y] : fq_zero();
 }
 
 __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int mode, uint32_t total, int W,
@@ -225,8 +225,8 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(zz, t);
-    uint32_t loc = t - zz.in[p].dom_off;
-    uint32_t ny = zz.in[p].sc_ni;
+    uint32_t loc = t - pinst(zz, p).dom_off;
+    uint32_t ny = pinst(zz, p).sc_ni;
     uint32_t w = loc / ny, y = loc % ny;
     (void)W;
     int pi = single ? 0 : p;
@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
 __device__ __forceinline__ void pqx_fold_at(const PqxArgs& a, int mode, uint32_t t, Fq r, Fq* __restrict__ T0,
                                             Fq* __restrict__ T1, Fq* __restrict__ T2) {
   int p = find_inst(a, t);
-  const PqxInst& d = a.in[p];
+  const PqxInst& d = pinst(a, p);
   uint32_t loc = t - d.dom_off;
   uint32_t ncol = d.sc_ni, nw = d.step_q;
   uint32_t x = loc % ncol;
@@ -272,7 +272,7 @@ __device__ __forceinline__ void pqx_fold_at(const PqxArgs& a, int mode, uint32_t
   } else {
     int ph = p + a.ninst;  // a.ninst already halved by the host
     zero_hi = ph >= a.zlen;
-    hi = zero_hi ? 0 : pqx_off(a.in[ph]) + ((size_t)q * a.in[ph].anw + w) * a.in[ph].ani + x;
+    hi = zero_hi ? 0 : pqx_off(pinst(a, ph)) + ((size_t)q * pinst(a, ph).anw + w) * pinst(a, ph).ani + x;
   }
   Fq* Ts[3] = {T0, T1, T2};
   Fq omr = fq_sub(fq_one(), r);
@@ -387,12 +387,15 @@ int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r) {
   return 0;
 }
 
-void pqx_fill_args(const PqxDev& T, PqxArgs& a) {
+// every instance's descriptor (host vector v) and the table-wide fields of a
+static void pqx_fill_args(const PqxDev& T, PqxArgs& a, std::vector<PqxInst>& v) {
   a.zlen = (int)T.zlen;
   a.ninst = (int)T.num_instances;
   a.nws = (int)T.num_witness_secs;
-  for (size_t p = 0; p < T.zlen && p < (size_t)kMaxP; p++) {
-    PqxInst& d = a.in[p];
+  a.ext = nullptr;
+  v.assign(T.zlen, PqxInst{});
+  for (size_t p = 0; p < T.zlen; p++) {
+    PqxInst& d = v[p];
     d.off_lo = (uint32_t)T.off[p];
     d.off_hi = (uint32_t)(T.off[p] >> 32);
     d.anp = (uint32_t)T.anp[p];
@@ -404,18 +407,32 @@ void pqx_fill_args(const PqxDev& T, PqxArgs& a) {
     d.sc_np = d.sc_ni = d.step_q = d.step_x = 1;
   }
 }
+// the descriptors into the kernel arguments, or - more than kMaxP instances - into device memory (workspace slot;
+// stream-ordered, so the next launch's copy into the same slot lands after this launch has read it)
+enum : size_t { kWsPqxA = 110, kWsPqxB = 111 };
+static int pqx_pack(spg_ctx* ctx, const std::vector<PqxInst>& v, PqxArgs& a, size_t slot) {
+  a.ext = nullptr;
+  for (size_t p = 0; p < v.size() && p < (size_t)kMaxP; p++) a.in[p] = v[p];
+  if (v.size() <= (size_t)kMaxP) return 0;
+  PqxInst* d = (PqxInst*)ws_get(ctx, slot, v.size() * sizeof(PqxInst));
+  if (!d) return set_err(ctx, SPG_E_NOMEM, "instance descriptors");
+  SPG_HIP(ctx, hipMemcpyAsync(d, v.data(), v.size() * sizeof(PqxInst), hipMemcpyHostToDevice, ctx->stream));
+  a.ext = d;
+  return 0;
+}
 
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
                 const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* out3) {
   PqxArgs a;
-  pqx_fill_args(T, a);
+  std::vector<PqxInst> v;
+  pqx_fill_args(T, a, v);
   size_t P = std::min(instance_len, sc_np.size());
-  if (P > (size_t)kMaxP || T.zlen > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
+  if (P > T.zlen) return set_err(ctx, SPG_E_ARG, "phase-1 domain wider than the table");
   a.P = (int)P;
   size_t dom = 0;
   for (size_t p = 0; p < P; p++) {
-    PqxInst& d = a.in[p];
+    PqxInst& d = v[p];
     d.dom_off = (uint32_t)dom;
     d.sc_np = (uint32_t)sc_np[p];
     d.sc_ni = (uint32_t)sc_nc[p];
@@ -424,6 +441,7 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
     dom += sc_np[p] * sc_nc[p];
   }
   if (dom >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "phase-1 domain too large");
+  if (int rc = pqx_pack(ctx, v, a, kWsPqxA)) return rc;
   int nb = grid_for((uint32_t)dom);
   {
     // B, C, D lo+hi per domain point, plus the three eq factor tables once
@@ -440,19 +458,22 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
                 const Fq* eq, Fq* partials, Fq* out3) {
   PqxArgs ab, zz;
-  pqx_fill_args(AB, ab);
-  pqx_fill_args(Z, zz);
+  std::vector<PqxInst> vab, vz;
+  pqx_fill_args(AB, ab, vab);
+  pqx_fill_args(Z, zz, vz);
   size_t P = std::min(instance_len, sc_ni.size());
-  if (P > (size_t)kMaxP || Z.zlen > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
+  if (P > Z.zlen) return set_err(ctx, SPG_E_ARG, "phase-2 domain wider than the table");
   ab.P = (int)AB.zlen;
   zz.P = (int)P;
   size_t W = std::min(witness_secs_len, nws_actual);
   size_t dom = 0;
   for (size_t p = 0; p < P; p++) {
-    zz.in[p].dom_off = (uint32_t)dom;
-    zz.in[p].sc_ni = (uint32_t)sc_ni[p];
+    vz[p].dom_off = (uint32_t)dom;
+    vz[p].sc_ni = (uint32_t)sc_ni[p];
     dom += W * sc_ni[p];
   }
+  if (int rc = pqx_pack(ctx, vab, ab, kWsPqxA)) return rc;
+  if (int rc = pqx_pack(ctx, vz, zz, kWsPqxB)) return rc;
   int nb = grid_for((uint32_t)dom);
   {
     KScope ks(ctx, "sc_phase2_eval", 128.0 * dom);  // ABC and Z, lo+hi per domain point
@@ -465,7 +486,7 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
 
 // DensePolynomialPqx::bound_poly(r, mode) applied to up to three tables of identical shape (T[0] owns shape)
 // host bookkeeping of one Pqx fold (the reference's field updates) and the kernel arguments; dom = entries
-static int pqx_prepare(spg_ctx* ctx, PqxDev& T, int mode, PqxArgs& a, size_t& dom) {
+static int pqx_prepare(spg_ctx* ctx, PqxDev& T, int mode, PqxArgs& a, size_t& dom, size_t slot) {
   size_t P = std::min(T.num_instances, T.zlen);
   // host-side size bookkeeping first (mirrors the reference's field updates)
   if (mode == MODE_P) {
@@ -478,13 +499,13 @@ static int pqx_prepare(spg_ctx* ctx, PqxDev& T, int mode, PqxArgs& a, size_t& do
   } else {
     T.max_num_inputs /= 2;
   }
-  pqx_fill_args(T, a);  // a.ninst / a.nws are the *new* values
-  if (P > (size_t)kMaxP) return set_err(ctx, SPG_E_ARG, "too many instances");
+  std::vector<PqxInst> v;
+  pqx_fill_args(T, a, v);  // a.ninst / a.nws are the *new* values
   a.P = (int)P;
   dom = 0;
   std::vector<size_t> np_after(T.num_proofs), ni_after(T.num_inputs);
   for (size_t p = 0; p < P; p++) {
-    PqxInst& d = a.in[p];
+    PqxInst& d = v[p];
     size_t rows, nw, cols;
     if (mode == MODE_P) {
       rows = 1;
@@ -512,13 +533,13 @@ static int pqx_prepare(spg_ctx* ctx, PqxDev& T, int mode, PqxArgs& a, size_t& do
   }
   T.num_proofs = np_after;
   T.num_inputs = ni_after;
-  return 0;
+  return pqx_pack(ctx, v, a, slot);
 }
 
 int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq* side, size_t side_len) {
   PqxArgs a;
   size_t dom = 0;
-  int rc = pqx_prepare(ctx, T, mode, a, dom);
+  int rc = pqx_prepare(ctx, T, mode, a, dom, kWsPqxA);
   if (rc) return rc;
   const size_t side_half = side ? side_len / 2 : 0;
   if (dom || side_half) {
@@ -535,8 +556,8 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq
 int pqx_bound2(spg_ctx* ctx, PqxDev& TA, PqxDev& TB, const Fq& r, int mode) {
   PqxArgs a, b;
   size_t da = 0, db = 0;
-  int rc = pqx_prepare(ctx, TA, mode, a, da);
-  if (!rc) rc = pqx_prepare(ctx, TB, mode, b, db);
+  int rc = pqx_prepare(ctx, TA, mode, a, da, kWsPqxA);
+  if (!rc) rc = pqx_prepare(ctx, TB, mode, b, db, kWsPqxB);
   if (rc) return rc;
   if (da + db) {
     KScope ks(ctx, "sc_fold", 96.0 * (double)(da + db));

@@ -14,6 +14,9 @@ CASES = {
 GPU_CASES = {
     "p2_x1024_q64": ([1024, 1024], [64, 64], 1, False),
     "p8_x256_q32_shared": ([256] * 8, [32] * 8, 1, True),
+    # more instances than fit in one launch's kernel arguments (kMaxP = 32): descriptors in device memory
+    "p40_ragged_2secs": ([16, 8, 32, 8] * 10, [4, 2, 1, 8] * 10, 2, False),
+    "p36_shared": ([16] * 36, [2] * 36, 1, True),
 }
 # SPARK (SparseMatPolyEvalProof) cases: the batch is [A_0, B_0, C_0, A_1, ...] of the workload's instance
 SPARK_CASES = {

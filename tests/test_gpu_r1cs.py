@@ -65,7 +65,7 @@ def test_r1cs_proof_is_repeatable(ctx, r1cs_gens):
     assert a == b and a != c
 
 
-@pytest.mark.parametrize("case", ["p3_ragged_3secs", "shared_p2", "p2_x1024_q64"])
+@pytest.mark.parametrize("case", ["p3_ragged_3secs", "shared_p2", "p2_x1024_q64", "p40_ragged_2secs"])
 def test_multi_evaluate_matches_oracle(ctx, oracle, case):
     """R1CSInstance::multi_evaluate on the GPU (k_sparse_eval) vs the oracle at random (rx, ry)."""
     import spg
