@@ -48,6 +48,7 @@ SNARK_CASES = {
                               init_vir=5, niu=5, schedule=[2, 0, 2, 2, 0, 2]),
 }
 GPU_SNARK_CASES = {
+    "b34_x32_q2": dict(num_blocks=34, log_cons=5, log_proofs=1, num_vars=32),  # > 32 block types (kMaxP)
     "b2_x1024_q8": dict(num_blocks=2, log_cons=10, log_proofs=3, num_vars=1024),
     "b2_x256_q64": dict(num_blocks=2, log_cons=8, log_proofs=6, num_vars=256),
     "mem_both_b2_x256_q32": dict(num_blocks=2, log_cons=8, log_proofs=5, num_vars=256, phy_ops=3, vir_ops=2,
