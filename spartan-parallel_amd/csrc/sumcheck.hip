@@ -129,6 +129,59 @@ __global__ void k_eq_table(FqArg32 r, Fq* __restrict__ out, size_t n, KBlob blob
   out[b] = acc;
 }
 
+// product of the eq factors of bits k0 .. k0+nb-1 of an index whose bits there are v (bit k <-> r[ell-1-k]),
+// in groups of four (dependent chain nb/4 + 2 multiplications)
+__device__ __forceinline__ Fq eq_bits(const Fq* rv, int ell, int k0, int nb, uint32_t v) {
+  auto factor = [&](int i) {
+    const Fq& rj = rv[ell - 1 - (k0 + i)];
+    return ((v >> i) & 1) ? rj : fq_sub(fq_one(), rj);
+  };
+  Fq acc = fq_one();
+  bool first = true;
+  int i = 0;
+  for (; i + 4 <= nb; i += 4) {
+    const Fq p = fq_mul(fq_mul(factor(i), factor(i + 1)), fq_mul(factor(i + 2), factor(i + 3)));
+    acc = first ? p : fq_mul(acc, p);
+    first = false;
+  }
+  for (; i < nb; i++) {
+    const Fq f = factor(i);
+    acc = first ? f : fq_mul(acc, f);
+    first = false;
+  }
+  return acc;
+}
+
+// Same table from LDS sub-tables: a block owns 2^lb consecutive entries (lb = min(ell, 8)); the low bits
+// split into two groups of <= 4 whose 16-entry factor tables and the block's high-bit product are built
+// by lanes of three different waves at once, then every entry is two multiplications. A lane's chain is
+// ~5 products instead of ell - 1 (+ ell/4 grouping): the launch is latency-bound at these sizes.
+template <bool BLOB>
+__global__ void __launch_bounds__(256) k_eq_table_lds(FqArg32 r, Fq* __restrict__ out, size_t n, KBlob blob,
+                                                      uint32_t* __restrict__ blob_dst) {
+  __shared__ Fq s_lo[16], s_mid[16], s_hi;
+  __shared__ Fq s_r[32];
+  const int t = threadIdx.x;
+  if (BLOB && blockIdx.x == 0)
+    for (int i = t; i < blob.nwords; i += blockDim.x) blob_dst[i] = blob.w[i];
+  const int ell = r.n;
+  // the challenges reach LDS in one parallel round trip (one word per lane) instead of a chain of
+  // scalar loads from the argument segment inside every lane's product loop
+  if (t < ell * 8) reinterpret_cast<uint32_t*>(s_r)[t] = reinterpret_cast<const uint32_t*>(r.v)[t];
+  __syncthreads();
+  const int lb = ell < 8 ? ell : 8;
+  const int nlo = lb >> 1, nmid = lb - nlo, nhi = ell - lb;
+  if (t < (1 << nlo)) s_lo[t] = eq_bits(s_r, ell, 0, nlo, (uint32_t)t);
+  else if (t >= 64 && t < 64 + (1 << nmid)) s_mid[t - 64] = eq_bits(s_r, ell, nlo, nmid, (uint32_t)(t - 64));
+  else if (t == 128) s_hi = eq_bits(s_r, ell, lb, nhi, (uint32_t)blockIdx.x);
+  __syncthreads();
+  const size_t b = (size_t)blockIdx.x * blockDim.x + t;
+  if (b >= n) return;
+  Fq v = fq_mul(s_mid[t >> nlo], s_lo[t & ((1 << nlo) - 1)]);
+  if (nhi) v = fq_mul(v, s_hi);
+  out[b] = v;
+}
+
 // factored form for large tables: out[b] = hi[b >> lo_bits] * lo[b & (2^lo_bits - 1)]
 __global__ void k_eq_combine(const Fq* __restrict__ hi, const Fq* __restrict__ lo, int lo_bits, Fq* __restrict__ out,
                              size_t n) {
@@ -350,14 +403,21 @@ int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out, const KBlob* blob,
   static KBlob none{};
   const KBlob& bl = blob ? *blob : none;
   uint32_t* bd = (uint32_t*)blob_dst;
+  // SPG_EQ_LDS=0 restores the one-lane-per-entry kernel (A/B switch)
+  static const bool lds_on = !getenv("SPG_EQ_LDS") || atoi(getenv("SPG_EQ_LDS")) != 0;
   auto launch = [&](const FqArg32& ra, Fq* o, size_t cnt, bool with_blob) {
     const dim3 g((unsigned)((cnt + 255) / 256));
-    if (with_blob)
+    if (lds_on) {
+      if (with_blob)
+        hipLaunchKernelGGL(k_eq_table_lds<true>, g, dim3(256), 0, ctx->stream, ra, o, cnt, bl, bd);
+      else
+        hipLaunchKernelGGL(k_eq_table_lds<false>, g, dim3(256), 0, ctx->stream, ra, o, cnt, none, nullptr);
+    } else if (with_blob)
       hipLaunchKernelGGL(k_eq_table<true>, g, dim3(256), 0, ctx->stream, ra, o, cnt, bl, bd);
     else
       hipLaunchKernelGGL(k_eq_table<false>, g, dim3(256), 0, ctx->stream, ra, o, cnt, none, nullptr);
   };
-  if (ell <= 12) {
+  if (ell <= (lds_on ? 16 : 12)) {
     launch(a, out, n, blob != nullptr);
   } else {  // eq(r) = eq(r_hi) (x) eq(r_lo): two small tables, then one multiplication per entry
     const int hb = ell / 2, lb = ell - hb;
