@@ -69,6 +69,10 @@ int spg_buf_upload(spg_ctx* ctx, const uint64_t* scalars_mont, size_t n, spg_buf
 int spg_buf_download(spg_ctx* ctx, const spg_buf* b, uint64_t* scalars_mont);
 size_t spg_buf_len(const spg_buf* b);
 int spg_buf_free(spg_ctx* ctx, spg_buf* b);
+/* EqPolynomial::new(r).evals() (src/dense_mlpoly.rs:76-92): the 2^ell table prod_j (b_j ? r_j : 1 - r_j),
+ * r[0] the most significant bit of the index, computed on the device into a new spg_buf (ell <= 30). The
+ * prover's sumchecks and SPARK build the same tables internally; this entry point exposes them. */
+int spg_eq_evals(spg_ctx* ctx, const uint64_t* r_mont, size_t ell, spg_buf** out);
 
 /* ---- generators ------------------------------------------------------------------------------
  * MultiCommitGens::new(n, label) (src/commitments.rs:15-33): n+1 points from SHAKE256(label ||

@@ -641,3 +641,26 @@ int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_h
 }
 
 }  // namespace spg
+
+// EqPolynomial::evals (src/dense_mlpoly.rs:76-92) into a new device vector of 2^ell scalars
+extern "C" int spg_eq_evals(spg_ctx* ctx, const uint64_t* r_mont, size_t ell, spg_buf** out) {
+  if (!ctx || !out || (!r_mont && ell)) return SPG_E_ARG;
+  if (ell > 30) return spg::set_err(ctx, SPG_E_ARG, "spg_eq_evals: at most 30 variables");
+  spg_buf* b = new spg_buf();
+  b->n = (size_t)1 << ell;
+  if (hipMalloc(&b->d, b->n * sizeof(spg::Fq)) != hipSuccess) {
+    delete b;
+    return spg::set_err(ctx, SPG_E_NOMEM, "spg_eq_evals");
+  }
+  std::vector<spg::Fq> r(ell);
+  if (ell) memcpy(r.data(), r_mont, ell * sizeof(spg::Fq));
+  int rc = spg::dev_eq_table(ctx, r.data(), (int)ell, b->d);
+  if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : spg::set_err(ctx, SPG_E_HIP, "spg_eq_evals");
+  if (rc) {
+    hipFree(b->d);
+    delete b;
+    return rc;
+  }
+  *out = b;
+  return SPG_OK;
+}

@@ -157,6 +157,18 @@ class Buf:
         self.ctx.check(lib().spg_buf_download(self.ctx.handle, self._h, _p(out)), "spg_buf_download")
         return out
 
+    @classmethod
+    def eq_evals(cls, ctx, r):
+        """EqPolynomial::new(r).evals() (src/dense_mlpoly.rs:76-92) built on the device (spg_eq_evals)."""
+        a = _scalars(r) if len(r) else np.zeros((0, 4), dtype=np.uint64)
+        b = cls.__new__(cls)
+        b.ctx = ctx
+        b.n = 1 << a.shape[0]
+        b._h = ctypes.c_void_p()
+        ctx.check(lib().spg_eq_evals(ctx.handle, _p(a), ctypes.c_size_t(a.shape[0]), ctypes.byref(b._h)),
+                  "spg_eq_evals")
+        return b
+
     def free(self):
         if self._h:
             lib().spg_buf_free(self.ctx.handle, self._h)
