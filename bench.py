@@ -229,9 +229,14 @@ def roofline_of(prof, traffic_file):
         tr = json.load(open(traffic_file))
         if dom in tr.get("kernels", {}):
             traffic = tr["kernels"][dom]["hbm_bytes_per_launch"]
-    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes_per_launch": nbytes / launches, "avg_launch_us": us / launches, "launches": launches}
+    per = nbytes / launches
+    out = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "algorithmic_bytes_per_launch": per, "avg_launch_us": us / launches, "launches": launches,
+           # a launch that moves < 64 MB cannot approach the HBM peak behind a ~4 us small-launch floor: its
+           # regime is the round-trip latency (transcript-sequential rounds over KB-sized vectors), DESIGN.md 4
+           "regime": "bandwidth" if per >= (64 << 20) else "latency"}
+    return out
 
 
 def main_snark(a):

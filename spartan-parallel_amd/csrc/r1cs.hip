@@ -896,10 +896,18 @@ int Prover::run_inner(Laps& lp) {
       polys.push_back(std::move(pr));
     }
   }
-  // LZ = bound(L) of each owned polynomial on this rank's device, then shared with every rank
+  // LZ = bound(L) of each owned polynomial on this rank's device, then shared with every rank. Every
+  // polynomial's eq(rl), partial column sums and LZ are queued back to back into disjoint workspace ranges and
+  // the LZ of all of them come back in one download (one host wait instead of one per polynomial).
   std::vector<Fq> lz_mine(lz_total, fq_zero());
   {
-    size_t o = 0;
+    struct BoundJob {
+      FqV rl;
+      size_t Ls, Rs, S, chunk, offL, offP, o;
+    };
+    std::vector<BoundJob> jobs;
+    size_t o = 0, totL = 0, totP = 0;
+    bool all_mine = true;
     for (auto& pr : polys) {
       size_t lnp = lg2(pr.np), lni = lg2(pr.ni);
       FqV r(rq.begin() + (nq - lnp), rq.end());
@@ -914,27 +922,42 @@ int Prover::run_inner(Laps& lp) {
       size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
       pr.R = eq_evals_host(rr);
       if (pr.mine) {
-        Fq* dL = (Fq*)ws_get(ctx, WS_L, Ls * sizeof(Fq) + 64);
-        uint32_t nbx = (uint32_t)((Rs + 255) / 256);
-        uint32_t S = (uint32_t)std::min<size_t>(Ls, 32);  // 32 partial rows: short column sums
-        uint32_t chunk = (uint32_t)((Ls + S - 1) / S);
-        S = (uint32_t)((Ls + chunk - 1) / chunk);
-        Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, (size_t)S * Rs * sizeof(Fq) + 64);
-        Fq* dout = (Fq*)ws_get(ctx, WS_BOUT, Rs * sizeof(Fq) + 64);
-        if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "bound");
-        rc = eq_table(ctx, rl, dL);
-        if (rc) return rc;
-        {
-          KScope ks(ctx, "poly_bound", 32.0 * Ls * Rs + 32.0 * Ls + 64.0 * S * Rs);
-          hipLaunchKernelGGL(k_bound_part, dim3(nbx, S), dim3(256), 0, s, wit.d_w + wit.off[pr.w][pr.p], dL,
-                             (uint32_t)Ls, (uint32_t)Rs, chunk, dpart);
-          hipLaunchKernelGGL(k_sum_cols, dim3(nbx), dim3(256), 0, s, dpart, S, (uint32_t)Rs, dout);
-        }
-        SPG_HIP(ctx, hipGetLastError());
-        rc = d2h_fq(ctx, dout, lz_mine.data() + o, Rs);
-        if (rc) return rc;
+        size_t S = std::min<size_t>(Ls, 32);  // 32 partial rows: short column sums
+        const size_t chunk = (Ls + S - 1) / S;
+        S = (Ls + chunk - 1) / chunk;
+        jobs.push_back({std::move(rl), Ls, Rs, S, chunk, totL, totP, o});
+        totL += Ls;
+        totP += S * Rs;
+      } else {
+        all_mine = false;
       }
       o += Rs;
+    }
+    if (!jobs.empty()) {
+      Fq* dL = (Fq*)ws_get(ctx, WS_L, totL * sizeof(Fq) + 64);
+      Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, totP * sizeof(Fq) + 64);
+      Fq* dout = (Fq*)ws_get(ctx, WS_BOUT, lz_total * sizeof(Fq) + 64);
+      if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "bound");
+      if (!all_mine) SPG_HIP(ctx, hipMemsetAsync(dout, 0, lz_total * sizeof(Fq), s));  // other ranks' ranges
+      for (size_t k = 0; k < jobs.size(); k++) {
+        const BoundJob& j = jobs[k];
+        rc = eq_table(ctx, j.rl, dL + j.offL);
+        if (rc) return rc;
+      }
+      size_t k = 0;
+      for (auto& pr : polys) {
+        if (!pr.mine) continue;
+        const BoundJob& j = jobs[k++];
+        const uint32_t nbx = (uint32_t)((j.Rs + 255) / 256);
+        KScope ks(ctx, "poly_bound", 32.0 * j.Ls * j.Rs + 32.0 * j.Ls + 64.0 * j.S * j.Rs);
+        hipLaunchKernelGGL(k_bound_part, dim3(nbx, (uint32_t)j.S), dim3(256), 0, s, wit.d_w + wit.off[pr.w][pr.p],
+                           dL + j.offL, (uint32_t)j.Ls, (uint32_t)j.Rs, (uint32_t)j.chunk, dpart + j.offP);
+        hipLaunchKernelGGL(k_sum_cols, dim3(nbx), dim3(256), 0, s, dpart + j.offP, (uint32_t)j.S, (uint32_t)j.Rs,
+                           dout + j.o);
+      }
+      SPG_HIP(ctx, hipGetLastError());
+      rc = d2h_fq(ctx, dout, lz_mine.data(), lz_total);
+      if (rc) return rc;
     }
   }
   {
