@@ -424,27 +424,61 @@ int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, co
   return dotproduct_log_prove(ctx, g, t, tape, LZ, fq_zero(), R, Zr, fq_zero(), out, &cy);
 }
 
-// out[s] = sum_i base[s * seglen + i] * eq[i], i < n, s < nseg; sharded: rank r sums its balanced share of i
-static int seg_dots(spg_ctx* ctx, const Fq* base, size_t seglen, size_t nseg, const Fq* d_eq, size_t n, FqV* out,
-                    const Shard& sh = Shard()) {
-  const size_t i0 = shard_begin(n, sh.n, sh.rank), i1 = shard_begin(n, sh.n, sh.rank + 1), nm = i1 - i0;
-  out->assign(nseg, fq_zero());
-  int rc = 0;
-  if (nm) {
-    unsigned nb = (unsigned)std::min<size_t>(nblk(nm), std::max<size_t>(1, 2048 / nseg));
-    Fq* part = (Fq*)ws_get(ctx, kWsSegPart, nseg * nb * sizeof(Fq) + 64);
-    Fq* dres = (Fq*)ws_get(ctx, kWsSeg, nseg * sizeof(Fq) + 64);
-    if (!part || !dres) rc = set_err(ctx, SPG_E_NOMEM, "seg_dots");
-    if (!rc) {
-      KScope ks(ctx, "spark_evaluate", 32.0 * nm * nseg + 32.0 * nm);
-      hipLaunchKernelGGL(k_seg_dot, dim3(nb, (unsigned)nseg), dim3(256), 0, ctx->stream, base + i0, seglen, d_eq + i0, nm,
-                         part);
-      hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)nseg), dim3(256), 0, ctx->stream, part, (int)nb, dres);
-      if (hipGetLastError() != hipSuccess) rc = set_err(ctx, SPG_E_HIP, "seg_dots launch");
-    }
-    if (!rc) rc = d2h_fq(ctx, dres, out->data(), nseg);
+// out[s] = sum_i base[s * seglen + i] * eq[i], i < n, s < nseg; sharded: rank r sums its balanced share of i.
+// Several such dot sets queued back to back into disjoint workspace ranges: one download (and, sharded, one
+// summing allgather) for all of them instead of one per set.
+struct SegDotJob {
+  const Fq* base;
+  size_t seglen, nseg;
+  const Fq* d_eq;
+  size_t n;
+  FqV* out;
+};
+static int seg_dots_multi(spg_ctx* ctx, const std::vector<SegDotJob>& jobs, const Shard& sh = Shard()) {
+  std::vector<unsigned> nbs(jobs.size(), 0);
+  size_t tot_part = 0, tot_res = 0;
+  bool all_local = true;
+  for (size_t k = 0; k < jobs.size(); k++) {
+    const SegDotJob& j = jobs[k];
+    const size_t nm = shard_begin(j.n, sh.n, sh.rank + 1) - shard_begin(j.n, sh.n, sh.rank);
+    if (nm) nbs[k] = (unsigned)std::min<size_t>(nblk(nm), std::max<size_t>(1, 2048 / j.nseg));
+    else all_local = false;
+    tot_part += j.nseg * nbs[k];
+    tot_res += j.nseg;
   }
-  return comm_sum_fq(ctx, sh, rc, out->data(), nseg);
+  FqV all(tot_res, fq_zero());
+  int rc = 0;
+  if (tot_part) {
+    Fq* part = (Fq*)ws_get(ctx, kWsSegPart, tot_part * sizeof(Fq) + 64);
+    Fq* dres = (Fq*)ws_get(ctx, kWsSeg, tot_res * sizeof(Fq) + 64);
+    if (!part || !dres) rc = set_err(ctx, SPG_E_NOMEM, "seg_dots");
+    if (!rc && !all_local && hipMemsetAsync(dres, 0, tot_res * sizeof(Fq), ctx->stream) != hipSuccess)
+      rc = set_err(ctx, SPG_E_HIP, "seg_dots memset");
+    size_t po = 0, ro = 0;
+    for (size_t k = 0; !rc && k < jobs.size(); k++) {
+      const SegDotJob& j = jobs[k];
+      if (nbs[k]) {
+        const size_t i0 = shard_begin(j.n, sh.n, sh.rank), nm = shard_begin(j.n, sh.n, sh.rank + 1) - i0;
+        KScope ks(ctx, "spark_evaluate", 32.0 * nm * j.nseg + 32.0 * nm);
+        hipLaunchKernelGGL(k_seg_dot, dim3(nbs[k], (unsigned)j.nseg), dim3(256), 0, ctx->stream, j.base + i0, j.seglen,
+                           j.d_eq + i0, nm, part + po);
+        hipLaunchKernelGGL(k_sum_seg, dim3((unsigned)j.nseg), dim3(256), 0, ctx->stream, part + po, (int)nbs[k],
+                           dres + ro);
+        if (hipGetLastError() != hipSuccess) rc = set_err(ctx, SPG_E_HIP, "seg_dots launch");
+      }
+      po += j.nseg * nbs[k];
+      ro += j.nseg;
+    }
+    if (!rc) rc = d2h_fq(ctx, dres, all.data(), tot_res);
+  }
+  rc = comm_sum_fq(ctx, sh, rc, all.data(), tot_res);
+  if (rc) return rc;
+  size_t ro = 0;
+  for (const SegDotJob& j : jobs) {
+    j.out->assign(all.begin() + ro, all.begin() + ro + j.nseg);
+    ro += j.nseg;
+  }
+  return 0;
 }
 
 // UniPoly::append_to_transcript (unipoly.rs:112-120)
@@ -1276,9 +1310,8 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   if (!rc) rc = eq_table(ctx, rand_mem, eq_mem);
   if (rc) return rc;
   FqV ev_der, ev_ops, ev_mem;
-  rc = seg_dots(ctx, derefs, N, 2 * B, eq_ops, N, &ev_der, sh);
-  if (!rc) rc = seg_dots(ctx, S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops, sh);
-  if (!rc) rc = seg_dots(ctx, S->d_comb_mem, cells, 2, eq_mem, cells, &ev_mem, sh);
+  rc = seg_dots_multi(ctx, {{derefs, N, 2 * B, eq_ops, N, &ev_der}, {S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops},
+                            {S->d_comb_mem, cells, 2, eq_mem, cells, &ev_mem}}, sh);
   if (rc) return rc;
   lp.lap("hash_evals");
   DotProductProofLogP pf_der, pf_ops, pf_mem;
