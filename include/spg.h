@@ -31,6 +31,7 @@ extern "C" {
 #define SPG_E_POINT -4     /* invalid compressed point (ProofVerifyError::DecompressionError) */
 #define SPG_E_NODEVICE -5  /* no usable gfx950 device */
 #define SPG_E_VERIFY -6    /* a proof did not verify (spg_last_error names the failed check) */
+#define SPG_E_CALLBACK -7  /* a caller-provided transcript callback returned non-zero */
 
 typedef struct spg_ctx spg_ctx;
 typedef struct spg_gens spg_gens;
@@ -143,6 +144,20 @@ int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_buf* Z, size_
 typedef struct spg_transcript spg_transcript;
 typedef struct spg_random_tape spg_random_tape;
 int spg_transcript_new(const char* label, spg_transcript** out);
+/* A transcript backed by the caller's own Fiat-Shamir state (SNARK::prove's `transcript: &mut Transcript`,
+ * src/lib.rs:1022, appended to from :1033 on; ProofTranscript src/transcript.rs:5-63). Every operation of the
+ * prover or verifier reduces to merlin's two primitives and is forwarded, in order, to
+ *   append(user, label, msg, len)         = Transcript::append_message(label, msg)
+ *   challenge(user, label, out, len)      = Transcript::challenge_bytes(label, out[..len])
+ * so whatever the caller appended before the call, and whatever it draws after it, continue one transcript.
+ * Labels are NUL-terminated; the labels libspg emits itself are string literals of the library (static storage,
+ * valid while libspg is loaded: a Rust shim may hand them to merlin as &'static [u8]). A callback returns 0 on
+ * success; the first non-zero return is latched: later operations are not forwarded, and the entry point that
+ * was running returns SPG_E_CALLBACK. spg_transcript_append_* / challenge_* on such a handle forward too. */
+typedef int (*spg_transcript_append_fn)(void* user, const char* label, const uint8_t* msg, size_t len);
+typedef int (*spg_transcript_challenge_fn)(void* user, const char* label, uint8_t* out, size_t len);
+int spg_transcript_new_callbacks(spg_transcript_append_fn append, spg_transcript_challenge_fn challenge, void* user,
+                                 spg_transcript** out);
 int spg_transcript_append_message(spg_transcript* t, const char* label, const uint8_t* msg, size_t len);
 /* ProofTranscript::append_scalar: label, Scalar::to_bytes (canonical LE) */
 int spg_transcript_append_scalar(spg_transcript* t, const char* label, const uint64_t* scalar_mont);

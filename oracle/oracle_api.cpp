@@ -69,6 +69,16 @@ void orc_merlin_simple(const char* label, const char* l1, const uint8_t* m1, siz
   t.challenge_bytes(l2, out, m);
 }
 
+// merlin Transcript as a handle (tests: the caller-side transcript behind spg_transcript_new_callbacks)
+void* orc_transcript_new(const char* label) { return new Transcript(label); }
+void orc_transcript_append(void* t, const char* label, const uint8_t* msg, size_t n) {
+  ((Transcript*)t)->append_message(label, msg, n);
+}
+void orc_transcript_challenge(void* t, const char* label, uint8_t* out, size_t n) {
+  ((Transcript*)t)->challenge_bytes(label, out, n);
+}
+void orc_transcript_free(void* t) { delete (Transcript*)t; }
+
 // ---- ristretto255 ----
 int orc_ge_decompress_compress(const uint8_t* in, uint8_t* out) {
   Ge p;
@@ -166,6 +176,34 @@ int orc_commit_rows(const uint8_t* bases, size_t nb, const uint8_t* h, const uin
 #include "../include/spg.h"
 #include "r1cs.hpp"
 
+extern "C" {
+// ---- UniPoly (src/unipoly.rs:23-111) and DensePolynomial::evaluate (src/dense_mlpoly.rs:361-367), for the
+// reference's own known-answer tests (unipoly.rs:127-181, dense_mlpoly.rs:1234-1252) ----
+// evals (n = 3 or 4) -> coeffs (n), then evaluate(r) -> *at_r, and decompress(compress(), e0 + e1) -> coeffs_rt
+void orc_unipoly(const uint64_t* evals, size_t n, const uint64_t* r, uint64_t* coeffs, uint64_t* at_r,
+                 uint64_t* coeffs_rt) {
+  FqVec e;
+  for (size_t i = 0; i < n; i++) e.push_back(ld(evals + 4 * i));
+  UniPoly u = UniPoly::from_evals(e);
+  for (size_t i = 0; i < u.coeffs.size(); i++) st(coeffs + 4 * i, u.coeffs[i]);
+  st(at_r, u.evaluate(ld(r)));
+  UniPoly d = UniPoly::decompress(u.compress(), fq_add(u.eval_at_zero(), u.eval_at_one()));
+  for (size_t i = 0; i < d.coeffs.size(); i++) st(coeffs_rt + 4 * i, d.coeffs[i]);
+}
+// DensePolynomial::new(Z).evaluate(r) -> out[0]; evaluate_with_LR (dense_mlpoly.rs:1212-1231: L.Z.R with the
+// factored eq tables) -> out[1]
+void orc_dense_eval(const uint64_t* Z, size_t n, const uint64_t* r, size_t ell, uint64_t* out) {
+  FqVec z, rv;
+  for (size_t i = 0; i < n; i++) z.push_back(ld(Z + 4 * i));
+  for (size_t i = 0; i < ell; i++) rv.push_back(ld(r + 4 * i));
+  DensePoly p(z);
+  st(out, p.evaluate(rv));
+  FqVec L, R;
+  eq_factored_evals(rv, &L, &R);
+  st(out + 4, dot(p.bound(L), R));
+}
+}
+
 static R1CSInstance inst_from_c(const spg_r1cs_instance* ci) {
   std::vector<std::vector<SparseEntry>> A, B, C;
   for (size_t p = 0; p < ci->num_instances; p++) {
@@ -214,19 +252,35 @@ extern "C" {
 // bincode(R1CSProof). proof_cap bytes available; *proof_len receives the size. gens label = gens_label,
 // gens_num_vars = the R1CSGens num_vars (power of two). challenges_out (optional) receives
 // rp | rq_rev | rx | rw||ry concatenated; ch_lens[4] their lengths.
+// the same on a caller's transcript handle (orc_transcript_new), which keeps its state after the proof
+int orc_r1cs_prove_tr(const spg_r1cs_instance* ci, size_t num_instances, size_t max_num_proofs,
+                      const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
+                      const spg_witness_sec* secs, size_t nws, const char* gens_label, size_t gens_num_vars,
+                      void* transcript, const uint64_t* tape_seed, uint8_t* proof, size_t proof_cap,
+                      size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens);
 int orc_r1cs_prove(const spg_r1cs_instance* ci, size_t num_instances, size_t max_num_proofs,
                    const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
                    const spg_witness_sec* secs, size_t nws, const char* gens_label, size_t gens_num_vars,
                    const char* transcript_label, const uint64_t* tape_seed, uint8_t* proof, size_t proof_cap,
                    size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  Transcript t(transcript_label);
+  return orc_r1cs_prove_tr(ci, num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs, secs, nws,
+                           gens_label, gens_num_vars, &t, tape_seed, proof, proof_cap, proof_len, challenges_out,
+                           ch_lens);
+}
+int orc_r1cs_prove_tr(const spg_r1cs_instance* ci, size_t num_instances, size_t max_num_proofs,
+                      const size_t* num_proofs, size_t max_num_inputs, const size_t* num_inputs,
+                      const spg_witness_sec* secs, size_t nws, const char* gens_label, size_t gens_num_vars,
+                      void* transcript, const uint64_t* tape_seed, uint8_t* proof, size_t proof_cap,
+                      size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
   try {
+    Transcript& t = *(Transcript*)transcript;
     R1CSInstance inst = inst_from_c(ci);
     std::vector<WitnessSec> ws;
     for (size_t i = 0; i < nws; i++) ws.push_back(ws_from_c(&secs[i]));
     std::vector<const WitnessSec*> wp;
     for (auto& w : ws) wp.push_back(&w);
     R1CSGens gens = R1CSGens::create(gens_label, gens_num_vars);
-    Transcript t(transcript_label);
     RandomTape tape("proof", ld(tape_seed));
     std::vector<size_t> np(num_proofs, num_proofs + num_instances), ni(num_inputs, num_inputs + num_instances);
     std::vector<FqVec> ch;
@@ -341,10 +395,23 @@ static double g_spark_prove_us = 0.0;
 // wall time of the last orc_spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove (CPU baseline)
 double orc_spark_last_prove_us() { return g_spark_prove_us; }
 
+// transcript != NULL: prove on that caller's handle (orc_transcript_new) instead of a fresh Transcript(label) and
+// skip the verification (returns 1)
+int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size_t gens_nnz, size_t gens_batch,
+                       const uint64_t* rx, size_t rx_len, const uint64_t* ry, size_t ry_len, const char* label,
+                       void* transcript, const uint64_t* tape_seed, uint8_t* comm_out, size_t comm_cap,
+                       size_t* comm_len, uint8_t* proof_out, size_t proof_cap, size_t* proof_len);
 int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t gens_nnz, size_t gens_batch,
                     const uint64_t* rx, size_t rx_len, const uint64_t* ry, size_t ry_len, const char* label,
                     const uint64_t* tape_seed, uint8_t* comm_out, size_t comm_cap, size_t* comm_len,
                     uint8_t* proof_out, size_t proof_cap, size_t* proof_len) {
+  return orc_spark_prove_tr(ci, gens_label, gens_nnz, gens_batch, rx, rx_len, ry, ry_len, label, nullptr, tape_seed,
+                            comm_out, comm_cap, comm_len, proof_out, proof_cap, proof_len);
+}
+int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size_t gens_nnz, size_t gens_batch,
+                       const uint64_t* rx, size_t rx_len, const uint64_t* ry, size_t ry_len, const char* label,
+                       void* transcript, const uint64_t* tape_seed, uint8_t* comm_out, size_t comm_cap,
+                       size_t* comm_len, uint8_t* proof_out, size_t proof_cap, size_t* proof_len) {
   try {
     R1CSInstance inst = inst_from_c(ci);
     std::vector<const SparseMat*> polys;
@@ -362,7 +429,8 @@ int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t 
     SparkCommitment comm = spark_multi_commit(polys, g, &dense);
     auto t0 = std::chrono::steady_clock::now();
     FqVec evals = inst.multi_evaluate(vx, vy);
-    Transcript t(label);
+    Transcript tl(label);
+    Transcript& t = transcript ? *(Transcript*)transcript : tl;
     RandomTape tape("proof", ld(tape_seed));
     SparkEvalProof pf = spark_prove(dense, vx, vy, evals, g, t, tape);
     g_spark_prove_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
@@ -374,6 +442,7 @@ int orc_spark_prove(const spg_r1cs_instance* ci, const char* gens_label, size_t 
     if (sc.b.size() > comm_cap || sp.b.size() > proof_cap) return -1;
     memcpy(comm_out, sc.b.data(), sc.b.size());
     memcpy(proof_out, sp.b.data(), sp.b.size());
+    if (transcript) return 1;
     Transcript tv(label);
     return spark_verify(pf, comm, vx, vy, evals, g, tv) ? 1 : 0;
   } catch (const std::string& e) {
@@ -466,6 +535,29 @@ extern "C" {
 // SNARK::multi_encode(block) / encode(pairwise) / encode(perm_root), then SNARK::prove under a fresh
 // Transcript(label) + RandomTape("proof", seed) with vars_gens = R1CSGens(gens_label, gens_num_vars); writes
 // bincode(SNARK). Returns 0 when the oracle's verifier accepts, >0 = failing verifier stage, <0 on error.
+// SNARK::prove alone on a caller's transcript handle (orc_transcript_new, possibly appended to already; it keeps
+// its state after the proof, as `transcript: &mut Transcript` does, src/lib.rs:1022). 0 on success.
+int orc_snark_prove_tr(const spg_snark_inputs* in_c, const spg_snark_instance* block_c,
+                       const spg_snark_instance* pairwise_c, const spg_snark_instance* perm_root_c,
+                       const char* gens_label, size_t gens_num_vars, void* transcript, const uint64_t* tape_seed,
+                       uint8_t* out, size_t cap, size_t* out_len) {
+  try {
+    SnarkIn in = snark_in_from_c(in_c);
+    SnarkInst block = snark_inst_from_c(block_c, true), pairwise = snark_inst_from_c(pairwise_c, false),
+              perm_root = snark_inst_from_c(perm_root_c, false);
+    R1CSGens vg = R1CSGens::create(gens_label, gens_num_vars);
+    RandomTape tape("proof", ld(tape_seed));
+    SNARKProof pf = snark_prove(in, block, pairwise, perm_root, vg, *(Transcript*)transcript, tape);
+    Ser s;
+    pf.ser(s);
+    *out_len = s.b.size();
+    if (s.b.size() > cap) return -1;
+    memcpy(out, s.b.data(), s.b.size());
+    return 0;
+  } catch (const std::string& e) {
+    return -2;
+  }
+}
 int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* block_c,
                     const spg_snark_instance* pairwise_c, const spg_snark_instance* perm_root_c, const char* gens_label,
                     size_t gens_num_vars, const char* label, const uint64_t* tape_seed, uint8_t* out, size_t cap,

@@ -98,6 +98,25 @@ def fq_batch_invert(a):
     return a, allinv
 
 
+# ---------------- UniPoly / MLE evaluation ----------------
+def unipoly(evals, r):
+    """UniPoly::from_evals (src/unipoly.rs:23-54) -> (coeffs, evaluate(r), decompress(compress(), e0 + e1).coeffs)"""
+    e = u64s(evals).reshape(-1, 4)
+    n = e.shape[0]
+    co, rt = np.zeros((n, 4), np.uint64), np.zeros((n, 4), np.uint64)
+    at = np.zeros(4, np.uint64)
+    lib().orc_unipoly(_p(e), ctypes.c_size_t(n), _p(u64s(r)), _p(co), _p(at), _p(rt))
+    return co, at, rt
+
+
+def dense_eval(Z, r):
+    """DensePolynomial::new(Z).evaluate(r) and evaluate_with_LR (src/dense_mlpoly.rs:361-367, 1212-1231)"""
+    z, rr = u64s(Z).reshape(-1, 4), u64s(r).reshape(-1, 4)
+    out = np.zeros((2, 4), np.uint64)
+    lib().orc_dense_eval(_p(z), ctypes.c_size_t(z.shape[0]), _p(rr), ctypes.c_size_t(rr.shape[0]), _p(out))
+    return out[0], out[1]
+
+
 # ---------------- hashing ----------------
 def keccak_f1600(state200):
     s = np.frombuffer(bytes(state200), dtype=np.uint8).copy()
@@ -118,6 +137,37 @@ def merlin_simple(label, l1, m1, l2, n):
     lib().orc_merlin_simple(ctypes.c_char_p(label), ctypes.c_char_p(l1), _p(m), ctypes.c_size_t(len(m1)),
                             ctypes.c_char_p(l2), _p(out), ctypes.c_size_t(n))
     return out.tobytes()
+
+
+class OracleTranscript:
+    """merlin Transcript of the oracle as a handle: the caller-side state behind spg_transcript_new_callbacks in the
+    drop-in tests (append_message / challenge_bytes, src/transcript.rs:5-63)"""
+
+    def __init__(self, label):
+        f = lib().orc_transcript_new
+        f.restype = ctypes.c_void_p
+        self.h = ctypes.c_void_p(f(ctypes.c_char_p(bytes(label))))
+
+    def append_message(self, label, msg):
+        m = np.frombuffer(bytes(msg) or b"\0", dtype=np.uint8).copy()
+        lib().orc_transcript_append(self.h, ctypes.c_char_p(bytes(label)), _p(m), ctypes.c_size_t(len(msg)))
+
+    def append_raw(self, label_ptr, msg_ptr, n):  # from a ctypes callback (pointers as given by libspg)
+        lib().orc_transcript_append(self.h, ctypes.c_char_p(label_ptr), ctypes.c_void_p(msg_ptr), ctypes.c_size_t(n))
+
+    def challenge_raw(self, label_ptr, out_ptr, n):
+        lib().orc_transcript_challenge(self.h, ctypes.c_char_p(label_ptr), ctypes.c_void_p(out_ptr), ctypes.c_size_t(n))
+
+    def challenge_bytes(self, label, n):
+        out = np.zeros(max(n, 1), dtype=np.uint8)
+        lib().orc_transcript_challenge(self.h, ctypes.c_char_p(bytes(label)), _p(out), ctypes.c_size_t(n))
+        return out[:n].tobytes()
+
+    def __del__(self):
+        try:
+            lib().orc_transcript_free(self.h)
+        except Exception:
+            pass
 
 
 # ---------------- ristretto ----------------
@@ -199,8 +249,10 @@ def commit_rows(bases, h, Z, L, R, blinds=None):
 
 
 # ---------------------------------------------------------------- R1CSProof
-def r1cs_prove(wl, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24, label=b"r1cs_test"):
-    """bincode(R1CSProof) and the challenge vectors [rp, rq_rev, rx, rw||ry] for an R1CSWorkload."""
+def r1cs_prove(wl, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24, label=b"r1cs_test",
+               transcript=None):
+    """bincode(R1CSProof) and the challenge vectors [rp, rq_rev, rx, rw||ry] for an R1CSWorkload (on a fresh
+    Transcript(label), or on the caller's OracleTranscript `transcript`, which keeps its state)."""
     import workload
 
     v = workload.CViews(wl)
@@ -210,11 +262,14 @@ def r1cs_prove(wl, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24
     ch = np.zeros((4096, 4), dtype=np.uint64)
     chl = (ctypes.c_size_t * 4)()
     seed = u64s(tape_seed)
-    rc = lib().orc_r1cs_prove(ctypes.byref(v.inst), ctypes.c_size_t(wl.P), ctypes.c_size_t(wl.max_num_proofs),
-                              v.num_proofs, ctypes.c_size_t(wl.max_num_inputs), v.num_inputs, v.secs,
-                              ctypes.c_size_t(wl.nws), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars),
-                              ctypes.c_char_p(label), _p(seed), _p(buf), ctypes.c_size_t(cap), ctypes.byref(ln),
-                              _p(ch), chl)
+    common = (ctypes.byref(v.inst), ctypes.c_size_t(wl.P), ctypes.c_size_t(wl.max_num_proofs), v.num_proofs,
+              ctypes.c_size_t(wl.max_num_inputs), v.num_inputs, v.secs, ctypes.c_size_t(wl.nws),
+              ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars))
+    tail = (_p(seed), _p(buf), ctypes.c_size_t(cap), ctypes.byref(ln), _p(ch), chl)
+    if transcript is None:
+        rc = lib().orc_r1cs_prove(*common, ctypes.c_char_p(label), *tail)
+    else:
+        rc = lib().orc_r1cs_prove_tr(*common, transcript.h, *tail)
     assert rc == 0, rc
     lens = list(chl)
     out, o = [], 0
@@ -251,9 +306,10 @@ def r1cs_multi_evaluate(wl, rx, ry):
 
 
 def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=None, gens_batch=3,
-                label=b"spark_test"):
+                label=b"spark_test", transcript=None):
     """SparseMatPolyEvalProof over [A_0, B_0, C_0, ...] of the workload's instance at (rx, ry):
-    (bincode(commitment), bincode(proof), verified)"""
+    (bincode(commitment), bincode(proof), verified); with an OracleTranscript `transcript` the proof runs on it
+    (no verification)"""
     import workload
 
     v = workload.CViews(wl)
@@ -265,9 +321,10 @@ def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=No
     pb = np.zeros(1 << 22, dtype=np.uint8)
     cl, pl = ctypes.c_size_t(0), ctypes.c_size_t(0)
     seed = u64s(tape_seed)
-    rc = lib().orc_spark_prove(ctypes.byref(v.inst), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_nnz),
+    rc = lib().orc_spark_prove_tr(ctypes.byref(v.inst), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_nnz),
                                ctypes.c_size_t(gens_batch), _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
-                               ctypes.c_size_t(ry.shape[0]), ctypes.c_char_p(label), _p(seed), _p(cb),
+                               ctypes.c_size_t(ry.shape[0]), ctypes.c_char_p(label),
+                               None if transcript is None else transcript.h, _p(seed), _p(cb),
                                ctypes.c_size_t(len(cb)), ctypes.byref(cl), _p(pb), ctypes.c_size_t(len(pb)),
                                ctypes.byref(pl))
     assert rc >= 0, rc
@@ -294,6 +351,21 @@ def snark_prove(wl, tape_seed, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 2
                                ctypes.c_char_p(label), _p(seed), _p(out), ctypes.c_size_t(cap), ctypes.byref(ln))
     assert rc >= 0, rc
     return out[: ln.value].tobytes(), rc
+
+
+def snark_prove_on(wl, tape_seed, transcript, gens_label=b"gens_r1cs_sat", gens_num_vars=1 << 24, cap=1 << 24):
+    """SNARK::prove on the caller's OracleTranscript (which keeps its state, as `&mut Transcript`) -> bincode(SNARK)"""
+    import workload
+
+    v = workload.SnarkViews(wl)
+    out = np.zeros(cap, dtype=np.uint8)
+    ln = ctypes.c_size_t(0)
+    seed = u64s(tape_seed)
+    rc = lib().orc_snark_prove_tr(ctypes.byref(v.inputs), ctypes.byref(v.block), ctypes.byref(v.pairwise),
+                                  ctypes.byref(v.perm_root), ctypes.c_char_p(gens_label), ctypes.c_size_t(gens_num_vars),
+                                  transcript.h, _p(seed), _p(out), ctypes.c_size_t(cap), ctypes.byref(ln))
+    assert rc == 0, rc
+    return out[: ln.value].tobytes()
 
 
 def snark_last_prove_us():

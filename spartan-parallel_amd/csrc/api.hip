@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include "comm.hpp"
 #include "ctx.hpp"
 #include "hpool.hpp"
 
@@ -230,8 +231,10 @@ std::vector<int> choose_pool_cpus(int device) {
   else
     std::stable_sort(cand.begin(), cand.end(), [](const std::pair<double, std::vector<int>>& a,
                                                   const std::pair<double, std::vector<int>>& b) { return a.first < b.first; });
-  const char* lr = getenv("LOCAL_RANK");  // torchrun: one process per GPU, or several sharing one in rehearsals
-  const size_t slot = lr ? (size_t)atoi(lr) : (size_t)device;
+  // torchrun: one process per GPU, or several sharing one in rehearsals. Without LOCAL_RANK the least busy domain:
+  // a prover started next to a running one sees that one's spinning workers in the sample and goes elsewhere
+  const char* lr = getenv("LOCAL_RANK");
+  const size_t slot = lr ? (size_t)atoi(lr) : 0;
   return cand[slot % cand.size()].second;
 }
 
@@ -301,16 +304,13 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SPG_E_NODEVICE;
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return SPG_E_NODEVICE;
   if (hipSetDevice(device) != hipSuccess) return SPG_E_HIP;
-  // (before the host buffers below are first touched, so they live on that NUMA node)
-  // SPG_PIN (default on): the host pool (created on first use) and this thread on one L3 domain (CCD) local to the
-  // GPU, the least busy one (spg::choose_pool_cpus)
+  // SPG_PIN (default on): the host pool's workers (created on first use) on one L3 domain (CCD) local to the GPU, the
+  // least busy one (spg::choose_pool_cpus); the calling thread joins them only inside prover calls (spg::HostPin)
+  // and keeps its own affinity otherwise
   const char* pin = getenv("SPG_PIN");
   if ((!pin || atoi(pin) != 0) && spg::pool_cpus().empty()) {
     std::vector<int> cpus = spg::choose_pool_cpus(device);
-    if (!cpus.empty()) {
-      spg::pool_cpus() = cpus;
-      spg::pin_thread(cpus);
-    }
+    if (!cpus.empty()) spg::pool_cpus() = cpus;
   }
   spg_ctx* c = new spg_ctx();
   c->device = device;
@@ -373,23 +373,12 @@ int comm_allgather(spg_ctx* c, const Shard& sh, int status, const void* send, si
     return status;
   }
   if (!c->allgather) return set_err(c, SPG_E_ARG, "no communicator set (spg_set_comm)");
-  // [status (8 bytes) | payload] per rank
-  const size_t rec = 8 + bytes;
-  std::vector<uint8_t> mine(rec, 0), all(rec * sh.n);
-  int64_t st = status;
-  memcpy(mine.data(), &st, 8);
-  if (bytes) memcpy(mine.data() + 8, send, bytes);
-  if (c->allgather(c->comm_user, mine.data(), rec, all.data()) != 0)
-    return set_err(c, SPG_E_HIP, "allgather callback failed");
-  recv.resize(bytes * sh.n);
-  int first = status;
-  for (int q = 0; q < sh.n; q++) {
-    int64_t s;
-    memcpy(&s, all.data() + q * rec, 8);
-    if (!first && s) first = set_err(c, (int)s, "a peer rank failed (status " + std::to_string(s) + ")");
-    if (bytes) memcpy(recv.data() + q * bytes, all.data() + q * rec + 8, bytes);
-  }
-  return first;
+  int64_t first = 0;
+  if (allgather_with_status(c->allgather, c->comm_user, sh.n, status, send, bytes, recv, &first) != 0)
+    return set_err(c, SPG_E_HIP, "allgather failed");
+  if (status) return status;
+  if (first) return set_err(c, (int)first, "a peer rank failed (status " + std::to_string(first) + ")");
+  return 0;
 }
 
 int comm_sum_fq(spg_ctx* c, const Shard& sh, int status, Fq* v, size_t n) {
@@ -397,12 +386,7 @@ int comm_sum_fq(spg_ctx* c, const Shard& sh, int status, Fq* v, size_t n) {
   std::vector<uint8_t> r;
   int rc = comm_allgather(c, sh, status, v, n * sizeof(Fq), r);
   if (rc) return rc;
-  const Fq* a = (const Fq*)r.data();
-  for (size_t i = 0; i < n; i++) {
-    Fq acc = a[i];
-    for (int q = 1; q < sh.n; q++) acc = fq_add(acc, a[q * n + i]);
-    v[i] = acc;
-  }
+  sum_over_ranks(r.data(), sh.n, n, v);
   return 0;
 }
 

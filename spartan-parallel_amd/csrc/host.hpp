@@ -15,6 +15,7 @@
 #include <memory>
 #include <vector>
 
+#include "../../include/spg.h"
 #include "curve.hpp"
 #include "hcurve.hpp"
 #include "hpool.hpp"
@@ -67,25 +68,53 @@ struct Writer {
   }
 };
 
+// The caller's transcript behind spg_transcript_new_callbacks: every append_message / challenge_bytes of the
+// prover is forwarded, so the caller's merlin::Transcript stays the one Fiat-Shamir state (SNARK::prove's
+// `transcript: &mut Transcript`, src/lib.rs:1022). The first failing callback is kept in `failed`; later
+// operations are skipped (challenges read as zero) and the entry point returns SPG_E_CALLBACK.
+struct TrCallbacks {
+  spg_transcript_append_fn append = nullptr;
+  spg_transcript_challenge_fn challenge = nullptr;
+  void* user = nullptr;
+  int failed = 0;
+};
+
 struct Tr {
   Merlin m;
+  std::shared_ptr<TrCallbacks> cb;  // null: the library's own merlin transcript
   explicit Tr(const char* label) : m(label) {}
-  void msg(const char* label, const char* s) { m.message(label, s, strlen(s)); }
+  // the two merlin operations every ProofTranscript method reduces to (src/transcript.rs:13-46)
+  void message(const char* label, const void* data, size_t n) {
+    if (!cb) return m.message(label, data, n);
+    if (cb->failed) return;
+    const int rc = cb->append(cb->user, label, (const uint8_t*)data, n);
+    if (rc) cb->failed = rc;
+  }
+  void challenge_bytes(const char* label, void* dst, size_t n) {
+    if (!cb) return m.challenge(label, dst, n);
+    if (!cb->failed) {
+      const int rc = cb->challenge(cb->user, label, (uint8_t*)dst, n);
+      if (rc) cb->failed = rc;
+    }
+    if (cb->failed) memset(dst, 0, n);
+  }
+  int failed() const { return cb ? cb->failed : 0; }
+  void msg(const char* label, const char* s) { message(label, s, strlen(s)); }
   void protocol(const char* name) { msg("protocol-name", name); }
   void scalar(const char* label, const Fq& a) {
     uint8_t b[32];
     fq_le_bytes(a, b);
-    m.message(label, b, 32);
+    message(label, b, 32);
   }
-  void point(const char* label, const Pt& p) { m.message(label, p.b, 32); }
+  void point(const char* label, const Pt& p) { message(label, p.b, 32); }
   void u64(const char* label, uint64_t x) {
     uint8_t b[8];
     for (int i = 0; i < 8; i++) b[i] = (uint8_t)(x >> (8 * i));
-    m.message(label, b, 8);
+    message(label, b, 8);
   }
   Fq challenge(const char* label) {
     uint8_t b[64];
-    m.challenge(label, b, 64);
+    challenge_bytes(label, b, 64);
     return fq_from_wide(b);
   }
   FqV challenges(const char* label, size_t n) {

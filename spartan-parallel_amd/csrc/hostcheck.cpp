@@ -9,9 +9,11 @@
 #include <memory>
 #include <random>
 
+#include "comm.hpp"
 #include "curve.hpp"
-#include "hpool.hpp"
 #include "hcurve.hpp"
+#include "hostmath.hpp"
+#include "hpool.hpp"
 #include "keccak.hpp"
 
 using namespace spg;
@@ -159,23 +161,39 @@ int spgh_hcurve_check(const uint8_t* uni, const uint8_t* k, size_t n) {
   return bad;
 }
 
-// The cross-rank step of the sharded R1CSProof (r1cs.hip, Prover::sum_ranks): gather every rank's three
-// partial round sums through the caller's allgather and add them mod q.
-int spgh_allgather_sum(int (*fn)(void*, const void*, size_t, void*), void* user, int nranks, const uint64_t* mine,
-                       uint64_t* out) {
-  using namespace spg;
-  std::vector<uint8_t> recv(96 * (size_t)nranks);
-  if (fn(user, mine, 96, recv.data()) != 0) return -1;
-  for (int k = 0; k < 3; k++) {
-    Fq acc = fq_zero();
-    for (int r = 0; r < nranks; r++) {
-      Fq v;
-      memcpy(v.l, recv.data() + 96 * r + 32 * k, 32);
-      acc = fq_add(acc, v);
-    }
-    memcpy(out + 4 * k, acc.l, 32);
-  }
+// The cross-rank exchange of every sharded call (comm.hpp: api.hip's comm_sum_fq, which Prover::sum_ranks and the
+// SPARK / multi_evaluate shards use): gather every rank's status and n partial scalars through the caller's
+// allgather and sum them mod q. Returns the transport's error (-1), else the first non-zero status of any rank
+// (so a failing rank fails every rank alike), else 0 with out = the sums.
+int spgh_comm_sum(spg_allgather_fn fn, void* user, int nranks, int status, const uint64_t* mine, size_t n,
+                  uint64_t* out) {
+  std::vector<Fq> v(n);
+  for (size_t i = 0; i < n; i++) v[i] = ldq(mine + 4 * i);
+  std::vector<uint8_t> all;
+  int64_t first = 0;
+  if (allgather_with_status(fn, user, nranks, status, v.data(), n * sizeof(Fq), all, &first) != 0) return -1;
+  if (first) return (int)first;
+  sum_over_ranks(all.data(), nranks, n, v.data());
+  for (size_t i = 0; i < n; i++) stq(out + 4 * i, v[i]);
   return 0;
+}
+
+// the prover's host scalar helpers (hostmath.hpp): UniPoly::from_evals of degree 3 -> coeffs[4] and evaluate(r)
+void spgh_uni_from_evals3(const uint64_t* evals, const uint64_t* r, uint64_t* coeffs, uint64_t* at_r) {
+  Fq e[4];
+  for (int i = 0; i < 4; i++) e[i] = ldq(evals + 4 * i);
+  FqV c = uni_from_evals3(e);
+  for (int i = 0; i < 4; i++) stq(coeffs + 4 * i, c[i]);
+  stq(at_r, uni_eval(c, ldq(r)));
+}
+// DensePolynomial::evaluate of n host scalars at r (ell scalars) and EqPolynomial::evals(r) (2^ell scalars)
+void spgh_dense_eval(const uint64_t* Z, size_t n, const uint64_t* r, size_t ell, uint64_t* out, uint64_t* chis) {
+  FqV z(n), rv(ell);
+  for (size_t i = 0; i < n; i++) z[i] = ldq(Z + 4 * i);
+  for (size_t i = 0; i < ell; i++) rv[i] = ldq(r + 4 * i);
+  stq(out, dense_eval_host(z, rv));
+  FqV e = eq_evals_host(rv);
+  for (size_t i = 0; i < e.size(); i++) stq(chis + 4 * i, e[i]);
 }
 
 // The host pool (hpool.hpp) under stress: `bursts` parallel_for calls of random size 1..max_n on a fresh

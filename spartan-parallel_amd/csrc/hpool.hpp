@@ -19,6 +19,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <mutex>
@@ -42,6 +44,45 @@ inline void pin_thread(const std::vector<int>& cpus) {
   CPU_ZERO(&set);
   for (int c : cpus) CPU_SET(c, &set);
   pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+// Scoped placement of the calling thread on the pool's CPUs for the duration of one prover call; the caller's
+// own mask is restored on return, so the library never changes the affinity that threads or processes a host
+// application creates later inherit (only the pool workers stay pinned).
+struct HostPin {
+  cpu_set_t saved;
+  bool on = false;
+  HostPin() {
+    const std::vector<int>& c = pool_cpus();
+    if (c.empty() || pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) != 0) return;
+    pin_thread(c);
+    on = true;
+  }
+  ~HostPin() {
+    if (on) pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
+  }
+  HostPin(const HostPin&) = delete;
+  HostPin& operator=(const HostPin&) = delete;
+};
+
+// CPUs this process may use: its affinity mask, capped by the cgroup v2 CPU quota (cpu.max), divided among the
+// LOCAL_WORLD_SIZE processes of a node that share them (torchrun sets it; one process per GPU)
+inline int usable_cpus() {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : (int)std::thread::hardware_concurrency();
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[64] = {0};
+    long period = 0;
+    if (fscanf(f, "%63s %ld", q, &period) == 2 && period > 0 && q[0] != 'm') {
+      const long quota = atol(q);
+      if (quota > 0) n = std::min(n, (int)std::max(1L, (quota + period - 1) / period));
+    }
+    fclose(f);
+  }
+  const char* lws = getenv("LOCAL_WORLD_SIZE");
+  if (lws && atoi(lws) > 1) n = std::max(1, n / atoi(lws));
+  return n < 1 ? 1 : n;
 }
 
 class Pool {
@@ -159,11 +200,11 @@ class Pool {
 inline int pool_threads() {
   const char* e = getenv("SPG_POOL_THREADS");
   if (e) return atoi(e);
-  unsigned hw = std::thread::hardware_concurrency();
-  int n = hw > 1 ? (int)hw - 1 : 0;
-  // 7 workers + the caller: measured best on the GPU box (16-CPU quota per process; 15 workers were
-  // 2-5 ms slower per SNARK::prove, scripts/pool_sweep.sh), and it leaves room for HIP's own threads
-  return n > 7 ? 7 : n;
+  // at most 7 workers + the caller: measured best on the GPU box (16-CPU quota per process; 15 workers were
+  // 2-5 ms slower per SNARK::prove, scripts/pool_sweep.sh), and it leaves room for HIP's own threads; fewer
+  // when the process' share of CPUs (usable_cpus) is smaller, so co-located provers do not oversubscribe
+  const int n = usable_cpus() - 1;
+  return n < 0 ? 0 : (n > 7 ? 7 : n);
 }
 inline Pool& pool() {
   static Pool p(pool_threads());

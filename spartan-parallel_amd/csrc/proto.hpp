@@ -191,6 +191,13 @@ struct spg_transcript {
   spg::Tr t;
   explicit spg_transcript(const char* l) : t(l) {}
 };
+namespace spg {
+// an entry point's return code with a failed transcript callback taking precedence (SPG_E_CALLBACK)
+inline int tr_status(spg_ctx* ctx, const Tr& t, int rc) {
+  if (t.failed()) return set_err(ctx, SPG_E_CALLBACK, "transcript callback returned " + std::to_string(t.failed()));
+  return rc;
+}
+}  // namespace spg
 struct spg_random_tape {
   spg::Tape t;
   spg_random_tape(const char* n, const spg::Fq& s) : t(n, s) {}

@@ -218,11 +218,7 @@ __global__ void __launch_bounds__(256) k_sum_segments(const Fq* __restrict__ par
 }
 
 // ------------------------------------------------------------------------------------ host helpers
-
-// EqPolynomial::evals (dense_mlpoly.rs:76-92)
-// DensePolynomial::new(z).evaluate(r) for short host vectors
-
-// UniPoly::from_evals for degree 3 (unipoly.rs:23-54) and evaluate (:72-80)
+// (eq tables, UniPoly::from_evals, short MLE evaluations: hostmath.hpp)
 
 // ZK sumcheck round bookkeeping shared by phase 1 and phase 2 (sumcheck.rs:1247-1370).
 // The RandomTape is a transcript that only ever absorbs labels, so the values a round draws do not depend on
@@ -395,32 +391,13 @@ int Prover::run() {
   return rc0;
 }
 
-// ---- cross-rank exchange (identity when nranks == 1)
+// ---- cross-rank exchange (identity when nranks == 1): comm.hpp through api.hip's comm_allgather, so every exchange
+// carries this rank's status and a failure on one rank fails all of them
 int Prover::allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv) {
-  recv.resize(bytes * nranks);
-  if (nranks == 1) {
-    memcpy(recv.data(), send, bytes);
-    return 0;
-  }
-  if (!ctx->allgather) return set_err(ctx, SPG_E_ARG, "no communicator set (spg_set_comm)");
-  if (ctx->allgather(ctx->comm_user, send, bytes, recv.data()) != 0)
-    return set_err(ctx, SPG_E_HIP, "allgather callback failed");
-  return 0;
+  return comm_allgather(ctx, Shard{(int)rank, (int)nranks}, 0, send, bytes, recv);
 }
 // (e0, e2, e3) summed over the ranks' instance shards
-int Prover::sum_ranks(Fq e[3]) {
-  if (nranks == 1) return 0;
-  std::vector<uint8_t> r;
-  int rc = allgather(e, 3 * sizeof(Fq), r);
-  if (rc) return rc;
-  const Fq* v = (const Fq*)r.data();
-  for (int k = 0; k < 3; k++) {
-    Fq acc = fq_zero();
-    for (size_t q = 0; q < nranks; q++) acc = fq_add(acc, v[3 * q + k]);
-    e[k] = acc;
-  }
-  return 0;
-}
+int Prover::sum_ranks(Fq e[3]) { return comm_sum_fq(ctx, Shard{(int)rank, (int)nranks}, 0, e, 3); }
 // per local instance p, the element (p, 0, 0, 0) of each table -> the same for all P instances, on the host
 int Prover::gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full) {
   const size_t k = tabs.size(), PL = (P + nranks - 1) / nranks;  // the largest shard; slots per rank
@@ -1079,25 +1056,36 @@ extern "C" int spg_transcript_new(const char* label, spg_transcript** out) {
   *out = new spg_transcript(label);
   return SPG_OK;
 }
+extern "C" int spg_transcript_new_callbacks(spg_transcript_append_fn append, spg_transcript_challenge_fn challenge,
+                                            void* user, spg_transcript** out) {
+  if (!append || !challenge || !out) return SPG_E_ARG;
+  spg_transcript* t = new spg_transcript("");  // its own merlin state is never used
+  t->t.cb = std::make_shared<TrCallbacks>();
+  t->t.cb->append = append;
+  t->t.cb->challenge = challenge;
+  t->t.cb->user = user;
+  *out = t;
+  return SPG_OK;
+}
 extern "C" int spg_transcript_append_message(spg_transcript* t, const char* label, const uint8_t* msg, size_t len) {
   if (!t || !label || (!msg && len)) return SPG_E_ARG;
-  t->t.m.message(label, msg, len);
-  return SPG_OK;
+  t->t.message(label, msg, len);
+  return t->t.failed() ? SPG_E_CALLBACK : SPG_OK;
 }
 extern "C" int spg_transcript_append_scalar(spg_transcript* t, const char* label, const uint64_t* scalar_mont) {
   if (!t || !label || !scalar_mont) return SPG_E_ARG;
   t->t.scalar(label, ld_fq(scalar_mont));
-  return SPG_OK;
+  return t->t.failed() ? SPG_E_CALLBACK : SPG_OK;
 }
 extern "C" int spg_transcript_challenge_scalar(spg_transcript* t, const char* label, uint64_t* out_mont) {
   if (!t || !label || !out_mont) return SPG_E_ARG;
   st_fq(out_mont, t->t.challenge(label));
-  return SPG_OK;
+  return t->t.failed() ? SPG_E_CALLBACK : SPG_OK;
 }
 extern "C" int spg_transcript_challenge_bytes(spg_transcript* t, const char* label, uint8_t* out, size_t len) {
   if (!t || !label || (!out && len)) return SPG_E_ARG;
-  t->t.m.challenge(label, out, len);
-  return SPG_OK;
+  t->t.challenge_bytes(label, out, len);
+  return t->t.failed() ? SPG_E_CALLBACK : SPG_OK;
 }
 extern "C" int spg_transcript_free(spg_transcript* t) {
   delete t;
@@ -1414,13 +1402,11 @@ static int check_prove_args(spg_ctx* ctx, const spg_r1cs_inst* inst, size_t num_
   return SPG_OK;
 }
 
-extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst,
-                              size_t num_instances, size_t max_num_proofs, const size_t* num_proofs,
-                              size_t max_num_inputs, const size_t* num_inputs, const spg_r1cs_witness* wit,
-                              spg_transcript* transcript, spg_random_tape* tape, uint8_t* proof, size_t proof_cap,
-                              size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
-  if (!ctx || !gens || !inst || !num_proofs || !num_inputs || !wit || !transcript || !tape || !proof_len)
-    return SPG_E_ARG;
+static int r1cs_prove_impl(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst,
+                           size_t num_instances, size_t max_num_proofs, const size_t* num_proofs,
+                           size_t max_num_inputs, const size_t* num_inputs, const spg_r1cs_witness* wit,
+                           spg_transcript* transcript, spg_random_tape* tape, uint8_t* proof, size_t proof_cap,
+                           size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
   Prover pr(ctx, const_cast<spg_r1cs_gens*>(gens)->g, *inst, *wit, transcript->t, tape->t);
   pr.rank = (size_t)ctx->rank;
   pr.nranks = (size_t)ctx->nranks;
@@ -1461,6 +1447,19 @@ extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg
   if (!proof || wr.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, wr.out.data(), wr.out.size());
   return SPG_OK;
+}
+
+extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1cs_inst* inst,
+                              size_t num_instances, size_t max_num_proofs, const size_t* num_proofs,
+                              size_t max_num_inputs, const size_t* num_inputs, const spg_r1cs_witness* wit,
+                              spg_transcript* transcript, spg_random_tape* tape, uint8_t* proof, size_t proof_cap,
+                              size_t* proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  if (!ctx || !gens || !inst || !num_proofs || !num_inputs || !wit || !transcript || !tape || !proof_len)
+    return SPG_E_ARG;
+  HostPin pin;
+  return tr_status(ctx, transcript->t,
+                   r1cs_prove_impl(ctx, gens, inst, num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs,
+                                   wit, transcript, tape, proof, proof_cap, proof_len, challenges_out, ch_lens));
 }
 
 // R1CSInstance::multi_evaluate (src/r1csinstance.rs:583-596) / evaluate (:632-641):

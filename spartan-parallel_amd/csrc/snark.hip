@@ -681,7 +681,7 @@ int mem_gen(size_t width, Rows mems, size_t total, const Fq& r, const Fq& tau, b
 
 }  // namespace
 
-extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_comp* pairwise, spg_snark_comp* perm_root,
+static int spg_snark_prove_impl(spg_ctx* ctx, spg_snark_comp* block, spg_snark_comp* pairwise, spg_snark_comp* perm_root,
                                const spg_snark_wit* W, spg_r1cs_gens* vars_gens, spg_transcript* transcript,
                                spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
   if (!ctx || !block || !pairwise || !perm_root || !W || !vars_gens || !transcript || !tape_h || !proof_len)
@@ -698,7 +698,7 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   t.protocol("Spartan SNARK proof");
   const bool dbg0 = getenv("SPG_DEBUG_SNARK") != nullptr;
   auto fp = [&](const char* where) {
-    if (!dbg0) return;
+    if (!dbg0 || t.cb) return;  // (a fork of a caller-backed transcript cannot be taken)
     Tr c = t;
     Fq x = c.challenge("dbg");
     fprintf(stderr, "fp %s %08x\n", where, x.l[0]);
@@ -1264,4 +1264,12 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, w.out.data(), w.out.size());
   return SPG_OK;
+}
+
+extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_comp* pairwise, spg_snark_comp* perm_root,
+                               const spg_snark_wit* W, spg_r1cs_gens* vars_gens, spg_transcript* transcript,
+                               spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  if (!ctx || !transcript) return SPG_E_ARG;
+  spg::HostPin pin;
+  return spg::tr_status(ctx, transcript->t, spg_snark_prove_impl(ctx, block, pairwise, perm_root, W, vars_gens, transcript, tape_h, proof, proof_cap, proof_len));
 }

@@ -1385,7 +1385,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
 
 }  // namespace spg
 
-extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+static int spg_spark_prove_impl(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
                                size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
                                spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
   if (!ctx || !S || !transcript || !tape_h || !proof_len || (!rx && rx_len) || (!ry && ry_len) || !evals_in)
@@ -1401,4 +1401,12 @@ extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, s
   if (!proof || w.out.size() > proof_cap) return set_err(ctx, SPG_E_ARG, "proof buffer too small");
   memcpy(proof, w.out.data(), w.out.size());
   return SPG_OK;
+}
+
+extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                               size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
+                               spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  if (!ctx || !transcript) return SPG_E_ARG;
+  spg::HostPin pin;
+  return spg::tr_status(ctx, transcript->t, spg_spark_prove_impl(ctx, S, rx, rx_len, ry, ry_len, evals_in, n_evals, transcript, tape_h, proof, proof_cap, proof_len));
 }

@@ -1358,7 +1358,7 @@ bool snark_verify(SnarkVerifier& v, const SnarkV& pf, const spg_snark_inputs& in
 }  // namespace
 
 // ------------------------------------------------------------------------------------ C-ABI
-extern "C" int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
+static int spg_snark_verify_impl(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
                                 const spg_snark_comp* perm_root, const spg_snark_inputs* inputs,
                                 spg_r1cs_gens* vars_gens, spg_transcript* transcript, const uint8_t* proof,
                                 size_t proof_len) {
@@ -1369,6 +1369,9 @@ extern "C" int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const
       !in.block_num_proofs || !in.block_num_phy_ops || !in.block_num_vir_ops || (in.input_len && !in.input) ||
       !in.output || (in.input_len && !in.input_liveness))
     return set_err(ctx, SPG_E_ARG, "snark verify: public inputs incomplete");
+  for (size_t b = 0; b < in.block_num_instances_bound; b++)  // SNARK::verify's assertion, src/lib.rs:2829-2831
+    if (in.block_num_proofs[b] > in.block_max_num_proofs)
+      return set_err(ctx, SPG_E_ARG, "snark verify: block_num_proofs[b] > block_max_num_proofs");
   SnarkCompView vb, vp, vr;
   if (snark_comp_view(block, &vb) || snark_comp_view(pairwise, &vp) || snark_comp_view(perm_root, &vr))
     return set_err(ctx, SPG_E_ARG, "snark verify: instance commitments incomplete");
@@ -1387,8 +1390,17 @@ extern "C" int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const
   return SPG_OK;
 }
 
+extern "C" int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
+                                const spg_snark_comp* perm_root, const spg_snark_inputs* inputs,
+                                spg_r1cs_gens* vars_gens, spg_transcript* transcript, const uint8_t* proof,
+                                size_t proof_len) {
+  if (!ctx || !transcript) return SPG_E_ARG;
+  spg::HostPin pin;
+  return spg::tr_status(ctx, transcript->t, spg_snark_verify_impl(ctx, block, pairwise, perm_root, inputs, vars_gens, transcript, proof, proof_len));
+}
+
 /* SparseMatPolyEvalProof::verify (src/sparse_mlpoly.rs:1566-1610) against the commitment held by s */
-extern "C" int spg_spark_verify(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+static int spg_spark_verify_impl(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
                                 size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
                                 const uint8_t* proof, size_t proof_len) {
   if (!ctx || !S || !transcript || (!rx && rx_len) || (!ry && ry_len) || (!evals_in && n_evals) || (!proof && proof_len))
@@ -1414,6 +1426,14 @@ extern "C" int spg_spark_verify(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, 
   return SPG_OK;
 }
 
+extern "C" int spg_spark_verify(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, size_t rx_len, const uint64_t* ry,
+                                size_t ry_len, const uint64_t* evals_in, size_t n_evals, spg_transcript* transcript,
+                                const uint8_t* proof, size_t proof_len) {
+  if (!ctx || !transcript) return SPG_E_ARG;
+  spg::HostPin pin;
+  return spg::tr_status(ctx, transcript->t, spg_spark_verify_impl(ctx, S, rx, rx_len, ry, ry_len, evals_in, n_evals, transcript, proof, proof_len));
+}
+
 extern "C" int spg_r1cs_gens_commit(spg_ctx* ctx, const spg_r1cs_gens* gens, const uint64_t* Z, size_t n, uint8_t* out,
                                     size_t out_cap, size_t* L_out) {
   if (!ctx || !gens || (!Z && n) || !L_out) return SPG_E_ARG;
@@ -1432,7 +1452,7 @@ extern "C" int spg_r1cs_gens_commit(spg_ctx* ctx, const spg_r1cs_gens* gens, con
   return SPG_OK;
 }
 
-extern "C" int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t num_instances, size_t max_num_proofs,
+static int spg_r1cs_verify_impl(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t num_instances, size_t max_num_proofs,
                                const size_t* num_proofs, size_t max_num_inputs, const spg_witness_comm* secs, size_t nws,
                                size_t num_cons, const uint64_t* evals, spg_transcript* transcript, const uint8_t* proof,
                                size_t proof_len, uint64_t* challenges_out, size_t* ch_lens) {
@@ -1440,6 +1460,19 @@ extern "C" int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t n
     return SPG_E_ARG;
   if (!is_pow2(max_num_proofs) || !is_pow2(max_num_inputs) || !is_pow2(num_cons) || nws > 8)
     return set_err(ctx, SPG_E_ARG, "r1cs verify: sizes");
+  // the round counts below take lg2 of these: a count that is not a power of two or exceeds its maximum would
+  // index the challenge vectors out of range (R1CSProof::verify asserts the same shapes on the prover's side)
+  for (size_t p = 0; p < num_instances; p++)
+    if (!is_pow2(num_proofs[p]) || num_proofs[p] > max_num_proofs)
+      return set_err(ctx, SPG_E_ARG, "r1cs verify: num_proofs[p] must be a power of two <= max_num_proofs");
+  for (size_t i = 0; i < nws; i++) {
+    const spg_witness_comm& c = secs[i];
+    if (c.num_instances != 1 && c.num_instances != num_instances) return set_err(ctx, SPG_E_ARG, "r1cs verify: section instances");
+    for (size_t p = 0; p < c.num_instances && c.num_proofs && c.num_inputs; p++)
+      if (!is_pow2(c.num_proofs[p]) || c.num_proofs[p] > max_num_proofs || !is_pow2(c.num_inputs[p]) ||
+          c.num_inputs[p] > max_num_inputs)
+        return set_err(ctx, SPG_E_ARG, "r1cs verify: section shape (powers of two within the maxima)");
+  }
   std::vector<VSec> vs(nws);
   std::vector<const VSec*> ws;
   for (size_t i = 0; i < nws; i++) {
@@ -1481,4 +1514,13 @@ extern "C" int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t n
     }
   }
   return SPG_OK;
+}
+
+extern "C" int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t num_instances, size_t max_num_proofs,
+                               const size_t* num_proofs, size_t max_num_inputs, const spg_witness_comm* secs, size_t nws,
+                               size_t num_cons, const uint64_t* evals, spg_transcript* transcript, const uint8_t* proof,
+                               size_t proof_len, uint64_t* challenges_out, size_t* ch_lens) {
+  if (!ctx || !transcript) return SPG_E_ARG;
+  spg::HostPin pin;
+  return spg::tr_status(ctx, transcript->t, spg_r1cs_verify_impl(ctx, gens, num_instances, max_num_proofs, num_proofs, max_num_inputs, secs, nws, num_cons, evals, transcript, proof, proof_len, challenges_out, ch_lens));
 }

@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPG_LIB") or os.path.join(_HERE, "lib", "libspg.so")
 
 SPG_ERRORS = {-1: "SPG_E_ARG", -2: "SPG_E_NOMEM", -3: "SPG_E_HIP", -4: "SPG_E_POINT", -5: "SPG_E_NODEVICE",
-              -6: "SPG_E_VERIFY"}
+              -6: "SPG_E_VERIFY", -7: "SPG_E_CALLBACK"}
 
 _lib = None
 
@@ -252,8 +252,16 @@ class Gens:
 
 
 # ---------------------------------------------------------------- Fiat-Shamir objects
+# int (*spg_transcript_append_fn)(void* user, const char* label, const uint8_t* msg, size_t len)
+# int (*spg_transcript_challenge_fn)(void* user, const char* label, uint8_t* out, size_t len)
+TRANSCRIPT_APPEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t)
+TRANSCRIPT_CHALLENGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+                                           ctypes.c_size_t)
+
+
 class Transcript:
-    """ProofTranscript over merlin (src/transcript.rs:5-63), host object in libspg."""
+    """ProofTranscript over merlin (src/transcript.rs:5-63), host object in libspg; or, with from_callbacks, a view
+    of the caller's own transcript (every append_message / challenge_bytes is forwarded to it)."""
 
     def __init__(self, label):
         self._h = ctypes.c_void_p()
@@ -261,14 +269,46 @@ class Transcript:
         if rc != 0:
             raise SpgError(f"spg_transcript_new: {SPG_ERRORS.get(rc, rc)}")
 
+    @classmethod
+    def from_callbacks(cls, append, challenge):
+        """spg_transcript_new_callbacks: append(label: bytes, msg: bytes) and challenge(label: bytes, n) -> n bytes
+        are the caller's merlin append_message / challenge_bytes; an exception in either is a failed callback
+        (the running call returns SPG_E_CALLBACK)."""
+
+        def app(user, label, msg, n):
+            try:
+                append(label, ctypes.string_at(msg, n) if n else b"")
+                return 0
+            except Exception:  # noqa: BLE001 - reported through the return code
+                return 1
+
+        def chal(user, label, out, n):
+            try:
+                b = challenge(label, n)
+                assert len(b) == n
+                if n:
+                    ctypes.memmove(out, b, n)
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        t = cls.__new__(cls)
+        t._cbs = (TRANSCRIPT_APPEND_FN(app), TRANSCRIPT_CHALLENGE_FN(chal))  # keep the thunks alive
+        t._h = ctypes.c_void_p()
+        rc = lib().spg_transcript_new_callbacks(t._cbs[0], t._cbs[1], None, ctypes.byref(t._h))
+        if rc != 0:
+            raise SpgError(f"spg_transcript_new_callbacks: {SPG_ERRORS.get(rc, rc)}")
+        return t
+
     @property
     def handle(self):
         return self._h
 
     def append_message(self, label, msg):
         m = np.frombuffer(bytes(msg), dtype=np.uint8).copy() if msg else np.zeros(1, np.uint8)
-        assert lib().spg_transcript_append_message(self._h, ctypes.c_char_p(bytes(label)), _p(m),
-                                                   ctypes.c_size_t(len(msg))) == 0
+        rc = lib().spg_transcript_append_message(self._h, ctypes.c_char_p(bytes(label)), _p(m), ctypes.c_size_t(len(msg)))
+        if rc != 0:
+            raise SpgError(f"spg_transcript_append_message: {SPG_ERRORS.get(rc, rc)}")
 
     def append_scalar(self, label, s):
         a = _scalars(s)
@@ -281,8 +321,9 @@ class Transcript:
 
     def challenge_bytes(self, label, n):
         out = np.zeros(max(n, 1), dtype=np.uint8)
-        assert lib().spg_transcript_challenge_bytes(self._h, ctypes.c_char_p(bytes(label)), _p(out),
-                                                    ctypes.c_size_t(n)) == 0
+        rc = lib().spg_transcript_challenge_bytes(self._h, ctypes.c_char_p(bytes(label)), _p(out), ctypes.c_size_t(n))
+        if rc != 0:
+            raise SpgError(f"spg_transcript_challenge_bytes: {SPG_ERRORS.get(rc, rc)}")
         return out[:n].tobytes()
 
     def __del__(self):

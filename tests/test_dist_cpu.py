@@ -1,6 +1,7 @@
 """Multi-process path on the CPU (gloo, world_size 2): the allgather adapter that shards R1CSProof::prove
-across ranks (spg.torch_allgather -> spg_set_comm) carries each rank's partial round sums to every rank,
-and the C-side combine (hostcheck's copy of Prover::sum_ranks) adds them exactly mod q."""
+across ranks (spg.torch_allgather -> spg_set_comm) carries each rank's partial round sums to every rank, and
+the product's exchange code (comm.hpp, which api.hip's comm_sum_fq and so Prover::sum_ranks run; exported by
+libspg_hostcheck.so) adds them exactly mod q and fails every rank alike when one rank reports an error."""
 import ctypes
 import os
 import socket
@@ -38,13 +39,18 @@ def _worker(rank, world, port, q):
         mine = rng.integers(0, 2**63, (3, 4), dtype=np.uint64)
         mine[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
         out = np.zeros((3, 4), dtype=np.uint64)
-        rc = hc.spgh_allgather_sum(fn, None, world, mine.ctypes.data_as(ctypes.c_void_p),
-                                   out.ctypes.data_as(ctypes.c_void_p))
+        rc = hc.spgh_comm_sum(fn, None, world, 0, mine.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(3),
+                              out.ctypes.data_as(ctypes.c_void_p))
+        # an error on the last rank only (a local HIP failure, -3): every rank's exchange returns it
+        junk = np.zeros((3, 4), dtype=np.uint64)
+        rc_fail = hc.spgh_comm_sum(fn, None, world, -3 if rank == world - 1 else 0,
+                                   mine.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(3),
+                                   junk.ctypes.data_as(ctypes.c_void_p))
         # raw gather through the same adapter: rank-ordered concatenation
         raw = (ctypes.c_uint8 * (8 * world))()
         send = (ctypes.c_uint8 * 8)(*([rank + 1] * 8))
         rc2 = fn(None, ctypes.addressof(send), 8, ctypes.addressof(raw))
-        q.put((rank, rc, rc2, mine.tolist(), out.tolist(), list(raw)))
+        q.put((rank, rc, rc2, mine.tolist(), out.tolist(), list(raw), rc_fail))
     finally:
         dist.destroy_process_group()
 
@@ -62,8 +68,8 @@ def test_allgather_sum_two_ranks(oracle):
     res.sort()
     parts = [np.array(r[3], dtype=np.uint64) for r in res]
     expect = oracle.fq_op("add", parts[0], parts[1])
-    for rank, rc, rc2, _, out, raw in res:
-        assert rc == 0 and rc2 == 0
+    for rank, rc, rc2, _, out, raw, rc_fail in res:
+        assert rc == 0 and rc2 == 0 and rc_fail == -3
         assert np.array_equal(np.array(out, dtype=np.uint64), expect)
         assert raw == [1] * 8 + [2] * 8
 

@@ -60,3 +60,20 @@ def test_eq_ref_matches_python_integers(oracle):
             ev[i] = s * ri[j] % Q
             ev[i - 1] = (s - ev[i]) % Q
     assert [to_int(x) for x in eq_ref(oracle, r)] == ev
+
+
+@pytest.mark.gpu
+def test_mle_kat_on_device_eq_table(ctx, oracle):
+    """src/dense_mlpoly.rs:1234-1252: Z = [1, 2, 1, 4] evaluated at r = [4, 3] through the device chi table is 28"""
+    import spg
+
+    def m(x):
+        v = x * R % Q
+        return np.array([(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+
+    chi = spg.Buf.eq_evals(ctx, np.stack([m(4), m(3)])).download()
+    Z = np.stack([m(x) for x in (1, 2, 1, 4)])
+    acc = np.zeros(4, np.uint64)
+    for z, c in zip(Z, chi):
+        acc = oracle.fq_op("add", acc, oracle.fq_op("mul", z, c))[0]
+    assert np.array_equal(acc, m(28))

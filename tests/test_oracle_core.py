@@ -192,3 +192,26 @@ def test_commit_rows_matches_msm(oracle):
     rows_b = oracle.commit_rows(pts[:R], pts[R].tobytes(), Z, L, R, bl)
     for i in range(L):
         assert rows_b[i].tobytes() == oracle.msm(pts[: R + 1], np.concatenate([Z[i * R:(i + 1) * R], bl[i:i + 1]]))
+
+
+def test_unipoly_kats(oracle, kat):
+    """src/unipoly.rs:127-181: from_evals of 2x^2+3x+1 and x^3+2x^2+3x+1, their coefficients, the compress /
+    decompress(e0 + e1) round trip and evaluate (at 3 -> 28 for the quadratic, at 4 -> 109 for the cubic)"""
+    for deg in ("quad", "cubic"):
+        evals = [mont(x) for x in kat[f"unipoly_{deg}_evals"]]
+        co, at4, rt = oracle.unipoly(evals, mont(4))
+        assert [val(c) for c in co] == kat[f"unipoly_{deg}_coeffs"]
+        assert np.array_equal(rt, co)
+        assert val(at4) == kat[f"unipoly_{deg}_eval_at_4"]
+        assert val(co[0]) == kat[f"unipoly_{deg}_evals"][0]  # eval_at_zero
+        assert sum(val(c) for c in co) % Q == kat[f"unipoly_{deg}_evals"][1]  # eval_at_one
+    _, at3, _ = oracle.unipoly([mont(x) for x in kat["unipoly_quad_evals"]], mont(3))
+    assert val(at3) == 28  # unipoly.rs:151-152
+
+
+def test_mle_evaluation_kat(oracle, kat):
+    """src/dense_mlpoly.rs:1234-1252 check_polynomial_evaluation: Z = [1, 2, 1, 4], r = [4, 3] -> 28, by evaluate
+    and by evaluate_with_LR (the factored L . Z . R form a Hyrax opening computes)"""
+    ev, ev_lr = oracle.dense_eval([mont(x) for x in kat["mle_Z"]], [mont(x) for x in kat["mle_r"]])
+    assert val(ev) == kat["mle_eval"] == 28
+    assert np.array_equal(ev, ev_lr)

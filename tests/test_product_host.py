@@ -211,3 +211,41 @@ def test_host_radix51_curve_matches_device_form(hc):
     bad = lib.spgh_hcurve_check(uni.ctypes.data_as(ctypes.c_void_p), k.ctypes.data_as(ctypes.c_void_p),
                                 ctypes.c_size_t(n))
     assert bad == 0
+
+
+def _mont(x):
+    R = 2**256
+    v = x * R % Q
+    return np.array([(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+
+
+def _val(m):
+    return sum(int(x) << (64 * i) for i, x in enumerate(m)) * pow(2**256, -1, Q) % Q
+
+
+def test_product_unipoly_kat(hc):
+    """the prover's round polynomial (hostmath.hpp uni_from_evals3 / uni_eval, the code every ZK and SPARK
+    sumcheck round runs) on the reference's cubic KAT, src/unipoly.rs:156-181: evals (1, 7, 23, 55) ->
+    x^3 + 2x^2 + 3x + 1, value 109 at 4; and a random cubic against Lagrange interpolation"""
+    ev = np.stack([_mont(x) for x in (1, 7, 23, 55)])
+    co, at = np.zeros((4, 4), np.uint64), np.zeros(4, np.uint64)
+    hc.spgh_uni_from_evals3(_p(ev), _p(_mont(4)), _p(co), _p(at))
+    assert [_val(c) for c in co] == [1, 3, 2, 1] and _val(at) == 109
+    rng = np.random.default_rng(7)
+    cs = [int(x) for x in rng.integers(0, 2**62, 4)]
+    f = lambda x: sum(c * x**i for i, c in enumerate(cs)) % Q  # noqa: E731
+    ev = np.stack([_mont(f(x)) for x in range(4)])
+    hc.spgh_uni_from_evals3(_p(ev), _p(_mont(11)), _p(co), _p(at))
+    assert [_val(c) for c in co] == cs and _val(at) == f(11)
+
+
+def test_product_mle_kat(hc):
+    """hostmath.hpp dense_eval_host / eq_evals_host on src/dense_mlpoly.rs:1234-1252: Z = [1, 2, 1, 4] at r = [4, 3]
+    is 28; the eq table is big-endian in r (r[0] the most significant index bit, dense_mlpoly.rs:76-92)"""
+    Z = np.stack([_mont(x) for x in (1, 2, 1, 4)])
+    r = np.stack([_mont(4), _mont(3)])
+    out, chis = np.zeros(4, np.uint64), np.zeros((4, 4), np.uint64)
+    hc.spgh_dense_eval(_p(Z), ctypes.c_size_t(4), _p(r), ctypes.c_size_t(2), _p(out), _p(chis))
+    assert _val(out) == 28
+    r0, r1 = 4, 3
+    assert [_val(c) for c in chis] == [(1 - r0) * (1 - r1) % Q, (1 - r0) * r1 % Q, r0 * (1 - r1) % Q, r0 * r1 % Q]

@@ -41,3 +41,54 @@ def test_random_tape_deterministic():
     c = spg.RandomTape(b"proof", workload.tape_seed(b"other"))
     x, y, z = a.random_scalar(b"t1"), b.random_scalar(b"t1"), c.random_scalar(b"t1")
     assert np.array_equal(x, y) and not np.array_equal(x, z)
+
+
+def _oracle_backed(oracle, label, pre=()):
+    """an spg transcript whose state is the caller's (oracle) merlin transcript, after the caller's own appends"""
+    import spg
+
+    t = oracle.OracleTranscript(label)
+    for lbl, msg in pre:
+        t.append_message(lbl, msg)
+    return t, spg.Transcript.from_callbacks(t.append_message, t.challenge_bytes)
+
+
+def test_callback_transcript_continues_caller_state(oracle):
+    """spg_transcript_new_callbacks (SNARK::prove's `&mut Transcript`, src/lib.rs:1022): operations through the
+    handle land in the caller's transcript, interleaved with the caller's own, exactly as one merlin transcript"""
+    import spg
+
+    pre = [(b"caller", b"appended before the call")]
+    back, cb = _oracle_backed(oracle, b"drop-in", pre)
+    ref = spg.Transcript(b"drop-in")
+    for lbl, msg in pre:
+        ref.append_message(lbl, msg)
+    for t in (cb, ref):
+        t.append_message(b"protocol-name", b"Spartan SNARK proof")
+        t.append_scalar(b"num_ios", np.array([1, 2, 3, 4], dtype=np.uint64))
+    assert np.array_equal(cb.challenge_scalar(b"tau"), ref.challenge_scalar(b"tau"))
+    assert cb.challenge_bytes(b"c", 17) == ref.challenge_bytes(b"c", 17)
+    back.append_message(b"caller-after", b"x")  # the caller keeps using its transcript directly
+    ref.append_message(b"caller-after", b"x")
+    assert back.challenge_bytes(b"final", 32) == ref.challenge_bytes(b"final", 32)
+
+
+def test_callback_transcript_failure_is_latched():
+    """a failing callback: that operation and every later one report SPG_E_CALLBACK (challenges read as zero)"""
+    import pytest
+    import spg
+
+    calls = []
+
+    def app(label, msg):
+        calls.append(label)
+        if label == b"bad":
+            raise RuntimeError("caller transcript refused")
+
+    t = spg.Transcript.from_callbacks(app, lambda label, n: b"\x01" * n)
+    t.append_message(b"ok", b"1")
+    with pytest.raises(spg.SpgError, match="SPG_E_CALLBACK"):
+        t.append_message(b"bad", b"2")
+    with pytest.raises(spg.SpgError, match="SPG_E_CALLBACK"):
+        t.challenge_bytes(b"after", 4)
+    assert calls == [b"ok", b"bad"]
