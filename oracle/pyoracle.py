@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "build", "liboracle.so")
 _lib = None
 
 

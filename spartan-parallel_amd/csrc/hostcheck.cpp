@@ -226,3 +226,80 @@ long spgh_pool_stress(int workers, int bursts, int max_n, int delay_us, unsigned
 }
 
 }  // extern "C"
+
+#ifdef SPGH_MAIN
+// TSan driver (make sanitize -> lib/spg_pool_tsan): the pool stress test with its race-window delays, then the
+// cross-rank exchange (comm.hpp) over an in-process allgather between threads, one thread per rank.
+#include <stdio.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+
+namespace {
+struct Barrier {
+  std::mutex mu;
+  std::condition_variable cv;
+  int n, waiting = 0;
+  unsigned gen = 0;
+  explicit Barrier(int k) : n(k) {}
+  void arrive_and_wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    const unsigned g = gen;
+    if (++waiting == n) {
+      waiting = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+struct ThreadComm {  // allgather between `n` threads through one shared buffer and a barrier per phase
+  int n;
+  std::vector<uint8_t> buf;
+  Barrier bar;
+  explicit ThreadComm(int nr) : n(nr), bar(nr) {}
+};
+struct RankUser {
+  ThreadComm* c;
+  int rank;
+};
+int thread_allgather(void* user, const void* send, size_t bytes, void* recv) {
+  RankUser* u = (RankUser*)user;
+  ThreadComm* c = u->c;
+  if (u->rank == 0) c->buf.assign(bytes * c->n, 0);
+  c->bar.arrive_and_wait();
+  memcpy(c->buf.data() + bytes * u->rank, send, bytes);
+  c->bar.arrive_and_wait();
+  memcpy(recv, c->buf.data(), bytes * c->n);
+  c->bar.arrive_and_wait();
+  return 0;
+}
+}  // namespace
+
+int main() {
+  long bad = spgh_pool_stress(7, 300, 64, 0, 1) + spgh_pool_stress(7, 100, 16, 20, 2) + spgh_pool_stress(3, 200, 9, 5, 3);
+  const int n = 4;
+  ThreadComm comm(n);
+  std::vector<std::thread> ts;
+  std::vector<int> rcs(n), fails(n);
+  std::vector<std::vector<uint64_t>> outs(n, std::vector<uint64_t>(12));
+  for (int r = 0; r < n; r++)
+    ts.emplace_back([&, r] {
+      RankUser u{&comm, r};
+      std::vector<uint64_t> mine(12);
+      for (int i = 0; i < 12; i++) mine[i] = (uint64_t)(r + 1) * (i % 4 == 3 ? 1 : 1000003);
+      rcs[r] = spgh_comm_sum(thread_allgather, &u, n, 0, mine.data(), 3, outs[r].data());
+      std::vector<uint64_t> junk(12);
+      fails[r] = spgh_comm_sum(thread_allgather, &u, n, r == 2 ? -3 : 0, mine.data(), 3, junk.data());
+    });
+  for (auto& t : ts) t.join();
+  for (int r = 0; r < n; r++) {
+    bad += rcs[r] != 0 || fails[r] != -3;
+    bad += outs[r] != outs[0];
+  }
+  printf("pool stress + thread exchange: %ld violations\n", bad);
+  return bad ? 1 : 0;
+}
+#endif

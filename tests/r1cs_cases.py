@@ -50,6 +50,8 @@ SNARK_CASES = {
 GPU_SNARK_CASES = {
     "b34_x32_q2": dict(num_blocks=34, log_cons=5, log_proofs=1, num_vars=32),  # > 32 block types (kMaxP)
     "b2_x1024_q8": dict(num_blocks=2, log_cons=10, log_proofs=3, num_vars=1024),
+    # SURVEY 8d config 1 exactly: 2 block types x 2 executions x 2^10 constraints (2^12), num_vars 2^10
+    "b2_x1024_q2": dict(num_blocks=2, log_cons=10, log_proofs=1, num_vars=1024),
     "b2_x256_q64": dict(num_blocks=2, log_cons=8, log_proofs=6, num_vars=256),
     "mem_both_b2_x256_q32": dict(num_blocks=2, log_cons=8, log_proofs=5, num_vars=256, phy_ops=3, vir_ops=2,
                                  init_phy=20, init_vir=7, niu=5),

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HC = os.path.join(ROOT, "spartan-parallel_amd", "lib", "libspg_hostcheck.so")
+HC = os.environ.get("SPG_HOSTCHECK_LIB") or os.path.join(ROOT, "spartan-parallel_amd", "lib", "libspg_hostcheck.so")
 Q = 2**252 + 27742317777372353535851937790883648493
 P = 2**255 - 19
 
