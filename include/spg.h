@@ -62,6 +62,10 @@ int spg_set_comm(spg_ctx* ctx, int rank, int nranks, spg_allgather_fn fn, void* 
  * by those launches as modelled in DESIGN.md, 0 where not modelled); reset != 0 clears the tallies. */
 int spg_prof_enable(spg_ctx* ctx, int on);
 int spg_prof_read(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, int max, int reset);
+/* the same plus the modelled VALU work of those launches in curve mixed additions (ops; 0 where not modelled):
+ * one per nonzero signed window digit of the MSM kernels */
+int spg_prof_read2(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, double* ops, int max,
+                   int reset);
 
 /* ---- device-resident scalar vectors (HBM) ----------------------------------------------------
  * Tables the prover keeps resident between calls (witness polynomials, sumcheck tables). */

@@ -391,7 +391,7 @@ extern "C" {
 // Proves SparseMatPolyEvalProof at (rx, ry) for evals = multi_evaluate(rx, ry) under a fresh
 // Transcript(label) + RandomTape("proof", seed), writes bincode(commitment) and bincode(proof), then runs
 // the verifier on a fresh transcript. Returns 1 if it verifies, 0 if not, <0 on error.
-static double g_spark_prove_us = 0.0;
+static thread_local double g_spark_prove_us = 0.0;
 // wall time of the last orc_spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove (CPU baseline)
 double orc_spark_last_prove_us() { return g_spark_prove_us; }
 
@@ -455,8 +455,8 @@ int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size
 
 namespace {
 using namespace orc;
-double g_snark_verify_us = 0;
-double g_snark_prove_us = 0.0;
+thread_local double g_snark_verify_us = 0;
+thread_local double g_snark_prove_us = 0.0;
 
 SnarkIn snark_in_from_c(const spg_snark_inputs* c) {
   SnarkIn in;

@@ -169,10 +169,11 @@ static inline bool fe_sqrt_ratio_m1(const Fe& u, const Fe& v, const Fe& sqrt_m1,
   return correct || flipped;
 }
 
-static inline const RConsts& rconsts() {
-  static RConsts c;
-  static bool init = false;
-  if (!init) {
+// computed once; the function-local static makes the first use thread-safe (bench.py runs one oracle prove per
+// host core concurrently for the all-cores CPU baseline)
+static inline RConsts rconsts_compute() {
+  RConsts c;
+  {
     // d = -121665/121666
     c.d = fe_mul(fe_neg(fe_small(121665)), fe_invert(fe_small(121666)));
     c.d2 = fe_add(c.d, c.d);
@@ -198,8 +199,11 @@ static inline const RConsts& rconsts() {
     c.one_minus_d_sq = fe_sub(fe_one(), fe_sq(c.d));
     Fe dm1 = fe_sub(c.d, fe_one());
     c.d_minus_one_sq = fe_sq(dm1);
-    init = true;
   }
+  return c;
+}
+static inline const RConsts& rconsts() {
+  static const RConsts c = rconsts_compute();
   return c;
 }
 

@@ -277,11 +277,12 @@ static hipEvent_t pool_event(spg_ctx* c) {
   return e;
 }
 
-KScope::KScope(spg_ctx* ctx, const char* name, double bytes) : c(ctx), idx(-1) {
+KScope::KScope(spg_ctx* ctx, const char* name, double bytes, double ops) : c(ctx), idx(-1) {
   if (!c->prof_on) return;
   spg_ctx::ProfRec r;
   r.name = name;
   r.bytes = bytes;
+  r.ops = ops;
   r.a = pool_event(c);
   r.b = pool_event(c);
   hipEventRecord(r.a, c->stream);
@@ -398,10 +399,10 @@ extern "C" int spg_prof_enable(spg_ctx* c, int on) {
   return SPG_OK;
 }
 
-// Resolves pending kernel timings; writes up to `max` (name, launches, total_us, bytes) records.
+// Resolves pending kernel timings; writes up to `max` (name, launches, total_us, bytes, ops) records.
 // names: max x 32 chars (NUL-terminated). Returns the number of records, or a negative error.
-extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, int max,
-                             int reset) {
+extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, double* ops,
+                              int max, int reset) {
   if (!c) return SPG_E_ARG;
   hipStreamSynchronize(c->stream);
   for (auto& r : c->prof_pending) {
@@ -411,6 +412,7 @@ extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* to
     acc.launches += 1;
     acc.us += ms * 1000.0;
     acc.bytes += r.bytes;
+    acc.ops += r.ops;
     c->ev_pool.push_back(r.a);
     c->ev_pool.push_back(r.b);
   }
@@ -425,10 +427,15 @@ extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* to
     if (launches) launches[k] = kv.second.launches;
     if (total_us) total_us[k] = kv.second.us;
     if (bytes) bytes[k] = kv.second.bytes;
+    if (ops) ops[k] = kv.second.ops;
     k++;
   }
   if (reset) c->prof_acc.clear();
   return k;
+}
+extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, int max,
+                             int reset) {
+  return spg_prof_read2(c, names, launches, total_us, bytes, nullptr, max, reset);
 }
 
 // ---- device-resident scalar vectors ----

@@ -285,6 +285,12 @@ __global__ void __launch_bounds__(64) k_segments(const uint32_t* __restrict__ it
   segS[t] = run;
 }
 
+// the algorithmic work of a fixed-base MSM pass over `scalars` scalars with c-bit signed windows: one mixed
+// addition per nonzero digit, W = 253/c + 1 windows, a digit being zero with probability 2^-c
+static inline double madds_model(double scalars, int c) {
+  return scalars * (double)(253 / c + 1) * (1.0 - 1.0 / (double)(1 << c));
+}
+
 static bool use_quad() {
   static const bool on = !getenv("SPG_SMSM_QUAD") || atoi(getenv("SPG_SMSM_QUAD")) != 0;
   return on;
@@ -613,7 +619,8 @@ int bullet_round_device(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const 
                ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, nullptr};
   *seq_out = a.seq;
   constexpr int C = 7, NB = 1 << (C - 1);
-  KScope ks(ctx, "msm_bullet_round");
+  // VALU model: one mixed addition per nonzero signed 7-bit digit of the L and R MSMs' n/2 scalars each
+  KScope ks(ctx, "msm_bullet_round", 0.0, madds_model(n, C));
   if (n / 2 <= 64)
     hipLaunchKernelGGL((k_bullet_round_q<C, 64>), dim3(NB + 1, 2), dim3(64), 0, ctx->stream, a);
   else if (n / 2 <= 128)
@@ -691,8 +698,8 @@ static void launch_small(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const 
   constexpr int NB = 1 << (C - 1);
   {
     // threads per block = the scalars of one MSM rounded up (a smaller LDS tree and more resident blocks)
-    KScope ks(ctx, "msm_small_bucket");
     const int per = n + (bl ? 1 : 0);
+    KScope ks(ctx, "msm_small_bucket", 0.0, madds_model((double)B * per, C));
     const Fq* blp = bl ? bl : sc;
     if (per <= 64)
       SMSM_LAUNCH(64, sc, idx, blp, bl ? 1 : 0, n, n1, off, h,
@@ -715,8 +722,8 @@ template <int C>
 static void launch_buckets(spg_ctx* ctx, const Fq* sc, const uint32_t* idx, const Fq* bl, int n, int n1, int off, int h,
                            const Niels* tab, Ext* bk, int B, hipStream_t s) {
   constexpr int NB = 1 << (C - 1);
-  KScope ks(ctx, "msm_small_bucket");
   const int per = n + (bl ? 1 : 0);
+  KScope ks(ctx, "msm_small_bucket", 0.0, madds_model((double)B * per, C));
   const Fq* blp = bl ? bl : sc;
   if (per <= 64)
     SMSM_LAUNCH(64, sc, idx, blp, bl ? 1 : 0, n, n1, off, h, tab,
@@ -951,7 +958,7 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
                      (int)nkeys);
   // the item count is only known on the device: launch the upper bound, threads past item_off[nkeys] exit
   {
-    KScope ks(ctx, "msm_bucket_items");
+    KScope ks(ctx, "msm_bucket_items", 0.0, madds_model((double)B * per, c));
     hipLaunchKernelGGL(k_items, dim3((unsigned)((max_items + 255) / 256)), dim3(256), 0, s, item_key, item_off,
                        off, hist, entries, g->table, partial, item_off + nkeys);
   }
@@ -1123,6 +1130,14 @@ extern "C" int spg_gens_free(spg_ctx* ctx, spg_gens* g) {
   return SPG_OK;
 }
 
+// one large MSM (msm_big.hip): sum_i s_i G[gen_offset + i] (+ blind h) of n device scalars into a host point
+int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
+                   const Fq* d_blind, h::HExt* out);
+static bool use_big() {
+  static const bool on = !getenv("SPG_MSM_BIG") || atoi(getenv("SPG_MSM_BIG")) != 0;
+  return on;
+}
+
 static int msm_host(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars, size_t n, size_t B,
                     const uint64_t* blinds, uint8_t* out) {
   if (!ctx || !g || !out || (!scalars && n)) return SPG_E_ARG;
@@ -1141,6 +1156,18 @@ static int msm_host(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const ui
   if (n) SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars, sb, hipMemcpyHostToDevice, s));
   if (blinds) SPG_HIP(ctx, hipMemcpyAsync(d_bl, blinds, B * sizeof(Fq), hipMemcpyHostToDevice, s));
   const bool small = B <= kSmallMaxB && n + (blinds ? 1 : 0) <= kSmallMaxN;
+  if (!small && B == 1 && n && use_big()) {  // one large MSM (config 2): msm_big.hip, encoded on the host
+    h::HExt r;
+    timer_start(ctx);
+    int rc = msm_single_big(ctx, g, gen_offset, d_s, n, d_bl, &r);
+    timer_stop(ctx);
+    if (rc) return rc;
+    h::hext_compress(r, out);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    ctx->last_us = ms * 1000.0;
+    return SPG_OK;
+  }
   Ext* d_ext = small ? (Ext*)ws_get(ctx, 14, B * sizeof(Ext) + 64) : nullptr;
   if (small && !d_ext) return set_err(ctx, SPG_E_NOMEM, "msm output");
   timer_start(ctx);
@@ -1184,6 +1211,21 @@ extern "C" int spg_msm_partial(spg_ctx* ctx, const spg_gens* g, size_t gen_offse
   if (!d_s) return set_err(ctx, SPG_E_NOMEM, "scalar upload");
   Ext* d_ext = (Ext*)(d_s + n);
   SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars_mont, n * sizeof(Fq), hipMemcpyHostToDevice, s));
+  if (n > kSmallMaxN && use_big()) {  // msm_big.hip; the host point's coordinates as canonical bytes
+    h::HExt r;
+    timer_start(ctx);
+    int rc = msm_single_big(ctx, g, gen_offset, d_s, n, nullptr, &r);
+    timer_stop(ctx);
+    if (rc) return rc;
+    h::fe_to_bytes(r.X, out_ext);
+    h::fe_to_bytes(r.Y, out_ext + 32);
+    h::fe_to_bytes(r.Z, out_ext + 64);
+    h::fe_to_bytes(r.T, out_ext + 96);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    ctx->last_us = ms * 1000.0;
+    return SPG_OK;
+  }
   timer_start(ctx);
   int rc = n <= kSmallMaxN ? msm_small_device(ctx, g, gen_offset, d_s, n, 1, nullptr, d_ext, nullptr, -1)
                            : msm_batch_device(ctx, g, gen_offset, d_s, n, 1, nullptr, nullptr, nullptr, -1, d_ext);

@@ -1,0 +1,297 @@
+// spg — one large MSM (GroupElement::vartime_multiscalar_mul, src/group.rs:98-116; Commitments::commit with a
+// blind, src/commitments.rs:87-92) on MI355X: the config-2 shape (2^16 points), spg_msm and the
+// spg_msm_partial shards of an MSM split over GPUs.
+//
+// The batch pipeline of msm.hip sizes its window for many MSMs at once (c = 16 for one 2^16 MSM: 2^15 buckets),
+// and for a single MSM its bucket reduction sum_v v B_v -- a chain of dependent group additions -- dominated
+// (65 % of 604 us). Here the window is chosen for one MSM: c = 12 signed digits (2^11 buckets, 22 windows),
+// fixed-base over the resident 2^k P_i tables (no doublings), and every phase is either throughput-bound with the
+// chip full or a short dependent chain:
+//   k_big_digits   block-local LDS histograms of the signed digits (digits kept in HBM as int16)
+//   hipcub scan    over the [bucket][block] histogram matrix: each (bucket, block) pair's entry range
+//   k_big_scatter  counting-sort scatter of (table index | sign) into bucket order, LDS cursors
+//   k_big_chunks   one workgroup's work list: bucket v split into chunks of <= CH entries (skewed scalars only
+//                  lengthen the list, never a workgroup)
+//   k_big_accum    one workgroup per chunk: 64 quads (4 lanes per point, quad.hpp) each add ~CH/64 table entries,
+//                  then an LDS tree -> the chunk's sum
+//   k_big_groups   one workgroup per 64 consecutive buckets: bucket sums from their chunks, a suffix scan and a tree
+//                  give W_g = sum_j (j + 1) B_{64 g + j} and G_g = sum_j B_{64 g + j}
+//   host           sum_v v B_v = sum_g W_g + 64 sum_g g G_g over the NB/64 groups (radix-2^51 additions at ~0.1 us
+//                  each on a host core, where one dependent GPU addition costs ~2 us), then the encoding.
+#include <hipcub/hipcub.hpp>
+
+#include "ctx.hpp"
+#include "hcurve.hpp"
+#include "quad.hpp"
+
+namespace spg {
+
+namespace {
+
+constexpr int kBigBS = 256;      // threads per workgroup (64 quads)
+constexpr int kBigQuads = kBigBS / 4;
+constexpr int kBigGroup = 64;    // buckets per k_big_groups workgroup
+
+struct BigArgs {
+  const Fq* scalars;
+  const Fq* blind;  // scalar n when per = n + 1; always a valid pointer (a wave-uniform load may be issued as a
+                    // scalar load ahead of its branch, which EXEC does not mask)
+  int n, per;       // per = n (+1 with a blind)
+  int gen_offset, h_index, n1;
+  int G, spb;       // digit blocks, scalars per block
+  int16_t* digits;  // [W][per]
+  uint32_t* bh;     // [NB][G] block histograms (+ a zero at [NB * G])
+  uint32_t* off;    // their exclusive scan: the entry range of each (bucket, block); off[NB * G] = total
+  uint32_t* entries;
+};
+
+template <int C>
+__global__ void __launch_bounds__(kBigBS) k_big_digits(BigArgs a) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  __shared__ uint32_t cnt[NB];
+  const int blk = blockIdx.x, t = threadIdx.x;
+  for (int k = t; k < NB; k += kBigBS) cnt[k] = 0;
+  __syncthreads();
+  const int i0 = blk * a.spb, i1 = min(a.per, i0 + a.spb);
+  for (int i = i0 + t; i < i1; i += kBigBS) {
+    const Fq k = fq_from_mont(i < a.n ? a.scalars[i] : a.blind[0]);  // Scalar::to_bytes (src/scalar/mod.rs:32-36)
+    int carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int bit = w * C, li = bit >> 5, of = bit & 31;
+      uint32_t v = k.l[li] >> of;
+      if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+      int d = (int)(v & MASK) + carry;
+      carry = d > NB ? 1 : 0;
+      d -= carry << C;
+      a.digits[(size_t)w * a.per + i] = (int16_t)d;
+      if (d) atomicAdd(&cnt[(d < 0 ? -d : d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = t; k < NB; k += kBigBS) a.bh[(size_t)k * a.G + blk] = cnt[k];
+  if (blk == 0 && t == 0) a.bh[(size_t)NB * a.G] = 0;
+}
+
+template <int C>
+__global__ void __launch_bounds__(kBigBS) k_big_scatter(BigArgs a) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  __shared__ uint32_t cur[NB];
+  const int blk = blockIdx.x, t = threadIdx.x;
+  for (int k = t; k < NB; k += kBigBS) cur[k] = a.off[(size_t)k * a.G + blk];
+  __syncthreads();
+  const int i0 = blk * a.spb, i1 = min(a.per, i0 + a.spb);
+  for (int i = i0 + t; i < i1; i += kBigBS) {
+    const uint32_t gidx = i < a.n ? (uint32_t)(a.gen_offset + i) : (uint32_t)a.h_index;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int d = a.digits[(size_t)w * a.per + i];
+      if (d) {
+        const uint32_t slot = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+        a.entries[slot] = ((uint32_t)(w * C) * (uint32_t)a.n1 + gidx) | (d < 0 ? 0x80000000u : 0u);
+      }
+    }
+  }
+}
+
+struct Chunk {
+  uint32_t key, start, len, pad;
+};
+
+// one 1024-thread block: bucket v = key + 1 holds entries [bh[key G], bh[(key + 1) G]); it becomes
+// ceil(count / ch) chunks; first[key] = its first chunk, first[NB] = the number of chunks
+__global__ void __launch_bounds__(1024) k_big_chunks(const uint32_t* __restrict__ bh, int G, int NB, uint32_t ch,
+                                                     Chunk* __restrict__ chunks, uint32_t* __restrict__ first) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int per_t = (NB + 1023) / 1024, k0 = t * per_t, k1 = min(NB, k0 + per_t);
+  uint32_t mine = 0;
+  for (int k = k0; k < k1; k++) {
+    const uint32_t c = bh[(size_t)(k + 1) * G] - bh[(size_t)k * G];
+    mine += (c + ch - 1) / ch;
+  }
+  part[t] = mine;
+  __syncthreads();
+  for (int s = 1; s < 1024; s <<= 1) {  // inclusive Hillis-Steele scan of the per-thread chunk counts
+    const uint32_t x = t >= s ? part[t - s] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - mine;
+  for (int k = k0; k < k1; k++) {
+    const uint32_t s = bh[(size_t)k * G], c = bh[(size_t)(k + 1) * G] - s;
+    first[k] = run;
+    for (uint32_t o = 0; o < c; o += ch) chunks[run++] = Chunk{(uint32_t)k, s + o, min(ch, c - o), 0u};
+  }
+  if (t == 1023) first[NB] = part[1023];
+}
+
+// one workgroup (64 quads) per chunk; grid = an upper bound of the chunk count
+__global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ chunks,
+                                                      const uint32_t* __restrict__ nchunks,
+                                                      const uint32_t* __restrict__ entries,
+                                                      const Niels* __restrict__ tab, Ext* __restrict__ sums) {
+  __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
+  const uint32_t cid = blockIdx.x;
+  if (cid >= *nchunks) return;  // whole workgroups exit together
+  const int t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const Chunk c = chunks[cid];
+  Ext acc = ext_identity();
+  // software-pipelined: the table coordinate of entry e + 64 is loaded while entry e is added
+  uint32_t e = slot;
+  Fp qv;
+  bool neg = false;
+  if (e < c.len) qv = niels_coord(tab, entries[c.start + e], q, &neg);
+  while (e < c.len) {
+    const uint32_t e2 = e + kBigQuads;
+    Fp qn;
+    bool nn = false;
+    if (e2 < c.len) qn = niels_coord(tab, entries[c.start + e2], q, &nn);
+    acc = quad_madd(acc, qv, neg, q);
+    qv = qn;
+    neg = nn;
+    e = e2;
+  }
+  for (int d = kBigQuads / 2; d >= 1; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put_op<kBigQuads>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<kBigQuads>(pts, slot, q), q);
+    __syncthreads();
+  }
+  if (t == 0) sums[cid] = acc;
+}
+
+// one workgroup (64 quads) per group g of 64 buckets: quad j holds B = bucket 64 g + j + 1 (its chunks summed);
+// the suffix scan S_j = sum_{u >= j} B_u and the tree sum_j S_j = sum_j (j + 1) B_j; out[2 g] = that weighted
+// sum, out[2 g + 1] = S_0 = the group's plain sum
+__global__ void __launch_bounds__(kBigBS) k_big_groups(const Ext* __restrict__ sums, const uint32_t* __restrict__ first,
+                                                       Ext* __restrict__ out) {
+  __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
+  const int t = threadIdx.x, q = t & 3, slot = t >> 2, g = blockIdx.x;
+  const int key = g * kBigGroup + slot;
+  Ext B = ext_identity();
+  bool any = false;
+  for (uint32_t c = first[key]; c < first[key + 1]; c++) {
+    B = any ? quad_add(B, sums[c], q) : sums[c];
+    any = true;
+  }
+  Ext suf = B;
+  for (int d = 1; d < kBigQuads; d <<= 1) {
+    quad_put_op<kBigQuads>(pts, slot, suf, q);
+    __syncthreads();
+    if (slot + d < kBigQuads) suf = quad_add_op(suf, quad_get_op<kBigQuads>(pts, slot + d, q), q);
+    __syncthreads();
+  }
+  if (slot == 0 && q == 0) out[2 * g + 1] = suf;
+  Ext acc = suf;
+  for (int d = kBigQuads / 2; d >= 1; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put_op<kBigQuads>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<kBigQuads>(pts, slot, q), q);
+    __syncthreads();
+  }
+  if (t == 0) out[2 * g] = acc;
+}
+
+int big_window() {
+  static const int c = getenv("SPG_BIG_C") ? atoi(getenv("SPG_BIG_C")) : 12;
+  return c < 8 ? 8 : (c > 14 ? 14 : c);
+}
+
+template <int C>
+int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev, int* ngroups) {
+  constexpr int W = 253 / C + 1;
+  constexpr int NB = 1 << (C - 1);
+  hipStream_t s = ctx->stream;
+  const size_t E = (size_t)a.per * W;
+  // chunk size: the mean bucket load rounded up to whole passes of the 64 quads (random scalars: about one chunk
+  // per bucket), at least 2 entries per quad
+  const uint32_t ch = (uint32_t)std::max<size_t>(2 * kBigQuads, ((E / NB + kBigQuads - 1) / kBigQuads + 1) * kBigQuads);
+  const size_t max_chunks = E / ch + NB + 1;
+  a.digits = (int16_t*)ws_get(ctx, 20, E * sizeof(int16_t) + 64);
+  a.bh = (uint32_t*)ws_get(ctx, 21, ((size_t)NB * a.G + 1) * 4 + 64);
+  a.off = (uint32_t*)ws_get(ctx, 27, ((size_t)NB * a.G + 1) * 4 + 64);
+  a.entries = (uint32_t*)ws_get(ctx, 22, E * 4 + 64);
+  Chunk* chunks = (Chunk*)ws_get(ctx, 23, max_chunks * sizeof(Chunk));
+  uint32_t* first = (uint32_t*)ws_get(ctx, 24, (NB + 1) * 4 + 64);
+  Ext* sums = (Ext*)ws_get(ctx, 25, max_chunks * sizeof(Ext));
+  if (!a.digits || !a.bh || !a.off || !a.entries || !chunks || !first || !sums) return set_err(ctx, SPG_E_NOMEM, "msm workspace");
+  const int nkeys = NB * a.G + 1;
+  size_t tmp_bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, a.bh, a.off, nkeys, s);
+  void* tmp = ws_get(ctx, 26, tmp_bytes + 16);
+  if (!tmp) return set_err(ctx, SPG_E_NOMEM, "msm scan workspace");
+  {
+    KScope ks(ctx, "msm_big_sort");
+    hipLaunchKernelGGL(k_big_digits<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
+    SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, a.bh, a.off, nkeys, s));
+    hipLaunchKernelGGL(k_big_scatter<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
+    hipLaunchKernelGGL(k_big_chunks, dim3(1), dim3(1024), 0, s, a.off, a.G, NB, ch, chunks, first);
+  }
+  {
+    KScope ks(ctx, "msm_big_accum", 0.0, (double)a.per * W * (1.0 - 1.0 / (double)(1 << C)));
+    hipLaunchKernelGGL(k_big_accum, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first + NB, a.entries,
+                       g->table, sums);
+  }
+  {
+    KScope ks(ctx, "msm_big_groups");
+    hipLaunchKernelGGL(k_big_groups, dim3(NB / kBigGroup), dim3(kBigBS), 0, s, sums, first, host_groups_dev);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  *ngroups = NB / kBigGroup;
+  return 0;
+}
+
+}  // namespace
+
+// sum_i s_i G[gen_offset + i] (+ blind h) of n device scalars, into *out (host point)
+int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
+                   const Fq* d_blind, h::HExt* out) {
+  const int c = big_window();
+  const int per = (int)n + (d_blind ? 1 : 0);
+  SPG_CHECK(ctx, n >= 1 && (size_t)per * (253 / c + 1) < 0x7fffffffULL, "msm too large");
+  SPG_CHECK(ctx, (size_t)kTableRows * (g->n + 1) < 0x7fffffffULL, "generator table too large");
+  BigArgs a{};
+  a.scalars = d_scalars;
+  a.blind = d_blind ? d_blind : d_scalars;
+  a.n = (int)n;
+  a.per = per;
+  a.gen_offset = (int)gen_offset;
+  a.h_index = (int)g->n;
+  a.n1 = (int)(g->n + 1);
+  // digit blocks: about 4 scalars per thread, at most 512 blocks (the histogram matrix is NB x G)
+  a.G = std::max(1, std::min(512, (per + 4 * kBigBS - 1) / (4 * kBigBS)));
+  a.spb = (per + a.G - 1) / a.G;
+  int ng = 0, rc = 0;
+  Ext* res = (Ext*)ctx->d_res;  // the coherent result page: 2 NB / 64 points (<= 256 at c = 14)
+  static_assert(kResScalars * sizeof(Fq) >= 2 * (1 << 13) / kBigGroup * sizeof(Ext), "result page too small");
+  switch (c) {
+    case 8: rc = launch_big<8>(ctx, g, a, res, &ng); break;
+    case 9: rc = launch_big<9>(ctx, g, a, res, &ng); break;
+    case 10: rc = launch_big<10>(ctx, g, a, res, &ng); break;
+    case 11: rc = launch_big<11>(ctx, g, a, res, &ng); break;
+    case 12: rc = launch_big<12>(ctx, g, a, res, &ng); break;
+    case 13: rc = launch_big<13>(ctx, g, a, res, &ng); break;
+    default: rc = launch_big<14>(ctx, g, a, res, &ng); break;
+  }
+  if (rc) return rc;
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // sum_v v B_v = sum_g W_g + 64 sum_g g G_g, with sum_g g G_g = sum_{g >= 1} sum_{h >= g} G_h
+  const Ext* r = (const Ext*)ctx->res;
+  h::HExt wsum = h::hext_from_dev(r[0]), S = h::hext_identity(), T = h::hext_identity();
+  for (int gi = ng - 1; gi >= 1; gi--) {
+    wsum = h::hext_add(wsum, h::hext_from_dev(r[2 * gi]));
+    S = h::hext_add(S, h::hext_from_dev(r[2 * gi + 1]));
+    T = h::hext_add(T, S);
+  }
+  for (int k = 0; k < 6; k++) T = h::hext_dbl(T);  // x 64 = kBigGroup
+  static_assert(kBigGroup == 64, "six doublings");
+  *out = h::hext_add(wsum, T);
+  return 0;
+}
+
+}  // namespace spg

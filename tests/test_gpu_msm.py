@@ -152,3 +152,63 @@ def test_commit_rows_wide(ctx, oracle):
     Z = rand_fq(oracle, np.random.default_rng(14), L * R)
     Z[5 * R: 6 * R] = 0
     assert np.array_equal(g.commit_rows(Z, L, R), oracle.commit_rows(pts[:R], pts[R].tobytes(), Z, L, R))
+
+
+@pytest.fixture(scope="module")
+def gens_big(ctx):
+    import spg
+
+    return spg.Gens(ctx, 20000, b"spg_big_msm")
+
+
+def test_msm_big_edge_and_skew(ctx, oracle, gens_big):
+    """one MSM larger than the latency path (msm_big.hip): edge scalars, an all-zero stretch, a bucket holding most
+    entries (one scalar repeated: its digits pile into a few buckets, which split into many chunks), a blind, and
+    a generator offset, against the oracle"""
+    n = 20000
+    pts = gens_big.compressed()
+    rng = np.random.default_rng(20000)
+    s = rand_fq(oracle, rng, n)
+    one = oracle.fq_from_u64(1)
+    edge = [np.zeros(4, np.uint64), one[0], oracle.fq_from_u64(2)[0], oracle.fq_op("neg", one)[0],
+            oracle.fq_from_raw([0, 0, 0, 1 << 60]), oracle.fq_from_raw([2**64 - 1, 2**64 - 1, 2**64 - 1, (1 << 60) - 1])]
+    for i, e in enumerate(edge):
+        s[i] = e
+    s[100:400] = 0
+    assert gens_big.msm(s) == oracle.msm(pts[:n], s), "edge"
+    skew = np.tile(s[9], (n, 1))
+    skew[::7] = s[::7]
+    assert gens_big.msm(skew) == oracle.msm(pts[:n], skew), "skewed"
+    bl = rand_fq(oracle, rng, 1)
+    exp = oracle.msm(np.concatenate([pts[:n], pts[n:n + 1]]), np.concatenate([s, bl]))
+    assert gens_big.msm(s, blind=bl) == exp, "blind"
+    m = n - 1500
+    assert gens_big.msm(s[:m], gen_offset=1500) == oracle.msm(pts[1500:n], s[:m]), "offset"
+    zeros = np.zeros((n, 4), np.uint64)
+    assert gens_big.msm(zeros) == bytes(32), "identity"
+
+
+@pytest.mark.parametrize("c", ["8", "10", "13", "14"])
+def test_msm_big_windows(oracle, c):
+    """every window width of the large-MSM path (SPG_BIG_C, a fresh process reads it) gives the oracle's 2^16 MSM"""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 1 << 16
+    code = (
+        "import sys, numpy as np; sys.path[:0] = [%r, %r]\n"
+        "import spg, pyoracle\n"
+        "ctx = spg.Context(0)\n"
+        "g = spg.Gens(ctx, %d, b'spg_bench_msm')\n"
+        "rng = np.random.default_rng(%s)\n"
+        "s = pyoracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * %d, dtype=np.uint8).tobytes())\n"
+        "print(g.msm(s).hex())\n"
+    ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "oracle"), n, c, n)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_C=c), capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rng = np.random.default_rng(int(c))
+    s = rand_fq(oracle, rng, n)
+    pts = oracle.gens_stream(b"spg_bench_msm", n + 1)
+    assert out.stdout.split()[-1] == oracle.msm(pts[:n], s).hex()
