@@ -56,6 +56,15 @@ double spg_last_kernel_us(const spg_ctx* ctx);
  * allgather, e.g. RCCL / torch.distributed); it returns 0 on success. nranks == 1 clears it. */
 typedef int (*spg_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
 int spg_set_comm(spg_ctx* ctx, int rank, int nranks, spg_allgather_fn fn, void* user);
+/* The same with libspg's own transport: RCCL (librccl.so.1, opened at first use) on the context's stream, one
+ * process per GPU; no caller code runs per exchange. Rank 0 makes the 128-byte id with spg_rccl_unique_id and
+ * hands it to every rank by any channel of the caller's (e.g. a torch.distributed broadcast); every rank then calls
+ * spg_set_comm_rccl (collective: it returns once all nranks have joined). An exchange that a dead peer never
+ * completes fails after 120 s (the communicator is aborted) instead of hanging. */
+int spg_rccl_unique_id(uint8_t id[128]);
+int spg_set_comm_rccl(spg_ctx* ctx, const uint8_t id[128], int rank, int nranks);
+/* one allgather over the context's transport (callback or RCCL): the `bytes` of rank k land at recv + k*bytes */
+int spg_comm_allgather(spg_ctx* ctx, const void* send, size_t bytes, void* recv);
 
 /* per-kernel timing on the context stream (events; off by default). spg_prof_read resolves them and
  * returns up to `max` records (name[32], launches, total microseconds, algorithmic HBM bytes moved

@@ -340,6 +340,7 @@ extern "C" int spg_free(spg_ctx* c) {
   if (!c) return SPG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  if (c->comm_owned_free) c->comm_owned_free(c->comm_owned);
   for (auto& s : c->ws)
     if (s.p) hipFree(s.p);
   if (c->pinned) hipHostFree(c->pinned);
@@ -359,6 +360,9 @@ extern "C" double spg_last_kernel_us(const spg_ctx* c) { return c ? c->last_us :
 
 extern "C" int spg_set_comm(spg_ctx* c, int rank, int nranks, spg_allgather_fn fn, void* user) {
   if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return SPG_E_ARG;
+  if (c->comm_owned_free) c->comm_owned_free(c->comm_owned);
+  c->comm_owned = nullptr;
+  c->comm_owned_free = nullptr;
   c->rank = rank;
   c->nranks = nranks;
   c->allgather = fn;

@@ -37,6 +37,9 @@ struct spg_ctx {
   int rank = 0, nranks = 1;
   spg_allgather_fn allgather = nullptr;
   void* comm_user = nullptr;
+  // a transport the library owns (spg_set_comm_rccl), released by the next spg_set_comm* or spg_free
+  void* comm_owned = nullptr;
+  void (*comm_owned_free)(void*) = nullptr;
   double last_us = 0.0;
   std::string err;
   // workspace slots: grown on demand, reused across calls (no allocation in steady state)

@@ -1130,9 +1130,11 @@ extern "C" int spg_gens_free(spg_ctx* ctx, spg_gens* g) {
   return SPG_OK;
 }
 
+namespace spg {
 // one large MSM (msm_big.hip): sum_i s_i G[gen_offset + i] (+ blind h) of n device scalars into a host point
 int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
                    const Fq* d_blind, h::HExt* out);
+}  // namespace spg
 static bool use_big() {
   static const bool on = !getenv("SPG_MSM_BIG") || atoi(getenv("SPG_MSM_BIG")) != 0;
   return on;

@@ -28,6 +28,7 @@ namespace spg {
 
 namespace {
 
+// workspace slots 100..107 (msm.hip 0..18, proto.hip 20..24, r1cs.hip 30.., spark.hip 60.., snark / verify 91..96)
 constexpr int kBigBS = 256;      // threads per workgroup (64 quads)
 constexpr int kBigQuads = kBigBS / 4;
 constexpr int kBigGroup = 64;    // buckets per k_big_groups workgroup
@@ -212,18 +213,18 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
   // per bucket), at least 2 entries per quad
   const uint32_t ch = (uint32_t)std::max<size_t>(2 * kBigQuads, ((E / NB + kBigQuads - 1) / kBigQuads + 1) * kBigQuads);
   const size_t max_chunks = E / ch + NB + 1;
-  a.digits = (int16_t*)ws_get(ctx, 20, E * sizeof(int16_t) + 64);
-  a.bh = (uint32_t*)ws_get(ctx, 21, ((size_t)NB * a.G + 1) * 4 + 64);
-  a.off = (uint32_t*)ws_get(ctx, 27, ((size_t)NB * a.G + 1) * 4 + 64);
-  a.entries = (uint32_t*)ws_get(ctx, 22, E * 4 + 64);
-  Chunk* chunks = (Chunk*)ws_get(ctx, 23, max_chunks * sizeof(Chunk));
-  uint32_t* first = (uint32_t*)ws_get(ctx, 24, (NB + 1) * 4 + 64);
-  Ext* sums = (Ext*)ws_get(ctx, 25, max_chunks * sizeof(Ext));
+  a.digits = (int16_t*)ws_get(ctx, 100, E * sizeof(int16_t) + 64);
+  a.bh = (uint32_t*)ws_get(ctx, 101, ((size_t)NB * a.G + 1) * 4 + 64);
+  a.off = (uint32_t*)ws_get(ctx, 102, ((size_t)NB * a.G + 1) * 4 + 64);
+  a.entries = (uint32_t*)ws_get(ctx, 103, E * 4 + 64);
+  Chunk* chunks = (Chunk*)ws_get(ctx, 104, max_chunks * sizeof(Chunk));
+  uint32_t* first = (uint32_t*)ws_get(ctx, 105, (NB + 1) * 4 + 64);
+  Ext* sums = (Ext*)ws_get(ctx, 106, max_chunks * sizeof(Ext));
   if (!a.digits || !a.bh || !a.off || !a.entries || !chunks || !first || !sums) return set_err(ctx, SPG_E_NOMEM, "msm workspace");
   const int nkeys = NB * a.G + 1;
   size_t tmp_bytes = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, a.bh, a.off, nkeys, s);
-  void* tmp = ws_get(ctx, 26, tmp_bytes + 16);
+  void* tmp = ws_get(ctx, 107, tmp_bytes + 16);
   if (!tmp) return set_err(ctx, SPG_E_NOMEM, "msm scan workspace");
   {
     KScope ks(ctx, "msm_big_sort");

@@ -94,6 +94,35 @@ class Context:
         fn = allgather_fn if allgather_fn is not None else ctypes.cast(None, ALLGATHER_FN)
         self.check(lib().spg_set_comm(self._h, ctypes.c_int(rank), ctypes.c_int(nranks), fn, None), "spg_set_comm")
 
+    def set_comm_rccl(self, rank, nranks, dist=None, unique_id=None):
+        """spg_set_comm_rccl: libspg's own RCCL transport on the context stream. Rank 0's 128-byte id
+        (spg_rccl_unique_id) reaches every rank through `dist` (torch.distributed broadcast_object_list over the
+        default group) unless unique_id is given."""
+        if unique_id is None:
+            buf = (ctypes.c_uint8 * 128)()
+            if rank == 0:
+                rc = lib().spg_rccl_unique_id(buf)
+                if rc != 0:
+                    raise SpgError(f"spg_rccl_unique_id: {SPG_ERRORS.get(rc, rc)}")
+            if nranks > 1:
+                obj = [bytes(buf) if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                unique_id = obj[0]
+            else:
+                unique_id = bytes(buf)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._comm = None
+        self.check(lib().spg_set_comm_rccl(self._h, uid, ctypes.c_int(rank), ctypes.c_int(nranks)), "spg_set_comm_rccl")
+
+    def comm_allgather(self, data, nranks):
+        """spg_comm_allgather over the context's transport: every rank's `data` (equal lengths), rank-ordered"""
+        n = len(data)
+        src = (ctypes.c_uint8 * max(n, 1)).from_buffer_copy(bytes(data) or b"\0")
+        dst = (ctypes.c_uint8 * max(n * nranks, 1))()
+        self.check(lib().spg_comm_allgather(self._h, src, ctypes.c_size_t(n), dst), "spg_comm_allgather")
+        raw = bytes(dst)
+        return [raw[k * n:(k + 1) * n] for k in range(nranks)]
+
     def last_kernel_us(self):
         return lib().spg_last_kernel_us(self._h)
 
