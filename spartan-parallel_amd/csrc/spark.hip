@@ -563,12 +563,19 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
   FqV rand;
   Laps lp;
   lp.title = "ProductCircuitEvalProofBatched::prove";
+  // W > 1: a failure on this rank alone (allocation, HIP, mailbox) is not returned at once -- the peers would wait
+  // in the next exchange. The rank stops working (`fail`, skip mode) but keeps the exchange sequence, whose
+  // shape depends only on public sizes, until its status reaches every rank: in the next sharded round's
+  // exchange, or in the status exchange that ends the function. A failure learned in an exchange is known to
+  // every rank (`shared`) and returns at once.
+  int fail = 0;
+  bool shared = false;
   for (size_t layer = L; layer-- > 0;) {
     const size_t half = M >> (layer + 1);  // |left| = |right| = |C| (global)
     // where this layer's vectors live: local shares (sharded), the replicated top tree, or the whole tree
     const bool sharded = W > 1 && layer < lgm;
     const size_t hl = sharded ? half / W : half;  // entries of each vector held here
-    int rc = 0;
+    int rc = fail;
     int cur = 0;  // the buffer holding the shared eq vector C
     const bool with_dotp = layer == 0 && !dotp.empty();
     std::vector<Triple> tr;
@@ -593,15 +600,21 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       memcpy(blob.w, tr.data(), tr.size() * sizeof(Triple));
       memcpy((uint8_t*)blob.w + tr_bytes, coeffs.data(), coeffs.size() * sizeof(Fq));
       blob.nwords = (int)(blob_bytes / 4);
-    } else {  // free again here (the previous layer ended with a mailbox wait after its last launch)
+    } else if (!rc) {  // free again here (the previous layer ended with a mailbox wait after its last launch)
       uint8_t* st = (uint8_t*)pinned_get(ctx, blob_bytes + 64);
-      if (!st) return set_err(ctx, SPG_E_NOMEM, "layer staging");
-      memcpy(st, tr.data(), tr.size() * sizeof(Triple));
-      memcpy(st + tr_bytes, coeffs.data(), coeffs.size() * sizeof(Fq));
-      SPG_HIP(ctx, hipMemcpyAsync(ddesc, st, blob_bytes, hipMemcpyHostToDevice, s));
+      if (!st) {
+        rc = set_err(ctx, SPG_E_NOMEM, "layer staging");
+      } else {
+        memcpy(st, tr.data(), tr.size() * sizeof(Triple));
+        memcpy(st + tr_bytes, coeffs.data(), coeffs.size() * sizeof(Fq));
+        if (hipMemcpyAsync(ddesc, st, blob_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+          rc = set_err(ctx, SPG_E_HIP, "layer descriptors upload");
+      }
     }
     const KBlob* bp = in_args ? &blob : nullptr;
-    if (sharded) {  // local eq share: eq(rand)[W i' + r] = eq(rand_hi)[i'] * eq(rand_lo)[r]
+    if (rc) {
+      // skip mode: no device work this layer
+    } else if (sharded) {  // local eq share: eq(rand)[W i' + r] = eq(rand_hi)[i'] * eq(rand_lo)[r]
       const size_t nh = rand.size() - lgW;
       rc = dev_eq_table(ctx, rand.data(), (int)nh, cbuf[0], bp, ddesc);
       Fq sc = fq_one();
@@ -611,7 +624,7 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     } else {
       rc = dev_eq_table(ctx, rand.data(), (int)rand.size(), cbuf[0], bp, ddesc);
     }
-    if (rc) return rc;
+    if (rc && W == 1) return rc;
     lp.lap("layer_setup");
     LayerProofP lpf;
     FqV r_prod;
@@ -642,7 +655,13 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks; with
     // close_after the layer's (or the shard's) final entries follow in `fin`
     static const bool ends_on = !getenv("SPG_LAYER_ENDS") || atoi(getenv("SPG_LAYER_ENDS")) != 0;
-    auto run_rounds = [&](size_t log_len, bool local, bool close_after, FqV* fin) -> int {
+    auto run_rounds = [&](size_t log_len, bool local, bool close_after, FqV* fin, int status) -> int {
+      if (status) {  // skip mode: the first local round's exchange carries the failure to every rank
+        if (!local || log_len == 0) return status;
+        Fq none[3] = {fq_zero(), fq_zero(), fq_zero()};
+        shared = true;
+        return comm_sum_fq(ctx, sh, status, none, 3);
+      }
       while (log_len > 0) {
         log_len--;
         const size_t len = (size_t)1 << log_len;
@@ -689,10 +708,14 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
                                cbuf[cur ^ 1], part, ctx->d_counter, ctx->d_mbox, seq, nullptr);
         }
         if (pending) cur ^= 1;
-        SPG_HIP(ctx, hipGetLastError());
         FqV ev(ends ? 3 + 6 * tr.size() : 3);
-        int rc2 = mbox_wait(ctx, ctx->mbox_seq, ev.data(), (int)ev.size());
-        if (local) rc2 = comm_sum_fq(ctx, sh, rc2, ev.data(), 3);
+        const hipError_t le = hipGetLastError();
+        int rc2 = le != hipSuccess ? set_err(ctx, SPG_E_HIP, std::string("layer round: ") + hipGetErrorString(le))
+                                   : mbox_wait(ctx, ctx->mbox_seq, ev.data(), (int)ev.size());
+        if (local) {
+          rc2 = comm_sum_fq(ctx, sh, rc2, ev.data(), 3);
+          if (rc2) shared = true;
+        }
         if (rc2) return rc2;
         lp.lap("round_eval_wait");
         r_pend = host_round(ev.data());
@@ -714,33 +737,42 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     if (sharded) {
       // gather: every vector has one entry per rank left; rank q's entry is global index q
       FqV mine;
-      rc = run_rounds(lg2(hl), true, true, &mine);
+      rc = run_rounds(lg2(hl), true, true, &mine, rc);
+      if (rc && shared) return rc;
       mine.resize(3 * tr.size(), fq_zero());
       std::vector<uint8_t> all;
       rc = comm_allgather(ctx, sh, rc, mine.data(), 3 * tr.size() * sizeof(Fq), all);
-      if (rc) return rc;
+      if (rc) return rc;  // known to every rank
       const Fq* g = (const Fq*)all.data();
       const size_t nt = tr.size();
       uint8_t* st = (uint8_t*)pinned_get(ctx, 3 * nt * W * sizeof(Fq) + tr_bytes + 64);
-      if (!st) return set_err(ctx, SPG_E_NOMEM, "gather staging");
-      Fq* hv = (Fq*)(st + tr_bytes);
-      for (size_t c = 0; c < nt; c++)
-        for (size_t k = 0; k < 3; k++)
-          for (size_t q = 0; q < W; q++) hv[(3 * c + k) * W + q] = g[q * 3 * nt + 3 * c + k];
-      for (size_t c = 0; c < nt; c++) {
-        const bool own_c = tr[c].C != nullptr;
-        tr[c] = {gbuf + 3 * c * W, gbuf + (3 * c + 1) * W, own_c ? gbuf + (3 * c + 2) * W : nullptr};
+      if (!st) {
+        rc = set_err(ctx, SPG_E_NOMEM, "gather staging");
+      } else {
+        Fq* hv = (Fq*)(st + tr_bytes);
+        for (size_t c = 0; c < nt; c++)
+          for (size_t k = 0; k < 3; k++)
+            for (size_t q = 0; q < W; q++) hv[(3 * c + k) * W + q] = g[q * 3 * nt + 3 * c + k];
+        for (size_t c = 0; c < nt; c++) {
+          const bool own_c = tr[c].C != nullptr;
+          tr[c] = {gbuf + 3 * c * W, gbuf + (3 * c + 1) * W, own_c ? gbuf + (3 * c + 2) * W : nullptr};
+        }
+        memcpy(st, tr.data(), nt * sizeof(Triple));
+        if (hipMemcpyAsync(ddesc, st, nt * sizeof(Triple), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(gbuf, hv, 3 * nt * W * sizeof(Fq), hipMemcpyHostToDevice, s) != hipSuccess ||
+            // the product circuits' shared eq vector (every product triple gathered the same entries)
+            (nc && hipMemcpyAsync(cbuf[cur], gbuf + 2 * W, W * sizeof(Fq), hipMemcpyDeviceToDevice, s) != hipSuccess))
+          rc = set_err(ctx, SPG_E_HIP, "gathered entries upload");
       }
-      memcpy(st, tr.data(), nt * sizeof(Triple));
-      SPG_HIP(ctx, hipMemcpyAsync(ddesc, st, nt * sizeof(Triple), hipMemcpyHostToDevice, s));
-      SPG_HIP(ctx, hipMemcpyAsync(gbuf, hv, 3 * nt * W * sizeof(Fq), hipMemcpyHostToDevice, s));
-      if (nc)  // the product circuits' shared eq vector (every product triple gathered the same entries)
-        SPG_HIP(ctx, hipMemcpyAsync(cbuf[cur], gbuf + 2 * W, W * sizeof(Fq), hipMemcpyDeviceToDevice, s));
-      rc = run_rounds(lgW, false, true, &fin);
+      rc = run_rounds(lgW, false, true, &fin, rc);
     } else {
-      rc = run_rounds(lg2(hl), false, true, &fin);
+      rc = run_rounds(lg2(hl), false, true, &fin, rc);
     }
-    if (rc) return rc;
+    if (rc && (W == 1 || shared)) return rc;
+    if (rc) {  // this rank alone: skip mode until an exchange carries it
+      fail = rc;
+      continue;
+    }
     for (size_t c = 0; c < nc; c++) {
       lpf.left.push_back(fin[3 * c]);
       lpf.right.push_back(fin[3 * c + 1]);
@@ -765,6 +797,11 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     rand.insert(rand.end(), r_prod.begin(), r_prod.end());
     out->layers.push_back(std::move(lpf));
     lp.lap("layer_finals");
+  }
+  if (W > 1) {  // every rank's status, so a failure still pending here fails every rank alike
+    std::vector<uint8_t> none;
+    const int rc = comm_allgather(ctx, sh, fail, nullptr, 0, none);
+    if (rc) return rc;
   }
   lp.print();
   *rand_out = rand;
