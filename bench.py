@@ -39,9 +39,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (/opt/skills/guides/MI355X_MICROARCH.md)
-# whole-GPU ext_madd throughput at 8 resident 256-thread blocks per CU, measured on MI355X by
+# whole-GPU ext_madd throughput at 8 resident 256-thread blocks per CU (3.00e10/s), measured on MI355X by
 # scripts/micro/ext_throughput.hip (output: profiles/r03_ext_throughput.txt)
-MADD_PEAK = 2.66e10
+MADD_PEAK = 3.0e10
 GENS_LABEL = b"gens_r1cs_sat"
 GENS_NUM_VARS = 1 << 24  # TOTAL_NUM_VARS_BOUND = 10^7 -> 2^24 (examples/interface.rs:557-563)
 CONFIGS = {

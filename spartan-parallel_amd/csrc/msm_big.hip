@@ -20,6 +20,10 @@
 //                  each on a host core, where one dependent GPU addition costs ~2 us), then the encoding.
 #include <hipcub/hipcub.hpp>
 
+#include <stdio.h>
+
+#include <vector>
+
 #include "ctx.hpp"
 #include "hcurve.hpp"
 #include "quad.hpp"
@@ -135,11 +139,13 @@ __global__ void __launch_bounds__(1024) k_big_chunks(const uint32_t* __restrict_
 __global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ chunks,
                                                       const uint32_t* __restrict__ nchunks,
                                                       const uint32_t* __restrict__ entries,
-                                                      const Niels* __restrict__ tab, Ext* __restrict__ sums) {
+                                                      const Niels* __restrict__ tab, Ext* __restrict__ sums,
+                                                      unsigned long long* probe) {
   __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
   const uint32_t cid = blockIdx.x;
   if (cid >= *nchunks) return;  // whole workgroups exit together
   const int t = threadIdx.x, q = t & 3, slot = t >> 2;
+  if (probe && t == 0) probe[4 * cid] = wall_clock64();
   const Chunk c = chunks[cid];
   Ext acc = ext_identity();
   // software-pipelined: the table coordinate of entry e + 64 is loaded while entry e is added
@@ -157,6 +163,10 @@ __global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ 
     neg = nn;
     e = e2;
   }
+  if (probe) {
+    __syncthreads();
+    if (t == 0) probe[4 * cid + 1] = wall_clock64();
+  }
   for (int d = kBigQuads / 2; d >= 1; d >>= 1) {
     if (slot >= d && slot < 2 * d) quad_put_op<kBigQuads>(pts, slot - d, acc, q);
     __syncthreads();
@@ -164,21 +174,27 @@ __global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ 
     __syncthreads();
   }
   if (t == 0) sums[cid] = acc;
+  if (probe && t == 0) probe[4 * cid + 2] = wall_clock64();
 }
 
 // one workgroup (64 quads) per group g of 64 buckets: quad j holds B = bucket 64 g + j + 1 (its chunks summed);
 // the suffix scan S_j = sum_{u >= j} B_u and the tree sum_j S_j = sum_j (j + 1) B_j; out[2 g] = that weighted
 // sum, out[2 g + 1] = S_0 = the group's plain sum
 __global__ void __launch_bounds__(kBigBS) k_big_groups(const Ext* __restrict__ sums, const uint32_t* __restrict__ first,
-                                                       Ext* __restrict__ out) {
+                                                       Ext* __restrict__ out, unsigned long long* probe) {
   __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
   const int t = threadIdx.x, q = t & 3, slot = t >> 2, g = blockIdx.x;
   const int key = g * kBigGroup + slot;
+  if (probe && t == 0) probe[4 * g] = wall_clock64();
   Ext B = ext_identity();
   bool any = false;
   for (uint32_t c = first[key]; c < first[key + 1]; c++) {
     B = any ? quad_add(B, sums[c], q) : sums[c];
     any = true;
+  }
+  if (probe) {
+    __syncthreads();
+    if (t == 0) probe[4 * g + 1] = wall_clock64();
   }
   Ext suf = B;
   for (int d = 1; d < kBigQuads; d <<= 1) {
@@ -188,6 +204,7 @@ __global__ void __launch_bounds__(kBigBS) k_big_groups(const Ext* __restrict__ s
     __syncthreads();
   }
   if (slot == 0 && q == 0) out[2 * g + 1] = suf;
+  if (probe && t == 0) probe[4 * g + 2] = wall_clock64();
   Ext acc = suf;
   for (int d = kBigQuads / 2; d >= 1; d >>= 1) {
     if (slot >= d && slot < 2 * d) quad_put_op<kBigQuads>(pts, slot - d, acc, q);
@@ -196,6 +213,7 @@ __global__ void __launch_bounds__(kBigBS) k_big_groups(const Ext* __restrict__ s
     __syncthreads();
   }
   if (t == 0) out[2 * g] = acc;
+  if (probe && t == 0) probe[4 * g + 3] = wall_clock64();
 }
 
 int big_window() {
@@ -233,16 +251,57 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
     hipLaunchKernelGGL(k_big_scatter<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
     hipLaunchKernelGGL(k_big_chunks, dim3(1), dim3(1024), 0, s, a.off, a.G, NB, ch, chunks, first);
   }
+  // SPG_BIG_PROBE=1: per-workgroup phase timestamps of the accumulation and the group reduction, on stderr
+  static const bool probe_on = getenv("SPG_BIG_PROBE") != nullptr;
+  unsigned long long* pa = nullptr;
+  unsigned long long* pg = nullptr;
+  if (probe_on) {
+    SPG_HIP(ctx, hipMalloc(&pa, 4 * max_chunks * 8));
+    SPG_HIP(ctx, hipMalloc(&pg, 4 * (NB / kBigGroup) * 8));
+    SPG_HIP(ctx, hipMemsetAsync(pa, 0, 4 * max_chunks * 8, s));
+  }
   {
     KScope ks(ctx, "msm_big_accum", 0.0, (double)a.per * W * (1.0 - 1.0 / (double)(1 << C)));
     hipLaunchKernelGGL(k_big_accum, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first + NB, a.entries,
-                       g->table, sums);
+                       g->table, sums, pa);
   }
   {
     KScope ks(ctx, "msm_big_groups");
-    hipLaunchKernelGGL(k_big_groups, dim3(NB / kBigGroup), dim3(kBigBS), 0, s, sums, first, host_groups_dev);
+    hipLaunchKernelGGL(k_big_groups, dim3(NB / kBigGroup), dim3(kBigBS), 0, s, sums, first, host_groups_dev, pg);
   }
   SPG_HIP(ctx, hipGetLastError());
+  if (probe_on) {
+    std::vector<unsigned long long> A(4 * max_chunks), Gp(4 * (NB / kBigGroup));
+    SPG_HIP(ctx, (hipMemcpyAsync)(A.data(), pa, A.size() * 8, hipMemcpyDeviceToHost, s));
+    SPG_HIP(ctx, (hipMemcpyAsync)(Gp.data(), pg, Gp.size() * 8, hipMemcpyDeviceToHost, s));
+    SPG_HIP(ctx, hipStreamSynchronize(s));
+    unsigned long long a0 = ~0ull, a1 = 0;
+    double madd = 0, tree = 0;
+    size_t cnt = 0;
+    for (size_t i = 0; i < max_chunks; i++) {
+      if (!A[4 * i]) continue;
+      a0 = std::min(a0, A[4 * i]);
+      a1 = std::max(a1, A[4 * i + 2]);
+      madd += (double)(A[4 * i + 1] - A[4 * i]);
+      tree += (double)(A[4 * i + 2] - A[4 * i + 1]);
+      cnt++;
+    }
+    fprintf(stderr, "[spg] big accum: %zu chunks, span %.1f us, per chunk: adds %.1f us, tree %.1f us\n", cnt,
+            (a1 - a0) / 100.0, madd / cnt / 100.0, tree / cnt / 100.0);
+    const int ng = NB / kBigGroup;
+    unsigned long long g0 = ~0ull, g1 = 0;
+    double ph[3] = {0, 0, 0};
+    for (int i = 0; i < ng; i++) {
+      g0 = std::min(g0, Gp[4 * i]);
+      g1 = std::max(g1, Gp[4 * i + 3]);
+      for (int k = 0; k < 3; k++) ph[k] += (double)(Gp[4 * i + k + 1] - Gp[4 * i + k]);
+    }
+    fprintf(stderr, "[spg] big groups: %d groups, span %.1f us, gap after accum %.1f us; per group: bucket sums %.1f, "
+            "scan %.1f, tree %.1f us\n", ng, (g1 - g0) / 100.0, ((double)g0 - (double)a1) / 100.0, ph[0] / ng / 100.0,
+            ph[1] / ng / 100.0, ph[2] / ng / 100.0);
+    hipFree(pa);
+    hipFree(pg);
+  }
   *ngroups = NB / kBigGroup;
   return 0;
 }
