@@ -4,18 +4,18 @@
 //
 // The batch pipeline of msm.hip sizes its window for many MSMs at once (c = 16 for one 2^16 MSM: 2^15 buckets),
 // and for a single MSM its bucket reduction sum_v v B_v -- a chain of dependent group additions -- dominated
-// (65 % of 604 us). Here the window is chosen for one MSM: c = 12 signed digits (2^11 buckets, 22 windows),
+// (65 % of 604 us). Here the window is chosen for one MSM (c = 11..12 signed digits, 2^10..2^11 buckets),
 // fixed-base over the resident 2^k P_i tables (no doublings), and every phase is either throughput-bound with the
-// chip full or a short dependent chain:
+// chip full or a short dependent chain (c = 11 by default: 1024 buckets, 24 windows):
 //   k_big_digits   block-local LDS histograms of the signed digits (digits kept in HBM as int16)
 //   hipcub scan    over the [bucket][block] histogram matrix: each (bucket, block) pair's entry range
 //   k_big_scatter  counting-sort scatter of (table index | sign) into bucket order, LDS cursors
 //   k_big_chunks   one workgroup's work list: bucket v split into chunks of <= CH entries (skewed scalars only
 //                  lengthen the list, never a workgroup)
 //   k_big_accum    one workgroup per chunk: 64 quads (4 lanes per point, quad.hpp) each add ~CH/64 table entries,
-//                  then an LDS tree -> the chunk's sum
-//   k_big_groups   one workgroup per 64 consecutive buckets: bucket sums from their chunks, a suffix scan and a tree
-//                  give W_g = sum_j (j + 1) B_{64 g + j} and G_g = sum_j B_{64 g + j}
+//                  then an LDS tree -> the chunk's sum; the workgroup finishing the last chunk of a group of 64
+//                  buckets then reduces that group: bucket sums from their chunks, a suffix scan and a tree give
+//                  W_g = sum_j (j + 1) B_{64 g + j} and G_g = sum_j B_{64 g + j}
 //   host           sum_v v B_v = sum_g W_g + 64 sum_g g G_g over the NB/64 groups (radix-2^51 additions at ~0.1 us
 //                  each on a host core, where one dependent GPU addition costs ~2 us), then the encoding.
 #include <hipcub/hipcub.hpp>
@@ -35,7 +35,7 @@ namespace {
 // workspace slots 100..107 (msm.hip 0..18, proto.hip 20..24, r1cs.hip 30.., spark.hip 60.., snark / verify 91..96)
 constexpr int kBigBS = 256;      // threads per workgroup (64 quads)
 constexpr int kBigQuads = kBigBS / 4;
-constexpr int kBigGroup = 64;    // buckets per k_big_groups workgroup
+constexpr int kBigGroup = 64;    // buckets per group reduction (big_group)
 
 struct BigArgs {
   const Fq* scalars;
@@ -109,7 +109,8 @@ struct Chunk {
 // one 1024-thread block: bucket v = key + 1 holds entries [bh[key G], bh[(key + 1) G]); it becomes
 // ceil(count / ch) chunks; first[key] = its first chunk, first[NB] = the number of chunks
 __global__ void __launch_bounds__(1024) k_big_chunks(const uint32_t* __restrict__ bh, int G, int NB, uint32_t ch,
-                                                     Chunk* __restrict__ chunks, uint32_t* __restrict__ first) {
+                                                     Chunk* __restrict__ chunks, uint32_t* __restrict__ first,
+                                                     unsigned* __restrict__ gcnt, Ext* __restrict__ out) {
   __shared__ uint32_t part[1024];
   const int t = threadIdx.x;
   const int per_t = (NB + 1023) / 1024, k0 = t * per_t, k1 = min(NB, k0 + per_t);
@@ -133,17 +134,60 @@ __global__ void __launch_bounds__(1024) k_big_chunks(const uint32_t* __restrict_
     for (uint32_t o = 0; o < c; o += ch) chunks[run++] = Chunk{(uint32_t)k, s + o, min(ch, c - o), 0u};
   }
   if (t == 1023) first[NB] = part[1023];
+  __syncthreads();
+  // the group tickets of k_big_accum, and the sums of groups no chunk will report (no entries at all)
+  if (t < NB / kBigGroup) {
+    gcnt[t] = 0u;
+    if (first[(t + 1) * kBigGroup] == first[t * kBigGroup]) out[2 * t] = out[2 * t + 1] = ext_identity();
+  }
 }
 
-// one workgroup (64 quads) per chunk; grid = an upper bound of the chunk count
+// Group g of 64 buckets (run by the workgroup that finishes the group's last chunk): quad j holds
+// B = bucket 64 g + j + 1 (its chunks summed); the suffix scan S_j = sum_{u >= j} B_u and the tree
+// sum_j S_j = sum_j (j + 1) B_j; out[2 g] = that weighted sum, out[2 g + 1] = S_0 = the group's plain sum
+__device__ __forceinline__ void big_group(int g, const Ext* __restrict__ sums, const uint32_t* __restrict__ first,
+                                          Ext* __restrict__ out, uint32_t* pts) {
+  const int t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int key = g * kBigGroup + slot;
+  Ext B = ext_identity();
+  bool any = false;
+  for (uint32_t c = first[key]; c < first[key + 1]; c++) {
+    B = any ? quad_add(B, sums[c], q) : sums[c];
+    any = true;
+  }
+  Ext suf = B;
+  for (int d = 1; d < kBigQuads; d <<= 1) {
+    quad_put_op<kBigQuads>(pts, slot, suf, q);
+    __syncthreads();
+    if (slot + d < kBigQuads) suf = quad_add_op(suf, quad_get_op<kBigQuads>(pts, slot + d, q), q);
+    __syncthreads();
+  }
+  if (slot == 0 && q == 0) out[2 * g + 1] = suf;
+  Ext acc = suf;
+  for (int d = kBigQuads / 2; d >= 1; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put_op<kBigQuads>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<kBigQuads>(pts, slot, q), q);
+    __syncthreads();
+  }
+  if (t == 0) out[2 * g] = acc;
+}
+
+// one workgroup (64 quads) per chunk; grid = an upper bound of the chunk count. The workgroup that finishes the last
+// chunk of a group of 64 buckets (ticket gcnt[g]) goes on to that group's reduction (big_group): no second launch,
+// and the groups reduce while other chunks still accumulate.
+// Cross-XCD hand-off as in grid_reduce3 (sumcheck.hip): plain stores + agent-scope release before the ticket,
+// agent-scope acquire in the reducer before plain loads (the per-XCD L2s are not coherent).
 __global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ chunks,
-                                                      const uint32_t* __restrict__ nchunks,
+                                                      const uint32_t* __restrict__ first,
                                                       const uint32_t* __restrict__ entries,
                                                       const Niels* __restrict__ tab, Ext* __restrict__ sums,
+                                                      unsigned* __restrict__ gcnt, Ext* __restrict__ out, int NB,
                                                       unsigned long long* probe) {
   __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
+  __shared__ bool last;
   const uint32_t cid = blockIdx.x;
-  if (cid >= *nchunks) return;  // whole workgroups exit together
+  if (cid >= first[NB]) return;  // whole workgroups exit together
   const int t = threadIdx.x, q = t & 3, slot = t >> 2;
   if (probe && t == 0) probe[4 * cid] = wall_clock64();
   const Chunk c = chunks[cid];
@@ -173,51 +217,30 @@ __global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ 
     if (slot < d) acc = quad_add_op(acc, quad_get_op<kBigQuads>(pts, slot, q), q);
     __syncthreads();
   }
-  if (t == 0) sums[cid] = acc;
-  if (probe && t == 0) probe[4 * cid + 2] = wall_clock64();
-}
-
-// one workgroup (64 quads) per group g of 64 buckets: quad j holds B = bucket 64 g + j + 1 (its chunks summed);
-// the suffix scan S_j = sum_{u >= j} B_u and the tree sum_j S_j = sum_j (j + 1) B_j; out[2 g] = that weighted
-// sum, out[2 g + 1] = S_0 = the group's plain sum
-__global__ void __launch_bounds__(kBigBS) k_big_groups(const Ext* __restrict__ sums, const uint32_t* __restrict__ first,
-                                                       Ext* __restrict__ out, unsigned long long* probe) {
-  __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
-  const int t = threadIdx.x, q = t & 3, slot = t >> 2, g = blockIdx.x;
-  const int key = g * kBigGroup + slot;
-  if (probe && t == 0) probe[4 * g] = wall_clock64();
-  Ext B = ext_identity();
-  bool any = false;
-  for (uint32_t c = first[key]; c < first[key + 1]; c++) {
-    B = any ? quad_add(B, sums[c], q) : sums[c];
-    any = true;
+  const int g = (int)(c.key / kBigGroup);
+  if (t == 0) {
+    sums[cid] = acc;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t total = first[(g + 1) * kBigGroup] - first[g * kBigGroup];
+    last = __hip_atomic_fetch_add(&gcnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (probe) probe[4 * cid + 2] = wall_clock64();
   }
-  if (probe) {
-    __syncthreads();
-    if (t == 0) probe[4 * g + 1] = wall_clock64();
-  }
-  Ext suf = B;
-  for (int d = 1; d < kBigQuads; d <<= 1) {
-    quad_put_op<kBigQuads>(pts, slot, suf, q);
-    __syncthreads();
-    if (slot + d < kBigQuads) suf = quad_add_op(suf, quad_get_op<kBigQuads>(pts, slot + d, q), q);
-    __syncthreads();
-  }
-  if (slot == 0 && q == 0) out[2 * g + 1] = suf;
-  if (probe && t == 0) probe[4 * g + 2] = wall_clock64();
-  Ext acc = suf;
-  for (int d = kBigQuads / 2; d >= 1; d >>= 1) {
-    if (slot >= d && slot < 2 * d) quad_put_op<kBigQuads>(pts, slot - d, acc, q);
-    __syncthreads();
-    if (slot < d) acc = quad_add_op(acc, quad_get_op<kBigQuads>(pts, slot, q), q);
-    __syncthreads();
-  }
-  if (t == 0) out[2 * g] = acc;
-  if (probe && t == 0) probe[4 * g + 3] = wall_clock64();
+  __syncthreads();
+  if (!last) return;
+  big_group(g, sums, first, out, pts);
+  if (probe && t == 0) probe[4 * cid + 3] = wall_clock64();
 }
 
 int big_window() {
-  static const int c = getenv("SPG_BIG_C") ? atoi(getenv("SPG_BIG_C")) : 12;
+  // c = 11 (1024 buckets, 24 windows): measured best for 2^16 points against 12 and 13 (scripts/gpu_r03d.sh); a
+  // smaller bucket set shortens the group reductions at the end more than its extra windows cost
+  static const int c = getenv("SPG_BIG_C") ? atoi(getenv("SPG_BIG_C")) : 11;
   return c < 8 ? 8 : (c > 14 ? 14 : c);
 }
 
@@ -237,8 +260,9 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
   a.entries = (uint32_t*)ws_get(ctx, 103, E * 4 + 64);
   Chunk* chunks = (Chunk*)ws_get(ctx, 104, max_chunks * sizeof(Chunk));
   uint32_t* first = (uint32_t*)ws_get(ctx, 105, (NB + 1) * 4 + 64);
+  unsigned* gcnt = (unsigned*)ws_get(ctx, 108, (NB / kBigGroup) * 4 + 64);
   Ext* sums = (Ext*)ws_get(ctx, 106, max_chunks * sizeof(Ext));
-  if (!a.digits || !a.bh || !a.off || !a.entries || !chunks || !first || !sums) return set_err(ctx, SPG_E_NOMEM, "msm workspace");
+  if (!a.digits || !a.bh || !a.off || !a.entries || !chunks || !first || !gcnt || !sums) return set_err(ctx, SPG_E_NOMEM, "msm workspace");
   const int nkeys = NB * a.G + 1;
   size_t tmp_bytes = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, a.bh, a.off, nkeys, s);
@@ -249,35 +273,29 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
     hipLaunchKernelGGL(k_big_digits<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
     SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, a.bh, a.off, nkeys, s));
     hipLaunchKernelGGL(k_big_scatter<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
-    hipLaunchKernelGGL(k_big_chunks, dim3(1), dim3(1024), 0, s, a.off, a.G, NB, ch, chunks, first);
+    hipLaunchKernelGGL(k_big_chunks, dim3(1), dim3(1024), 0, s, a.off, a.G, NB, ch, chunks, first, gcnt,
+                       host_groups_dev);
   }
-  // SPG_BIG_PROBE=1: per-workgroup phase timestamps of the accumulation and the group reduction, on stderr
+  // SPG_BIG_PROBE=1: per-workgroup phase timestamps of the accumulation (+ group reductions), on stderr
   static const bool probe_on = getenv("SPG_BIG_PROBE") != nullptr;
   unsigned long long* pa = nullptr;
-  unsigned long long* pg = nullptr;
   if (probe_on) {
     SPG_HIP(ctx, hipMalloc(&pa, 4 * max_chunks * 8));
-    SPG_HIP(ctx, hipMalloc(&pg, 4 * (NB / kBigGroup) * 8));
     SPG_HIP(ctx, hipMemsetAsync(pa, 0, 4 * max_chunks * 8, s));
   }
   {
     KScope ks(ctx, "msm_big_accum", 0.0, (double)a.per * W * (1.0 - 1.0 / (double)(1 << C)));
-    hipLaunchKernelGGL(k_big_accum, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first + NB, a.entries,
-                       g->table, sums, pa);
-  }
-  {
-    KScope ks(ctx, "msm_big_groups");
-    hipLaunchKernelGGL(k_big_groups, dim3(NB / kBigGroup), dim3(kBigBS), 0, s, sums, first, host_groups_dev, pg);
+    hipLaunchKernelGGL(k_big_accum, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first, a.entries,
+                       g->table, sums, gcnt, host_groups_dev, NB, pa);
   }
   SPG_HIP(ctx, hipGetLastError());
   if (probe_on) {
-    std::vector<unsigned long long> A(4 * max_chunks), Gp(4 * (NB / kBigGroup));
+    std::vector<unsigned long long> A(4 * max_chunks);
     SPG_HIP(ctx, (hipMemcpyAsync)(A.data(), pa, A.size() * 8, hipMemcpyDeviceToHost, s));
-    SPG_HIP(ctx, (hipMemcpyAsync)(Gp.data(), pg, Gp.size() * 8, hipMemcpyDeviceToHost, s));
     SPG_HIP(ctx, hipStreamSynchronize(s));
-    unsigned long long a0 = ~0ull, a1 = 0;
-    double madd = 0, tree = 0;
-    size_t cnt = 0;
+    unsigned long long a0 = ~0ull, a1 = 0, g1 = 0;
+    double madd = 0, tree = 0, grp = 0;
+    size_t cnt = 0, ng = 0;
     for (size_t i = 0; i < max_chunks; i++) {
       if (!A[4 * i]) continue;
       a0 = std::min(a0, A[4 * i]);
@@ -285,22 +303,16 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
       madd += (double)(A[4 * i + 1] - A[4 * i]);
       tree += (double)(A[4 * i + 2] - A[4 * i + 1]);
       cnt++;
+      if (A[4 * i + 3]) {
+        g1 = std::max(g1, A[4 * i + 3]);
+        grp += (double)(A[4 * i + 3] - A[4 * i + 2]);
+        ng++;
+      }
     }
-    fprintf(stderr, "[spg] big accum: %zu chunks, span %.1f us, per chunk: adds %.1f us, tree %.1f us\n", cnt,
-            (a1 - a0) / 100.0, madd / cnt / 100.0, tree / cnt / 100.0);
-    const int ng = NB / kBigGroup;
-    unsigned long long g0 = ~0ull, g1 = 0;
-    double ph[3] = {0, 0, 0};
-    for (int i = 0; i < ng; i++) {
-      g0 = std::min(g0, Gp[4 * i]);
-      g1 = std::max(g1, Gp[4 * i + 3]);
-      for (int k = 0; k < 3; k++) ph[k] += (double)(Gp[4 * i + k + 1] - Gp[4 * i + k]);
-    }
-    fprintf(stderr, "[spg] big groups: %d groups, span %.1f us, gap after accum %.1f us; per group: bucket sums %.1f, "
-            "scan %.1f, tree %.1f us\n", ng, (g1 - g0) / 100.0, ((double)g0 - (double)a1) / 100.0, ph[0] / ng / 100.0,
-            ph[1] / ng / 100.0, ph[2] / ng / 100.0);
+    fprintf(stderr, "[spg] big accum: %zu chunks, span %.1f us (groups done at %.1f us); per chunk: adds %.1f us, "
+            "tree %.1f us; per group reduction %.1f us (%zu)\n", cnt, (a1 - a0) / 100.0, (g1 - a0) / 100.0,
+            madd / cnt / 100.0, tree / cnt / 100.0, ng ? grp / ng / 100.0 : 0.0, ng);
     hipFree(pa);
-    hipFree(pg);
   }
   *ngroups = NB / kBigGroup;
   return 0;
@@ -323,8 +335,9 @@ int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq*
   a.gen_offset = (int)gen_offset;
   a.h_index = (int)g->n;
   a.n1 = (int)(g->n + 1);
-  // digit blocks: about 4 scalars per thread, at most 512 blocks (the histogram matrix is NB x G)
-  a.G = std::max(1, std::min(512, (per + 4 * kBigBS - 1) / (4 * kBigBS)));
+  // digit blocks: SPG_BIG_SPT scalars per thread (default 1), at most 512 blocks (the histogram matrix is NB x G)
+  static const int spt = getenv("SPG_BIG_SPT") ? std::max(1, atoi(getenv("SPG_BIG_SPT"))) : 1;
+  a.G = std::max(1, std::min(512, (per + spt * kBigBS - 1) / (spt * kBigBS)));
   a.spb = (per + a.G - 1) / a.G;
   int ng = 0, rc = 0;
   Ext* res = (Ext*)ctx->d_res;  // the coherent result page: 2 NB / 64 points (<= 256 at c = 14)

@@ -106,3 +106,23 @@ def test_verify_rejects_swapped_parts(ctx, vars_gens, a, b):
     assert swapped != p
     ok, why = prog.verify(swapped)
     assert not ok, f"accepted with {a} and {b} exchanged"
+
+
+def test_verify_rejects_noncanonical_scalar_limbs(ctx, vars_gens):
+    """A proof scalar whose four limbs are >= q (here m + q for the prover's m, the same residue mod q). The
+    reference deserialises `Scalar([u64; 4])` without a range check (src/scalar/ristretto255.rs:198) and then runs
+    its Montgomery arithmetic on an out-of-range input, whose result is not defined by the field; libspg's reader
+    rejects such limbs as malformed. This is a deliberate, stricter deviation, pinned here."""
+    from proof_layout import snark_proof_fields
+
+    Q = 2**252 + 27742317777372353535851937790883648493
+    prog = Program(ctx, vars_gens, "b2_x32_q2")
+    fields = [f for f in snark_proof_fields(prog.proof) if f[0].endswith(".z1")]
+    assert fields
+    name, s, e = fields[0]
+    m = int.from_bytes(prog.proof[s:e], "little")
+    assert m < Q
+    bad = bytearray(prog.proof)
+    bad[s:e] = (m + Q).to_bytes(32, "little")
+    ok, why = prog.verify(bytes(bad))
+    assert not ok and "malformed" in why, (name, why)
