@@ -1,0 +1,10 @@
+#!/bin/bash
+# round-3: SNARK parity after the commit-queue merge, A/B against HEAD's build, host fixed-base table micro
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+timeout -k 10 60 ./scripts/micro/host_tables > gpurun_out/host_tables.txt 2>&1; cat gpurun_out/host_tables.txt
+timeout -k 10 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_snark.py tests/test_gpu_dropin.py > gpurun_out/t_snark.log 2>&1
+rc=$?; tail -3 gpurun_out/t_snark.log; [ $rc -eq 0 ] || exit $rc
+bash scripts/ab_lib.sh lib/libspg_base.so lib/libspg.so 3

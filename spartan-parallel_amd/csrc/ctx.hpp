@@ -133,6 +133,8 @@ int msm_small_buckets(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const 
 // the latency path for many small rows (Hyrax rows of <= ~1K scalars): compressed outputs, d_out: B x 32 (device)
 int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                          uint8_t* d_out);
+// n extended points (device) -> n x 32 encoded bytes (device), one lane per point, stream-ordered
+int compress_ext_device(spg_ctx* ctx, const Ext* d_ext, size_t n, uint8_t* d_out);
 
 // one Bullet round (msm.hip k_bullet_round_q): applies round k-1's fold with (u, uinv) to the device state
 // (aa: Montgomery, cw: plain integers; in -> out, double-buffered), then the bucket sums of the round's L and

@@ -787,6 +787,15 @@ __global__ void __launch_bounds__(256) k_compress_ext(const Ext* __restrict__ in
   if (i < n) ext_compress(in[i], out + 32 * i);
 }
 
+// n extended points -> n x 32 encoded bytes (device), stream-ordered
+int compress_ext_device(spg_ctx* ctx, const Ext* d_ext, size_t n, uint8_t* d_out) {
+  if (!n) return 0;
+  KScope ks(ctx, "msm_compress");
+  hipLaunchKernelGGL(k_compress_ext, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, d_ext, n, d_out);
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
 // B MSMs of n scalars (rows of a Hyrax commitment) through the latency path, compressed on the device
 int msm_small_compressed(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                          uint8_t* d_out) {

@@ -153,6 +153,14 @@ ProverGens gens_view(spg_gens* dev, size_t nv);
 int commit_dev(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t nv, std::vector<Pt>* out, const Shard& sh = Shard());
 // L rows of R consecutive device scalars -> L row commitments (host)
 int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out);
+// several row sets at once: the sets that take the latency path's device final (R <= 256, 64 < L <= 65535) are
+// launched back to back and encoded by one k_compress_ext launch with one download; the others as commit_rows
+struct RowJob {
+  const Fq* d_Z;
+  size_t R, L;
+  Pt* out;
+};
+int commit_rows_many(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs);
 // the same split over the ranks of sh (every rank returns all L commitments)
 int commit_rows_sh(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out, const Shard& sh);
 // PolyCommitment::append_to_transcript

@@ -436,13 +436,18 @@ struct CQ {
       it.out->assign((size_t)1 << (nv / 2), Pt());
       if (!is_early(it) && std::find(widths.begin(), widths.end(), R) == widths.end()) widths.push_back(R);
     }
-    for (size_t R : widths) {
-      size_t total = 0;
-      for (auto& it : items)
-        if (!is_early(it) && ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) == R) total += it.len;
-      Fq* d = (Fq*)ws_get(ctx, 91, total * sizeof(Fq) + 64);
-      if (!d) return set_err(ctx, SPG_E_NOMEM, "commit staging");
-      size_t o = 0;
+    // one staging range per width, every width's rows committed together (the latency-path widths share one
+    // encoding launch and one download)
+    size_t total = 0;
+    for (auto& it : items)
+      if (!is_early(it)) total += it.len;
+    Fq* d = (Fq*)ws_get(ctx, 91, total * sizeof(Fq) + 64);
+    if (total && !d) return set_err(ctx, SPG_E_NOMEM, "commit staging");
+    std::vector<std::vector<Pt>> rows(widths.size());
+    std::vector<RowJob> jobs;
+    size_t o = 0;
+    for (size_t w = 0; w < widths.size(); w++) {
+      const size_t R = widths[w], o0 = o;
       for (auto& it : items) {
         if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
         if (it.host)
@@ -451,14 +456,17 @@ struct CQ {
           SPG_HIP(ctx, hipMemcpyAsync(d + o, it.dev, it.len * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
         o += it.len;
       }
-      std::vector<Pt> rows(total / R);
-      int rc = commit_rows(ctx, g, d, R, total / R, rows.data());
-      if (rc) return rc;
-      o = 0;
+      rows[w].resize((o - o0) / R);
+      jobs.push_back({d + o0, R, (o - o0) / R, rows[w].data()});
+    }
+    int rc = commit_rows_many(ctx, g, jobs);
+    if (rc) return rc;
+    for (size_t w = 0; w < widths.size(); w++) {
+      size_t ro = 0;
       for (auto& it : items) {
-        if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != R) continue;
-        std::copy(rows.begin() + o, rows.begin() + o + it.out->size(), it.out->begin());
-        o += it.out->size();
+        if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != widths[w]) continue;
+        std::copy(rows[w].begin() + ro, rows[w].begin() + ro + it.out->size(), it.out->begin());
+        ro += it.out->size();
       }
     }
     if (early_L) {

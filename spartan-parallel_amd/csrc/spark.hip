@@ -292,7 +292,8 @@ static const size_t kHostFinalRows = 64;  // latency-path commits of at most thi
 enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
-  kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp
+  kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp,  // 60 .. 89
+  kWsMultiExt = 120, kWsMultiOut  // (snark.hip uses 91 .. 93, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -350,6 +351,44 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
     if (trace2)
       fprintf(stderr, "[spg] commit rows=%zu R=%zu %s %.0f us\n", nb, R, small ? "small" : "batch",
               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+  return 0;
+}
+
+int commit_rows_many(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs) {
+  auto merged = [&](const RowJob& j) { return j.R <= kSmallRowMax && j.L > kHostFinalRows && j.L <= 65535; };
+  size_t tot = 0;
+  for (const RowJob& j : jobs) {
+    if (j.R > g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: rows wider than the generators");
+    if (merged(j)) tot += j.L;
+  }
+  if (tot) {
+    Ext* d_ext = (Ext*)ws_get(ctx, kWsMultiExt, tot * sizeof(Ext) + 64);
+    uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsMultiOut, 32 * tot + 64);
+    if (!d_ext || !d_out) return set_err(ctx, SPG_E_NOMEM, "commit rows");
+    size_t o = 0;
+    for (const RowJob& j : jobs) {
+      if (!merged(j)) continue;
+      int rc = msm_small_device(ctx, g.dev, 0, j.d_Z, j.R, j.L, nullptr, d_ext + o, nullptr, -1);
+      if (rc) return rc;
+      o += j.L;
+    }
+    int rc = compress_ext_device(ctx, d_ext, tot, d_out);
+    if (rc) return rc;
+    std::vector<Pt> rows(tot);
+    SPG_HIP(ctx, hipMemcpyAsync(rows.data(), d_out, 32 * tot, hipMemcpyDeviceToHost, ctx->stream));
+    SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    o = 0;
+    for (const RowJob& j : jobs) {
+      if (!merged(j)) continue;
+      std::copy(rows.begin() + o, rows.begin() + o + j.L, j.out);
+      o += j.L;
+    }
+  }
+  for (const RowJob& j : jobs) {
+    if (merged(j)) continue;
+    int rc = commit_rows(ctx, g, j.d_Z, j.R, j.L, j.out);
+    if (rc) return rc;
   }
   return 0;
 }
