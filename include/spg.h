@@ -117,6 +117,12 @@ int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* Z_mont, siz
  * so the partials of all ranks add exactly. Same group.rs:98-116 semantics as spg_msm without the blind. */
 int spg_msm_partial(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont, size_t n,
                     uint8_t out_ext[128]);
+/* The same two over scalars already resident in HBM (buf[offset .. offset + n), e.g. a witness uploaded once):
+ * no host-to-device copy inside the call. spg_msm_buf has no blind (vartime_multiscalar_mul). */
+int spg_msm_partial_buf(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const spg_buf* buf, size_t offset,
+                        size_t n, uint8_t out_ext[128]);
+int spg_msm_buf(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const spg_buf* buf, size_t offset, size_t n,
+                uint8_t out[32]);
 /* Host only, needs no device or context: the sum of k partial points (k x 128 bytes, spg_msm_partial layout)
  * encoded as a 32-byte CompressedRistretto (RFC 9496 ENCODE). */
 int spg_points_sum_compress(const uint8_t* parts, size_t k, uint8_t out[32]);

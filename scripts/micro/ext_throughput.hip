@@ -5,6 +5,7 @@
 #include <stdio.h>
 
 #include "../../spartan-parallel_amd/csrc/curve.hpp"
+#include "../../spartan-parallel_amd/csrc/quad.hpp"
 
 using namespace spg;
 
@@ -18,6 +19,7 @@ __global__ void __launch_bounds__(256) k_thr(const Fp* in, Fp* out, int iters) {
     if (W == 0) a = fp_mul(a, b);
     if (W == 1) P = ext_add(P, P);
     if (W == 2) P = ext_madd(P, N, false);
+    if (W == 3) P = quad_madd(P, b, false, t & 3);  // 4 lanes per point: ops counted per quad below
   }
   out[blockIdx.x * 256 + threadIdx.x] = fp_add(a, P.X);
 }
@@ -37,7 +39,7 @@ void run(const char* name, Fp* in, Fp* out, int ncu) {
     hipEventSynchronize(e1);
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
-    const double ops = (double)blocks * 256 * iters;
+    const double ops = (double)blocks * 256 * iters / (W == 3 ? 4 : 1);
     printf("%-8s blocks/CU=%d  %.3f ms  %.3e ops/s  %.2f us per dependent op\n", name, bpc, ms, ops / (ms * 1e-3),
            ms * 1e3 / iters);
   }
@@ -54,5 +56,6 @@ int main() {
   run<0>("fp_mul", in, out, ncu);
   run<1>("ext_add", in, out, ncu);
   run<2>("ext_madd", in, out, ncu);
+  run<3>("quad_madd", in, out, ncu);
   return 0;
 }

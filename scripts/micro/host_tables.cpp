@@ -53,6 +53,14 @@ int main() {
     const int reps = 400;
     for (int r = 0; r < reps; r++) sink ^= hg.commit_many(calls[r % calls.size()])[0].b[0];
     const double us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+    t0 = clk::now();
+    for (int r = 0; r < reps; r++) {
+      auto& c = calls[r % calls.size()];
+      h::HExt a = hg.msm(c[0].first, c[0].second), b = hg.msm(c[1].first, c[1].second);
+      sink ^= compress(a).b[0] ^ compress(b).b[0];
+    }
+    const double us1 = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+    printf("[1 thread: %.2f us] ", us1);
     printf("tables of %2d generators (%5.1f MB): 2 x %d-term commit_many %.2f us\n", G, G * 32 * 256 * 120.0 / 1e6,
            terms, us);
   }

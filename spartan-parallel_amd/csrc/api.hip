@@ -81,6 +81,12 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes) {
   return s.p;
 }
 
+bool failpoint(const spg_ctx* c, const char* site) {
+  static const char* fp = getenv("SPG_FAILPOINT");
+  static const int fr = getenv("SPG_FAILPOINT_RANK") ? atoi(getenv("SPG_FAILPOINT_RANK")) : 0;
+  return fp && strcmp(fp, site) == 0 && c->rank == fr;
+}
+
 int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n) {
   auto t0 = std::chrono::steady_clock::now();
   for (uint64_t it = 0;; it++) {

@@ -87,6 +87,9 @@ void print_copy_counts();  // and reset
 static const int kTableRows = 254;  // bit offsets 0..253 cover every window of a 253-bit scalar
 
 int set_err(spg_ctx* c, int code, const std::string& msg);
+// test failpoint: true when SPG_FAILPOINT names `site` and SPG_FAILPOINT_RANK (default 0) is this context's rank
+// (tests/test_gpu_dist.py injects a failure on one rank of a sharded proof this way; unset in production)
+bool failpoint(const spg_ctx* c, const char* site);
 
 #define SPG_HIP(ctx, call)                                                                     \
   do {                                                                                         \

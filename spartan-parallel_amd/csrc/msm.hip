@@ -231,16 +231,6 @@ __global__ void k_item_keys(const uint32_t* __restrict__ item_off, uint32_t* __r
   for (uint32_t it = item_off[key]; it < item_off[key + 1]; it++) item_key[it] = (uint32_t)key;
 }
 
-__device__ __forceinline__ Ext load_signed(const Niels* __restrict__ tab, uint32_t e) {
-  Niels q = tab[e & 0x7fffffffu];
-  if (e >> 31) {
-    Fp t = q.ypx;
-    q.ypx = q.ymx;
-    q.ymx = t;
-    q.t2d = fp_neg(q.t2d);
-  }
-  return niels_to_ext(q);
-}
 
 __global__ void __launch_bounds__(256) k_items(const uint32_t* __restrict__ item_key,
                                                const uint32_t* __restrict__ item_off,
@@ -1206,6 +1196,40 @@ extern "C" int spg_msm(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const
   return msm_host(ctx, g, gen_offset, scalars_mont, n, 1, blind_mont, out);
 }
 
+// sum_i d_s[i] G[gen_offset + i] of n device scalars, uncompressed: X, Y, Z, T as 32 little-endian bytes each
+static int msm_partial_dev(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_s, size_t n,
+                           uint8_t out_ext[128]) {
+  hipStream_t s = ctx->stream;
+  if (n > kSmallMaxN && use_big()) {  // msm_big.hip; the host point's coordinates as canonical bytes
+    h::HExt r;
+    timer_start(ctx);
+    int rc = msm_single_big(ctx, g, gen_offset, d_s, n, nullptr, &r);
+    timer_stop(ctx);
+    if (rc) return rc;
+    h::fe_to_bytes(r.X, out_ext);
+    h::fe_to_bytes(r.Y, out_ext + 32);
+    h::fe_to_bytes(r.Z, out_ext + 64);
+    h::fe_to_bytes(r.T, out_ext + 96);
+  } else {
+    Ext* d_ext = (Ext*)ws_get(ctx, 19, sizeof(Ext) + 64);
+    if (!d_ext) return set_err(ctx, SPG_E_NOMEM, "msm output");
+    timer_start(ctx);
+    int rc = n <= kSmallMaxN ? msm_small_device(ctx, g, gen_offset, d_s, n, 1, nullptr, d_ext, nullptr, -1)
+                             : msm_batch_device(ctx, g, gen_offset, d_s, n, 1, nullptr, nullptr, nullptr, -1, d_ext);
+    if (rc) return rc;
+    timer_stop(ctx);
+    Ext r;
+    SPG_HIP(ctx, hipMemcpyAsync(&r, d_ext, sizeof(Ext), hipMemcpyDeviceToHost, s));
+    SPG_HIP(ctx, hipStreamSynchronize(s));
+    static_assert(sizeof(Ext) == 128, "Ext is X, Y, Z, T of 32 bytes");
+    memcpy(out_ext, &r, sizeof(Ext));
+  }
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+  ctx->last_us = ms * 1000.0;
+  return SPG_OK;
+}
+
 // one shard of an MSM that is split over devices: the sum stays uncompressed so that the partials
 // of all ranks add exactly; spg_points_sum_compress adds and encodes them on the host
 extern "C" int spg_msm_partial(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const uint64_t* scalars_mont,
@@ -1217,40 +1241,33 @@ extern "C" int spg_msm_partial(spg_ctx* ctx, const spg_gens* g, size_t gen_offse
     memcpy(out_ext, &id, sizeof(Ext));
     return SPG_OK;
   }
-  hipStream_t s = ctx->stream;
-  Fq* d_s = (Fq*)ws_get(ctx, 0, n * sizeof(Fq) + sizeof(Ext) + 64);
+  Fq* d_s = (Fq*)ws_get(ctx, 0, n * sizeof(Fq) + 64);
   if (!d_s) return set_err(ctx, SPG_E_NOMEM, "scalar upload");
-  Ext* d_ext = (Ext*)(d_s + n);
-  SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars_mont, n * sizeof(Fq), hipMemcpyHostToDevice, s));
-  if (n > kSmallMaxN && use_big()) {  // msm_big.hip; the host point's coordinates as canonical bytes
-    h::HExt r;
-    timer_start(ctx);
-    int rc = msm_single_big(ctx, g, gen_offset, d_s, n, nullptr, &r);
-    timer_stop(ctx);
-    if (rc) return rc;
-    h::fe_to_bytes(r.X, out_ext);
-    h::fe_to_bytes(r.Y, out_ext + 32);
-    h::fe_to_bytes(r.Z, out_ext + 64);
-    h::fe_to_bytes(r.T, out_ext + 96);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-    ctx->last_us = ms * 1000.0;
+  SPG_HIP(ctx, hipMemcpyAsync(d_s, scalars_mont, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+  return msm_partial_dev(ctx, g, gen_offset, d_s, n, out_ext);
+}
+
+// the same over scalars already resident in HBM: buf[offset .. offset + n)
+extern "C" int spg_msm_partial_buf(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const spg_buf* buf,
+                                   size_t offset, size_t n, uint8_t out_ext[128]) {
+  if (!ctx || !g || !buf || !out_ext) return SPG_E_ARG;
+  if (offset > buf->n || n > buf->n - offset) return set_err(ctx, SPG_E_ARG, "msm_partial_buf: range past the buffer");
+  if (gen_offset + n > g->n) return set_err(ctx, SPG_E_ARG, "MSM longer than the generator set");
+  if (n == 0) {
+    const Ext id = ext_identity();
+    memcpy(out_ext, &id, sizeof(Ext));
     return SPG_OK;
   }
-  timer_start(ctx);
-  int rc = n <= kSmallMaxN ? msm_small_device(ctx, g, gen_offset, d_s, n, 1, nullptr, d_ext, nullptr, -1)
-                           : msm_batch_device(ctx, g, gen_offset, d_s, n, 1, nullptr, nullptr, nullptr, -1, d_ext);
+  return msm_partial_dev(ctx, g, gen_offset, buf->d + offset, n, out_ext);
+}
+
+// GroupElement::vartime_multiscalar_mul over resident scalars, compressed
+extern "C" int spg_msm_buf(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const spg_buf* buf, size_t offset,
+                           size_t n, uint8_t out[32]) {
+  uint8_t ext[128];
+  const int rc = spg_msm_partial_buf(ctx, g, gen_offset, buf, offset, n, ext);
   if (rc) return rc;
-  timer_stop(ctx);
-  Ext r;
-  SPG_HIP(ctx, hipMemcpyAsync(&r, d_ext, sizeof(Ext), hipMemcpyDeviceToHost, s));
-  SPG_HIP(ctx, hipStreamSynchronize(s));
-  static_assert(sizeof(Ext) == 128, "Ext is X, Y, Z, T of 32 bytes");
-  memcpy(out_ext, &r, sizeof(Ext));
-  float ms = 0.f;
-  hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
-  ctx->last_us = ms * 1000.0;
-  return SPG_OK;
+  return spg_points_sum_compress(ext, 1, out);
 }
 
 // host only (no device): sum of k partial points (X, Y, Z, T; 32 little-endian bytes each, any representative

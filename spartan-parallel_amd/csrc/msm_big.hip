@@ -9,13 +9,14 @@
 // chip full or a short dependent chain (c = 11 by default: 1024 buckets, 24 windows):
 //   k_big_digits   block-local LDS histograms of the signed digits (digits kept in HBM as int16)
 //   hipcub scan    over the [bucket][block] histogram matrix: each (bucket, block) pair's entry range
-//   k_big_scatter  counting-sort scatter of (table index | sign) into bucket order, LDS cursors
-//   k_big_chunks   one workgroup's work list: bucket v split into chunks of <= CH entries (skewed scalars only
-//                  lengthen the list, never a workgroup)
-//   k_big_accum    one workgroup per chunk: 64 quads (4 lanes per point, quad.hpp) each add ~CH/64 table entries,
-//                  then an LDS tree -> the chunk's sum; the workgroup finishing the last chunk of a group of 64
-//                  buckets then reduces that group: bucket sums from their chunks, a suffix scan and a tree give
-//                  W_g = sum_j (j + 1) B_{64 g + j} and G_g = sum_j B_{64 g + j}
+//   k_big_scatter  counting-sort scatter of (table index | sign) into bucket order, LDS cursors; its block 0 also
+//                  writes the accumulation's work list: bucket v split into chunks of <= CH entries (skewed scalars
+//                  only lengthen the list, never a workgroup)
+//   k_big_accum    one workgroup per chunk: each lane adds every 256th entry of the chunk (one-lane mixed
+//                  additions), the 256 lane sums meet in LDS (quad.hpp: 4 lanes per point) -> the chunk's sum; the
+//                  workgroup finishing the last chunk of a group of 64 buckets then reduces that group: bucket sums
+//                  from their chunks, a suffix scan and a tree give W_g = sum_j (j + 1) B_{64 g + j} and
+//                  G_g = sum_j B_{64 g + j}
 //   host           sum_v v B_v = sum_g W_g + 64 sum_g g G_g over the NB/64 groups (radix-2^51 additions at ~0.1 us
 //                  each on a host core, where one dependent GPU addition costs ~2 us), then the encoding.
 #include <hipcub/hipcub.hpp>
@@ -32,7 +33,7 @@ namespace spg {
 
 namespace {
 
-// workspace slots 100..107 (msm.hip 0..18, proto.hip 20..24, r1cs.hip 30.., spark.hip 60.., snark / verify 91..96)
+// workspace slots 100..108 (msm.hip 0..18, proto.hip 20..24, r1cs.hip 30.., spark.hip 60.., snark / verify 91..96)
 constexpr int kBigBS = 256;      // threads per workgroup (64 quads)
 constexpr int kBigQuads = kBigBS / 4;
 constexpr int kBigGroup = 64;    // buckets per group reduction (big_group)
@@ -48,6 +49,10 @@ struct BigArgs {
   uint32_t* bh;     // [NB][G] block histograms (+ a zero at [NB * G])
   uint32_t* off;    // their exclusive scan: the entry range of each (bucket, block); off[NB * G] = total
   uint32_t* entries;
+};
+
+struct Chunk {
+  uint32_t key, start, len, pad;
 };
 
 template <int C>
@@ -80,12 +85,55 @@ __global__ void __launch_bounds__(kBigBS) k_big_digits(BigArgs a) {
   if (blk == 0 && t == 0) a.bh[(size_t)NB * a.G] = 0;
 }
 
+// one workgroup of BS threads: bucket v = key + 1 holds entries [bh[key G], bh[(key + 1) G]); it becomes
+// ceil(count / ch) chunks; first[key] = its first chunk, first[NB] = the number of chunks
+template <int BS>
+__device__ __forceinline__ void big_chunks(const uint32_t* __restrict__ bh, int G, int NB, uint32_t ch,
+                                           Chunk* __restrict__ chunks, uint32_t* __restrict__ first,
+                                           unsigned* __restrict__ gcnt, Ext* __restrict__ out, uint32_t* part) {
+  const int t = threadIdx.x;
+  const int per_t = (NB + BS - 1) / BS, k0 = t * per_t, k1 = min(NB, k0 + per_t);
+  uint32_t mine = 0;
+  for (int k = k0; k < k1; k++) {
+    const uint32_t c = bh[(size_t)(k + 1) * G] - bh[(size_t)k * G];
+    mine += (c + ch - 1) / ch;
+  }
+  part[t] = mine;
+  __syncthreads();
+  for (int s = 1; s < BS; s <<= 1) {  // inclusive Hillis-Steele scan of the per-thread chunk counts
+    const uint32_t x = t >= s ? part[t - s] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - mine;
+  for (int k = k0; k < k1; k++) {
+    const uint32_t s = bh[(size_t)k * G], c = bh[(size_t)(k + 1) * G] - s;
+    first[k] = run;
+    for (uint32_t o = 0; o < c; o += ch) chunks[run++] = Chunk{(uint32_t)k, s + o, min(ch, c - o), 0u};
+  }
+  if (t == BS - 1) first[NB] = part[BS - 1];
+  __syncthreads();
+  // the group tickets of k_big_accum, and the sums of groups no chunk will report (no entries at all)
+  for (int g = t; g < NB / kBigGroup; g += BS) {
+    gcnt[g] = 0u;
+    if (first[(g + 1) * kBigGroup] == first[g * kBigGroup]) out[2 * g] = out[2 * g + 1] = ext_identity();
+  }
+}
+
+// (block 0 also builds the accumulation's chunk list from the scanned histogram: one launch fewer)
 template <int C>
-__global__ void __launch_bounds__(kBigBS) k_big_scatter(BigArgs a) {
+__global__ void __launch_bounds__(kBigBS) k_big_scatter(BigArgs a, uint32_t ch, Chunk* __restrict__ chunks,
+                                                        uint32_t* __restrict__ first, unsigned* __restrict__ gcnt,
+                                                        Ext* __restrict__ out) {
   constexpr int W = 253 / C + 1;
   constexpr int NB = 1 << (C - 1);
   __shared__ uint32_t cur[NB];
   const int blk = blockIdx.x, t = threadIdx.x;
+  if (blk == 0) {
+    __shared__ uint32_t part[kBigBS];
+    big_chunks<kBigBS>(a.off, a.G, NB, ch, chunks, first, gcnt, out, part);
+  }
   for (int k = t; k < NB; k += kBigBS) cur[k] = a.off[(size_t)k * a.G + blk];
   __syncthreads();
   const int i0 = blk * a.spb, i1 = min(a.per, i0 + a.spb);
@@ -99,46 +147,6 @@ __global__ void __launch_bounds__(kBigBS) k_big_scatter(BigArgs a) {
         a.entries[slot] = ((uint32_t)(w * C) * (uint32_t)a.n1 + gidx) | (d < 0 ? 0x80000000u : 0u);
       }
     }
-  }
-}
-
-struct Chunk {
-  uint32_t key, start, len, pad;
-};
-
-// one 1024-thread block: bucket v = key + 1 holds entries [bh[key G], bh[(key + 1) G]); it becomes
-// ceil(count / ch) chunks; first[key] = its first chunk, first[NB] = the number of chunks
-__global__ void __launch_bounds__(1024) k_big_chunks(const uint32_t* __restrict__ bh, int G, int NB, uint32_t ch,
-                                                     Chunk* __restrict__ chunks, uint32_t* __restrict__ first,
-                                                     unsigned* __restrict__ gcnt, Ext* __restrict__ out) {
-  __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  const int per_t = (NB + 1023) / 1024, k0 = t * per_t, k1 = min(NB, k0 + per_t);
-  uint32_t mine = 0;
-  for (int k = k0; k < k1; k++) {
-    const uint32_t c = bh[(size_t)(k + 1) * G] - bh[(size_t)k * G];
-    mine += (c + ch - 1) / ch;
-  }
-  part[t] = mine;
-  __syncthreads();
-  for (int s = 1; s < 1024; s <<= 1) {  // inclusive Hillis-Steele scan of the per-thread chunk counts
-    const uint32_t x = t >= s ? part[t - s] : 0u;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - mine;
-  for (int k = k0; k < k1; k++) {
-    const uint32_t s = bh[(size_t)k * G], c = bh[(size_t)(k + 1) * G] - s;
-    first[k] = run;
-    for (uint32_t o = 0; o < c; o += ch) chunks[run++] = Chunk{(uint32_t)k, s + o, min(ch, c - o), 0u};
-  }
-  if (t == 1023) first[NB] = part[1023];
-  __syncthreads();
-  // the group tickets of k_big_accum, and the sums of groups no chunk will report (no entries at all)
-  if (t < NB / kBigGroup) {
-    gcnt[t] = 0u;
-    if (first[(t + 1) * kBigGroup] == first[t * kBigGroup]) out[2 * t] = out[2 * t + 1] = ext_identity();
   }
 }
 
@@ -173,18 +181,26 @@ __device__ __forceinline__ void big_group(int g, const Ext* __restrict__ sums, c
   if (t == 0) out[2 * g] = acc;
 }
 
-// one workgroup (64 quads) per chunk; grid = an upper bound of the chunk count. The workgroup that finishes the last
-// chunk of a group of 64 buckets (ticket gcnt[g]) goes on to that group's reduction (big_group): no second launch,
-// and the groups reduce while other chunks still accumulate.
+// one workgroup per chunk; grid = an upper bound of the chunk count. The workgroup that finishes the last chunk
+// of a group of 64 buckets (ticket gcnt[g]) goes on to that group's reduction (big_group): no second launch, and
+// the groups reduce while other chunks still accumulate.
+//   LANE = false: 64 quads (4 lanes per point, quad.hpp) each add ~CH/64 table entries.
+//   LANE = true (default, SPG_BIG_ITEMS=0 selects the other): every lane adds every 256th entry of the chunk in
+//     one-lane mixed additions (~6 at c = 11 on random scalars: one chunk per bucket; the one-lane form issues
+//     ~1.5x fewer instructions per addition than the quad split: 3.0e10 vs 2.0e10 madd/s whole-chip in
+//     scripts/micro/ext_throughput), then the 256 lane sums meet in LDS: quad j adds sums 4j .. 4j + 3.
+// Either way an LDS quad tree then gives the chunk's sum.
 // Cross-XCD hand-off as in grid_reduce3 (sumcheck.hip): plain stores + agent-scope release before the ticket,
 // agent-scope acquire in the reducer before plain loads (the per-XCD L2s are not coherent).
-__global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ chunks,
-                                                      const uint32_t* __restrict__ first,
-                                                      const uint32_t* __restrict__ entries,
-                                                      const Niels* __restrict__ tab, Ext* __restrict__ sums,
-                                                      unsigned* __restrict__ gcnt, Ext* __restrict__ out, int NB,
-                                                      unsigned long long* probe) {
-  __shared__ uint32_t pts[soa_words<Ext, kBigQuads>()];
+template <bool LANE>
+__global__ void __launch_bounds__(kBigBS, 4) k_big_accum(const Chunk* __restrict__ chunks,
+                                                         const uint32_t* __restrict__ first,
+                                                         const uint32_t* __restrict__ entries,
+                                                         const Niels* __restrict__ tab, Ext* __restrict__ sums,
+                                                         unsigned* __restrict__ gcnt, Ext* __restrict__ out, int NB,
+                                                         unsigned long long* probe) {
+  // LANE: the lane sums (SoA over 256), then the quad tree's operands; else the quad tree's operands only
+  __shared__ uint32_t pts[LANE ? soa_words<Ext, kBigBS>() : soa_words<Ext, kBigQuads>()];
   __shared__ bool last;
   const uint32_t cid = blockIdx.x;
   if (cid >= first[NB]) return;  // whole workgroups exit together
@@ -192,20 +208,36 @@ __global__ void __launch_bounds__(kBigBS) k_big_accum(const Chunk* __restrict__ 
   if (probe && t == 0) probe[4 * cid] = wall_clock64();
   const Chunk c = chunks[cid];
   Ext acc = ext_identity();
-  // software-pipelined: the table coordinate of entry e + 64 is loaded while entry e is added
-  uint32_t e = slot;
-  Fp qv;
-  bool neg = false;
-  if (e < c.len) qv = niels_coord(tab, entries[c.start + e], q, &neg);
-  while (e < c.len) {
-    const uint32_t e2 = e + kBigQuads;
-    Fp qn;
-    bool nn = false;
-    if (e2 < c.len) qn = niels_coord(tab, entries[c.start + e2], q, &nn);
-    acc = quad_madd(acc, qv, neg, q);
-    qv = qn;
-    neg = nn;
-    e = e2;
+  if (LANE) {
+    Ext P = ext_identity();
+    if ((uint32_t)t < c.len) {
+      P = load_signed(tab, entries[c.start + t]);
+      for (uint32_t e = t + kBigBS; e < c.len; e += kBigBS) {
+        const uint32_t x = entries[c.start + e];
+        P = ext_madd(P, tab[x & 0x7fffffffu], (x >> 31) != 0);
+      }
+    }
+    soa_put<kBigBS>(pts, t, P);
+    __syncthreads();
+    acc = soa_get<kBigBS, Ext>(pts, 4 * slot);
+    for (int k = 1; k < 4; k++) acc = quad_add(acc, soa_get<kBigBS, Ext>(pts, 4 * slot + k), q);
+    __syncthreads();
+  } else {
+    // software-pipelined: the table coordinate of entry e + 64 is loaded while entry e is added
+    uint32_t e = slot;
+    Fp qv;
+    bool neg = false;
+    if (e < c.len) qv = niels_coord(tab, entries[c.start + e], q, &neg);
+    while (e < c.len) {
+      const uint32_t e2 = e + kBigQuads;
+      Fp qn;
+      bool nn = false;
+      if (e2 < c.len) qn = niels_coord(tab, entries[c.start + e2], q, &nn);
+      acc = quad_madd(acc, qv, neg, q);
+      qv = qn;
+      neg = nn;
+      e = e2;
+    }
   }
   if (probe) {
     __syncthreads();
@@ -250,9 +282,13 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
   constexpr int NB = 1 << (C - 1);
   hipStream_t s = ctx->stream;
   const size_t E = (size_t)a.per * W;
-  // chunk size: the mean bucket load rounded up to whole passes of the 64 quads (random scalars: about one chunk
-  // per bucket), at least 2 entries per quad
-  const uint32_t ch = (uint32_t)std::max<size_t>(2 * kBigQuads, ((E / NB + kBigQuads - 1) / kBigQuads + 1) * kBigQuads);
+  static const bool lane = !getenv("SPG_BIG_ITEMS") || atoi(getenv("SPG_BIG_ITEMS")) != 0;
+  // chunk size: the mean bucket load rounded up to whole passes of the 64 quads (random scalars: about one chunk per
+  // bucket), at least 2 entries per quad; the lane form takes up to 8 entries per lane (a bucket with more -- skewed
+  // scalars -- splits into several chunks)
+  const uint32_t ch = lane ? 8 * kBigBS
+                           : (uint32_t)std::max<size_t>(2 * kBigQuads,
+                                                        ((E / NB + kBigQuads - 1) / kBigQuads + 1) * kBigQuads);
   const size_t max_chunks = E / ch + NB + 1;
   a.digits = (int16_t*)ws_get(ctx, 100, E * sizeof(int16_t) + 64);
   a.bh = (uint32_t*)ws_get(ctx, 101, ((size_t)NB * a.G + 1) * 4 + 64);
@@ -272,9 +308,7 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
     KScope ks(ctx, "msm_big_sort");
     hipLaunchKernelGGL(k_big_digits<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
     SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, a.bh, a.off, nkeys, s));
-    hipLaunchKernelGGL(k_big_scatter<C>, dim3(a.G), dim3(kBigBS), 0, s, a);
-    hipLaunchKernelGGL(k_big_chunks, dim3(1), dim3(1024), 0, s, a.off, a.G, NB, ch, chunks, first, gcnt,
-                       host_groups_dev);
+    hipLaunchKernelGGL(k_big_scatter<C>, dim3(a.G), dim3(kBigBS), 0, s, a, ch, chunks, first, gcnt, host_groups_dev);
   }
   // SPG_BIG_PROBE=1: per-workgroup phase timestamps of the accumulation (+ group reductions), on stderr
   static const bool probe_on = getenv("SPG_BIG_PROBE") != nullptr;
@@ -285,8 +319,12 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
   }
   {
     KScope ks(ctx, "msm_big_accum", 0.0, (double)a.per * W * (1.0 - 1.0 / (double)(1 << C)));
-    hipLaunchKernelGGL(k_big_accum, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first, a.entries,
-                       g->table, sums, gcnt, host_groups_dev, NB, pa);
+    if (lane)
+      hipLaunchKernelGGL(k_big_accum<true>, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first, a.entries,
+                         g->table, sums, gcnt, host_groups_dev, NB, pa);
+    else
+      hipLaunchKernelGGL(k_big_accum<false>, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first,
+                         a.entries, g->table, sums, gcnt, host_groups_dev, NB, pa);
   }
   SPG_HIP(ctx, hipGetLastError());
   if (probe_on) {

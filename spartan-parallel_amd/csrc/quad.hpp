@@ -75,6 +75,17 @@ __device__ __forceinline__ Fp niels_coord(const Niels* __restrict__ tab, uint32_
   const int which = q >= 2 ? 2 : ((q == 0) != *neg ? 1 : 0);  // Niels field order: ypx, ymx, t2d
   return reinterpret_cast<const Fp*>(tab + (ent & 0x7fffffffu))[which];
 }
+// table entry (index | sign << 31) as an extended point, negated when the sign bit is set
+__device__ __forceinline__ Ext load_signed(const Niels* __restrict__ tab, uint32_t e) {
+  Niels q = tab[e & 0x7fffffffu];
+  if (e >> 31) {
+    Fp t = q.ypx;
+    q.ypx = q.ymx;
+    q.ymx = t;
+    q.t2d = fp_neg(q.t2d);
+  }
+  return niels_to_ext(q);
+}
 // P + (+-Niels); qv is this lane's Niels coordinate: lane 0 the "minus" one (neg ? ypx : ymx), lane 1 the
 // "plus" one (neg ? ymx : ypx), lane 2 t2d (lane 3 ignores it); -Q has C negated (cneg)
 __device__ __forceinline__ Ext quad_madd(const Ext& P, const Fp& qv, bool neg, int q) {

@@ -615,6 +615,7 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     const bool sharded = W > 1 && layer < lgm;
     const size_t hl = sharded ? half / W : half;  // entries of each vector held here
     int rc = fail;
+    if (!rc && sharded && failpoint(ctx, "spark_layer")) rc = set_err(ctx, SPG_E_HIP, "failpoint spark_layer");
     int cur = 0;  // the buffer holding the shared eq vector C
     const bool with_dotp = layer == 0 && !dotp.empty();
     std::vector<Triple> tr;

@@ -45,3 +45,12 @@ def gpu_partial(gens, scalars):
         return gens.msm_partial(s[lo:hi], gen_offset=lo)
 
     return f
+
+
+def gpu_partial_resident(gens, buf):
+    """partial(lo, hi) over a device generator set and device-resident scalars (a spg.Buf uploaded once)"""
+
+    def f(lo, hi):
+        return gens.msm_partial_buf(buf, offset=lo, n=hi - lo, gen_offset=lo)
+
+    return f

@@ -254,6 +254,24 @@ class Gens:
         self.ctx.check(rc, "spg_msm_partial")
         return out.tobytes()
 
+    def msm_partial_buf(self, buf, offset=0, n=None, gen_offset=0):
+        """spg_msm_partial_buf: the partial sum of scalars already resident in HBM (a Buf), 128 bytes"""
+        n = buf.n - offset if n is None else n
+        out = np.zeros(128, dtype=np.uint8)
+        rc = lib().spg_msm_partial_buf(self.ctx.handle, self._h, ctypes.c_size_t(gen_offset), buf._h,
+                                       ctypes.c_size_t(offset), ctypes.c_size_t(n), _p(out))
+        self.ctx.check(rc, "spg_msm_partial_buf")
+        return out.tobytes()
+
+    def msm_buf(self, buf, offset=0, n=None, gen_offset=0):
+        """spg_msm_buf: vartime_multiscalar_mul of resident scalars, 32-byte compression"""
+        n = buf.n - offset if n is None else n
+        out = np.zeros(32, dtype=np.uint8)
+        rc = lib().spg_msm_buf(self.ctx.handle, self._h, ctypes.c_size_t(gen_offset), buf._h, ctypes.c_size_t(offset),
+                               ctypes.c_size_t(n), _p(out))
+        self.ctx.check(rc, "spg_msm_buf")
+        return out.tobytes()
+
     def commit_rows(self, Z, L, R, blinds=None):
         z = _scalars(Z)
         assert z.shape[0] == L * R

@@ -100,8 +100,12 @@ SPARK_SHARD_CASES = {  # (R1CS shape as in r1cs_cases, world sizes)
 }
 
 
-def _spark_worker(rank, world, port, case, q):
+def _spark_worker(rank, world, port, case, q, failpoint=None):
     import sys
+
+    if failpoint:  # read by libspg at its first check (tests only): this rank fails inside a sharded layer
+        os.environ["SPG_FAILPOINT"] = failpoint
+        os.environ["SPG_FAILPOINT_RANK"] = str(world - 1)
 
     sys.path[:0] = [os.path.join(ROOT, "spartan-parallel_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
     import torch.distributed as dist
@@ -174,6 +178,24 @@ def test_sharded_spark_matches_oracle(oracle, case, world):
         assert err is None, err
         assert cm == rcomm, f"rank {rank} commitment differs"
         assert pf == ref, f"rank {rank} proof differs"
+
+
+def test_sharded_spark_rank_failure_fails_every_rank():
+    """a failure on one rank inside a sharded SPARK layer (test failpoint) reaches every rank through the next
+    exchange (skip mode): all ranks return an error, none blocks in a collective"""
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_spark_worker, args=(r, world, port, "p2_x64_2secs", qq, "spark_layer"))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([qq.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for rank, _, _, pf, err in res:
+        assert pf is None and err, f"rank {rank} did not fail: {res}"
 
 
 # ---- libspg's own RCCL transport (spg_set_comm_rccl) ----------------------------------------------------------

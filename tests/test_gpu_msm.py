@@ -212,3 +212,54 @@ def test_msm_big_windows(oracle, c):
     s = rand_fq(oracle, rng, n)
     pts = oracle.gens_stream(b"spg_bench_msm", n + 1)
     assert out.stdout.split()[-1] == oracle.msm(pts[:n], s).hex()
+
+
+def test_msm_resident_scalars(ctx, oracle):
+    """spg_msm_buf / spg_msm_partial_buf over scalars uploaded once (the config-2 bench's entry points) give the
+    oracle's MSM: whole vector (large path), shards that add up, a small range (latency path), empty and bad ranges"""
+    import spg
+
+    n = 1 << 16
+    g = spg.Gens(ctx, n, b"spg_bench_msm")
+    rng = np.random.default_rng(11)
+    s = rand_fq(oracle, rng, n)
+    buf = spg.Buf(ctx, s)
+    pts = oracle.gens_stream(b"spg_bench_msm", n + 1)
+    ref = oracle.msm(pts[:n], s)
+    assert g.msm_buf(buf) == ref
+    cuts = [0, 1000, 1001, 40000, n]
+    parts = [g.msm_partial_buf(buf, offset=lo, n=hi - lo, gen_offset=lo) for lo, hi in zip(cuts, cuts[1:])]
+    assert spg.points_sum_compress(parts) == ref
+    assert g.msm_buf(buf, offset=7, n=300, gen_offset=7) == oracle.msm(pts[7:307], s[7:307])
+    assert g.msm_buf(buf, offset=5, n=0) == bytes(32)
+    with pytest.raises(spg.SpgError):
+        g.msm_buf(buf, offset=n - 10, n=11)
+
+
+@pytest.mark.parametrize("form", ["0", "1"])
+def test_msm_big_accumulation_forms(oracle, form):
+    """both accumulation forms of the large-MSM path (SPG_BIG_ITEMS: 0 quad chunks, 1 lane-then-quad buckets)
+    give the oracle's 2^16 MSM, skewed scalars included"""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 1 << 16
+    code = (
+        "import sys, numpy as np; sys.path[:0] = [%r, %r]\n"
+        "import spg, pyoracle\n"
+        "ctx = spg.Context(0)\n"
+        "g = spg.Gens(ctx, %d, b'spg_bench_msm')\n"
+        "rng = np.random.default_rng(5)\n"
+        "s = pyoracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * %d, dtype=np.uint8).tobytes())\n"
+        "s[: %d // 2] = s[0]\n"  # half the scalars equal: every window's digit repeats (one bucket per window)
+        "print(g.msm(s).hex())\n"
+    ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "oracle"), n, n, n)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_ITEMS=form), capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rng = np.random.default_rng(5)
+    s = rand_fq(oracle, rng, n)
+    s[: n // 2] = s[0]
+    pts = oracle.gens_stream(b"spg_bench_msm", n + 1)
+    assert out.stdout.split()[-1] == oracle.msm(pts[:n], s).hex()
