@@ -347,6 +347,7 @@ extern "C" int spg_free(spg_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   if (c->comm_owned_free) c->comm_owned_free(c->comm_owned);
+  if (c->wt_cache) spg_r1cs_witness_free(c, c->wt_cache);
   for (auto& s : c->ws)
     if (s.p) hipFree(s.p);
   if (c->pinned) hipHostFree(c->pinned);

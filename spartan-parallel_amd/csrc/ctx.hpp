@@ -40,6 +40,9 @@ struct spg_ctx {
   // a transport the library owns (spg_set_comm_rccl), released by the next spg_set_comm* or spg_free
   void* comm_owned = nullptr;
   void (*comm_owned_free)(void*) = nullptr;
+  // SNARK::prove's per-prove witness sections (pairwise / perm-root R1CSProofs): kept between proves, refilled in
+  // place, so a prove allocates and frees no device memory (a hipFree synchronises the device: ~0.2 ms)
+  spg_r1cs_witness* wt_cache = nullptr;
   double last_us = 0.0;
   std::string err;
   // workspace slots: grown on demand, reused across calls (no allocation in steady state)

@@ -135,7 +135,17 @@ class Pool {
       cv_.notify_all();
     }
     work(g, &f, n);
-    while (remaining_.load() > 0) std::this_thread::yield();
+    // the workers finish within microseconds: spin (a yield is a system call that may still be running when the
+    // last task ends), yielding only after ~50k polls
+    for (unsigned k = 0; remaining_.load() > 0; k++) {
+      if (k < 50000) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      } else {
+        std::this_thread::yield();
+      }
+    }
   }
 
  private:
