@@ -356,32 +356,63 @@ SPG_HD Fq fq_from_u64(uint64_t x) {
   return fq_to_mont(t);
 }
 #if !defined(__HIP_DEVICE_COMPILE__)
-// Host inverse by the binary extended Euclidean algorithm on 4 x 64-bit limbs: ~5x faster than the
-// Fermat chain below on a CPU. Variable time, which is fine here: the prover only inverts public
-// Fiat-Shamir challenges (BulletReductionProof's u, src/nizk/bullet.rs:100). Same value as Scalar::invert
-// (src/scalar/ristretto255.rs:541-595); 0 maps to 0 like the Fermat chain.
+// Host inverse: Kaliski's almost-Montgomery inverse on 4 x 64-bit limbs, runs of trailing zeros shifted out at
+// once (__builtin_ctzll). Invariant q = u s + v r; it ends with r' = am^-1 2^k mod q, n <= k <= 2n, and one
+// Montgomery product with the precomputed R^3 2^-k turns that into (a^-1) R for am = a R. Variable time, which is
+// fine here: the prover only inverts public Fiat-Shamir challenges (BulletReductionProof's u, src/nizk/bullet.rs:100).
+// Same value as Scalar::invert (src/scalar/ristretto255.rs:541-595); 0 maps to 0 like the Fermat chain.
+// tests/test_product_host.py::test_fq_ops[invert] checks it against the oracle.
+struct FqInvTable {
+  Fq c[512];  // c[k] = R^3 2^-k mod q (Montgomery form of R^2 2^-k)
+  FqInvTable() {
+    typedef unsigned __int128 u128;
+    static const uint64_t q[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0ULL, 0x1000000000000000ULL};
+    // x = R^3 mod q: fq_r2() is R^2 mod q in plain limbs; R^3 = fq_mul(R^2, R^2) (Montgomery: R^4 R^-1)
+    const Fq r3 = fq_mul(fq_r2(), fq_r2());
+    uint64_t x[4];
+    for (int i = 0; i < 4; i++) x[i] = (uint64_t)r3.l[2 * i] | ((uint64_t)r3.l[2 * i + 1] << 32);
+    for (int k = 0; k < 512; k++) {
+      for (int i = 0; i < 4; i++) {
+        c[k].l[2 * i] = (uint32_t)x[i];
+        c[k].l[2 * i + 1] = (uint32_t)(x[i] >> 32);
+      }
+      if (x[0] & 1) {  // x + q (x < q < 2^253: no overflow)
+        u128 cy = 0;
+        for (int i = 0; i < 4; i++) {
+          cy += (u128)x[i] + q[i];
+          x[i] = (uint64_t)cy;
+          cy >>= 64;
+        }
+      }
+      for (int i = 0; i < 3; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 63);
+      x[3] >>= 1;
+    }
+  }
+};
 inline Fq fq_inv_host(const Fq& am) {
   typedef unsigned __int128 u128;
   static const uint64_t q[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0ULL, 0x1000000000000000ULL};
-  const Fq c = fq_from_mont(am);
-  uint64_t u[4], v[4] = {q[0], q[1], q[2], q[3]}, x1[4] = {1, 0, 0, 0}, x2[4] = {0, 0, 0, 0};
-  for (int i = 0; i < 4; i++) u[i] = (uint64_t)c.l[2 * i] | ((uint64_t)c.l[2 * i + 1] << 32);
-  if ((u[0] | u[1] | u[2] | u[3]) == 0) return fq_zero();
-  auto is_one = [](const uint64_t* a) { return a[0] == 1 && (a[1] | a[2] | a[3]) == 0; };
-  auto geq = [](const uint64_t* a, const uint64_t* b) {
-    for (int i = 3; i >= 0; i--)
-      if (a[i] != b[i]) return a[i] > b[i];
-    return true;
+  static const FqInvTable tab;
+  uint64_t u[4] = {q[0], q[1], q[2], q[3]}, v[4], r[4] = {0, 0, 0, 0}, s[4] = {1, 0, 0, 0};
+  for (int i = 0; i < 4; i++) v[i] = (uint64_t)am.l[2 * i] | ((uint64_t)am.l[2 * i + 1] << 32);
+  if ((v[0] | v[1] | v[2] | v[3]) == 0) return fq_zero();
+  auto shr = [](uint64_t* a, int t) {  // 0 < t < 64
+    for (int i = 0; i < 3; i++) a[i] = (a[i] >> t) | (a[i + 1] << (64 - t));
+    a[3] >>= t;
   };
-  auto sub = [](uint64_t* a, const uint64_t* b) {  // a -= b (no underflow by construction)
+  auto shl = [](uint64_t* a, int t) {  // 0 < t < 64, no overflow by the invariant (r, s < 2q < 2^254)
+    for (int i = 3; i > 0; i--) a[i] = (a[i] << t) | (a[i - 1] >> (64 - t));
+    a[0] <<= t;
+  };
+  auto sub = [](uint64_t* a, const uint64_t* b) {  // a -= b, a >= b
     uint64_t bw = 0;
     for (int i = 0; i < 4; i++) {
-      u128 d = (u128)a[i] - b[i] - bw;
+      const u128 d = (u128)a[i] - b[i] - bw;
       a[i] = (uint64_t)d;
       bw = (uint64_t)(d >> 64) & 1;
     }
   };
-  auto add = [](uint64_t* a, const uint64_t* b) {  // a += b (sum < 2^256)
+  auto add = [](uint64_t* a, const uint64_t* b) {  // a += b, no overflow
     u128 cy = 0;
     for (int i = 0; i < 4; i++) {
       cy += (u128)a[i] + b[i];
@@ -389,31 +420,56 @@ inline Fq fq_inv_host(const Fq& am) {
       cy >>= 64;
     }
   };
-  auto shr1 = [](uint64_t* a) {
-    for (int i = 0; i < 3; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 63);
-    a[3] >>= 1;
+  auto gt = [](const uint64_t* a, const uint64_t* b) {
+    for (int i = 3; i >= 0; i--)
+      if (a[i] != b[i]) return a[i] > b[i];
+    return false;
   };
-  auto half_mod = [&](uint64_t* x) {  // x / 2 mod q (x < q < 2^253, so x + q does not overflow)
-    if (x[0] & 1) add(x, q);
-    shr1(x);
+  auto ctz = [](const uint64_t* a) {  // a != 0
+    for (int i = 0; i < 4; i++)
+      if (a[i]) return 64 * i + __builtin_ctzll(a[i]);
+    return 256;
   };
-  auto sub_mod = [&](uint64_t* a, const uint64_t* b) {  // a = a - b mod q (a, b < q)
-    if (!geq(a, b)) add(a, q);
-    sub(a, b);
-  };
-  while (!is_one(u) && !is_one(v)) {
-    while (!(u[0] & 1)) { shr1(u); half_mod(x1); }
-    while (!(v[0] & 1)) { shr1(v); half_mod(x2); }
-    if (geq(u, v)) { sub(u, v); sub_mod(x1, x2); }
-    else { sub(v, u); sub_mod(x2, x1); }
+  int k = 0;
+  while (v[0] | v[1] | v[2] | v[3]) {
+    if (!(u[0] & 1)) {
+      for (int t = ctz(u); t > 0; t -= 63) {
+        const int c = t < 63 ? t : 63;
+        shr(u, c);
+        shl(s, c);
+        k += c;
+      }
+    } else if (!(v[0] & 1)) {
+      for (int t = ctz(v); t > 0; t -= 63) {
+        const int c = t < 63 ? t : 63;
+        shr(v, c);
+        shl(r, c);
+        k += c;
+      }
+    } else if (gt(u, v)) {
+      sub(u, v);
+      shr(u, 1);
+      add(r, s);
+      shl(s, 1);
+      k++;
+    } else {
+      sub(v, u);
+      shr(v, 1);
+      add(s, r);
+      shl(r, 1);
+      k++;
+    }
   }
-  const uint64_t* r = is_one(u) ? x1 : x2;
-  Fq out;
+  if (!gt(q, r)) sub(r, q);  // r < q
+  uint64_t o[4] = {q[0], q[1], q[2], q[3]};
+  sub(o, r);  // am^-1 2^k mod q (r != 0 for am != 0)
+  Fq y;
   for (int i = 0; i < 4; i++) {
-    out.l[2 * i] = (uint32_t)r[i];
-    out.l[2 * i + 1] = (uint32_t)(r[i] >> 32);
+    y.l[2 * i] = (uint32_t)o[i];
+    y.l[2 * i + 1] = (uint32_t)(o[i] >> 32);
   }
-  return fq_to_mont(out);
+  // y = a^-1 R^-1 2^k; fq_mul(y, R^3 2^-k) = a^-1 R
+  return fq_mul(y, tab.c[k]);
 }
 #endif
 

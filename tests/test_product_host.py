@@ -34,7 +34,7 @@ def rand_fq(oracle, rng, n):
                                      ("mul", 8), ("mul", 9)])  # 8, 9: the device's product-scanning and CIOS forms
 def test_fq_ops(oracle, hc, op, code):
     rng = np.random.default_rng(code)
-    n = 4000 if code != 5 else 200
+    n = 4000 if code != 5 else 2000
     a, b = rand_fq(oracle, rng, n), rand_fq(oracle, rng, n)
     a[0] = 0
     a[1] = oracle.fq_from_u64(1)
@@ -42,6 +42,9 @@ def test_fq_ops(oracle, hc, op, code):
     a[3] = b[3] = oracle.fq_op("neg", oracle.fq_from_u64(1))[0]  # (q-1)^2
     if code == 5:
         a[0] = oracle.fq_from_u64(3)
+        for i, x in enumerate([2, 4, 1 << 40, 12345678901234567]):  # long runs of trailing zeros
+            a[4 + i] = oracle.fq_from_u64(x)
+        a[8] = oracle.fq_op("neg", oracle.fq_from_u64(2))[0]
     out = np.zeros_like(a)
     hc.spgh_fq_op(code, _p(a), _p(b), _p(out), ctypes.c_size_t(n))
     ref = oracle.fq_op(op, a, b) if op in ("add", "sub", "mul") else oracle.fq_op(op, a)
