@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out"
 export TMPDIR=/tmp
 cd /tmp
-BA="--steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+BA="--steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:---extras none}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- \
   python3 "$R/bench.py" $BA > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err" || exit $?
 echo "stats done"
