@@ -4,7 +4,7 @@
 VAR=$1; VALS=$2; REPS=${3:-3}; K=$4
 for r in $(seq $REPS); do
   for v in $VALS; do
-    env $VAR=$v timeout -k 5 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/b_ab.json 2>/dev/null || exit $?
+    env $VAR=$v timeout -k 5 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/b_ab.json 2>/dev/null || exit $?
     echo "$VAR=$v $(python -c 'import json,sys;d=json.load(open("gpurun_out/b_ab.json"));k=d["kernels"].get(sys.argv[1],{});print(d["ms_per_step"], d.get("ms_per_step_median"), d.get("ms_per_step_min"), "dev", d["device_busy_ms_per_step"], sys.argv[1], k.get("ms_per_step"), k.get("launches_per_step"))' $K)"
   done
 done

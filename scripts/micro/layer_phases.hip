@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <chrono>
 #include <vector>
@@ -15,6 +17,87 @@ using namespace spg;
 
 namespace spg {
 int set_err(spg_ctx*, int code, const std::string&) { return code; }
+}
+
+// the "armed" hand-off: the kernel of round i is launched before the host knows round i's challenge and waits
+// (thread 0, bounded) for a host-written doorbell carrying it; one workgroup (the K == 1 rounds of the prover)
+template <int BS>
+__global__ void __launch_bounds__(BS) k_armed(const uint32_t* __restrict__ db, uint32_t dseq, const Triple* __restrict__ tr,
+                                              const Fq* __restrict__ coeff, int nt, int log_len, int do_fold,
+                                              const Fq* __restrict__ cin, Fq* __restrict__ cout, uint32_t* __restrict__ mb,
+                                              uint32_t seq) {
+  __shared__ uint32_t rw[8];
+  __shared__ int go;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    const unsigned long long t0 = wall_clock64();
+    int ok = 1;
+    while (__hip_atomic_load(db, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != dseq) {
+      if (wall_clock64() - t0 > 200000000ull) {
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    for (int j = 0; j < 8; j++) rw[j] = __hip_atomic_load(db + 8 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    go = ok;
+  }
+  __syncthreads();
+  if (!go) return;
+  Fq r;
+  for (int j = 0; j < 8; j++) r.l[j] = rw[j];
+  Fq e = layer_round_elems(tr, coeff, nt, log_len, do_fold, r, cin, cout, t >> 2, BS / 4, nullptr);
+  quad_block_sum<BS>(e);
+  if (t < 3) {
+    for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  if (t == 0) __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int BS>
+static void run_armed(int nt, int log_len, Fq* cin, Fq* cout, Triple* dtr, Fq* dcoef, uint32_t* mb_dev,
+                      volatile uint32_t* mb_host, uint32_t* db_dev, volatile uint32_t* db_host) {
+  const int R = 40;
+  uint32_t seq = 50000, dseq = 0;
+  db_host[0] = 0;
+  for (int j = 0; j < 8; j++) db_host[8 + j] = 0x01234567u * (j + 3) & 0x0fffffffu;
+  hipDeviceSynchronize();
+  // launch round 1 armed; then per round: doorbell i, launch i + 1 armed, wait mailbox i, ~1 us of host work
+  hipLaunchKernelGGL(k_armed<BS>, dim3(1), dim3(BS), 0, 0, db_dev, dseq + 1, dtr, dcoef, nt, log_len, 1, cin, cout, mb_dev,
+                     seq + 1);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 1; i <= R; i++) {
+    __atomic_store_n(db_host, dseq + i, __ATOMIC_RELEASE);
+    if (i < R)
+      hipLaunchKernelGGL(k_armed<BS>, dim3(1), dim3(BS), 0, 0, db_dev, dseq + i + 1, dtr, dcoef, nt, log_len, 1, cin, cout,
+                         mb_dev, seq + i + 1);
+    while (__atomic_load_n(mb_host, __ATOMIC_ACQUIRE) != seq + (uint32_t)i) {
+    }
+    const auto h = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - h < std::chrono::microseconds(1)) {
+    }
+  }
+  const double rt = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
+  hipDeviceSynchronize();
+  // the same rounds with one launch per round after the host work (the prover's pattern), for comparison
+  t0 = std::chrono::steady_clock::now();
+  Fq r;
+  for (int j = 0; j < 8; j++) r.l[j] = 0x01234567u * (j + 3) & 0x0fffffffu;
+  for (int i = 1; i <= R; i++) {
+    const uint32_t s = seq + 1000 + i;
+    hipLaunchKernelGGL(k_layer_round_q<BS>, dim3(1), dim3(BS), 0, 0, dtr, dcoef, nt, log_len, 1, r, cin, cout, nullptr,
+                       nullptr, mb_dev, s, nullptr, 0);
+    while (__atomic_load_n(mb_host, __ATOMIC_ACQUIRE) != s) {
+    }
+    const auto h = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - h < std::chrono::microseconds(1)) {
+    }
+  }
+  const double rl = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
+  hipDeviceSynchronize();
+  printf("armed nt=%2d len=%4d BS=%3d: armed round %.1f us, launch-per-round %.1f us (1 us host work each)\n", nt,
+         1 << log_len, BS, rt, rl);
 }
 
 template <int BS, bool Q = false>
@@ -86,6 +169,16 @@ int main() {
   hipHostGetDevicePointer((void**)&mbd, mbh, 0);
   unsigned long long* probe;
   hipMalloc(&probe, 8 * 4096 * 8);
+  void* dbh;
+  uint32_t* dbd;
+  hipHostMalloc(&dbh, 4096, hipHostMallocCoherent | hipHostMallocMapped);
+  hipHostGetDevicePointer((void**)&dbd, dbh, 0);
+  for (int rep = 0; rep < 2; rep++) {
+    run_armed<64>(1, 0, cin, cout, dtr, dcoef, mbd, (volatile uint32_t*)mbh, dbd, (volatile uint32_t*)dbh);
+    run_armed<256>(8, 3, cin, cout, dtr, dcoef, mbd, (volatile uint32_t*)mbh, dbd, (volatile uint32_t*)dbh);
+    run_armed<256>(6, 5, cin, cout, dtr, dcoef, mbd, (volatile uint32_t*)mbh, dbd, (volatile uint32_t*)dbh);
+  }
+  if (getenv("ARMED_ONLY")) return 0;
   for (int fold = 0; fold < 2; fold++) {
     run<64, true>(1, 0, fold, 1, vec, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
     run<256, true>(8, 3, fold, 1, vec, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
