@@ -193,17 +193,11 @@ __device__ __forceinline__ void big_group(int g, const Ext* __restrict__ sums, c
 // Cross-XCD hand-off as in grid_reduce3 (sumcheck.hip): plain stores + agent-scope release before the ticket,
 // agent-scope acquire in the reducer before plain loads (the per-XCD L2s are not coherent).
 template <bool LANE>
-__global__ void __launch_bounds__(kBigBS, 4) k_big_accum(const Chunk* __restrict__ chunks,
-                                                         const uint32_t* __restrict__ first,
-                                                         const uint32_t* __restrict__ entries,
-                                                         const Niels* __restrict__ tab, Ext* __restrict__ sums,
-                                                         unsigned* __restrict__ gcnt, Ext* __restrict__ out, int NB,
-                                                         unsigned long long* probe) {
-  // LANE: the lane sums (SoA over 256), then the quad tree's operands; else the quad tree's operands only
-  __shared__ uint32_t pts[LANE ? soa_words<Ext, kBigBS>() : soa_words<Ext, kBigQuads>()];
-  __shared__ bool last;
-  const uint32_t cid = blockIdx.x;
-  if (cid >= first[NB]) return;  // whole workgroups exit together
+__device__ __forceinline__ void big_chunk(uint32_t cid, const Chunk* __restrict__ chunks,
+                                          const uint32_t* __restrict__ first, const uint32_t* __restrict__ entries,
+                                          const Niels* __restrict__ tab, Ext* __restrict__ sums,
+                                          unsigned* __restrict__ gcnt, Ext* __restrict__ out,
+                                          unsigned long long* probe, uint32_t* pts, bool& last) {
   const int t = threadIdx.x, q = t & 3, slot = t >> 2;
   if (probe && t == 0) probe[4 * cid] = wall_clock64();
   const Chunk c = chunks[cid];
@@ -269,6 +263,25 @@ __global__ void __launch_bounds__(kBigBS, 4) k_big_accum(const Chunk* __restrict
   if (probe && t == 0) probe[4 * cid + 3] = wall_clock64();
 }
 
+// grid: the LANE form launches one workgroup per bucket (random scalars: one chunk per bucket) and loops over any
+// further chunks (skewed scalars), so no surplus workgroups are dispatched; the quad form one per chunk bound
+template <bool LANE>
+__global__ void __launch_bounds__(kBigBS, 4) k_big_accum(const Chunk* __restrict__ chunks,
+                                                         const uint32_t* __restrict__ first,
+                                                         const uint32_t* __restrict__ entries,
+                                                         const Niels* __restrict__ tab, Ext* __restrict__ sums,
+                                                         unsigned* __restrict__ gcnt, Ext* __restrict__ out, int NB,
+                                                         unsigned long long* probe) {
+  // LANE: the lane sums (SoA over 256), then the quad tree's operands; else the quad tree's operands only
+  __shared__ uint32_t pts[LANE ? soa_words<Ext, kBigBS>() : soa_words<Ext, kBigQuads>()];
+  __shared__ bool last;
+  const uint32_t n = first[NB];
+  for (uint32_t cid = blockIdx.x; cid < n; cid += gridDim.x) {  // uniform per workgroup
+    big_chunk<LANE>(cid, chunks, first, entries, tab, sums, gcnt, out, probe, pts, last);
+    __syncthreads();  // pts / last are reused by the next chunk
+  }
+}
+
 int big_window() {
   // c = 11 (1024 buckets, 24 windows): measured best for 2^16 points against 12 and 13 (scripts/gpu_r03d.sh); a
   // smaller bucket set shortens the group reductions at the end more than its extra windows cost
@@ -320,8 +333,8 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
   {
     KScope ks(ctx, "msm_big_accum", 0.0, (double)a.per * W * (1.0 - 1.0 / (double)(1 << C)));
     if (lane)
-      hipLaunchKernelGGL(k_big_accum<true>, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first, a.entries,
-                         g->table, sums, gcnt, host_groups_dev, NB, pa);
+      hipLaunchKernelGGL(k_big_accum<true>, dim3((unsigned)std::min<size_t>(max_chunks, NB)), dim3(kBigBS), 0, s,
+                         chunks, first, a.entries, g->table, sums, gcnt, host_groups_dev, NB, pa);
     else
       hipLaunchKernelGGL(k_big_accum<false>, dim3((unsigned)max_chunks), dim3(kBigBS), 0, s, chunks, first,
                          a.entries, g->table, sums, gcnt, host_groups_dev, NB, pa);
@@ -331,13 +344,15 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
     std::vector<unsigned long long> A(4 * max_chunks);
     SPG_HIP(ctx, (hipMemcpyAsync)(A.data(), pa, A.size() * 8, hipMemcpyDeviceToHost, s));
     SPG_HIP(ctx, hipStreamSynchronize(s));
-    unsigned long long a0 = ~0ull, a1 = 0, g1 = 0;
+    unsigned long long a0 = ~0ull, a1 = 0, g1 = 0, s1 = 0, mx = 0;
     double madd = 0, tree = 0, grp = 0;
     size_t cnt = 0, ng = 0;
     for (size_t i = 0; i < max_chunks; i++) {
       if (!A[4 * i]) continue;
       a0 = std::min(a0, A[4 * i]);
+      s1 = std::max(s1, A[4 * i]);
       a1 = std::max(a1, A[4 * i + 2]);
+      mx = std::max(mx, A[4 * i + 1] - A[4 * i]);
       madd += (double)(A[4 * i + 1] - A[4 * i]);
       tree += (double)(A[4 * i + 2] - A[4 * i + 1]);
       cnt++;
@@ -347,9 +362,21 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
         ng++;
       }
     }
-    fprintf(stderr, "[spg] big accum: %zu chunks, span %.1f us (groups done at %.1f us); per chunk: adds %.1f us, "
-            "tree %.1f us; per group reduction %.1f us (%zu)\n", cnt, (a1 - a0) / 100.0, (g1 - a0) / 100.0,
-            madd / cnt / 100.0, tree / cnt / 100.0, ng ? grp / ng / 100.0 : 0.0, ng);
+    double xs[8] = {0}, xm[8] = {0};
+    size_t xn[8] = {0};
+    for (size_t i = 0; i < max_chunks; i++) {  // by workgroup index mod 8 (the XCD of a round-robin dispatch)
+      if (!A[4 * i]) continue;
+      const double d = (double)(A[4 * i + 1] - A[4 * i]) / 100.0;
+      xs[i % 8] += d;
+      xm[i % 8] = std::max(xm[i % 8], d);
+      xn[i % 8]++;
+    }
+    for (int x = 0; x < 8; x++)
+      if (xn[x]) fprintf(stderr, "[spg]   blockIdx %% 8 = %d: adds mean %.1f max %.1f us\n", x, xs[x] / xn[x], xm[x]);
+    fprintf(stderr, "[spg] big accum: %zu chunks, span %.1f us (groups done at %.1f us, last chunk start at %.1f us); "
+            "per chunk: adds %.1f us (max %.1f), tree %.1f us; per group reduction %.1f us (%zu)\n", cnt,
+            (a1 - a0) / 100.0, (g1 - a0) / 100.0, (s1 - a0) / 100.0, madd / cnt / 100.0, mx / 100.0, tree / cnt / 100.0,
+            ng ? grp / ng / 100.0 : 0.0, ng);
     hipFree(pa);
   }
   *ngroups = NB / kBigGroup;
