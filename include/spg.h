@@ -234,7 +234,10 @@ typedef struct {
 /* R1CSProof::verify (src/r1csproof.rs:687-954) of bincode(R1CSProof) bytes: evals = the claimed (A, B, C)(rx, ry)
  * bound with eq(rp) (multi_evaluate_bound_rp), num_cons = the instance's max_num_cons. 0 when the proof verifies
  * (and, when challenges_out != NULL, rp | rq_rev | rx | rw||ry with their lengths in ch_lens[4], as
- * spg_r1cs_prove returns them), SPG_E_VERIFY when it does not. */
+ * spg_r1cs_prove returns them), SPG_E_VERIFY when it does not. challenges_out must hold
+ * lg(num_instances) + lg(max_num_proofs) + lg(num_cons) + lg(nws) + lg(max_num_inputs) scalars (4 u64 each, lg
+ * rounded up). Shapes are checked before any proof byte is read: every num_proofs[p] a power of two no larger
+ * than max_num_proofs, section shapes consistent with the instance (else SPG_E_ARG). */
 int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t num_instances, size_t max_num_proofs,
                     const size_t* num_proofs, size_t max_num_inputs, const spg_witness_comm* secs, size_t nws,
                     size_t num_cons, const uint64_t* evals, spg_transcript* transcript, const uint8_t* proof,
