@@ -175,6 +175,43 @@ __global__ void k_sum_cols(const Fq* __restrict__ part, uint32_t S, uint32_t Rs,
   out[i] = acc;
 }
 
+// every witness polynomial's L.Z bound of one proof in two launches (instead of two per polynomial): job k's
+// partial rows are blocks [b0, b0 + nbx * S) of the first launch, its column sums blocks [c0, c0 + nbx) of the second
+struct BoundDesc {
+  const Fq* Z;
+  uint32_t offL, Ls, Rs, chunk, S, offP, o, b0, c0;
+};
+constexpr int kBoundMax = 32;
+struct BoundJobs {
+  BoundDesc d[kBoundMax];
+  int n;
+};
+__device__ __forceinline__ int bound_job(const BoundJobs& j, uint32_t b, bool cols) {
+  int k = 0;
+  while (k + 1 < j.n && (cols ? j.d[k + 1].c0 : j.d[k + 1].b0) <= b) k++;
+  return k;
+}
+__global__ void __launch_bounds__(256) k_bound_part_multi(BoundJobs jobs, const Fq* __restrict__ L, Fq* __restrict__ part) {
+  const int k = bound_job(jobs, blockIdx.x, false);
+  const BoundDesc& d = jobs.d[k];
+  const uint32_t nbx = (d.Rs + 255) / 256, rel = blockIdx.x - d.b0, y = rel / nbx;
+  const uint32_t i = (rel % nbx) * 256 + threadIdx.x;
+  if (i >= d.Rs) return;
+  const uint32_t j0 = y * d.chunk, j1 = min(d.Ls, j0 + d.chunk);
+  Fq acc = fq_zero();
+  for (uint32_t j = j0; j < j1; j++) acc = fq_add(acc, fq_mul(L[d.offL + j], d.Z[(size_t)j * d.Rs + i]));
+  part[d.offP + (size_t)y * d.Rs + i] = acc;
+}
+__global__ void __launch_bounds__(256) k_sum_cols_multi(BoundJobs jobs, const Fq* __restrict__ part, Fq* __restrict__ out) {
+  const int k = bound_job(jobs, blockIdx.x, true);
+  const BoundDesc& d = jobs.d[k];
+  const uint32_t i = (blockIdx.x - d.c0) * 256 + threadIdx.x;
+  if (i >= d.Rs) return;
+  Fq acc = fq_zero();
+  for (uint32_t y = 0; y < d.S; y++) acc = fq_add(acc, part[d.offP + (size_t)y * d.Rs + i]);
+  out[d.o + i] = acc;
+}
+
 // SparseMatPolynomial::evaluate_with_tables (src/sparse_mlpoly.rs:427-436) for every matrix of the
 // instance at once: segment s = 3p + m (A, B, C of matrix instance p); one thread per CSR row computes
 // eq_rx[row] * sum_e val_e * eq_ry[col_e]; blocks publish partial sums, k_sum_segments adds them.
@@ -916,21 +953,43 @@ int Prover::run_inner(Laps& lp) {
       Fq* dout = (Fq*)ws_get(ctx, WS_BOUT, lz_total * sizeof(Fq) + 64);
       if (!dL || !dpart || !dout) return set_err(ctx, SPG_E_NOMEM, "bound");
       if (!all_mine) SPG_HIP(ctx, hipMemsetAsync(dout, 0, lz_total * sizeof(Fq), s));  // other ranks' ranges
+      // one eq table per distinct rl (polynomials of one shape share it)
+      std::vector<size_t> eq_at(jobs.size());
       for (size_t k = 0; k < jobs.size(); k++) {
-        const BoundJob& j = jobs[k];
-        rc = eq_table(ctx, j.rl, dL + j.offL);
-        if (rc) return rc;
+        size_t same = k;
+        for (size_t m = 0; m < k; m++)
+          if (jobs[m].rl.size() == jobs[k].rl.size() &&
+              memcmp(jobs[m].rl.data(), jobs[k].rl.data(), jobs[k].rl.size() * sizeof(Fq)) == 0) {
+            same = m;
+            break;
+          }
+        eq_at[k] = same == k ? jobs[k].offL : eq_at[same];
+        if (same == k) {
+          rc = eq_table(ctx, jobs[k].rl, dL + jobs[k].offL);
+          if (rc) return rc;
+        }
       }
-      size_t k = 0;
-      for (auto& pr : polys) {
-        if (!pr.mine) continue;
-        const BoundJob& j = jobs[k++];
-        const uint32_t nbx = (uint32_t)((j.Rs + 255) / 256);
-        KScope ks(ctx, "poly_bound", 32.0 * j.Ls * j.Rs + 32.0 * j.Ls + 64.0 * j.S * j.Rs);
-        hipLaunchKernelGGL(k_bound_part, dim3(nbx, (uint32_t)j.S), dim3(256), 0, s, wit.d_w + wit.off[pr.w][pr.p],
-                           dL + j.offL, (uint32_t)j.Ls, (uint32_t)j.Rs, (uint32_t)j.chunk, dpart + j.offP);
-        hipLaunchKernelGGL(k_sum_cols, dim3(nbx), dim3(256), 0, s, dpart + j.offP, (uint32_t)j.S, (uint32_t)j.Rs,
-                           dout + j.o);
+      std::vector<const PolyRef*> mine;
+      for (auto& pr : polys)
+        if (pr.mine) mine.push_back(&pr);
+      double bytes = 0;
+      for (const BoundJob& j : jobs) bytes += 32.0 * j.Ls * j.Rs + 32.0 * j.Ls + 64.0 * j.S * j.Rs;
+      KScope ks(ctx, "poly_bound", bytes);
+      for (size_t k0 = 0; k0 < jobs.size(); k0 += kBoundMax) {  // two launches per kBoundMax polynomials
+        BoundJobs bj;
+        bj.n = (int)std::min<size_t>(kBoundMax, jobs.size() - k0);
+        uint32_t nb = 0, nc = 0;
+        for (int q = 0; q < bj.n; q++) {
+          const BoundJob& j = jobs[k0 + q];
+          const PolyRef& pr = *mine[k0 + q];
+          const uint32_t nbx = (uint32_t)((j.Rs + 255) / 256);
+          bj.d[q] = {wit.d_w + wit.off[pr.w][pr.p], (uint32_t)eq_at[k0 + q], (uint32_t)j.Ls, (uint32_t)j.Rs,
+                     (uint32_t)j.chunk, (uint32_t)j.S, (uint32_t)j.offP, (uint32_t)j.o, nb, nc};
+          nb += nbx * (uint32_t)j.S;
+          nc += nbx;
+        }
+        hipLaunchKernelGGL(k_bound_part_multi, dim3(nb), dim3(256), 0, s, bj, dL, dpart);
+        hipLaunchKernelGGL(k_sum_cols_multi, dim3(nc), dim3(256), 0, s, bj, dpart, dout);
       }
       SPG_HIP(ctx, hipGetLastError());
       rc = d2h_fq(ctx, dout, lz_mine.data(), lz_total);
@@ -954,9 +1013,9 @@ int Prover::run_inner(Laps& lp) {
   pf.comm_vars_at_ry_list.assign(nws, {});
   {
     size_t k = 0;
+    std::vector<CJob> cj;  // every evaluation's commitment in one host burst
     for (size_t i = 0; i < nws; i++) {
       eval_list.push_back({});
-      pf.comm_vars_at_ry_list.push_back({});
       for (size_t p = 0; p < wit.num_proofs[i].size(); p++, k++) {
         PolyRef& pr = polys[k];
         Fq ev = fq_zero();
@@ -964,8 +1023,14 @@ int Prover::run_inner(Laps& lp) {
         pr.ev = ev;
         size_t lni = lg2(pr.ni);
         eval_list[i].push_back(pr.ni >= Y ? ev : fq_mul(ev, ry_factors[ny - lni]));
-        pf.comm_vars_at_ry_list[i].push_back(commit_batch(g, {CJob(g.gens_1, {ev}, fq_zero())})[0]);
+        cj.push_back(CJob(g.gens_1, {ev}, fq_zero()));
       }
+    }
+    const std::vector<Pt> cv = commit_batch(g, cj);
+    k = 0;
+    for (size_t i = 0; i < nws; i++) {
+      pf.comm_vars_at_ry_list.push_back({});
+      for (size_t p = 0; p < wit.num_proofs[i].size(); p++) pf.comm_vars_at_ry_list[i].push_back(cv[k++]);
     }
   }
   lp.lap("polyeval_bound");
