@@ -323,6 +323,7 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_cx, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->d_counter, 64) != hipSuccess ||
       hipMemset(c->d_counter, 0, 64) != hipSuccess) {
     delete c;
@@ -356,6 +357,7 @@ extern "C" int spg_free(spg_ctx* c) {
   if (c->d_counter) hipFree(c->d_counter);
   hipEventDestroy(c->ev0);
   hipEventDestroy(c->ev1);
+  if (c->ev_cx) hipEventDestroy(c->ev_cx);
   hipStreamDestroy(c->stream);
   delete c;
   return SPG_OK;

@@ -15,6 +15,7 @@ struct spg_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_cx = nullptr;  // DotProductProofLog: the Cx MSM's completion, ahead of Bullet round 0 on the stream
   void* pinned = nullptr;          // page-locked host staging (pinned_get), grown on demand
   size_t pinned_bytes = 0;
   // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into

@@ -321,25 +321,41 @@ static void host_fold_dots(FqV& aa, FqV& bb, FqV& cw, size_t n, size_t nn, bool 
 // (bullet_round_device): per round the host launches one kernel with (u, u^-1), then - while it runs - folds
 // its own copies of a, b, cw and computes c_L, c_R and the G_1 / h terms of L and R, waits for the bucket
 // sums (mailbox), finishes L and R on the pool and draws the next challenge. Same transcript, same points.
+// Round 0 of bullet_rounds_device launched ahead (with the Cx MSM, before the transcript yields r): its L and R
+// MSM scalars are a and the unit weights alone, and the r-dependent G_1 terms are added on the host afterwards.
+// x: the n scalars on the device (copied into the round state); *seq: round 0's mailbox number.
+static int bullet_round0_launch(spg_ctx* ctx, ProverGens& g, size_t n, const Fq* d_x, const uint32_t* d_idx,
+                                Ext* d_bk, uint32_t* seq) {
+  Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
+  if (!st) return set_err(ctx, SPG_E_NOMEM, "bullet state");
+  SPG_HIP(ctx, hipMemcpyAsync(st, d_x, n * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
+  return bullet_round_device(ctx, g.dev, st, st + 2 * n, st + n, st + 3 * n, d_idx, fq_zero(), fq_zero(), 0, (int)n,
+                             (int)n, d_bk, seq);
+}
+
 static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x, const FqV& a, const Fq& r,
                                 const FqV& v1, const FqV& v2, const uint32_t* d_idx, Ext* mbk, Ext* d_bk, FqV* aa,
-                                FqV* bb, FqV* cw, Fq* blind_fin, DotProductProofLogP* out) {
+                                FqV* bb, FqV* cw, Fq* blind_fin, DotProductProofLogP* out, bool pre0 = false,
+                                uint32_t seq0 = 0) {
   const size_t n = x.size();
   const size_t G1 = g.gens_1.G[0], H = g.gens_n.h;
   Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
   if (!st) return set_err(ctx, SPG_E_NOMEM, "bullet state");
   Fq* d_aa[2] = {st, st + n};
   Fq* d_cw[2] = {st + 2 * n, st + 3 * n};
-  uint8_t* stage = (uint8_t*)pinned_get(ctx, n * sizeof(Fq));
-  if (!stage) return set_err(ctx, SPG_E_NOMEM, "bullet staging");
-  memcpy(stage, x.data(), n * sizeof(Fq));
-  SPG_HIP(ctx, hipMemcpyAsync(d_aa[0], stage, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+  if (!pre0) {
+    uint8_t* stage = (uint8_t*)pinned_get(ctx, n * sizeof(Fq));
+    if (!stage) return set_err(ctx, SPG_E_NOMEM, "bullet staging");
+    memcpy(stage, x.data(), n * sizeof(Fq));
+    SPG_HIP(ctx, hipMemcpyAsync(d_aa[0], stage, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+  }
   Fq u = fq_zero(), uinv = fq_zero();
   size_t nk = n;
   for (int k = 0; nk != 1; k++) {
-    uint32_t seq = 0;
-    int rc = bullet_round_device(ctx, g.dev, d_aa[k & 1], d_cw[k & 1], d_aa[(k + 1) & 1], d_cw[(k + 1) & 1], d_idx, u,
-                                 uinv, k, (int)n, (int)nk, d_bk, &seq);
+    uint32_t seq = seq0;
+    int rc = k == 0 && pre0 ? 0
+                            : bullet_round_device(ctx, g.dev, d_aa[k & 1], d_cw[k & 1], d_aa[(k + 1) & 1],
+                                                  d_cw[(k + 1) & 1], d_idx, u, uinv, k, (int)n, (int)nk, d_bk, &seq);
     if (rc) return rc;
     g_msm_laps.lap("bullet_launch");
     Fq cL, cR;
@@ -409,9 +425,41 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     SPG_HIP(ctx, hipMemcpyAsync(d_idx, idx2.data(), idx2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   }
   using HostJob = std::pair<std::vector<size_t>, FqV>;
+  static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
+  static const bool ahead = !getenv("SPG_BULLET_AHEAD") || atoi(getenv("SPG_BULLET_AHEAD")) != 0;
+  const bool dev_path = dev_rounds && !on_host && n >= 2 && (n & (n - 1)) == 0;
+  // mapped host memory for the bucket sums: [Cx MSM (B = 1, up to 256 buckets)][Bullet rounds (2 x 65)]
+  const size_t cx_bytes = sizeof(Ext) * 256, br_bytes = sizeof(Ext) * 2 * (kBulletNB + 1) + 64;
+  void* d_map = nullptr;
+  uint8_t* mapped = dev_path ? (uint8_t*)mapped_get(ctx, cx_bytes + br_bytes, &d_map) : nullptr;
+  Ext* mbk = mapped ? (Ext*)(mapped + cx_bytes) : nullptr;
+  Ext* d_mbk = mapped ? (Ext*)((uint8_t*)d_map + cx_bytes) : nullptr;
   // Cx = x.commit(blind_x, gens_n)
   std::vector<Pt> pts;
-  if (on_host) {
+  bool pre0 = false;
+  uint32_t seq0 = 0;
+  if (mbk && ahead) {
+    // the Cx bucket sums, then Bullet round 0 (which needs no challenge), on the stream before the host waits
+    // for Cx: one device round trip fewer per proof
+    std::vector<Fq> hs(n2, fq_zero());
+    std::copy(x.begin(), x.end(), hs.begin());
+    hs[n + 1] = blind_x;
+    Fq* d_s = (Fq*)ws_get(ctx, 20, n2 * sizeof(Fq) + 64);
+    uint8_t* stage = (uint8_t*)pinned_get(ctx, n2 * sizeof(Fq) + 64);
+    if (!d_s || !stage) return set_err(ctx, SPG_E_NOMEM, "Cx");
+    memcpy(stage, hs.data(), n2 * sizeof(Fq));
+    SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, n2 * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+    int NB = 0;
+    int rc = msm_small_buckets(ctx, g.dev, 0, d_s, n2, 1, nullptr, d_idx, -1, (Ext*)d_map, &NB);
+    if (rc) return rc;
+    SPG_HIP(ctx, hipEventRecord(ctx->ev_cx, ctx->stream));
+    rc = bullet_round0_launch(ctx, g, n, d_s, d_idx, d_mbk, &seq0);
+    if (rc) return rc;
+    pre0 = true;
+    SPG_HIP(ctx, hipEventSynchronize(ctx->ev_cx));
+    pts.resize(1);
+    bucket_finals((const Ext*)mapped, 1, NB, pts.data());
+  } else if (on_host) {
     HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), x};
     j.first.push_back(kn.h);
     j.second.push_back(blind_x);
@@ -445,13 +493,9 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   }
   size_t nk = n, k = 0;
   g_msm_laps.lap("bullet_prep");
-  static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
-  void* d_map = nullptr;
-  Ext* mbk = (dev_rounds && !on_host && n >= 2 && (n & (n - 1)) == 0)
-                 ? (Ext*)mapped_get(ctx, sizeof(Ext) * 2 * (kBulletNB + 1) + 64, &d_map)
-                 : nullptr;
   if (mbk) {
-    int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, mbk, (Ext*)d_map, &aa, &bb, &cw, &blind_fin, out);
+    int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, mbk, d_mbk, &aa, &bb, &cw, &blind_fin, out, pre0,
+                                  seq0);
     if (rc) return rc;
     nk = 1;
   }
