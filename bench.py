@@ -50,7 +50,11 @@ CONFIGS = {
     "r1cs_2e16": ([1024, 1024], [32, 32], 1),
     "r1cs_2e22_p8": ([1024] * 8, [512] * 8, 1),
 }
-TRAFFIC = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json")]
+# per-launch HBM bytes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, scripts/pmc_traffic.py) of each workload's own
+# run: a kernel's traffic depends on its launch size, so one workload's figures are never reported for another
+TRAFFIC = {w: os.path.join(ROOT, "profiles", f) for w, f in (
+    ("snark", "r03_pmc_traffic.json"), ("msm16", "r03_pmc_traffic_msm_2e16.json"),
+    ("spark24", "r03_pmc_traffic_spark_2e24.json"))}
 
 
 def parse():
@@ -153,12 +157,10 @@ def profile_pass(ctx, step, steps):
 
 
 def traffic_of(kernel, traffic_file):
-    for f in ([traffic_file] if traffic_file else TRAFFIC):
-        if f and os.path.exists(f):
-            tr = json.load(open(f))
-            if kernel in tr.get("kernels", {}):
-                return tr["kernels"][kernel]["hbm_bytes_per_launch"]
-            return None
+    if traffic_file and os.path.exists(traffic_file):
+        tr = json.load(open(traffic_file))
+        if kernel in tr.get("kernels", {}):
+            return tr["kernels"][kernel]["hbm_bytes_per_launch"]
     return None
 
 
@@ -315,7 +317,7 @@ def main_snark(a):
     t_verify = (time.perf_counter() - t1) / 3
     N = wl.total_constraints
     value = N * env.world * a.steps / dt
-    roof, roof_h, roof_v = rooflines(prof, a.traffic)
+    roof, roof_h, roof_v = rooflines(prof, a.traffic or TRAFFIC["snark"])
     cpu = cpu_all = bitexact = cpu_verify_ms = None
     if env.rank == 0 and env.world == 1 and not a.no_cpu_baseline:
         po = oracle()
@@ -335,10 +337,10 @@ def main_snark(a):
         want = set(a.extras.split(","))
         if "msm" in want:
             extras["config2_msm"] = guarded(lambda: msm_core(env, ctx, 16, a.steps, a.warmup, not a.no_cpu_baseline,
-                                                             a.traffic))
+                                                             TRAFFIC["msm16"]))
         if "spark" in want:
             extras["config5_spark"] = guarded(lambda: spark_core(env, ctx, 24, a.cpu_log_nnz, 5, 1, "replicas",
-                                                                 not a.no_cpu_baseline, a.traffic))
+                                                                 not a.no_cpu_baseline, TRAFFIC["spark24"]))
     if env.rank == 0:
         out = {
             "metric": "R1CS constraints/sec (SNARK::prove) at 2^20 vars; proof bytes bit-exact",
@@ -551,7 +553,8 @@ def main_msm(a):
     import spg
 
     ctx = spg.Context(env.gpu)
-    out = msm_core(env, ctx, a.log_msm, a.steps, a.warmup, not a.no_cpu_baseline, a.traffic)
+    out = msm_core(env, ctx, a.log_msm, a.steps, a.warmup, not a.no_cpu_baseline,
+                   a.traffic or (TRAFFIC["msm16"] if a.log_msm == 16 else None))
     if env.rank == 0:
         out["vs_baseline"] = None
         print(json.dumps(out))
@@ -651,7 +654,7 @@ def main_spark(a):
 
     ctx = spg.Context(env.gpu)
     out = spark_core(env, ctx, a.log_nnz, a.cpu_log_nnz, a.steps, a.warmup, a.mode or "shard", not a.no_cpu_baseline,
-                     a.traffic)
+                     a.traffic or (TRAFFIC["spark24"] if a.log_nnz == 24 else None))
     if env.rank == 0:
         out["vs_baseline"] = None
         print(json.dumps(out))
