@@ -21,8 +21,9 @@ Rooflines: `roofline` belongs to the kernel with the most device time that has a
 mixed additions, one per nonzero signed window digit) against the measured whole-GPU ext_madd throughput, or
 algorithmic HBM bytes against 8 TB/s; `roofline_hbm` / `roofline_valu` give the largest kernel of each kind.
 Per-launch times are libspg's HIP events on its context stream (spg_prof_read2) in a profiling pass after the
-timed steps; `traffic` is the PMC-measured HBM bytes per launch from the committed rocprofv3 summary of this tree
-(scripts/gpu_profile.sh -> profiles/r03_pmc_traffic.json).
+timed steps; `traffic` is the PMC-measured HBM bytes per launch from the committed rocprofv3 summary of the same
+workload (TRAFFIC below: scripts/gpu_profile.sh, scripts/gpu_r03y.sh). `device_busy_ms_per_step` is the union of
+the timed intervals, since kernels on the context's second stream overlap those of the main one.
 `cpu_baseline` is the C++ CPU restatement of the reference (oracle/) on rank 0 at N = 1: one thread on the full
 workload, and `cpu_baseline_all_cores` the same work run as one independent prove per usable host core at once.
 """
@@ -151,9 +152,17 @@ def profile_pass(ctx, step, steps):
     ctx.prof_read(reset=True)
     for _ in range(steps):
         step()
-    prof = ctx.prof_read(reset=True, ops=True)
+    prof = Prof(ctx.prof_read(reset=True, ops=True))
     ctx.prof_enable(False)
+    busy = prof.pop("(device_busy)", None)
+    prof.busy_us = busy[1] if busy else sum(v[1] for v in prof.values())
     return prof
+
+
+class Prof(dict):
+    """per-kernel timings of a profile pass; busy_us = the device's busy time (union of the timed intervals: kernels
+    of the context's second stream overlap the main stream's, so the per-kernel sum overstates it)"""
+    busy_us = 0.0
 
 
 def traffic_of(kernel, traffic_file):
@@ -355,7 +364,7 @@ def main_snark(a):
             "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
             "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16],
-            "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
+            "device_busy_ms_per_step": round(prof.busy_us / a.steps / 1e3, 3),
             "value_incl_witness_upload": round(N * env.world / t_incl, 1),
             "ms_per_step_incl_witness_upload": round(t_incl * 1e3, 3),
             "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
@@ -442,7 +451,7 @@ def main_r1cs(a):
                        else f"replicas x{env.world}"},
             "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
             "proof_bitexact_vs_cpu": bitexact, "proof_sha256": sorted(proofs)[0][:16],
-            "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / a.steps / 1e3, 3),
+            "device_busy_ms_per_step": round(prof.busy_us / a.steps / 1e3, 3),
             "value_incl_witness_upload": round(units / t_incl, 1), "kernels": kernel_table(prof, a.steps)}))
     env.close()
 
@@ -508,7 +517,7 @@ def msm_core(env, ctx, log_msm, steps, warmup, cpu_on, traffic_file=None):
     prof = profile_pass(ctx, step, steps)
     roof, roof_h, roof_v = rooflines(prof, traffic_file)
     lo, hi = shard.chunk(n, env.rank, env.world)
-    dev_us = sum(v[1] for v in prof.values()) / steps
+    dev_us = prof.busy_us / steps
     madds = sum(v[3] for v in prof.values()) / steps
     cpu = cpu_all = bitexact = None
     if env.rank == 0 and cpu_on:
@@ -643,7 +652,7 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_sha256": sorted(proofs)[0][:16], "ranks_agree": same,
         "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
-        "device_busy_ms_per_step": round(sum(v[1] for v in prof.values()) / steps / 1e3, 3),
+        "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
         "kernels": kernel_table(prof, steps),
     }
 

@@ -68,7 +68,9 @@ int spg_comm_allgather(spg_ctx* ctx, const void* send, size_t bytes, void* recv)
 
 /* per-kernel timing on the context stream (events; off by default). spg_prof_read resolves them and
  * returns up to `max` records (name[32], launches, total microseconds, algorithmic HBM bytes moved
- * by those launches as modelled in DESIGN.md, 0 where not modelled); reset != 0 clears the tallies. */
+ * by those launches as modelled in DESIGN.md, 0 where not modelled); reset != 0 clears the tallies.
+ * The record named "(device_busy)" (0 launches) holds the union of the timed intervals: the device's busy time,
+ * which the per-kernel totals overstate where the context's two streams ran kernels at once. */
 int spg_prof_enable(spg_ctx* ctx, int on);
 int spg_prof_read(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, int max, int reset);
 /* the same plus the modelled VALU work of those launches in curve mixed additions (ops; 0 where not modelled):

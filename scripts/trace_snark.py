@@ -13,5 +13,5 @@ w = workload.SnarkWorkload(num_blocks=2, log_cons=10, log_proofs=k, num_vars=102
 v = workload.SnarkViews(w)
 b, p, pr = spg.SnarkComp(ctx, v.block, multi=True), spg.SnarkComp(ctx, v.pairwise), spg.SnarkComp(ctx, v.perm_root)
 wit = spg.SnarkWitness(ctx, v.inputs)
-for i in range(3):
+for i in range(int(os.environ.get("TRACE_REPS", "3"))):
     spg.snark_prove(ctx, b, p, pr, wit, g, spg.Transcript(b"t"), spg.RandomTape(b"proof", workload.tape_seed()))

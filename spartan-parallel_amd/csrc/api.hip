@@ -324,6 +324,8 @@ extern "C" int spg_init(int device, spg_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_cx, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->d_counter, 64) != hipSuccess ||
       hipMemset(c->d_counter, 0, 64) != hipSuccess) {
     delete c;
@@ -358,6 +360,11 @@ extern "C" int spg_free(spg_ctx* c) {
   hipEventDestroy(c->ev0);
   hipEventDestroy(c->ev1);
   if (c->ev_cx) hipEventDestroy(c->ev_cx);
+  if (c->ev_pre) hipEventDestroy(c->ev_pre);
+  if (c->stream2) {
+    hipStreamSynchronize(c->stream2);
+    hipStreamDestroy(c->stream2);
+  }
   hipStreamDestroy(c->stream);
   delete c;
   return SPG_OK;
@@ -418,6 +425,32 @@ extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* t
                               int max, int reset) {
   if (!c) return SPG_E_ARG;
   hipStreamSynchronize(c->stream);
+  hipStreamSynchronize(c->stream2);
+  // device busy time = the union of the timed intervals (kernels on the second stream overlap the main one's)
+  if (!c->prof_pending.empty()) {
+    std::vector<std::pair<float, float>> iv;
+    const hipEvent_t base = c->prof_pending.front().a;
+    for (auto& r : c->prof_pending) {
+      float s = 0.f, e = 0.f;
+      if (hipEventElapsedTime(&s, base, r.a) == hipSuccess && hipEventElapsedTime(&e, base, r.b) == hipSuccess)
+        iv.push_back({s, e});
+    }
+    std::sort(iv.begin(), iv.end());
+    double busy = 0, lo = 0, hi = 0;
+    bool open = false;
+    for (auto& x : iv) {
+      if (open && x.first <= hi) {
+        hi = std::max<double>(hi, x.second);
+        continue;
+      }
+      if (open) busy += hi - lo;
+      lo = x.first;
+      hi = x.second;
+      open = true;
+    }
+    if (open) busy += hi - lo;
+    c->prof_acc["(device_busy)"].us += busy * 1000.0;
+  }
   for (auto& r : c->prof_pending) {
     float ms = 0.f;
     hipEventElapsedTime(&ms, r.a, r.b);

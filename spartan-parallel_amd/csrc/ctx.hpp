@@ -16,6 +16,10 @@ struct spg_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_cx = nullptr;  // DotProductProofLog: the Cx MSM's completion, ahead of Bullet round 0 on the stream
+  // second stream: SNARK::prove's latency-path witness commits run on it beside the early block_vars MSM on `stream`;
+  // ev_pre marks the point of `stream` they follow (everything queued before that MSM)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_pre = nullptr;
   void* pinned = nullptr;          // page-locked host staging (pinned_get), grown on demand
   size_t pinned_bytes = 0;
   // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into

@@ -219,10 +219,10 @@ __global__ void __launch_bounds__(256) k_digits_rows(MsmArgs a) {
   }
 }
 
-__global__ void k_item_counts(const uint32_t* __restrict__ hist, uint32_t* __restrict__ items, int nkeys) {
+__global__ void k_item_counts(const uint32_t* __restrict__ hist, uint32_t* __restrict__ items, int nkeys, uint32_t K) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > nkeys) return;
-  items[i] = i < nkeys ? (hist[i] + kItemK - 1) / kItemK : 0u;
+  items[i] = i < nkeys ? (hist[i] + K - 1) / K : 0u;
 }
 
 __global__ void k_item_keys(const uint32_t* __restrict__ item_off, uint32_t* __restrict__ item_key, int nkeys) {
@@ -885,7 +885,9 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   const size_t nkeys = B * (size_t)NB;
   const size_t per = n + (d_blinds ? 1 : 0);
   const size_t max_entries = B * per * (size_t)W;
-  const size_t max_items = max_entries / kItemK + nkeys + 1;
+  static const int item_k = getenv("SPG_ITEM_K") ? std::max(1, atoi(getenv("SPG_ITEM_K"))) : kItemK;
+  static const int seg_m = getenv("SPG_SEG_M") ? std::max(1, atoi(getenv("SPG_SEG_M"))) : kSegM;
+  const size_t max_items = max_entries / item_k + nkeys + 1;
   SPG_CHECK(ctx, max_entries < 0x7fffffffULL, "msm batch too large");
   SPG_CHECK(ctx, (size_t)kTableRows * (g->n + 1) < 0x7fffffffULL, "generator table too large");
 
@@ -897,7 +899,7 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   uint32_t* entries = (uint32_t*)ws_get(ctx, 6, max_entries * 4 + 4);
   uint32_t* item_key = (uint32_t*)ws_get(ctx, 7, max_items * 4);
   Ext* partial = (Ext*)ws_get(ctx, 8, max_items * sizeof(Ext));
-  const int m = NB < kSegM ? NB : kSegM;  // buckets per segment
+  const int m = NB < seg_m ? NB : seg_m;  // buckets per segment
   const int S = NB / m;
   int log2m = 0;
   while ((1 << log2m) < m) log2m++;
@@ -948,7 +950,7 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
   // scans over nkeys+1 entries (hist[nkeys] == 0 so off[nkeys] = total entries)
   if (!rows) SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, hist, off, (int)(nkeys + 1), s));
   hipLaunchKernelGGL(k_item_counts, dim3((unsigned)((nkeys + 1 + 255) / 256)), dim3(256), 0, s, hist, items,
-                     (int)nkeys);
+                     (int)nkeys, (uint32_t)item_k);
   SPG_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, items, item_off, (int)(nkeys + 1), s));
 
   if (!rows) {

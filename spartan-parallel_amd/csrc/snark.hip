@@ -420,6 +420,7 @@ struct CQ {
     Fq* d = (Fq*)ws_get(ctx, 92, total * sizeof(Fq) + 64);
     uint8_t* out = (uint8_t*)ws_get(ctx, 93, 32 * (total / R) + 64);
     if (!d || !out) return set_err(ctx, SPG_E_NOMEM, "early commit staging");
+    SPG_HIP(ctx, hipEventRecord(ctx->ev_pre, ctx->stream));  // flush()'s side stream starts from here
     size_t o = 0;
     for (auto& it : its) {
       SPG_HIP(ctx, hipMemcpyAsync(d + o, it.first, it.second * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
@@ -445,6 +446,49 @@ struct CQ {
       it.out->assign((size_t)1 << (nv / 2), Pt());
       if (!is_early(it) && std::find(widths.begin(), widths.end(), R) == widths.end()) widths.push_back(R);
     }
+    // While the early MSM runs, the other rows go to the device on the second stream: their uploads and
+    // latency-path MSMs then overlap it instead of queueing behind it. Rows of at most kSideMaxR scalars take
+    // commit_rows' latency path, whose workspace slots, mapped buckets and staging the batch pipeline of the early
+    // MSM never touches; wider rows stay on the main stream.
+    static const size_t kSideMaxR = 256;
+    static const bool side_on = !getenv("SPG_CQ_SIDE") || atoi(getenv("SPG_CQ_SIDE")) != 0;
+    bool side = side_on && early_L > 0;
+    for (size_t R : widths) side = side && R <= kSideMaxR;
+    Laps lp;
+    lp.title = "commit queue flush";
+    lp.on = lp.on && getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2;
+    const hipStream_t main_stream = ctx->stream;
+    if (side) {
+      SPG_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_pre, 0));
+      ctx->stream = ctx->stream2;
+    }
+    int rc = flush_rows(ctx, g, widths);
+    ctx->stream = main_stream;
+    if (rc) return rc;
+    lp.lap(side ? "rows_side" : "rows");
+    if (early_L) {
+      std::vector<Pt> rows(early_L);
+      SPG_HIP(ctx, hipMemcpyAsync(rows.data(), early_out, 32 * early_L, hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      size_t o = 0;
+      for (const Fq* d : early_dev)  // rows in launch order
+        for (auto& it : items)
+          if (it.dev == d) {
+            std::copy(rows.begin() + o, rows.begin() + o + it.out->size(), it.out->begin());
+            o += it.out->size();
+          }
+      early_dev.clear();
+      early_L = 0;
+    }
+    lp.lap("early_wait");
+    for (auto& it : items) append_polycomm(t, "poly_commitment", *it.out);
+    items.clear();
+    lp.lap("append");
+    lp.print();
+    return 0;
+  }
+  // the rows of every item outside the early group, on ctx->stream; synchronous
+  int flush_rows(spg_ctx* ctx, ProverGens& g, const std::vector<size_t>& widths) {
     // one staging range per width, every width's rows committed together (the latency-path widths share one
     // encoding launch and one download)
     size_t total = 0;
@@ -478,22 +522,6 @@ struct CQ {
         ro += it.out->size();
       }
     }
-    if (early_L) {
-      std::vector<Pt> rows(early_L);
-      SPG_HIP(ctx, hipMemcpyAsync(rows.data(), early_out, 32 * early_L, hipMemcpyDeviceToHost, ctx->stream));
-      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      size_t o = 0;
-      for (const Fq* d : early_dev)  // rows in launch order
-        for (auto& it : items)
-          if (it.dev == d) {
-            std::copy(rows.begin() + o, rows.begin() + o + it.out->size(), it.out->begin());
-            o += it.out->size();
-          }
-      early_dev.clear();
-      early_L = 0;
-    }
-    for (auto& it : items) append_polycomm(t, "poly_commitment", *it.out);
-    items.clear();
     return 0;
   }
 };
