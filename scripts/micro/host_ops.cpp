@@ -58,6 +58,34 @@ int main() {
   printf("commit_many 1 x 2 terms  %.3f us\n", us_per(2000, [&](int) { sink ^= hg.commit_many(one2)[0].b[0]; }));
   printf("commit_many 3 jobs (2,5,2) %.3f us\n", us_per(2000, [&](int) { sink ^= hg.commit_many(three)[0].b[0]; }));
   printf("sum_many 1 x 5 terms (no encoding) %.3f us\n", us_per(2000, [&](int) { acc = hg.sum_many(one5)[0]; }));
+  // host Bullet rounds (DotProductProofLog with n <= 32 on the host): two MSMs of n/2 + 2 terms per round over
+  // generator sets whose tables (~1 MB per generator) do not fit the caches; 8 sets of 34 generators rotated
+  {
+    const int G = 8 * 34;
+    std::vector<uint8_t> c2;
+    h::HExt R = P;
+    for (int i = 0; i < G; i++) {
+      Pt c = compress(R);
+      c2.insert(c2.end(), c.b, c.b + 32);
+      R = h::hext_add(R, h::hext_dbl(P));
+    }
+    HostGens big;
+    big.init(c2.data(), G);
+    std::vector<std::vector<Job>> rounds(8);
+    for (int set = 0; set < 8; set++) {
+      for (int b = 0; b < 2; b++) {
+        Job j;
+        for (int i = 0; i < 18; i++) {
+          j.first.push_back((size_t)(set * 34 + b * 16 + i));
+          j.second.push_back(fq_add(k, fq_from_u64(1000 * set + 100 * b + i)));
+        }
+        rounds[set].push_back(j);
+      }
+      big.commit_many(rounds[set]);  // tables
+    }
+    printf("host Bullet round (2 x 18 terms, 8 rotating sets) %.3f us\n",
+           us_per(400, [&](int i) { sink ^= big.commit_many(rounds[i % 8])[0].b[0]; }));
+  }
   printf("(sink %d %u)\n", (int)sink, a.l[0]);
   return 0;
 }

@@ -41,21 +41,32 @@ FqV pad_pow2(FqV v) {  // DensePolynomial::new pads to a power of two (dense_mlp
   v.resize(npow2(std::max<size_t>(v.size(), 1)), fq_zero());
   return v;
 }
-// DensePolynomial::bound (dense_mlpoly.rs:258-265) on a host polynomial
-FqV host_bound(const FqV& Z, const FqV& L) {
-  const size_t nv = lg2(Z.size()), Ls = (size_t)1 << (nv / 2), Rs = (size_t)1 << (nv - nv / 2);
-  FqV out(Rs, fq_zero());
-  // column slices over the pool when there are enough products (~25 ns each on a host core)
-  const int C = Ls * Rs >= 4096 && Rs >= 8 ? 8 : 1;
-  auto cols = [&](int c) {
-    const size_t i0 = Rs * c / C, i1 = Rs * (c + 1) / C;
-    for (size_t j = 0; j < Ls; j++)
-      for (size_t i = i0; i < i1; i++) out[i] = fq_add(out[i], fq_mul(L[j], Z[j * Rs + i]));
+// DensePolynomial::bound (dense_mlpoly.rs:258-265) of several host (Z, L) pairs in one pool burst: each job's columns are cut into slices of >= ~2048
+// products, all slices of all jobs go to the pool together (one wake-up instead of one per polynomial)
+std::vector<FqV> host_bounds(const std::vector<std::pair<const FqV*, const FqV*>>& jobs) {
+  std::vector<FqV> out(jobs.size());
+  struct Slice {
+    size_t j, Ls, Rs, i0, i1;
   };
-  if (C == 1)
-    cols(0);
-  else
-    pool().parallel_for(C, cols);
+  std::vector<Slice> sl;
+  for (size_t j = 0; j < jobs.size(); j++) {
+    const size_t nv = lg2(jobs[j].first->size()), Ls = (size_t)1 << (nv / 2), Rs = (size_t)1 << (nv - nv / 2);
+    out[j].assign(Rs, fq_zero());
+    const size_t C = std::max<size_t>(1, std::min<size_t>({8, Rs, Ls * Rs / 2048}));
+    for (size_t c = 0; c < C; c++) sl.push_back({j, Ls, Rs, Rs * c / C, Rs * (c + 1) / C});
+  }
+  auto run = [&](int k) {
+    const Slice& s = sl[k];
+    const FqV& Z = *jobs[s.j].first;
+    const FqV& L = *jobs[s.j].second;
+    FqV& o = out[s.j];
+    for (size_t j = 0; j < s.Ls; j++)
+      for (size_t i = s.i0; i < s.i1; i++) o[i] = fq_add(o[i], fq_mul(L[j], Z[j * s.Rs + i]));
+  };
+  if (sl.size() == 1)
+    run(0);
+  else if (!sl.empty())
+    pool().parallel_for((int)sl.size(), run);
   return out;
 }
 void eq_factored(const FqV& r, FqV* L, FqV* R) {
@@ -226,10 +237,14 @@ int prove_batched_points(spg_ctx* ctx, ProverGens& g, const FqV& Z, const std::v
     }
   }
   w.u64(Ls.size());
+  // every distinct point's L.Z bound up front, in one pool burst
+  std::vector<std::pair<const FqV*, const FqV*>> bj;
+  for (size_t i = 0; i < Ls.size(); i++) bj.push_back({&Z, &Ls[i]});
+  std::vector<FqV> LZs = host_bounds(bj);
   for (size_t i = 0; i < Ls.size(); i++) {
     DotProductProofLogP p;
     Pt cy;
-    int rc = dotproduct_log_prove(ctx, g, t, tape, host_bound(Z, Ls[i]), fq_zero(), Rs[i], Zc[i], fq_zero(), &p, &cy);
+    int rc = dotproduct_log_prove(ctx, g, t, tape, LZs[i], fq_zero(), Rs[i], Zc[i], fq_zero(), &p, &cy);
     if (rc) return rc;
     p.ser(w);
   }
@@ -244,6 +259,9 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
   std::vector<FqV> LZs, Rs;
   FqV Zc;
   Fq c_base = t.challenge("challenge_c"), c = fq_one();
+  // every polynomial's eq factors, then all L.Z bounds in one pool burst
+  std::vector<FqV> Lv(polys.size()), Rv(polys.size());
+  std::vector<std::pair<const FqV*, const FqV*>> bj;
   for (size_t i = 0; i < polys.size(); i++) {
     const size_t nv = lg2(polys[i]->size());
     FqV r = r_list[i];
@@ -251,8 +269,13 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
       r.insert(r.begin(), nv - r.size(), fq_zero());
     else
       r = FqV(r.end() - nv, r.end());
-    FqV L, R;
-    eq_factored(r, &L, &R);
+    eq_factored(r, &Lv[i], &Rv[i]);
+    bj.push_back({polys[i], &Lv[i]});
+  }
+  std::vector<FqV> LZall = host_bounds(bj);
+  for (size_t i = 0; i < polys.size(); i++) {
+    const size_t nv = lg2(polys[i]->size());
+    const FqV& R = Rv[i];
     size_t idx = keys.size();
     for (size_t k = 0; k < keys.size(); k++)
       if (keys[k].first == nv && keys[k].second.size() == R.size() &&
@@ -260,7 +283,7 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
         idx = k;
         break;
       }
-    FqV LZ = host_bound(*polys[i], L);
+    FqV& LZ = LZall[i];
     if (idx < keys.size()) {
       c = fq_mul(c, c_base);
       for (size_t j = 0; j < LZ.size(); j++) LZs[idx][j] = fq_add(LZs[idx][j], fq_mul(c, LZ[j]));
@@ -283,9 +306,39 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
   return 0;
 }
 
-// PolyEvalProof::prove_uni_batched_instances (dense_mlpoly.rs:1046-1130)
-int prove_uni_batched(spg_ctx* ctx, ProverGens& g, const std::vector<const FqV*>& polys, const Fq& r, const FqV& Zr,
-                      Tr& t, Tape& tape, Writer& w) {
+// The L.Z bounds of PolyEvalProof::prove_uni_batched_instances (dense_mlpoly.rs:1046-1130): L = (r^(Rs j))_j for
+// each polynomial size 2^nv, all bounds in one pool burst. The shift proof also reads its evaluations from them:
+// sum_k LZ[k] r^k = sum_i Z[i] r^i.
+std::vector<FqV> uni_bounds(const std::vector<const FqV*>& polys, const Fq& r) {
+  std::vector<size_t> nvs;
+  std::vector<FqV> Lv;
+  std::vector<size_t> li(polys.size());
+  for (size_t i = 0; i < polys.size(); i++) {
+    const size_t nv = lg2(polys[i]->size());
+    size_t k = 0;
+    while (k < nvs.size() && nvs[k] != nv) k++;
+    if (k == nvs.size()) {
+      Fq r_base = fq_one();
+      for (size_t e = 0; e < ((size_t)1 << (nv - nv / 2)); e++) r_base = fq_mul(r_base, r);
+      FqV L;
+      Fq lb = fq_one();
+      for (size_t e = 0; e < ((size_t)1 << (nv / 2)); e++) {
+        L.push_back(lb);
+        lb = fq_mul(lb, r_base);
+      }
+      nvs.push_back(nv);
+      Lv.push_back(L);
+    }
+    li[i] = k;
+  }
+  std::vector<std::pair<const FqV*, const FqV*>> bj;
+  for (size_t i = 0; i < polys.size(); i++) bj.push_back({polys[i], &Lv[li[i]]});
+  return host_bounds(bj);
+}
+
+// PolyEvalProof::prove_uni_batched_instances (dense_mlpoly.rs:1046-1130) from the bounds of uni_bounds(polys, r)
+int prove_uni_batched(spg_ctx* ctx, ProverGens& g, const std::vector<const FqV*>& polys, const std::vector<FqV>& LZs,
+                      const Fq& r, const FqV& Zr, Tr& t, Tape& tape, Writer& w) {
   t.protocol("polynomial evaluation proof");
   size_t max_nv = 0;
   for (auto p : polys) max_nv = std::max(max_nv, lg2(p->size()));
@@ -296,28 +349,11 @@ int prove_uni_batched(spg_ctx* ctx, ProverGens& g, const std::vector<const FqV*>
     R.push_back(rb);
     rb = fq_mul(rb, r);
   }
-  std::vector<std::pair<size_t, FqV>> Lmap;
   Fq c_base = t.challenge("challenge_c"), c = fq_one();
   FqV LZc(R_size, fq_zero());
   Fq Zrc = fq_zero();
   for (size_t i = 0; i < polys.size(); i++) {
-    const size_t nv = lg2(polys[i]->size());
-    const FqV* L = nullptr;
-    for (auto& kv : Lmap)
-      if (kv.first == nv) L = &kv.second;
-    if (!L) {
-      Fq r_base = fq_one();
-      for (size_t k = 0; k < ((size_t)1 << (nv - nv / 2)); k++) r_base = fq_mul(r_base, r);
-      FqV Lv;
-      Fq lb = fq_one();
-      for (size_t k = 0; k < ((size_t)1 << (nv / 2)); k++) {
-        Lv.push_back(lb);
-        lb = fq_mul(lb, r_base);
-      }
-      Lmap.push_back({nv, Lv});
-      L = &Lmap.back().second;
-    }
-    FqV LZ = host_bound(*polys[i], *L);
+    const FqV& LZ = LZs[i];
     for (size_t k = 0; k < R_size && k < LZ.size(); k++) LZc[k] = fq_add(LZc[k], fq_mul(c, LZ[k]));
     Zrc = fq_add(Zrc, fq_mul(c, Zr[i]));
     c = fq_mul(c, c_base);
@@ -1223,9 +1259,6 @@ static int spg_snark_prove_impl(spg_ctx* ctx, spg_snark_comp* block, spg_snark_c
       hl.push_back(6);
     }
     const size_t n = orig.size();
-    size_t max_size = 0;
-    for (auto p : orig) max_size = std::max(max_size, p->size());
-    for (auto p : shifted) max_size = std::max(max_size, p->size());
     std::vector<std::vector<Pt>> openings(n);
     {
       std::vector<CJob> jobs;
@@ -1240,31 +1273,31 @@ static int spg_snark_prove_impl(spg_ctx* ctx, spg_snark_comp* block, spg_snark_c
         }
     }
     const Fq c = t.challenge("challenge_c");
-    FqV rc_pow(max_size);
+    // the evaluations sum_k poly[k] c^k (lib.rs:2640-2655) from the uni-batched proof's L.Z bounds, computed once
+    // over the pool: sum_k LZ[k] c^k, LZ[k] = sum_j c^(Rs j) poly[j Rs + k]
+    std::vector<const FqV*> all(orig);
+    all.insert(all.end(), shifted.begin(), shifted.end());
+    const std::vector<FqV> LZs = uni_bounds(all, c);
+    size_t rs_max = 0;
+    for (auto& v : LZs) rs_max = std::max(rs_max, v.size());
+    FqV rc_pow(rs_max);
     {
       Fq nc = fq_one();
-      for (size_t i = 0; i < max_size; i++) {
+      for (size_t i = 0; i < rs_max; i++) {
         rc_pow[i] = nc;
         nc = fq_mul(nc, c);
       }
     }
-    FqV oe, se;
-    std::vector<CJob> jobs;
-    for (size_t p = 0; p < n; p++) {
-      Fq x = fq_zero(), y = fq_zero();
-      for (size_t k = 0; k < orig[p]->size(); k++) x = fq_add(x, fq_mul((*orig[p])[k], rc_pow[k]));
-      for (size_t k = 0; k < shifted[p]->size(); k++) y = fq_add(y, fq_mul((*shifted[p])[k], rc_pow[k]));
-      oe.push_back(x);
-      se.push_back(y);
+    FqV ev(2 * n);
+    for (size_t p = 0; p < 2 * n; p++) {
+      Fq x = fq_zero();
+      for (size_t k = 0; k < LZs[p].size(); k++) x = fq_add(x, fq_mul(LZs[p][k], rc_pow[k]));
+      ev[p] = x;
     }
-    for (auto& x : oe) jobs.push_back(CJob(g.gens_1, {x}, fq_zero()));
-    for (auto& y : se) jobs.push_back(CJob(g.gens_1, {y}, fq_zero()));
+    std::vector<CJob> jobs;
+    for (auto& x : ev) jobs.push_back(CJob(g.gens_1, {x}, fq_zero()));
     std::vector<Pt> ce = commit_batch(g, jobs);
-    std::vector<const FqV*> all(orig);
-    all.insert(all.end(), shifted.begin(), shifted.end());
-    FqV ev(oe);
-    ev.insert(ev.end(), se.begin(), se.end());
-    if ((rc = prove_uni_batched(ctx, g, all, c, ev, t, tape, w))) return rc;
+    if ((rc = prove_uni_batched(ctx, g, all, LZs, c, ev, t, tape, w))) return rc;
     w.pts(std::vector<Pt>(ce.begin(), ce.begin() + n));
     w.pts(std::vector<Pt>(ce.begin() + n, ce.end()));
     w.u64(n);
