@@ -1,0 +1,221 @@
+// spg — comb tables for batches of Hyrax row commitments (DensePolynomial::commit_inner, src/dense_mlpoly.rs:184-212,
+// through Commitments::commit, src/commitments.rs:69-92).
+//
+// A batch of B row MSMs over the SAME R <= 1024 generators (every Hyrax row of a polynomial, every polynomial of a
+// commit-queue group) is the prover's biggest latency item at the start of SNARK::prove: the 2 x 512 x 1024 block
+// witness is 1024 rows of 1024 scalars. The bucket pipeline (msm.hip) sorts 25 M signed digits into 1024 x 1024
+// buckets and then reduces 2 M buckets with running sums. Here the generators' small multiples are precomputed
+// instead, once per generator set, in HBM (288 GB per GPU leaves room for it):
+//   comb[w][s][m - 1] = m * 2^(c w) * G_s   (affine Niels, 96 B),  m = 1 .. 2^(c-1), w < W = 253 / c + 1,
+// s < R and one more slot for h. A signed c-bit digit d of scalar i in window w is then ONE table entry
+// +-comb[w][i][|d| - 1], and a row commitment is a plain sum of n W points: no digit sort, no buckets, no running
+// sums. With c = 12 (W = 22, 2048 multiples) the table is 22 x 1025 x 2048 x 96 B = 4.4 GB for R = 1024 and a row
+// costs 22 mixed additions per scalar (the bucket path: 24 at c = 11, plus its bucket reduction).
+//   k_comb_build : one lane per run of 64 consecutive multiples of one (w, s): the first by double-and-add, the
+//                  rest by repeated mixed addition; one batched inversion (Montgomery's trick over the run, Z
+//                  through a global scratch) to affine Niels.
+//   k_comb_accum : one 256-thread workgroup per row: every lane recodes its scalars (one every 256th) into signed
+//                  digits (staged in LDS) and adds their entries in one-lane mixed additions; the 256 lane sums meet
+//                  in LDS, 4 per quad, and a 6-level quad tree (quad.hpp) gives the row's point.
+// The points are the group elements the bucket path computes, so the encodings (k_compress_ext) are identical.
+#include <string.h>
+
+#include <atomic>
+
+#include "ctx.hpp"
+#include "lds.hpp"
+#include "quad.hpp"
+
+namespace spg {
+
+static constexpr int kCombC = 12;
+static constexpr int kCombW = 253 / kCombC + 1;     // 22 windows
+static constexpr int kCombNB = 1 << (kCombC - 1);   // 2048 multiples per (window, slot)
+static constexpr int kCombRun = 64;                 // multiples per build lane
+static constexpr size_t kCombMaxR = 1024;           // widest row the comb covers
+
+// lane L = ((w * NS + s) * runs + k): multiples k * Run + 1 .. (k + 1) * Run of 2^(c w) G_gen, gen = s (s < NS - 1)
+// or hgen (s = NS - 1)
+__global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab, int n1, int NS, int hgen,
+                                                   Niels* __restrict__ comb, Fp* __restrict__ zs, size_t lanes) {
+  const size_t L = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (L >= lanes) return;
+  constexpr int runs = kCombNB / kCombRun;
+  const int k = (int)(L % runs);
+  const size_t ws = L / runs;
+  const int s = (int)(ws % NS), w = (int)(ws / NS);
+  const int gen = s == NS - 1 ? hgen : s;
+  const Niels bn = tab[(size_t)(w * kCombC) * n1 + gen];
+  // (k Run + 1) * base, most significant bit first
+  const uint32_t m0 = (uint32_t)k * kCombRun + 1u;
+  Ext P = niels_to_ext(bn);
+  for (int b = 30 - __builtin_clz(m0); b >= 0; b--) {
+    P = ext_dbl(P);
+    if ((m0 >> b) & 1u) P = ext_madd(P, bn, false);
+  }
+  Niels* out = comb + ws * kCombNB + (size_t)k * kCombRun;
+  Fp* z = zs + L * kCombRun;
+  // forward: X, Y parked in the entry, the prefix product of the Z's in its third field, Z in the scratch
+  Fp pp = fp_one();
+  for (int j = 0; j < kCombRun; j++) {
+    if (j) P = ext_madd(P, bn, false);
+    pp = fp_mul(pp, P.Z);
+    out[j].ypx = P.X;
+    out[j].ymx = P.Y;
+    out[j].t2d = pp;
+    z[j] = P.Z;
+  }
+  // backward: 1/Z_j = (1 / prod_{i <= j} Z_i) * prod_{i < j} Z_i
+  Fp inv = fp_inv(pp);
+  for (int j = kCombRun - 1; j >= 0; j--) {
+    const Fp zi = j ? fp_mul(inv, out[j - 1].t2d) : inv;
+    if (j) inv = fp_mul(inv, z[j]);
+    const Fp x = fp_mul(out[j].ypx, zi), y = fp_mul(out[j].ymx, zi);
+    Niels r;
+    r.ypx = fp_canon(fp_add(y, x));
+    r.ymx = fp_canon(fp_sub(y, x));
+    r.t2d = fp_canon(fp_mul(fp_mul(x, y), c_d2()));
+    out[j] = r;
+  }
+}
+
+// one workgroup per row b: sum_i s_bi G_(gen_offset + i) (+ blind_b h) from the comb (NS slots, h in the last)
+__global__ void __launch_bounds__(256, 3) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
+                                                       int n, int gen_offset, const Niels* __restrict__ comb, int NS,
+                                                       Ext* __restrict__ out) {
+  constexpr uint32_t MASK = (1u << kCombC) - 1u;
+  // the digits of this lane's current scalar (int16 per window, lane-major so a lane reads only its own), then
+  // the lane sums and the quad tree's operands
+  __shared__ uint32_t pts[soa_words<Ext, 256>()];
+  static_assert(kCombW * 256 * 2 <= (int)sizeof(pts), "digit staging fits the point buffer");
+  int16_t* dg = reinterpret_cast<int16_t*>(pts);
+  const int b = blockIdx.x, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int per = n + (blinds ? 1 : 0);
+  const size_t wstride = (size_t)NS * kCombNB;
+  Ext P = ext_identity();
+  for (int i = t; i < per; i += 256) {
+    Fq sm;
+    int s;
+    if (i < n) {
+      sm = scalars[(size_t)b * n + i];
+      s = gen_offset + i;
+    } else {
+      sm = blinds[b];
+      s = NS - 1;
+    }
+    const Fq k = fq_from_mont(sm);
+    int carry = 0;
+#pragma unroll
+    for (int w = 0; w < kCombW; w++) {
+      const int bit = w * kCombC;
+      const int li = bit >> 5, of = bit & 31;
+      uint32_t v = k.l[li] >> of;
+      if (of + kCombC > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+      int d = (int)(v & MASK) + carry;
+      carry = d > kCombNB ? 1 : 0;
+      d -= carry << kCombC;
+      dg[w * 256 + t] = (int16_t)d;
+    }
+    const Niels* cs = comb + (size_t)s * kCombNB;
+#pragma unroll 1
+    for (int w = 0; w < kCombW; w++) {
+      const int d = dg[w * 256 + t];
+      if (d) P = ext_madd(P, cs[(size_t)w * wstride + (d < 0 ? -d : d) - 1], d < 0);
+    }
+  }
+  __syncthreads();
+  soa_put<256>(pts, t, P);
+  __syncthreads();
+  Ext acc = soa_get<256, Ext>(pts, 4 * slot);
+  for (int j = 1; j < 4; j++) acc = quad_add(acc, soa_get<256, Ext>(pts, 4 * slot + j), q);
+  __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put_op<64>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<64>(pts, slot, q), q);
+    __syncthreads();
+  }
+  if (t == 0) out[b] = acc;
+}
+
+// comb tables of all live generator sets, against the process-wide cap (SPG_COMB_GB, default 24)
+static std::atomic<size_t> g_comb_bytes{0};
+
+void comb_free(const spg_gens* g) {
+  if (!g || !g->comb) return;
+  hipFree(g->comb);
+  g_comb_bytes -= g->comb_bytes;
+  g->comb = nullptr;
+  g->comb_slots = 0;
+  g->comb_bytes = 0;
+}
+
+static bool comb_enabled() {
+  static const bool on = !getenv("SPG_COMB") || atoi(getenv("SPG_COMB")) != 0;
+  return on;
+}
+
+// returns 0 when g's comb covers generators [0, need) and h = hgen (hgen < 0: no blinds, any h slot), 1 when the
+// comb path does not apply here (disabled, too wide, over the memory cap, allocation refused), or an SPG error code
+static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen) {
+  if (!comb_enabled() || need > kCombMaxR) return 1;
+  if (g->comb && g->comb_slots >= need && (hgen < 0 || g->comb_h == hgen)) return 0;
+  if (hgen < 0) hgen = (int)g->n;
+  size_t cn = 256;
+  while (cn < need) cn *= 2;
+  cn = std::min(cn, g->n);
+  if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
+  const int NS = (int)cn + 1;
+  const size_t entries = (size_t)kCombW * NS * kCombNB, bytes = entries * sizeof(Niels);
+  static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 24.0) * (1ull << 30);
+  if (g_comb_bytes.load() - (g->comb ? g->comb_bytes : 0) + bytes > cap) return 1;
+  comb_free(g);
+  Niels* comb = nullptr;
+  Fp* zs = nullptr;
+  const size_t lanes = entries / kCombRun;
+  if (hipMalloc(&comb, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  if (hipMalloc(&zs, entries * sizeof(Fp)) != hipSuccess) {
+    (void)hipGetLastError();
+    hipFree(comb);
+    return 1;
+  }
+  hipLaunchKernelGGL(k_comb_build, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, ctx->stream, g->table,
+                     (int)(g->n + 1), NS, hgen, comb, zs, lanes);
+  const hipError_t e = hipGetLastError();
+  const hipError_t e2 = hipStreamSynchronize(ctx->stream);
+  hipFree(zs);
+  if (e != hipSuccess || e2 != hipSuccess) {
+    hipFree(comb);
+    return set_err(ctx, SPG_E_HIP, "comb table build");
+  }
+  g->comb = comb;
+  g->comb_slots = cn;
+  g->comb_h = hgen;
+  g->comb_bytes = bytes;
+  g_comb_bytes += bytes;
+  return 0;
+}
+
+// B row MSMs of n contiguous generators from gen_offset (+ blinds on h): SPG_OK with the rows' points in ext
+// (B Ext, device) and, when d_out is set, their encodings; kCombSkip when the comb does not apply (the caller
+// runs the bucket pipeline); or an SPG error code
+int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+             const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext) {
+  const int rc = comb_ensure(ctx, g, gen_offset + n, h_index);
+  if (rc == 1) return kCombSkip;
+  if (rc) return rc;
+  {
+    const double per = (double)(n + (d_blinds ? 1 : 0));
+    KScope ks(ctx, "msm_comb", 0.0, (double)B * per * kCombW * (1.0 - 1.0 / (double)(1 << kCombC)));
+    hipLaunchKernelGGL(k_comb_accum, dim3((unsigned)B), dim3(256), 0, ctx->stream, d_scalars, d_blinds, (int)n,
+                       (int)gen_offset, g->comb, (int)g->comb_slots + 1, ext);
+  }
+  if (d_out) return compress_ext_device(ctx, ext, B, d_out);
+  SPG_HIP(ctx, hipGetLastError());
+  return SPG_OK;
+}
+
+}  // namespace spg

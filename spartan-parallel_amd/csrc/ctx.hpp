@@ -83,6 +83,10 @@ struct spg_gens {
   spg::Niels* niels = nullptr;   // n+1 affine Niels points (device)
   spg::Niels* table = nullptr;   // [254][n+1] : table[k][i] = 2^k * P_i (device)
   uint8_t* compressed = nullptr; // (n+1) x 32 host copy
+  // comb.hip: small multiples of the first comb_slots generators and of generator comb_h, built on first use
+  mutable spg::Niels* comb = nullptr;
+  mutable size_t comb_slots = 0, comb_bytes = 0;
+  mutable int comb_h = -1;
 };
 
 namespace spg {
@@ -130,6 +134,11 @@ void timer_stop(spg_ctx* c);
 // B fixed-base MSMs of n scalars (device pointers) against generator table g; scalar i of MSM b uses
 // generator d_idx[b*n+i] when d_idx is given, else gen_offset + i; d_blinds (B) multiply generator
 // h_index (-1: g->n). d_out: B x 32 compressed bytes (device). Stream-ordered, no host sync.
+// comb.hip: batches of row MSMs from per-generator-set comb tables (kCombSkip: not applicable, use the buckets)
+static const int kCombSkip = -1;
+int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
+             const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext);
+void comb_free(const spg_gens* g);
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext = nullptr);
 

@@ -879,6 +879,14 @@ static void dispatch_digits_rows(int c, const MsmArgs& a, hipStream_t s) {
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext) {
   hipStream_t s = ctx->stream;
+  // many rows over contiguous generators: the comb tables (comb.hip) replace digit sort, buckets and running sums
+  if (!d_idx && B >= 64 && n <= 1024 && B * (n + (d_blinds ? 1 : 0)) >= ((size_t)1 << 14)) {
+    Ext* ext = d_ext ? d_ext : (Ext*)ws_get(ctx, 17, B * sizeof(Ext) + 64);
+    if (!ext) return set_err(ctx, SPG_E_NOMEM, "msm comb points");
+    const int hi = !d_blinds ? -1 : (h_index < 0 ? (int)g->n : (int)h_index);
+    const int rc = msm_comb(ctx, g, gen_offset, d_scalars, n, B, d_blinds, d_out, hi, ext);
+    if (rc != kCombSkip) return rc;
+  }
   const int c = pick_window(n + (d_blinds ? 1 : 0));
   const int NB = 1 << (c - 1);
   const int W = 253 / c + 1;
@@ -1128,6 +1136,7 @@ extern "C" int spg_gens_free(spg_ctx* ctx, spg_gens* g) {
   if (!g) return SPG_OK;
   if (g->niels) hipFree(g->niels);
   if (g->table) hipFree(g->table);
+  comb_free(g);
   delete[] g->compressed;
   delete g;
   return SPG_OK;

@@ -141,6 +141,30 @@ def test_msm_partial_shards(ctx, oracle, n, world):
     assert spg.points_sum_compress([parts[-1]]) == spg.points_sum_compress([ref])
 
 
+@pytest.mark.parametrize("L,R", [(64, 256), (100, 300), (72, 1000)])
+def test_commit_rows_comb(ctx, oracle, gens64, L, R):
+    """>= 64 rows of <= 1024 scalars (>= 2^14 in all) take the comb tables (comb.hip): one table entry per nonzero
+    signed 12-bit digit, no buckets. Edge scalars (0, 1, -1, 2^252, q - 2^252) put digits of every magnitude class,
+    the top window's carry and all-zero windows into the rows; with and without blinds, against the oracle"""
+    rng = np.random.default_rng(L * 7 + R)
+    pts = gens64.compressed()
+    Z = rand_fq(oracle, rng, L * R)
+    one = oracle.fq_from_u64(1)
+    minus1 = oracle.fq_op("neg", one)[0]
+    p252 = oracle.fq_from_raw([0, 0, 0, 1 << 60])
+    Z[0:R] = minus1
+    Z[R:2 * R] = p252
+    Z[2 * R:3 * R] = oracle.fq_op("neg", p252)[0]
+    Z[3 * R:4 * R] = 0
+    Z[4 * R:5 * R] = one
+    Z[5 * R::7] = minus1
+    assert np.array_equal(gens64.commit_rows(Z, L, R), oracle.commit_rows(pts[:R], pts[1024].tobytes(), Z, L, R))
+    bl = rand_fq(oracle, rng, L)
+    bl[0] = minus1
+    assert np.array_equal(gens64.commit_rows(Z, L, R, bl),
+                          oracle.commit_rows(pts[:R], pts[1024].tobytes(), Z, L, R, bl))
+
+
 def test_commit_rows_wide(ctx, oracle):
     """Hyrax rows of 2^14 scalars (window c = 14, 2^13 bucket counters) in batches of >= 64 rows take the LDS row
     sort too (the SPARK derefs / comb_ops commitments at 2^24 nonzeros have such rows)"""
