@@ -14,9 +14,9 @@
 //   k_comb_build : one lane per run of 64 consecutive multiples of one (w, s): the first by double-and-add, the
 //                  rest by repeated mixed addition; one batched inversion (Montgomery's trick over the run, Z
 //                  through a global scratch) to affine Niels.
-//   k_comb_accum : one 256-thread workgroup per row: every lane recodes its scalars (one every 256th) into signed
-//                  digits (staged in LDS) and adds their entries in one-lane mixed additions; the 256 lane sums meet
-//                  in LDS, 4 per quad, and a 6-level quad tree (quad.hpp) gives the row's point.
+//   k_comb_accum : 256-thread workgroups, S per row (S = 2 for 1024 rows of 1024): every lane recodes its scalars
+//                  into signed digits (staged in LDS) and adds their entries in one-lane mixed additions; the lane
+//                  sums meet per quad (DPP) and in a 6-level LDS quad tree (quad.hpp); k_comb_join adds a row's S parts.
 // The points are the group elements the bucket path computes, so the encodings (k_compress_ext) are identical.
 #include <string.h>
 
@@ -79,21 +79,22 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
   }
 }
 
-// one workgroup per row b: sum_i s_bi G_(gen_offset + i) (+ blind_b h) from the comb (NS slots, h in the last)
-__global__ void __launch_bounds__(256, 3) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
-                                                       int n, int gen_offset, const Niels* __restrict__ comb, int NS,
-                                                       Ext* __restrict__ out) {
+// workgroup (row b, part h) of S per row: sum over the row's scalars i = h * 256 + t + k * 256 S of s_bi G_(gen_offset
+// + i) (+ blind_b h in part 0) from the comb (NS slots, h in the last) into part[b S + h]. The lane sums meet per quad
+// by DPP broadcasts (no LDS), then in a 6-level LDS quad tree; LDS is the tree's 8 KB plus the 11 KB digit staging,
+// so 8 workgroups fit a CU (the one-lane madd throughput needs ~8 resident 256-thread workgroups per CU,
+// scripts/micro/ext_throughput), and S > 1 splits the rows when B alone would not give the chip that many
+__global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
+                                                    int n, int gen_offset, const Niels* __restrict__ comb, int NS,
+                                                    int S, Ext* __restrict__ part) {
   constexpr uint32_t MASK = (1u << kCombC) - 1u;
-  // the digits of this lane's current scalar (int16 per window, lane-major so a lane reads only its own), then
-  // the lane sums and the quad tree's operands
-  __shared__ uint32_t pts[soa_words<Ext, 256>()];
-  static_assert(kCombW * 256 * 2 <= (int)sizeof(pts), "digit staging fits the point buffer");
-  int16_t* dg = reinterpret_cast<int16_t*>(pts);
-  const int b = blockIdx.x, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  __shared__ int16_t dg[kCombW * 256];  // this lane's current scalar's digits (lane-major: a lane reads its own)
+  __shared__ uint32_t pts[soa_words<Ext, 64>()];
+  const int b = blockIdx.x / S, h = blockIdx.x % S, t = threadIdx.x, q = t & 3, slot = t >> 2;
   const int per = n + (blinds ? 1 : 0);
   const size_t wstride = (size_t)NS * kCombNB;
   Ext P = ext_identity();
-  for (int i = t; i < per; i += 256) {
+  for (int i = h * 256 + t; i < per; i += 256 * S) {
     Fq sm;
     int s;
     if (i < n) {
@@ -123,19 +124,37 @@ __global__ void __launch_bounds__(256, 3) k_comb_accum(const Fq* __restrict__ sc
       if (d) P = ext_madd(P, cs[(size_t)w * wstride + (d < 0 ? -d : d) - 1], d < 0);
     }
   }
-  __syncthreads();
-  soa_put<256>(pts, t, P);
-  __syncthreads();
-  Ext acc = soa_get<256, Ext>(pts, 4 * slot);
-  for (int j = 1; j < 4; j++) acc = quad_add(acc, soa_get<256, Ext>(pts, 4 * slot + j), q);
-  __syncthreads();
+  // the quad's four lane sums, broadcast to the quad one after another
+  Ext acc;
+  acc.X = fp_qbcast<0>(P.X);
+  acc.Y = fp_qbcast<0>(P.Y);
+  acc.Z = fp_qbcast<0>(P.Z);
+  acc.T = fp_qbcast<0>(P.T);
+  {
+    Ext o;
+    o.X = fp_qbcast<1>(P.X), o.Y = fp_qbcast<1>(P.Y), o.Z = fp_qbcast<1>(P.Z), o.T = fp_qbcast<1>(P.T);
+    acc = quad_add(acc, o, q);
+    o.X = fp_qbcast<2>(P.X), o.Y = fp_qbcast<2>(P.Y), o.Z = fp_qbcast<2>(P.Z), o.T = fp_qbcast<2>(P.T);
+    acc = quad_add(acc, o, q);
+    o.X = fp_qbcast<3>(P.X), o.Y = fp_qbcast<3>(P.Y), o.Z = fp_qbcast<3>(P.Z), o.T = fp_qbcast<3>(P.T);
+    acc = quad_add(acc, o, q);
+  }
   for (int d = 32; d >= 1; d >>= 1) {
     if (slot >= d && slot < 2 * d) quad_put_op<64>(pts, slot - d, acc, q);
     __syncthreads();
     if (slot < d) acc = quad_add_op(acc, quad_get_op<64>(pts, slot, q), q);
     __syncthreads();
   }
-  if (t == 0) out[b] = acc;
+  if (t == 0) part[blockIdx.x] = acc;
+}
+
+// one quad per row: out[b] = sum of the row's S parts
+__global__ void __launch_bounds__(256) k_comb_join(const Ext* __restrict__ part, int B, int S, Ext* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x, q = t & 3, b = t >> 2;
+  if (b >= B) return;  // whole quads exit together (B quads, 4 lanes each)
+  Ext acc = part[(size_t)b * S];
+  for (int h = 1; h < S; h++) acc = quad_add(acc, part[(size_t)b * S + h], q);
+  if (q == 0) out[b] = acc;
 }
 
 // comb tables of all live generator sets, against the process-wide cap (SPG_COMB_GB, default 24)
@@ -207,11 +226,21 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
   const int rc = comb_ensure(ctx, g, gen_offset + n, h_index);
   if (rc == 1) return kCombSkip;
   if (rc) return rc;
+  const size_t per = n + (d_blinds ? 1 : 0);
+  static const size_t want = getenv("SPG_COMB_WGS") ? (size_t)atol(getenv("SPG_COMB_WGS")) : 2048;
+  const size_t S = std::max<size_t>(1, std::min((want + B - 1) / B, (per + 255) / 256));
+  Ext* part = ext;
+  if (S > 1) {
+    part = (Ext*)ws_get(ctx, 25, B * S * sizeof(Ext) + 64);
+    if (!part) return set_err(ctx, SPG_E_NOMEM, "comb parts");
+  }
   {
-    const double per = (double)(n + (d_blinds ? 1 : 0));
     KScope ks(ctx, "msm_comb", 0.0, (double)B * per * kCombW * (1.0 - 1.0 / (double)(1 << kCombC)));
-    hipLaunchKernelGGL(k_comb_accum, dim3((unsigned)B), dim3(256), 0, ctx->stream, d_scalars, d_blinds, (int)n,
-                       (int)gen_offset, g->comb, (int)g->comb_slots + 1, ext);
+    hipLaunchKernelGGL(k_comb_accum, dim3((unsigned)(B * S)), dim3(256), 0, ctx->stream, d_scalars, d_blinds, (int)n,
+                       (int)gen_offset, g->comb, (int)g->comb_slots + 1, (int)S, part);
+    if (S > 1)
+      hipLaunchKernelGGL(k_comb_join, dim3((unsigned)((4 * B + 255) / 256)), dim3(256), 0, ctx->stream, part, (int)B,
+                         (int)S, ext);
   }
   if (d_out) return compress_ext_device(ctx, ext, B, d_out);
   SPG_HIP(ctx, hipGetLastError());
