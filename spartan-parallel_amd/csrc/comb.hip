@@ -28,24 +28,29 @@
 
 namespace spg {
 
-static constexpr int kCombC = 12;
-static constexpr int kCombW = 253 / kCombC + 1;     // 22 windows
-static constexpr int kCombNB = 1 << (kCombC - 1);   // 2048 multiples per (window, slot)
+// window width: 12 (22 windows, 2048 multiples: 4.4 GB at 1024 generators); SPG_COMB_C = 10 / 11 trade more windows
+// for a smaller table
+static int comb_c() {
+  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(12, atoi(getenv("SPG_COMB_C")))) : 12;
+  return c;
+}
 static constexpr int kCombRun = 64;                 // multiples per build lane
 static constexpr size_t kCombMaxR = 1024;           // widest row the comb covers
 
 // lane L = ((w * NS + s) * runs + k): multiples k * Run + 1 .. (k + 1) * Run of 2^(c w) G_gen, gen = s (s < NS - 1)
 // or hgen (s = NS - 1)
+template <int C>
 __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab, int n1, int NS, int hgen,
                                                    Niels* __restrict__ comb, Fp* __restrict__ zs, size_t lanes) {
+  constexpr int NB = 1 << (C - 1);
   const size_t L = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (L >= lanes) return;
-  constexpr int runs = kCombNB / kCombRun;
+  constexpr int runs = NB / kCombRun;
   const int k = (int)(L % runs);
   const size_t ws = L / runs;
   const int s = (int)(ws % NS), w = (int)(ws / NS);
   const int gen = s == NS - 1 ? hgen : s;
-  const Niels bn = tab[(size_t)(w * kCombC) * n1 + gen];
+  const Niels bn = tab[(size_t)(w * C) * n1 + gen];
   // (k Run + 1) * base, most significant bit first
   const uint32_t m0 = (uint32_t)k * kCombRun + 1u;
   Ext P = niels_to_ext(bn);
@@ -53,7 +58,7 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
     P = ext_dbl(P);
     if ((m0 >> b) & 1u) P = ext_madd(P, bn, false);
   }
-  Niels* out = comb + ws * kCombNB + (size_t)k * kCombRun;
+  Niels* out = comb + ws * NB + (size_t)k * kCombRun;
   Fp* z = zs + L * kCombRun;
   // forward: X, Y parked in the entry, the prefix product of the Z's in its third field, Z in the scratch
   Fp pp = fp_one();
@@ -84,15 +89,17 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
 // by DPP broadcasts (no LDS), then in a 6-level LDS quad tree; LDS is the tree's 8 KB plus the 11 KB digit staging,
 // so 8 workgroups fit a CU (the one-lane madd throughput needs ~8 resident 256-thread workgroups per CU,
 // scripts/micro/ext_throughput), and S > 1 splits the rows when B alone would not give the chip that many
+template <int C>
 __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
                                                     int n, int gen_offset, const Niels* __restrict__ comb, int NS,
                                                     int S, Ext* __restrict__ part) {
-  constexpr uint32_t MASK = (1u << kCombC) - 1u;
-  __shared__ int16_t dg[kCombW * 256];  // this lane's current scalar's digits (lane-major: a lane reads its own)
+  constexpr int W = 253 / C + 1, NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  __shared__ int16_t dg[W * 256];  // this lane's current scalar's digits (lane-major: a lane reads its own)
   __shared__ uint32_t pts[soa_words<Ext, 64>()];
   const int b = blockIdx.x / S, h = blockIdx.x % S, t = threadIdx.x, q = t & 3, slot = t >> 2;
   const int per = n + (blinds ? 1 : 0);
-  const size_t wstride = (size_t)NS * kCombNB;
+  const size_t wstride = (size_t)NS * NB;
   Ext P = ext_identity();
   for (int i = h * 256 + t; i < per; i += 256 * S) {
     Fq sm;
@@ -107,19 +114,19 @@ __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scala
     const Fq k = fq_from_mont(sm);
     int carry = 0;
 #pragma unroll
-    for (int w = 0; w < kCombW; w++) {
-      const int bit = w * kCombC;
+    for (int w = 0; w < W; w++) {
+      const int bit = w * C;
       const int li = bit >> 5, of = bit & 31;
       uint32_t v = k.l[li] >> of;
-      if (of + kCombC > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+      if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
       int d = (int)(v & MASK) + carry;
-      carry = d > kCombNB ? 1 : 0;
-      d -= carry << kCombC;
+      carry = d > NB ? 1 : 0;
+      d -= carry << C;
       dg[w * 256 + t] = (int16_t)d;
     }
-    const Niels* cs = comb + (size_t)s * kCombNB;
+    const Niels* cs = comb + (size_t)s * NB;
 #pragma unroll 1
-    for (int w = 0; w < kCombW; w++) {
+    for (int w = 0; w < W; w++) {
       const int d = dg[w * 256 + t];
       if (d) P = ext_madd(P, cs[(size_t)w * wstride + (d < 0 ? -d : d) - 1], d < 0);
     }
@@ -184,8 +191,8 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen) {
   while (cn < need) cn *= 2;
   cn = std::min(cn, g->n);
   if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
-  const int NS = (int)cn + 1;
-  const size_t entries = (size_t)kCombW * NS * kCombNB, bytes = entries * sizeof(Niels);
+  const int NS = (int)cn + 1, C = comb_c();
+  const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
   static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 24.0) * (1ull << 30);
   if (g_comb_bytes.load() - (g->comb ? g->comb_bytes : 0) + bytes > cap) return 1;
   comb_free(g);
@@ -201,8 +208,13 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen) {
     hipFree(comb);
     return 1;
   }
-  hipLaunchKernelGGL(k_comb_build, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, ctx->stream, g->table,
-                     (int)(g->n + 1), NS, hgen, comb, zs, lanes);
+  const dim3 gb((unsigned)((lanes + 63) / 64)), tb(64);
+  if (C == 10)
+    hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes);
+  else if (C == 11)
+    hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes);
+  else
+    hipLaunchKernelGGL(k_comb_build<12>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes);
   const hipError_t e = hipGetLastError();
   const hipError_t e2 = hipStreamSynchronize(ctx->stream);
   hipFree(zs);
@@ -235,9 +247,19 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
     if (!part) return set_err(ctx, SPG_E_NOMEM, "comb parts");
   }
   {
-    KScope ks(ctx, "msm_comb", 0.0, (double)B * per * kCombW * (1.0 - 1.0 / (double)(1 << kCombC)));
-    hipLaunchKernelGGL(k_comb_accum, dim3((unsigned)(B * S)), dim3(256), 0, ctx->stream, d_scalars, d_blinds, (int)n,
-                       (int)gen_offset, g->comb, (int)g->comb_slots + 1, (int)S, part);
+    const int C = comb_c();
+    KScope ks(ctx, "msm_comb", 0.0, (double)B * per * (253 / C + 1) * (1.0 - 1.0 / (double)(1 << C)));
+    const dim3 ga((unsigned)(B * S)), ta(256);
+    const int NS = (int)g->comb_slots + 1;
+    if (C == 10)
+      hipLaunchKernelGGL(k_comb_accum<10>, ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, g->comb,
+                         NS, (int)S, part);
+    else if (C == 11)
+      hipLaunchKernelGGL(k_comb_accum<11>, ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, g->comb,
+                         NS, (int)S, part);
+    else
+      hipLaunchKernelGGL(k_comb_accum<12>, ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, g->comb,
+                         NS, (int)S, part);
     if (S > 1)
       hipLaunchKernelGGL(k_comb_join, dim3((unsigned)((4 * B + 255) / 256)), dim3(256), 0, ctx->stream, part, (int)B,
                          (int)S, ext);
