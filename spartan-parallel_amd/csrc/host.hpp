@@ -260,6 +260,11 @@ struct HostGens {
     std::vector<size_t> tjob(terms.size());
     for (size_t j = 0; j < J; j++)
       for (size_t k = tfirst[j]; k < tfirst[j + 1]; k++) tjob[k] = j;
+    // The table entry of a unit depends only on the scalar byte, not on the running sum, so the entry kPf units
+    // ahead is prefetched while this one is added: a small DotProductProofLog's rounds read ~1000 random entries of
+    // ~1 MB tables per generator, which mostly miss the caches (host-path proofs 1.63 -> 0.98 ms per SNARK::prove in
+    // situ, scripts/gpu_r03zm.sh; a standalone micro with warm tables showed no gain). SPG_HOST_PREFETCH=0: off.
+    static const size_t kPf = getenv("SPG_HOST_PREFETCH") ? (size_t)atol(getenv("SPG_HOST_PREFETCH")) : 3;
     pool().parallel_for((int)S, [&](int si) {
       const size_t s = (size_t)si, u0 = slice_lo(s), u1 = slice_lo(s + 1);
       size_t u = u0;
@@ -267,6 +272,12 @@ struct HostGens {
         const size_t j = tjob[u / 32], ue = std::min(u1, 32 * tfirst[j + 1]);
         h::HExt acc = h::hext_identity();
         for (; u < ue; u++) {
+          if (kPf && u + kPf < u1) {
+            const Term& tp = terms[(u + kPf) / 32];
+            const char* e = (const char*)&tp.fb->tab[((u + kPf) % 32) * 256 + tp.b[(u + kPf) % 32]];
+            __builtin_prefetch(e);
+            __builtin_prefetch(e + sizeof(h::HNiels) - 1);
+          }
           const Term& tm = terms[u / 32];
           const int w = (int)(u % 32);
           if (tm.b[w]) acc = h::hext_madd(acc, tm.fb->tab[w * 256 + tm.b[w]]);

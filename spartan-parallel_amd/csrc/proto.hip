@@ -393,6 +393,9 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
 int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const FqV& x, const Fq& blind_x, const FqV& a,
                          const Fq& y, const Fq& blind_y, DotProductProofLogP* out, Pt* Cy_out) {
   g_msm_laps.lap("outside_bullet");
+  // SPG_TRACE >= 3: this proof's own laps (the difference of the cumulative ones), one line per proof
+  static const bool per_proof = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 3;
+  const std::vector<std::pair<std::string, double>> laps0 = per_proof ? g_msm_laps.acc : decltype(laps0)();
   t.protocol("dot product proof (log)");
   size_t n = x.size();
   size_t lg = 0;
@@ -606,6 +609,20 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   if (Cy_out) *Cy_out = Cy;
   g_msm_laps.lap("bullet_host");
   g_msm_laps.print();
+  if (per_proof) {
+    fprintf(stderr, "[spg] DotProductProofLog n=%zu %s:", n, on_host ? "host" : (mbk ? "device" : "device-flat"));
+    double tot = 0;
+    for (auto& a : g_msm_laps.acc) {
+      double before = 0;
+      for (auto& b : laps0)
+        if (b.first == a.first) before = b.second;
+      if (a.first != "outside_bullet" && a.second - before > 0.5) {
+        fprintf(stderr, " %s=%.0f", a.first.c_str(), a.second - before);
+        tot += a.second - before;
+      }
+    }
+    fprintf(stderr, " total=%.0f\n", tot);
+  }
   return 0;
 }
 
