@@ -37,6 +37,20 @@ void* pinned_get(spg_ctx* c, size_t bytes) {
   return c->pinned;
 }
 
+void* enc_stage_get(spg_ctx* c, size_t bytes) {
+  if (bytes <= c->enc_stage_bytes) return c->enc_stage;
+  if (c->enc_stage) hipHostFree(c->enc_stage);
+  c->enc_stage = nullptr;
+  c->enc_stage_bytes = 0;
+  const size_t sz = std::max<size_t>((bytes + (1 << 16) - 1) & ~(size_t)((1 << 16) - 1), 1 << 16);
+  if (hipHostMalloc(&c->enc_stage, sz) != hipSuccess) {
+    c->enc_stage = nullptr;
+    return nullptr;
+  }
+  c->enc_stage_bytes = sz;
+  return c->enc_stage;
+}
+
 void* mapped_get(spg_ctx* c, size_t bytes, void** dev) {
   static const bool on = !getenv("SPG_MAPPED_BUCKETS") || atoi(getenv("SPG_MAPPED_BUCKETS")) != 0;
   if (!on) return nullptr;
@@ -354,6 +368,7 @@ extern "C" int spg_free(spg_ctx* c) {
   for (auto& s : c->ws)
     if (s.p) hipFree(s.p);
   if (c->pinned) hipHostFree(c->pinned);
+  if (c->enc_stage) hipHostFree(c->enc_stage);
   if (c->mapped) hipHostFree(c->mapped);
   if (c->mbox) hipHostFree((void*)c->mbox);
   if (c->d_counter) hipFree(c->d_counter);

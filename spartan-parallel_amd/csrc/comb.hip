@@ -84,24 +84,28 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
   }
 }
 
-// workgroup (row b, part h) of S per row: sum over the row's scalars i = h * 256 + t + k * 256 S of s_bi G_(gen_offset
-// + i) (+ blind_b h in part 0) from the comb (NS slots, h in the last) into part[b S + h]. The lane sums meet per quad
-// by DPP broadcasts (no LDS), then in a 6-level LDS quad tree; LDS is the tree's 8 KB plus the 11 KB digit staging,
-// so 8 workgroups fit a CU (the one-lane madd throughput needs ~8 resident 256-thread workgroups per CU,
-// scripts/micro/ext_throughput), and S > 1 splits the rows when B alone would not give the chip that many
-template <int C>
+// workgroup (row b, part h) of S per row, G window groups per scalar: wave v of the workgroup takes window group
+// j = v mod G (uniform per wave, so no divergence) of its 64 scalars (v / G) * 64 + lane of the workgroup's 256 / G;
+// part h covers scalars h * 256/G + i_local + k * S * 256/G of the row (+ blind_b h as scalar n). A lane recomputes
+// the signed-digit carry into its group from the lower windows, stages its group's digits in LDS and adds their
+// entries in one-lane mixed additions; the lane sums meet per quad by DPP broadcasts (no LDS), then in a 6-level
+// LDS quad tree, one point per workgroup into part[b S + h]. G > 1 gives few rows (a SPARK derefs commit: 128 x 256)
+// more lanes, so each lane's chain of dependent additions is W / G long; with G = 1 and S = 2 the 1024-row block
+// witness fills the chip with 2048 workgroups (~8 per CU: LDS is the tree's 8 KB plus <= 11 KB of digits)
+template <int C, int G>
 __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
                                                     int n, int gen_offset, const Niels* __restrict__ comb, int NS,
                                                     int S, Ext* __restrict__ part) {
-  constexpr int W = 253 / C + 1, NB = 1 << (C - 1);
+  constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, SPW = 256 / G;
   constexpr uint32_t MASK = (1u << C) - 1u;
-  __shared__ int16_t dg[W * 256];  // this lane's current scalar's digits (lane-major: a lane reads its own)
+  __shared__ int16_t dg[WG * 256];  // this lane's digits of its group (lane-major: a lane reads its own)
   __shared__ uint32_t pts[soa_words<Ext, 64>()];
   const int b = blockIdx.x / S, h = blockIdx.x % S, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int wave = t >> 6, j = wave % G, w0 = j * WG, nx = W - w0 < WG ? W - w0 : WG;
   const int per = n + (blinds ? 1 : 0);
   const size_t wstride = (size_t)NS * NB;
   Ext P = ext_identity();
-  for (int i = h * 256 + t; i < per; i += 256 * S) {
+  for (int i = h * SPW + (wave / G) * 64 + (t & 63); i < per; i += SPW * S) {
     Fq sm;
     int s;
     if (i < n) {
@@ -115,6 +119,7 @@ __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scala
     int carry = 0;
 #pragma unroll
     for (int w = 0; w < W; w++) {
+      if (w >= w0 + WG) break;  // uniform per wave
       const int bit = w * C;
       const int li = bit >> 5, of = bit & 31;
       uint32_t v = k.l[li] >> of;
@@ -122,13 +127,13 @@ __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scala
       int d = (int)(v & MASK) + carry;
       carry = d > NB ? 1 : 0;
       d -= carry << C;
-      dg[w * 256 + t] = (int16_t)d;
+      if (w >= w0) dg[(w - w0) * 256 + t] = (int16_t)d;
     }
-    const Niels* cs = comb + (size_t)s * NB;
+    const Niels* cs = comb + (size_t)s * NB + (size_t)w0 * wstride;
 #pragma unroll 1
-    for (int w = 0; w < W; w++) {
-      const int d = dg[w * 256 + t];
-      if (d) P = ext_madd(P, cs[(size_t)w * wstride + (d < 0 ? -d : d) - 1], d < 0);
+    for (int x = 0; x < nx; x++) {
+      const int d = dg[x * 256 + t];
+      if (d) P = ext_madd(P, cs[(size_t)x * wstride + (d < 0 ? -d : d) - 1], d < 0);
     }
   }
   // the quad's four lane sums, broadcast to the quad one after another
@@ -240,10 +245,17 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
   if (rc) return rc;
   const size_t per = n + (d_blinds ? 1 : 0);
   static const size_t want = getenv("SPG_COMB_WGS") ? (size_t)atol(getenv("SPG_COMB_WGS")) : 2048;
-  const size_t S = std::max<size_t>(1, std::min((want + B - 1) / B, (per + 255) / 256));
+  // window groups per scalar: few rows get up to 4 lanes per scalar (>= 2^17 lanes when there are that few)
+  static const size_t gmax = getenv("SPG_COMB_GMAX") ? (size_t)atol(getenv("SPG_COMB_GMAX")) : 4;
+  size_t G = 1;
+  while (G < gmax && G < 4 && B * per * G < ((size_t)1 << 17)) G *= 2;
+  const size_t spw = 256 / G;
+  const size_t S = std::max<size_t>(1, std::min((want + B - 1) / B, (per + spw - 1) / spw));
   Ext* part = ext;
   if (S > 1) {
-    part = (Ext*)ws_get(ctx, 25, B * S * sizeof(Ext) + 64);
+    // the commit queue's second stream runs row commits while the main stream's block-witness commit is in flight:
+    // each stream has its own parts slot
+    part = (Ext*)ws_get(ctx, ctx->stream == ctx->stream2 ? 27 : 25, B * S * sizeof(Ext) + 64);
     if (!part) return set_err(ctx, SPG_E_NOMEM, "comb parts");
   }
   {
@@ -251,15 +263,22 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
     KScope ks(ctx, "msm_comb", 0.0, (double)B * per * (253 / C + 1) * (1.0 - 1.0 / (double)(1 << C)));
     const dim3 ga((unsigned)(B * S)), ta(256);
     const int NS = (int)g->comb_slots + 1;
-    if (C == 10)
-      hipLaunchKernelGGL(k_comb_accum<10>, ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, g->comb,
-                         NS, (int)S, part);
-    else if (C == 11)
-      hipLaunchKernelGGL(k_comb_accum<11>, ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, g->comb,
-                         NS, (int)S, part);
-    else
-      hipLaunchKernelGGL(k_comb_accum<12>, ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, g->comb,
-                         NS, (int)S, part);
+#define SPG_COMB_LAUNCH(CC, GG)                                                                                  \
+  hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, \
+                     g->comb, NS, (int)S, part)
+    const int key = C * 8 + (int)G;
+    switch (key) {
+      case 10 * 8 + 1: SPG_COMB_LAUNCH(10, 1); break;
+      case 10 * 8 + 2: SPG_COMB_LAUNCH(10, 2); break;
+      case 10 * 8 + 4: SPG_COMB_LAUNCH(10, 4); break;
+      case 11 * 8 + 1: SPG_COMB_LAUNCH(11, 1); break;
+      case 11 * 8 + 2: SPG_COMB_LAUNCH(11, 2); break;
+      case 11 * 8 + 4: SPG_COMB_LAUNCH(11, 4); break;
+      case 12 * 8 + 1: SPG_COMB_LAUNCH(12, 1); break;
+      case 12 * 8 + 2: SPG_COMB_LAUNCH(12, 2); break;
+      default: SPG_COMB_LAUNCH(12, 4); break;
+    }
+#undef SPG_COMB_LAUNCH
     if (S > 1)
       hipLaunchKernelGGL(k_comb_join, dim3((unsigned)((4 * B + 255) / 256)), dim3(256), 0, ctx->stream, part, (int)B,
                          (int)S, ext);

@@ -22,6 +22,8 @@ struct spg_ctx {
   hipEvent_t ev_pre = nullptr;
   void* pinned = nullptr;          // page-locked host staging (pinned_get), grown on demand
   size_t pinned_bytes = 0;
+  void* enc_stage = nullptr;       // page-locked staging of points encoded on the host (enc_stage_get)
+  size_t enc_stage_bytes = 0;
   // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into
   // directly (mapped_get): the host reads them after the stream synchronisation, no D2H copy launch
   void* mapped = nullptr;
@@ -121,6 +123,7 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
 // page-locked host staging of at least `bytes` (contents undefined; valid until the next larger request,
 // which synchronises the stream before freeing the old buffer)
 void* pinned_get(spg_ctx* c, size_t bytes);
+void* enc_stage_get(spg_ctx* c, size_t bytes);  // callers synchronise before returning: no copy is ever in flight
 
 // coherent mapped host memory of at least `bytes`: host pointer returned, device alias in *dev (contents
 // undefined; a larger request synchronises the stream before freeing the old buffer). Null when

@@ -293,7 +293,7 @@ enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
   kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp,  // 60 .. 89
-  kWsMultiExt = 120, kWsMultiOut  // (snark.hip uses 91 .. 93, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
+  kWsMultiExt = 120, kWsMultiOut, kWsCommitExt  // (snark.hip uses 91 .. 93, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -309,6 +309,44 @@ ProverGens gens_view(spg_gens* dev, size_t nv) {
   g.gens_1.G = {n};
   g.gens_1.h = n + 1;
   return g;
+}
+
+// Encodings of B device points into host Pt's. Up to SPG_HOST_ENC_MAX (384) points the points come down (128 B each)
+// and are encoded on the host pool: one encoding is a ~2.4 us inverse square root on a host core, while
+// k_compress_ext gives each point one GPU lane whose ~250 dependent squarings take ~130 us whatever the count.
+// Larger batches encode on the device (d_out: 32 B per point of device scratch).
+static int encode_points(spg_ctx* ctx, const Ext* d_ext, size_t B, Pt* out, uint8_t* d_out) {
+  static const size_t host_max = getenv("SPG_HOST_ENC_MAX") ? (size_t)atol(getenv("SPG_HOST_ENC_MAX")) : 384;
+  if (B <= host_max) {
+    Ext* h = (Ext*)enc_stage_get(ctx, B * sizeof(Ext));
+    if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
+    SPG_HIP(ctx, hipMemcpyAsync(h, d_ext, B * sizeof(Ext), hipMemcpyDeviceToHost, ctx->stream));
+    SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int C = B >= 16 ? (int)std::min<size_t>(B / 2, (size_t)pool().size() + 1) : 1;
+    auto enc = [&](int c) {
+      for (size_t i = B * c / C; i < B * (c + 1) / C; i++) out[i] = compress(h::hext_from_dev(h[i]));
+    };
+    if (C == 1)
+      enc(0);
+    else
+      pool().parallel_for(C, enc);
+    return 0;
+  }
+  int rc = compress_ext_device(ctx, d_ext, B, d_out);
+  if (rc) return rc;
+  SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, ctx->stream));
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// L rows of R device scalars on the latency-path generators into device points: the comb tables when they apply
+// (>= 64 rows, >= 2^14 scalars in all), else the latency-path bucket kernels
+static int rows_to_points(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Ext* d_ext) {
+  if (L >= 64 && L * R >= ((size_t)1 << 14)) {
+    const int rc = msm_comb(ctx, g.dev, 0, d_Z, R, L, nullptr, nullptr, -1, d_ext);
+    if (rc != kCombSkip) return rc;
+  }
+  return msm_small_device(ctx, g.dev, 0, d_Z, R, L, nullptr, d_ext, nullptr, -1);
 }
 
 // L Hyrax rows of R consecutive device scalars each -> L compressed row commitments (host). Rows of up to
@@ -340,10 +378,14 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
         SPG_HIP(ctx, hipMemcpyAsync(bk, d_bk, sizeof(Ext) * nb * NB, hipMemcpyDeviceToHost, ctx->stream));
       SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
       bucket_finals(bk, nb, NB, out + r0);
+    } else if (small) {
+      Ext* d_ext = (Ext*)ws_get(ctx, kWsCommitExt, sizeof(Ext) * nb + 64);
+      if (!d_ext) return set_err(ctx, SPG_E_NOMEM, "commit points");
+      int rc = rows_to_points(ctx, g, d_Z + r0 * R, R, nb, d_ext);
+      if (!rc) rc = encode_points(ctx, d_ext, nb, out + r0, d_out);  // synchronous: d_ext, d_out reused next chunk
+      if (rc) return rc;
     } else {
-      int rc = small ? msm_small_compressed(ctx, g.dev, 0, d_Z + r0 * R, R, nb, d_out)
-                     : msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr,
-                                        (long)(g.n_pc + 1));
+      int rc = msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr, (long)(g.n_pc + 1));
       if (rc) return rc;
       SPG_HIP(ctx, hipMemcpyAsync(out + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
       SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
@@ -369,15 +411,13 @@ int commit_rows_many(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& job
     size_t o = 0;
     for (const RowJob& j : jobs) {
       if (!merged(j)) continue;
-      int rc = msm_small_device(ctx, g.dev, 0, j.d_Z, j.R, j.L, nullptr, d_ext + o, nullptr, -1);
+      int rc = rows_to_points(ctx, g, j.d_Z, j.R, j.L, d_ext + o);
       if (rc) return rc;
       o += j.L;
     }
-    int rc = compress_ext_device(ctx, d_ext, tot, d_out);
-    if (rc) return rc;
     std::vector<Pt> rows(tot);
-    SPG_HIP(ctx, hipMemcpyAsync(rows.data(), d_out, 32 * tot, hipMemcpyDeviceToHost, ctx->stream));
-    SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = encode_points(ctx, d_ext, tot, rows.data(), d_out);
+    if (rc) return rc;
     o = 0;
     for (const RowJob& j : jobs) {
       if (!merged(j)) continue;
