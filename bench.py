@@ -369,6 +369,7 @@ def main_snark(a):
             "ms_per_step_incl_witness_upload": round(t_incl * 1e3, 3),
             "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
             "ms_per_step_min": round(min(laps) * 1e3, 3), "verify_ms": round(t_verify * 1e3, 2),
+            "ms_per_step_laps": [round(x * 1e3, 2) for x in laps],
             "verify_ok": verify_ok, "cpu_verify_ms_1thread": None if cpu_verify_ms is None else round(cpu_verify_ms, 1),
             "encode_s": round(t_encode, 3), "host_gen_s": round(t_gen, 3), "kernels": kernel_table(prof, a.steps),
         }
