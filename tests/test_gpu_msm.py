@@ -141,7 +141,9 @@ def test_msm_partial_shards(ctx, oracle, n, world):
     assert spg.points_sum_compress([parts[-1]]) == spg.points_sum_compress([ref])
 
 
-@pytest.mark.parametrize("L,R", [(64, 256), (100, 300), (72, 1000)])
+# (512, 64): latency-path rows through the comb with 4 window groups, encoded on the device (> 384 points);
+# (100, 100): below 2^14 scalars, latency-path buckets, encoded on the host pool
+@pytest.mark.parametrize("L,R", [(64, 256), (100, 300), (72, 1000), (512, 64), (100, 100)])
 def test_commit_rows_comb(ctx, oracle, gens64, L, R):
     """>= 64 rows of <= 1024 scalars (>= 2^14 in all) take the comb tables (comb.hip): one table entry per nonzero
     signed 12-bit digit, no buckets. Edge scalars (0, 1, -1, 2^252, q - 2^252) put digits of every magnitude class,
