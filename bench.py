@@ -8,12 +8,16 @@ torch.distributed.run, one rank per GPU.
     on a synthetic 2^20-constraint program (2 block types x 2^9 executions x 2^10 constraints), instances
     encoded and witness resident in HBM before the timed region; every step produces the full bincode(SNARK),
     compared byte-for-byte with the CPU oracle's. Multi-GPU: independent replicas (weak scaling).
-    At N = 1 the same line also carries SURVEY 8d config 2 (`config2_msm`: one 2^16-point MSM) and config 5
-    (`config5_spark`: multi_evaluate + SparseMatPolyEvalProof::prove over 3 x 2^24 nonzeros), each measured in
-    this run with its own roofline and CPU baselines (--extras none skips them).
+    At N = 1 the same line also carries every other single-GPU BASELINE config, each measured in this run with its
+    own roofline and CPU baselines (--extras none skips them): config 2 (`config2_msm`: one 2^16-point MSM;
+    `config2_rows`: the 1024 x 1024 Hyrax row commit of a 2^20-entry polynomial), config 4 on one GPU
+    (`config4_r1cs`: R1CSProof::prove over P = 8 x 2^9 x 2^10 = 2^22 constraints), config 5 (`config5_spark`:
+    multi_evaluate + SparseMatPolyEvalProof::prove over 3 x 2^24 nonzeros) and config 1 (`config1_cpu`: the 2^12
+    SNARK::prove on the CPU path alone, with the reference's per-phase Timer breakdown).
 --workload r1cs: R1CSProof::prove alone (src/r1csproof.rs:210-685); --mode shard splits ONE proof over the ranks
-    by instance with a per-round allgather (spg_set_comm); the shard default is SURVEY 8d config 4's shape,
-    P = 8 instances x 2^9 executions x 2^10 constraints = 2^22.
+    by instance with a per-round allgather; the shard default is SURVEY 8d config 4's shape, P = 8 instances x 2^9
+    executions x 2^10 constraints = 2^22. Sharded modes exchange over libspg's own RCCL transport
+    (spg_set_comm_rccl) whenever the backend is nccl; --comm callback selects the torch.distributed callback.
 --workload spark: SURVEY 8d config 5 alone; --workload msm: SURVEY 8d config 2 alone (both strong scaling
     over the ranks by default).
 
@@ -55,7 +59,8 @@ CONFIGS = {
 # run: a kernel's traffic depends on its launch size, so one workload's figures are never reported for another
 TRAFFIC = {w: os.path.join(ROOT, "profiles", f) for w, f in (
     ("snark", "r03_pmc_traffic.json"), ("msm16", "r03_pmc_traffic_msm_2e16.json"),
-    ("spark24", "r03_pmc_traffic_spark_2e24.json"))}
+    ("spark24", "r03_pmc_traffic_spark_2e24.json"), ("rows", "r04_pmc_traffic_rows_1024.json"),
+    ("r1cs22", "r04_pmc_traffic_r1cs_2e22.json"))}
 
 
 def parse():
@@ -77,9 +82,12 @@ def parse():
     ap.add_argument("--log-cons", type=int, default=10, help="snark: 2^k constraints per block")
     ap.add_argument("--log-proofs", type=int, default=9, help="snark: 2^k executions per block")
     ap.add_argument("--log-nnz", type=int, default=24, help="spark: 2^k nonzeros per matrix (x3 matrices)")
-    ap.add_argument("--cpu-log-nnz", type=int, default=15, help="spark: CPU baseline sample size")
-    ap.add_argument("--extras", default="msm,spark",
-                    help="snark at N = 1: the other BASELINE configs measured in the same run (msm, spark; 'none')")
+    ap.add_argument("--cpu-log-nnz", type=int, default=16, help="spark: CPU baseline sample size")
+    ap.add_argument("--extras", default="msm,rows,r1cs,spark,cpu1",
+                    help="snark at N = 1: the other BASELINE configs measured in the same run "
+                         "(msm, rows, r1cs, spark, cpu1; 'none')")
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "callback"],
+                    help="sharded modes: libspg's RCCL transport (auto: with the nccl backend) or the torch callback")
     ap.add_argument("--traffic", default=None, help="per-launch HBM bytes from rocprofv3 --pmc (scripts/pmc_traffic.py)")
     return ap.parse_args()
 
@@ -126,6 +134,19 @@ class Env:
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
+
+
+def install_comm(env, ctx, how="auto"):
+    """the exchange transport of a sharded call: libspg's own RCCL communicator (spg_set_comm_rccl: ncclAllGather on
+    the context's stream over xGMI, no Python per exchange) with the nccl backend, else the torch.distributed
+    callback (spg_set_comm); returns the transport's name"""
+    import spg
+
+    if how == "rccl" or (how == "auto" and env.backend == "nccl"):
+        ctx.set_comm_rccl(env.rank, env.world, env.dist)
+        return "rccl (spg_set_comm_rccl)"
+    ctx.set_comm(env.rank, env.world, spg.torch_allgather(env.dist, device=env.comm_device))
+    return f"callback (torch.distributed {env.backend})"
 
 
 def timed(env, step, steps, warmup):
@@ -344,12 +365,19 @@ def main_snark(a):
     extras = {}
     if env.world == 1 and a.extras != "none":
         want = set(a.extras.split(","))
+        cpu_on = not a.no_cpu_baseline
         if "msm" in want:
-            extras["config2_msm"] = guarded(lambda: msm_core(env, ctx, 16, a.steps, a.warmup, not a.no_cpu_baseline,
-                                                             TRAFFIC["msm16"]))
+            extras["config2_msm"] = guarded(lambda: msm_core(env, ctx, 16, a.steps, a.warmup, cpu_on, TRAFFIC["msm16"]))
+        if "rows" in want:
+            extras["config2_rows"] = guarded(lambda: rows_core(env, ctx, a.steps, a.warmup, cpu_on, TRAFFIC["rows"]))
+        if "r1cs" in want:
+            extras["config4_r1cs"] = guarded(lambda: r1cs_core(env, ctx, "r1cs_2e22_p8", False, 5, 1, cpu_on,
+                                                               TRAFFIC["r1cs22"]))
         if "spark" in want:
             extras["config5_spark"] = guarded(lambda: spark_core(env, ctx, 24, a.cpu_log_nnz, 5, 1, "replicas",
-                                                                 not a.no_cpu_baseline, TRAFFIC["spark24"]))
+                                                                 cpu_on, TRAFFIC["spark24"]))
+        if "cpu1" in want and cpu_on:
+            extras["config1_cpu"] = guarded(cpu1_core)
     if env.rank == 0:
         out = {
             "metric": "R1CS constraints/sec (SNARK::prove) at 2^20 vars; proof bytes bit-exact",
@@ -386,22 +414,26 @@ def guarded(fn):
         return {"error": repr(e)[:500]}
 
 
-# ---------------------------------------------------------------- R1CSProof::prove (config 4 when sharded)
-def main_r1cs(a):
-    env = Env(a)
+# ---------------------------------------------------------------- R1CSProof::prove (config 4)
+def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, comm="auto"):
+    """R1CSProof::prove (src/r1csproof.rs:210-685) on the CONFIGS shape `cfg`. shard: ONE proof split over the ranks by
+    instance, its per-round (e0, e2, e3) sums and the final gathers over the ranks (RCCL with the nccl
+    backend) -> strong scaling; else an independent proof per rank (weak). A step is one whole proof with the witness
+    resident in HBM. CPU baselines (rank 0, N = 1): the oracle on the full workload on 1 host thread (its bytes are
+    also the bit-exactness check), and one independent oracle proof per usable core on a 2^6-execution sample."""
     import spg
     import workload
 
-    shard = (a.mode or "replicas") == "shard" and env.world > 1
-    cfg = a.config or ("r1cs_2e22_p8" if shard else "r1cs_2e20")
     nc, npf, nws = CONFIGS[cfg]
-    ctx = spg.Context(env.gpu)
-    if shard:  # ONE proof of the configured shape split over the ranks by instance
+    transport = None
+    if shard:
         p0, p1 = spg.shard_range(len(nc), env.rank, env.world)
         wl = workload.R1CSWorkload(nc, npf, num_sections=nws, instances=range(p0, p1))
-        ctx.set_comm(env.rank, env.world, spg.torch_allgather(env.dist, device=env.comm_device))
+        transport = install_comm(env, ctx, comm)
     else:
-        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, seed=0x5350415254414E31 + env.rank)
+        p0 = p1 = None
+        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, seed=0x5350415254414E31 + env.rank,
+                                   instances=range(len(nc)))
     seed = workload.tape_seed()
     gens = spg.R1CSGens(ctx, GENS_LABEL, GENS_NUM_VARS)
     views = workload.CViews(wl)
@@ -417,18 +449,24 @@ def main_r1cs(a):
                                wl.num_inputs, spg.Transcript(b"r1cs_bench"), spg.RandomTape(b"proof", seed))
         return pf
 
-    dt, laps, proofs = timed(env, step, a.steps, a.warmup)
+    dt, laps, proofs = timed(env, step, steps, warmup)
     assert len(proofs) == 1, "proof bytes changed between steps"
-    prof = profile_pass(ctx, step, a.steps)
+    prof = profile_pass(ctx, step, steps)
     t1 = time.perf_counter()  # PCIe-inclusive variant: witness upload + prove (reported beside value)
     wit = upload()
     step()
     t_incl = time.perf_counter() - t1
+    same = None
+    if shard:  # every rank of one sharded proof must hold the same bytes
+        hs = [None] * env.world
+        env.dist.all_gather_object(hs, sorted(proofs))
+        same = all(h == hs[0] for h in hs)
+        ctx.set_comm(0, 1)
     N = wl.total_constraints  # one proof's constraints (the whole sharded proof, or one replica's)
     units = N if shard else N * env.world
-    roof, roof_h, roof_v = rooflines(prof, a.traffic)
-    cpu = bitexact = None
-    if env.rank == 0 and env.world == 1 and not a.no_cpu_baseline:
+    roof, roof_h, roof_v = rooflines(prof, traffic_file)
+    cpu = cpu_all = bitexact = None
+    if env.rank == 0 and env.world == 1 and cpu_on:
         po = oracle()
         tc = time.perf_counter()
         ref, _ = po.r1cs_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS, label=b"r1cs_bench")
@@ -437,24 +475,126 @@ def main_r1cs(a):
                "sample": f"full workload ({N} constraints), one R1CSProof::prove incl. R1CSGens derivation, "
                          f"{tcpu:.2f} s on 1 host thread"}
         bitexact = hashlib.sha256(ref).hexdigest() in proofs
+        ks = 6  # all cores: a 2^6-execution sample of the same shape per core
+        ws = workload.R1CSWorkload(nc, [min(x, 1 << ks) for x in npf], num_sections=nws, instances=range(len(nc)))
+        cpu_all = all_cores_baseline(
+            lambda: po.r1cs_prove(ws, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS, label=b"r1cs_bench"),
+            ws.total_constraints, "constraints/s",
+            f"R1CSProof::prove of {ws.P} instances x 2^{ks} executions x {nc[0]} constraints "
+            f"({ws.total_constraints} constraints) incl. R1CSGens derivation")
+    return {
+        "metric": "R1CS constraints/sec (R1CSProof::prove, data-parallel)", "value": round(units * steps / dt, 1),
+        "unit": "constraints/s", "n_gpus": env.world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 3), "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong" if shard else "weak",
+        "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255",
+        "data": "synthetic (chain-of-squarings R1CS, seeded), random-tape seed fixed",
+        "config": {"workload": "R1CSProof::prove (src/r1csproof.rs:210-685)", "shape": cfg, "num_instances": len(nc),
+                   "num_cons": nc[0], "num_proofs": npf[0], "witness_sections": nws, "constraints": N,
+                   "gens": "R1CSGens(gens_r1cs_sat, 2^24)",
+                   "parallelism": f"instance-sharded single proof x{env.world} ({transport})" if shard
+                   else f"replicas x{env.world}"},
+        "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
+        "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact, "proof_sha256": sorted(proofs)[0][:16],
+        "ranks_agree": same, "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
+        "value_incl_witness_upload": round(units / t_incl, 1), "kernels": kernel_table(prof, steps)}
+
+
+def main_r1cs(a):
+    env = Env(a)
+    import spg
+
+    shard = (a.mode or "replicas") == "shard" and env.world > 1
+    cfg = a.config or ("r1cs_2e22_p8" if shard else "r1cs_2e20")
+    ctx = spg.Context(env.gpu)
+    out = r1cs_core(env, ctx, cfg, shard, a.steps, a.warmup, not a.no_cpu_baseline,
+                    a.traffic or (TRAFFIC["r1cs22"] if cfg == "r1cs_2e22_p8" else None), a.comm)
     if env.rank == 0:
-        print(json.dumps({
-            "metric": "R1CS constraints/sec (R1CSProof::prove, data-parallel)", "value": round(units * a.steps / dt, 1),
-            "unit": "constraints/s", "n_gpus": env.world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if shard else "weak", "vs_baseline": None,
-            "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255",
-            "data": "synthetic (chain-of-squarings R1CS, seeded), random-tape seed fixed",
-            "config": {"workload": "R1CSProof::prove (src/r1csproof.rs:210-685)", "shape": cfg, "num_instances": wl.P,
-                       "num_cons": nc[0], "num_proofs": npf[0], "witness_sections": nws, "constraints": N,
-                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)",
-                       "parallelism": f"instance-sharded single proof x{env.world} ({env.backend})" if shard
-                       else f"replicas x{env.world}"},
-            "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
-            "proof_bitexact_vs_cpu": bitexact, "proof_sha256": sorted(proofs)[0][:16],
-            "device_busy_ms_per_step": round(prof.busy_us / a.steps / 1e3, 3),
-            "value_incl_witness_upload": round(units / t_incl, 1), "kernels": kernel_table(prof, a.steps)}))
+        out["vs_baseline"] = None
+        print(json.dumps(out))
     env.close()
+
+
+# ---------------------------------------------------------------- Hyrax row commit (config 2's row batch)
+def rows_core(env, ctx, steps, warmup, cpu_on, traffic_file=None, log_rows=10, log_width=10):
+    """SURVEY 8d config 2, second shape: DensePolynomial::commit_inner (src/dense_mlpoly.rs:184-212) of a
+    2^20-entry polynomial as 2^10 row MSMs of 2^10 scalars each (the block-witness commit of every config-3 prove),
+    generators MultiCommitGens(1024, spg_bench_rows), scalars resident in HBM. A step is the whole batch ending in
+    the 1024 compressed row commitments on the host."""
+    import numpy as np
+
+    import spg
+    import workload
+
+    L, R = 1 << log_rows, 1 << log_width
+    gens = spg.Gens(ctx, R, b"spg_bench_rows")
+    v, _ = workload.random_fq(L * R, 7)
+    Z = workload.to_mont_limbs([int(x) for x in v])
+    zbuf = spg.Buf(ctx, Z)
+    outs = set()
+
+    def step():
+        r = gens.commit_rows_buf(zbuf, L, R)
+        outs.add(r.tobytes())
+        return r.tobytes()
+
+    dt, laps, _ = timed(env, step, steps, warmup)
+    assert len(outs) == 1, "row commitments changed between steps"
+    prof = profile_pass(ctx, step, steps)
+    roof, roof_h, roof_v = rooflines(prof, traffic_file)
+    dev_us = prof.busy_us / steps
+    madds = sum(v[3] for v in prof.values()) / steps
+    cpu = cpu_all = bitexact = None
+    rows = np.frombuffer(sorted(outs)[0], dtype=np.uint8).reshape(L, 32)
+    if env.rank == 0 and cpu_on:
+        po = oracle()
+        pts = gens.compressed()
+        ref_pts = po.gens_stream(b"spg_bench_rows", R + 1)
+        ls = 64  # 1-thread sample: the first 64 rows (every row is an independent MSM of the same width)
+        tc = time.perf_counter()
+        ref = po.commit_rows(ref_pts[:R], ref_pts[R].tobytes(), Z[: ls * R], ls, R)
+        tcpu = time.perf_counter() - tc
+        bitexact = bool(np.array_equal(pts, ref_pts) and np.array_equal(ref, rows[:ls]))
+        cpu = {"value": round(ls * R / tcpu, 1), "unit": "points/s", "cores": 1, "kind": "port",
+               "sample": f"{ls} of the {L} rows ({ls} x {R} scalars; their bytes are the bit-exactness check) by the "
+                         f"oracle's Pippenger restatement, {tcpu:.2f} s on 1 host thread"}
+        cpu_all = all_cores_baseline(lambda: po.commit_rows(ref_pts[:R], ref_pts[R].tobytes(), Z[: ls * R], ls, R),
+                                     ls * R, "points/s", f"{ls} rows x {R} scalars by the oracle's Pippenger")
+    return {
+        "metric": "Hyrax row-commit points/sec (DensePolynomial::commit_inner, 2^%d rows x 2^%d)" % (log_rows, log_width),
+        "value": round(L * R * steps / dt, 1), "unit": "points/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 3), "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "dtype": "ristretto255 / fq252",
+        "data": "synthetic scalars (splitmix64 seed 7) resident in HBM, generators MultiCommitGens(1024, spg_bench_rows)",
+        "config": {"workload": "row-batch MSM, SURVEY 8d config 2 (1024 row-MSMs x 1024)", "rows": L, "width": R},
+        "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
+        "valu_whole_commit": {"madds_per_commit": madds, "device_us_per_commit": round(dev_us, 1),
+                              "madds_per_s": round(madds / (dev_us * 1e-6), 1) if dev_us else None,
+                              "frac_of_peak": round(madds / (dev_us * 1e-6) / MADD_PEAK, 4) if dev_us else None},
+        "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "rows_bitexact_vs_cpu": bitexact,
+        "rows_sha256": hashlib.sha256(sorted(outs)[0]).hexdigest()[:16], "kernels": kernel_table(prof, steps, top=8),
+    }
+
+
+# ---------------------------------------------------------------- config 1: the CPU path alone
+def cpu1_core(log_cons=10, log_proofs=1):
+    """SURVEY 8d config 1 (benches/snark.rs: synthetic R1CS of 2^12 constraints, CPU reference path only, plumbing):
+    one SNARK::prove of the 2-block x 2^log_proofs x 2^log_cons program by the CPU oracle on 1 host thread, with the
+    per-phase wall times under the labels of the reference's Timer scopes (src/timer.rs, src/lib.rs:1088-2692)."""
+    import workload
+
+    po = oracle()
+    wl = workload.SnarkWorkload(num_blocks=2, log_cons=log_cons, log_proofs=log_proofs, num_vars=1 << log_cons)
+    _, rc = po.snark_prove(wl, workload.tape_seed(), gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS,
+                           label=b"snark_bench")
+    tp = po.snark_last_prove_us() * 1e-6
+    N = wl.total_constraints
+    return {"metric": "R1CS constraints/sec (SNARK::prove), CPU path only", "value": round(N / tp, 1),
+            "unit": "constraints/s", "cores": 1, "kind": "port", "ms_per_prove": round(tp * 1e3, 2),
+            "config": {"workload": "SNARK::prove (src/lib.rs:971-2746), SURVEY 8d config 1", "constraints": N,
+                       "block_types": 2, "executions_per_block": 1 << log_proofs, "constraints_per_block": 1 << log_cons},
+            "oracle_verifier_status": rc,
+            "phases_ms": {k: round(us * 1e-3, 3) for k, us in po.snark_last_phases()}}
 
 
 # ---------------------------------------------------------------- MSM (config 2)
@@ -572,7 +712,7 @@ def main_msm(a):
 
 
 # ---------------------------------------------------------------- SPARK (config 5)
-def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_file=None):
+def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_file=None, comm="auto"):
     """SURVEY 8d config 5: SparseMatPolynomial::multi_evaluate + SparseMatPolyEvalProof::prove over the three
     2^k-nonzero matrices (A, B, C) with num_vars_x = num_vars_y = k. A step is one multi_evaluate at (rx, ry)
     plus one full SPARK evaluation proof (derefs, derefs commit, hash layer, product trees, batched layer
@@ -586,8 +726,7 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
     import workload
 
     shard = env.world > 1 and mode == "shard"
-    if shard:
-        ctx.set_comm(env.rank, env.world, spg.torch_allgather(env.dist, device=env.comm_device))
+    transport = install_comm(env, ctx, comm) if shard else None
     t0 = time.perf_counter()
     wl = workload.SparkWorkload(k)
     views = workload.CViews(wl)
@@ -625,22 +764,19 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         wc = workload.SparkWorkload(kc)
         rc_ = rng.integers(0, 1 << 63, size=(2 * kc, 4), dtype=np.uint64)
         rc_[:, 3] &= np.uint64((1 << 60) - 1)
-        tc = time.perf_counter()
         po.spark_prove(wc, rc_[:kc], rc_[kc:], seed)
-        t_all = time.perf_counter() - tc
         tcpu = po.spark_last_prove_us() * 1e-6
         sample = (f"3 x 2^{kc} nonzeros (same generator), multi_evaluate + SparseMatPolyEvalProof::prove")
         cpu = {"value": round(3 * (1 << kc) / tcpu, 1), "unit": "nonzeros/s", "cores": 1, "kind": "port",
-               "sample": f"{sample}, {tcpu:.2f} s on 1 host thread"}
-        # the concurrent copies also commit and verify (orc_spark_prove does all three): scale the wall time by the
-        # prove's share of one run
-        share = tcpu / t_all
+               "sample": f"{sample}, {tcpu:.2f} s on 1 host thread (the commitment is preprocessing, untimed)"}
+        # all cores: one oracle copy per usable core commits, all meet at a barrier, then all prove at once; the wall
+        # time runs from the first prove's start to the last one's end (verification skipped)
         k_all = usable_cores()
-        dt_all = run_threads(lambda: po.spark_prove(wc, rc_[:kc], rc_[kc:], seed), k_all)
-        cpu_all = {"value": round(3 * (1 << kc) * k_all / (dt_all * share), 1), "unit": "nonzeros/s",
-                   "cores": k_all, "kind": "port",
-                   "sample": f"{k_all} concurrent independent copies of: {sample}; {dt_all:.2f} s wall for commit + "
-                             f"prove + verify, scaled by the prove's {share:.2f} share of one run"}
+        dt_all = po.spark_concurrent_prove(wc, rc_[:kc], rc_[kc:], seed, k_all)
+        cpu_all = {"value": round(3 * (1 << kc) * k_all / dt_all, 1), "unit": "nonzeros/s", "cores": k_all,
+                   "kind": "port",
+                   "sample": f"{k_all} concurrent independent copies of: {sample}, proving together after a barrier; "
+                             f"{dt_all:.2f} s wall from the first prove's start to the last one's end"}
     return {
         "metric": "SPARK nonzeros/sec (sparse_mlpoly multi_evaluate + SparseMatPolyEvalProof::prove)",
         "value": round(value, 1), "unit": "nonzeros/s", "n_gpus": env.world, "steps": steps, "warmup": warmup,
@@ -649,7 +785,7 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         "dtype": "fq252 (8x u32 Montgomery limbs), ristretto255", "data": "synthetic (SURVEY 8d config 5 generator, seed 5)",
         "config": {"workload": "SparseMatPolyEvalProof::prove, batch 3 (src/sparse_mlpoly.rs:1497-1564)",
                    "log_nnz": k, "num_vars_x": k, "num_vars_y": k,
-                   "parallelism": f"one proof sharded x{env.world} ({env.backend})" if shard else f"replicas x{env.world}"},
+                   "parallelism": f"one proof sharded x{env.world} ({transport})" if shard else f"replicas x{env.world}"},
         "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_sha256": sorted(proofs)[0][:16], "ranks_agree": same,
         "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
@@ -664,7 +800,7 @@ def main_spark(a):
 
     ctx = spg.Context(env.gpu)
     out = spark_core(env, ctx, a.log_nnz, a.cpu_log_nnz, a.steps, a.warmup, a.mode or "shard", not a.no_cpu_baseline,
-                     a.traffic or (TRAFFIC["spark24"] if a.log_nnz == 24 else None))
+                     a.traffic or (TRAFFIC["spark24"] if a.log_nnz == 24 else None), a.comm)
     if env.rank == 0:
         out["vs_baseline"] = None
         print(json.dumps(out))

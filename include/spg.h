@@ -60,7 +60,8 @@ int spg_set_comm(spg_ctx* ctx, int rank, int nranks, spg_allgather_fn fn, void* 
  * process per GPU; no caller code runs per exchange. Rank 0 makes the 128-byte id with spg_rccl_unique_id and
  * hands it to every rank by any channel of the caller's (e.g. a torch.distributed broadcast); every rank then calls
  * spg_set_comm_rccl (collective: it returns once all nranks have joined). An exchange that a dead peer never
- * completes fails after 120 s (the communicator is aborted) instead of hanging. */
+ * completes fails after SPG_RCCL_TIMEOUT_S seconds (default 600) instead of hanging; the communicator is then
+ * aborted and stays unusable (every later exchange on it fails): install a new transport to continue. */
 int spg_rccl_unique_id(uint8_t id[128]);
 int spg_set_comm_rccl(spg_ctx* ctx, const uint8_t id[128], int rank, int nranks);
 /* one allgather over the context's transport (callback or RCCL): the `bytes` of rank k land at recv + k*bytes */

@@ -394,6 +394,23 @@ extern "C" {
 static thread_local double g_spark_prove_us = 0.0;
 // wall time of the last orc_spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove (CPU baseline)
 double orc_spark_last_prove_us() { return g_spark_prove_us; }
+// CPU-baseline mode (bench.py config 5, all cores): every orc_spark_prove calls `barrier` between its commitment and
+// its prove, so concurrent copies prove at the same time, and may skip the verification; each thread's prove window
+// (steady clock, microseconds) is kept for the caller to take the concurrent wall time from
+static void (*g_spark_barrier)() = nullptr;
+static bool g_spark_skip_verify = false;
+static thread_local double g_spark_w0 = 0.0, g_spark_w1 = 0.0;
+void orc_spark_baseline_mode(void (*barrier)(), int skip_verify) {
+  g_spark_barrier = barrier;
+  g_spark_skip_verify = skip_verify != 0;
+}
+void orc_spark_last_prove_window(double* t0, double* t1) {
+  *t0 = g_spark_w0;
+  *t1 = g_spark_w1;
+}
+static double steady_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // transcript != NULL: prove on that caller's handle (orc_transcript_new) instead of a fresh Transcript(label) and
 // skip the verification (returns 1)
@@ -427,13 +444,16 @@ int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size
     SparkGens g = SparkGens::create(gens_label, nvx, nvy, gens_nnz, gens_batch);
     MultiSparseDense dense;
     SparkCommitment comm = spark_multi_commit(polys, g, &dense);
+    if (g_spark_barrier) g_spark_barrier();
     auto t0 = std::chrono::steady_clock::now();
+    g_spark_w0 = steady_us();
     FqVec evals = inst.multi_evaluate(vx, vy);
     Transcript tl(label);
     Transcript& t = transcript ? *(Transcript*)transcript : tl;
     RandomTape tape("proof", ld(tape_seed));
     SparkEvalProof pf = spark_prove(dense, vx, vy, evals, g, t, tape);
     g_spark_prove_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    g_spark_w1 = steady_us();
     Ser sc, sp;
     comm.ser(sc);
     pf.ser(sp);
@@ -442,7 +462,7 @@ int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size
     if (sc.b.size() > comm_cap || sp.b.size() > proof_cap) return -1;
     memcpy(comm_out, sc.b.data(), sc.b.size());
     memcpy(proof_out, sp.b.data(), sp.b.size());
-    if (transcript) return 1;
+    if (transcript || g_spark_skip_verify) return 1;
     Transcript tv(label);
     return spark_verify(pf, comm, vx, vy, evals, g, tv) ? 1 : 0;
   } catch (const std::string& e) {
@@ -595,5 +615,15 @@ int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* bloc
   }
 }
 double orc_snark_last_prove_us() { return g_snark_prove_us; }
+// the last snark_prove's phases: up to `max` (name[32], microseconds) pairs, returns their count
+int orc_snark_last_phases(char* names, double* us, int max) {
+  int k = 0;
+  for (auto& l : g_snark_phases.laps) {
+    if (k >= max) break;
+    snprintf(names + 32 * k, 32, "%s", l.first.c_str());
+    us[k++] = l.second;
+  }
+  return k;
+}
 double orc_snark_last_verify_us() { return g_snark_verify_us; }
 }

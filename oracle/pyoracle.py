@@ -331,6 +331,41 @@ def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=No
     return cb[: cl.value].tobytes(), pb[: pl.value].tobytes(), rc == 1
 
 
+def spark_concurrent_prove(wl, rx, ry, tape_seed, k, gens_nnz=None):
+    """k concurrent oracle SPARK proves of the same workload on k threads (the ctypes calls release the GIL): each
+    thread commits, all meet at a barrier, then all prove at once (verification skipped). Returns the wall seconds from
+    the first prove's start to the last one's end."""
+    import threading
+
+    bar = threading.Barrier(k)
+    cb = ctypes.CFUNCTYPE(None)(lambda: bar.wait())
+    f = lib().orc_spark_baseline_mode
+    f(cb, ctypes.c_int(1))
+    wins, errs = [], []
+
+    def body():
+        try:
+            spark_prove(wl, rx, ry, tape_seed, gens_nnz=gens_nnz)
+            t0, t1 = ctypes.c_double(0), ctypes.c_double(0)
+            lib().orc_spark_last_prove_window(ctypes.byref(t0), ctypes.byref(t1))
+            wins.append((t0.value, t1.value))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            bar.abort()
+
+    try:
+        ts = [threading.Thread(target=body) for _ in range(k)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        f(None, ctypes.c_int(0))
+    if errs:
+        raise errs[0]
+    return (max(w[1] for w in wins) - min(w[0] for w in wins)) * 1e-6
+
+
 def spark_last_prove_us():
     """wall time (us) of the last spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove on the host"""
     f = lib().orc_spark_last_prove_us
@@ -366,6 +401,16 @@ def snark_prove_on(wl, tape_seed, transcript, gens_label=b"gens_r1cs_sat", gens_
                                   transcript.h, _p(seed), _p(out), ctypes.c_size_t(cap), ctypes.byref(ln))
     assert rc == 0, rc
     return out[: ln.value].tobytes()
+
+
+def snark_last_phases():
+    """[(phase, microseconds)] of the last snark_prove, under the reference's Timer labels (src/lib.rs:1088-2692)"""
+    f = lib().orc_snark_last_phases
+    f.restype = ctypes.c_int
+    names = ctypes.create_string_buffer(32 * 32)
+    us = (ctypes.c_double * 32)()
+    k = f(names, us, 32)
+    return [(names.raw[32 * i:32 * i + 32].split(b"\0")[0].decode(), us[i]) for i in range(k)]
 
 
 def snark_last_prove_us():

@@ -12,6 +12,7 @@
 // plus a verifier of the pieces that carry the argument's soundness (the three R1CSProofs with their
 // R1CSEvalProofs and the permutation-product identity), replaying SNARK::prove's transcript.
 #pragma once
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -390,12 +391,31 @@ struct SnarkTrace {  // what the verifier side needs besides the proof (for the 
 
 static inline WitnessSec dummy_sec() { return WitnessSec(); }
 
+// per-phase wall time of the last snark_prove, under the labels of the reference's Timer scopes (src/timer.rs;
+// lib.rs:1088-2692: inst_commit, block_sort, witness_gen, input_commit, Block Correctness Extract, Pairwise Check,
+// Perm Root, Perm Product, Shift Proofs, IO Proofs); read by orc_snark_last_phases (bench.py config 1)
+struct PhaseTimer {
+  std::vector<std::pair<std::string, double>> laps;
+  std::chrono::steady_clock::time_point t0;
+  void start() {
+    laps.clear();
+    t0 = std::chrono::steady_clock::now();
+  }
+  void lap(const char* name) {
+    const auto t1 = std::chrono::steady_clock::now();
+    laps.push_back({name, std::chrono::duration<double, std::micro>(t1 - t0).count()});
+    t0 = t1;
+  }
+};
+static PhaseTimer g_snark_phases;
+
 // SNARK::prove (lib.rs:971-2746)
 static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, SnarkInst& pairwise, SnarkInst& perm_root,
                                      const R1CSGens& vars_gens, Transcript& t, RandomTape& tape,
                                      SnarkTrace* tr = nullptr) {
   SnarkIn in = in0;
   SNARKProof pf;
+  g_snark_phases.start();
   t.append_protocol_name("Spartan SNARK proof");
   const bool dbg0 = getenv("SPG_DEBUG_SNARK") != nullptr;
   auto fp = [&](const char* where) {
@@ -442,6 +462,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   t.append_scalars("input_list", in.input);
   t.append_scalar("output_list", in.output);
 
+  g_snark_phases.lap("inst_commit");
   // ---- BLOCK SORT (lib.rs:1155-1198): stable, by decreasing num_proofs
   size_t block_num_instances = 0;
   for (auto n : in.block_num_proofs)
@@ -507,6 +528,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   R1CSInstance pairwise_sorted = pairwise.inst;
   pairwise_sorted.sort(pairwise_num_instances, pw_index);
 
+  g_snark_phases.lap("block_sort");
   // ---- WITNESS GEN: block (lib.rs:1299-1741)
   Fq comb_tau = t.challenge_scalar("challenge_tau");
   Fq comb_r = t.challenge_scalar("challenge_r");
@@ -680,6 +702,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   pf.vir_mem_addr_comm_w3 = vir_addr.c3;
   pf.vir_mem_addr_comm_w3_shifted = vir_addr.c3s;
 
+  g_snark_phases.lap("witness_gen");
   // ---- WITNESS COMMITMENTS (lib.rs:1957-2221)
   std::vector<DensePoly> block_poly_vars;
   for (size_t p = 0; p < block_num_instances; p++) {
@@ -725,6 +748,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
   WitnessSec addr_phy_mems_prover = t_phy > 0 ? WitnessSec::create({in.addr_phy_mems_list}, addr_poly_phy) : dummy_sec();
   WitnessSec addr_vir_mems_prover = t_vir > 0 ? WitnessSec::create({in.addr_vir_mems_list}, addr_poly_vir) : dummy_sec();
 
+  g_snark_phases.lap("input_commit");
   // ---- BLOCK_CORRECTNESS_EXTRACT (lib.rs:2223-2309)
   std::vector<FqVec> block_ch;
   pf.block_r1cs_sat_proof = R1CSProof::prove(
@@ -747,6 +771,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
     }
   }
 
+  g_snark_phases.lap("Block Correctness Extract");
   // ---- PAIRWISE_CHECK (lib.rs:2311-2424)
   size_t pairwise_size = std::max(std::max(consis_num_proofs, t_phy), t_vir);
   std::vector<size_t> inst_map, im2;
@@ -782,6 +807,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
         r1cs_eval_prove(pairwise.dense[0], rx, ry, pf.pairwise_check_inst_evals_list, pairwise.gens, t, tape);
   }
 
+  g_snark_phases.lap("Pairwise Check");
   // ---- PERM_ROOT (lib.rs:2426-2532)
   size_t perm_size = std::max({consis_num_proofs, t_iphy, t_ivir, t_phy, t_vir});
   std::vector<size_t> m1, m2, m3, m4;
@@ -808,6 +834,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
     pf.perm_root_r1cs_eval_proof = r1cs_eval_prove(perm_root.dense[0], rx, ry, e, perm_root.gens, t, tape);
   }
 
+  g_snark_phases.lap("Perm Root");
   // ---- PERM_PRODUCT_PROOF (lib.rs:2534-2609)
   {
     std::vector<const WitnessSec*> comps = {&perm_exec_w3_prover, &init_phy.w3, &init_vir.w3, &phy_addr.w3,
@@ -838,6 +865,7 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
     if (tr) tr->perm_inst_map = im;
   }
 
+  g_snark_phases.lap("Perm Product");
   // ---- SHIFT_PROOFS (lib.rs:2611-2668)
   {
     std::vector<const DensePoly*> orig = {&perm_exec_w3_prover.poly_w[0]}, shifted = {&perm_exec_w3s_prover.poly_w[0]};
@@ -874,11 +902,13 @@ static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, Snark
     pf.shift_proof = shift_proofs_prove(orig, shifted, hl, gpc, t, tape);
   }
 
+  g_snark_phases.lap("Shift Proofs");
   // ---- IO_PROOFS (lib.rs:2670-2693)
   pf.io_proof = io_proofs_prove(exec_inputs_prover.poly_w[0], num_ios, niu, consis_num_proofs, input_block_num,
                                 output_block_num, in.input_liveness, in.input_offset, in.output_offset, in.input,
                                 in.output, in.output_exec_num, gpc, t, tape);
 
+  g_snark_phases.lap("IO Proofs");
   if (tr) {
     auto secs = [](const std::vector<const WitnessSec*>& ws, const std::vector<std::vector<PolyCommitment>>& comm,
                    std::vector<std::vector<size_t>>* ni, std::vector<std::vector<size_t>>* np,

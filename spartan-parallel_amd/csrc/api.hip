@@ -16,7 +16,7 @@
 namespace spg {
 
 int set_err(spg_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
+  if (c) c->err = c->ws_violation.empty() ? msg : c->ws_violation + " (then: " + msg + ")";
   return code;
 }
 
@@ -76,15 +76,33 @@ void* mapped_get(spg_ctx* c, size_t bytes, void** dev) {
 }
 
 void* ws_get(spg_ctx* c, size_t slot, size_t bytes) {
-  if (c->ws.size() <= slot) c->ws.resize(slot + 1);
-  spg_ctx::Slot& s = c->ws[slot];
-  if (s.bytes >= bytes && s.p) return s.p;
+  std::vector<spg_ctx::Slot>& space = c->stream2 && c->stream == c->stream2 ? c->ws2 : c->ws;
+  if (space.size() <= slot) space.resize(slot + 1);
+  spg_ctx::Slot& s = space[slot];
+#ifdef SPG_CHECKED
+  // two streams of one context must never share a slot while the previous owner may still read or write it (the
+  // commit queue's side stream once did: the bench's repeated proves saw different bytes)
+  if (s.p && s.owner && s.owner != c->stream && hipStreamQuery(s.owner) == hipErrorNotReady) {
+    char m[160];
+    snprintf(m, sizeof m, "workspace slot %zu taken by stream %p while stream %p still has work queued on it", slot,
+             (void*)c->stream, (void*)s.owner);
+    fprintf(stderr, "[spg checked] %s\n", m);
+    if (c->ws_violation.empty()) c->ws_violation = m;
+    return nullptr;
+  }
+#endif
+  if (s.p && s.bytes >= bytes) {
+    s.owner = c->stream;
+    return s.p;
+  }
   if (s.p) {
     hipStreamSynchronize(c->stream);
+    if (s.owner && s.owner != c->stream) hipStreamSynchronize(s.owner);
     hipFree(s.p);
     s.p = nullptr;
     s.bytes = 0;
   }
+  s.owner = c->stream;
   size_t want = bytes < 256 ? 256 : bytes;
   want += want / 4;  // headroom so repeated slightly-larger calls do not reallocate
   if (hipMalloc(&s.p, want) != hipSuccess) {
@@ -363,10 +381,12 @@ extern "C" int spg_free(spg_ctx* c) {
   if (!c) return SPG_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->comm_owned_free) c->comm_owned_free(c->comm_owned);
   if (c->wt_cache) spg_r1cs_witness_free(c, c->wt_cache);
-  for (auto& s : c->ws)
-    if (s.p) hipFree(s.p);
+  for (auto* space : {&c->ws, &c->ws2})
+    for (auto& s : *space)
+      if (s.p) hipFree(s.p);
   if (c->pinned) hipHostFree(c->pinned);
   if (c->enc_stage) hipHostFree(c->enc_stage);
   if (c->mapped) hipHostFree(c->mapped);
@@ -409,6 +429,8 @@ int comm_allgather(spg_ctx* c, const Shard& sh, int status, const void* send, si
     return status;
   }
   if (!c->allgather) return set_err(c, SPG_E_ARG, "no communicator set (spg_set_comm)");
+  // a caller transcript that failed on this rank is this rank's failure (TrFailScope)
+  if (!status && c->tr_failed && *c->tr_failed) status = set_err(c, SPG_E_CALLBACK, "transcript callback failed");
   int64_t first = 0;
   if (allgather_with_status(c->allgather, c->comm_user, sh.n, status, send, bytes, recv, &first) != 0)
     return set_err(c, SPG_E_HIP, "allgather failed");

@@ -173,12 +173,16 @@ __global__ void __launch_bounds__(256) k_comb_join(const Ext* __restrict__ part,
 static std::atomic<size_t> g_comb_bytes{0};
 
 void comb_free(const spg_gens* g) {
-  if (!g || !g->comb) return;
-  hipFree(g->comb);
-  g_comb_bytes -= g->comb_bytes;
-  g->comb = nullptr;
-  g->comb_slots = 0;
-  g->comb_bytes = 0;
+  if (!g) return;
+  std::lock_guard<std::mutex> lk(g->comb_mu);
+  g->comb_retired.push_back(g->comb);
+  for (auto& c : g->comb_retired) {
+    if (!c.p) continue;
+    hipFree(c.p);
+    g_comb_bytes -= c.bytes;
+  }
+  g->comb_retired.clear();
+  g->comb = spg_gens::Comb();
 }
 
 static bool comb_enabled() {
@@ -186,21 +190,29 @@ static bool comb_enabled() {
   return on;
 }
 
-// returns 0 when g's comb covers generators [0, need) and h = hgen (hgen < 0: no blinds, any h slot), 1 when the
-// comb path does not apply here (disabled, too wide, over the memory cap, allocation refused), or an SPG error code
-static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen) {
+// returns 0 with *use = a table covering generators [0, need) and h = hgen (hgen < 0: no blinds, any h slot); 1 when
+// the comb path does not apply here (disabled, too wide, over the memory cap, allocation refused, or a table for
+// another h exists: blinded rows on a second h take the bucket path rather than rebuilding gigabytes), or an SPG
+// error code. *use stays valid until the gens is freed.
+static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, spg_gens::Comb* use) {
   if (!comb_enabled() || need > kCombMaxR) return 1;
-  if (g->comb && g->comb_slots >= need && (hgen < 0 || g->comb_h == hgen)) return 0;
-  if (hgen < 0) hgen = (int)g->n;
-  size_t cn = 256;
+  std::lock_guard<std::mutex> lk(g->comb_mu);
+  const spg_gens::Comb cur = g->comb;
+  if (cur.p && hgen >= 0 && cur.h != hgen) return 1;
+  if (cur.p && cur.slots >= need) {
+    *use = cur;
+    return 0;
+  }
+  if (hgen < 0) hgen = cur.p ? cur.h : (int)g->n;
+  // a rebuild only ever grows (never below the table it replaces)
+  size_t cn = std::max<size_t>(256, cur.slots);
   while (cn < need) cn *= 2;
   cn = std::min(cn, g->n);
   if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
   const int NS = (int)cn + 1, C = comb_c();
   const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
   static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 24.0) * (1ull << 30);
-  if (g_comb_bytes.load() - (g->comb ? g->comb_bytes : 0) + bytes > cap) return 1;
-  comb_free(g);
+  if (g_comb_bytes.load() + bytes > cap) return 1;
   Niels* comb = nullptr;
   Fp* zs = nullptr;
   const size_t lanes = entries / kCombRun;
@@ -227,11 +239,10 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen) {
     hipFree(comb);
     return set_err(ctx, SPG_E_HIP, "comb table build");
   }
-  g->comb = comb;
-  g->comb_slots = cn;
-  g->comb_h = hgen;
-  g->comb_bytes = bytes;
+  if (cur.p) g->comb_retired.push_back(cur);
+  g->comb = spg_gens::Comb{comb, cn, bytes, hgen};
   g_comb_bytes += bytes;
+  *use = g->comb;
   return 0;
 }
 
@@ -240,7 +251,8 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen) {
 // runs the bucket pipeline); or an SPG error code
 int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
              const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext) {
-  const int rc = comb_ensure(ctx, g, gen_offset + n, h_index);
+  spg_gens::Comb cb;
+  const int rc = comb_ensure(ctx, g, gen_offset + n, h_index, &cb);
   if (rc == 1) return kCombSkip;
   if (rc) return rc;
   const size_t per = n + (d_blinds ? 1 : 0);
@@ -254,18 +266,18 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
   Ext* part = ext;
   if (S > 1) {
     // the commit queue's second stream runs row commits while the main stream's block-witness commit is in flight:
-    // each stream has its own parts slot
-    part = (Ext*)ws_get(ctx, ctx->stream == ctx->stream2 ? 27 : 25, B * S * sizeof(Ext) + 64);
+    // ws_get gives each stream its own slot space
+    part = (Ext*)ws_get(ctx, 25, B * S * sizeof(Ext) + 64);
     if (!part) return set_err(ctx, SPG_E_NOMEM, "comb parts");
   }
   {
     const int C = comb_c();
     KScope ks(ctx, "msm_comb", 0.0, (double)B * per * (253 / C + 1) * (1.0 - 1.0 / (double)(1 << C)));
     const dim3 ga((unsigned)(B * S)), ta(256);
-    const int NS = (int)g->comb_slots + 1;
+    const int NS = (int)cb.slots + 1;
 #define SPG_COMB_LAUNCH(CC, GG)                                                                                  \
   hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, \
-                     g->comb, NS, (int)S, part)
+                     cb.p, NS, (int)S, part)
     const int key = C * 8 + (int)G;
     switch (key) {
       case 10 * 8 + 1: SPG_COMB_LAUNCH(10, 1); break;

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <initializer_list>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -52,12 +53,20 @@ struct spg_ctx {
   spg_r1cs_witness* wt_cache = nullptr;
   double last_us = 0.0;
   std::string err;
-  // workspace slots: grown on demand, reused across calls (no allocation in steady state)
+  // workspace slots: grown on demand, reused across calls (no allocation in steady state). Each stream has its own
+  // slot space (ws for `stream`, ws2 for `stream2`), so work queued on the two streams at once can never share a
+  // buffer by slot number. `owner` records the stream that took the slot; the checked build (make checked,
+  // -DSPG_CHECKED) refuses a slot that another stream still has work queued on.
   struct Slot {
     void* p = nullptr;
     size_t bytes = 0;
+    hipStream_t owner = nullptr;
   };
-  std::vector<Slot> ws;
+  std::vector<Slot> ws, ws2;
+  std::string ws_violation;  // checked build: the first cross-stream slot conflict (prefixed to the error text)
+  // the transcript of the prove in progress when it forwards to caller callbacks (TrCallbacks::failed): every
+  // cross-rank exchange carries its failure as this rank's status, so all ranks fail together
+  const int* tr_failed = nullptr;
   // optional per-kernel timing (spg_prof_enable): event pairs resolved lazily in spg_prof_read
   bool prof_on = false;
   struct ProfRec {
@@ -85,10 +94,18 @@ struct spg_gens {
   spg::Niels* niels = nullptr;   // n+1 affine Niels points (device)
   spg::Niels* table = nullptr;   // [254][n+1] : table[k][i] = 2^k * P_i (device)
   uint8_t* compressed = nullptr; // (n+1) x 32 host copy
-  // comb.hip: small multiples of the first comb_slots generators and of generator comb_h, built on first use
-  mutable spg::Niels* comb = nullptr;
-  mutable size_t comb_slots = 0, comb_bytes = 0;
-  mutable int comb_h = -1;
+  // comb.hip: a table of small multiples of generators [0, slots) and of generator h, built on first use under
+  // comb_mu (contexts on several threads may share one gens). A published table is never freed while the gens
+  // lives -- a context may still have launches reading it queued: a wider table replaces it for new launches and
+  // the old one waits in comb_retired until spg_gens_free.
+  struct Comb {
+    spg::Niels* p = nullptr;
+    size_t slots = 0, bytes = 0;
+    int h = -1;
+  };
+  mutable std::mutex comb_mu;
+  mutable Comb comb;
+  mutable std::vector<Comb> comb_retired;
 };
 
 namespace spg {

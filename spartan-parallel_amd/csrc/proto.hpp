@@ -205,6 +205,14 @@ inline int tr_status(spg_ctx* ctx, const Tr& t, int rc) {
   if (t.failed()) return set_err(ctx, SPG_E_CALLBACK, "transcript callback returned " + std::to_string(t.failed()));
   return rc;
 }
+// for the duration of a sharded prove: every cross-rank exchange carries this transcript's callback failure as the
+// rank's status (comm_allgather), so a rank whose caller transcript failed stops every rank in that exchange instead
+// of feeding partial sums built from zeroed challenges into it
+struct TrFailScope {
+  spg_ctx* c;
+  TrFailScope(spg_ctx* ctx, const Tr& t) : c(ctx) { c->tr_failed = t.cb ? &t.cb->failed : nullptr; }
+  ~TrFailScope() { c->tr_failed = nullptr; }
+};
 }  // namespace spg
 struct spg_random_tape {
   spg::Tape t;

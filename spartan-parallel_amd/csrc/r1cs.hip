@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include "comm.hpp"
 #include "hostpoly.hpp"
 #include "proto.hpp"
 #include "lds.hpp"
@@ -415,6 +416,14 @@ struct Prover {
   }
   int allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv);
   int sum_ranks(Fq e[3]);
+  // the exchanges of a sharded prove, in order (payload bytes per rank): their sequence depends only on public
+  // sizes, so a rank that fails locally between two of them takes part in the next one with its failure as status
+  // (run()) and every rank returns from that same exchange -- none is left blocked in a later one
+  std::vector<size_t> xplan;
+  size_t xdone = 0;
+  bool xshared = false;  // an exchange already returned a failure to every rank
+  void plan_exchanges(size_t np, size_t nq, size_t nx, size_t nw, size_t ny);
+  int exchange(const void* send, size_t bytes, std::vector<uint8_t>& recv);
   int gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full);
 
   int run();
@@ -425,16 +434,75 @@ int Prover::run() {
   Laps lp;
   int rc0 = run_inner(lp);
   lp.print();
+  if (rc0 && nranks > 1 && !xshared && xdone < xplan.size()) {
+    // this rank failed alone: the next exchange of the plan carries the failure to every rank
+    std::vector<uint8_t> none(xplan[xdone], 0), r;
+    xdone++;
+    comm_allgather(ctx, Shard{(int)rank, (int)nranks}, rc0, none.data(), none.size(), r);
+  }
   return rc0;
 }
 
 // ---- cross-rank exchange (identity when nranks == 1): comm.hpp through api.hip's comm_allgather, so every exchange
 // carries this rank's status and a failure on one rank fails all of them
-int Prover::allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv) {
-  return comm_allgather(ctx, Shard{(int)rank, (int)nranks}, 0, send, bytes, recv);
+int Prover::exchange(const void* send, size_t bytes, std::vector<uint8_t>& recv) {
+  const Shard sh{(int)rank, (int)nranks};
+  if (nranks > 1 && (xdone >= xplan.size() || xplan[xdone] != bytes)) {
+    // the plan is a restatement of run_inner's control flow; a mismatch is a library bug
+    const int rc = set_err(ctx, SPG_E_ARG, "sharded R1CSProof: exchange " + std::to_string(xdone) + " of " +
+                                               std::to_string(bytes) + " bytes is not in the exchange plan");
+    xshared = true;
+    std::vector<uint8_t> r;
+    comm_allgather(ctx, sh, rc, send, bytes, r);
+    return rc;
+  }
+  xdone++;
+  const int rc = comm_allgather(ctx, sh, 0, send, bytes, recv);
+  if (rc) xshared = true;
+  return rc;
 }
+int Prover::allgather(const void* send, size_t bytes, std::vector<uint8_t>& recv) { return exchange(send, bytes, recv); }
 // (e0, e2, e3) summed over the ranks' instance shards
-int Prover::sum_ranks(Fq e[3]) { return comm_sum_fq(ctx, Shard{(int)rank, (int)nranks}, 0, e, 3); }
+int Prover::sum_ranks(Fq e[3]) {
+  if (nranks == 1) return 0;
+  std::vector<uint8_t> r;
+  const int rc = exchange(e, 3 * sizeof(Fq), r);
+  if (rc) return rc;
+  sum_over_ranks(r.data(), (int)nranks, 3, e);
+  return 0;
+}
+// Witness-section polynomials' L.Z widths: Rs = 2^(nv - nv/2) of each (section, instance) polynomial (the bound
+// rows that the LZ allgather carries)
+static size_t lz_width(size_t np, size_t ni) {
+  const size_t nv = lg2(np) + lg2(ni);
+  return (size_t)1 << (nv - nv / 2);
+}
+void Prover::plan_exchanges(size_t np, size_t nq, size_t nx, size_t nw, size_t ny) {
+  xplan.clear();
+  xdone = 0;
+  xshared = false;
+  if (nranks == 1) return;
+  const size_t PL = (P + nranks - 1) / nranks, sum = 3 * sizeof(Fq);
+  // phase 1: one sum per x / q round, the gather of Az, Bz, Cz before the instance rounds
+  const size_t r1 = nx + nq + np;
+  if (r1 && nx + nq == 0) xplan.push_back(PL * 3 * sizeof(Fq));
+  for (size_t j = 0; j < r1; j++) {
+    if (j < nx + nq) xplan.push_back(sum);
+    if (j + 1 == nx + nq && np > 0) xplan.push_back(PL * 3 * sizeof(Fq));
+  }
+  // phase 2: one sum per y / w round, the gather of Z (and ABC unless shared) before the instance rounds
+  const size_t k2 = inst.num_instances == 1 ? 1 : 2, r2 = ny + nw + np;
+  if (r2 && ny + nw == 0) xplan.push_back(PL * k2 * sizeof(Fq));
+  for (size_t j = 0; j < r2; j++) {
+    if (j < ny + nw) xplan.push_back(sum);
+    if (j + 1 == ny + nw && np > 0) xplan.push_back(PL * k2 * sizeof(Fq));
+  }
+  // the L.Z bounds of every witness polynomial
+  size_t lz_total = 0;
+  for (size_t i = 0; i < nws; i++)
+    for (size_t p = 0; p < wit.num_proofs[i].size(); p++) lz_total += lz_width(wit.num_proofs[i][p], wit.num_inputs[i][p]);
+  xplan.push_back(lz_total * sizeof(Fq));
+}
 // per local instance p, the element (p, 0, 0, 0) of each table -> the same for all P instances, on the host
 int Prover::gather_first(const std::vector<const PqxDev*>& tabs, std::vector<std::vector<Fq>>& full) {
   const size_t k = tabs.size(), PL = (P + nranks - 1) / nranks;  // the largest shard; slots per rank
@@ -501,6 +569,7 @@ int Prover::run_inner(Laps& lp) {
   std::vector<size_t> block_num_cons(P);
   for (size_t p = 0; p < P; p++) block_num_cons[p] = inst.num_cons[inst.num_instances == 1 ? 0 : p];
   size_t np = lg2(npow2(P)), nq = lg2(max_np), nx = lg2(num_cons), nw = lg2(nws), ny = lg2(Y);
+  plan_exchanges(np, nq, nx, nw, ny);
   // this rank's instances [p0, p1): everything O(N) lives only here; nranks == 1 -> all of them
   const size_t PLn = p1 - p0;
   std::vector<size_t> l_proofs(num_proofs.begin() + p0, num_proofs.begin() + p1);
@@ -694,6 +763,7 @@ int Prover::run_inner(Laps& lp) {
       int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       Fq e[3];
       rc = eval_wait(ctx, e);
+      if (!rc && j == 1 && failpoint(ctx, "r1cs_round")) rc = set_err(ctx, SPG_E_HIP, "failpoint r1cs_round");
       if (!rc && mode != MODE_P) rc = sum_ranks(e);
       if (rc) return rc;
       lp.lap("p1_eval");
@@ -1483,7 +1553,7 @@ static int r1cs_prove_impl(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg_r1
     // leaving the others blocked in the first round's allgather
     int32_t mine = rc_args;
     std::vector<uint8_t> all;
-    int rc = pr.allgather(&mine, sizeof(mine), all);
+    int rc = comm_allgather(ctx, Shard{(int)pr.rank, (int)pr.nranks}, 0, &mine, sizeof(mine), all);
     if (rc) return rc;
     for (size_t q = 0; q < pr.nranks && !rc_args; q++)
       if (((const int32_t*)all.data())[q]) rc_args = set_err(ctx, SPG_E_ARG, "a peer rank rejected its arguments");
@@ -1522,6 +1592,7 @@ extern "C" int spg_r1cs_prove(spg_ctx* ctx, const spg_r1cs_gens* gens, const spg
   if (!ctx || !gens || !inst || !num_proofs || !num_inputs || !wit || !transcript || !tape || !proof_len)
     return SPG_E_ARG;
   HostPin pin;
+  TrFailScope tfs(ctx, transcript->t);
   return tr_status(ctx, transcript->t,
                    r1cs_prove_impl(ctx, gens, inst, num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs,
                                    wit, transcript, tape, proof, proof_cap, proof_len, challenges_out, ch_lens));

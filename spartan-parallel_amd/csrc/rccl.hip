@@ -6,12 +6,16 @@
 // load it. Every exchange is a few hundred bytes (the status word + 3 scalars of a round, or a W-entry tree level):
 // host staging (page-locked) -> device send buffer -> ncclAllGather -> device receive buffer -> host staging, all
 // on ctx->stream, then one bounded wait that polls ncclCommGetAsyncError, so a dead peer fails the call (the comm is
-// aborted) instead of hanging it.
+// aborted) instead of hanging it. The wait is SPG_RCCL_TIMEOUT_S seconds (default 600: a peer may legitimately
+// spend minutes in a first-use table build before its next exchange). A timed-out or failed communicator is aborted
+// and stays unusable: every later exchange on it fails at once, and the caller installs a new transport.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
+#include <stdlib.h>
 #include <string>
 
 #include "ctx.hpp"
@@ -64,12 +68,26 @@ struct RcclComm {
   bool dead = false;
 };
 
+// true once ctx->stream holds no queued work (bounded: an aborted collective should drain at once)
+bool drain(hipStream_t s, int seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e == hipSuccess;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(seconds)) return false;
+  }
+}
+
 void rccl_free(void* p) {
   RcclComm* c = (RcclComm*)p;
   if (!c) return;
   if (c->comm) (c->dead ? api().abort : api().destroy)(c->comm);
-  if (c->d_buf) hipFree(c->d_buf);
-  if (c->h_buf) hipHostFree(c->h_buf);
+  // the stream may still hold the aborted exchange's copies: the staging buffers outlive them (a dead communicator
+  // whose stream never drains leaks them rather than freeing memory a copy may still touch)
+  if (!c->dead || drain(c->ctx->stream, 10)) {
+    if (c->d_buf) hipFree(c->d_buf);
+    if (c->h_buf) hipHostFree(c->h_buf);
+  }
   delete c;
 }
 
@@ -105,6 +123,7 @@ int rccl_allgather(void* user, const void* send, size_t bytes, void* recv) {
   if ((hipMemcpyAsync)(c->h_buf + c->cap, d_recv, bytes * (size_t)c->nranks, hipMemcpyDeviceToHost, s) != hipSuccess)
     return -1;
   // bounded wait: a peer that died leaves the collective pending forever
+  static const long timeout_s = getenv("SPG_RCCL_TIMEOUT_S") ? std::max(1L, atol(getenv("SPG_RCCL_TIMEOUT_S"))) : 600L;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(s);
@@ -112,10 +131,11 @@ int rccl_allgather(void* user, const void* send, size_t bytes, void* recv) {
     if (e != hipErrorNotReady) return -1;
     ncclResult_t ae = ncclSuccess;
     if (a.async_error(c->comm, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress) ||
-        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(timeout_s)) {
       c->dead = true;
       a.abort(c->comm);
       c->comm = nullptr;
+      drain(s, 10);
       return -1;
     }
   }

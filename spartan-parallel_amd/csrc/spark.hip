@@ -1525,5 +1525,6 @@ extern "C" int spg_spark_prove(spg_ctx* ctx, spg_spark* S, const uint64_t* rx, s
                                spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
   if (!ctx || !transcript) return SPG_E_ARG;
   spg::HostPin pin;
+  spg::TrFailScope tfs(ctx, transcript->t);
   return spg::tr_status(ctx, transcript->t, spg_spark_prove_impl(ctx, S, rx, rx_len, ry, ry_len, evals_in, n_evals, transcript, tape_h, proof, proof_cap, proof_len));
 }

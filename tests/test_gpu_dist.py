@@ -28,10 +28,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, q, bad_shard=False):
+def _worker(rank, world, port, case, q, bad_shard=False, failpoint=None, cb_fail=False):
     import sys
 
-    sys.path[:0] = [os.path.join(ROOT, "spartan-parallel_amd")]
+    if failpoint:  # read by libspg at its first check (tests only): the last rank fails inside a phase-1 round
+        os.environ["SPG_FAILPOINT"] = failpoint
+        os.environ["SPG_FAILPOINT_RANK"] = str(world - 1)
+    sys.path[:0] = [os.path.join(ROOT, "spartan-parallel_amd"), os.path.join(ROOT, "oracle")]
     import torch.distributed as dist
 
     import spg
@@ -53,8 +56,9 @@ def _worker(rank, world, port, case, q, bad_shard=False):
         if bad_shard and rank == world - 1:
             shard = (0, 1)  # this rank uploads a shard that does not hold its instances
         wit = spg.R1CSWitness(ctx, v.secs, wl.nws, shard=shard)
+        tr = _caller_transcript(b"r1cs_test", rank == world - 1) if cb_fail else spg.Transcript(b"r1cs_test")
         pf, ch = spg.r1cs_prove(ctx, gens, inst, wit, wl.P, wl.max_num_proofs, wl.num_proofs, wl.max_num_inputs,
-                                wl.num_inputs, spg.Transcript(b"r1cs_test"), spg.RandomTape(b"proof", workload.tape_seed()))
+                                wl.num_inputs, tr, spg.RandomTape(b"proof", workload.tape_seed()))
         q.put((rank, pf, None))
     except Exception as e:  # noqa: BLE001
         q.put((rank, None, repr(e)))
@@ -62,17 +66,51 @@ def _worker(rank, world, port, case, q, bad_shard=False):
         dist.destroy_process_group()
 
 
-def _run(case, world, bad_shard=False):
+def _caller_transcript(label, refuse):
+    """the caller's own merlin transcript (the oracle's restatement) behind spg_transcript_new_callbacks; with
+    `refuse` its 40th append raises, i.e. the callback fails mid-proof on this rank only"""
+    import pyoracle
+    import spg
+
+    t = pyoracle.OracleTranscript(label)
+    n = [0]
+
+    def app(lbl, msg):
+        n[0] += 1
+        if refuse and n[0] == 40:
+            raise RuntimeError("caller transcript refused")
+        t.append_message(lbl, msg)
+
+    return spg.Transcript.from_callbacks(app, t.challenge_bytes)
+
+
+def _collect(ps, q, world, timeout):
+    """every rank's result, or a failure naming the ranks that never reported (blocked in an exchange)"""
+    import queue
+
+    res = []
+    try:
+        for _ in range(world):
+            res.append(q.get(timeout=timeout))
+    except queue.Empty:
+        pass
+    for p in ps:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.terminate()
+    assert len(res) == world, f"only ranks {sorted(r[0] for r in res)} of {world} returned: a rank is blocked"
+    return sorted(res, key=lambda r: r[0])
+
+
+def _run(case, world, bad_shard=False, failpoint=None, cb_fail=False, timeout=300):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, case, q, bad_shard)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, case, q, bad_shard, failpoint, cb_fail))
+          for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
-    for p in ps:
-        p.join(timeout=60)
-    return res
+    return _collect(ps, q, world, timeout)
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
@@ -92,6 +130,25 @@ def test_sharded_bad_shard_fails_every_rank():
     assert all(pf is None and err for _, pf, err in res), res
 
 
+def test_sharded_r1cs_rank_failure_fails_every_rank():
+    """a failure on one rank inside a phase-1 round of a sharded R1CSProof (test failpoint, before that round's
+    exchange): the failing rank takes part in the next exchange of the plan with its status, so every rank returns an
+    error and none blocks in a later exchange"""
+    res = _run("p4_ragged_3secs", 2, failpoint="r1cs_round", timeout=120)
+    for rank, pf, err in res:
+        assert pf is None and err, f"rank {rank} did not fail: {res}"
+    assert "failpoint" in res[1][2] and "peer rank failed" in res[0][2], res
+
+
+def test_sharded_r1cs_callback_failure_fails_every_rank():
+    """the caller transcript of one rank fails mid-proof: its failure rides the next exchange as that rank's status
+    (TrFailScope), so the healthy rank returns an error too instead of a proof built on zeroed challenges"""
+    res = _run("p4_ragged_3secs", 2, cb_fail=True, timeout=120)
+    for rank, pf, err in res:
+        assert pf is None and err, f"rank {rank} did not fail: {res}"
+    assert "SPG_E_CALLBACK" in res[1][2], res
+
+
 # ---- sharded SPARK (SURVEY 8e: SparseMatPolyEvalProof over W processes; multi_evaluate rows split) ----------
 SPARK_SHARD_CASES = {  # (R1CS shape as in r1cs_cases, world sizes)
     "p2_x64_2secs": [2, 4, 3],
@@ -100,7 +157,7 @@ SPARK_SHARD_CASES = {  # (R1CS shape as in r1cs_cases, world sizes)
 }
 
 
-def _spark_worker(rank, world, port, case, q, failpoint=None):
+def _spark_worker(rank, world, port, case, q, failpoint=None, cb_fail=False, rccl=False):
     import sys
 
     if failpoint:  # read by libspg at its first check (tests only): this rank fails inside a sharded layer
@@ -127,14 +184,19 @@ def _spark_worker(rank, world, port, case, q, failpoint=None):
         nx = (wl.max_num_cons - 1).bit_length()
         ny = (wl.num_vars - 1).bit_length()
         rx, ry = _spark_point(nx, ny)
-        ctx = spg.Context(0)
-        ctx.set_comm(rank, world, spg.torch_allgather(dist))
+        if rccl:  # one GPU per rank, libspg's own transport
+            ctx = spg.Context(rank)
+            ctx.set_comm_rccl(rank, world, dist)
+        else:
+            ctx = spg.Context(0)
+            ctx.set_comm(rank, world, spg.torch_allgather(dist))
         v = workload.CViews(wl)
         gens_nnz = len(wl.entries) * max(max(int(m.shape[0]) for m in mats) for mats in wl.entries)
         comm = spg.SparkCommitment(ctx, v.inst, b"gens_r1cs_eval", gens_nnz, 3)
         inst = spg.R1CSInst(ctx, v.inst)
         evals = spg.r1cs_multi_evaluate(ctx, inst, len(wl.entries), rx, ry)
-        proof = comm.prove(rx, ry, evals, spg.Transcript(b"spark_test"), spg.RandomTape(b"proof", workload.tape_seed()))
+        tr = _caller_transcript(b"spark_test", rank == world - 1) if cb_fail else spg.Transcript(b"spark_test")
+        proof = comm.prove(rx, ry, evals, tr, spg.RandomTape(b"proof", workload.tape_seed()))
         q.put((rank, comm.bytes, np.asarray(evals).tobytes(), proof, None))
     except Exception as e:  # noqa: BLE001
         q.put((rank, None, None, None, repr(e)))
@@ -178,6 +240,21 @@ def test_sharded_spark_matches_oracle(oracle, case, world):
         assert err is None, err
         assert cm == rcomm, f"rank {rank} commitment differs"
         assert pf == ref, f"rank {rank} proof differs"
+
+
+def test_sharded_spark_callback_failure_fails_every_rank():
+    """one rank's caller transcript fails mid-proof of a sharded SPARK proof: every rank returns an error"""
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_spark_worker, args=(r, world, port, "p2_x64_2secs", qq, None, True))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = _collect(ps, qq, world, 120)
+    for rank, _, _, pf, err in res:
+        assert pf is None and err, f"rank {rank} did not fail: {res}"
 
 
 def test_sharded_spark_rank_failure_fails_every_rank():
@@ -274,3 +351,29 @@ def test_rccl_two_gpus_sharded_r1cs(oracle):
     for rank, pf, err in res:
         assert err is None, err
         assert pf == ref, f"rank {rank} proof differs"
+
+
+def test_rccl_two_gpus_sharded_spark(oracle):
+    """a sharded SPARK proof over the RCCL transport, one process per GPU (needs >= 2 GPUs on the box): every rank
+    emits the single-process oracle's commitment and proof"""
+    import torch
+
+    import workload
+    from test_oracle_spark import spark_inputs
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one GPU per rank; this box has one")
+    case = "p2_x64_2secs"
+    wl, rx, ry = spark_inputs(oracle, case)
+    rcomm, ref, ok = oracle.spark_prove(wl, rx, ry, workload.tape_seed())
+    assert ok
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_spark_worker, args=(r, 2, port, case, qq, None, False, True)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = _collect(ps, qq, 2, 300)
+    for rank, cm, _, pf, err in res:
+        assert err is None, err
+        assert cm == rcomm and pf == ref, f"rank {rank} differs"
