@@ -47,6 +47,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (/opt/skills/guides/MI355X_MICROARCH.
 # whole-GPU ext_madd throughput at 8 resident 256-thread blocks per CU (3.00e10/s), measured on MI355X by
 # scripts/micro/ext_throughput.hip (output: profiles/r03_ext_throughput.txt)
 MADD_PEAK = 3.0e10
+# issue-rate ceiling of the same addition: ext_madd compiles to 1,527 VALU instructions per lane-addition (511 of them
+# v_mad_u64_u32; `hipcc -S` of scripts/micro/ext_throughput.hip, k_thr<2> loop body); 1,024 SIMDs issuing one wave64
+# VALU instruction per 2 cycles at 2.4 GHz bound it at 1024 * 2.4e9 / (2 * 1527) * 64 = 5.15e10 madd/s if every
+# instruction were full rate -- an upper bound (64-bit multiply-adds are not), of which MADD_PEAK is 0.58
+MADD_ISSUE_CEILING = 1024 * 2.4e9 / (2 * 1527) * 64
 GENS_LABEL = b"gens_r1cs_sat"
 GENS_NUM_VARS = 1 << 24  # TOTAL_NUM_VARS_BOUND = 10^7 -> 2^24 (examples/interface.rs:557-563)
 CONFIGS = {
@@ -218,12 +223,21 @@ def roofline_valu(prof, traffic_file=None):
     if not cand:
         return None
     dom = max(cand, key=lambda k: cand[k][1])
-    launches, us, _, ops = cand[dom]
+    launches, us, nbytes, ops = cand[dom]
     achieved = ops / (us * 1e-6)
-    return {"bound": "valu", "kernel": dom, "achieved": round(achieved, 1), "peak": MADD_PEAK, "unit": "ext_madd/s",
-            "frac": round(achieved / MADD_PEAK, 5), "traffic": traffic_of(dom, traffic_file),
-            "algorithmic_madds_per_launch": ops / launches, "avg_launch_us": us / launches, "launches": launches,
-            "peak_source": "scripts/micro/ext_throughput.hip, 8 blocks/CU (profiles/r03_ext_throughput.txt)"}
+    traffic = traffic_of(dom, traffic_file)
+    out = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 1), "peak": MADD_PEAK, "unit": "ext_madd/s",
+           "frac": round(achieved / MADD_PEAK, 5), "traffic": traffic,
+           "algorithmic_madds_per_launch": ops / launches, "avg_launch_us": us / launches, "launches": launches,
+           "peak_source": "measured whole-GPU ext_madd throughput, scripts/micro/ext_throughput.hip, 8 blocks/CU "
+                          "(profiles/r03_ext_throughput.txt)",
+           "issue_rate_ceiling": round(MADD_ISSUE_CEILING, 1),
+           "frac_of_issue_ceiling": round(achieved / MADD_ISSUE_CEILING, 5)}
+    if nbytes:  # the kernel's table reads are modelled too: its traffic against them
+        out["algorithmic_bytes_per_launch"] = nbytes / launches
+        if traffic:
+            out["traffic_over_algorithmic"] = round(traffic / (nbytes / launches), 3)
+    return out
 
 
 def rooflines(prof, traffic_file=None):

@@ -337,14 +337,73 @@ int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_comp* pairwis
                     const spg_snark_wit* wit, spg_r1cs_gens* vars_gens, spg_transcript* transcript,
                     spg_random_tape* tape, uint8_t* proof, size_t proof_cap, size_t* proof_len);
 
-/* SNARK::verify (src/lib.rs:2750-3881): replays the transcript from the public inputs (the spg_snark_inputs sizes,
- * input / output / liveness and the init memory lists; block_vars, exec_inputs and the address lists are not
- * read), the three encoded instances (their SPARK commitments) and the proof bytes, and runs every check of the
- * reference verifier. transcript must be a fresh one with the prover's label. Returns 0 when the proof verifies,
- * SPG_E_VERIFY when it does not (malformed bytes included), another negative code on bad arguments. */
+/* SNARK::verify (src/lib.rs:2750-3881) on the prover's own argument block: replays the transcript from the public
+ * inputs (the spg_snark_inputs sizes, input / output / liveness and the init memory lists; block_vars, exec_inputs
+ * and the address lists are not read), the three encoded instances (their SPARK commitments) and the proof bytes,
+ * and runs every check of the reference verifier. transcript: the verifier's transcript in the state the prover's
+ * was in when SNARK::prove began -- a fresh one with the prover's label, or the caller's own `&mut Transcript` behind
+ * spg_transcript_new_callbacks after the same appends. Returns 0 when the proof verifies, SPG_E_VERIFY when it does
+ * not (malformed bytes included), another negative code on bad arguments. */
 int spg_snark_verify(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
                      const spg_snark_comp* perm_root, const spg_snark_inputs* inputs, spg_r1cs_gens* vars_gens,
                      spg_transcript* transcript, const uint8_t* proof, size_t proof_len);
+
+/* ---- the verifier's side of the boundary: what SNARK::verify is given (src/lib.rs:2750-2798), no witness data and
+ * no sparse matrices. The prover exports its commitments once (preprocessing output, as SNARK::encode returns
+ * ComputationCommitment to the caller); the verifier loads them from bytes. */
+/* bincode(Vec<ComputationCommitment>) of an encoded instance (as_list != 0: block_comm_list), or of its single
+ * ComputationCommitment (pairwise_check_comm, perm_root_comm); *len = the size even when it does not fit */
+int spg_snark_comm_bytes(spg_ctx* ctx, const spg_snark_comp* comp, int as_list, uint8_t* out, size_t cap, size_t* len);
+/* block_comm_map: list g (lens[g] entries, concatenated in idx) = the matrix indices 3p + m commitment g covers */
+int spg_snark_comm_map(spg_ctx* ctx, const spg_snark_comp* comp, size_t* idx, size_t idx_cap, size_t* lens,
+                       size_t lens_cap, size_t* n_lists);
+/* A verifier-side instance from commitment bytes (replaces the ComputationCommitment + SNARKGens arguments of
+ * SNARK::verify, src/lib.rs:2781-2797): bytes = as above; map_idx / map_lens / n_map = block_comm_map for a list
+ * (ignored for a single commitment); num_cons = block_num_cons / pairwise_check_num_cons / perm_root_num_cons;
+ * gens_* = the SNARKGens::new(num_cons, num_vars, num_instances, num_nz_entries) arguments. Derives the
+ * gens_r1cs_eval generators; SPG_E_ARG for bytes that do not decode or do not fit them. Free with
+ * spg_snark_comp_free; it serves spg_snark_verify_public only (it cannot prove). */
+int spg_snark_comm_load(spg_ctx* ctx, const uint8_t* bytes, size_t len, int as_list, const size_t* map_idx,
+                        const size_t* map_lens, size_t n_map, size_t num_cons, size_t gens_num_cons,
+                        size_t gens_num_vars, size_t gens_num_instances, size_t gens_num_nz_entries,
+                        spg_snark_comp** out);
+/* SNARK::verify's public arguments, in its order and meaning (src/lib.rs:2750-2798). Scalars are [u8; 32]
+ * canonical little-endian bytes (Scalar::from_bytes; non-canonical bytes are SPG_E_ARG, where the reference's
+ * unwrap panics). input_stack / input_mem are the public input stack and memory: the verifier builds and commits
+ * their init lists itself (src/lib.rs:3274-3333), and a non-empty list's total_num_init_*_mem_accesses must be its
+ * length's next power of two (the reference's assert). */
+typedef struct {
+  size_t input_block_num, output_block_num;
+  const uint8_t* input_liveness; /* [input_len] */
+  size_t input_len;
+  size_t func_input_width, input_offset, output_offset;
+  const uint8_t* input;       /* [input_len][32] */
+  const uint8_t* input_stack; /* [input_stack_len][32] */
+  size_t input_stack_len;
+  const uint8_t* input_mem;   /* [input_mem_len][32] */
+  size_t input_mem_len;
+  const uint8_t* output;      /* [32] */
+  size_t output_exec_num;
+  size_t num_vars, num_ios;
+  size_t max_block_num_phy_ops;
+  const size_t* block_num_phy_ops; /* [block_num_instances_bound] */
+  size_t max_block_num_vir_ops;
+  const size_t* block_num_vir_ops; /* [block_num_instances_bound] */
+  size_t mem_addr_ts_bits_size, num_inputs_unpadded;
+  const size_t* block_num_vars; /* [block_num_instances_bound] */
+  size_t block_num_instances_bound, block_max_num_proofs;
+  const size_t* block_num_proofs; /* [block_num_instances_bound] */
+  size_t block_num_cons;
+  size_t consis_num_proofs, total_num_init_phy_mem_accesses, total_num_init_vir_mem_accesses,
+      total_num_phy_mem_accesses, total_num_vir_mem_accesses;
+  size_t pairwise_check_num_cons, perm_root_num_cons;
+} spg_snark_public;
+/* SNARK::verify from what the reference verifier holds: the loaded commitments, the public arguments, vars_gens and
+ * the caller's transcript (any state: a fresh one with the prover's label, or the caller's own behind
+ * spg_transcript_new_callbacks). Same return codes as spg_snark_verify. */
+int spg_snark_verify_public(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
+                            const spg_snark_comp* perm_root, const spg_snark_public* pub, spg_r1cs_gens* vars_gens,
+                            spg_transcript* transcript, const uint8_t* proof, size_t proof_len);
 
 #ifdef __cplusplus
 }

@@ -578,6 +578,30 @@ int orc_snark_prove_tr(const spg_snark_inputs* in_c, const spg_snark_instance* b
     return -2;
   }
 }
+// SNARK::prove on the caller's prover transcript handle, then SNARK::verify of the same proof on the caller's verifier
+// transcript handle (each in whatever state the caller left it, as `&mut Transcript`): the oracle's verdict on a
+// caller transcript (0 = accepted, >0 = the failing verifier stage, <0 on error)
+int orc_snark_prove_verify_tr(const spg_snark_inputs* in_c, const spg_snark_instance* block_c,
+                              const spg_snark_instance* pairwise_c, const spg_snark_instance* perm_root_c,
+                              const char* gens_label, size_t gens_num_vars, void* prover_tr, void* verifier_tr,
+                              const uint64_t* tape_seed, uint8_t* out, size_t cap, size_t* out_len) {
+  try {
+    SnarkIn in = snark_in_from_c(in_c);
+    SnarkInst block = snark_inst_from_c(block_c, true), pairwise = snark_inst_from_c(pairwise_c, false),
+              perm_root = snark_inst_from_c(perm_root_c, false);
+    R1CSGens vg = R1CSGens::create(gens_label, gens_num_vars);
+    RandomTape tape("proof", ld(tape_seed));
+    SNARKProof pf = snark_prove(in, block, pairwise, perm_root, vg, *(Transcript*)prover_tr, tape);
+    Ser s;
+    pf.ser(s);
+    *out_len = s.b.size();
+    if (s.b.size() > cap) return -1;
+    memcpy(out, s.b.data(), s.b.size());
+    return snark_verify(pf, in, block, pairwise, perm_root, vg, *(Transcript*)verifier_tr);
+  } catch (const std::string& e) {
+    return -2;
+  }
+}
 int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* block_c,
                     const spg_snark_instance* pairwise_c, const spg_snark_instance* perm_root_c, const char* gens_label,
                     size_t gens_num_vars, const char* label, const uint64_t* tape_seed, uint8_t* out, size_t cap,

@@ -403,6 +403,24 @@ def snark_prove_on(wl, tape_seed, transcript, gens_label=b"gens_r1cs_sat", gens_
     return out[: ln.value].tobytes()
 
 
+def snark_prove_verify_on(wl, tape_seed, prover_transcript, verifier_transcript, gens_label=b"gens_r1cs_sat",
+                          gens_num_vars=1 << 24, cap=1 << 24):
+    """SNARK::prove on the caller's prover OracleTranscript, then the oracle's SNARK::verify on the caller's verifier
+    OracleTranscript (both keep their state) -> (bincode(SNARK), verdict: 0 = accepted, >0 = failing stage)"""
+    import workload
+
+    v = workload.SnarkViews(wl)
+    out = np.zeros(cap, dtype=np.uint8)
+    ln = ctypes.c_size_t(0)
+    seed = u64s(tape_seed)
+    rc = lib().orc_snark_prove_verify_tr(ctypes.byref(v.inputs), ctypes.byref(v.block), ctypes.byref(v.pairwise),
+                                         ctypes.byref(v.perm_root), ctypes.c_char_p(gens_label),
+                                         ctypes.c_size_t(gens_num_vars), prover_transcript.h, verifier_transcript.h,
+                                         _p(seed), _p(out), ctypes.c_size_t(cap), ctypes.byref(ln))
+    assert rc >= 0, rc
+    return out[: ln.value].tobytes(), rc
+
+
 def snark_last_phases():
     """[(phase, microseconds)] of the last snark_prove, under the reference's Timer labels (src/lib.rs:1088-2692)"""
     f = lib().orc_snark_last_phases

@@ -143,4 +143,134 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
   }
 }
 
+// ---- one Bullet round from the comb table (the default device form) -------------------------------------
+// The same round as k_bullet_round_q, without buckets. The L and R MSMs are over the ORIGINAL generators G_0..G_{n-1}
+// of the proof, whose generator set keeps the comb table of comb.hip: comb[w][s][m - 1] = m 2^(12 w) G_s. A 12-bit
+// signed digit d of scalar p in window w is then one entry +-comb[w][gidx_p][|d| - 1], and an MSM is a plain sum of
+// its 22 P entries -- no bucket weights, so the host finishes with a plain sum of partial points instead of the
+// buckets' running sums, and no workgroup needs more than its own scalars:
+//   quad (p, j) of MSM b (G quads per scalar) adds the entries of windows j*WG .. j*WG + WG - 1 of scalar p
+//   (WG = ceil(22 / G) dependent quad mixed additions), its Niels coordinates all loaded up front;
+//   the workgroup's BS/4 quad sums meet in an LDS quad tree down to R points, written to parts[b][wg][0..R).
+// The scalar of quad (p, j): its three operand products of the fold (u a[ia], u^-1 a[ia + nk], cw[j] f) are one
+// product on lanes 0..2 of the quad (operands selected per lane), then av = lane0 + lane1, cv = lane2 by DPP and
+// k = av cv: two dependent field products instead of four. The j = 0 quads of workgroup column 0 write the folded
+// state for the next round (every (ia, jw) pair once), as k_bullet_round_q's v = 1 workgroups do.
+struct BulletCombArgs {
+  const Fq* aa_in;
+  const Fq* cw_in;
+  Fq* aa_out;
+  Fq* cw_out;
+  const uint32_t* gidx;  // generator index of weight j (n entries)
+  Fq u, uinv;
+  int k, n, nk;
+  const Niels* comb;
+  int NS;        // comb slots + 1 (the h slot): the stride between windows is NS * 2048 entries
+  int R;         // points each workgroup leaves (a power of two <= BS / 4)
+  Ext* parts;    // [2][gridDim.x][R] (mapped host memory)
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq;
+};
+
+__device__ __forceinline__ Fq fq_qbcast_lane(const Fq& a, int lane) {
+  Fp x;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x.l[i] = a.l[i];
+  Fp r = lane == 0 ? fp_qbcast<0>(x) : (lane == 1 ? fp_qbcast<1>(x) : fp_qbcast<2>(x));
+  Fq o;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.l[i] = r.l[i];
+  return o;
+}
+
+template <int G, int BS>
+__global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
+  constexpr int C = 12, W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  __shared__ uint32_t pts[soa_words<Ext, S>()];
+  __shared__ bool last;
+  const int b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int P = a.n / 2, nk = a.nk, nh = nk / 2;
+  const int gq = blockIdx.x * S + slot;  // quad index within MSM b
+  const int p = gq / G, jg = gq - p * G, w0 = jg * WG;
+  Ext acc = ext_identity();
+  if (p < P) {
+    const int blk = p / nh, off = p - blk * nh;
+    const int ia = b ? off + nh : off;
+    const int j = blk * nk + (b ? 0 : nh) + off;
+    Fq av, cv;
+    if (a.k == 0) {
+      av = a.aa_in[ia];
+      cv = fq_zero();
+      cv.l[0] = 1u;  // cw = 1: the product below takes av out of Montgomery form
+    } else {
+      // lanes 0, 1, 2: u a[ia], u^-1 a[ia + nk], cw[j] f; lane 3 repeats lane 0
+      const Fq x = q == 1 ? a.aa_in[ia + nk] : (q == 2 ? a.cw_in[j] : a.aa_in[ia]);
+      const Fq y = q == 1 ? a.uinv : (q == 2 ? ((j & (2 * nk - 1)) < nk ? a.uinv : a.u) : a.u);
+      const Fq r = fq_mul(x, y);
+      av = fq_add(fq_qbcast_lane(r, 0), fq_qbcast_lane(r, 1));
+      cv = fq_qbcast_lane(r, 2);
+    }
+    if (jg == 0 && q == 0) {  // the folded state, every (ia, j) once over the two MSMs
+      if (blk == 0) a.aa_out[ia] = av;
+      a.cw_out[j] = cv;
+    }
+    const Fq k = fq_mul(av, cv);  // canonical scalar (cw is a plain integer)
+    const int s = (int)a.gidx[j];
+    // signed 12-bit digits; the entries of windows w0 .. w0 + WG - 1 shift into ent[] in window order (static
+    // register indices; a short last group leaves its leading slots empty)
+    uint32_t ent[WG];
+#pragma unroll
+    for (int x = 0; x < WG; x++) ent[x] = 0xffffffffu;
+    int carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int bit = w * C;
+      const int li = bit >> 5, of = bit & 31;
+      uint32_t v = k.l[li] >> of;
+      if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+      int d = (int)(v & MASK) + carry;
+      carry = d > NB ? 1 : 0;
+      d -= carry << C;
+      if (w >= w0 && w < w0 + WG) {
+#pragma unroll
+        for (int x = 0; x + 1 < WG; x++) ent[x] = ent[x + 1];
+        ent[WG - 1] = d == 0 ? 0xffffffffu
+                             : ((uint32_t)((w * a.NS + s) * NB + (d < 0 ? -d : d) - 1) | (d < 0 ? 0x80000000u : 0u));
+      }
+    }
+    // every entry's coordinate in flight before the first addition
+    Fp qv[WG];
+    bool ng[WG];
+#pragma unroll
+    for (int x = 0; x < WG; x++)
+      if (ent[x] != 0xffffffffu) qv[x] = niels_coord(a.comb, ent[x], q, &ng[x]);
+#pragma unroll
+    for (int x = 0; x < WG; x++)
+      if (ent[x] != 0xffffffffu) acc = quad_madd(acc, qv[x], ng[x], q);
+  }
+  for (int d = S / 2; d >= a.R; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put_op<S>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<S>(pts, slot, q), q);
+    __syncthreads();
+  }
+  if (slot < a.R && q == 0) a.parts[((size_t)b * gridDim.x + blockIdx.x) * a.R + slot] = acc;
+  __syncthreads();
+  if (t == 0) {
+    // the parts (mapped host memory) and the folded state (HBM) before the ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.x * gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mbox_post(a.mb, a.seq, nullptr, 0);
+    }
+  }
+}
+
 }  // namespace spg

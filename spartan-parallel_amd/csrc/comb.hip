@@ -35,15 +35,17 @@ static int comb_c() {
   return c;
 }
 static constexpr int kCombRun = 64;                 // multiples per build lane
-static constexpr size_t kCombMaxR = 1024;           // widest row the comb covers
+static constexpr size_t kCombMaxR = 16384;          // widest row the comb covers (70 GB of table at c = 12)
 
 // lane L = ((w * NS + s) * runs + k): multiples k * Run + 1 .. (k + 1) * Run of 2^(c w) G_gen, gen = s (s < NS - 1)
 // or hgen (s = NS - 1)
+// (lanes lane0 .. lane0 + chunk of the whole table per launch: the Z scratch covers one chunk)
 template <int C>
 __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab, int n1, int NS, int hgen,
-                                                   Niels* __restrict__ comb, Fp* __restrict__ zs, size_t lanes) {
+                                                   Niels* __restrict__ comb, Fp* __restrict__ zs, size_t lanes,
+                                                   size_t lane0) {
   constexpr int NB = 1 << (C - 1);
-  const size_t L = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t L = lane0 + (size_t)blockIdx.x * 64 + threadIdx.x;
   if (L >= lanes) return;
   constexpr int runs = NB / kCombRun;
   const int k = (int)(L % runs);
@@ -59,7 +61,7 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
     if ((m0 >> b) & 1u) P = ext_madd(P, bn, false);
   }
   Niels* out = comb + ws * NB + (size_t)k * kCombRun;
-  Fp* z = zs + L * kCombRun;
+  Fp* z = zs + (L - lane0) * kCombRun;
   // forward: X, Y parked in the entry, the prefix product of the Z's in its third field, Z in the scratch
   Fp pp = fp_one();
   for (int j = 0; j < kCombRun; j++) {
@@ -211,27 +213,31 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
   const int NS = (int)cn + 1, C = comb_c();
   const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
-  static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 24.0) * (1ull << 30);
+  static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 96.0) * (1ull << 30);
   if (g_comb_bytes.load() + bytes > cap) return 1;
   Niels* comb = nullptr;
   Fp* zs = nullptr;
   const size_t lanes = entries / kCombRun;
+  // built a window at a time: the Z scratch holds one window's entries (107 MB at 2^14 generators, not 23 GB)
+  const size_t chunk = lanes / (size_t)(253 / C + 1);
   if (hipMalloc(&comb, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return 1;
   }
-  if (hipMalloc(&zs, entries * sizeof(Fp)) != hipSuccess) {
+  if (hipMalloc(&zs, chunk * kCombRun * sizeof(Fp)) != hipSuccess) {
     (void)hipGetLastError();
     hipFree(comb);
     return 1;
   }
-  const dim3 gb((unsigned)((lanes + 63) / 64)), tb(64);
-  if (C == 10)
-    hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes);
-  else if (C == 11)
-    hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes);
-  else
-    hipLaunchKernelGGL(k_comb_build<12>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes);
+  const dim3 gb((unsigned)((chunk + 63) / 64)), tb(64);
+  for (size_t l0 = 0; l0 < lanes; l0 += chunk) {
+    if (C == 10)
+      hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+    else if (C == 11)
+      hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+    else
+      hipLaunchKernelGGL(k_comb_build<12>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+  }
   const hipError_t e = hipGetLastError();
   const hipError_t e2 = hipStreamSynchronize(ctx->stream);
   hipFree(zs);
@@ -244,6 +250,10 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   g_comb_bytes += bytes;
   *use = g->comb;
   return 0;
+}
+
+int comb_get(spg_ctx* ctx, const spg_gens* g, size_t need, spg_gens::Comb* out) {
+  return comb_ensure(ctx, g, need, -1, out);
 }
 
 // B row MSMs of n contiguous generators from gen_offset (+ blinds on h): SPG_OK with the rows' points in ext

@@ -159,6 +159,9 @@ static const int kCombSkip = -1;
 int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
              const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext);
 void comb_free(const spg_gens* g);
+// g's comb table covering generators [0, need) (built on first use): 0 with *out set, 1 when the comb does not
+// apply (disabled, too wide, over the memory cap), or an SPG error code
+int comb_get(spg_ctx* ctx, const spg_gens* g, size_t need, spg_gens::Comb* out);
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext = nullptr);
 
@@ -184,6 +187,13 @@ int bullet_round_device(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const 
                         const uint32_t* gidx, const Fq& u, const Fq& uinv, int k, int n, int nk, Ext* d_buckets,
                         uint32_t* seq_out);
 static const int kBulletNB = 64;  // buckets per MSM of bullet_round_device (c = 7)
+// the comb form of a Bullet round (bullet.hpp k_bullet_comb): partial points of the L and R MSMs, 2 x *per_msm Ext
+// into d_parts (at most kBulletPartsMax per MSM), completion posted to the mailbox with *seq_out; the host adds each
+// MSM's parts. Returns 1 when g has no comb table for these generators (the caller takes the bucket form).
+static const int kBulletPartsMax = 512;
+int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
+                      const uint32_t* gidx, size_t gmax, const Fq& u, const Fq& uinv, int k, int n, int nk,
+                      Ext* d_parts, uint32_t* seq_out, int* per_msm);
 
 // the mailbox page: sequence number (word 0), then up to kMboxScalars scalars from word 8
 static const size_t kMboxBytes = 65536;

@@ -623,6 +623,58 @@ int bullet_round_device(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const 
   return 0;
 }
 
+// the comb form's launch shape by MSM size P = n / 2: G quads per scalar (window groups of ceil(22 / G)), BS threads,
+// R points per workgroup (SPG_BCOMB_G / SPG_BCOMB_BS / SPG_BCOMB_R override, for A/B runs)
+static void bullet_comb_shape(int P, int* G, int* BS, int* R) {
+  static const int eg = getenv("SPG_BCOMB_G") ? atoi(getenv("SPG_BCOMB_G")) : 0;
+  static const int ebs = getenv("SPG_BCOMB_BS") ? atoi(getenv("SPG_BCOMB_BS")) : 0;
+  static const int er = getenv("SPG_BCOMB_R") ? atoi(getenv("SPG_BCOMB_R")) : 0;
+  *G = P >= 512 ? 4 : 8;
+  *BS = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
+  *R = 4;
+  if (eg == 4 || eg == 8 || eg == 11) *G = eg;
+  if (ebs == 64 || ebs == 128 || ebs == 256) *BS = ebs;
+  if (er >= 1 && er <= *BS / 4 && (er & (er - 1)) == 0) *R = er;
+}
+
+int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
+                      const uint32_t* gidx, size_t gmax, const Fq& u, const Fq& uinv, int k, int n, int nk,
+                      Ext* d_parts, uint32_t* seq_out, int* per_msm) {
+  SPG_CHECK(ctx, n >= 2 && (n & (n - 1)) == 0 && nk >= 2 && nk <= n && (n % nk) == 0, "bullet round: bad sizes");
+  static const bool on = !getenv("SPG_BULLET_COMB") || atoi(getenv("SPG_BULLET_COMB")) != 0;
+  if (!on) return 1;
+  spg_gens::Comb cb;
+  const int rc = comb_get(ctx, g, gmax, &cb);
+  if (rc) return rc == 1 ? 1 : rc;
+  int G, BS, R;
+  bullet_comb_shape(n / 2, &G, &BS, &R);
+  const int S = BS / 4, quads = (n / 2) * G, wgs = (quads + S - 1) / S;
+  if (wgs * R > kBulletPartsMax) return 1;
+  BulletCombArgs a{aa_in, cw_in, aa_out, cw_out, gidx, u, uinv, k, n, nk, cb.p, (int)cb.slots + 1, R, d_parts,
+                   ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq};
+  *seq_out = a.seq;
+  *per_msm = wgs * R;
+  const int W = 22, WG = (W + G - 1) / G;
+  (void)WG;
+  // VALU model: one mixed addition per nonzero signed 12-bit digit of the n/2 scalars of each of the two MSMs
+  // algorithmic bytes: every nonzero digit's 96-byte comb entry, the fold's reads and writes (aa: 2 nk in, nk out;
+  // cw: n in, n out; gidx: n)
+  const double entries = (double)n * 22.0 * (1.0 - 1.0 / 4096.0);
+  KScope ks(ctx, "msm_bullet_round", 96.0 * entries + 96.0 * nk + 68.0 * n, entries);
+  const dim3 grid((unsigned)wgs, 2);
+#define SPG_BCOMB(GG, BB) hipLaunchKernelGGL((k_bullet_comb<GG, BB>), grid, dim3(BB), 0, ctx->stream, a)
+  if (G == 4) {
+    if (BS == 64) SPG_BCOMB(4, 64); else if (BS == 128) SPG_BCOMB(4, 128); else SPG_BCOMB(4, 256);
+  } else if (G == 8) {
+    if (BS == 64) SPG_BCOMB(8, 64); else if (BS == 128) SPG_BCOMB(8, 128); else SPG_BCOMB(8, 256);
+  } else {
+    if (BS == 64) SPG_BCOMB(11, 64); else if (BS == 128) SPG_BCOMB(11, 128); else SPG_BCOMB(11, 256);
+  }
+#undef SPG_BCOMB
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
 // the latency-path bucket kernel, quad form unless SPG_SMSM_QUAD=0
 #define SMSM_LAUNCH(BSZ, ...)                                                                   \
   do {                                                                                          \
@@ -879,8 +931,11 @@ static void dispatch_digits_rows(int c, const MsmArgs& a, hipStream_t s) {
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext) {
   hipStream_t s = ctx->stream;
-  // many rows over contiguous generators: the comb tables (comb.hip) replace digit sort, buckets and running sums
-  if (!d_idx && B >= 64 && n <= 1024 && B * (n + (d_blinds ? 1 : 0)) >= ((size_t)1 << 14)) {
+  // the comb tables (comb.hip) replace digit sort, buckets and running sums: batches of >= 64 rows over <= 1024 generators, and the large batches of wider rows
+  // (up to 2^14 generators: the SPARK derefs / comb_ops commits at 2^24 nonzeros), whose bucket path spends as much
+  // time in its digit sort and bucket reduction as in its additions
+  const size_t tot = B * (n + (d_blinds ? 1 : 0));
+  if (!d_idx && B >= 64 && (n <= 1024 ? tot >= ((size_t)1 << 14) : (n <= 16384 && tot >= ((size_t)1 << 22)))) {
     Ext* ext = d_ext ? d_ext : (Ext*)ws_get(ctx, 17, B * sizeof(Ext) + 64);
     if (!ext) return set_err(ctx, SPG_E_NOMEM, "msm comb points");
     const int hi = !d_blinds ? -1 : (h_index < 0 ? (int)g->n : (int)h_index);

@@ -223,6 +223,30 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extr
   });
 }
 
+// B MSMs finished from their partial points (the comb form of a Bullet round): MSM b = the sum of bk[b per ..
+// b per + per) (+ extra[b]), encoded; chunks of each MSM's parts spread over the pool, the last chunk of an MSM to
+// finish adds the chunk sums and encodes
+static void parts_finals(const Ext* bk, size_t B, size_t per, Pt* out, const h::HExt* extra) {
+  const int threads = pool().size() + 1;
+  const int K = (int)std::max<size_t>(1, std::min<size_t>(per / 8, (size_t)threads / std::max<size_t>(B, 1)));
+  std::vector<h::HExt> part(B * K);
+  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[B]);
+  for (size_t b = 0; b < B; b++) left[b].store(K);
+  pool().parallel_for((int)(B * K), [&](int task) {
+    const size_t b = task / K, c = task % K;
+    const size_t lo = per * c / K, hi = per * (c + 1) / K;
+    h::HExt acc = h::hext_from_dev(bk[b * per + lo]);
+    for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(bk[b * per + i]));
+    part[task] = acc;
+    if (left[b].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+      h::HExt sum = part[b * K];
+      for (int k = 1; k < K; k++) sum = h::hext_add(sum, part[b * K + k]);
+      if (extra) sum = h::hext_add(sum, extra[b]);
+      out[b] = compress(sum);
+    }
+  });
+}
+
 // B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
 // h_idx (optional, host, B x n): generator indices uploaded with the scalars in the same copy, d_idx unused
 static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& hs, size_t n, size_t B,
@@ -324,19 +348,33 @@ static void host_fold_dots(FqV& aa, FqV& bb, FqV& cw, size_t n, size_t nn, bool 
 // Round 0 of bullet_rounds_device launched ahead (with the Cx MSM, before the transcript yields r): its L and R
 // MSM scalars are a and the unit weights alone, and the r-dependent G_1 terms are added on the host afterwards.
 // x: the n scalars on the device (copied into the round state); *seq: round 0's mailbox number.
+// One device Bullet round: the comb form (k_bullet_comb; partial points, *per = parts per MSM) when the generator set
+// has a comb table for the proof's generators (gmax = the largest generator index + 1), else the bucket form
+// (k_bullet_round_q; *per = 0: 2 x (64 + 1) bucket sums)
+static int bullet_round_launch(spg_ctx* ctx, ProverGens& g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
+                               const uint32_t* d_idx, size_t gmax, const Fq& u, const Fq& uinv, int k, size_t n,
+                               size_t nk, Ext* d_bk, uint32_t* seq, int* per) {
+  *per = 0;
+  int rc = bullet_round_comb(ctx, g.dev, aa_in, cw_in, aa_out, cw_out, d_idx, gmax, u, uinv, k, (int)n, (int)nk, d_bk,
+                             seq, per);
+  if (rc != 1) return rc;
+  *per = 0;
+  return bullet_round_device(ctx, g.dev, aa_in, cw_in, aa_out, cw_out, d_idx, u, uinv, k, (int)n, (int)nk, d_bk, seq);
+}
+
 static int bullet_round0_launch(spg_ctx* ctx, ProverGens& g, size_t n, const Fq* d_x, const uint32_t* d_idx,
-                                Ext* d_bk, uint32_t* seq) {
+                                size_t gmax, Ext* d_bk, uint32_t* seq, int* per) {
   Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
   if (!st) return set_err(ctx, SPG_E_NOMEM, "bullet state");
   SPG_HIP(ctx, hipMemcpyAsync(st, d_x, n * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
-  return bullet_round_device(ctx, g.dev, st, st + 2 * n, st + n, st + 3 * n, d_idx, fq_zero(), fq_zero(), 0, (int)n,
-                             (int)n, d_bk, seq);
+  return bullet_round_launch(ctx, g, st, st + 2 * n, st + n, st + 3 * n, d_idx, gmax, fq_zero(), fq_zero(), 0, n, n,
+                             d_bk, seq, per);
 }
 
 static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x, const FqV& a, const Fq& r,
-                                const FqV& v1, const FqV& v2, const uint32_t* d_idx, Ext* mbk, Ext* d_bk, FqV* aa,
-                                FqV* bb, FqV* cw, Fq* blind_fin, DotProductProofLogP* out, bool pre0 = false,
-                                uint32_t seq0 = 0) {
+                                const FqV& v1, const FqV& v2, const uint32_t* d_idx, size_t gmax, Ext* mbk, Ext* d_bk,
+                                FqV* aa, FqV* bb, FqV* cw, Fq* blind_fin, DotProductProofLogP* out, bool pre0 = false,
+                                uint32_t seq0 = 0, int per0 = 0) {
   const size_t n = x.size();
   const size_t G1 = g.gens_1.G[0], H = g.gens_n.h;
   Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
@@ -353,9 +391,10 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
   size_t nk = n;
   for (int k = 0; nk != 1; k++) {
     uint32_t seq = seq0;
+    int per = per0;
     int rc = k == 0 && pre0 ? 0
-                            : bullet_round_device(ctx, g.dev, d_aa[k & 1], d_cw[k & 1], d_aa[(k + 1) & 1],
-                                                  d_cw[(k + 1) & 1], d_idx, u, uinv, k, (int)n, (int)nk, d_bk, &seq);
+                            : bullet_round_launch(ctx, g, d_aa[k & 1], d_cw[k & 1], d_aa[(k + 1) & 1], d_cw[(k + 1) & 1],
+                                                  d_idx, gmax, u, uinv, k, n, nk, d_bk, &seq, &per);
     if (rc) return rc;
     g_msm_laps.lap("bullet_launch");
     Fq cL, cR;
@@ -367,7 +406,10 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
     if (rc) return rc;
     g_msm_laps.lap("msm_device");
     Pt LR[2];
-    bucket_finals(mbk, 2, kBulletNB, LR, ex.data(), true);
+    if (per)
+      parts_finals(mbk, 2, (size_t)per, LR, ex.data());
+    else
+      bucket_finals(mbk, 2, kBulletNB, LR, ex.data(), true);
     g_msm_laps.lap("msm_host_final");
     t.point("L", LR[0]);
     t.point("R", LR[1]);
@@ -431,8 +473,12 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
   static const bool ahead = !getenv("SPG_BULLET_AHEAD") || atoi(getenv("SPG_BULLET_AHEAD")) != 0;
   const bool dev_path = dev_rounds && !on_host && n >= 2 && (n & (n - 1)) == 0;
-  // mapped host memory for the bucket sums: [Cx MSM (B = 1, up to 256 buckets)][Bullet rounds (2 x 65)]
-  const size_t cx_bytes = sizeof(Ext) * 256, br_bytes = sizeof(Ext) * 2 * (kBulletNB + 1) + 64;
+  // mapped host memory for the bucket sums: [Cx MSM (B = 1, up to 256 buckets)][Bullet rounds: 2 x 65 buckets, or
+  // 2 x up to kBulletPartsMax partial points of the comb form]
+  const size_t cx_bytes = sizeof(Ext) * 256,
+               br_bytes = sizeof(Ext) * 2 * std::max<size_t>(kBulletNB + 1, kBulletPartsMax) + 64;
+  size_t gmax = 0;  // the comb form needs the table to cover G_0 .. G_{n-1} of this proof
+  for (size_t j = 0; j < n; j++) gmax = std::max(gmax, kn.G[j] + 1);
   void* d_map = nullptr;
   uint8_t* mapped = dev_path ? (uint8_t*)mapped_get(ctx, cx_bytes + br_bytes, &d_map) : nullptr;
   Ext* mbk = mapped ? (Ext*)(mapped + cx_bytes) : nullptr;
@@ -441,6 +487,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   std::vector<Pt> pts;
   bool pre0 = false;
   uint32_t seq0 = 0;
+  int per0 = 0;
   if (mbk && ahead) {
     // the Cx bucket sums, then Bullet round 0 (which needs no challenge), on the stream before the host waits
     // for Cx: one device round trip fewer per proof
@@ -456,7 +503,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     int rc = msm_small_buckets(ctx, g.dev, 0, d_s, n2, 1, nullptr, d_idx, -1, (Ext*)d_map, &NB);
     if (rc) return rc;
     SPG_HIP(ctx, hipEventRecord(ctx->ev_cx, ctx->stream));
-    rc = bullet_round0_launch(ctx, g, n, d_s, d_idx, d_mbk, &seq0);
+    rc = bullet_round0_launch(ctx, g, n, d_s, d_idx, gmax, d_mbk, &seq0, &per0);
     if (rc) return rc;
     pre0 = true;
     SPG_HIP(ctx, hipEventSynchronize(ctx->ev_cx));
@@ -497,8 +544,8 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   size_t nk = n, k = 0;
   g_msm_laps.lap("bullet_prep");
   if (mbk) {
-    int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, mbk, d_mbk, &aa, &bb, &cw, &blind_fin, out, pre0,
-                                  seq0);
+    int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, gmax, mbk, d_mbk, &aa, &bb, &cw, &blind_fin, out,
+                                  pre0, seq0, per0);
     if (rc) return rc;
     nk = 1;
   }

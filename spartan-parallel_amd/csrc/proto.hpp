@@ -179,6 +179,12 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
                        const uint8_t* label, size_t label_len, size_t gens_nvx, size_t gens_nvy, size_t gens_nnz,
                        size_t gens_batch, spg_spark** out, const Shard& sh = Shard());
 void spark_comm_ser(const spg_spark* S, Writer& w);
+// a verifier-side SPARK commitment: the SparseMatPolyCommitment fields (sparse_mlpoly.rs:319-325, read from bytes) with
+// the generators SparseMatPolyCommitmentGens::new(label, gens_nvx, gens_nvy, gens_nnz, gens_batch) derives, and no
+// dense representation (spg_snark_comm_load); SPG_E_ARG when the fields do not fit those generators
+int spark_from_comm(spg_ctx* ctx, size_t B, size_t N, size_t cells, const std::vector<Pt>& comm_ops,
+                    const std::vector<Pt>& comm_mem, const uint8_t* label, size_t label_len, size_t gens_nvx,
+                    size_t gens_nvy, size_t gens_nnz, size_t gens_batch, spg_spark** out);
 void spark_comm_append(const spg_spark* S, Tr& t);
 // sh.n > 1: one proof as an SPMD collective over the ranks of sh (every rank holds the whole dense representation
 // and returns the same bytes); see spark.hip "sharded proof"
@@ -243,4 +249,7 @@ struct SnarkCompView {
   const std::vector<spg_spark*>* sparks;
 };
 int snark_comp_view(const spg_snark_comp* C, SnarkCompView* v);
+// a verifier-side encoded instance (spg_snark_comm_load): no sparse matrices, no device instance
+spg_snark_comp* snark_comp_from_parts(size_t num_instances, size_t max_num_cons, size_t num_vars,
+                                      std::vector<std::vector<size_t>> label_map, std::vector<spg_spark*> sparks);
 }  // namespace spg

@@ -626,8 +626,53 @@ extern "C" int spg_snark_encode(spg_ctx* ctx, const spg_snark_instance* si, int 
 }
 extern "C" int spg_snark_comp_free(spg_ctx* ctx, spg_snark_comp* C) { return snark_comp_free(ctx, C); }
 
+// bincode(Vec<ComputationCommitment>) (as_list) or bincode(ComputationCommitment) of an encoded instance:
+// R1CSCommitment { num_cons: num_instances * max_num_cons, num_vars, comm } (src/r1csinstance.rs:60-64, 700-705)
+extern "C" int spg_snark_comm_bytes(spg_ctx* ctx, const spg_snark_comp* C, int as_list, uint8_t* out, size_t cap,
+                                    size_t* len) {
+  if (!ctx || !C || !len || C->sparks.empty()) return SPG_E_ARG;
+  if (!as_list && C->sparks.size() != 1) return set_err(ctx, SPG_E_ARG, "several commitments: ask for the list");
+  Writer w;
+  if (as_list) w.u64(C->sparks.size());
+  for (const spg_spark* S : C->sparks) {
+    w.u64(C->num_instances * C->max_num_cons);
+    w.u64(C->num_vars);
+    spark_comm_ser(S, w);
+  }
+  *len = w.out.size();
+  if (!out || w.out.size() > cap) return set_err(ctx, SPG_E_ARG, "commitment buffer too small");
+  memcpy(out, w.out.data(), w.out.size());
+  return SPG_OK;
+}
+
+// block_comm_map (src/lib.rs:2781): list g holds the matrix indices 3p + m that commitment g covers
+extern "C" int spg_snark_comm_map(spg_ctx* ctx, const spg_snark_comp* C, size_t* idx, size_t idx_cap, size_t* lens,
+                                  size_t lens_cap, size_t* n_lists) {
+  if (!ctx || !C || !n_lists) return SPG_E_ARG;
+  *n_lists = C->label_map.size();
+  size_t tot = 0;
+  for (auto& l : C->label_map) tot += l.size();
+  if (!idx || !lens || tot > idx_cap || C->label_map.size() > lens_cap) return set_err(ctx, SPG_E_ARG, "map buffer too small");
+  size_t o = 0;
+  for (size_t g = 0; g < C->label_map.size(); g++) {
+    lens[g] = C->label_map[g].size();
+    for (size_t k : C->label_map[g]) idx[o++] = k;
+  }
+  return SPG_OK;
+}
+
 namespace spg {
 // what SNARK::verify reads of an encoded instance (verify.hip)
+spg_snark_comp* snark_comp_from_parts(size_t num_instances, size_t max_num_cons, size_t num_vars,
+                                      std::vector<std::vector<size_t>> label_map, std::vector<spg_spark*> sparks) {
+  spg_snark_comp* C = new spg_snark_comp();
+  C->num_instances = num_instances;
+  C->max_num_cons = max_num_cons;
+  C->num_vars = num_vars;
+  C->label_map = std::move(label_map);
+  C->sparks = std::move(sparks);
+  return C;
+}
 int snark_comp_view(const spg_snark_comp* C, SnarkCompView* v) {
   if (!C || C->sparks.empty() || C->label_map.size() != C->sparks.size()) return SPG_E_ARG;
   v->num_instances = C->num_instances;

@@ -1190,6 +1190,42 @@ int spark_commit_polys(spg_ctx* ctx, const std::vector<SparsePoly>& polys, size_
   return SPG_OK;
 }
 
+int spark_from_comm(spg_ctx* ctx, size_t B, size_t N, size_t cells, const std::vector<Pt>& comm_ops,
+                    const std::vector<Pt>& comm_mem, const uint8_t* label, size_t label_len, size_t gens_nvx,
+                    size_t gens_nvy, size_t gens_nnz, size_t gens_batch, spg_spark** out) {
+  const size_t nv_ops = lg2(npow2(gens_nnz)) + lg2(npow2(gens_batch * 5));
+  const size_t nv_mem = std::max(gens_nvx, gens_nvy) + 1;
+  const size_t nv_der = lg2(npow2(gens_nnz)) + lg2(npow2(gens_batch * 2));
+  // the shapes multi_commit gives: N a power of two >= 2, cells a power of two, and one Hyrax row commitment per row
+  // of comb_ops (npow2(5 B N) entries) and comb_mem (2 cells entries)
+  if (!B || N < 2 || !is_pow2(N) || !cells || !is_pow2(cells) || B > (1u << 20) || N > (1ull << 32) ||
+      cells > (1ull << 32) || lg2(npow2(5 * B * N)) > nv_ops || lg2(npow2(2 * B * N)) > nv_der || lg2(2 * cells) > nv_mem)
+    return set_err(ctx, SPG_E_ARG, "SPARK commitment sizes do not fit the generators");
+  const size_t ops_nv = lg2(npow2(5 * B * N)), mem_nv = lg2(2 * cells);
+  if (comm_ops.size() != ((size_t)1 << (ops_nv / 2)) || comm_mem.size() != ((size_t)1 << (mem_nv / 2)))
+    return set_err(ctx, SPG_E_ARG, "SPARK commitment row counts do not match its sizes");
+  spg_spark* S = new spg_spark();
+  S->B = B;
+  S->N = N;
+  S->cells = cells;
+  S->comb_ops_len = npow2(5 * B * N);
+  S->comb_mem_len = 2 * cells;
+  size_t nmax = 0;
+  for (size_t nv : {nv_ops, nv_mem, nv_der}) nmax = std::max(nmax, (size_t)1 << (nv - nv / 2));
+  const int rc = spg_gens_derive(ctx, label, label_len, nmax + 1, &S->dev);
+  if (rc) {
+    delete S;
+    return rc;
+  }
+  S->g_ops = gens_view(S->dev, nv_ops);
+  S->g_mem = gens_view(S->dev, nv_mem);
+  S->g_der = gens_view(S->dev, nv_der);
+  S->comm_ops = comm_ops;
+  S->comm_mem = comm_mem;
+  *out = S;
+  return SPG_OK;
+}
+
 // bincode(SparseMatPolyCommitment) (sparse_mlpoly.rs:319-325)
 void spark_comm_ser(const spg_spark* S, Writer& w) {
   w.u64(S->B);

@@ -1023,9 +1023,18 @@ PolyComm commit_vec(spg_ctx* ctx, ProverGens& g, FqV Z) {
 
 const size_t INIT_PHY_MEM_WIDTH = 4, INIT_VIR_MEM_WIDTH = 4, PHY_MEM_WIDTH = 4, VIR_MEM_WIDTH = 8;
 
+// the public values SNARK::verify converts from bytes (src/lib.rs:2836-2850): input, output, and the input stack /
+// input memory whose init lists the verifier commits itself (:3274-3333); n = the list's length (unpadded)
+struct SnarkPub {
+  FqV input;
+  Fq output;
+  FqV stack, mem;
+};
+
 // SNARK::verify (src/lib.rs:2750-3881)
-bool snark_verify(SnarkVerifier& v, const SnarkV& pf, const spg_snark_inputs& in, const SnarkCompView& block,
-                  const SnarkCompView& pairwise, const SnarkCompView& perm_root, ProverGens& gpc) {
+bool snark_verify(SnarkVerifier& v, const SnarkV& pf, const spg_snark_inputs& in, const SnarkPub& pub,
+                  const SnarkCompView& block, const SnarkCompView& pairwise, const SnarkCompView& perm_root,
+                  ProverGens& gpc) {
   Tr& t = v.t;
   const size_t niu = in.num_inputs_unpadded, num_ios = in.num_ios, Bb = in.block_num_instances_bound;
   std::vector<size_t> bnv_all(in.block_num_vars, in.block_num_vars + Bb), bnp_all(in.block_num_proofs, in.block_num_proofs + Bb);
@@ -1060,9 +1069,8 @@ bool snark_verify(SnarkVerifier& v, const SnarkV& pf, const spg_snark_inputs& in
   for (size_t gi = 0; gi < block.sparks->size(); gi++) comm_append(block, gi);
   comm_append(pairwise, 0);
   comm_append(perm_root, 0);
-  FqV input;
-  for (size_t i = 0; i < in.input_len; i++) input.push_back(ld_fq(in.input + 4 * i));
-  const Fq output = ld_fq(in.output);
+  const FqV& input = pub.input;
+  const Fq output = pub.output;
   app("input_block_num", in.input_block_num);
   app("output_block_num", in.output_block_num);
   t.scalars("input_list", input);
@@ -1127,24 +1135,24 @@ bool snark_verify(SnarkVerifier& v, const SnarkV& pf, const spg_snark_inputs& in
   }
   for (auto& c : pf.block_comm_vars_list) append_polycomm(t, "poly_commitment", c);
   append_polycomm(t, "poly_commitment", pf.exec_comm_inputs[0]);
-  // the verifier commits the init lists itself from the public input stack / memory (lib.rs:3274-3333)
-  auto init_vsec = [&](size_t total, size_t n, const uint64_t* lst, size_t width) {
+  // the verifier commits the init lists itself from the public input stack / memory (lib.rs:3274-3333): rows
+  // (1, 0, i, value_i) for the list, zero rows up to the padded total
+  auto init_vsec = [&](size_t total, const FqV& vals, size_t width) {
     VSec s;
-    if (n == 0) return s;
+    if (vals.empty()) return s;
     FqV flat(total * width, fq_zero());
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0; i < vals.size(); i++) {
       flat[i * width] = fq_one();
       flat[i * width + 2] = fq_from_u64(i);
-      flat[i * width + 3] = ld_fq(lst + 4 * (i * INIT_PHY_MEM_WIDTH + 3));
+      flat[i * width + 3] = vals[i];
     }
     const PolyComm c = commit_vec(v.ctx, gpc, flat);
     append_polycomm(t, "poly_commitment", c);
     return vsec({width}, {total}, {c});
   };
-  if (in.total_num_init_phy_mem_accesses && !in.init_phy_mems) return v.fail("init_phy_mems missing");
-  if (in.total_num_init_vir_mem_accesses && !in.init_vir_mems) return v.fail("init_vir_mems missing");
-  const VSec init_phy_v = init_vsec(t_iphy, in.total_num_init_phy_mem_accesses, in.init_phy_mems, INIT_PHY_MEM_WIDTH);
-  const VSec init_vir_v = init_vsec(t_ivir, in.total_num_init_vir_mem_accesses, in.init_vir_mems, INIT_VIR_MEM_WIDTH);
+  if (pub.stack.size() > t_iphy || pub.mem.size() > t_ivir) return v.fail("init memory lists longer than their totals");
+  const VSec init_phy_v = init_vsec(t_iphy, pub.stack, INIT_PHY_MEM_WIDTH);
+  const VSec init_vir_v = init_vsec(t_ivir, pub.mem, INIT_VIR_MEM_WIDTH);
   VSec addr_phy_v, addr_phy_sv, addr_vir_v, addr_vir_sv, ts_bits_v;
   if (t_phy > 0) {
     append_polycomm(t, "poly_commitment", pf.addr_comm_phy_mems);
@@ -1379,10 +1387,20 @@ static int spg_snark_verify_impl(spg_ctx* ctx, const spg_snark_comp* block, cons
   SnarkV pf;
   Rd r(proof, proof_len);
   if (!rd_snark(r, pf)) return set_err(ctx, SPG_E_VERIFY, "snark verify: malformed proof bytes");
+  // the public values of this entry point: Montgomery limbs, and the init lists as full rows (column 3 = the value)
+  SnarkPub pub;
+  for (size_t i = 0; i < in.input_len; i++) pub.input.push_back(ld_fq(in.input + 4 * i));
+  pub.output = ld_fq(in.output);
+  if ((in.total_num_init_phy_mem_accesses && !in.init_phy_mems) || (in.total_num_init_vir_mem_accesses && !in.init_vir_mems))
+    return set_err(ctx, SPG_E_ARG, "snark verify: init memory lists missing");
+  for (size_t i = 0; i < in.total_num_init_phy_mem_accesses; i++)
+    pub.stack.push_back(ld_fq(in.init_phy_mems + 4 * (i * INIT_PHY_MEM_WIDTH + 3)));
+  for (size_t i = 0; i < in.total_num_init_vir_mem_accesses; i++)
+    pub.mem.push_back(ld_fq(in.init_vir_mems + 4 * (i * INIT_VIR_MEM_WIDTH + 3)));
   SnarkVerifier v(ctx, transcript->t);
   bool ok = false;
   try {
-    ok = snark_verify(v, pf, in, vb, vp, vr, vars_gens->g);
+    ok = snark_verify(v, pf, in, pub, vb, vp, vr, vars_gens->g);
   } catch (const Fail& f) {
     v.fail(f.what);
   }
@@ -1523,4 +1541,192 @@ extern "C" int spg_r1cs_verify(spg_ctx* ctx, const spg_r1cs_gens* gens, size_t n
   if (!ctx || !transcript) return SPG_E_ARG;
   spg::HostPin pin;
   return spg::tr_status(ctx, transcript->t, spg_r1cs_verify_impl(ctx, gens, num_instances, max_num_proofs, num_proofs, max_num_inputs, secs, nws, num_cons, evals, transcript, proof, proof_len, challenges_out, ch_lens));
+}
+
+// ------------------------------------------------------------------------------------ verifier from bytes
+// SNARK::verify's commitment arguments (src/lib.rs:2781-2797: block_comm_map + block_comm_list + block_gens,
+// pairwise_check_comm + pairwise_check_gens, perm_root_comm + perm_root_gens) as the verifier holds them: the
+// bincode bytes of the ComputationCommitment(s) and the SNARKGens::new arguments, no sparse matrices.
+extern "C" int spg_snark_comm_load(spg_ctx* ctx, const uint8_t* bytes, size_t len, int as_list, const size_t* map_idx,
+                                   const size_t* map_lens, size_t n_map, size_t num_cons, size_t gens_num_cons,
+                                   size_t gens_num_vars, size_t gens_num_instances, size_t gens_num_nz_entries,
+                                   spg_snark_comp** out) {
+  if (!ctx || !bytes || !out || !num_cons || !gens_num_cons || !gens_num_vars || !gens_num_instances ||
+      !gens_num_nz_entries)
+    return SPG_E_ARG;
+  SPG_HIP(ctx, hipSetDevice(ctx->device));
+  Rd r(bytes, len);
+  const size_t n = as_list ? r.len(56) : 1;
+  if (r.bad || n == 0) return set_err(ctx, SPG_E_ARG, "comm load: malformed commitment list");
+  // SNARKGens::new -> R1CSCommitmentGens::new("gens_r1cs_eval", num_instances, num_cons, num_vars, num_nz_entries)
+  // (src/lib.rs:164-185, src/r1csinstance.rs:39-56), as spg_snark_encode derives it
+  const size_t Pg = npow2(gens_num_instances);
+  const size_t gens_nvx = lg2(Pg) + lg2(npow2(gens_num_cons)), gens_nvy = lg2(npow2(gens_num_vars));
+  const size_t gens_nnz = Pg * gens_num_nz_entries;
+  static const char kLabel[] = "gens_r1cs_eval";
+  std::vector<spg_spark*> sparks;
+  size_t comm_cons = 0, comm_vars = 0;
+  auto fail = [&](const char* why) {
+    for (auto* S : sparks) spg_spark_free(ctx, S);
+    return set_err(ctx, SPG_E_ARG, std::string("comm load: ") + why);
+  };
+  for (size_t g = 0; g < n; g++) {
+    const size_t nc = (size_t)r.u64(), nv = (size_t)r.u64();  // R1CSCommitment { num_cons, num_vars, comm }
+    const size_t B = (size_t)r.u64(), N = (size_t)r.u64(), cells = (size_t)r.u64();
+    std::vector<Pt> ops = r.pts(), mem = r.pts();
+    if (r.bad) return fail("malformed commitment bytes");
+    if (g && (nc != comm_cons || nv != comm_vars)) return fail("commitments of one list disagree on num_cons / num_vars");
+    comm_cons = nc;
+    comm_vars = nv;
+    spg_spark* S = nullptr;
+    const int rc = spark_from_comm(ctx, B, N, cells, ops, mem, (const uint8_t*)kLabel, sizeof(kLabel) - 1, gens_nvx,
+                                   gens_nvy, gens_nnz, 3, &S);
+    if (rc) {
+      for (auto* S2 : sparks) spg_spark_free(ctx, S2);
+      return rc;
+    }
+    sparks.push_back(S);
+  }
+  if (r.o != r.n) return fail("trailing bytes");
+  if (!is_pow2(num_cons) || comm_cons % num_cons || !is_pow2(comm_vars)) return fail("num_cons does not divide the commitment's");
+  const size_t P = comm_cons / num_cons;
+  // the matrix map: block_comm_map for a list, every matrix of the instance for a single commitment
+  std::vector<std::vector<size_t>> label_map;
+  if (as_list) {
+    if (!map_idx || !map_lens || n_map != n) return fail("one map list per commitment");
+    size_t o = 0;
+    std::vector<int> seen(3 * P, 0);
+    for (size_t g = 0; g < n; g++) {
+      if (map_lens[g] != sparks[g]->B) return fail("map list length differs from the commitment's batch size");
+      label_map.push_back(std::vector<size_t>(map_idx + o, map_idx + o + map_lens[g]));
+      for (size_t k : label_map.back())
+        if (k >= 3 * P || seen[k]++) return fail("map index out of range or repeated");
+      o += map_lens[g];
+    }
+  } else {
+    if (sparks[0]->B != 3 * P) return fail("a single commitment covers the 3 matrices of every instance");
+    label_map.push_back({});
+    for (size_t k = 0; k < 3 * P; k++) label_map[0].push_back(k);
+  }
+  for (auto* S : sparks)
+    if (S->cells != ((size_t)1 << std::max<size_t>(std::max(lg2(num_cons), lg2(comm_vars)), 1)))
+      return fail("SPARK memory size differs from num_cons / num_vars");
+  *out = snark_comp_from_parts(P, num_cons, comm_vars, std::move(label_map), std::move(sparks));
+  return SPG_OK;
+}
+
+namespace {
+bool scalar_from_bytes(const uint8_t* b, Fq* out) {  // Scalar::from_bytes: canonical little-endian, else None
+  uint64_t w[4];
+  for (int i = 0; i < 4; i++) {
+    w[i] = 0;
+    for (int k = 0; k < 8; k++) w[i] |= (uint64_t)b[8 * i + k] << (8 * k);
+  }
+  Fq a;
+  for (int i = 0; i < 8; i++) a.l[i] = (uint32_t)(w[i / 2] >> (32 * (i % 2)));
+  const uint32_t Q[8] = {SPG_Q0, SPG_Q1, SPG_Q2, SPG_Q3, 0u, 0u, 0u, SPG_Q7};
+  uint32_t br = 0;
+  for (int i = 0; i < 8; i++) subb(a.l[i], Q[i], br, br);
+  if (!br) return false;  // a >= q
+  *out = fq_to_mont(a);
+  return true;
+}
+}  // namespace
+
+static int spg_snark_verify_public_impl(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
+                                        const spg_snark_comp* perm_root, const spg_snark_public* pb,
+                                        spg_r1cs_gens* vars_gens, spg_transcript* transcript, const uint8_t* proof,
+                                        size_t proof_len) {
+  if (!ctx || !block || !pairwise || !perm_root || !pb || !vars_gens || !transcript || (!proof && proof_len))
+    return SPG_E_ARG;
+  const spg_snark_public& a = *pb;
+  if (!a.block_num_instances_bound || !a.num_inputs_unpadded || !a.num_ios || !a.block_num_vars || !a.block_num_proofs ||
+      !a.block_num_phy_ops || !a.block_num_vir_ops || (a.input_len && (!a.input || !a.input_liveness)) || !a.output ||
+      (a.input_stack_len && !a.input_stack) || (a.input_mem_len && !a.input_mem))
+    return set_err(ctx, SPG_E_ARG, "snark verify: public inputs incomplete");
+  if (!a.consis_num_proofs) return set_err(ctx, SPG_E_ARG, "snark verify: consis_num_proofs must be positive");
+  // the reference's assertions (src/lib.rs:3276-3281, 3305-3310): an init list's total is its padded length
+  if (a.input_stack_len ? a.total_num_init_phy_mem_accesses != npow2(a.input_stack_len) : a.total_num_init_phy_mem_accesses)
+    return set_err(ctx, SPG_E_ARG, "snark verify: total_num_init_phy_mem_accesses != input_stack.len().next_power_of_two()");
+  if (a.input_mem_len ? a.total_num_init_vir_mem_accesses != npow2(a.input_mem_len) : a.total_num_init_vir_mem_accesses)
+    return set_err(ctx, SPG_E_ARG, "snark verify: total_num_init_vir_mem_accesses != input_mem.len().next_power_of_two()");
+
+  // Scalar::from_bytes(..).unwrap() on every public scalar (src/lib.rs:2836-2850): non-canonical bytes are rejected
+  SnarkPub pub;
+  Fq x;
+  for (size_t i = 0; i < a.input_len; i++) {
+    if (!scalar_from_bytes(a.input + 32 * i, &x)) return set_err(ctx, SPG_E_ARG, "snark verify: input not canonical");
+    pub.input.push_back(x);
+  }
+  for (size_t i = 0; i < a.input_stack_len; i++) {
+    if (!scalar_from_bytes(a.input_stack + 32 * i, &x)) return set_err(ctx, SPG_E_ARG, "snark verify: input_stack not canonical");
+    pub.stack.push_back(x);
+  }
+  for (size_t i = 0; i < a.input_mem_len; i++) {
+    if (!scalar_from_bytes(a.input_mem + 32 * i, &x)) return set_err(ctx, SPG_E_ARG, "snark verify: input_mem not canonical");
+    pub.mem.push_back(x);
+  }
+  if (!scalar_from_bytes(a.output, &pub.output)) return set_err(ctx, SPG_E_ARG, "snark verify: output not canonical");
+  for (size_t b = 0; b < a.block_num_instances_bound; b++)  // src/lib.rs:2829-2831
+    if (a.block_num_proofs[b] > a.block_max_num_proofs)
+      return set_err(ctx, SPG_E_ARG, "snark verify: block_num_proofs[b] > block_max_num_proofs");
+  // the internal argument block (sizes only; the lists are in pub)
+  spg_snark_inputs in;
+  memset(&in, 0, sizeof in);
+  in.input_block_num = a.input_block_num;
+  in.output_block_num = a.output_block_num;
+  in.input_liveness = a.input_liveness;
+  in.input_len = a.input_len;
+  in.func_input_width = a.func_input_width;
+  in.input_offset = a.input_offset;
+  in.output_offset = a.output_offset;
+  in.output_exec_num = a.output_exec_num;
+  in.num_vars = a.num_vars;
+  in.num_ios = a.num_ios;
+  in.max_block_num_phy_ops = a.max_block_num_phy_ops;
+  in.block_num_phy_ops = a.block_num_phy_ops;
+  in.max_block_num_vir_ops = a.max_block_num_vir_ops;
+  in.block_num_vir_ops = a.block_num_vir_ops;
+  in.mem_addr_ts_bits_size = a.mem_addr_ts_bits_size;
+  in.num_inputs_unpadded = a.num_inputs_unpadded;
+  in.block_num_vars = a.block_num_vars;
+  in.block_num_instances_bound = a.block_num_instances_bound;
+  in.block_max_num_proofs = a.block_max_num_proofs;
+  in.block_num_proofs = a.block_num_proofs;
+  in.consis_num_proofs = a.consis_num_proofs;
+  in.total_num_init_phy_mem_accesses = a.total_num_init_phy_mem_accesses;
+  in.total_num_init_vir_mem_accesses = a.total_num_init_vir_mem_accesses;
+  in.total_num_phy_mem_accesses = a.total_num_phy_mem_accesses;
+  in.total_num_vir_mem_accesses = a.total_num_vir_mem_accesses;
+  SnarkCompView vb, vp, vr;
+  if (snark_comp_view(block, &vb) || snark_comp_view(pairwise, &vp) || snark_comp_view(perm_root, &vr))
+    return set_err(ctx, SPG_E_ARG, "snark verify: instance commitments incomplete");
+  // the commitments' instance sizes are SNARK::verify's block_num_cons / pairwise_check_num_cons / perm_root_num_cons
+  if (vb.max_num_cons != a.block_num_cons || vp.max_num_cons != a.pairwise_check_num_cons ||
+      vr.max_num_cons != a.perm_root_num_cons)
+    return set_err(ctx, SPG_E_ARG, "snark verify: num_cons arguments differ from the loaded commitments");
+  SPG_HIP(ctx, hipSetDevice(ctx->device));
+  SnarkV pf;
+  Rd r(proof, proof_len);
+  if (!rd_snark(r, pf)) return set_err(ctx, SPG_E_VERIFY, "snark verify: malformed proof bytes");
+  SnarkVerifier v(ctx, transcript->t);
+  bool ok = false;
+  try {
+    ok = snark_verify(v, pf, in, pub, vb, vp, vr, vars_gens->g);
+  } catch (const Fail& f) {
+    v.fail(f.what);
+  }
+  if (!ok) return set_err(ctx, SPG_E_VERIFY, std::string("snark verify: ") + (v.failed ? v.failed : "rejected"));
+  return SPG_OK;
+}
+
+extern "C" int spg_snark_verify_public(spg_ctx* ctx, const spg_snark_comp* block, const spg_snark_comp* pairwise,
+                                       const spg_snark_comp* perm_root, const spg_snark_public* pub,
+                                       spg_r1cs_gens* vars_gens, spg_transcript* transcript, const uint8_t* proof,
+                                       size_t proof_len) {
+  if (!ctx || !transcript) return SPG_E_ARG;
+  spg::HostPin pin;
+  return spg::tr_status(ctx, transcript->t,
+                        spg_snark_verify_public_impl(ctx, block, pairwise, perm_root, pub, vars_gens, transcript, proof,
+                                                     proof_len));
 }

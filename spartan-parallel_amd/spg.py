@@ -649,6 +649,48 @@ class SnarkComp:
     def handle(self):
         return self._h
 
+    def comm_bytes(self, as_list):
+        """bincode(Vec<ComputationCommitment>) (as_list) or bincode(ComputationCommitment) (spg_snark_comm_bytes)"""
+        ln = ctypes.c_size_t(0)
+        lib().spg_snark_comm_bytes(self.ctx.handle, self._h, ctypes.c_int(1 if as_list else 0), None,
+                                   ctypes.c_size_t(0), ctypes.byref(ln))
+        buf = np.zeros(max(ln.value, 1), dtype=np.uint8)
+        self.ctx.check(lib().spg_snark_comm_bytes(self.ctx.handle, self._h, ctypes.c_int(1 if as_list else 0),
+                                                  _p(buf), ctypes.c_size_t(ln.value), ctypes.byref(ln)),
+                       "spg_snark_comm_bytes")
+        return buf[: ln.value].tobytes()
+
+    def comm_map(self):
+        """block_comm_map: one list of matrix indices 3p + m per commitment (spg_snark_comm_map)"""
+        idx = np.zeros(1 << 16, dtype=np.uintp)
+        lens = np.zeros(1 << 12, dtype=np.uintp)
+        n = ctypes.c_size_t(0)
+        self.ctx.check(lib().spg_snark_comm_map(self.ctx.handle, self._h, _p(idx), ctypes.c_size_t(len(idx)), _p(lens),
+                                                ctypes.c_size_t(len(lens)), ctypes.byref(n)), "spg_snark_comm_map")
+        out, o = [], 0
+        for g in range(n.value):
+            out.append([int(x) for x in idx[o:o + int(lens[g])]])
+            o += int(lens[g])
+        return out
+
+    @classmethod
+    def load(cls, ctx, comm, as_list, comm_map, num_cons, gens):
+        """a verifier-side instance from ComputationCommitment bytes (spg_snark_comm_load): comm_map = block_comm_map
+        for a list, num_cons = block_num_cons / pairwise_check_num_cons / perm_root_num_cons, gens = the
+        SNARKGens::new(num_cons, num_vars, num_instances, num_nz_entries) arguments"""
+        c = cls.__new__(cls)
+        c.ctx = ctx
+        c._h = ctypes.c_void_p()
+        buf = np.frombuffer(bytes(comm), dtype=np.uint8).copy() if len(comm) else np.zeros(1, np.uint8)
+        flat = np.array([k for l in (comm_map or []) for k in l] or [0], dtype=np.uintp)
+        lens = np.array([len(l) for l in (comm_map or [])] or [0], dtype=np.uintp)
+        ctx.check(lib().spg_snark_comm_load(ctx.handle, _p(buf), ctypes.c_size_t(len(comm)),
+                                            ctypes.c_int(1 if as_list else 0), _p(flat), _p(lens),
+                                            ctypes.c_size_t(len(comm_map or [])), ctypes.c_size_t(num_cons),
+                                            *[ctypes.c_size_t(x) for x in gens], ctypes.byref(c._h)),
+                  "spg_snark_comm_load")
+        return c
+
     def __del__(self):
         try:
             if self._h:
@@ -703,6 +745,19 @@ def snark_verify(ctx, block, pairwise, perm_root, inputs, vars_gens, transcript,
     if rc == SPG_E_VERIFY:
         return False, lib().spg_last_error(ctx.handle).decode(errors="replace")
     ctx.check(rc, "spg_snark_verify")
+    return True, ""
+
+
+def snark_verify_public(ctx, block, pairwise, perm_root, public, vars_gens, transcript, proof):
+    """SNARK::verify from what the reference verifier is given (spg_snark_verify_public): SnarkComp.load'ed
+    commitments and `public` (a workload.CSnarkPublic). Returns (True, "") / (False, reason); raises on bad arguments."""
+    buf = np.frombuffer(bytes(proof), dtype=np.uint8).copy() if len(proof) else np.zeros(1, np.uint8)
+    rc = lib().spg_snark_verify_public(ctx.handle, block.handle, pairwise.handle, perm_root.handle,
+                                       ctypes.byref(public), vars_gens.handle, transcript.handle, _p(buf),
+                                       ctypes.c_size_t(len(proof)))
+    if rc == SPG_E_VERIFY:
+        return False, lib().spg_last_error(ctx.handle).decode(errors="replace")
+    ctx.check(rc, "spg_snark_verify_public")
     return True, ""
 
 

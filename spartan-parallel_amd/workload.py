@@ -588,6 +588,92 @@ class CSnarkInputs(ctypes.Structure):
                                        "addr_vir_mems", "addr_ts_bits")]
 
 
+class CSnarkPublic(ctypes.Structure):
+    """include/spg.h spg_snark_public: SNARK::verify's public arguments (src/lib.rs:2750-2798)"""
+    _fields_ = [(n, ctypes.c_size_t) for n in ("input_block_num", "output_block_num")] + [
+        ("input_liveness", ctypes.c_void_p), ("input_len", ctypes.c_size_t)] + [
+        (n, ctypes.c_size_t) for n in ("func_input_width", "input_offset", "output_offset")] + [
+        ("input", ctypes.c_void_p), ("input_stack", ctypes.c_void_p), ("input_stack_len", ctypes.c_size_t),
+        ("input_mem", ctypes.c_void_p), ("input_mem_len", ctypes.c_size_t), ("output", ctypes.c_void_p),
+        ("output_exec_num", ctypes.c_size_t), ("num_vars", ctypes.c_size_t), ("num_ios", ctypes.c_size_t),
+        ("max_block_num_phy_ops", ctypes.c_size_t), ("block_num_phy_ops", ctypes.POINTER(ctypes.c_size_t)),
+        ("max_block_num_vir_ops", ctypes.c_size_t), ("block_num_vir_ops", ctypes.POINTER(ctypes.c_size_t)),
+        ("mem_addr_ts_bits_size", ctypes.c_size_t), ("num_inputs_unpadded", ctypes.c_size_t),
+        ("block_num_vars", ctypes.POINTER(ctypes.c_size_t)), ("block_num_instances_bound", ctypes.c_size_t),
+        ("block_max_num_proofs", ctypes.c_size_t), ("block_num_proofs", ctypes.POINTER(ctypes.c_size_t)),
+        ("block_num_cons", ctypes.c_size_t)] + [
+        (n, ctypes.c_size_t) for n in ("consis_num_proofs", "total_num_init_phy_mem_accesses",
+                                       "total_num_init_vir_mem_accesses", "total_num_phy_mem_accesses",
+                                       "total_num_vir_mem_accesses", "pairwise_check_num_cons", "perm_root_num_cons")]
+
+
+def scalar_bytes(vals):
+    """canonical scalars (python ints < q) -> (n, 32) little-endian bytes, the reference's [u8; 32]"""
+    out = np.zeros((len(vals), 32), dtype=np.uint8)
+    for i, v in enumerate(vals):
+        out[i] = np.frombuffer(int(v).to_bytes(32, "little"), dtype=np.uint8)
+    return out
+
+
+class SnarkPublic:
+    """What the reference verifier of a SnarkWorkload is given (spg_snark_public): the public values as [u8; 32]
+    bytes, the input stack / memory (not their init lists) and the sizes, plus the verifier-side commitment
+    arguments: num_cons and SNARKGens::new arguments of each instance (as SnarkViews encodes them)."""
+
+    def __init__(self, wl):
+        self.keep = []
+
+        def arr(a):
+            a = np.ascontiguousarray(a)
+            self.keep.append(a)
+            return a.ctypes.data
+
+        def sz(v):
+            a = _sz(v)
+            self.keep.append(a)
+            return a
+
+        npow = lambda v: 0 if v == 0 else 1 << (v - 1).bit_length()
+        stack, mem = list(getattr(wl, "input_stack", [])), list(getattr(wl, "input_mem", []))
+        c = CSnarkPublic()
+        c.input_block_num, c.output_block_num = wl.input_block_num, wl.output_block_num
+        c.input_liveness = arr(np.array(wl.input_liveness, dtype=np.uint8))
+        c.input_len = len(wl.input_liveness)
+        c.func_input_width, c.input_offset, c.output_offset = wl.func_input_width, wl.input_offset, wl.output_offset
+        c.input = arr(scalar_bytes([0, 0, wl.x0]))
+        c.input_stack = arr(scalar_bytes(stack)) if stack else None
+        c.input_stack_len = len(stack)
+        c.input_mem = arr(scalar_bytes(mem)) if mem else None
+        c.input_mem_len = len(mem)
+        c.output = arr(scalar_bytes([wl.output]))
+        c.output_exec_num = wl.output_exec_num
+        c.num_vars, c.num_ios = wl.num_vars, wl.num_ios
+        c.max_block_num_phy_ops = max(wl.block_num_phy_ops)
+        c.block_num_phy_ops = sz(wl.block_num_phy_ops)
+        c.max_block_num_vir_ops = max(wl.block_num_vir_ops)
+        c.block_num_vir_ops = sz(wl.block_num_vir_ops)
+        c.mem_addr_ts_bits_size = wl.mem_addr_ts_bits_size
+        c.num_inputs_unpadded = wl.num_inputs_unpadded
+        c.block_num_vars = sz(wl.num_vars_per_block)
+        c.block_num_instances_bound = wl.num_blocks
+        c.block_max_num_proofs = wl.block_max_num_proofs
+        c.block_num_proofs = sz(wl.block_num_proofs)
+        c.block_num_cons = wl.block_inst[1]
+        c.consis_num_proofs = wl.consis_num_proofs
+        c.total_num_init_phy_mem_accesses = npow(len(stack))
+        c.total_num_init_vir_mem_accesses = npow(len(mem))
+        c.total_num_phy_mem_accesses = len(getattr(wl, "addr_phy_mems", []))
+        c.total_num_vir_mem_accesses = len(getattr(wl, "addr_vir_mems", []))
+        c.pairwise_check_num_cons = wl.pairwise_inst[1]
+        c.perm_root_num_cons = wl.perm_root_inst[1]
+        self.c = c
+        B = wl.num_blocks
+        # (num_cons, SNARKGens::new arguments) per instance, as SnarkViews passes them to the encoder
+        self.block_gens = (wl.block_max_num_cons, wl.block_num_vars, B, wl.block_nnz)
+        self.pairwise_gens = (wl.pairwise_max_num_cons, 4 * wl.pairwise_num_vars, 3, wl.pairwise_nnz)
+        self.perm_root_gens = (wl.perm_root_num_cons, 8 * wl.num_ios, 1, wl.perm_root_nnz)
+
+
 class SnarkViews:
     """C views (include/spg.h spg_snark_inputs / spg_snark_instance) of a SnarkWorkload; keeps buffers alive."""
 

@@ -110,7 +110,7 @@ def test_commit_rows(ctx, oracle, gens64, L, R):
 
 
 def test_large_msm_2e16_property(ctx, oracle):
-    """Config-2 size: a 2^16-point MSM equals the sum of 16 disjoint 4096-point MSMs computed by the oracle."""
+    """Config-2 size: a 2^16-point MSM (spg_msm) equals the oracle's vartime Pippenger MSM of the same 2^16 pairs."""
     import spg
 
     n = 1 << 16

@@ -87,10 +87,11 @@ def test_circ_program_on_gpu(ctx, vars_gens, tmp_path, case):
     assert hashlib.sha256(proof).hexdigest() == golden["proof_sha256"]
 
 
-@pytest.mark.parametrize("host_max", ["0", "4096"])
-def test_bullet_paths(host_max):
-    """every DotProductProofLog through the device Bullet rounds (SPG_BULLET_HOST_MAX=0) or every one on the host
-    pool (4096): the same bytes as the golden proof (a fresh process reads the switch)"""
+@pytest.mark.parametrize("host_max,comb", [("0", "1"), ("0", "0"), ("4096", "1")])
+def test_bullet_paths(host_max, comb):
+    """every DotProductProofLog through the device Bullet rounds (SPG_BULLET_HOST_MAX=0) -- in the comb form
+    (k_bullet_comb, the default) or the bucket form (SPG_BULLET_COMB=0, k_bullet_round_q) -- or every one on the
+    host pool (4096): the same bytes as the golden proof (a fresh process reads the switches)"""
     import subprocess
     import sys
 
@@ -106,7 +107,8 @@ def test_bullet_paths(host_max):
         "(p,) = gpu_snark(ctx, g, workload.SnarkWorkload(**SNARK_CASES[%r]), workload.tape_seed())\n"
         "print(hashlib.sha256(p).hexdigest())\n"
     ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "tests"), case)
-    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BULLET_HOST_MAX=host_max),
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BULLET_HOST_MAX=host_max,
+                                                               SPG_BULLET_COMB=comb),
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     golden = json.load(open(os.path.join(G, "snark_proofs.json")))[case]

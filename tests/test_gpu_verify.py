@@ -126,3 +126,99 @@ def test_verify_rejects_noncanonical_scalar_limbs(ctx, vars_gens):
     bad[s:e] = (m + Q).to_bytes(32, "little")
     ok, why = prog.verify(bytes(bad))
     assert not ok and "malformed" in why, (name, why)
+
+
+# ---- the verifier's side of the boundary: commitment bytes + public arguments (spg_snark_verify_public) ----------
+PUBLIC_CASES = {
+    "b2_x32_q2": dict(num_blocks=2, log_cons=5, log_proofs=1, num_vars=32),
+    # input stack / memory of power-of-two lengths: SNARK::verify asserts total_num_init_*_mem_accesses ==
+    # input_{stack,mem}.len().next_power_of_two() (src/lib.rs:3276-3281)
+    "mem_pow2_b3_x64_q2": dict(num_blocks=3, log_cons=6, log_proofs=1, num_vars=64, phy_ops=1, vir_ops=2, init_phy=4,
+                               init_vir=8, niu=5),
+}
+PRE = [(b"app-domain", b"verifier session"), (b"app-nonce", bytes(range(24)))]
+
+
+def _pre_transcript(oracle, label, pre):
+    t = oracle.OracleTranscript(label)
+    for lbl, msg in pre:
+        t.append_message(lbl, msg)
+    return t
+
+
+@pytest.mark.parametrize("case", sorted(PUBLIC_CASES))
+def test_verify_from_commitment_bytes_on_caller_transcript(ctx, oracle, vars_gens, case):
+    """The verifier holds only what SNARK::verify is given (src/lib.rs:2750-2798): the ComputationCommitment bytes the
+    prover's encoder exported, block_comm_map, the SNARKGens arguments, the public values as [u8; 32] (input stack
+    and memory, not their init lists) and its own `&mut Transcript` after application pre-appends (behind
+    spg_transcript_new_callbacks). Its verdicts must agree with the CPU oracle's verifier on the same transcripts:
+    accept with the prover's pre-appends (and leave the caller transcript in the oracle verifier's state), reject with
+    other pre-appends, and reject when one commitment row is swapped for another."""
+    import spg
+    import workload
+
+    wl = workload.SnarkWorkload(**PUBLIC_CASES[case])
+    v = workload.SnarkViews(wl)
+    pub = workload.SnarkPublic(wl)
+    seed = workload.tape_seed()
+    # prover side: encode, export the commitments, prove on the caller's pre-appended transcript
+    block = spg.SnarkComp(ctx, v.block, multi=True)
+    pairwise = spg.SnarkComp(ctx, v.pairwise)
+    perm_root = spg.SnarkComp(ctx, v.perm_root)
+    cb, cmap = block.comm_bytes(True), block.comm_map()
+    cp, cr = pairwise.comm_bytes(False), perm_root.comm_bytes(False)
+    tp = _pre_transcript(oracle, b"snark_pub", PRE)
+    proof = spg.snark_prove(ctx, block, pairwise, perm_root, spg.SnarkWitness(ctx, v.inputs), vars_gens,
+                            spg.Transcript.from_callbacks(tp.append_message, tp.challenge_bytes),
+                            spg.RandomTape(b"proof", seed))
+    del block, pairwise, perm_root
+    # the oracle: the same proof on the same pre-appends, and its verdict on a verifier transcript with them
+    ovt = _pre_transcript(oracle, b"snark_pub", PRE)
+    ref, verdict = oracle.snark_prove_verify_on(wl, seed, _pre_transcript(oracle, b"snark_pub", PRE), ovt)
+    assert proof == ref and verdict == 0
+    # verifier side, from bytes alone
+    c = pub.c
+    vb = spg.SnarkComp.load(ctx, cb, True, cmap, c.block_num_cons, pub.block_gens)
+    vp = spg.SnarkComp.load(ctx, cp, False, None, c.pairwise_check_num_cons, pub.pairwise_gens)
+    vr = spg.SnarkComp.load(ctx, cr, False, None, c.perm_root_num_cons, pub.perm_root_gens)
+
+    def verify(pre, comms=(vb, vp, vr)):
+        t = _pre_transcript(oracle, b"snark_pub", pre)
+        ok, why = spg.snark_verify_public(ctx, *comms, c, vars_gens,
+                                          spg.Transcript.from_callbacks(t.append_message, t.challenge_bytes), proof)
+        return ok, why, t
+
+    ok, why, t = verify(PRE)
+    assert ok, why
+    assert t.challenge_bytes(b"after", 32) == ovt.challenge_bytes(b"after", 32), "verifier transcripts diverge"
+    other = PRE[:1] + [(b"app-nonce", bytes(range(1, 25)))]
+    ok, _, _ = verify(other)
+    _, overdict = oracle.snark_prove_verify_on(wl, seed, _pre_transcript(oracle, b"snark_pub", PRE),
+                                               _pre_transcript(oracle, b"snark_pub", other))
+    assert not ok and overdict != 0, "verdicts on other pre-appends: product accepted or oracle accepted"
+    # a verifier holding a wrong commitment: the first two row commitments of the perm-root comb_ops swapped
+    bad = bytearray(cr)
+    o = 8 * 5 + 8  # num_cons, num_vars, batch_size, num_ops, num_mem_cells, then comm_comb_ops' length
+    if len(bad) >= o + 64:
+        bad[o:o + 32], bad[o + 32:o + 64] = cr[o + 32:o + 64], cr[o:o + 32]
+        if bytes(bad) != cr:
+            vr_bad = spg.SnarkComp.load(ctx, bytes(bad), False, None, c.perm_root_num_cons, pub.perm_root_gens)
+            ok, _, _ = verify(PRE, (vb, vp, vr_bad))
+            assert not ok, "a swapped commitment row was accepted"
+
+
+def test_comm_load_rejects_malformed_bytes(ctx, vars_gens):
+    """truncated or trailing commitment bytes, a wrong num_cons and a map that does not cover the batch are argument
+    errors, not a verifier that silently checks against something else"""
+    import spg
+    import workload
+
+    wl = workload.SnarkWorkload(**PUBLIC_CASES["b2_x32_q2"])
+    v = workload.SnarkViews(wl)
+    pub = workload.SnarkPublic(wl)
+    block = spg.SnarkComp(ctx, v.block, multi=True)
+    cb, cmap = block.comm_bytes(True), block.comm_map()
+    n = pub.c.block_num_cons
+    for bad, m, nc in ((cb[:-1], cmap, n), (cb + b"\0", cmap, n), (cb, cmap, 3 * n), (cb, [l[:-1] for l in cmap], n)):
+        with pytest.raises(spg.SpgError, match="SPG_E_ARG"):
+            spg.SnarkComp.load(ctx, bad, True, m, nc, pub.block_gens)
