@@ -631,7 +631,7 @@ static void bullet_comb_shape(int P, int* G, int* BS, int* R) {
   static const int er = getenv("SPG_BCOMB_R") ? atoi(getenv("SPG_BCOMB_R")) : 0;
   *G = P >= 512 ? 4 : 8;
   *BS = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
-  *R = 4;
+  *R = P >= 2048 ? 1 : 4;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
   if (eg == 4 || eg == 8 || eg == 11) *G = eg;
   if (ebs == 64 || ebs == 128 || ebs == 256) *BS = ebs;
   if (er >= 1 && er <= *BS / 4 && (er & (er - 1)) == 0) *R = er;

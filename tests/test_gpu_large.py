@@ -260,6 +260,11 @@ def _spark_full_worker(rank, world, port, q):
     import hashlib
     import sys
 
+    # three processes share the test box's one GPU here: the ranks commit through the bucket pipeline (a 2^14-generator
+    # comb table is 70 GB per process), while the unsharded proof in the parent took the comb path -- the two forms
+    # compute the same group elements, so the bytes must agree either way
+    os.environ["SPG_COMB_GB"] = "8"
+
     sys.path[:0] = [os.path.join(ROOT, "spartan-parallel_amd"), os.path.join(ROOT, "tests")]
     import torch.distributed as dist
 
