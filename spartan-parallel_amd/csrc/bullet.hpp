@@ -273,4 +273,59 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
   }
 }
 
+// B plain MSMs from the comb table, sum_i s_{b,i} G_{idx_{b,i}} (Montgomery scalars), left as partial points: the Cx
+// commitment of a device DotProductProofLog (its blind term is added on the host). The same quads, window groups and
+// workgroup trees as k_bullet_comb; parts[b][wg][0..R).
+template <int G, int BS>
+__global__ void __launch_bounds__(BS) k_comb_msm_parts(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
+                                                       int n, const Niels* __restrict__ comb, int NS, int R,
+                                                       Ext* __restrict__ parts) {
+  constexpr int C = 12, W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
+  constexpr uint32_t MASK = (1u << C) - 1u;
+  __shared__ uint32_t pts[soa_words<Ext, S>()];
+  const int b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int gq = blockIdx.x * S + slot;
+  const int p = gq / G, jg = gq - p * G, w0 = jg * WG;
+  Ext acc = ext_identity();
+  if (p < n) {
+    const Fq k = fq_from_mont(scalars[(size_t)b * n + p]);
+    const int s = (int)idx[(size_t)b * n + p];
+    uint32_t ent[WG];
+#pragma unroll
+    for (int x = 0; x < WG; x++) ent[x] = 0xffffffffu;
+    int carry = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const int bit = w * C;
+      const int li = bit >> 5, of = bit & 31;
+      uint32_t v = k.l[li] >> of;
+      if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+      int d = (int)(v & MASK) + carry;
+      carry = d > NB ? 1 : 0;
+      d -= carry << C;
+      if (w >= w0 && w < w0 + WG) {
+#pragma unroll
+        for (int x = 0; x + 1 < WG; x++) ent[x] = ent[x + 1];
+        ent[WG - 1] = d == 0 ? 0xffffffffu
+                             : ((uint32_t)((w * NS + s) * NB + (d < 0 ? -d : d) - 1) | (d < 0 ? 0x80000000u : 0u));
+      }
+    }
+    Fp qv[WG];
+    bool ng[WG];
+#pragma unroll
+    for (int x = 0; x < WG; x++)
+      if (ent[x] != 0xffffffffu) qv[x] = niels_coord(comb, ent[x], q, &ng[x]);
+#pragma unroll
+    for (int x = 0; x < WG; x++)
+      if (ent[x] != 0xffffffffu) acc = quad_madd(acc, qv[x], ng[x], q);
+  }
+  for (int d = S / 2; d >= R; d >>= 1) {
+    if (slot >= d && slot < 2 * d) quad_put_op<S>(pts, slot - d, acc, q);
+    __syncthreads();
+    if (slot < d) acc = quad_add_op(acc, quad_get_op<S>(pts, slot, q), q);
+    __syncthreads();
+  }
+  if (slot < R && q == 0) parts[((size_t)b * gridDim.x + blockIdx.x) * R + slot] = acc;
+}
+
 }  // namespace spg

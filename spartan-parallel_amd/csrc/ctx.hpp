@@ -191,6 +191,10 @@ static const int kBulletNB = 64;  // buckets per MSM of bullet_round_device (c =
 // into d_parts (at most kBulletPartsMax per MSM), completion posted to the mailbox with *seq_out; the host adds each
 // MSM's parts. Returns 1 when g has no comb table for these generators (the caller takes the bucket form).
 static const int kBulletPartsMax = 512;
+// B MSMs of n Montgomery scalars over generators d_idx[b n + i] (< gmax) from g's comb table, as B x *per_msm partial
+// points into d_parts (stream-ordered, no completion post); 1 when the comb does not apply
+int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const uint32_t* d_idx, size_t gmax, int n,
+                   int B, Ext* d_parts, int* per_msm);
 int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
                       const uint32_t* gidx, size_t gmax, const Fq& u, const Fq& uinv, int k, int n, int nk,
                       Ext* d_parts, uint32_t* seq_out, int* per_msm);

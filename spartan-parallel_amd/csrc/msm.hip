@@ -675,6 +675,35 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   return 0;
 }
 
+int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const uint32_t* d_idx, size_t gmax, int n,
+                   int B, Ext* d_parts, int* per_msm) {
+  static const bool on = !getenv("SPG_BULLET_COMB") || atoi(getenv("SPG_BULLET_COMB")) != 0;
+  if (!on || n < 1) return 1;
+  spg_gens::Comb cb;
+  const int rc = comb_get(ctx, g, gmax, &cb);
+  if (rc) return rc == 1 ? 1 : rc;
+  int G, BS, R;
+  bullet_comb_shape(std::max(2, n), &G, &BS, &R);
+  const int S = BS / 4, wgs = (n * G + S - 1) / S;
+  if (wgs * R > kBulletPartsMax) return 1;
+  *per_msm = wgs * R;
+  KScope ks(ctx, "msm_comb_parts", 0.0, (double)B * n * 22.0 * (1.0 - 1.0 / 4096.0));
+  const dim3 grid((unsigned)wgs, (unsigned)B);
+  const int NS = (int)cb.slots + 1;
+#define SPG_CMP(GG, BB) \
+  hipLaunchKernelGGL((k_comb_msm_parts<GG, BB>), grid, dim3(BB), 0, ctx->stream, d_scalars, d_idx, n, cb.p, NS, R, d_parts)
+  if (G == 4) {
+    if (BS == 64) SPG_CMP(4, 64); else if (BS == 128) SPG_CMP(4, 128); else SPG_CMP(4, 256);
+  } else if (G == 8) {
+    if (BS == 64) SPG_CMP(8, 64); else if (BS == 128) SPG_CMP(8, 128); else SPG_CMP(8, 256);
+  } else {
+    if (BS == 64) SPG_CMP(11, 64); else if (BS == 128) SPG_CMP(11, 128); else SPG_CMP(11, 256);
+  }
+#undef SPG_CMP
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
 // the latency-path bucket kernel, quad form unless SPG_SMSM_QUAD=0
 #define SMSM_LAUNCH(BSZ, ...)                                                                   \
   do {                                                                                          \

@@ -366,8 +366,9 @@ static int bullet_round0_launch(spg_ctx* ctx, ProverGens& g, size_t n, const Fq*
                                 size_t gmax, Ext* d_bk, uint32_t* seq, int* per) {
   Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
   if (!st) return set_err(ctx, SPG_E_NOMEM, "bullet state");
-  SPG_HIP(ctx, hipMemcpyAsync(st, d_x, n * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
-  return bullet_round_launch(ctx, g, st, st + 2 * n, st + n, st + 3 * n, d_idx, gmax, fq_zero(), fq_zero(), 0, n, n,
+  // round 0 reads a = x where the Cx MSM's scalars already are, and writes the state round 1 reads (aa[1], cw[1]);
+  // no later round reads aa[0] before writing it
+  return bullet_round_launch(ctx, g, d_x, st + 2 * n, st + n, st + 3 * n, d_idx, gmax, fq_zero(), fq_zero(), 0, n, n,
                              d_bk, seq, per);
 }
 
@@ -458,24 +459,27 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   // generator indices G_0..G_{n-1}, G_1, h for B = 2 MSMs, uploaded once for all rounds
   const size_t n2 = n + 2;
   uint32_t* d_idx = nullptr;
+  using HostJob = std::pair<std::vector<size_t>, FqV>;
+  static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
+  static const bool ahead = !getenv("SPG_BULLET_AHEAD") || atoi(getenv("SPG_BULLET_AHEAD")) != 0;
+  const bool dev_path = dev_rounds && !on_host && n >= 2 && (n & (n - 1)) == 0;
+  std::vector<uint32_t> idx2;
   if (!on_host) {
-    std::vector<uint32_t> idx2(2 * n2);
+    idx2.resize(2 * n2);
     for (size_t b = 0; b < 2; b++) {
       for (size_t j = 0; j < n; j++) idx2[b * n2 + j] = (uint32_t)kn.G[j];
       idx2[b * n2 + n] = G1;
       idx2[b * n2 + n + 1] = H;
     }
-    d_idx = (uint32_t*)ws_get(ctx, 21, idx2.size() * 4 + 64);
-    if (!d_idx) return set_err(ctx, SPG_E_NOMEM, "bullet indices");
-    SPG_HIP(ctx, hipMemcpyAsync(d_idx, idx2.data(), idx2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (!(dev_path && ahead)) {  // (the ahead path uploads them with the Cx scalars)
+      d_idx = (uint32_t*)ws_get(ctx, 21, idx2.size() * 4 + 64);
+      if (!d_idx) return set_err(ctx, SPG_E_NOMEM, "bullet indices");
+      SPG_HIP(ctx, hipMemcpyAsync(d_idx, idx2.data(), idx2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
   }
-  using HostJob = std::pair<std::vector<size_t>, FqV>;
-  static const bool dev_rounds = !getenv("SPG_BULLET_DEV") || atoi(getenv("SPG_BULLET_DEV")) != 0;
-  static const bool ahead = !getenv("SPG_BULLET_AHEAD") || atoi(getenv("SPG_BULLET_AHEAD")) != 0;
-  const bool dev_path = dev_rounds && !on_host && n >= 2 && (n & (n - 1)) == 0;
   // mapped host memory for the bucket sums: [Cx MSM (B = 1, up to 256 buckets)][Bullet rounds: 2 x 65 buckets, or
   // 2 x up to kBulletPartsMax partial points of the comb form]
-  const size_t cx_bytes = sizeof(Ext) * 256,
+  const size_t cx_bytes = sizeof(Ext) * std::max<size_t>(256, kBulletPartsMax),
                br_bytes = sizeof(Ext) * 2 * std::max<size_t>(kBulletNB + 1, kBulletPartsMax) + 64;
   size_t gmax = 0;  // the comb form needs the table to cover G_0 .. G_{n-1} of this proof
   for (size_t j = 0; j < n; j++) gmax = std::max(gmax, kn.G[j] + 1);
@@ -491,24 +495,37 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   if (mbk && ahead) {
     // the Cx bucket sums, then Bullet round 0 (which needs no challenge), on the stream before the host waits
     // for Cx: one device round trip fewer per proof
-    std::vector<Fq> hs(n2, fq_zero());
-    std::copy(x.begin(), x.end(), hs.begin());
-    hs[n + 1] = blind_x;
-    Fq* d_s = (Fq*)ws_get(ctx, 20, n2 * sizeof(Fq) + 64);
-    uint8_t* stage = (uint8_t*)pinned_get(ctx, n2 * sizeof(Fq) + 64);
-    if (!d_s || !stage) return set_err(ctx, SPG_E_NOMEM, "Cx");
-    memcpy(stage, hs.data(), n2 * sizeof(Fq));
-    SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, n2 * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
-    int NB = 0;
-    int rc = msm_small_buckets(ctx, g.dev, 0, d_s, n2, 1, nullptr, d_idx, -1, (Ext*)d_map, &NB);
+    // one page-locked copy: the Cx scalars (x, 0, blind_x), then the generator indices of every round
+    const size_t sb = n2 * sizeof(Fq), ib = idx2.size() * 4;
+    Fq* d_s = (Fq*)ws_get(ctx, 20, sb + ib + 64);
+    uint8_t* stage = (uint8_t*)pinned_get(ctx, sb + ib + 64);
+    if (!d_s || !stage || idx2.empty()) return set_err(ctx, SPG_E_NOMEM, "Cx");
+    memcpy(stage, x.data(), n * sizeof(Fq));
+    memset(stage + n * sizeof(Fq), 0, sizeof(Fq));
+    memcpy(stage + (n + 1) * sizeof(Fq), &blind_x, sizeof(Fq));
+    memcpy(stage + sb, idx2.data(), ib);
+    SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, sb + ib, hipMemcpyHostToDevice, ctx->stream));
+    d_idx = (uint32_t*)((uint8_t*)d_s + sb);
+    // Cx from the comb table as partial points (+ blind_x h on the host), or the bucket sums of the latency path
+    int NB = 0, cper = 0;
+    int rc = comb_msm_parts(ctx, g.dev, d_s, d_idx, gmax, (int)n, 1, (Ext*)d_map, &cper);
+    if (rc == 1) {
+      cper = 0;
+      rc = msm_small_buckets(ctx, g.dev, 0, d_s, n2, 1, nullptr, d_idx, -1, (Ext*)d_map, &NB);
+    }
     if (rc) return rc;
     SPG_HIP(ctx, hipEventRecord(ctx->ev_cx, ctx->stream));
     rc = bullet_round0_launch(ctx, g, n, d_s, d_idx, gmax, d_mbk, &seq0, &per0);
     if (rc) return rc;
     pre0 = true;
+    h::HExt blind_h;
+    if (cper) blind_h = g.host.sum_many({{{(size_t)H}, {blind_x}}})[0];  // while the device works
     SPG_HIP(ctx, hipEventSynchronize(ctx->ev_cx));
     pts.resize(1);
-    bucket_finals((const Ext*)mapped, 1, NB, pts.data());
+    if (cper)
+      parts_finals((const Ext*)mapped, 1, (size_t)cper, pts.data(), &blind_h);
+    else
+      bucket_finals((const Ext*)mapped, 1, NB, pts.data());
   } else if (on_host) {
     HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), x};
     j.first.push_back(kn.h);

@@ -251,6 +251,96 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
   grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
+// ---- quad forms of the round evaluations (small rounds: latency-bound) ------------------------------------------
+// A round whose domain leaves the chip mostly idle is bound by the dependent chain of one thread's products (about
+// ten Fq products per point in phase 1, each ~0.6 us on one wave). Here a quad (4 lanes) takes each point and its
+// lanes compute the point's independent products side by side (operands selected per lane, exchanged by DPP quad
+// broadcasts): three levels of products in phase 1, two in phase 2. Lane 0 accumulates e0, lane 1 e2, lane 2 e3.
+template <int K>
+__device__ __forceinline__ Fq fq_qb(const Fq& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ Fq fq_pick(int q, const Fq& a0, const Fq& a1, const Fq& a2, const Fq& a3) {
+  return q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
+}
+
+__global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint32_t total, uint32_t proof_len,
+                                                       uint32_t cons_len, uint32_t instance_len,
+                                                       const Fq* __restrict__ Ap, const Fq* __restrict__ Aq,
+                                                       const Fq* __restrict__ Ax, const Fq* __restrict__ B,
+                                                       const Fq* __restrict__ C, const Fq* __restrict__ D,
+                                                       Fq* __restrict__ partials, unsigned* __restrict__ counter,
+                                                       uint32_t* __restrict__ mb, uint32_t seq) {
+  const int q = threadIdx.x & 3;
+  Fq acc = fq_zero();
+  for (uint32_t t = blockIdx.x * 64 + (threadIdx.x >> 2); t < total; t += gridDim.x * 64) {  // uniform per quad
+    int p = find_inst(a, t);
+    const PqxInst& d = pinst(a, p);
+    uint32_t loc = t - d.dom_off;
+    uint32_t qq = loc / d.sc_ni, x = loc % d.sc_ni;
+    size_t base = pqx_off(d) + (size_t)qq * d.anw * d.ani + x;
+    bool zero_hi;
+    size_t hi;
+    if (mode == MODE_X) {
+      zero_hi = d.ni == 1;
+      hi = base + d.ni / 2;
+    } else if (mode == MODE_Q) {
+      zero_hi = d.np == 1;
+      hi = base + (size_t)(d.np / 2) * d.anw * d.ani;
+    } else {
+      int ph = p + a.ninst / 2;
+      zero_hi = ph >= a.zlen;
+      hi = zero_hi ? 0 : pqx_off(pinst(a, ph)) + (size_t)qq * pinst(a, ph).anw * pinst(a, ph).ani + x;
+    }
+    const Fq b_lo = B[base], c_lo = C[base], d_lo = D[base];
+    const Fq b_hi = zero_hi ? fq_zero() : B[hi], c_hi = zero_hi ? fq_zero() : C[hi], d_hi = zero_hi ? fq_zero() : D[hi];
+    const Fq b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo), d2 = fq_sub(fq_dbl(d_hi), d_lo);
+    const Fq b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
+    const uint32_t iq = qq * d.step_q, ix = x * d.step_x;
+    // level 1: lane 0 Ap Aq (lo), lane 1 the hi eq prefix (modes P / Q) or b3 c3 (mode X), lane 2 b c, lane 3 b2 c2
+    Fq u1, v1;
+    if (q == 0) {
+      u1 = Ap[p];
+      v1 = Aq[iq];
+    } else if (q == 1) {
+      if (mode == MODE_X) {
+        u1 = b3;
+        v1 = c3;
+      } else {
+        u1 = mode == MODE_P ? Ap[p + instance_len] : Ap[p];
+        v1 = mode == MODE_P ? Aq[iq] : Aq[iq + proof_len];
+      }
+    } else {
+      u1 = q == 2 ? b_lo : b2;
+      v1 = q == 2 ? c_lo : c2;
+    }
+    const Fq r1 = fq_mul(u1, v1);
+    const Fq apq = fq_qb<0>(r1), r1_1 = fq_qb<1>(r1), bc_lo = fq_qb<2>(r1), bc2 = fq_qb<3>(r1);
+    // level 2: lane 0 a_lo = apq Ax[x], lane 1 a_hi, lane 2 b3 c3 (modes P / Q)
+    const Fq u2 = q == 1 && mode != MODE_X ? r1_1 : (q == 2 ? b3 : apq);
+    const Fq v2 = q == 2 ? c3 : (q == 1 && mode == MODE_X ? Ax[ix + cons_len] : Ax[ix]);
+    const Fq r2 = fq_mul(u2, v2);
+    const Fq a_lo = fq_qb<0>(r2), a_hi = fq_qb<1>(r2);
+    const Fq bc3 = mode == MODE_X ? r1_1 : fq_qb<2>(r2);
+    // level 3: lane 0 e0 = a (b c - d) at X = 0, lane 1 at X = 2, lane 2 at X = 3
+    const Fq a2 = fq_sub(fq_dbl(a_hi), a_lo), a3 = fq_sub(fq_add(a2, a_hi), a_lo);
+    const Fq u3 = fq_pick(q, a_lo, a2, a3, a_lo);
+    const Fq v3 = fq_pick(q, fq_sub(bc_lo, d_lo), fq_sub(bc2, d2), fq_sub(bc3, d3), fq_sub(bc_lo, d_lo));
+    acc = fq_add(acc, fq_mul(u3, v3));
+  }
+  const Fq z = fq_zero();
+  grid_reduce3(q == 0 ? acc : z, q == 1 ? acc : z, q == 2 ? acc : z, partials, counter, mb, seq);
+}
+
+__global__ void __launch_bounds__(256) k_phase2_eval_q(PqxArgs ab, PqxArgs zz, int mode, uint32_t total,
+                                                       bool single, uint32_t instance_len, const Fq* __restrict__ eq,
+                                                       const Fq* __restrict__ B, const Fq* __restrict__ C,
+                                                       Fq* __restrict__ partials, unsigned* __restrict__ counter,
+                                                       uint32_t* __restrict__ mb, uint32_t seq);
+
 // ---------------------------------------------------------------- phase 2 round evaluation
 // domain: p < Pd, w < W, y < sc_ni[p] ; B = ABC table (instance pi = single ? 0 : p), C = Z table
 __device__ __forceinline__ Fq pqx_get(const PqxArgs& a, const Fq* T, int p, uint32_t w, uint32_t y) {
@@ -294,6 +384,33 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
     e3 = fq_add(e3, fq_mul(fq_mul(a3, b3), c3));
   }
   grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
+}
+
+// quad form of k_phase2_eval: lane 0 / 1 / 2 forms the point's product at X = 0 / 2 / 3 as (a b) c, two levels
+__global__ void __launch_bounds__(256) k_phase2_eval_q(PqxArgs ab, PqxArgs zz, int mode, uint32_t total,
+                                                       bool single, uint32_t instance_len, const Fq* __restrict__ eq,
+                                                       const Fq* __restrict__ B, const Fq* __restrict__ C,
+                                                       Fq* __restrict__ partials, unsigned* __restrict__ counter,
+                                                       uint32_t* __restrict__ mb, uint32_t seq) {
+  const int q = threadIdx.x & 3;
+  Fq acc = fq_zero();
+  for (uint32_t t = blockIdx.x * 64 + (threadIdx.x >> 2); t < total; t += gridDim.x * 64) {  // uniform per quad
+    int p = find_inst(zz, t);
+    uint32_t loc = t - pinst(zz, p).dom_off;
+    uint32_t ny = pinst(zz, p).sc_ni;
+    uint32_t w = loc / ny, y = loc % ny;
+    int pi = single ? 0 : p;
+    const Fq a_lo = eq[p];
+    const Fq a_hi = mode == MODE_P ? eq[p + instance_len] : a_lo;
+    const Fq b_lo = pqx_get(ab, B, pi, w, y), c_lo = pqx_get(zz, C, p, w, y);
+    const Fq b_hi = pqx_get_high(ab, B, pi, w, y, mode), c_hi = pqx_get_high(zz, C, p, w, y, mode);
+    const Fq a2 = fq_sub(fq_dbl(a_hi), a_lo), b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo);
+    const Fq a3 = fq_sub(fq_add(a2, a_hi), a_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo);
+    const Fq ab_ = fq_mul(fq_pick(q, a_lo, a2, a3, a_lo), fq_pick(q, b_lo, b2, b3, b_lo));
+    acc = fq_add(acc, fq_mul(ab_, fq_pick(q, c_lo, c2, c3, c_lo)));
+  }
+  const Fq z = fq_zero();
+  grid_reduce3(q == 0 ? acc : z, q == 1 ? acc : z, q == 2 ? acc : z, partials, counter, mb, seq);
 }
 
 // ---------------------------------------------------------------- Pqx folds (custom_dense_mlpoly.rs:205-289)
@@ -379,6 +496,12 @@ __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, co
 }
 
 // ---------------------------------------------------------------- host launchers
+// round evaluations over at most this many domain points take the quad form (SPG_SC_QUAD_MAX; 0 = never): below it
+// the chip is not full and a point's chain of products sets the time
+static size_t sc_quad_max() {
+  static const size_t m = getenv("SPG_SC_QUAD_MAX") ? (size_t)atol(getenv("SPG_SC_QUAD_MAX")) : ((size_t)1 << 16);
+  return m;
+}
 static int grid_for(uint32_t total) {
   int nb = (int)((total + 255) / 256);
   if (nb > 1024) nb = 1024;
@@ -502,13 +625,14 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
   }
   if (dom >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "phase-1 domain too large");
   if (int rc = pqx_pack(ctx, v, a, kWsPqxA)) return rc;
-  int nb = grid_for((uint32_t)dom);
+  const bool quad = dom <= sc_quad_max();
+  const int nb = quad ? grid_for((uint32_t)(4 * dom)) : grid_for((uint32_t)dom);
   {
     // B, C, D lo+hi per domain point, plus the three eq factor tables once
     KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len));
-    hipLaunchKernelGGL(k_phase1_eval, dim3(nb), dim3(256), 0, ctx->stream, a, mode, (uint32_t)dom,
-                       (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq, Ax, B, C, D,
-                       partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
+    hipLaunchKernelGGL(quad ? k_phase1_eval_q : k_phase1_eval, dim3(nb), dim3(256), 0, ctx->stream, a, mode,
+                       (uint32_t)dom, (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq, Ax, B,
+                       C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
   }
   SPG_HIP(ctx, hipGetLastError());
   return eval_reduce_finish(ctx, out3);
@@ -534,11 +658,17 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
   }
   if (int rc = pqx_pack(ctx, vab, ab, kWsPqxA)) return rc;
   if (int rc = pqx_pack(ctx, vz, zz, kWsPqxB)) return rc;
-  int nb = grid_for((uint32_t)dom);
+  const bool quad = dom <= sc_quad_max();
+  const int nb = quad ? grid_for((uint32_t)(4 * dom)) : grid_for((uint32_t)dom);
   {
     KScope ks(ctx, "sc_phase2_eval", 128.0 * dom);  // ABC and Z, lo+hi per domain point
-    hipLaunchKernelGGL(k_phase2_eval, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, (int)W,
-                       single, (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
+    if (quad)
+      hipLaunchKernelGGL(k_phase2_eval_q, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, single,
+                         (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
+    else
+      hipLaunchKernelGGL(k_phase2_eval, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, (int)W,
+                         single, (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, ctx->d_mbox,
+                         ++ctx->mbox_seq);
   }
   SPG_HIP(ctx, hipGetLastError());
   return eval_reduce_finish(ctx, out3);

@@ -87,6 +87,32 @@ def test_circ_program_on_gpu(ctx, vars_gens, tmp_path, case):
     assert hashlib.sha256(proof).hexdigest() == golden["proof_sha256"]
 
 
+@pytest.mark.parametrize("quad_max", ["0", "1099511627776"])
+def test_sumcheck_eval_forms(quad_max):
+    """the R1CSProof round evaluations in the one-thread-per-point form everywhere (SPG_SC_QUAD_MAX=0) or in the
+    quad form everywhere (2^40): the same bytes as the golden proof (the default mixes them by round size)"""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    case = "mem_both_b3_x64_q2"
+    code = (
+        "import sys, hashlib; sys.path[:0] = [%r, %r]\n"
+        "import spg, workload\n"
+        "from r1cs_cases import SNARK_CASES\n"
+        "from test_gpu_snark import gpu_snark, GENS_LABEL, GENS_NV\n"
+        "ctx = spg.Context(0)\n"
+        "g = spg.R1CSGens(ctx, GENS_LABEL, GENS_NV)\n"
+        "(p,) = gpu_snark(ctx, g, workload.SnarkWorkload(**SNARK_CASES[%r]), workload.tape_seed())\n"
+        "print(hashlib.sha256(p).hexdigest())\n"
+    ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "tests"), case)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_SC_QUAD_MAX=quad_max),
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    golden = json.load(open(os.path.join(G, "snark_proofs.json")))[case]
+    assert out.stdout.split()[-1] == golden["proof_sha256"]
+
+
 @pytest.mark.parametrize("host_max,comb", [("0", "1"), ("0", "0"), ("4096", "1")])
 def test_bullet_paths(host_max, comb):
     """every DotProductProofLog through the device Bullet rounds (SPG_BULLET_HOST_MAX=0) -- in the comb form
