@@ -23,6 +23,8 @@
 #include <atomic>
 
 #include "ctx.hpp"
+#include "hcurve.hpp"
+#include "hpool.hpp"
 #include "lds.hpp"
 #include "quad.hpp"
 
@@ -35,7 +37,14 @@ static int comb_c() {
   return c;
 }
 static constexpr int kCombRun = 64;                 // multiples per build lane
-static constexpr size_t kCombMaxR = 16384;          // widest row the comb covers (70 GB of table at c = 12)
+static constexpr size_t kCombMaxR = 65536;          // most generators a table covers
+static constexpr size_t kCombWide = 16384;          // tables past this many generators take the narrow window
+// wider tables take c = 9 (SPG_COMB_C_WIDE: 9 or 10): 2^16 generators are 29 x 65537 x 256 x 96 B = 47 GB, where
+// c = 12 would need 283 GB
+static int comb_c_for(size_t slots) {
+  static const int cw = getenv("SPG_COMB_C_WIDE") ? std::max(9, std::min(10, atoi(getenv("SPG_COMB_C_WIDE")))) : 9;
+  return slots > kCombWide ? cw : comb_c();
+}
 
 // lane L = ((w * NS + s) * runs + k): multiples k * Run + 1 .. (k + 1) * Run of 2^(c w) G_gen, gen = s (s < NS - 1)
 // or hgen (s = NS - 1)
@@ -211,7 +220,7 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   while (cn < need) cn *= 2;
   cn = std::min(cn, g->n);
   if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
-  const int NS = (int)cn + 1, C = comb_c();
+  const int NS = (int)cn + 1, C = comb_c_for(cn);
   const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
   static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 96.0) * (1ull << 30);
   if (g_comb_bytes.load() + bytes > cap) return 1;
@@ -231,7 +240,9 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   }
   const dim3 gb((unsigned)((chunk + 63) / 64)), tb(64);
   for (size_t l0 = 0; l0 < lanes; l0 += chunk) {
-    if (C == 10)
+    if (C == 9)
+      hipLaunchKernelGGL(k_comb_build<9>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+    else if (C == 10)
       hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
     else if (C == 11)
       hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
@@ -246,7 +257,7 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
     return set_err(ctx, SPG_E_HIP, "comb table build");
   }
   if (cur.p) g->comb_retired.push_back(cur);
-  g->comb = spg_gens::Comb{comb, cn, bytes, hgen};
+  g->comb = spg_gens::Comb{comb, cn, bytes, hgen, C};
   g_comb_bytes += bytes;
   *use = g->comb;
   return 0;
@@ -281,7 +292,7 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
     if (!part) return set_err(ctx, SPG_E_NOMEM, "comb parts");
   }
   {
-    const int C = comb_c();
+    const int C = cb.c;
     KScope ks(ctx, "msm_comb", 0.0, (double)B * per * (253 / C + 1) * (1.0 - 1.0 / (double)(1 << C)));
     const dim3 ga((unsigned)(B * S)), ta(256);
     const int NS = (int)cb.slots + 1;
@@ -290,6 +301,9 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
                      cb.p, NS, (int)S, part)
     const int key = C * 8 + (int)G;
     switch (key) {
+      case 9 * 8 + 1: SPG_COMB_LAUNCH(9, 1); break;
+      case 9 * 8 + 2: SPG_COMB_LAUNCH(9, 2); break;
+      case 9 * 8 + 4: SPG_COMB_LAUNCH(9, 4); break;
       case 10 * 8 + 1: SPG_COMB_LAUNCH(10, 1); break;
       case 10 * 8 + 2: SPG_COMB_LAUNCH(10, 2); break;
       case 10 * 8 + 4: SPG_COMB_LAUNCH(10, 4); break;
@@ -308,6 +322,62 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
   if (d_out) return compress_ext_device(ctx, ext, B, d_out);
   SPG_HIP(ctx, hipGetLastError());
   return SPG_OK;
+}
+
+// One large MSM from the comb table: the rows kernel with B = 1 and S workgroups, whose S partial points go to mapped
+// host memory and are added on the host pool (k_comb_join would add them on one quad, a chain of S additions)
+int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
+                    const Fq* d_blind, h::HExt* out) {
+  spg_gens::Comb cb;
+  const int rc = comb_ensure(ctx, g, gen_offset + n, d_blind ? (int)g->n : -1, &cb);
+  if (rc) return rc;
+  const size_t per = n + (d_blind ? 1 : 0);
+  // window groups per scalar (a lane's chain is W / G mixed additions) and workgroups: ~4 waves per SIMD
+  static const size_t gsel = getenv("SPG_BIG_COMB_G") ? (size_t)atol(getenv("SPG_BIG_COMB_G")) : 4;
+  const size_t G = gsel == 1 || gsel == 2 ? gsel : 4, spw = 256 / G;
+  const size_t S = std::max<size_t>(1, (per + spw - 1) / spw);
+  void* d_map = nullptr;
+  Ext* parts = (Ext*)mapped_get(ctx, S * sizeof(Ext), &d_map);
+  if (!parts) return 1;
+  const int C = cb.c, NS = (int)cb.slots + 1;
+  {
+    KScope ks(ctx, "msm_comb_single", 0.0, (double)per * (253 / C + 1) * (1.0 - 1.0 / (double)(1 << C)));
+    const dim3 ga((unsigned)S), ta(256);
+#define SPG_CS(CC, GG)                                                                                          \
+  hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blind, (int)n, (int)gen_offset, \
+                     cb.p, NS, (int)S, (Ext*)d_map)
+    const int key = C * 8 + (int)G;
+    switch (key) {
+      case 9 * 8 + 1: SPG_CS(9, 1); break;
+      case 9 * 8 + 2: SPG_CS(9, 2); break;
+      case 9 * 8 + 4: SPG_CS(9, 4); break;
+      case 10 * 8 + 1: SPG_CS(10, 1); break;
+      case 10 * 8 + 2: SPG_CS(10, 2); break;
+      case 10 * 8 + 4: SPG_CS(10, 4); break;
+      case 11 * 8 + 1: SPG_CS(11, 1); break;
+      case 11 * 8 + 2: SPG_CS(11, 2); break;
+      case 11 * 8 + 4: SPG_CS(11, 4); break;
+      case 12 * 8 + 1: SPG_CS(12, 1); break;
+      case 12 * 8 + 2: SPG_CS(12, 2); break;
+      default: SPG_CS(12, 4); break;
+    }
+#undef SPG_CS
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // the S parts over the pool: contiguous chunks, then their sums on this thread
+  const int K = (int)std::max<size_t>(1, std::min<size_t>(S / 16, (size_t)pool().size() + 1));
+  std::vector<h::HExt> part(K);
+  pool().parallel_for(K, [&](int c) {
+    const size_t lo = S * c / K, hi = S * (c + 1) / K;
+    h::HExt acc = h::hext_from_dev(parts[lo]);
+    for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(parts[i]));
+    part[c] = acc;
+  });
+  h::HExt sum = part[0];
+  for (int c = 1; c < K; c++) sum = h::hext_add(sum, part[c]);
+  *out = sum;
+  return 0;
 }
 
 }  // namespace spg

@@ -102,6 +102,7 @@ struct spg_gens {
     spg::Niels* p = nullptr;
     size_t slots = 0, bytes = 0;
     int h = -1;
+    int c = 12;  // window width: 253 / c + 1 windows of 2^(c-1) multiples per generator
   };
   mutable std::mutex comb_mu;
   mutable Comb comb;

@@ -646,6 +646,7 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   spg_gens::Comb cb;
   const int rc = comb_get(ctx, g, gmax, &cb);
   if (rc) return rc == 1 ? 1 : rc;
+  if (cb.c != 12) return 1;  // the kernels take 12-bit windows
   int G, BS, R;
   bullet_comb_shape(n / 2, &G, &BS, &R);
   const int S = BS / 4, quads = (n / 2) * G, wgs = (quads + S - 1) / S;
@@ -682,6 +683,7 @@ int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const u
   spg_gens::Comb cb;
   const int rc = comb_get(ctx, g, gmax, &cb);
   if (rc) return rc == 1 ? 1 : rc;
+  if (cb.c != 12) return 1;
   int G, BS, R;
   bullet_comb_shape(std::max(2, n), &G, &BS, &R);
   const int S = BS / 4, wgs = (n * G + S - 1) / S;

@@ -385,9 +385,20 @@ int launch_big(spg_ctx* ctx, const spg_gens* g, BigArgs a, Ext* host_groups_dev,
 
 }  // namespace
 
+// comb.hip: the same sum from g's comb table (h = generator g->n), summed on the host; 1 when the comb does not apply
+int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
+                    const Fq* d_blind, h::HExt* out);
+
 // sum_i s_i G[gen_offset + i] (+ blind h) of n device scalars, into *out (host point)
 int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
                    const Fq* d_blind, h::HExt* out) {
+  // large MSMs over a generator set that can keep a comb table (comb.hip; <= 2^16 generators, 47 GB at c = 9):
+  // no digit sort and no bucket reduction (SPG_BIG_COMB=0: always the bucket pipeline below)
+  static const bool comb_on = !getenv("SPG_BIG_COMB") || atoi(getenv("SPG_BIG_COMB")) != 0;
+  if (comb_on && n >= ((size_t)1 << 14)) {
+    const int rc = msm_single_comb(ctx, g, gen_offset, d_scalars, n, d_blind, out);
+    if (rc != 1) return rc;
+  }
   const int c = big_window();
   const int per = (int)n + (d_blind ? 1 : 0);
   SPG_CHECK(ctx, n >= 1 && (size_t)per * (253 / c + 1) < 0x7fffffffULL, "msm too large");

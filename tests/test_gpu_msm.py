@@ -188,7 +188,8 @@ def gens_big(ctx):
 
 
 def test_msm_big_edge_and_skew(ctx, oracle, gens_big):
-    """one MSM larger than the latency path (msm_big.hip): edge scalars, an all-zero stretch, a bucket holding most
+    """one MSM larger than the latency path (msm_big.hip; >= 2^14 points: from the comb table, comb.hip
+    msm_single_comb): edge scalars, an all-zero stretch, a bucket holding most
     entries (one scalar repeated: its digits pile into a few buckets, which split into many chunks), a blind, and
     a generator offset, against the oracle"""
     n = 20000
@@ -216,7 +217,8 @@ def test_msm_big_edge_and_skew(ctx, oracle, gens_big):
 
 @pytest.mark.parametrize("c", ["8", "10", "13", "14"])
 def test_msm_big_windows(oracle, c):
-    """every window width of the large-MSM path (SPG_BIG_C, a fresh process reads it) gives the oracle's 2^16 MSM"""
+    """every window width of the large-MSM bucket path (SPG_BIG_C with SPG_BIG_COMB=0, a fresh process reads them)
+    gives the oracle's 2^16 MSM (the default takes the comb table for MSMs of >= 2^14 points)"""
     import subprocess
     import sys
 
@@ -231,8 +233,8 @@ def test_msm_big_windows(oracle, c):
         "s = pyoracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * %d, dtype=np.uint8).tobytes())\n"
         "print(g.msm(s).hex())\n"
     ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "oracle"), n, c, n)
-    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_C=c), capture_output=True,
-                         text=True, timeout=240)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_C=c, SPG_BIG_COMB="0"),
+                         capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     rng = np.random.default_rng(int(c))
     s = rand_fq(oracle, rng, n)
@@ -281,8 +283,8 @@ def test_msm_big_accumulation_forms(oracle, form):
         "s[: %d // 2] = s[0]\n"  # half the scalars equal: every window's digit repeats (one bucket per window)
         "print(g.msm(s).hex())\n"
     ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "oracle"), n, n, n)
-    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_ITEMS=form), capture_output=True,
-                         text=True, timeout=240)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_ITEMS=form, SPG_BIG_COMB="0"),
+                         capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     rng = np.random.default_rng(5)
     s = rand_fq(oracle, rng, n)
