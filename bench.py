@@ -26,7 +26,7 @@ mixed additions, one per nonzero signed window digit) against the measured whole
 algorithmic HBM bytes against 8 TB/s; `roofline_hbm` / `roofline_valu` give the largest kernel of each kind.
 Per-launch times are libspg's HIP events on its context stream (spg_prof_read2) in a profiling pass after the
 timed steps; `traffic` is the PMC-measured HBM bytes per launch from the committed rocprofv3 summary of the same
-workload (TRAFFIC below: scripts/gpu_profile.sh, scripts/gpu_r03y.sh). `device_busy_ms_per_step` is the union of
+workload (TRAFFIC below: scripts/gpu_run.sh PMC=1, session r03y). `device_busy_ms_per_step` is the union of
 the timed intervals, since kernels on the context's second stream overlap those of the main one.
 `cpu_baseline` is the C++ CPU restatement of the reference (oracle/) on rank 0 at N = 1: one thread on the full
 workload, and `cpu_baseline_all_cores` the same work run as one independent prove per usable host core at once.

@@ -263,7 +263,7 @@ struct HostGens {
     // The table entry of a unit depends only on the scalar byte, not on the running sum, so the entry kPf units
     // ahead is prefetched while this one is added: a small DotProductProofLog's rounds read ~1000 random entries of
     // ~1 MB tables per generator, which mostly miss the caches (host-path proofs 1.63 -> 0.98 ms per SNARK::prove in
-    // situ, scripts/gpu_r03zm.sh; a standalone micro with warm tables showed no gain). SPG_HOST_PREFETCH=0: off.
+    // situ, session r03zm; a standalone micro with warm tables showed no gain). SPG_HOST_PREFETCH=0: off.
     static const size_t kPf = getenv("SPG_HOST_PREFETCH") ? (size_t)atol(getenv("SPG_HOST_PREFETCH")) : 3;
     pool().parallel_for((int)S, [&](int si) {
       const size_t s = (size_t)si, u0 = slice_lo(s), u1 = slice_lo(s + 1);

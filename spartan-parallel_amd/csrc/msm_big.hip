@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(kBigBS, 4) k_big_accum(const Chunk* __restrict
 }
 
 int big_window() {
-  // c = 11 (1024 buckets, 24 windows): measured best for 2^16 points against 12 and 13 (scripts/gpu_r03d.sh); a
+  // c = 11 (1024 buckets, 24 windows): measured best for 2^16 points against 12 and 13 (session r03d); a
   // smaller bucket set shortens the group reductions at the end more than its extra windows cost
   static const int c = getenv("SPG_BIG_C") ? atoi(getenv("SPG_BIG_C")) : 11;
   return c < 8 ? 8 : (c > 14 ? 14 : c);
