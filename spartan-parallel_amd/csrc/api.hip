@@ -137,6 +137,11 @@ int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n) {
   return 0;
 }
 
+void down_post(spg_ctx* ctx, uint32_t seq, const Fq& r) {
+  for (int i = 0; i < 8; i++) ctx->down[8 + i] = r.l[i];
+  __atomic_store_n(ctx->down, seq, __ATOMIC_RELEASE);
+}
+
 struct SegArgs {
   const Fq* p[kSegMax];
   uint32_t off[kSegMax + 1];
@@ -364,15 +369,17 @@ extern "C" int spg_init(int device, spg_ctx** out) {
     return SPG_E_HIP;
   }
   void* mb = nullptr;
-  if (hipHostMalloc(&mb, 2 * spg::kMboxBytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+  if (hipHostMalloc(&mb, 2 * spg::kMboxBytes + 4096, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_mbox, mb, 0) != hipSuccess) {
     delete c;
     return SPG_E_HIP;
   }
-  memset(mb, 0, 2 * spg::kMboxBytes);
+  memset(mb, 0, 2 * spg::kMboxBytes + 4096);
   c->mbox = (volatile uint32_t*)mb;
   c->res = (spg::Fq*)((uint8_t*)mb + spg::kMboxBytes);
   c->d_res = (spg::Fq*)((uint8_t*)c->d_mbox + spg::kMboxBytes);
+  c->down = (volatile uint32_t*)((uint8_t*)mb + 2 * spg::kMboxBytes);
+  c->d_down = (uint32_t*)((uint8_t*)c->d_mbox + 2 * spg::kMboxBytes);
   *out = c;
   return SPG_OK;
 }

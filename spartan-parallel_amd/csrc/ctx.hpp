@@ -37,6 +37,11 @@ struct spg_ctx {
   volatile uint32_t* mbox = nullptr;
   uint32_t* d_mbox = nullptr;
   uint32_t mbox_seq = 0;
+  // the reverse direction (coherent, mapped host memory after the result page): the host answers a persistent
+  // kernel's posted round with the round's challenge and the round's sequence number (spg::down_post); the kernel's
+  // workgroups poll word 0 (layer.hpp, k_layer_persist)
+  volatile uint32_t* down = nullptr;
+  uint32_t* d_down = nullptr;
   // result page (coherent, mapped host memory next to the mailbox): d2h_multi's gather kernel writes the
   // scalars the host needs there, so a download is one small kernel + a stream synchronisation, no blit copy
   spg::Fq* res = nullptr;
@@ -216,6 +221,9 @@ inline int d2h_multi(spg_ctx* ctx, std::initializer_list<FqSeg> segs, Fq* h) {
 }
 // waits (spinning, bounded) until the mailbox carries sequence number `seq`, then copies n scalars out
 int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n);
+// the host's answer to a persistent kernel: r in words 8..15, then (x86 stores are ordered) seq in word 0
+static const uint32_t kDownAbort = 0xffffffffu;
+void down_post(spg_ctx* ctx, uint32_t seq, const Fq& r);
 
 // device side of the mailbox: the scalars, then (after a system-scope release fence) the sequence number
 __device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* v, int n) {

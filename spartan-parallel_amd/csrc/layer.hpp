@@ -337,6 +337,173 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   }
 }
 
+// ---- persistent form: the remaining rounds of a layer in one launch ------------------------------------------------
+// A launched round costs a host launch (~4 us) and a doorbell-to-first-wave delay (~5 us) on top of its work, and the
+// layer rounds are transcript-sequential. Here the workgroups stay resident over the rounds: after posting round k's
+// (e0, e2, e3) they wait for the host's answer in the downbox (coherent host memory: the round's challenge, then its
+// mailbox sequence number), fold with it and go on. Entries written in one round are read by other workgroups in the
+// next, so every access to the vectors inside the launch is an `sc1` access (agent-scope relaxed atomics: L1 bypassed,
+// written through) and each workgroup drains its stores before its ticket (MI355X_MICROARCH hand-off table, row 1;
+// the host's answer comes only after the last ticket). The layer's last round posts every vector's two entries from
+// the workgroup that takes the last ticket, so the host folds the final claims itself. Every wave leaves the loop on
+// the last round, on the host's abort word, or after `timeout` ticks without an answer.
+typedef __attribute__((address_space(1))) uint64_t gu64;  // global (not flat) accesses: the sc1 hand-off needs them
+__device__ __forceinline__ Fq ld_sc1(const Fq* p) {
+  Fq r;
+  gu64* w = (gu64*)p;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t v = __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.l[2 * i] = (uint32_t)v;
+    r.l[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+  return r;
+}
+__device__ __forceinline__ void st_sc1(Fq* p, const Fq& v) {
+  gu64* w = (gu64*)p;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    __hip_atomic_store(w + i, (uint64_t)v.l[2 * i] | ((uint64_t)v.l[2 * i + 1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Fq fold_at_sc1(const Fq* p, int k, int fl, const Fq& r) {
+  const Fq lo = ld_sc1(p + k);
+  return fq_add(lo, fq_mul(r, fq_sub(ld_sc1(p + k + fl), lo)));
+}
+// layer_round_elems with sc1 accesses
+__device__ __forceinline__ Fq layer_round_elems_sc1(const Triple* __restrict__ tr, const Fq* __restrict__ coeff, int nt,
+                                                    int log_len, int do_fold, const Fq& r, const Fq* cin, Fq* cout,
+                                                    long u0, long ustride) {
+  const int q = threadIdx.x & 3, len = 1 << log_len;
+  const int pt = q < 3 ? q : 0;
+  const long total = (long)nt << log_len;
+  Fq e = fq_zero();
+  for (long u = u0; u < total; u += ustride) {
+    const int c = (int)(u >> log_len), i = (int)(u & (len - 1));
+    const Triple x = tr[c];
+    const Fq* Cp = x.C ? x.C : cin;
+    const Fq* src = pt == 0 ? x.A : (pt == 1 ? x.B : Cp);
+    Fq lo, hi;
+    if (do_fold) {
+      const int fl = 2 * len;
+      lo = fold_at_sc1(src, i, fl, r);
+      hi = fold_at_sc1(src, i + len, fl, r);
+      Fq* dst = q == 0 ? x.A : (q == 1 ? x.B : (q == 2 ? (x.C ? x.C : (c == 0 ? cout : nullptr)) : nullptr));
+      if (dst) {
+        st_sc1(dst + i, lo);
+        st_sc1(dst + i + len, hi);
+      }
+    } else {
+      lo = ld_sc1(src + i);
+      hi = ld_sc1(src + i + len);
+    }
+    const Fq al = fq_qbcast<0>(lo), ah = fq_qbcast<0>(hi), bl = fq_qbcast<1>(lo), bh = fq_qbcast<1>(hi);
+    const Fq cl = fq_qbcast<2>(lo), ch = fq_qbcast<2>(hi);
+    const Fq k = coeff[c];
+    e = fq_add(e, fq_mul(fq_mul(fq_mul(line_at(al, ah, pt), line_at(bl, bh, pt)), line_at(cl, ch, pt)), k));
+  }
+  return e;
+}
+struct PersistArgs {
+  const Triple* tr;
+  const Fq* coeff;
+  int nt;
+  int rounds;        // rounds in this launch: round k works on vectors of half length 2^(rounds - 1 - k)
+  int do_fold;       // the first round applies the fold pending from the round before the launch
+  Fq r;              // ... with this challenge
+  Fq* cb[2];         // the shared eq vector's ping-pong pair; cb[cur] holds it
+  int cur;
+  Fq* partials;
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq0;     // mailbox sequence number of round 0 (round k: seq0 + k)
+  uint32_t* down;    // the host's answers
+  int ends;          // the last round posts every vector's two entries after the sums (3 + 6 nt scalars)
+  unsigned long long timeout;  // wall_clock64 ticks a workgroup waits for an answer before it gives up
+};
+static const uint32_t kDownAbortDev = 0xffffffffu;  // = kDownAbort (ctx.hpp)
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_persist(PersistArgs A) {
+  __shared__ bool last;
+  __shared__ uint32_t rsh[9];
+  const int t = threadIdx.x, q = t & 3;
+  int do_fold = A.do_fold, cur = A.cur;
+  Fq r = A.r;
+  for (int k = 0; k < A.rounds; k++) {
+    const int lg = A.rounds - 1 - k;
+    const uint32_t seq = A.seq0 + (uint32_t)k;
+    Fq* cin = A.cb[cur];
+    Fq* cout = A.cb[cur ^ 1];
+    Fq e = layer_round_elems_sc1(A.tr, A.coeff, A.nt, lg, do_fold, r, cin, cout, ((long)blockIdx.x * BS + t) >> 2,
+                                 (long)gridDim.x * (BS / 4));
+    if (do_fold) cur ^= 1;
+    quad_block_sum<BS>(e);
+    if (t < 3)
+      for (int j = 0; j < 8; j++)
+        __hip_atomic_store(&A.partials[3 * blockIdx.x + t].l[j], e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its vector and partial stores are out
+    __syncthreads();
+    if (t == 0)
+      last = __hip_atomic_fetch_add(A.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (last) {
+      Fq a = fq_zero();
+      if (q < 3)
+        for (unsigned j = t >> 2; j < gridDim.x; j += BS / 4) {
+          Fq o;
+          for (int i = 0; i < 8; i++)
+            o.l[i] = __hip_atomic_load(&A.partials[3 * j + q].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          a = fq_add(a, o);
+        }
+      quad_block_sum<BS>(a);
+      if (lg == 0 && A.ends) {  // every vector's entries 0 and 1 (this round's folded values; C in cb[cur])
+        for (int u = t; u < 3 * A.nt; u += BS) {
+          const int c = u / 3, p = u % 3;
+          const Triple x = A.tr[c];
+          const Fq* v = p == 0 ? x.A : (p == 1 ? x.B : (x.C ? x.C : A.cb[cur]));
+          const Fq lo = ld_sc1(v), hi = ld_sc1(v + 1);
+          uint32_t* d = A.mb + 8 + 8 * (3 + 6 * c + 2 * p);
+          for (int j = 0; j < 8; j++) {
+            __hip_atomic_store(d + j, lo.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(d + 8 + j, hi.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+      }
+      if (t < 3)
+        for (int j = 0; j < 8; j++) __hip_atomic_store(A.mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __syncthreads();
+      if (t == 0) {
+        __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ticket is re-armed before the host can answer
+        __hip_atomic_store(A.mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (lg == 0) return;  // the layer's last round: nothing to wait for
+    if (t == 0) {  // one lane per workgroup polls the downbox
+      const unsigned long long t0 = wall_clock64();
+      uint32_t v;
+      uint32_t ok = 1;
+      while ((v = __hip_atomic_load(A.down, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != seq) {
+        if (v == kDownAbortDev || wall_clock64() - t0 > A.timeout) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the challenge is read after the matching sequence number
+      if (ok)
+        for (int i = 0; i < 8; i++) rsh[i] = __hip_atomic_load(A.down + 8 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      rsh[8] = ok;
+    }
+    __syncthreads();
+    if (!rsh[8]) return;
+    for (int i = 0; i < 8; i++) r.l[i] = rsh[i];
+    do_fold = 1;
+    __syncthreads();  // rsh and `last` are rewritten in the next round
+  }
+}
+
 // ---- big rounds: one thread per index i over every product circuit (throughput form) -----------------------------
 // Triples 0 .. np-1 share the eq vector C (cin -> cout); since e_X = sum_i C_i(X) sum_c k_c A_c(X) B_c(X), the
 // thread for index i folds C once, then per circuit folds A and B, scales A's two entries by k_c and adds the three

@@ -23,6 +23,7 @@ struct PqxInst {
   uint32_t dom_off;          // offset of this instance in a kernel's flattened domain
   uint32_t sc_np, sc_ni;     // sumcheck-local sizes for the round (already halved)
   uint32_t step_q, step_x;   // proof_len / sc_np, cons_len / sc_ni (phase 1)
+  uint32_t fstride;          // fused fold + eval: element stride to the pending fold's partner (0: scale by 1 - r)
 };
 
 struct PqxArgs {

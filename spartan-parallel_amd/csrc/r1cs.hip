@@ -369,8 +369,14 @@ struct ZKRounds {
 // workspace slots used here (msm.hip uses 0..12, proto.hip 20..22)
 enum {
   WS_AZ = 30, WS_BZ, WS_CZ, WS_Z, WS_ABC, WS_TP, WS_TQ, WS_TX, WS_EQRX, WS_EQP, WS_PART, WS_OUT3, WS_DESC,
-  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2
+  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2, WS_TQ2, WS_TX2
 };
+// phase-1 rounds in modes x and q fold inside the next round's evaluation (sumcheck.hip, FOLD kernels); SPG_SC_FUSE=0
+// restores the separate fold launch
+static bool sc_fuse_on() {
+  static const bool on = !getenv("SPG_SC_FUSE") || atoi(getenv("SPG_SC_FUSE")) != 0;
+  return on;
+}
 
 struct Prover {
   spg_ctx* ctx;
@@ -717,7 +723,7 @@ int Prover::run_inner(Laps& lp) {
     const Fq* Ap_l = Ap + p0;  // eq(tau_p) indexed by the global instance in the x / q rounds
     // round j's evaluation is enqueued right after round j-1's folds, so it runs on the device while the
     // host finishes round j-1's proof (comm_eval, DotProductProof); eval_wait then collects (e0, e2, e3)
-    auto launch_eval = [&](size_t j) -> int {
+    auto launch_eval = [&](size_t j, const FoldPlan* fold) -> int {
       int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       if (cons_len > 1) cons_len /= 2;
       else if (proof_len > 1) proof_len /= 2;
@@ -732,8 +738,16 @@ int Prover::run_inner(Laps& lp) {
         if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
       }
       return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap_l, Aq, Ax, T->d, TB,
-                         TC, partials, nullptr);
+                         TC, partials, nullptr, fold);
     };
+    // the other halves of the Aq / Ax ping-pong pairs (a fused fold writes the folded side table there)
+    Fq* Aq2 = nullptr;
+    Fq* Ax2 = nullptr;
+    if (sc_fuse_on()) {
+      Aq2 = (Fq*)ws_get(ctx, WS_TQ2, (sizeof(Fq) << nq) + 64);
+      Ax2 = (Fq*)ws_get(ctx, WS_TX2, (sizeof(Fq) << nx) + 64);
+      if (!Aq2 || !Ax2) return set_err(ctx, SPG_E_NOMEM, "eq tables");
+    }
     // before the first instance round: collect every instance's remaining (Az, Bz, Cz) value
     auto to_compact = [&]() -> int {
       std::vector<std::vector<Fq>> full;
@@ -756,7 +770,7 @@ int Prover::run_inner(Laps& lp) {
       return 0;
     };
     if (rounds && nx + nq == 0) rc = to_compact();
-    if (!rc && rounds) rc = launch_eval(0);
+    if (!rc && rounds) rc = launch_eval(0, nullptr);
     if (rc) return rc;
     zk.init(g, tape, rounds, fq_zero(), fq_zero());  // host precomputation while round 0 evaluates
     for (size_t j = 0; j < rounds; j++) {
@@ -769,13 +783,31 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p1_eval");
       Fq r_j = zk.begin(g, t, j, e);
       lp.lap("p1_host");
-      // the round's eq factor is bound in the same launch as Az, Bz, Cz
+      // the round's eq factor is bound in the same launch as Az, Bz, Cz: by the next round's evaluation (fused) when
+      // one follows in mode x or q on the same tables, else by a fold launch of its own
       Fq* side = mode == MODE_P ? Ap : (mode == MODE_Q ? Aq : Ax);
       size_t& side_len = mode == MODE_P ? lenP : (mode == MODE_Q ? lenQ : lenX);
-      rc = pqx_bound(ctx, *T, TB, TC, r_j, mode, side, side_len);
-      side_len /= 2;
-      if (!rc && j + 1 == nx + nq && np > 0) rc = to_compact();
-      if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
+      const bool compact_next = j + 1 == nx + nq && np > 0;
+      const int next_mode = j + 1 < nx ? MODE_X : (j + 1 < nx + nq ? MODE_Q : MODE_P);
+      if (Aq2 && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
+        FoldPlan fp;
+        rc = pqx_fold_plan(ctx, *T, mode, &fp);
+        Fq*& cur = mode == MODE_Q ? Aq : Ax;
+        Fq*& alt = mode == MODE_Q ? Aq2 : Ax2;
+        fp.arg.r = r_j;
+        fp.arg.fmode = mode;
+        fp.arg.side_in = cur;
+        fp.arg.side_out = alt;
+        fp.arg.side_half = (uint32_t)(side_len / 2);
+        std::swap(cur, alt);
+        side_len /= 2;
+        if (!rc) rc = launch_eval(j + 1, &fp);
+      } else {
+        rc = pqx_bound(ctx, *T, TB, TC, r_j, mode, side, side_len);
+        side_len /= 2;
+        if (!rc && compact_next) rc = to_compact();
+        if (!rc && j + 1 < rounds) rc = launch_eval(j + 1, nullptr);
+      }
       if (rc) return rc;
       lp.lap("p1_fold");
       zk.finish(g, t, tape, j, r_j);

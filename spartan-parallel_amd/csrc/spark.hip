@@ -732,9 +732,70 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       lpf.polys.push_back({poly[0], poly[2], poly[3]});
       return r_j;
     };
+    // the remaining log_len rounds of the layer in one persistent launch (layer.hpp, k_layer_persist): the host
+    // answers each posted round through the downbox instead of launching the next one
+    auto run_persist = [&](size_t log_len, bool close_after, FqV* fin) -> int {
+      const int R = (int)log_len;
+      const size_t nt = tr.size();
+      static const size_t max_wgs = getenv("SPG_PERSIST_WGS") ? (size_t)atol(getenv("SPG_PERSIST_WGS")) : 64;
+      const unsigned K = (unsigned)std::max<size_t>(1, std::min<size_t>(((nt << (R - 1)) * 4 + 255) / 256, max_wgs));
+      const bool ends = close_after && 3 + 6 * nt <= kMboxScalars;
+      PersistArgs A;
+      A.tr = dtr;
+      A.coeff = dcoef;
+      A.nt = (int)nt;
+      A.rounds = R;
+      A.do_fold = pending ? 1 : 0;
+      A.r = r_pend;
+      A.cb[0] = cbuf[0];
+      A.cb[1] = cbuf[1];
+      A.cur = cur;
+      A.partials = part;
+      A.counter = ctx->d_counter;
+      A.mb = ctx->d_mbox;
+      A.seq0 = ctx->mbox_seq + 1;
+      A.down = ctx->d_down;
+      A.ends = ends ? 1 : 0;
+      A.timeout = 2000000000ULL;  // 20 s of the 100 MHz wall clock
+      ctx->mbox_seq += (uint32_t)R;
+      ctx->down[0] = 0;  // clear a previous launch's abort word
+      {
+        KScope ks(ctx, "spark_layer_persist");
+        hipLaunchKernelGGL(k_layer_persist<256>, dim3(K), dim3(256), 0, s, A);
+      }
+      const hipError_t le = hipGetLastError();
+      if (le != hipSuccess) return set_err(ctx, SPG_E_HIP, std::string("layer rounds: ") + hipGetErrorString(le));
+      for (int k = 0; k < R; k++) {
+        const bool last_round = k == R - 1;
+        FqV ev(last_round && ends ? 3 + 6 * nt : 3);
+        const int rc2 = mbox_wait(ctx, A.seq0 + (uint32_t)k, ev.data(), (int)ev.size());
+        if (rc2) {
+          if (!last_round) down_post(ctx, kDownAbort, fq_zero());  // every workgroup leaves its wait
+          return rc2;
+        }
+        lp.lap("round_eval_wait");
+        if (pending) cur ^= 1;
+        r_pend = host_round(ev.data());
+        pending = true;
+        lp.lap("round_host");
+        if (!last_round) {
+          down_post(ctx, A.seq0 + (uint32_t)k, r_pend);
+        } else if (ends) {  // bound_poly_var_top of the length-2 vectors, on the host
+          fin->resize(3 * nt);
+          for (size_t c = 0; c < 3 * nt; c++) {
+            const Fq lo = ev[3 + 2 * c], hi = ev[4 + 2 * c];
+            (*fin)[c] = fq_add(lo, fq_mul(r_pend, fq_sub(hi, lo)));
+          }
+          pending = false;
+          return 0;
+        }
+      }
+      return close_after ? close(*fin) : 0;
+    };
     // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks; with
     // close_after the layer's (or the shard's) final entries follow in `fin`
     static const bool ends_on = !getenv("SPG_LAYER_ENDS") || atoi(getenv("SPG_LAYER_ENDS")) != 0;
+    static const bool persist_on = !getenv("SPG_LAYER_PERSIST") || atoi(getenv("SPG_LAYER_PERSIST")) != 0;
     auto run_rounds = [&](size_t log_len, bool local, bool close_after, FqV* fin, int status) -> int {
       if (status) {  // skip mode: the first local round's exchange carries the failure to every rank
         if (!local || log_len == 0) return status;
@@ -742,14 +803,19 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         shared = true;
         return comm_sum_fq(ctx, sh, status, none, 3);
       }
+      static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
+      static const size_t wide_min = getenv("SPG_WIDE_MIN") ? (size_t)atol(getenv("SPG_WIDE_MIN")) : ((size_t)1 << 19);
+      static const size_t persist_max = getenv("SPG_PERSIST_MAX") ? (size_t)atol(getenv("SPG_PERSIST_MAX")) : 4096;
       while (log_len > 0) {
+        const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
+        // every remaining round is a quad round of at most persist_max elements: one persistent launch for them all
+        if (persist_on && quad && !local && (tr.size() << (log_len - 1)) <= persist_max &&
+            ngroups * ((size_t)1 << (log_len - 1)) < wide_min)
+          return run_persist(log_len, close_after, fin);
         log_len--;
         const size_t len = (size_t)1 << log_len;
         unsigned K;
         int BS;
-        static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
-        static const size_t wide_min = getenv("SPG_WIDE_MIN") ? (size_t)atol(getenv("SPG_WIDE_MIN")) : ((size_t)1 << 19);
-        const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
         // algorithmic HBM bytes of the round: per distinct vector (A, B of every triple; the shared C once; each
         // dot-product circuit's own C) and index, 2 entries read, or with the pending fold 4 read + 2 written
         const double layer_bytes = (pending ? 192.0 : 64.0) * (double)len * (double)(2 * tr.size() + ngroups);

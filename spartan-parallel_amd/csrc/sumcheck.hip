@@ -199,28 +199,50 @@ __global__ void k_fold_top(Fq* __restrict__ v, size_t n, Fq r) {
 }
 
 // ---------------------------------------------------------------- phase 1 round evaluation
+// Fused fold + eval (FOLD): the previous round's bound_poly_var_{x,q} of Az, Bz, Cz and of its eq side table is applied
+// by this round's evaluation to exactly the entries it reads. Every live entry of the folded tables is the lo or the hi
+// entry of one domain point, so the thread that reads it folds it (T[s] + r (T[s + fstride] - T[s]), or (1 - r) T[s]
+// for a dimension already of size 1) and writes it back in place; the partner entries lie outside the new live region
+// and nobody writes them. The side table is folded into the other ping-pong buffer (its old entries are read by many
+// points), by a grid-stride pass over its new half. One launch per round instead of two.
+__device__ __forceinline__ Fq fold_read(const Fq* T, size_t s, uint32_t fs, const Fq& r, const Fq& omr) {
+  const Fq lo = T[s];
+  return fs ? fq_add(lo, fq_mul(r, fq_sub(T[s + fs], lo))) : fq_mul(omr, lo);
+}
+__device__ __forceinline__ Fq fold_side(const FoldArg& F, uint32_t i) {
+  const Fq lo = F.side_in[i];
+  return fq_add(lo, fq_mul(F.r, fq_sub(F.side_in[i + F.side_half], lo)));
+}
+__device__ __forceinline__ void fold_side_pass(const FoldArg& F, uint32_t gt, uint32_t gstride) {
+  for (uint32_t i = gt; i < F.side_half; i += gstride) F.side_out[i] = fold_side(F, i);
+}
+
+template <bool FOLD>
 __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32_t total, uint32_t proof_len,
                                                      uint32_t cons_len, uint32_t instance_len,
                                                      const Fq* __restrict__ Ap, const Fq* __restrict__ Aq,
-                                                     const Fq* __restrict__ Ax, const Fq* __restrict__ B,
-                                                     const Fq* __restrict__ C, const Fq* __restrict__ D,
-                                                     Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                     uint32_t* __restrict__ mb, uint32_t seq) {
+                                                     const Fq* __restrict__ Ax, Fq* __restrict__ B, Fq* __restrict__ C,
+                                                     Fq* __restrict__ D, Fq* __restrict__ partials,
+                                                     unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
+                                                     uint32_t seq, FoldArg F) {
+  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
+  const Fq omr = fq_sub(fq_one(), F.r);
+  auto eq_q = [&](uint32_t i) { return FOLD && F.fmode == MODE_Q ? fold_side(F, i) : Aq[i]; };
+  auto eq_x = [&](uint32_t i) { return FOLD && F.fmode == MODE_X ? fold_side(F, i) : Ax[i]; };
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(a, t);
     const PqxInst& d = pinst(a, p);
     uint32_t loc = t - d.dom_off;
     uint32_t q = loc / d.sc_ni, x = loc % d.sc_ni;
-    Fq apq = fq_mul(Ap[p], Aq[q * d.step_q]);
-    Fq a_lo = fq_mul(apq, Ax[x * d.step_x]);
+    const Fq aq_lo = eq_q(q * d.step_q), ax_lo = eq_x(x * d.step_x);
+    Fq apq = fq_mul(Ap[p], aq_lo);
+    Fq a_lo = fq_mul(apq, ax_lo);
     Fq a_hi;
-    if (mode == MODE_P) a_hi = fq_mul(fq_mul(Ap[p + instance_len], Aq[q * d.step_q]), Ax[x * d.step_x]);
-    else if (mode == MODE_Q) a_hi = fq_mul(fq_mul(Ap[p], Aq[q * d.step_q + proof_len]), Ax[x * d.step_x]);
-    else a_hi = fq_mul(apq, Ax[x * d.step_x + cons_len]);
+    if (mode == MODE_P) a_hi = fq_mul(fq_mul(Ap[p + instance_len], aq_lo), ax_lo);
+    else if (mode == MODE_Q) a_hi = fq_mul(fq_mul(Ap[p], eq_q(q * d.step_q + proof_len)), ax_lo);
+    else a_hi = fq_mul(apq, eq_x(x * d.step_x + cons_len));
     size_t base = pqx_off(d) + (size_t)q * d.anw * d.ani + x;
-    Fq b_lo = B[base], c_lo = C[base], d_lo = D[base];
-    Fq b_hi, c_hi, d_hi;
     bool zero_hi;
     size_t hi;
     if (mode == MODE_X) {
@@ -234,10 +256,32 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
       zero_hi = ph >= a.zlen;
       hi = zero_hi ? 0 : pqx_off(pinst(a, ph)) + (size_t)q * pinst(a, ph).anw * pinst(a, ph).ani + x;
     }
-    if (zero_hi) {
-      b_hi = fq_zero(); c_hi = fq_zero(); d_hi = fq_zero();
+    Fq b_lo, c_lo, d_lo, b_hi = fq_zero(), c_hi = fq_zero(), d_hi = fq_zero();
+    if (FOLD) {
+      const uint32_t fs = d.fstride;
+      b_lo = fold_read(B, base, fs, F.r, omr);
+      c_lo = fold_read(C, base, fs, F.r, omr);
+      d_lo = fold_read(D, base, fs, F.r, omr);
+      B[base] = b_lo;
+      C[base] = c_lo;
+      D[base] = d_lo;
+      if (!zero_hi) {
+        b_hi = fold_read(B, hi, fs, F.r, omr);
+        c_hi = fold_read(C, hi, fs, F.r, omr);
+        d_hi = fold_read(D, hi, fs, F.r, omr);
+        B[hi] = b_hi;
+        C[hi] = c_hi;
+        D[hi] = d_hi;
+      }
     } else {
-      b_hi = B[hi]; c_hi = C[hi]; d_hi = D[hi];
+      b_lo = B[base];
+      c_lo = C[base];
+      d_lo = D[base];
+      if (!zero_hi) {
+        b_hi = B[hi];
+        c_hi = C[hi];
+        d_hi = D[hi];
+      }
     }
     // comb(A, B, C, D) = A * (B*C - D) at X = 0, 2, 3
     e0 = fq_add(e0, fq_mul(a_lo, fq_sub(fq_mul(b_lo, c_lo), d_lo)));
@@ -267,14 +311,19 @@ __device__ __forceinline__ Fq fq_pick(int q, const Fq& a0, const Fq& a1, const F
   return q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
 }
 
+// FOLD: a level 0 first applies the pending fold, lane 0 to B's lo and hi entries, lane 1 to C's, lane 2 to D's and
+// lane 3 to the two entries of the folded eq side table the point reads; the values go round the quad by DPP.
+template <bool FOLD>
 __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint32_t total, uint32_t proof_len,
                                                        uint32_t cons_len, uint32_t instance_len,
                                                        const Fq* __restrict__ Ap, const Fq* __restrict__ Aq,
-                                                       const Fq* __restrict__ Ax, const Fq* __restrict__ B,
-                                                       const Fq* __restrict__ C, const Fq* __restrict__ D,
+                                                       const Fq* __restrict__ Ax, Fq* __restrict__ B,
+                                                       Fq* __restrict__ C, Fq* __restrict__ D,
                                                        Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                       uint32_t* __restrict__ mb, uint32_t seq) {
+                                                       uint32_t* __restrict__ mb, uint32_t seq, FoldArg F) {
   const int q = threadIdx.x & 3;
+  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
+  const Fq omr = fq_sub(fq_one(), F.r);
   Fq acc = fq_zero();
   for (uint32_t t = blockIdx.x * 64 + (threadIdx.x >> 2); t < total; t += gridDim.x * 64) {  // uniform per quad
     int p = find_inst(a, t);
@@ -295,23 +344,68 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
       zero_hi = ph >= a.zlen;
       hi = zero_hi ? 0 : pqx_off(pinst(a, ph)) + (size_t)qq * pinst(a, ph).anw * pinst(a, ph).ani + x;
     }
-    const Fq b_lo = B[base], c_lo = C[base], d_lo = D[base];
-    const Fq b_hi = zero_hi ? fq_zero() : B[hi], c_hi = zero_hi ? fq_zero() : C[hi], d_hi = zero_hi ? fq_zero() : D[hi];
+    const uint32_t iq = qq * d.step_q, ix = x * d.step_x;
+    Fq b_lo, c_lo, d_lo, b_hi, c_hi, d_hi;
+    Fq aq_lo, aq_hi, ax_lo, ax_hi;  // the eq entries levels 1 and 2 read
+    if (FOLD) {
+      Fq f_lo, f_hi = fq_zero();
+      if (q < 3) {
+        Fq* T = q == 0 ? B : (q == 1 ? C : D);
+        f_lo = fold_read(T, base, d.fstride, F.r, omr);
+        T[base] = f_lo;
+        if (!zero_hi) {
+          f_hi = fold_read(T, hi, d.fstride, F.r, omr);
+          T[hi] = f_hi;
+        }
+      } else {
+        const bool sx = F.fmode == MODE_X;
+        f_lo = fold_side(F, sx ? ix : iq);
+        if (sx ? mode == MODE_X : mode == MODE_Q) f_hi = fold_side(F, sx ? ix + cons_len : iq + proof_len);
+      }
+      b_lo = fq_qb<0>(f_lo);
+      b_hi = fq_qb<0>(f_hi);
+      c_lo = fq_qb<1>(f_lo);
+      c_hi = fq_qb<1>(f_hi);
+      d_lo = fq_qb<2>(f_lo);
+      d_hi = fq_qb<2>(f_hi);
+      const Fq s_lo = fq_qb<3>(f_lo), s_hi = fq_qb<3>(f_hi);
+      if (F.fmode == MODE_X) {
+        ax_lo = s_lo;
+        ax_hi = s_hi;
+        aq_lo = Aq[iq];
+        aq_hi = mode == MODE_Q ? Aq[iq + proof_len] : aq_lo;
+      } else {
+        aq_lo = s_lo;
+        aq_hi = s_hi;
+        ax_lo = Ax[ix];
+        ax_hi = ax_lo;
+      }
+    } else {
+      b_lo = B[base];
+      c_lo = C[base];
+      d_lo = D[base];
+      b_hi = zero_hi ? fq_zero() : B[hi];
+      c_hi = zero_hi ? fq_zero() : C[hi];
+      d_hi = zero_hi ? fq_zero() : D[hi];
+      aq_lo = Aq[iq];
+      aq_hi = mode == MODE_Q ? Aq[iq + proof_len] : aq_lo;
+      ax_lo = Ax[ix];
+      ax_hi = mode == MODE_X ? Ax[ix + cons_len] : ax_lo;
+    }
     const Fq b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo), d2 = fq_sub(fq_dbl(d_hi), d_lo);
     const Fq b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
-    const uint32_t iq = qq * d.step_q, ix = x * d.step_x;
     // level 1: lane 0 Ap Aq (lo), lane 1 the hi eq prefix (modes P / Q) or b3 c3 (mode X), lane 2 b c, lane 3 b2 c2
     Fq u1, v1;
     if (q == 0) {
       u1 = Ap[p];
-      v1 = Aq[iq];
+      v1 = aq_lo;
     } else if (q == 1) {
       if (mode == MODE_X) {
         u1 = b3;
         v1 = c3;
       } else {
         u1 = mode == MODE_P ? Ap[p + instance_len] : Ap[p];
-        v1 = mode == MODE_P ? Aq[iq] : Aq[iq + proof_len];
+        v1 = mode == MODE_P ? aq_lo : aq_hi;
       }
     } else {
       u1 = q == 2 ? b_lo : b2;
@@ -321,7 +415,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
     const Fq apq = fq_qb<0>(r1), r1_1 = fq_qb<1>(r1), bc_lo = fq_qb<2>(r1), bc2 = fq_qb<3>(r1);
     // level 2: lane 0 a_lo = apq Ax[x], lane 1 a_hi, lane 2 b3 c3 (modes P / Q)
     const Fq u2 = q == 1 && mode != MODE_X ? r1_1 : (q == 2 ? b3 : apq);
-    const Fq v2 = q == 2 ? c3 : (q == 1 && mode == MODE_X ? Ax[ix + cons_len] : Ax[ix]);
+    const Fq v2 = q == 2 ? c3 : (q == 1 && mode == MODE_X ? ax_hi : ax_lo);
     const Fq r2 = fq_mul(u2, v2);
     const Fq a_lo = fq_qb<0>(r2), a_hi = fq_qb<1>(r2);
     const Fq bc3 = mode == MODE_X ? r1_1 : fq_qb<2>(r2);
@@ -606,7 +700,7 @@ static int pqx_pack(spg_ctx* ctx, const std::vector<PqxInst>& v, PqxArgs& a, siz
 
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
-                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* out3) {
+                const Fq* Ax, Fq* B, Fq* C, Fq* D, Fq* partials, Fq* out3, const FoldPlan* fold) {
   PqxArgs a;
   std::vector<PqxInst> v;
   pqx_fill_args(T, a, v);
@@ -623,16 +717,26 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
     d.step_x = (uint32_t)(cons_len / sc_nc[p]);
     dom += sc_np[p] * sc_nc[p];
   }
+  if (fold) {
+    if (mode == MODE_P || fold->stride.size() < P) return set_err(ctx, SPG_E_ARG, "fused fold: bad plan");
+    for (size_t p = 0; p < P; p++) v[p].fstride = fold->stride[p];
+  }
   if (dom >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "phase-1 domain too large");
   if (int rc = pqx_pack(ctx, v, a, kWsPqxA)) return rc;
   const bool quad = dom <= sc_quad_max();
   const int nb = quad ? grid_for((uint32_t)(4 * dom)) : grid_for((uint32_t)dom);
-  {
+  if (!fold) {
     // B, C, D lo+hi per domain point, plus the three eq factor tables once
     KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len));
-    hipLaunchKernelGGL(quad ? k_phase1_eval_q : k_phase1_eval, dim3(nb), dim3(256), 0, ctx->stream, a, mode,
-                       (uint32_t)dom, (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq, Ax, B,
-                       C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
+    hipLaunchKernelGGL(quad ? k_phase1_eval_q<false> : k_phase1_eval<false>, dim3(nb), dim3(256), 0, ctx->stream, a,
+                       mode, (uint32_t)dom, (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq,
+                       Ax, B, C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, FoldArg{});
+  } else {
+    // per point: B, C, D lo + hi and their fold partners read, lo + hi written; the side table's half once
+    KScope ks(ctx, "sc_phase1_fold_eval", 576.0 * dom + 96.0 * fold->arg.side_half + 64.0 * (instance_len + proof_len));
+    hipLaunchKernelGGL(quad ? k_phase1_eval_q<true> : k_phase1_eval<true>, dim3(nb), dim3(256), 0, ctx->stream, a,
+                       mode, (uint32_t)dom, (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq,
+                       Ax, B, C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, fold->arg);
   }
   SPG_HIP(ctx, hipGetLastError());
   return eval_reduce_finish(ctx, out3);
@@ -739,6 +843,27 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq
     hipLaunchKernelGGL(k_pqx_fold, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, a, mode,
                        (uint32_t)dom, r, T.d, d1, d2, side, (uint32_t)side_half);
     SPG_HIP(ctx, hipGetLastError());
+  }
+  return 0;
+}
+
+int pqx_fold_plan(spg_ctx* ctx, PqxDev& T, int mode, FoldPlan* fp) {
+  if (mode != MODE_X && mode != MODE_Q) return set_err(ctx, SPG_E_ARG, "fused fold: mode");
+  const size_t P = std::min(T.num_instances, T.zlen);
+  fp->stride.assign(T.zlen, 0);
+  for (size_t p = 0; p < P; p++) {  // the partner of pqx_fold_at, from the sizes before the fold
+    const size_t n = mode == MODE_X ? T.num_inputs[p] : T.num_proofs[p];
+    const size_t row = mode == MODE_X ? 1 : T.anw[p] * T.ani[p];
+    const size_t s = n == 1 ? 0 : (n / 2) * row;
+    if (s >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "fused fold: stride");
+    fp->stride[p] = (uint32_t)s;
+  }
+  // the size bookkeeping of pqx_prepare (mirrors the reference's field updates)
+  if (mode == MODE_Q) T.max_num_proofs /= 2;
+  else T.max_num_inputs /= 2;
+  for (size_t p = 0; p < P; p++) {
+    size_t& n = mode == MODE_X ? T.num_inputs[p] : T.num_proofs[p];
+    if (n != 1) n /= 2;
   }
   return 0;
 }

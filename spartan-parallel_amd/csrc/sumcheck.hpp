@@ -27,10 +27,26 @@ int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out, const KBlob* blob 
 // DensePolynomial::bound_poly_var_top on a device vector of length len
 int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r);
 
+// the previous round's fold, applied by the phase-1 evaluation that follows it (one launch: fused fold + eval)
+struct FoldArg {  // kernel argument
+  Fq r;
+  int fmode;            // MODE_X: the side table is Ax; MODE_Q: Aq
+  const Fq* side_in;    // the side eq table before the fold (2 side_half entries)
+  Fq* side_out;         // its folded half (the other ping-pong buffer)
+  uint32_t side_half;
+};
+struct FoldPlan {
+  FoldArg arg;
+  std::vector<uint32_t> stride;  // per instance: element stride to the fold partner (0: scale by 1 - r)
+};
+// DensePolynomialPqx::bound_poly's size bookkeeping for mode X or Q on the host, without a launch; the fold itself is
+// then carried by the next phase1_eval (fold != nullptr)
+int pqx_fold_plan(spg_ctx* ctx, PqxDev& T, int mode, FoldPlan* fp);
+
 // one phase-1 round: (e0, e2, e3) of eq(p,q,x) * (B*C - D)  (src/sumcheck.rs:1173-1245)
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
-                const Fq* Ax, const Fq* B, const Fq* C, const Fq* D, Fq* partials, Fq* out3);
+                const Fq* Ax, Fq* B, Fq* C, Fq* D, Fq* partials, Fq* out3, const FoldPlan* fold = nullptr);
 // one phase-2 round: (e0, e2, e3) of eq(p) * ABC * Z  (src/sumcheck.rs:881-941)
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,

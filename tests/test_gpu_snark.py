@@ -87,10 +87,24 @@ def test_circ_program_on_gpu(ctx, vars_gens, tmp_path, case):
     assert hashlib.sha256(proof).hexdigest() == golden["proof_sha256"]
 
 
-@pytest.mark.parametrize("quad_max", ["0", "1099511627776"])
-def test_sumcheck_eval_forms(quad_max):
-    """the R1CSProof round evaluations in the one-thread-per-point form everywhere (SPG_SC_QUAD_MAX=0) or in the
-    quad form everywhere (2^40): the same bytes as the golden proof (the default mixes them by round size)"""
+ROUND_FORMS = {
+    "eval_one_thread": {"SPG_SC_QUAD_MAX": "0"},
+    "eval_quad_everywhere": {"SPG_SC_QUAD_MAX": str(1 << 40)},
+    "fold_launches": {"SPG_SC_FUSE": "0"},
+    "layer_launches": {"SPG_LAYER_PERSIST": "0"},
+    "layer_persist_one_wg": {"SPG_PERSIST_WGS": "1", "SPG_PERSIST_MAX": str(1 << 20)},
+    "layer_persist_wide": {"SPG_PERSIST_WGS": "256", "SPG_PERSIST_MAX": str(1 << 20)},
+    "layer_persist_no_ends": {"SPG_LAYER_ENDS": "0"},
+}
+
+
+@pytest.mark.parametrize("form", sorted(ROUND_FORMS))
+def test_round_forms(form):
+    """the sumcheck rounds in every launch form, against the golden proof's bytes (the default mixes them by round
+    size; a fresh process reads the switches): R1CSProof evaluations one thread per point (SPG_SC_QUAD_MAX=0) or a
+    quad per point everywhere; phase-1 folds as launches of their own (SPG_SC_FUSE=0) instead of inside the next
+    round's evaluation; SPARK layer rounds as one launch each (SPG_LAYER_PERSIST=0) instead of the persistent launch,
+    which also runs with one workgroup over every round, with 256 workgroups, and without posting the layer's entries"""
     import subprocess
     import sys
 
@@ -106,7 +120,7 @@ def test_sumcheck_eval_forms(quad_max):
         "(p,) = gpu_snark(ctx, g, workload.SnarkWorkload(**SNARK_CASES[%r]), workload.tape_seed())\n"
         "print(hashlib.sha256(p).hexdigest())\n"
     ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "tests"), case)
-    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_SC_QUAD_MAX=quad_max),
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **ROUND_FORMS[form]),
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     golden = json.load(open(os.path.join(G, "snark_proofs.json")))[case]
