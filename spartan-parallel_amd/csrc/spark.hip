@@ -809,7 +809,9 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       while (log_len > 0) {
         const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
         // every remaining round is a quad round of at most persist_max elements: one persistent launch for them all
-        if (persist_on && quad && !local && (tr.size() << (log_len - 1)) <= persist_max &&
+        // (one process per GPU only: processes sharing a GPU time-slice its queues, and a resident loop could then
+        // wait out its timeout while descheduled)
+        if (persist_on && quad && !local && ctx->nranks == 1 && (tr.size() << (log_len - 1)) <= persist_max &&
             ngroups * ((size_t)1 << (log_len - 1)) < wide_min)
           return run_persist(log_len, close_after, fin);
         log_len--;
