@@ -369,7 +369,7 @@ struct ZKRounds {
 // workspace slots used here (msm.hip uses 0..12, proto.hip 20..22)
 enum {
   WS_AZ = 30, WS_BZ, WS_CZ, WS_Z, WS_ABC, WS_TP, WS_TQ, WS_TX, WS_EQRX, WS_EQP, WS_PART, WS_OUT3, WS_DESC,
-  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2, WS_TQ2, WS_TX2
+  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2, WS_TQ2, WS_TX2, WS_ABC2
 };
 // phase-1 rounds in modes x and q fold inside the next round's evaluation (sumcheck.hip, FOLD kernels); SPG_SC_FUSE=0
 // restores the separate fold launch
@@ -919,7 +919,7 @@ int Prover::run_inner(Laps& lp) {
     PqxDev Zc, ABCc;
     PqxDev *TZ = &Zp, *TA = &ABC;
     const Fq* eq_l = eq_p + p0;
-    auto launch_eval = [&](size_t j) -> int {
+    auto launch_eval = [&](size_t j, const Fold2* fold) -> int {
       int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       if (inputs_len > 1) inputs_len /= 2;
       else if (ws_len > 1) ws_len /= 2;
@@ -932,8 +932,14 @@ int Prover::run_inner(Laps& lp) {
       for (size_t p = 0; p < sc_ni.size(); p++)
         if (mode == MODE_X && sc_ni[p] > 1) sc_ni[p] /= 2;
       return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, sc_ni, eq_l, partials,
-                         nullptr);
+                         nullptr, fold);
     };
+    // one ABC serving every instance is folded into this buffer by a fused round (then the two swap)
+    Fq* ABC2 = nullptr;
+    if (sc_fuse_on() && single) {
+      ABC2 = (Fq*)ws_get(ctx, WS_ABC2, btot * sizeof(Fq) + 64);
+      if (!ABC2) return set_err(ctx, SPG_E_NOMEM, "ABC");
+    }
     auto to_compact = [&]() -> int {
       std::vector<std::vector<Fq>> full;
       int r2 = single ? gather_first({&Zp}, full) : gather_first({&Zp, &ABC}, full);
@@ -954,7 +960,7 @@ int Prover::run_inner(Laps& lp) {
       return 0;
     };
     if (rounds && ny + nw == 0) rc = to_compact();
-    if (!rc && rounds) rc = launch_eval(0);
+    if (!rc && rounds) rc = launch_eval(0, nullptr);
     if (rc) return rc;
     zk.init(g, tape, rounds, claim2, blind2);  // host precomputation while round 0 evaluates
     for (size_t j = 0; j < rounds; j++) {
@@ -966,11 +972,27 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p2_eval");
       Fq r_j = zk.begin(g, t, j, e);
       lp.lap("p2_host");
-      if (mode == MODE_P) { rc = dev_fold_top(ctx, eq_p, lenP, r_j); lenP /= 2; }
-      if (!rc && (mode != MODE_P || !single)) rc = pqx_bound2(ctx, *TA, *TZ, r_j, mode);
-      else if (!rc) rc = pqx_bound(ctx, *TZ, nullptr, nullptr, r_j, mode);
-      if (!rc && j + 1 == ny + nw && np > 0) rc = to_compact();
-      if (!rc && j + 1 < rounds) rc = launch_eval(j + 1);
+      const bool compact_next = j + 1 == ny + nw && np > 0;
+      const int next_mode = j + 1 < ny ? MODE_X : (j + 1 < ny + nw ? MODE_W : MODE_P);
+      if (sc_fuse_on() && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
+        // the fold rides in the next round's evaluation (k_phase2_eval<true>)
+        Fold2 f;
+        rc = pqx_fold_plan(ctx, *TA, mode, &f.a);
+        if (!rc) rc = pqx_fold_plan(ctx, *TZ, mode, &f.z);
+        f.arg.r = r_j;
+        f.arg.fmode = mode;
+        f.arg.fw = f.z.fw;
+        f.arg.ping = single ? 1 : 0;
+        f.arg.b_out = single ? ABC2 : TA->d;
+        if (!rc) rc = launch_eval(j + 1, &f);
+        if (!rc && single) std::swap(TA->d, ABC2);
+      } else {
+        if (mode == MODE_P) { rc = dev_fold_top(ctx, eq_p, lenP, r_j); lenP /= 2; }
+        if (!rc && (mode != MODE_P || !single)) rc = pqx_bound2(ctx, *TA, *TZ, r_j, mode);
+        else if (!rc) rc = pqx_bound(ctx, *TZ, nullptr, nullptr, r_j, mode);
+        if (!rc && compact_next) rc = to_compact();
+        if (!rc && j + 1 < rounds) rc = launch_eval(j + 1, nullptr);
+      }
       if (rc) return rc;
       lp.lap("p2_fold");
       zk.finish(g, t, tape, j, r_j);

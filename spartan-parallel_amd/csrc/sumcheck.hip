@@ -429,12 +429,6 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
   grid_reduce3(q == 0 ? acc : z, q == 1 ? acc : z, q == 2 ? acc : z, partials, counter, mb, seq);
 }
 
-__global__ void __launch_bounds__(256) k_phase2_eval_q(PqxArgs ab, PqxArgs zz, int mode, uint32_t total,
-                                                       bool single, uint32_t instance_len, const Fq* __restrict__ eq,
-                                                       const Fq* __restrict__ B, const Fq* __restrict__ C,
-                                                       Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                       uint32_t* __restrict__ mb, uint32_t seq);
-
 // ---------------------------------------------------------------- phase 2 round evaluation
 // domain: p < Pd, w < W, y < sc_ni[p] ; B = ABC table (instance pi = single ? 0 : p), C = Z table
 __device__ __forceinline__ Fq pqx_get(const PqxArgs& a, const Fq* T, int p, uint32_t w, uint32_t y) {
@@ -454,11 +448,58 @@ __device__ __forceinline__ Fq pqx_get_high(const PqxArgs& a, const Fq* T, int p,
   return ph < a.zlen ? T[pqx_off(pinst(a, ph)) + (size_t)w * pinst(a, ph).ani + y] : fq_zero();
 }
 
+// Fused fold + eval (FOLD), as in phase 1: the previous round's bound_poly_var_{x,w} of ABC and Z is applied to the
+// entries a point reads. Z entries (and ABC entries when every instance has its own) are read by one point each and
+// folded in place; one ABC shared by every instance is read by all of them, so it is folded into its ping-pong buffer,
+// written by instance 0's points (which read every live ABC entry).
+__device__ __forceinline__ long pq_lo(const PqxArgs& a, int p, uint32_t w, uint32_t y) {
+  if (p >= a.zlen) return -1;
+  const PqxInst& d = pinst(a, p);
+  if (w >= d.anw || y >= d.ani) return -1;
+  return (long)(pqx_off(d) + (size_t)w * d.ani + y);
+}
+// the hi entry of modes X and W (pqx_get_high), with its witness-section coordinate
+__device__ __forceinline__ long pq_hi(const PqxArgs& a, int p, uint32_t w, uint32_t y, int mode, uint32_t* wc) {
+  const PqxInst& d = pinst(a, p);
+  if (mode == MODE_X) {
+    *wc = w;
+    return d.ni == 1 ? -1 : (long)(pqx_off(d) + (size_t)w * d.ani + y + d.ni / 2);
+  }
+  const uint32_t wh = w + a.nws / 2;
+  *wc = wh;
+  return wh < d.anw ? (long)(pqx_off(d) + (size_t)wh * d.ani + y) : -1;
+}
+__device__ __forceinline__ Fq fold2_at(const Fq* T, long s, const PqxInst& d, uint32_t wc, const Fold2Arg& F,
+                                       const Fq& omr) {
+  const Fq lo = T[s];
+  const bool pair = d.fstride && (F.fmode != MODE_W || wc + F.fw < d.anw);
+  return pair ? fq_add(lo, fq_mul(F.r, fq_sub(T[s + d.fstride], lo))) : fq_mul(omr, lo);
+}
+// this point's ABC (tb = 0) or Z (tb = 1) lo and hi entries, folded and written back
+__device__ __forceinline__ void fold2_pair(const PqxArgs& a, Fq* T, int p, uint32_t w, uint32_t y, int mode,
+                                           const Fold2Arg& F, const Fq& omr, Fq* out, bool write, Fq& lo, Fq& hi) {
+  const long sl = pq_lo(a, p, w, y);
+  uint32_t wc;
+  const long sh = pq_hi(a, p, w, y, mode, &wc);
+  lo = fq_zero();
+  hi = fq_zero();
+  if (sl >= 0) {
+    lo = fold2_at(T, sl, pinst(a, p), w, F, omr);
+    if (write) out[sl] = lo;
+  }
+  if (sh >= 0) {
+    hi = fold2_at(T, sh, pinst(a, p), wc, F, omr);
+    if (write) out[sh] = hi;
+  }
+}
+
+template <bool FOLD>
 __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int mode, uint32_t total, int W,
                                                      bool single, uint32_t instance_len, const Fq* __restrict__ eq,
-                                                     const Fq* __restrict__ B, const Fq* __restrict__ C,
+                                                     Fq* __restrict__ B, Fq* __restrict__ C,
                                                      Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                     uint32_t* __restrict__ mb, uint32_t seq) {
+                                                     uint32_t* __restrict__ mb, uint32_t seq, Fold2Arg F) {
+  const Fq omr = fq_sub(fq_one(), F.r);
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(zz, t);
@@ -469,8 +510,16 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
     int pi = single ? 0 : p;
     Fq a_lo = eq[p];
     Fq a_hi = mode == MODE_P ? eq[p + instance_len] : a_lo;
-    Fq b_lo = pqx_get(ab, B, pi, w, y), c_lo = pqx_get(zz, C, p, w, y);
-    Fq b_hi = pqx_get_high(ab, B, pi, w, y, mode), c_hi = pqx_get_high(zz, C, p, w, y, mode);
+    Fq b_lo, b_hi, c_lo, c_hi;
+    if (FOLD) {
+      fold2_pair(ab, B, pi, w, y, mode, F, omr, F.b_out, !F.ping || p == 0, b_lo, b_hi);
+      fold2_pair(zz, C, p, w, y, mode, F, omr, C, true, c_lo, c_hi);
+    } else {
+      b_lo = pqx_get(ab, B, pi, w, y);
+      c_lo = pqx_get(zz, C, p, w, y);
+      b_hi = pqx_get_high(ab, B, pi, w, y, mode);
+      c_hi = pqx_get_high(zz, C, p, w, y, mode);
+    }
     e0 = fq_add(e0, fq_mul(fq_mul(a_lo, b_lo), c_lo));
     Fq a2 = fq_sub(fq_dbl(a_hi), a_lo), b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo);
     e2 = fq_add(e2, fq_mul(fq_mul(a2, b2), c2));
@@ -480,13 +529,16 @@ __global__ void __launch_bounds__(256) k_phase2_eval(PqxArgs ab, PqxArgs zz, int
   grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
-// quad form of k_phase2_eval: lane 0 / 1 / 2 forms the point's product at X = 0 / 2 / 3 as (a b) c, two levels
+// quad form of k_phase2_eval: lane 0 / 1 / 2 forms the point's product at X = 0 / 2 / 3 as (a b) c, two levels (FOLD:
+// a level 0 first, lane 0 folding the ABC entries and lane 1 the Z entries, exchanged by DPP)
+template <bool FOLD>
 __global__ void __launch_bounds__(256) k_phase2_eval_q(PqxArgs ab, PqxArgs zz, int mode, uint32_t total,
                                                        bool single, uint32_t instance_len, const Fq* __restrict__ eq,
-                                                       const Fq* __restrict__ B, const Fq* __restrict__ C,
+                                                       Fq* __restrict__ B, Fq* __restrict__ C,
                                                        Fq* __restrict__ partials, unsigned* __restrict__ counter,
-                                                       uint32_t* __restrict__ mb, uint32_t seq) {
+                                                       uint32_t* __restrict__ mb, uint32_t seq, Fold2Arg F) {
   const int q = threadIdx.x & 3;
+  const Fq omr = fq_sub(fq_one(), F.r);
   Fq acc = fq_zero();
   for (uint32_t t = blockIdx.x * 64 + (threadIdx.x >> 2); t < total; t += gridDim.x * 64) {  // uniform per quad
     int p = find_inst(zz, t);
@@ -496,8 +548,21 @@ __global__ void __launch_bounds__(256) k_phase2_eval_q(PqxArgs ab, PqxArgs zz, i
     int pi = single ? 0 : p;
     const Fq a_lo = eq[p];
     const Fq a_hi = mode == MODE_P ? eq[p + instance_len] : a_lo;
-    const Fq b_lo = pqx_get(ab, B, pi, w, y), c_lo = pqx_get(zz, C, p, w, y);
-    const Fq b_hi = pqx_get_high(ab, B, pi, w, y, mode), c_hi = pqx_get_high(zz, C, p, w, y, mode);
+    Fq b_lo, b_hi, c_lo, c_hi;
+    if (FOLD) {
+      Fq f_lo = fq_zero(), f_hi = fq_zero();
+      if (q == 0) fold2_pair(ab, B, pi, w, y, mode, F, omr, F.b_out, !F.ping || p == 0, f_lo, f_hi);
+      else if (q == 1) fold2_pair(zz, C, p, w, y, mode, F, omr, C, true, f_lo, f_hi);
+      b_lo = fq_qb<0>(f_lo);
+      b_hi = fq_qb<0>(f_hi);
+      c_lo = fq_qb<1>(f_lo);
+      c_hi = fq_qb<1>(f_hi);
+    } else {
+      b_lo = pqx_get(ab, B, pi, w, y);
+      c_lo = pqx_get(zz, C, p, w, y);
+      b_hi = pqx_get_high(ab, B, pi, w, y, mode);
+      c_hi = pqx_get_high(zz, C, p, w, y, mode);
+    }
     const Fq a2 = fq_sub(fq_dbl(a_hi), a_lo), b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo);
     const Fq a3 = fq_sub(fq_add(a2, a_hi), a_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo);
     const Fq ab_ = fq_mul(fq_pick(q, a_lo, a2, a3, a_lo), fq_pick(q, b_lo, b2, b3, b_lo));
@@ -744,7 +809,7 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
 
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
-                const Fq* eq, Fq* partials, Fq* out3) {
+                const Fq* eq, Fq* partials, Fq* out3, const Fold2* fold) {
   PqxArgs ab, zz;
   std::vector<PqxInst> vab, vz;
   pqx_fill_args(AB, ab, vab);
@@ -760,19 +825,28 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
     vz[p].sc_ni = (uint32_t)sc_ni[p];
     dom += W * sc_ni[p];
   }
+  if (fold) {
+    if (mode == MODE_P || fold->a.stride.size() < vab.size() || fold->z.stride.size() < P)
+      return set_err(ctx, SPG_E_ARG, "fused fold: bad plan");
+    for (size_t p = 0; p < vab.size(); p++) vab[p].fstride = fold->a.stride[p];
+    for (size_t p = 0; p < P; p++) vz[p].fstride = fold->z.stride[p];
+  }
   if (int rc = pqx_pack(ctx, vab, ab, kWsPqxA)) return rc;
   if (int rc = pqx_pack(ctx, vz, zz, kWsPqxB)) return rc;
   const bool quad = dom <= sc_quad_max();
   const int nb = quad ? grid_for((uint32_t)(4 * dom)) : grid_for((uint32_t)dom);
+  const Fold2Arg fa = fold ? fold->arg : Fold2Arg{};
   {
-    KScope ks(ctx, "sc_phase2_eval", 128.0 * dom);  // ABC and Z, lo+hi per domain point
+    // ABC and Z lo+hi per domain point; fused: their fold partners read and the folded entries written too
+    KScope ks(ctx, fold ? "sc_phase2_fold_eval" : "sc_phase2_eval", (fold ? 384.0 : 128.0) * dom);
     if (quad)
-      hipLaunchKernelGGL(k_phase2_eval_q, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, single,
-                         (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
+      hipLaunchKernelGGL(fold ? k_phase2_eval_q<true> : k_phase2_eval_q<false>, dim3(nb), dim3(256), 0, ctx->stream,
+                         ab, zz, mode, (uint32_t)dom, single, (uint32_t)instance_len, eq, AB.d, Z.d, partials,
+                         ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, fa);
     else
-      hipLaunchKernelGGL(k_phase2_eval, dim3(nb), dim3(256), 0, ctx->stream, ab, zz, mode, (uint32_t)dom, (int)W,
-                         single, (uint32_t)instance_len, eq, AB.d, Z.d, partials, ctx->d_counter, ctx->d_mbox,
-                         ++ctx->mbox_seq);
+      hipLaunchKernelGGL(fold ? k_phase2_eval<true> : k_phase2_eval<false>, dim3(nb), dim3(256), 0, ctx->stream, ab, zz,
+                         mode, (uint32_t)dom, (int)W, single, (uint32_t)instance_len, eq, AB.d, Z.d, partials,
+                         ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, fa);
   }
   SPG_HIP(ctx, hipGetLastError());
   return eval_reduce_finish(ctx, out3);
@@ -848,9 +922,21 @@ int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq
 }
 
 int pqx_fold_plan(spg_ctx* ctx, PqxDev& T, int mode, FoldPlan* fp) {
-  if (mode != MODE_X && mode != MODE_Q) return set_err(ctx, SPG_E_ARG, "fused fold: mode");
+  if (mode != MODE_X && mode != MODE_Q && mode != MODE_W) return set_err(ctx, SPG_E_ARG, "fused fold: mode");
   const size_t P = std::min(T.num_instances, T.zlen);
   fp->stride.assign(T.zlen, 0);
+  fp->fw = 0;
+  if (mode == MODE_W) {  // partner w + nws / 2, when that section exists (pqx_fold_at)
+    const size_t fw = T.num_witness_secs / 2;
+    for (size_t p = 0; p < P; p++) {
+      const size_t s = fw * T.ani[p];
+      if (s >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "fused fold: stride");
+      fp->stride[p] = (uint32_t)s;
+    }
+    fp->fw = (uint32_t)fw;
+    T.num_witness_secs = fw;
+    return 0;
+  }
   for (size_t p = 0; p < P; p++) {  // the partner of pqx_fold_at, from the sizes before the fold
     const size_t n = mode == MODE_X ? T.num_inputs[p] : T.num_proofs[p];
     const size_t row = mode == MODE_X ? 1 : T.anw[p] * T.ani[p];

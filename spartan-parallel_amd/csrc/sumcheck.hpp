@@ -38,10 +38,23 @@ struct FoldArg {  // kernel argument
 struct FoldPlan {
   FoldArg arg;
   std::vector<uint32_t> stride;  // per instance: element stride to the fold partner (0: scale by 1 - r)
+  uint32_t fw = 0;               // mode W: the witness-section count after the fold (a partner exists iff w + fw < anw)
 };
-// DensePolynomialPqx::bound_poly's size bookkeeping for mode X or Q on the host, without a launch; the fold itself is
-// then carried by the next phase1_eval (fold != nullptr)
+// DensePolynomialPqx::bound_poly's size bookkeeping for mode X, Q or W on the host, without a launch; the fold itself
+// is then carried by the next phase1_eval / phase2_eval (fold != nullptr)
 int pqx_fold_plan(spg_ctx* ctx, PqxDev& T, int mode, FoldPlan* fp);
+// phase 2's pending fold of ABC and Z, applied by the next phase2_eval
+struct Fold2Arg {  // kernel argument
+  Fq r;
+  int fmode;     // MODE_X or MODE_W
+  uint32_t fw;
+  Fq* b_out;     // ABC's folded entries: ABC itself, or its ping-pong buffer when one ABC serves every instance
+  int ping;      // b_out is the ping-pong buffer (written by instance 0's points only)
+};
+struct Fold2 {
+  FoldPlan a, z;  // strides of ABC and Z
+  Fold2Arg arg;
+};
 
 // one phase-1 round: (e0, e2, e3) of eq(p,q,x) * (B*C - D)  (src/sumcheck.rs:1173-1245)
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
@@ -50,7 +63,7 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
 // one phase-2 round: (e0, e2, e3) of eq(p) * ABC * Z  (src/sumcheck.rs:881-941)
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,
-                const Fq* eq, Fq* partials, Fq* out3);
+                const Fq* eq, Fq* partials, Fq* out3, const Fold2* fold = nullptr);
 // DensePolynomialPqx::bound_poly on T (and d1, d2 sharing T's shape, may be null)
 // side (optional): a dense vector of side_len entries bound by the same r in the same launch
 // (DensePolynomial::bound_poly_var_top, as dev_fold_top) - the round's eq factor in phase 1

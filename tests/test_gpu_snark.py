@@ -102,7 +102,7 @@ ROUND_FORMS = {
 def test_round_forms(form):
     """the sumcheck rounds in every launch form, against the golden proof's bytes (the default mixes them by round
     size; a fresh process reads the switches): R1CSProof evaluations one thread per point (SPG_SC_QUAD_MAX=0) or a
-    quad per point everywhere; phase-1 folds as launches of their own (SPG_SC_FUSE=0) instead of inside the next
+    quad per point everywhere; phase-1 and phase-2 folds as launches of their own (SPG_SC_FUSE=0) instead of inside the next
     round's evaluation; SPARK layer rounds as one launch each (SPG_LAYER_PERSIST=0) instead of the persistent launch,
     which also runs with one workgroup over every round, with 256 workgroups, and without posting the layer's entries"""
     import subprocess
