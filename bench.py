@@ -26,8 +26,10 @@ mixed additions, one per nonzero signed window digit) against the measured whole
 algorithmic HBM bytes against 8 TB/s; `roofline_hbm` / `roofline_valu` give the largest kernel of each kind.
 Per-launch times are libspg's HIP events on its context stream (spg_prof_read2) in a profiling pass after the
 timed steps; `traffic` is the PMC-measured HBM bytes per launch from the committed rocprofv3 summary of the same
-workload (TRAFFIC below: scripts/gpu_run.sh PMC=1, session r03y). `device_busy_ms_per_step` is the union of
-the timed intervals, since kernels on the context's second stream overlap those of the main one.
+workload (TRAFFIC below: scripts/gpu_run.sh PMC=1). `device_busy_ms_per_step` is the union of the timed
+intervals, since kernels on the context's second stream overlap those of the main one, without the resident
+layer-round launches (their intervals include the host's answers between rounds);
+`device_busy_incl_resident_ms_per_step` counts them too.
 `cpu_baseline` is the C++ CPU restatement of the reference (oracle/) on rank 0 at N = 1: one thread on the full
 workload, and `cpu_baseline_all_cores` the same work run as one independent prove per usable host core at once.
 """
@@ -81,9 +83,10 @@ def parse():
                          "default: shard for --workload spark / msm, replicas otherwise")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--log-msm", type=int, default=16, help="msm: 2^k (scalar, generator) pairs")
-    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark", "msm"],
+    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark", "msm", "rows"],
                     help="snark: the headline metric (SNARK::prove, SURVEY 8d config 3); r1cs: its block "
-                         "R1CSProof::prove alone; spark: SURVEY 8d config 5 (SPARK); msm: config 2")
+                         "R1CSProof::prove alone; spark: SURVEY 8d config 5 (SPARK); msm: config 2; rows: config 2's "
+                         "1024 x 1024 row batch")
     ap.add_argument("--log-cons", type=int, default=10, help="snark: 2^k constraints per block")
     ap.add_argument("--log-proofs", type=int, default=9, help="snark: 2^k executions per block")
     ap.add_argument("--log-nnz", type=int, default=24, help="spark: 2^k nonzeros per matrix (x3 matrices)")
@@ -181,14 +184,19 @@ def profile_pass(ctx, step, steps):
     prof = Prof(ctx.prof_read(reset=True, ops=True))
     ctx.prof_enable(False)
     busy = prof.pop("(device_busy)", None)
+    res = prof.pop("(device_busy_resident)", None)
     prof.busy_us = busy[1] if busy else sum(v[1] for v in prof.values())
+    prof.busy_resident_us = res[1] if res else prof.busy_us
     return prof
 
 
 class Prof(dict):
     """per-kernel timings of a profile pass; busy_us = the device's busy time (union of the timed intervals: kernels
-    of the context's second stream overlap the main stream's, so the per-kernel sum overstates it)"""
+    of the context's second stream overlap the main stream's, so the per-kernel sum overstates it), leaving out the
+    resident launches (spark_layer_persist: their interval spans the host's answers between rounds);
+    busy_resident_us = the union with them"""
     busy_us = 0.0
+    busy_resident_us = 0.0
 
 
 def traffic_of(kernel, traffic_file):
@@ -407,6 +415,7 @@ def main_snark(a):
             "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16],
             "device_busy_ms_per_step": round(prof.busy_us / a.steps / 1e3, 3),
+            "device_busy_incl_resident_ms_per_step": round(prof.busy_resident_us / a.steps / 1e3, 3),
             "value_incl_witness_upload": round(N * env.world / t_incl, 1),
             "ms_per_step_incl_witness_upload": round(t_incl * 1e3, 3),
             "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
@@ -821,9 +830,21 @@ def main_spark(a):
     env.close()
 
 
+def main_rows(a):
+    env = Env(a)
+    import spg
+
+    ctx = spg.Context(env.gpu)
+    out = rows_core(env, ctx, a.steps, a.warmup, not a.no_cpu_baseline, a.traffic or TRAFFIC["rows"])
+    if env.rank == 0:
+        out["vs_baseline"] = None
+        print(json.dumps(out))
+    env.close()
+
+
 def main():
     a = parse()
-    {"snark": main_snark, "r1cs": main_r1cs, "spark": main_spark, "msm": main_msm}[a.workload](a)
+    {"snark": main_snark, "r1cs": main_r1cs, "spark": main_spark, "msm": main_msm, "rows": main_rows}[a.workload](a)
 
 
 if __name__ == "__main__":

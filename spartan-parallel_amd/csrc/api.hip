@@ -470,30 +470,39 @@ extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* t
   if (!c) return SPG_E_ARG;
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->stream2);
-  // device busy time = the union of the timed intervals (kernels on the second stream overlap the main one's)
+  // device busy time = the union of the timed intervals (kernels on the second stream overlap the main one's).
+  // A resident launch (scope name ending in "_persist") spans the host's answers between its rounds, so it is left
+  // out of "(device_busy)" and counted only in "(device_busy_resident)", the union over every launch.
   if (!c->prof_pending.empty()) {
-    std::vector<std::pair<float, float>> iv;
+    std::vector<std::pair<float, float>> iv, iv_all;
     const hipEvent_t base = c->prof_pending.front().a;
     for (auto& r : c->prof_pending) {
       float s = 0.f, e = 0.f;
-      if (hipEventElapsedTime(&s, base, r.a) == hipSuccess && hipEventElapsedTime(&e, base, r.b) == hipSuccess)
-        iv.push_back({s, e});
+      if (hipEventElapsedTime(&s, base, r.a) == hipSuccess && hipEventElapsedTime(&e, base, r.b) == hipSuccess) {
+        iv_all.push_back({s, e});
+        const size_t n = r.name.size();
+        if (!(n >= 8 && r.name.compare(n - 8, 8, "_persist") == 0)) iv.push_back({s, e});
+      }
     }
-    std::sort(iv.begin(), iv.end());
-    double busy = 0, lo = 0, hi = 0;
-    bool open = false;
-    for (auto& x : iv) {
-      if (open && x.first <= hi) {
-        hi = std::max<double>(hi, x.second);
-        continue;
+    auto union_ms = [](std::vector<std::pair<float, float>>& v) {
+      std::sort(v.begin(), v.end());
+      double busy = 0, lo = 0, hi = 0;
+      bool open = false;
+      for (auto& x : v) {
+        if (open && x.first <= hi) {
+          hi = std::max<double>(hi, x.second);
+          continue;
+        }
+        if (open) busy += hi - lo;
+        lo = x.first;
+        hi = x.second;
+        open = true;
       }
       if (open) busy += hi - lo;
-      lo = x.first;
-      hi = x.second;
-      open = true;
-    }
-    if (open) busy += hi - lo;
-    c->prof_acc["(device_busy)"].us += busy * 1000.0;
+      return busy;
+    };
+    c->prof_acc["(device_busy)"].us += union_ms(iv) * 1000.0;
+    c->prof_acc["(device_busy_resident)"].us += union_ms(iv_all) * 1000.0;
   }
   for (auto& r : c->prof_pending) {
     float ms = 0.f;

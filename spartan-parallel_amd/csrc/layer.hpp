@@ -8,6 +8,13 @@
 
 namespace spg {
 
+// a system-scope release before a host-visible signal (the light build drains write-through stores instead)
+#ifdef SPG_LIGHT_FENCE
+#define SPG_SYS_RELEASE() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define SPG_SYS_RELEASE() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "")
+#endif
+
 struct Triple {
   Fq *A, *B, *C;
 };
@@ -179,7 +186,7 @@ __global__ void __launch_bounds__(256) k_layer_close(const Triple* __restrict__ 
       for (int i = 0; i < 8; i++)
         __hip_atomic_store(mb + 8 + 8 * (3 * c + k) + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  SPG_SYS_RELEASE();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -288,7 +295,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   // before the sequence number
   Fq e = layer_round_elems(tr, coeff, nt, log_len, do_fold, r, cin, cout, ((long)blockIdx.x * BS + t) >> 2,
                            (long)gridDim.x * (BS / 4), ends && gridDim.x == 1 ? mb : nullptr);
-  if (ends) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (ends) SPG_SYS_RELEASE();
   if (pr && t == 0) pr[1] = wall_clock64();
   quad_block_sum<BS>(e);
   if (pr && t == 0) pr[2] = wall_clock64();
@@ -296,7 +303,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
     if (ends) __syncthreads();
     if (t < 3) {
       for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      SPG_SYS_RELEASE();
     }
     if (t == 0) {
       __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -329,7 +336,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   quad_block_sum<BS>(a);
   if (t < 3) {
     for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    SPG_SYS_RELEASE();
   }
   if (t == 0) {
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -347,25 +354,6 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
 // the host's answer comes only after the last ticket). The layer's last round posts every vector's two entries from
 // the workgroup that takes the last ticket, so the host folds the final claims itself. Every wave leaves the loop on
 // the last round, on the host's abort word, or after `timeout` ticks without an answer.
-typedef __attribute__((address_space(1))) uint64_t gu64;  // global (not flat) accesses: the sc1 hand-off needs them
-__device__ __forceinline__ Fq ld_sc1(const Fq* p) {
-  Fq r;
-  gu64* w = (gu64*)p;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint64_t v = __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r.l[2 * i] = (uint32_t)v;
-    r.l[2 * i + 1] = (uint32_t)(v >> 32);
-  }
-  return r;
-}
-__device__ __forceinline__ void st_sc1(Fq* p, const Fq& v) {
-  gu64* w = (gu64*)p;
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-    __hip_atomic_store(w + i, (uint64_t)v.l[2 * i] | ((uint64_t)v.l[2 * i + 1] << 32), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ Fq fold_at_sc1(const Fq* p, int k, int fl, const Fq& r) {
   const Fq lo = ld_sc1(p + k);
   return fq_add(lo, fq_mul(r, fq_sub(ld_sc1(p + k + fl), lo)));
@@ -420,6 +408,8 @@ struct PersistArgs {
   uint32_t* down;    // the host's answers
   int ends;          // the last round posts every vector's two entries after the sums (3 + 6 nt scalars)
   unsigned long long timeout;  // wall_clock64 ticks a workgroup waits for an answer before it gives up
+  uint32_t* relay;   // non-null: workgroup 0 alone polls the host and copies each answer here (HBM: [0] sequence
+                     // number, [8..15] challenge) for the others, instead of every workgroup reading host memory
 };
 static const uint32_t kDownAbortDev = 0xffffffffu;  // = kDownAbort (ctx.hpp)
 template <int BS>
@@ -471,7 +461,7 @@ __global__ void __launch_bounds__(BS) k_layer_persist(PersistArgs A) {
       }
       if (t < 3)
         for (int j = 0; j < 8; j++) __hip_atomic_store(A.mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      SPG_SYS_RELEASE();
       __syncthreads();
       if (t == 0) {
         __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -480,21 +470,34 @@ __global__ void __launch_bounds__(BS) k_layer_persist(PersistArgs A) {
       }
     }
     if (lg == 0) return;  // the layer's last round: nothing to wait for
-    if (t == 0) {  // one lane per workgroup polls the downbox
+    if (t == 0) {  // one lane per workgroup polls the downbox (or, relayed, workgroup 0's copy in HBM)
+      const bool host = !A.relay || blockIdx.x == 0;
+      uint32_t* src = host ? A.down : A.relay;
       const unsigned long long t0 = wall_clock64();
       uint32_t v;
       uint32_t ok = 1;
-      while ((v = __hip_atomic_load(A.down, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != seq) {
-        if (v == kDownAbortDev || wall_clock64() - t0 > A.timeout) {
+      while ((v = host ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                       : __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != seq) {
+        if (v == kDownAbortDev || v == (seq | 0x80000000u) || wall_clock64() - t0 > A.timeout) {
           ok = 0;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (host) __builtin_amdgcn_s_sleep(8);
+        else __builtin_amdgcn_s_sleep(1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the challenge is read after the matching sequence number
       if (ok)
-        for (int i = 0; i < 8; i++) rsh[i] = __hip_atomic_load(A.down + 8 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int i = 0; i < 8; i++)
+          rsh[i] = host ? __hip_atomic_load(src + 8 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                        : __hip_atomic_load(src + 8 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       rsh[8] = ok;
+      if (A.relay && blockIdx.x == 0) {  // the others' copy: challenge, drained, then the number (or the abort word)
+        if (ok)
+          for (int i = 0; i < 8; i++) __hip_atomic_store(A.relay + 8 + i, rsh[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (this round's abort word: a stale value of an earlier launch never equals it)
+        __hip_atomic_store(A.relay, ok ? seq : (seq | 0x80000000u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     __syncthreads();
     if (!rsh[8]) return;

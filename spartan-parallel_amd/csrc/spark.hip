@@ -293,6 +293,7 @@ enum : size_t {
   kWsCommit = 60, kWsL, kWsBoundPart, kWsBound, kWsSegPart, kWsSeg, kWsC, kWsTriples, kWsCoeff, kWsFoldPtr,
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
   kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp,  // 60 .. 89
+  kWsRelay = 94,
   kWsMultiExt = 120, kWsMultiOut, kWsCommitExt  // (snark.hip uses 91 .. 93, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
 };
 
@@ -757,6 +758,12 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       A.down = ctx->d_down;
       A.ends = ends ? 1 : 0;
       A.timeout = 2000000000ULL;  // 20 s of the 100 MHz wall clock
+      static const bool relay_on = !getenv("SPG_PERSIST_RELAY") || atoi(getenv("SPG_PERSIST_RELAY")) != 0;
+      A.relay = nullptr;
+      if (relay_on && K > 1) {
+        A.relay = (uint32_t*)ws_get(ctx, kWsRelay, 64);
+        if (!A.relay) return set_err(ctx, SPG_E_NOMEM, "layer relay");
+      }
       ctx->mbox_seq += (uint32_t)R;
       ctx->down[0] = 0;  // clear a previous launch's abort word
       {
@@ -795,7 +802,9 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     // rounds while the vectors (2 len entries here) have len >= 1; `local` rounds sum over the ranks; with
     // close_after the layer's (or the shard's) final entries follow in `fin`
     static const bool ends_on = !getenv("SPG_LAYER_ENDS") || atoi(getenv("SPG_LAYER_ENDS")) != 0;
-    static const bool persist_on = !getenv("SPG_LAYER_PERSIST") || atoi(getenv("SPG_LAYER_PERSIST")) != 0;
+    // off by default: same-box A/B (profiles/r04_ab_persist_fuse_bcomb.txt) measured 21.5 ms per prove with the
+    // resident launches against 18.9 ms without
+    static const bool persist_on = getenv("SPG_LAYER_PERSIST") && atoi(getenv("SPG_LAYER_PERSIST")) != 0;
     auto run_rounds = [&](size_t log_len, bool local, bool close_after, FqV* fin, int status) -> int {
       if (status) {  // skip mode: the first local round's exchange carries the failure to every rank
         if (!local || log_len == 0) return status;

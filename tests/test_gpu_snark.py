@@ -91,10 +91,11 @@ ROUND_FORMS = {
     "eval_one_thread": {"SPG_SC_QUAD_MAX": "0"},
     "eval_quad_everywhere": {"SPG_SC_QUAD_MAX": str(1 << 40)},
     "fold_launches": {"SPG_SC_FUSE": "0"},
-    "layer_launches": {"SPG_LAYER_PERSIST": "0"},
-    "layer_persist_one_wg": {"SPG_PERSIST_WGS": "1", "SPG_PERSIST_MAX": str(1 << 20)},
-    "layer_persist_wide": {"SPG_PERSIST_WGS": "256", "SPG_PERSIST_MAX": str(1 << 20)},
-    "layer_persist_no_ends": {"SPG_LAYER_ENDS": "0"},
+    "layer_persist": {"SPG_LAYER_PERSIST": "1"},
+    "layer_persist_host_polls": {"SPG_LAYER_PERSIST": "1", "SPG_PERSIST_RELAY": "0"},
+    "layer_persist_one_wg": {"SPG_LAYER_PERSIST": "1", "SPG_PERSIST_WGS": "1", "SPG_PERSIST_MAX": str(1 << 20)},
+    "layer_persist_wide": {"SPG_LAYER_PERSIST": "1", "SPG_PERSIST_WGS": "256", "SPG_PERSIST_MAX": str(1 << 20)},
+    "layer_persist_no_ends": {"SPG_LAYER_PERSIST": "1", "SPG_LAYER_ENDS": "0"},
 }
 
 
@@ -103,8 +104,9 @@ def test_round_forms(form):
     """the sumcheck rounds in every launch form, against the golden proof's bytes (the default mixes them by round
     size; a fresh process reads the switches): R1CSProof evaluations one thread per point (SPG_SC_QUAD_MAX=0) or a
     quad per point everywhere; phase-1 and phase-2 folds as launches of their own (SPG_SC_FUSE=0) instead of inside the next
-    round's evaluation; SPARK layer rounds as one launch each (SPG_LAYER_PERSIST=0) instead of the persistent launch,
-    which also runs with one workgroup over every round, with 256 workgroups, and without posting the layer's entries"""
+    round's evaluation; SPARK layer rounds in the resident launch (SPG_LAYER_PERSIST=1; the default launches each
+    round), with workgroup 0 relaying the host's answer or every workgroup polling the host, with one workgroup over
+    every round, with 256 workgroups, and without posting the layer's entries"""
     import subprocess
     import sys
 
