@@ -256,21 +256,6 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
     if (slot < d) acc = quad_add_op(acc, quad_get_op<S>(pts, slot, q), q);
     __syncthreads();
   }
-#ifdef SPG_LIGHT_FENCE
-  // the parts go to mapped host memory write-through, drained by every storing wave before the barrier; the folded
-  // state (HBM) is read by the next launch only, after the kernel boundary
-  if (slot < a.R && q == 0) st_sys_ext(&a.parts[((size_t)b * gridDim.x + blockIdx.x) * a.R + slot], acc);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           gridDim.x * gridDim.y - 1;
-    if (last) {
-      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      mbox_post(a.mb, a.seq, nullptr, 0);
-    }
-  }
-#else
   if (slot < a.R && q == 0) a.parts[((size_t)b * gridDim.x + blockIdx.x) * a.R + slot] = acc;
   __syncthreads();
   if (t == 0) {
@@ -286,7 +271,6 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
       mbox_post(a.mb, a.seq, nullptr, 0);
     }
   }
-#endif
 }
 
 // B plain MSMs from the comb table, sum_i s_{b,i} G_{idx_{b,i}} (Montgomery scalars), left as partial points: the Cx

@@ -72,13 +72,6 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
     return;
   }
   if (t == 0) {
-#ifdef SPG_LIGHT_FENCE
-    st_sc1(&partials[3 * blockIdx.x], v0);
-    st_sc1(&partials[3 * blockIdx.x + 1], v1);
-    st_sc1(&partials[3 * blockIdx.x + 2], v2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-#else
     partials[3 * blockIdx.x] = v0;
     partials[3 * blockIdx.x + 1] = v1;
     partials[3 * blockIdx.x + 2] = v2;
@@ -90,21 +83,14 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-#endif
   }
   __syncthreads();
   if (!last) return;
   Fq a = fq_zero(), b = fq_zero(), c = fq_zero();
   for (unsigned i = t; i < gridDim.x; i += 256) {
-#ifdef SPG_LIGHT_FENCE
-    a = fq_add(a, ld_sc1(&partials[3 * i]));
-    b = fq_add(b, ld_sc1(&partials[3 * i + 1]));
-    c = fq_add(c, ld_sc1(&partials[3 * i + 2]));
-#else
     a = fq_add(a, partials[3 * i]);
     b = fq_add(b, partials[3 * i + 1]);
     c = fq_add(c, partials[3 * i + 2]);
-#endif
   }
   block_sum3(a, b, c);
   if (t == 0) {
