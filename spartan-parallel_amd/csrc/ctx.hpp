@@ -254,6 +254,19 @@ __device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* 
   __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// three scalars (a sumcheck round's e0, e2, e3) without a local array: the array form's runtime-indexed loop put it
+// in scratch memory, and a kernel with a private segment costs more to dispatch
+__device__ __forceinline__ void mbox_post3(uint32_t* mb, uint32_t seq, const Fq& a, const Fq& b, const Fq& c) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    __hip_atomic_store(mb + 8 + i, a.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(mb + 16 + i, b.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(mb + 24 + i, c.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- multi-process collectives (spg_set_comm) -----------------------------------------------------------
 // One shard of an SPMD call: rank `rank` of `n` processes (n == 1: this process alone, no communication).
 struct Shard {

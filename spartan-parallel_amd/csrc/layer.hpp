@@ -5,6 +5,7 @@
 
 #include "ctx.hpp"
 #include "lds.hpp"
+#include "qsum.hpp"
 
 namespace spg {
 
@@ -129,8 +130,7 @@ __global__ void __launch_bounds__(BS) k_layer_round(const Triple* __restrict__ t
   if (pr && t == 0) pr[2] = wall_clock64();
   if (gridDim.x == 1) {
     if (t == 0) {
-      const Fq rr[3] = {e0, e2, e3};
-      mbox_post(mb, seq, rr, 3);
+      mbox_post3(mb, seq, e0, e2, e3);
       if (pr) pr[3] = wall_clock64();
     }
     return;
@@ -159,8 +159,7 @@ __global__ void __launch_bounds__(BS) k_layer_round(const Triple* __restrict__ t
   }
   block_sum3_t0<BS>(a, b, cc);
   if (t == 0) {
-    const Fq rr[3] = {a, b, cc};
-    mbox_post(mb, seq, rr, 3);
+    mbox_post3(mb, seq, a, b, cc);
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -196,39 +195,6 @@ __device__ __forceinline__ Fq fq_qbcast(const Fq& a) {
 #pragma unroll
   for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
   return r;
-}
-__device__ __forceinline__ Fq fq_shfl_xor(const Fq& a, int m) {
-  Fq r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__shfl_xor((int)a.l[i], m);
-  return r;
-}
-// value at X = 0, 2, 3 (p = 0, 1, 2) of the line through (0, lo), (1, hi)
-__device__ __forceinline__ Fq line_at(const Fq& lo, const Fq& hi, int p) {
-  const Fq d = fq_sub(hi, lo), x2 = fq_add(hi, d);
-  return p == 0 ? lo : (p == 1 ? x2 : fq_add(x2, d));
-}
-// sums of the values of lanes with equal (thread & 3) over a block of BS threads: quads of a wave by
-// cross-quad shuffles, then waves through LDS; the sum for q is left in thread q (q < 3)
-template <int BS>
-__device__ __forceinline__ void quad_block_sum(Fq& e) {
-  constexpr int NW = BS / 64;
-  __shared__ uint32_t wsum[NW > 1 ? NW : 1][3][8];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-#pragma unroll
-  for (int m = 4; m < 64; m <<= 1) e = fq_add(e, fq_shfl_xor(e, m));
-  if (NW > 1) {
-    if (lane < 3)
-      for (int j = 0; j < 8; j++) wsum[w][lane][j] = e.l[j];
-    __syncthreads();
-    if (w == 0 && lane < 3)
-      for (int v = 1; v < NW; v++) {
-        Fq o;
-        for (int j = 0; j < 8; j++) o.l[j] = wsum[v][lane][j];
-        e = fq_add(e, o);
-      }
-    __syncthreads();
-  }
 }
 // the elements u = u0, u0 + ustride, ... of one round (a quad per element): this lane's share of its point's sum
 // ends (a layer's last round, one workgroup): lane p < 3 also writes its vector's two entries (lo, hi) to mailbox
@@ -595,8 +561,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_wide(const Triple* __restric
   }
   block_sum3_t0<BS>(a, b, cc);
   if (t == 0) {
-    const Fq rr[3] = {a, b, cc};
-    mbox_post(mb, seq, rr, 3);
+    mbox_post3(mb, seq, a, b, cc);
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

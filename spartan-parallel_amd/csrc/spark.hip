@@ -161,8 +161,7 @@ __global__ void __launch_bounds__(1024) k_layer_tiny(const Triple* __restrict__ 
   }
   block_sum3_t0<1024>(e0, e2, e3);
   if (t == 0) {
-    const Fq rr[3] = {e0, e2, e3};
-    mbox_post(mb, seq, rr, 3);
+    mbox_post3(mb, seq, e0, e2, e3);
   }
 }
 // one batched cubic sumcheck round over nt triples (A_c, B_c, C_c) of length 2 * len:
@@ -210,8 +209,7 @@ __global__ void __launch_bounds__(256) k_layer_eval(const Triple* __restrict__ t
   }
   block_sum3_sp(a, b, c);
   if (threadIdx.x == 0) {
-    const Fq r[3] = {a, b, c};
-    mbox_post(mb, seq, r, 3);
+    mbox_post3(mb, seq, a, b, c);
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

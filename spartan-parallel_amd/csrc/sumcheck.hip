@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include "lds.hpp"
+#include "qsum.hpp"
 #include "sumcheck.hpp"
 
 namespace spg {
@@ -66,8 +67,7 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
   const int t = threadIdx.x;
   if (gridDim.x == 1) {  // a one-block round posts directly: no partials, ticket or second reduction
     if (t == 0) {
-      const Fq r[3] = {v0, v1, v2};
-      mbox_post(mb, seq, r, 3);
+      mbox_post3(mb, seq, v0, v1, v2);
     }
     return;
   }
@@ -94,8 +94,7 @@ __device__ __forceinline__ void grid_reduce3(Fq v0, Fq v1, Fq v2, Fq* __restrict
   }
   block_sum3(a, b, c);
   if (t == 0) {
-    const Fq r[3] = {a, b, c};
-    mbox_post(mb, seq, r, 3);
+    mbox_post3(mb, seq, a, b, c);
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -227,21 +226,24 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
                                                      uint32_t seq, FoldArg F) {
   if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
   const Fq omr = fq_sub(fq_one(), F.r);
-  auto eq_q = [&](uint32_t i) { return FOLD && F.fmode == MODE_Q ? fold_side(F, i) : Aq[i]; };
-  auto eq_x = [&](uint32_t i) { return FOLD && F.fmode == MODE_X ? fold_side(F, i) : Ax[i]; };
+  // the eq entries a point reads (folded on the fly when the pending fold binds that side table); no lambdas over
+  // the by-value kernel arguments, which put them on the stack (scratch memory)
+  const bool fq_side = FOLD && F.fmode == MODE_Q, fx_side = FOLD && F.fmode == MODE_X;
+#define EQ_Q(i) (fq_side ? fold_side(F, (i)) : Aq[(i)])
+#define EQ_X(i) (fx_side ? fold_side(F, (i)) : Ax[(i)])
   Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
   for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
     int p = find_inst(a, t);
     const PqxInst& d = pinst(a, p);
     uint32_t loc = t - d.dom_off;
     uint32_t q = loc / d.sc_ni, x = loc % d.sc_ni;
-    const Fq aq_lo = eq_q(q * d.step_q), ax_lo = eq_x(x * d.step_x);
+    const Fq aq_lo = EQ_Q(q * d.step_q), ax_lo = EQ_X(x * d.step_x);
     Fq apq = fq_mul(Ap[p], aq_lo);
     Fq a_lo = fq_mul(apq, ax_lo);
     Fq a_hi;
     if (mode == MODE_P) a_hi = fq_mul(fq_mul(Ap[p + instance_len], aq_lo), ax_lo);
-    else if (mode == MODE_Q) a_hi = fq_mul(fq_mul(Ap[p], eq_q(q * d.step_q + proof_len)), ax_lo);
-    else a_hi = fq_mul(apq, eq_x(x * d.step_x + cons_len));
+    else if (mode == MODE_Q) a_hi = fq_mul(fq_mul(Ap[p], EQ_Q(q * d.step_q + proof_len)), ax_lo);
+    else a_hi = fq_mul(apq, EQ_X(x * d.step_x + cons_len));
     size_t base = pqx_off(d) + (size_t)q * d.anw * d.ani + x;
     bool zero_hi;
     size_t hi;
@@ -292,6 +294,8 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
     Fq c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
     e3 = fq_add(e3, fq_mul(a3, fq_sub(fq_mul(b3, c3), d3)));
   }
+#undef EQ_Q
+#undef EQ_X
   grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
@@ -307,8 +311,12 @@ __device__ __forceinline__ Fq fq_qb(const Fq& a) {
   for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K * 0x55, 0xf, 0xf, false);
   return r;
 }
+// word-wise selects: a select of whole structs became a runtime-indexed stack array (scratch memory)
 __device__ __forceinline__ Fq fq_pick(int q, const Fq& a0, const Fq& a1, const Fq& a2, const Fq& a3) {
-  return q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = q == 0 ? a0.l[i] : (q == 1 ? a1.l[i] : (q == 2 ? a2.l[i] : a3.l[i]));
+  return r;
 }
 
 // FOLD: a level 0 first applies the pending fold, lane 0 to B's lo and hi entries, lane 1 to C's, lane 2 to D's and
@@ -425,8 +433,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
     const Fq v3 = fq_pick(q, fq_sub(bc_lo, d_lo), fq_sub(bc2, d2), fq_sub(bc3, d3), fq_sub(bc_lo, d_lo));
     acc = fq_add(acc, fq_mul(u3, v3));
   }
-  const Fq z = fq_zero();
-  grid_reduce3(q == 0 ? acc : z, q == 1 ? acc : z, q == 2 ? acc : z, partials, counter, mb, seq);
+  quad_grid_post<256>(acc, partials, counter, mb, seq);
 }
 
 // ---------------------------------------------------------------- phase 2 round evaluation
@@ -568,8 +575,7 @@ __global__ void __launch_bounds__(256) k_phase2_eval_q(PqxArgs ab, PqxArgs zz, i
     const Fq ab_ = fq_mul(fq_pick(q, a_lo, a2, a3, a_lo), fq_pick(q, b_lo, b2, b3, b_lo));
     acc = fq_add(acc, fq_mul(ab_, fq_pick(q, c_lo, c2, c3, c_lo)));
   }
-  const Fq z = fq_zero();
-  grid_reduce3(q == 0 ? acc : z, q == 1 ? acc : z, q == 2 ? acc : z, partials, counter, mb, seq);
+  quad_grid_post<256>(acc, partials, counter, mb, seq);
 }
 
 // ---------------------------------------------------------------- Pqx folds (custom_dense_mlpoly.rs:205-289)
