@@ -12,7 +12,7 @@
 
 namespace spg {
 
-static const int kMaxP = 8;  // instances whose descriptors ride in the kernel arguments (small kernargs; two PqxArgs stay under
+static const int kMaxP = 32;  // instances whose descriptors ride in the kernel arguments (two PqxArgs stay under
                               // the 4 KiB kernarg budget); more go to device memory (PqxArgs::ext)
 
 // per-instance view passed by value to kernels
