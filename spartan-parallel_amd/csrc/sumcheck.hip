@@ -212,7 +212,13 @@ __device__ __forceinline__ Fq fold_side(const FoldArg& F, uint32_t i) {
   const Fq lo = F.side_in[i];
   return fq_add(lo, fq_mul(F.r, fq_sub(F.side_in[i + F.side_half], lo)));
 }
-__device__ __forceinline__ void fold_side_pass(const FoldArg& F, uint32_t gt, uint32_t gstride) {
+// the side table's new half: by the threads the round's points leave idle when there are enough of them (so its
+// load-multiply-store chain is not in front of a busy thread's point), else by every thread, grid-stride
+__device__ __forceinline__ void fold_side_pass(const FoldArg& F, uint32_t gt, uint32_t gstride, uint32_t busy) {
+  if (busy <= gstride && gstride - busy >= F.side_half) {
+    if (gt >= busy && gt - busy < F.side_half) F.side_out[gt - busy] = fold_side(F, gt - busy);
+    return;
+  }
   for (uint32_t i = gt; i < F.side_half; i += gstride) F.side_out[i] = fold_side(F, i);
 }
 
@@ -224,7 +230,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
                                                      Fq* __restrict__ D, Fq* __restrict__ partials,
                                                      unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
                                                      uint32_t seq, FoldArg F) {
-  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
+  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256, total);
   const Fq omr = fq_sub(fq_one(), F.r);
   // the eq entries a point reads (folded on the fly when the pending fold binds that side table); no lambdas over
   // the by-value kernel arguments, which put them on the stack (scratch memory)
@@ -330,7 +336,7 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
                                                        Fq* __restrict__ partials, unsigned* __restrict__ counter,
                                                        uint32_t* __restrict__ mb, uint32_t seq, FoldArg F) {
   const int q = threadIdx.x & 3;
-  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
+  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256, total > (1u << 30) ? ~0u : 4 * total);
   const Fq omr = fq_sub(fq_one(), F.r);
   Fq acc = fq_zero();
   for (uint32_t t = blockIdx.x * 64 + (threadIdx.x >> 2); t < total; t += gridDim.x * 64) {  // uniform per quad
