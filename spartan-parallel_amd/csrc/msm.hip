@@ -629,12 +629,18 @@ static void bullet_comb_shape(int P, int* G, int* BS, int* R) {
   static const int eg = getenv("SPG_BCOMB_G") ? atoi(getenv("SPG_BCOMB_G")) : 0;
   static const int ebs = getenv("SPG_BCOMB_BS") ? atoi(getenv("SPG_BCOMB_BS")) : 0;
   static const int er = getenv("SPG_BCOMB_R") ? atoi(getenv("SPG_BCOMB_R")) : 0;
-  *G = P >= 2048 ? 4 : 8;  // G = 8 also at P = 512: same-box A/B 1.92 -> 1.88 ms of Bullet rounds per prove
+  // same-box A/Bs on the 2^20 SNARK (Bullet device ms per prove; profiles/r04_ab_bullet_shapes.txt): G 4 -> 8 at
+  // P = 512: 1.92 -> 1.88; G 8 -> 11 (two dependent quad additions per quad): 1.87 -> 1.81; R 4 -> 8 (one tree level
+  // fewer, twice the host-summed parts): 1.89 -> 1.74, R = 16: 1.85
+  *G = P >= 2048 ? 4 : 11;
   *BS = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
-  *R = P >= 2048 ? 1 : 4;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
+  *R = P >= 2048 ? 1 : 8;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
   if (eg == 4 || eg == 8 || eg == 11) *G = eg;
   if (ebs == 64 || ebs == 128 || ebs == 256) *BS = ebs;
   if (er >= 1 && er <= *BS / 4 && (er & (er - 1)) == 0) *R = er;
+  // at most kBulletPartsMax parts per MSM (the host staging): fewer points per workgroup for the largest proofs
+  const int wgs = (P * *G + *BS / 4 - 1) / (*BS / 4);
+  while (*R > 1 && wgs * *R > kBulletPartsMax) *R /= 2;
 }
 
 int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
