@@ -15,6 +15,11 @@ from collections import defaultdict
 
 # device kernel symbol -> libspg profiling scope name (spg_prof_read)
 NAMES = {
+    # fused fold + evaluation instances first (first match wins)
+    "k_phase1_eval_q<true>": "sc_phase1_fold_eval", "k_phase1_eval<true>": "sc_phase1_fold_eval",
+    "k_phase2_eval_q<true>": "sc_phase2_fold_eval", "k_phase2_eval<true>": "sc_phase2_fold_eval",
+    "k_bullet_comb": "msm_bullet_round", "k_comb_msm_parts": "msm_comb_parts", "k_comb_accum": "msm_comb",
+    "k_layer_persist": "spark_layer_persist",
     "k_phase1_eval": "sc_phase1_eval", "k_phase2_eval": "sc_phase2_eval", "k_pqx_fold": "sc_fold",
     "k_spmv": "spmv_block", "k_z_fill": "z_fill", "k_abc": "eval_table_abc", "k_bound_part": "poly_bound",
     "k_fold_top": "fold_dense", "k_eq_table": "eq_table", "k_cubic_eval": "sc_cubic_eval",
@@ -31,6 +36,10 @@ NAMES = {
 
 def scope(kname):
     for k, v in NAMES.items():
+        if "<" in k:  # a template instance: "spg::k_x<true>(...)"
+            if ("::" + k) in kname:
+                return v
+            continue
         if k + "(" in kname or kname.endswith(k) or ("::" + k) in kname:
             return v
     return None
