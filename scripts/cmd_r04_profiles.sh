@@ -3,3 +3,6 @@ for w in "msm:--workload msm" "rows:--workload rows" "r1cs22:--workload r1cs --c
   tag=${w%%:*}; args=${w#*:}
   TAG=${tag}_ PROF=1 PMC=1 PROF_ARGS="$args" T_PROF=300 bash scripts/gpu_run.sh || exit 1
 done
+# per-proof Bullet / DotProductProofLog lines of one headline prove (SPG_TRACE=3)
+SPG_TRACE=3 TRACE_REPS=2 timeout -k 10 200 python scripts/trace_snark.py 2> gpurun_out/trace3.err > /dev/null || exit 1
+grep -c "" gpurun_out/trace3.err
