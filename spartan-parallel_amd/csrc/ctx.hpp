@@ -246,16 +246,11 @@ __device__ __forceinline__ void st_sc1(Fq* p, const Fq& v) {
     __hip_atomic_store(w + i, (uint64_t)v.l[2 * i] | ((uint64_t)v.l[2 * i + 1] << 32), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
-// The mailbox words are system-scope atomic stores, which write through to host memory; draining them (vmcnt(0))
-// orders them before the sequence number. A release fence would also write back every dirty line of the XCD's L2
-// (buffer_wbl2), which the host never reads: the in-place folds' entries are read by the next launch only.
-__device__ __forceinline__ void mbox_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// device side of the mailbox: the scalars, drained, then the sequence number
+// device side of the mailbox: the scalars, then (after a system-scope release fence) the sequence number
 __device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* v, int n) {
   for (int k = 0; k < n; k++)
     for (int i = 0; i < 8; i++) __hip_atomic_store(mb + 8 + 8 * k + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  mbox_drain();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -268,7 +263,7 @@ __device__ __forceinline__ void mbox_post3(uint32_t* mb, uint32_t seq, const Fq&
     __hip_atomic_store(mb + 16 + i, b.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(mb + 24 + i, c.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  mbox_drain();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

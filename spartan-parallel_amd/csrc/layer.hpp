@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) k_layer_close(const Triple* __restrict__ 
       for (int i = 0; i < 8; i++)
         __hip_atomic_store(mb + 8 + 8 * (3 * c + k) + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  mbox_drain();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   // before the sequence number
   Fq e = layer_round_elems(tr, coeff, nt, log_len, do_fold, r, cin, cout, ((long)blockIdx.x * BS + t) >> 2,
                            (long)gridDim.x * (BS / 4), ends && gridDim.x == 1 ? mb : nullptr);
-  if (ends) mbox_drain();
+  if (ends) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (pr && t == 0) pr[1] = wall_clock64();
   quad_block_sum<BS>(e);
   if (pr && t == 0) pr[2] = wall_clock64();
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
     if (ends) __syncthreads();
     if (t < 3) {
       for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      mbox_drain();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     if (t == 0) {
       __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   quad_block_sum<BS>(a);
   if (t < 3) {
     for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    mbox_drain();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
   if (t == 0) {
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -420,7 +420,7 @@ __global__ void __launch_bounds__(BS) k_layer_persist(PersistArgs A) {
       }
       if (t < 3)
         for (int j = 0; j < 8; j++) __hip_atomic_store(A.mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      mbox_drain();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __syncthreads();
       if (t == 0) {
         __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -54,7 +54,7 @@ __device__ __forceinline__ void quad_grid_post(Fq e, Fq* __restrict__ partials, 
   if (gridDim.x == 1) {  // lanes 0..2 of wave 0 post e0, e2, e3, then lane 0 the sequence number
     if (t < 3) {
       for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      mbox_drain();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     if (t == 0) __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
@@ -72,7 +72,7 @@ __device__ __forceinline__ void quad_grid_post(Fq e, Fq* __restrict__ partials, 
   quad_block_sum<BS>(a);
   if (t < 3) {
     for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    mbox_drain();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
   if (t == 0) {
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
