@@ -204,9 +204,20 @@ __global__ void k_fold_top(Fq* __restrict__ v, size_t n, Fq r) {
 // for a dimension already of size 1) and writes it back in place; the partner entries lie outside the new live region
 // and nobody writes them. The side table is folded into the other ping-pong buffer (its old entries are read by many
 // points), by a grid-stride pass over its new half. One launch per round instead of two.
-__device__ __forceinline__ Fq fold_read(const Fq* T, size_t s, uint32_t fs, const Fq& r, const Fq& omr) {
-  const Fq lo = T[s];
-  return fs ? fq_add(lo, fq_mul(r, fq_sub(T[s + fs], lo))) : fq_mul(omr, lo);
+// the lo and hi entries (hi only when present) and their partners, all loaded before anything is written back (a
+// store between them would order the hi loads behind the lo product), folded, then written back in place
+__device__ __forceinline__ void fold_pair_rw(Fq* T, size_t lo_i, size_t hi_i, bool has_hi, uint32_t fs, const Fq& r,
+                                             const Fq& omr, Fq& lo, Fq& hi) {
+  const Fq a = T[lo_i], ap = fs ? T[lo_i + fs] : a;
+  Fq b = fq_zero(), bp = fq_zero();
+  if (has_hi) {
+    b = T[hi_i];
+    bp = fs ? T[hi_i + fs] : b;
+  }
+  lo = fs ? fq_add(a, fq_mul(r, fq_sub(ap, a))) : fq_mul(omr, a);
+  hi = has_hi ? (fs ? fq_add(b, fq_mul(r, fq_sub(bp, b))) : fq_mul(omr, b)) : fq_zero();
+  T[lo_i] = lo;
+  if (has_hi) T[hi_i] = hi;
 }
 __device__ __forceinline__ Fq fold_side(const FoldArg& F, uint32_t i) {
   const Fq lo = F.side_in[i];
@@ -267,20 +278,9 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
     Fq b_lo, c_lo, d_lo, b_hi = fq_zero(), c_hi = fq_zero(), d_hi = fq_zero();
     if (FOLD) {
       const uint32_t fs = d.fstride;
-      b_lo = fold_read(B, base, fs, F.r, omr);
-      c_lo = fold_read(C, base, fs, F.r, omr);
-      d_lo = fold_read(D, base, fs, F.r, omr);
-      B[base] = b_lo;
-      C[base] = c_lo;
-      D[base] = d_lo;
-      if (!zero_hi) {
-        b_hi = fold_read(B, hi, fs, F.r, omr);
-        c_hi = fold_read(C, hi, fs, F.r, omr);
-        d_hi = fold_read(D, hi, fs, F.r, omr);
-        B[hi] = b_hi;
-        C[hi] = c_hi;
-        D[hi] = d_hi;
-      }
+      fold_pair_rw(B, base, hi, !zero_hi, fs, F.r, omr, b_lo, b_hi);
+      fold_pair_rw(C, base, hi, !zero_hi, fs, F.r, omr, c_lo, c_hi);
+      fold_pair_rw(D, base, hi, !zero_hi, fs, F.r, omr, d_lo, d_hi);
     } else {
       b_lo = B[base];
       c_lo = C[base];
@@ -360,17 +360,24 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
     }
     const uint32_t iq = qq * d.step_q, ix = x * d.step_x;
     Fq b_lo, c_lo, d_lo, b_hi, c_hi, d_hi;
-    Fq aq_lo, aq_hi, ax_lo, ax_hi;  // the eq entries levels 1 and 2 read
+    // the eq entries levels 1 and 2 read, loaded up front (those of a side table the pending fold binds come
+    // folded from lane 3 below)
+    Fq aq_lo, aq_hi, ax_lo, ax_hi;
+    const bool side_q = FOLD && F.fmode == MODE_Q, side_x = FOLD && F.fmode == MODE_X;
+    if (!side_q) {
+      aq_lo = Aq[iq];
+      aq_hi = mode == MODE_Q ? Aq[iq + proof_len] : aq_lo;
+    }
+    if (!side_x) {
+      ax_lo = Ax[ix];
+      ax_hi = mode == MODE_X ? Ax[ix + cons_len] : ax_lo;
+    }
+    const Fq ap_lo = Ap[p], ap_hi = mode == MODE_P ? Ap[p + instance_len] : ap_lo;
     if (FOLD) {
       Fq f_lo, f_hi = fq_zero();
       if (q < 3) {
         Fq* T = q == 0 ? B : (q == 1 ? C : D);
-        f_lo = fold_read(T, base, d.fstride, F.r, omr);
-        T[base] = f_lo;
-        if (!zero_hi) {
-          f_hi = fold_read(T, hi, d.fstride, F.r, omr);
-          T[hi] = f_hi;
-        }
+        fold_pair_rw(T, base, hi, !zero_hi, d.fstride, F.r, omr, f_lo, f_hi);
       } else {
         const bool sx = F.fmode == MODE_X;
         f_lo = fold_side(F, sx ? ix : iq);
@@ -383,16 +390,12 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
       d_lo = fq_qb<2>(f_lo);
       d_hi = fq_qb<2>(f_hi);
       const Fq s_lo = fq_qb<3>(f_lo), s_hi = fq_qb<3>(f_hi);
-      if (F.fmode == MODE_X) {
+      if (side_x) {
         ax_lo = s_lo;
         ax_hi = s_hi;
-        aq_lo = Aq[iq];
-        aq_hi = mode == MODE_Q ? Aq[iq + proof_len] : aq_lo;
       } else {
         aq_lo = s_lo;
         aq_hi = s_hi;
-        ax_lo = Ax[ix];
-        ax_hi = ax_lo;
       }
     } else {
       b_lo = B[base];
@@ -401,24 +404,20 @@ __global__ void __launch_bounds__(256) k_phase1_eval_q(PqxArgs a, int mode, uint
       b_hi = zero_hi ? fq_zero() : B[hi];
       c_hi = zero_hi ? fq_zero() : C[hi];
       d_hi = zero_hi ? fq_zero() : D[hi];
-      aq_lo = Aq[iq];
-      aq_hi = mode == MODE_Q ? Aq[iq + proof_len] : aq_lo;
-      ax_lo = Ax[ix];
-      ax_hi = mode == MODE_X ? Ax[ix + cons_len] : ax_lo;
     }
     const Fq b2 = fq_sub(fq_dbl(b_hi), b_lo), c2 = fq_sub(fq_dbl(c_hi), c_lo), d2 = fq_sub(fq_dbl(d_hi), d_lo);
     const Fq b3 = fq_sub(fq_add(b2, b_hi), b_lo), c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
     // level 1: lane 0 Ap Aq (lo), lane 1 the hi eq prefix (modes P / Q) or b3 c3 (mode X), lane 2 b c, lane 3 b2 c2
     Fq u1, v1;
     if (q == 0) {
-      u1 = Ap[p];
+      u1 = ap_lo;
       v1 = aq_lo;
     } else if (q == 1) {
       if (mode == MODE_X) {
         u1 = b3;
         v1 = c3;
       } else {
-        u1 = mode == MODE_P ? Ap[p + instance_len] : Ap[p];
+        u1 = ap_hi;
         v1 = mode == MODE_P ? aq_lo : aq_hi;
       }
     } else {
@@ -496,14 +495,11 @@ __device__ __forceinline__ void fold2_pair(const PqxArgs& a, Fq* T, int p, uint3
   const long sh = pq_hi(a, p, w, y, mode, &wc);
   lo = fq_zero();
   hi = fq_zero();
-  if (sl >= 0) {
-    lo = fold2_at(T, sl, pinst(a, p), w, F, omr);
-    if (write) out[sl] = lo;
-  }
-  if (sh >= 0) {
-    hi = fold2_at(T, sh, pinst(a, p), wc, F, omr);
-    if (write) out[sh] = hi;
-  }
+  // both folds before either write-back (a store in between would order the hi loads behind the lo product)
+  if (sl >= 0) lo = fold2_at(T, sl, pinst(a, p), w, F, omr);
+  if (sh >= 0) hi = fold2_at(T, sh, pinst(a, p), wc, F, omr);
+  if (write && sl >= 0) out[sl] = lo;
+  if (write && sh >= 0) out[sh] = hi;
 }
 
 template <bool FOLD>
