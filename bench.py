@@ -65,7 +65,7 @@ CONFIGS = {
 # per-launch HBM bytes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, scripts/pmc_traffic.py) of each workload's own
 # run: a kernel's traffic depends on its launch size, so one workload's figures are never reported for another
 TRAFFIC = {w: os.path.join(ROOT, "profiles", f) for w, f in (
-    ("snark", "r04_pmc_traffic.json"), ("msm16", "r03_pmc_traffic_msm_2e16.json"),
+    ("snark", "r04_pmc_traffic.json"), ("msm16", "r04_pmc_traffic_msm_2e16.json"),
     ("spark24", "r03_pmc_traffic_spark_2e24.json"), ("rows", "r04_pmc_traffic_rows_1024.json"),
     ("r1cs22", "r04_pmc_traffic_r1cs_2e22.json"))}
 
@@ -199,11 +199,17 @@ class Prof(dict):
     busy_resident_us = 0.0
 
 
+# scopes that share a device kernel with another scope: the PMC passes name the kernel (scripts/pmc_traffic.py), and a
+# workload's own traffic file holds only its own launches of it
+SCOPE_KERNEL = {"msm_comb_single": "msm_comb"}
+
+
 def traffic_of(kernel, traffic_file):
     if traffic_file and os.path.exists(traffic_file):
-        tr = json.load(open(traffic_file))
-        if kernel in tr.get("kernels", {}):
-            return tr["kernels"][kernel]["hbm_bytes_per_launch"]
+        tr = json.load(open(traffic_file)).get("kernels", {})
+        for k in (kernel, SCOPE_KERNEL.get(kernel)):
+            if k in tr:
+                return tr[k]["hbm_bytes_per_launch"]
     return None
 
 
