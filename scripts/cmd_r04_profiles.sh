@@ -1,6 +1,8 @@
 # kernel stats + PMC traffic of the single-GPU extras, each from its own workload run (nested gpu_run.sh calls
 # with only the profiling steps: the outer call's TESTS / BENCH / CMD switches are cleared)
-for w in ${PROFILE_WORKLOADS:-"msm:--workload msm" "rows:--workload rows" "r1cs22:--workload r1cs --config r1cs_2e22_p8" "spark24:--workload spark --log-nnz 24"}; do
+# PROFILE_WORKLOADS: "tag:bench args|tag:bench args|..."
+IFS='|' read -r -a WL <<< "${PROFILE_WORKLOADS:-msm:--workload msm|rows:--workload rows|r1cs22:--workload r1cs --config r1cs_2e22_p8|spark24:--workload spark --log-nnz 24}"
+for w in "${WL[@]}"; do
   tag=${w%%:*}; args=${w#*:}
   env -u TESTS -u BENCH -u CMD -u SMOKE TAG=${tag}_ PROF=1 PMC=1 PROF_ARGS="$args" T_PROF=300 bash scripts/gpu_run.sh || exit 1
 done
