@@ -392,9 +392,10 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
 // sum_i s_i G[gen_offset + i] (+ blind h) of n device scalars, into *out (host point)
 int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
                    const Fq* d_blind, h::HExt* out) {
-  // large MSMs over a generator set that can keep a comb table (comb.hip; <= 2^16 generators, 47 GB at c = 9):
-  // no digit sort and no bucket reduction (SPG_BIG_COMB=0: always the bucket pipeline below)
-  static const bool comb_on = !getenv("SPG_BIG_COMB") || atoi(getenv("SPG_BIG_COMB")) != 0;
+  // SPG_BIG_COMB=1: large MSMs over a generator set that can keep a comb table (comb.hip; <= 2^16 generators, 47 GB
+  // at c = 9) take it -- no digit sort, no bucket reduction. Off by default: same-box A/B at 2^16 points, 0.204-0.209
+  // ms per call for the buckets below against 0.210-0.213 ms (profiles/r04_ab_combwgs_bigcomb.txt)
+  static const bool comb_on = getenv("SPG_BIG_COMB") && atoi(getenv("SPG_BIG_COMB")) != 0;
   if (comb_on && n >= ((size_t)1 << 14)) {
     const int rc = msm_single_comb(ctx, g, gen_offset, d_scalars, n, d_blind, out);
     if (rc != 1) return rc;

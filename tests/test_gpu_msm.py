@@ -188,10 +188,34 @@ def gens_big(ctx):
 
 
 def test_msm_big_edge_and_skew(ctx, oracle, gens_big):
-    """one MSM larger than the latency path (msm_big.hip; >= 2^14 points: from the comb table, comb.hip
-    msm_single_comb): edge scalars, an all-zero stretch, a bucket holding most
-    entries (one scalar repeated: its digits pile into a few buckets, which split into many chunks), a blind, and
-    a generator offset, against the oracle"""
+    """one MSM larger than the latency path (msm_big.hip's bucket pipeline, the default): edge scalars, an all-zero
+    stretch, a bucket holding most entries (one scalar repeated: its digits pile into a few buckets, which split into
+    many chunks), a blind, and a generator offset, against the oracle"""
+    edge_and_skew_checks(oracle, gens_big)
+
+
+def test_msm_single_comb_edge_and_skew():
+    """the same checks through the comb table (SPG_BIG_COMB=1: comb.hip msm_single_comb, c = 9 windows over the
+    20001-slot table), in a fresh process that reads the switch"""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path[:0] = [%r, %r, %r]\n"
+        "import spg, pyoracle\n"
+        "from test_gpu_msm import edge_and_skew_checks\n"
+        "ctx = spg.Context(0)\n"
+        "edge_and_skew_checks(pyoracle, spg.Gens(ctx, 20000, b'spg_big_msm'))\n"
+        "print('ok')\n"
+    ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "oracle"), os.path.join(root, "tests"))
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_COMB="1"), capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[-1] == "ok"
+
+
+def edge_and_skew_checks(oracle, gens_big):
     n = 20000
     pts = gens_big.compressed()
     rng = np.random.default_rng(20000)
@@ -218,7 +242,7 @@ def test_msm_big_edge_and_skew(ctx, oracle, gens_big):
 @pytest.mark.parametrize("c", ["8", "10", "13", "14"])
 def test_msm_big_windows(oracle, c):
     """every window width of the large-MSM bucket path (SPG_BIG_C with SPG_BIG_COMB=0, a fresh process reads them)
-    gives the oracle's 2^16 MSM (the default takes the comb table for MSMs of >= 2^14 points)"""
+    gives the oracle's 2^16 MSM"""
     import subprocess
     import sys
 
