@@ -1,4 +1,4 @@
-# kernel stats + PMC traffic of the single-GPU extras, each from its own workload run (nested gpu_run.sh calls
+# kernel stats + PMC traffic of the single-GPU extras (run as CMD of scripts/gpu_run.sh), each from its own workload run (nested gpu_run.sh calls
 # with only the profiling steps: the outer call's TESTS / BENCH / CMD switches are cleared)
 # PROFILE_WORKLOADS: "tag:bench args|tag:bench args|..."
 IFS='|' read -r -a WL <<< "${PROFILE_WORKLOADS:-msm:--workload msm|rows:--workload rows|r1cs22:--workload r1cs --config r1cs_2e22_p8|spark24:--workload spark --log-nnz 24}"
