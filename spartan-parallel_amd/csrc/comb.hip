@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256) k_comb_join(const Ext* __restrict__ part,
   if (q == 0) out[b] = acc;
 }
 
-// comb tables of all live generator sets, against the process-wide cap (SPG_COMB_GB, default 24)
+// comb tables of all live generator sets, against the process-wide cap (SPG_COMB_GB, default 96)
 static std::atomic<size_t> g_comb_bytes{0};
 
 void comb_free(const spg_gens* g) {
