@@ -14,6 +14,7 @@ for set in "$@"; do
     bhost) AB_KERNEL=msm_bullet_round bash scripts/ab_env.sh SPG_BULLET_HOST_MAX "0 8 32" 2 ;;
     build) AB_KERNEL=${AB_KERNEL:-sc_phase1_fold_eval,sc_phase2_fold_eval,spark_layer_round,msm_bullet_round} \
              bash scripts/ab_env.sh SPG_LIB "$L/libspg_prev.so $L/libspg.so" ${AB_REPS:-3} ;;
+    zside) AB_KERNEL=z_fill,spmv_block,sc_phase1_fold_eval bash scripts/ab_env.sh SPG_Z_SIDE "0 1" ${AB_REPS:-3} ;;
     combwgs) AB_KERNEL=msm_comb bash scripts/ab_env.sh SPG_COMB_WGS "1024 2048 4096" 2 ;;
     bigcomb) AB_KERNEL=msm_comb_single,msm_big_accum,msm_big_sort BENCH_ARGS="--workload msm" \
                bash scripts/ab_env.sh SPG_BIG_COMB "0 1" 3 ;;

@@ -363,6 +363,7 @@ extern "C" int spg_init(int device, spg_ctx** out) {
       hipEventCreateWithFlags(&c->ev_cx, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->d_counter, 64) != hipSuccess ||
       hipMemset(c->d_counter, 0, 64) != hipSuccess) {
     delete c;
@@ -403,6 +404,7 @@ extern "C" int spg_free(spg_ctx* c) {
   hipEventDestroy(c->ev1);
   if (c->ev_cx) hipEventDestroy(c->ev_cx);
   if (c->ev_pre) hipEventDestroy(c->ev_pre);
+  if (c->ev_side) hipEventDestroy(c->ev_side);
   if (c->stream2) {
     hipStreamSynchronize(c->stream2);
     hipStreamDestroy(c->stream2);

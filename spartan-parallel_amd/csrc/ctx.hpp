@@ -21,6 +21,8 @@ struct spg_ctx {
   // ev_pre marks the point of `stream` they follow (everything queued before that MSM)
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_pre = nullptr;
+  // R1CS proof: the Z table's fill on `stream2` (beside Az/Bz/Cz and phase 1 on `stream`); phase 2 waits on it
+  hipEvent_t ev_side = nullptr;
   void* pinned = nullptr;          // page-locked host staging (pinned_get), grown on demand
   size_t pinned_bytes = 0;
   void* enc_stage = nullptr;       // page-locked staging of points encoded on the host (enc_stage_get)

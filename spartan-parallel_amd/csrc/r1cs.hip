@@ -89,7 +89,7 @@ __global__ void k_z_fill(const ZDesc* __restrict__ zd, int P, const SecDesc* __r
 }
 
 struct SpDesc {
-  uint64_t dom_off, out_off, z_off;
+  uint64_t dom_off, out_off;
   uint32_t pi, lg_q, nrows, lg_rows, ni, lg_ni;
 };
 struct MatDesc {
@@ -97,10 +97,12 @@ struct MatDesc {
   uint64_t cp;
 };
 
-// Az/Bz/Cz[p][q_rev][x_rev] = sum_e val_e * z[p][q][col_e / Y][col_e % Y]
+// Az/Bz/Cz[p][q_rev][x_rev] = sum_e val_e * z[p][q][col_e / Y][col_e % Y], z gathered from the witness sections
+// themselves (the mapping k_z_fill applies), so the Z table's fill is off this kernel's path
 __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int P, const MatDesc* __restrict__ md,
                                               const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
-                                              const Fq* __restrict__ val, const Fq* __restrict__ Z, int nws, uint32_t Y,
+                                              const Fq* __restrict__ val, const SecDesc* __restrict__ sec,
+                                              const Fq* __restrict__ wbuf, int nws, uint32_t Y,
                                               Fq* __restrict__ Az, Fq* __restrict__ Bz, Fq* __restrict__ Cz,
                                               uint64_t total) {
   uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -109,9 +111,7 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
   const SpDesc d = sd[p];
   uint64_t loc = t - d.dom_off;
   uint32_t row = (uint32_t)(loc % d.nrows), q = (uint32_t)(loc / d.nrows);
-  uint32_t qr = brev(q, d.lg_q);
-  const Fq* zq = Z + d.z_off + (size_t)qr * nws * d.ni;
-  size_t o = d.out_off + (size_t)qr * d.nrows + brev(row, d.lg_rows);
+  size_t o = d.out_off + (size_t)brev(q, d.lg_q) * d.nrows + brev(row, d.lg_rows);
   Fq* outs[3] = {Az, Bz, Cz};
 #pragma unroll
   for (int m = 0; m < 3; m++) {
@@ -121,7 +121,10 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
     for (uint32_t e = e0; e < e1; e++) {
       uint32_t c = col[e];
       uint32_t w = c / Y, i = c % Y;
-      if (w < (uint32_t)nws && i < d.ni) s = fq_add(s, fq_mul(val[e], zq[(size_t)w * d.ni + brev(i, d.lg_ni)]));
+      if (w < (uint32_t)nws && i < d.ni) {
+        const SecDesc x = sec[(size_t)w * P + p];
+        if (i < x.ni) s = fq_add(s, fq_mul(val[e], wbuf[x.off + (size_t)(x.np == 1 ? 0 : q) * x.ni + i]));
+      }
     }
     outs[m][o] = s;
   }
@@ -603,6 +606,19 @@ int Prover::run_inner(Laps& lp) {
   Zp.num_inputs = l_inputs;
   Zp.d = (Fq*)ws_get(ctx, WS_Z, ztot * sizeof(Fq) + 64);
   if (!Zp.d) return set_err(ctx, SPG_E_NOMEM, "Z table");
+  static const bool z_side = !getenv("SPG_Z_SIDE") || atoi(getenv("SPG_Z_SIDE")) != 0;
+  // whatever way this returns, `stream` is ordered after the fill before anything later reuses the Z slot
+  struct SideJoin {
+    spg_ctx* c;
+    bool armed = false;
+    int join() {
+      if (!armed) return 0;
+      armed = false;
+      return hipStreamWaitEvent(c->stream, c->ev_side, 0) == hipSuccess ? 0 : set_err(c, SPG_E_HIP, "z_fill join");
+    }
+    ~SideJoin() { join(); }
+  } z_join{ctx};
+  SecDesc* dsec = nullptr;
   {
     std::vector<ZDesc> zd(PLn);
     std::vector<SecDesc> sd(nws * PLn);
@@ -621,14 +637,28 @@ int Prover::run_inner(Laps& lp) {
       }
     }
     ZDesc* dz;
-    SecDesc* ds;
     int rc = upload_desc(zd, 0, &dz);
-    if (!rc) rc = upload_desc(sd, 65536, &ds);
+    if (!rc) rc = upload_desc(sd, 65536, &dsec);
     if (rc) return rc;
-    KScope ks(ctx, "z_fill", 64.0 * ztot);
-    hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, s, dz, (int)PLn, ds, (int)nws, wit.d_w, Zp.d,
-                       (uint64_t)ztot);
+    // k_spmv gathers from the witness itself, so the fill only has to land before phase 2: on the second stream
+    // it overlaps Az/Bz/Cz and the phase-1 rounds (same-box A/B: DESIGN §4, round 4)
+    const hipStream_t main_stream = ctx->stream;
+    if (z_side) {
+      SPG_HIP(ctx, hipEventRecord(ctx->ev_pre, main_stream));
+      SPG_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_pre, 0));
+      ctx->stream = ctx->stream2;
+    }
+    {
+      KScope ks(ctx, "z_fill", 64.0 * ztot);
+      hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec, (int)nws,
+                         wit.d_w, Zp.d, (uint64_t)ztot);
+    }
+    ctx->stream = main_stream;
     SPG_HIP(ctx, hipGetLastError());
+    if (z_side) {
+      SPG_HIP(ctx, hipEventRecord(ctx->ev_side, ctx->stream2));
+      z_join.armed = true;
+    }
   }
 
   // ---- tau tables (identical on every rank)
@@ -683,7 +713,6 @@ int Prover::run_inner(Laps& lp) {
       size_t pi = inst.num_instances == 1 ? 0 : p0 + p;
       sd[p].dom_off = Az.off[p];
       sd[p].out_off = Az.off[p];
-      sd[p].z_off = Zp.off[p];
       sd[p].pi = (uint32_t)pi;
       sd[p].lg_q = (uint32_t)lg2(l_proofs[p]);
       sd[p].nrows = (uint32_t)l_cons[p];
@@ -698,7 +727,7 @@ int Prover::run_inner(Laps& lp) {
     // outputs, CSR row pointers, and per visited entry its column, value and z gather
     KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
     hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr, inst.d_col,
-                       inst.d_val, Zp.d, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
+                       inst.d_val, dsec, wit.d_w, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
     SPG_HIP(ctx, hipGetLastError());
   }
 
@@ -897,6 +926,8 @@ int Prover::run_inner(Laps& lp) {
                        inst.d_cval, eq_rx, (uint32_t)Y, r_A, r_B, r_C, ABC.d, (uint64_t)btot);
     SPG_HIP(ctx, hipGetLastError());
   }
+  rc = z_join.join();  // the Z table's first use
+  if (rc) return rc;
   for (size_t k = 0; k < rq_rev.size(); k++) {  // Z.bound_poly_vars_rq(rq_rev)
     rc = pqx_bound(ctx, Zp, nullptr, nullptr, rq_rev[k], MODE_Q);
     if (rc) return rc;
