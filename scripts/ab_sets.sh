@@ -11,6 +11,7 @@ for set in "$@"; do
     bcomb) AB_KERNEL=msm_bullet_round bash scripts/ab_env.sh SPG_BULLET_COMB "0 1" 2 ;;
     bshape) AB_KERNEL=msm_bullet_round bash scripts/ab_env.sh SPG_BCOMB_R "4 8 16" 2 &&
             AB_KERNEL=msm_bullet_round bash scripts/ab_env.sh SPG_BCOMB_G "8 11" 2 ;;
+    bbs) AB_KERNEL=msm_bullet_round bash scripts/ab_env.sh SPG_BCOMB_BS "0 64 128" 2 ;;
     bhost) AB_KERNEL=msm_bullet_round bash scripts/ab_env.sh SPG_BULLET_HOST_MAX "0 8 32" 2 ;;
     build) AB_KERNEL=${AB_KERNEL:-sc_phase1_fold_eval,sc_phase2_fold_eval,spark_layer_round,msm_bullet_round} \
              bash scripts/ab_env.sh SPG_LIB "$L/libspg_prev.so $L/libspg.so" ${AB_REPS:-3} ;;

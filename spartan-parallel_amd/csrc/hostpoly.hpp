@@ -1,6 +1,7 @@
 // spg — small host-side helpers shared by the prover drivers (r1cs.hip, spark.hip): sizes, eq tables,
 // round polynomials, scalar (de)serialisation at the C-ABI.
 #pragma once
+#include <initializer_list>
 #include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,6 +37,16 @@ inline void st_fq(uint64_t* v, const Fq& a) {
 inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 inline int eq_table(spg_ctx* ctx, const FqV& r, Fq* out) { return dev_eq_table(ctx, r.data(), (int)r.size(), out); }
+struct EqOut {
+  const FqV& r;
+  Fq* out;
+};
+// the tables one prover step needs together, in as few launches as dev_eq_tables can pack them
+inline int eq_tables(spg_ctx* ctx, std::initializer_list<EqOut> l) {
+  std::vector<EqJob> j;
+  for (const EqOut& e : l) j.push_back({e.r.data(), (int)e.r.size(), e.out});
+  return dev_eq_tables(ctx, j.data(), (int)j.size());
+}
 
 struct Laps {  // SPG_TRACE=1: wall-time breakdown of a host orchestration
   const char* title = "R1CSProof::prove";

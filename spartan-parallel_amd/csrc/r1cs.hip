@@ -42,6 +42,9 @@ struct spg_r1cs_witness {
   size_t nws = 0;
   std::vector<std::vector<size_t>> num_proofs, num_inputs;  // [w][p]
   std::vector<std::vector<uint64_t>> off;                   // [w][p] element offset into d_w
+  // [w][p] device address of the instance's w_mat: d_w + off, or a caller's resident device buffer used in place
+  // (witness_from_parts); nullptr: held by another rank
+  std::vector<std::vector<const spg::Fq*>> ptr;
   spg::Fq* d_w = nullptr;
   size_t total = 0;
 };
@@ -67,13 +70,13 @@ struct ZDesc {
   uint32_t lg_q, ni, lg_ni, pad;
 };
 struct SecDesc {
-  uint64_t off;
+  const Fq* w;  // the instance's w_mat (spg_r1cs_witness::ptr)
   uint32_t np, ni;
 };
 
 // Z[p][q_rev][w][x_rev] = w_mat_w[pw][qw][x]  (zero beyond the section's width)
 __global__ void k_z_fill(const ZDesc* __restrict__ zd, int P, const SecDesc* __restrict__ sd, int nws,
-                         const Fq* __restrict__ wbuf, Fq* __restrict__ Z, uint64_t total) {
+                         Fq* __restrict__ Z, uint64_t total) {
   uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= total) return;
   int p = find_desc(zd, P, t);
@@ -84,7 +87,7 @@ __global__ void k_z_fill(const ZDesc* __restrict__ zd, int P, const SecDesc* __r
   uint32_t w = (uint32_t)(rest % nws), q = (uint32_t)(rest / nws);
   const SecDesc s = sd[(size_t)w * P + p];
   Fq v = fq_zero();
-  if (i < s.ni) v = wbuf[s.off + (size_t)(s.np == 1 ? 0 : q) * s.ni + i];
+  if (i < s.ni) v = s.w[(size_t)(s.np == 1 ? 0 : q) * s.ni + i];
   Z[d.z_off + ((size_t)brev(q, d.lg_q) * nws + w) * d.ni + brev(i, d.lg_ni)] = v;
 }
 
@@ -101,8 +104,8 @@ struct MatDesc {
 // themselves (the mapping k_z_fill applies), so the Z table's fill is off this kernel's path
 __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int P, const MatDesc* __restrict__ md,
                                               const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
-                                              const Fq* __restrict__ val, const SecDesc* __restrict__ sec,
-                                              const Fq* __restrict__ wbuf, int nws, uint32_t Y,
+                                              const Fq* __restrict__ val, const SecDesc* __restrict__ sec, int nws,
+                                              uint32_t Y,
                                               Fq* __restrict__ Az, Fq* __restrict__ Bz, Fq* __restrict__ Cz,
                                               uint64_t total) {
   uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -123,7 +126,7 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
       uint32_t w = c / Y, i = c % Y;
       if (w < (uint32_t)nws && i < d.ni) {
         const SecDesc x = sec[(size_t)w * P + p];
-        if (i < x.ni) s = fq_add(s, fq_mul(val[e], wbuf[x.off + (size_t)(x.np == 1 ? 0 : q) * x.ni + i]));
+        if (i < x.ni) s = fq_add(s, fq_mul(val[e], x.w[(size_t)(x.np == 1 ? 0 : q) * x.ni + i]));
       }
     }
     outs[m][o] = s;
@@ -630,8 +633,8 @@ int Prover::run_inner(Laps& lp) {
       zd[p].lg_ni = (uint32_t)lg2(l_inputs[p]);
       for (size_t w = 0; w < nws; w++) {
         size_t pw = wit.num_proofs[w].size() == 1 ? 0 : p0 + p;
-        if (wit.off[w][pw] == kNotResident) return set_err(ctx, SPG_E_ARG, "witness shard does not hold instance");
-        sd[w * PLn + p].off = wit.off[w][pw];
+        if (!wit.ptr[w][pw]) return set_err(ctx, SPG_E_ARG, "witness shard does not hold instance");
+        sd[w * PLn + p].w = wit.ptr[w][pw];
         sd[w * PLn + p].np = (uint32_t)wit.num_proofs[w][pw];
         sd[w * PLn + p].ni = (uint32_t)wit.num_inputs[w][pw];
       }
@@ -651,7 +654,7 @@ int Prover::run_inner(Laps& lp) {
     {
       KScope ks(ctx, "z_fill", 64.0 * ztot);
       hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec, (int)nws,
-                         wit.d_w, Zp.d, (uint64_t)ztot);
+                         Zp.d, (uint64_t)ztot);
     }
     ctx->stream = main_stream;
     SPG_HIP(ctx, hipGetLastError());
@@ -670,9 +673,7 @@ int Prover::run_inner(Laps& lp) {
   Fq* Aq = (Fq*)ws_get(ctx, WS_TQ, (sizeof(Fq) << nq) + 64);
   Fq* Ax = (Fq*)ws_get(ctx, WS_TX, (sizeof(Fq) << nx) + 64);
   if (!Ap || !Aq || !Ax) return set_err(ctx, SPG_E_NOMEM, "eq tables");
-  int rc = eq_table(ctx, tau_p, Ap);
-  if (!rc) rc = eq_table(ctx, tau_q, Aq);
-  if (!rc) rc = eq_table(ctx, tau_x, Ax);
+  int rc = eq_tables(ctx, {{tau_p, Ap}, {tau_q, Aq}, {tau_x, Ax}});
   if (rc) return rc;
 
   // ---- Az, Bz, Cz = multiply_vec_block (p, q_rev, 0, x_rev) for the local instances
@@ -727,7 +728,7 @@ int Prover::run_inner(Laps& lp) {
     // outputs, CSR row pointers, and per visited entry its column, value and z gather
     KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
     hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr, inst.d_col,
-                       inst.d_val, dsec, wit.d_w, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
+                       inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
     SPG_HIP(ctx, hipGetLastError());
   }
 
@@ -1110,6 +1111,7 @@ int Prover::run_inner(Laps& lp) {
       if (!all_mine) SPG_HIP(ctx, hipMemsetAsync(dout, 0, lz_total * sizeof(Fq), s));  // other ranks' ranges
       // one eq table per distinct rl (polynomials of one shape share it)
       std::vector<size_t> eq_at(jobs.size());
+      std::vector<EqJob> eqs;
       for (size_t k = 0; k < jobs.size(); k++) {
         size_t same = k;
         for (size_t m = 0; m < k; m++)
@@ -1119,11 +1121,10 @@ int Prover::run_inner(Laps& lp) {
             break;
           }
         eq_at[k] = same == k ? jobs[k].offL : eq_at[same];
-        if (same == k) {
-          rc = eq_table(ctx, jobs[k].rl, dL + jobs[k].offL);
-          if (rc) return rc;
-        }
+        if (same == k) eqs.push_back({jobs[k].rl.data(), (int)jobs[k].rl.size(), dL + jobs[k].offL});
       }
+      rc = dev_eq_tables(ctx, eqs.data(), (int)eqs.size());
+      if (rc) return rc;
       std::vector<const PolyRef*> mine;
       for (auto& pr : polys)
         if (pr.mine) mine.push_back(&pr);
@@ -1138,7 +1139,7 @@ int Prover::run_inner(Laps& lp) {
           const BoundJob& j = jobs[k0 + q];
           const PolyRef& pr = *mine[k0 + q];
           const uint32_t nbx = (uint32_t)((j.Rs + 255) / 256);
-          bj.d[q] = {wit.d_w + wit.off[pr.w][pr.p], (uint32_t)eq_at[k0 + q], (uint32_t)j.Ls, (uint32_t)j.Rs,
+          bj.d[q] = {wit.ptr[pr.w][pr.p], (uint32_t)eq_at[k0 + q], (uint32_t)j.Ls, (uint32_t)j.Rs,
                      (uint32_t)j.chunk, (uint32_t)j.S, (uint32_t)j.offP, (uint32_t)j.o, nb, nc};
           nb += nbx * (uint32_t)j.S;
           nc += nbx;
@@ -1506,6 +1507,9 @@ static int witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, si
     delete W;
     return set_err(ctx, SPG_E_NOMEM, "witness upload");
   }
+  W->ptr.resize(nws);
+  for (size_t w = 0; w < nws; w++)
+    for (uint64_t o : W->off[w]) W->ptr[w].push_back(o == kNotResident ? nullptr : W->d_w + o);
   for (size_t w = 0; w < nws; w++)
     for (size_t p = 0; p < secs[w].num_instances; p++) {
       if (W->off[w][p] == kNotResident) continue;
@@ -1539,32 +1543,59 @@ int witness_from_parts(spg_ctx* ctx, const std::vector<WPart>& secs, spg_r1cs_wi
       total += w.num_proofs[p] * w.num_inputs[p];
     }
   }
+  // parts already resident on this device (SNARK::prove's block_vars and exec buffers, alive and unchanged for
+  // the whole prove) are read in place; only host parts are copied into d_w
+  auto on_device = [](const void* q) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();  // an unregistered host pointer: not an error of the prove
+      return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+  };
+  static const bool in_place = !getenv("SPG_WIT_IN_PLACE") || atoi(getenv("SPG_WIT_IN_PLACE")) != 0;
+  std::vector<std::vector<char>> dev(secs.size());
+  size_t host_total = 0;
+  for (size_t w = 0; w < secs.size(); w++)
+    for (size_t p = 0; p < secs[w].num_proofs.size(); p++) {
+      const bool d = in_place && on_device(secs[w].src[p]);
+      dev[w].push_back(d);
+      if (!d) host_total += secs[w].num_proofs[p] * secs[w].num_inputs[p];
+    }
+  (void)total;
   spg_r1cs_witness* W = *inout;
-  if (W && W->total < total) {
+  if (W && W->total < host_total) {
     spg_r1cs_witness_free(ctx, W);
     W = nullptr;
   }
   if (!W) {
     W = new spg_r1cs_witness();
-    if (hipMalloc(&W->d_w, total * sizeof(Fq) + 64) != hipSuccess) {
+    if (hipMalloc(&W->d_w, host_total * sizeof(Fq) + 64) != hipSuccess) {
       delete W;
       *inout = nullptr;
       return set_err(ctx, SPG_E_NOMEM, "witness");
     }
-    W->total = total;
+    W->total = host_total;
   }
   *inout = W;
   W->nws = secs.size();
   W->num_proofs.assign(secs.size(), {});
   W->num_inputs.assign(secs.size(), {});
   W->off.assign(secs.size(), {});
+  W->ptr.assign(secs.size(), {});
   size_t o = 0;
   for (size_t w = 0; w < secs.size(); w++)
     for (size_t p = 0; p < secs[w].num_proofs.size(); p++) {
       size_t n = secs[w].num_proofs[p] * secs[w].num_inputs[p];
       W->num_proofs[w].push_back(secs[w].num_proofs[p]);
       W->num_inputs[w].push_back(secs[w].num_inputs[p]);
+      if (dev[w][p]) {
+        W->off[w].push_back(0);
+        W->ptr[w].push_back(secs[w].src[p]);
+        continue;
+      }
       W->off[w].push_back(o);
+      W->ptr[w].push_back(W->d_w + o);
       SPG_HIP(ctx, hipMemcpyAsync(W->d_w + o, secs[w].src[p], n * sizeof(Fq), hipMemcpyDefault, ctx->stream));
       o += n;
     }
@@ -1728,8 +1759,7 @@ extern "C" int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, 
   SPG_HIP(ctx, hipMemcpyAsync(dmd, md.data(), Pm * sizeof(MatDesc), hipMemcpyHostToDevice, s));
   SPG_HIP(ctx, hipMemcpyAsync(drr, rr.data(), 2 * Pm * 4, hipMemcpyHostToDevice, s));
   timer_start(ctx);
-  int rc = eq_table(ctx, vx, erx);
-  if (!rc) rc = eq_table(ctx, vy, ery);
+  int rc = eq_tables(ctx, {{vx, erx}, {vy, ery}});
   if (rc) return rc;
   {
     KScope ks(ctx, "sparse_eval", 68.0 * visits + 40.0 * rows);

@@ -147,8 +147,13 @@ int sat_prove(spg_ctx* ctx, spg_r1cs_gens* gens, spg_r1cs_inst* inst, size_t P, 
               const std::vector<size_t>& num_proofs, size_t max_ni, const std::vector<size_t>& num_inputs,
               const std::vector<WPart>& secs, spg_r1cs_witness** W, spg_transcript* t, spg_random_tape* tape,
               SatOut* out) {
+  Laps lp;
+  lp.title = "sat_prove";
+  lp.on = lp.on && atoi(getenv("SPG_TRACE")) >= 2;
   int rc = witness_from_parts(ctx, secs, W);
   if (rc) return rc;
+  lp.lap("witness_from_parts");
+  lp.print();
   std::vector<uint8_t> buf(1 << 22);
   std::vector<uint64_t> ch(4 * 4096);
   size_t len = 0, chl[4] = {0, 0, 0, 0};

@@ -155,14 +155,11 @@ __device__ __forceinline__ Fq eq_bits(const Fq* rv, int ell, int k0, int nb, uin
 // split into two groups of <= 4 whose 16-entry factor tables and the block's high-bit product are built
 // by lanes of three different waves at once, then every entry is two multiplications. A lane's chain is
 // ~5 products instead of ell - 1 (+ ell/4 grouping): the launch is latency-bound at these sizes.
-template <bool BLOB>
-__global__ void __launch_bounds__(256) k_eq_table_lds(FqArg32 r, Fq* __restrict__ out, size_t n, KBlob blob,
-                                                      uint32_t* __restrict__ blob_dst) {
+// the table's entries [bid * 256, bid * 256 + 256) of one block
+__device__ __forceinline__ void eq_lds_block(const FqArg32& r, Fq* __restrict__ out, size_t n, uint32_t bid) {
   __shared__ Fq s_lo[16], s_mid[16], s_hi;
   __shared__ Fq s_r[32];
   const int t = threadIdx.x;
-  if (BLOB && blockIdx.x == 0)
-    for (int i = t; i < blob.nwords; i += blockDim.x) blob_dst[i] = blob.w[i];
   const int ell = r.n;
   // the challenges reach LDS in one parallel round trip (one word per lane) instead of a chain of
   // scalar loads from the argument segment inside every lane's product loop
@@ -172,13 +169,34 @@ __global__ void __launch_bounds__(256) k_eq_table_lds(FqArg32 r, Fq* __restrict_
   const int nlo = lb >> 1, nmid = lb - nlo, nhi = ell - lb;
   if (t < (1 << nlo)) s_lo[t] = eq_bits(s_r, ell, 0, nlo, (uint32_t)t);
   else if (t >= 64 && t < 64 + (1 << nmid)) s_mid[t - 64] = eq_bits(s_r, ell, nlo, nmid, (uint32_t)(t - 64));
-  else if (t == 128) s_hi = eq_bits(s_r, ell, lb, nhi, (uint32_t)blockIdx.x);
+  else if (t == 128) s_hi = eq_bits(s_r, ell, lb, nhi, bid);
   __syncthreads();
-  const size_t b = (size_t)blockIdx.x * blockDim.x + t;
+  const size_t b = (size_t)bid * blockDim.x + t;
   if (b >= n) return;
   Fq v = fq_mul(s_mid[t >> nlo], s_lo[t & ((1 << nlo) - 1)]);
   if (nhi) v = fq_mul(v, s_hi);
   out[b] = v;
+}
+
+// Same table from LDS sub-tables: a block owns 2^lb consecutive entries (lb = min(ell, 8)); the low bits
+// split into two groups of <= 4 whose 16-entry factor tables and the block's high-bit product are built
+// by lanes of three different waves at once, then every entry is two multiplications. A lane's chain is
+// ~5 products instead of ell - 1 (+ ell/4 grouping): the launch is latency-bound at these sizes.
+template <bool BLOB>
+__global__ void __launch_bounds__(256) k_eq_table_lds(FqArg32 r, Fq* __restrict__ out, size_t n, KBlob blob,
+                                                      uint32_t* __restrict__ blob_dst) {
+  if (BLOB && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < blob.nwords; i += blockDim.x) blob_dst[i] = blob.w[i];
+  eq_lds_block(r, out, n, blockIdx.x);
+}
+
+// up to three tables in one launch (their blocks back to back): the tables a prover needs at one point
+// (tau_p, tau_q, tau_x; eq(rx), eq(ry); ...) cost one launch on the stream instead of one each
+__global__ void __launch_bounds__(256) k_eq_tables_lds(EqTablesArg a) {
+  const uint32_t bx = blockIdx.x;
+  if (a.nj > 2 && bx >= a.b0[2]) eq_lds_block(a.r[2], a.out[2], a.n[2], bx - a.b0[2]);
+  else if (a.nj > 1 && bx >= a.b0[1]) eq_lds_block(a.r[1], a.out[1], a.n[1], bx - a.b0[1]);
+  else eq_lds_block(a.r[0], a.out[0], a.n[0], bx);
 }
 
 // factored form for large tables: out[b] = hi[b >> lo_bits] * lo[b & (2^lo_bits - 1)]
@@ -726,6 +744,47 @@ int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out, const KBlob* blob,
   }
   SPG_HIP(ctx, hipGetLastError());
   return 0;
+}
+
+int dev_eq_tables(spg_ctx* ctx, const EqJob* jobs, int nj) {
+  static const bool lds_on = !getenv("SPG_EQ_LDS") || atoi(getenv("SPG_EQ_LDS")) != 0;
+  static const bool multi_on = !getenv("SPG_EQ_MULTI") || atoi(getenv("SPG_EQ_MULTI")) != 0;
+  EqTablesArg a;
+  a.nj = 0;
+  uint32_t blocks = 0;
+  double bytes = 0;
+  auto flush = [&]() -> int {
+    if (!a.nj) return 0;
+    KScope ks(ctx, "eq_table", bytes);
+    hipLaunchKernelGGL(k_eq_tables_lds, dim3(blocks), dim3(256), 0, ctx->stream, a);
+    a.nj = 0;
+    blocks = 0;
+    bytes = 0;
+    SPG_HIP(ctx, hipGetLastError());
+    return 0;
+  };
+  for (int k = 0; k < nj; k++) {
+    const EqJob& j = jobs[k];
+    if (j.ell < 0 || j.ell > 32) return set_err(ctx, SPG_E_ARG, "eq table: too many variables");
+    if (!multi_on || !lds_on || j.ell > 16) {  // the one-table path (large tables: factored form)
+      int rc = dev_eq_table(ctx, j.r, j.ell, j.out);
+      if (rc) return rc;
+      continue;
+    }
+    const size_t n = (size_t)1 << j.ell;
+    a.r[a.nj].n = j.ell;
+    for (int i = 0; i < j.ell; i++) a.r[a.nj].v[i] = j.r[i];
+    a.out[a.nj] = j.out;
+    a.n[a.nj] = n;
+    a.b0[a.nj] = blocks;
+    blocks += (uint32_t)((n + 255) / 256);
+    bytes += 32.0 * n;
+    if (++a.nj == EqTablesArg::kMax) {
+      int rc = flush();
+      if (rc) return rc;
+    }
+  }
+  return flush();
 }
 
 int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r) {

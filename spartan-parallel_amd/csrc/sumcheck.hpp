@@ -24,6 +24,22 @@ struct KBlob {
 };
 // EqPolynomial::evals(r[0..ell]) into out[2^ell] (device); with blob, also blob->w[0..nwords) -> blob_dst
 int dev_eq_table(spg_ctx* ctx, const Fq* r, int ell, Fq* out, const KBlob* blob = nullptr, void* blob_dst = nullptr);
+// several EqPolynomial::evals tables at once: tables of <= 2^16 entries share launches (up to
+// EqTablesArg::kMax per launch), larger ones go through dev_eq_table
+struct EqJob {
+  const Fq* r;
+  int ell;
+  Fq* out;
+};
+struct EqTablesArg {  // kernel argument of k_eq_tables_lds
+  static constexpr int kMax = 3;
+  FqArg32 r[kMax];
+  Fq* out[kMax];
+  uint64_t n[kMax];
+  uint32_t b0[kMax];  // first block of table k
+  int nj;
+};
+int dev_eq_tables(spg_ctx* ctx, const EqJob* jobs, int nj);
 // DensePolynomial::bound_poly_var_top on a device vector of length len
 int dev_fold_top(spg_ctx* ctx, Fq* v, size_t len, const Fq& r);
 
