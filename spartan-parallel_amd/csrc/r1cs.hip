@@ -183,7 +183,8 @@ __global__ void k_sum_cols(const Fq* __restrict__ part, uint32_t S, uint32_t Rs,
 }
 
 // every witness polynomial's L.Z bound of one proof in two launches (instead of two per polynomial): job k's
-// partial rows are blocks [b0, b0 + nbx * S) of the first launch, its column sums blocks [c0, c0 + nbx) of the second
+// partial rows are blocks [b0, b0 + nbx * S) of the first launch, its column sums blocks
+// [c0, c0 + ceil(Rs / kSumCols)) of the second
 struct BoundDesc {
   const Fq* Z;
   uint32_t offL, Ls, Rs, chunk, S, offP, o, b0, c0;
@@ -209,14 +210,27 @@ __global__ void __launch_bounds__(256) k_bound_part_multi(BoundJobs jobs, const 
   for (uint32_t j = j0; j < j1; j++) acc = fq_add(acc, fq_mul(L[d.offL + j], d.Z[(size_t)j * d.Rs + i]));
   part[d.offP + (size_t)y * d.Rs + i] = acc;
 }
+// a block owns kSumCols columns of one job and 256 / kSumCols lanes per column split its S partials, then an LDS
+// tree (one lane per column made S dependent additions)
+constexpr int kSumCols = 16;
 __global__ void __launch_bounds__(256) k_sum_cols_multi(BoundJobs jobs, const Fq* __restrict__ part, Fq* __restrict__ out) {
+  __shared__ Fq sm[256];
+  constexpr int YL = 256 / kSumCols;
   const int k = bound_job(jobs, blockIdx.x, true);
   const BoundDesc& d = jobs.d[k];
-  const uint32_t i = (blockIdx.x - d.c0) * 256 + threadIdx.x;
-  if (i >= d.Rs) return;
+  const int t = threadIdx.x, y0 = t / kSumCols;
+  const uint32_t i = (blockIdx.x - d.c0) * kSumCols + t % kSumCols;
   Fq acc = fq_zero();
-  for (uint32_t y = 0; y < d.S; y++) acc = fq_add(acc, part[d.offP + (size_t)y * d.Rs + i]);
-  out[d.o + i] = acc;
+  if (i < d.Rs)
+    for (uint32_t y = y0; y < d.S; y += YL) acc = fq_add(acc, part[d.offP + (size_t)y * d.Rs + i]);
+  sm[t] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int h = YL / 2; h >= 1; h >>= 1) {
+    if (y0 < h) sm[t] = fq_add(sm[t], sm[t + kSumCols * h]);
+    __syncthreads();
+  }
+  if (y0 == 0 && i < d.Rs) out[d.o + i] = sm[t];
 }
 
 // SparseMatPolynomial::evaluate_with_tables (src/sparse_mlpoly.rs:427-436) for every matrix of the
@@ -1142,7 +1156,7 @@ int Prover::run_inner(Laps& lp) {
           bj.d[q] = {wit.ptr[pr.w][pr.p], (uint32_t)eq_at[k0 + q], (uint32_t)j.Ls, (uint32_t)j.Rs,
                      (uint32_t)j.chunk, (uint32_t)j.S, (uint32_t)j.offP, (uint32_t)j.o, nb, nc};
           nb += nbx * (uint32_t)j.S;
-          nc += nbx;
+          nc += (uint32_t)((j.Rs + kSumCols - 1) / kSumCols);
         }
         hipLaunchKernelGGL(k_bound_part_multi, dim3(nb), dim3(256), 0, s, bj, dL, dpart);
         hipLaunchKernelGGL(k_sum_cols_multi, dim3(nc), dim3(256), 0, s, bj, dpart, dout);

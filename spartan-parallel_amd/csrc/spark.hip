@@ -266,12 +266,26 @@ __global__ void __launch_bounds__(256) k_bound_rows(const Fq* __restrict__ Z, co
   for (size_t j = j0; j < j1; j++) acc = fq_add(acc, fq_mul(L[j], Z[j * Rs + i]));
   part[(size_t)blockIdx.y * Rs + i] = acc;
 }
-__global__ void k_bound_sum(const Fq* __restrict__ part, size_t S, size_t Rs, Fq* __restrict__ out) {
-  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= Rs) return;
+// out[i] = sum_y part[y][i]: a block owns 16 columns and 16 lanes per column split the S partials (S reaches
+// thousands when Rs is small, and one lane per column made that a chain of S dependent additions), then an LDS tree
+constexpr int kBoundSumCols = 16;
+__global__ void __launch_bounds__(256) k_bound_sum(const Fq* __restrict__ part, size_t S, size_t Rs,
+                                                   Fq* __restrict__ out) {
+  __shared__ Fq sm[256];
+  const int t = threadIdx.x, c = t % kBoundSumCols, y0 = t / kBoundSumCols;
+  const size_t i = (size_t)blockIdx.x * kBoundSumCols + c;
+  constexpr int YL = 256 / kBoundSumCols;
   Fq acc = fq_zero();
-  for (size_t y = 0; y < S; y++) acc = fq_add(acc, part[y * Rs + i]);
-  out[i] = acc;
+  if (i < Rs)
+    for (size_t y = y0; y < S; y += YL) acc = fq_add(acc, part[y * Rs + i]);
+  sm[t] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int h = YL / 2; h >= 1; h >>= 1) {
+    if (y0 < h) sm[t] = fq_add(sm[t], sm[t + kBoundSumCols * h]);
+    __syncthreads();
+  }
+  if (y0 == 0 && i < Rs) out[i] = sm[t];
 }
 
 }  // namespace spg
@@ -491,7 +505,8 @@ int poly_eval_prove(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, const FqV& r, co
       KScope ks(ctx, "spark_bound", 32.0 * (double)Lm * Rs + 64.0 * S * Rs);
       hipLaunchKernelGGL(k_bound_rows, dim3(nblk(Rs), (unsigned)S), dim3(256), 0, ctx->stream, d_Z + j0 * Rs, dL + j0,
                          Lm, Rs, chunk, dpart);
-      hipLaunchKernelGGL(k_bound_sum, dim3(nblk(Rs)), dim3(256), 0, ctx->stream, dpart, S, Rs, dout);
+      hipLaunchKernelGGL(k_bound_sum, dim3((unsigned)((Rs + kBoundSumCols - 1) / kBoundSumCols)), dim3(256), 0,
+                         ctx->stream, dpart, S, Rs, dout);
       if (hipGetLastError() != hipSuccess) rc = set_err(ctx, SPG_E_HIP, "poly_eval_prove launch");
     }
     if (!rc) rc = d2h_fq(ctx, dout, LZ.data(), Rs);
@@ -1402,8 +1417,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     rc = comm_allgather(ctx, sh, rc, nullptr, 0, none);
   }
   if (rc) return rc;
-  rc = eq_table(ctx, ex, mem_rx);
-  if (!rc) rc = eq_table(ctx, ey, mem_ry);
+  rc = eq_tables(ctx, {{ex, mem_rx}, {ey, mem_ry}});
   if (rc) return rc;
   // Derefs (sparse_mlpoly.rs:51-67): comb = row derefs ++ col derefs, zero-padded
   if (der_len > 2 * BN) SPG_HIP(ctx, hipMemsetAsync(derefs + 2 * BN, 0, (der_len - 2 * BN) * sizeof(Fq), s));
@@ -1534,8 +1548,7 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
   lp.lap("layer_sumchecks");
   // ---- HashLayerProof (sparse_mlpoly.rs:805-918)
   t.protocol("Sparse polynomial hash layer proof");
-  rc = eq_table(ctx, rand_ops, eq_ops);
-  if (!rc) rc = eq_table(ctx, rand_mem, eq_mem);
+  rc = eq_tables(ctx, {{rand_ops, eq_ops}, {rand_mem, eq_mem}});
   if (rc) return rc;
   FqV ev_der, ev_ops, ev_mem;
   rc = seg_dots_multi(ctx, {{derefs, N, 2 * B, eq_ops, N, &ev_der}, {S->d_comb_ops, N, 5 * B, eq_ops, N, &ev_ops},
