@@ -415,17 +415,27 @@ struct Prover {
   Prover(spg_ctx* c, ProverGens& gg, const spg_r1cs_inst& in, const spg_r1cs_witness& w, Tr& tt, Tape& tp)
       : ctx(c), g(gg), inst(in), wit(w), t(tt), tape(tp) {}
 
+  // descriptors are staged in desc_host (256-byte aligned, at most 1 MB per proof) and go up to the device in one
+  // copy per flush_desc(); a staged descriptor's device address is valid for kernels launched after that flush
+  size_t desc_cur = 0, desc_done = 0;
+  uint8_t* desc_dev = nullptr;
   template <class D>
-  int upload_desc(const std::vector<D>& v, size_t byte_off, D** dptr) {
-    uint8_t* base = (uint8_t*)ws_get(ctx, WS_DESC, 1 << 20);
-    if (!base) return set_err(ctx, SPG_E_NOMEM, "descriptor buffer");
-    size_t bytes = v.size() * sizeof(D);
-    if (byte_off + bytes > (1 << 20)) return set_err(ctx, SPG_E_ARG, "too many descriptors");
-    if (desc_host.size() < byte_off + bytes) desc_host.resize(byte_off + bytes);
-    memcpy(desc_host.data() + byte_off, v.data(), bytes);
-    SPG_HIP(ctx, hipMemcpyAsync(base + byte_off, desc_host.data() + byte_off, bytes, hipMemcpyHostToDevice,
-                                ctx->stream));
-    *dptr = (D*)(base + byte_off);
+  int stage_desc(const std::vector<D>& v, D** dptr) {
+    if (!desc_dev && !(desc_dev = (uint8_t*)ws_get(ctx, WS_DESC, 1 << 20)))
+      return set_err(ctx, SPG_E_NOMEM, "descriptor buffer");
+    const size_t bytes = v.size() * sizeof(D), off = (desc_cur + 255) & ~(size_t)255;
+    if (off + bytes > (1 << 20)) return set_err(ctx, SPG_E_ARG, "too many descriptors");
+    if (desc_host.size() < off + bytes) desc_host.resize(off + bytes);
+    memcpy(desc_host.data() + off, v.data(), bytes);
+    *dptr = (D*)(desc_dev + off);
+    desc_cur = off + bytes;
+    return 0;
+  }
+  int flush_desc() {
+    if (desc_cur > desc_done)
+      SPG_HIP(ctx, hipMemcpyAsync(desc_dev + desc_done, desc_host.data() + desc_done, desc_cur - desc_done,
+                                  hipMemcpyHostToDevice, ctx->stream));
+    desc_done = desc_cur;
     return 0;
   }
 
@@ -623,6 +633,29 @@ int Prover::run_inner(Laps& lp) {
   Zp.num_inputs = l_inputs;
   Zp.d = (Fq*)ws_get(ctx, WS_Z, ztot * sizeof(Fq) + 64);
   if (!Zp.d) return set_err(ctx, SPG_E_NOMEM, "Z table");
+  // ---- Az, Bz, Cz = multiply_vec_block (p, q_rev, 0, x_rev) for the local instances
+  PqxDev Az;
+  Az.zlen = PLn;
+  Az.off.resize(PLn);
+  Az.anp = l_proofs;
+  Az.anw.assign(PLn, 1);
+  Az.ani = l_cons;
+  size_t atot = 0;
+  for (size_t p = 0; p < PLn; p++) {
+    Az.off[p] = atot;
+    atot += l_proofs[p] * l_cons[p];
+  }
+  Az.total = atot;
+  Az.num_instances = npow2(P);
+  Az.max_num_proofs = max_np;
+  Az.num_witness_secs = 1;
+  Az.max_num_inputs = num_cons;
+  Az.num_proofs = l_proofs;
+  Az.num_inputs = l_cons;
+  Az.d = (Fq*)ws_get(ctx, WS_AZ, atot * sizeof(Fq) + 64);
+  Fq* Bz = (Fq*)ws_get(ctx, WS_BZ, atot * sizeof(Fq) + 64);
+  Fq* Cz = (Fq*)ws_get(ctx, WS_CZ, atot * sizeof(Fq) + 64);
+  if (!Az.d || !Bz || !Cz) return set_err(ctx, SPG_E_NOMEM, "Az/Bz/Cz");
   static const bool z_side = !getenv("SPG_Z_SIDE") || atoi(getenv("SPG_Z_SIDE")) != 0;
   // whatever way this returns, `stream` is ordered after the fill before anything later reuses the Z slot
   struct SideJoin {
@@ -635,7 +668,13 @@ int Prover::run_inner(Laps& lp) {
     }
     ~SideJoin() { join(); }
   } z_join{ctx};
+  // every descriptor of the setup kernels (Z fill, Az/Bz/Cz) goes up in one host-to-device copy
   SecDesc* dsec = nullptr;
+  ZDesc* dz = nullptr;
+  MatDesc* dmd = nullptr;
+  SpDesc* dsd = nullptr;
+  double visits = 0;
+  int rc = 0;
   {
     std::vector<ZDesc> zd(PLn);
     std::vector<SecDesc> sd(nws * PLn);
@@ -653,10 +692,32 @@ int Prover::run_inner(Laps& lp) {
         sd[w * PLn + p].ni = (uint32_t)wit.num_inputs[w][pw];
       }
     }
-    ZDesc* dz;
-    int rc = upload_desc(zd, 0, &dz);
-    if (!rc) rc = upload_desc(sd, 65536, &dsec);
+    std::vector<MatDesc> md(inst.num_instances);
+    for (size_t p = 0; p < inst.num_instances; p++) {
+      for (int m = 0; m < 3; m++) md[p].rp[m] = inst.rp_off[3 * p + m];
+      md[p].cp = inst.cp_off[p];
+    }
+    std::vector<SpDesc> spd(PLn);
+    for (size_t p = 0; p < PLn; p++) {
+      size_t pi = inst.num_instances == 1 ? 0 : p0 + p;
+      spd[p].dom_off = Az.off[p];
+      spd[p].out_off = Az.off[p];
+      spd[p].pi = (uint32_t)pi;
+      spd[p].lg_q = (uint32_t)lg2(l_proofs[p]);
+      spd[p].nrows = (uint32_t)l_cons[p];
+      spd[p].lg_rows = (uint32_t)lg2(l_cons[p]);
+      spd[p].ni = (uint32_t)l_inputs[p];
+      spd[p].lg_ni = (uint32_t)lg2(l_inputs[p]);
+      visits += (double)l_proofs[p] * (inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2]);
+    }
+    rc = stage_desc(zd, &dz);
+    if (!rc) rc = stage_desc(sd, &dsec);
+    if (!rc) rc = stage_desc(md, &dmd);
+    if (!rc) rc = stage_desc(spd, &dsd);
+    if (!rc) rc = flush_desc();
     if (rc) return rc;
+  }
+  {
     // k_spmv gathers from the witness itself, so the fill only has to land before phase 2: on the second stream
     // it overlaps Az/Bz/Cz and the phase-1 rounds (same-box A/B: DESIGN §4, round 4)
     const hipStream_t main_stream = ctx->stream;
@@ -687,59 +748,10 @@ int Prover::run_inner(Laps& lp) {
   Fq* Aq = (Fq*)ws_get(ctx, WS_TQ, (sizeof(Fq) << nq) + 64);
   Fq* Ax = (Fq*)ws_get(ctx, WS_TX, (sizeof(Fq) << nx) + 64);
   if (!Ap || !Aq || !Ax) return set_err(ctx, SPG_E_NOMEM, "eq tables");
-  int rc = eq_tables(ctx, {{tau_p, Ap}, {tau_q, Aq}, {tau_x, Ax}});
+  rc = eq_tables(ctx, {{tau_p, Ap}, {tau_q, Aq}, {tau_x, Ax}});
   if (rc) return rc;
 
-  // ---- Az, Bz, Cz = multiply_vec_block (p, q_rev, 0, x_rev) for the local instances
-  PqxDev Az;
-  Az.zlen = PLn;
-  Az.off.resize(PLn);
-  Az.anp = l_proofs;
-  Az.anw.assign(PLn, 1);
-  Az.ani = l_cons;
-  size_t atot = 0;
-  for (size_t p = 0; p < PLn; p++) {
-    Az.off[p] = atot;
-    atot += l_proofs[p] * l_cons[p];
-  }
-  Az.total = atot;
-  Az.num_instances = npow2(P);
-  Az.max_num_proofs = max_np;
-  Az.num_witness_secs = 1;
-  Az.max_num_inputs = num_cons;
-  Az.num_proofs = l_proofs;
-  Az.num_inputs = l_cons;
-  Az.d = (Fq*)ws_get(ctx, WS_AZ, atot * sizeof(Fq) + 64);
-  Fq* Bz = (Fq*)ws_get(ctx, WS_BZ, atot * sizeof(Fq) + 64);
-  Fq* Cz = (Fq*)ws_get(ctx, WS_CZ, atot * sizeof(Fq) + 64);
-  if (!Az.d || !Bz || !Cz) return set_err(ctx, SPG_E_NOMEM, "Az/Bz/Cz");
-  std::vector<MatDesc> md(inst.num_instances);
-  for (size_t p = 0; p < inst.num_instances; p++) {
-    for (int m = 0; m < 3; m++) md[p].rp[m] = inst.rp_off[3 * p + m];
-    md[p].cp = inst.cp_off[p];
-  }
-  MatDesc* dmd;
-  rc = upload_desc(md, 2 * 65536, &dmd);
-  if (rc) return rc;
-  {
-    std::vector<SpDesc> sd(PLn);
-    double visits = 0;
-    for (size_t p = 0; p < PLn; p++) {
-      size_t pi = inst.num_instances == 1 ? 0 : p0 + p;
-      sd[p].dom_off = Az.off[p];
-      sd[p].out_off = Az.off[p];
-      sd[p].pi = (uint32_t)pi;
-      sd[p].lg_q = (uint32_t)lg2(l_proofs[p]);
-      sd[p].nrows = (uint32_t)l_cons[p];
-      sd[p].lg_rows = (uint32_t)lg2(l_cons[p]);
-      sd[p].ni = (uint32_t)l_inputs[p];
-      sd[p].lg_ni = (uint32_t)lg2(l_inputs[p]);
-      visits += (double)l_proofs[p] * (inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2]);
-    }
-    SpDesc* dsd;
-    rc = upload_desc(sd, 3 * 65536, &dsd);
-    if (rc) return rc;
-    // outputs, CSR row pointers, and per visited entry its column, value and z gather
+  {  // ---- Az, Bz, Cz: outputs, CSR row pointers, and per visited entry its column, value and z gather
     KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
     hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr, inst.d_col,
                        inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
@@ -934,7 +946,8 @@ int Prover::run_inner(Laps& lp) {
       visits += inst.nnz[3 * pi] + inst.nnz[3 * pi + 1] + inst.nnz[3 * pi + 2];
     }
     AbcDesc* dad;
-    rc = upload_desc(ad, 4 * 65536, &dad);
+    rc = stage_desc(ad, &dad);
+    if (!rc) rc = flush_desc();
     if (rc) return rc;
     KScope ks(ctx, "eval_table_abc", 32.0 * btot + 4.0 * btot + 68.0 * visits);
     hipLaunchKernelGGL(k_abc, dim3(blocks_for(btot)), dim3(256), 0, s, dad, (int)Abn, dmd, inst.d_colptr, inst.d_crow,
@@ -1770,8 +1783,12 @@ extern "C" int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, 
   }
   MatDesc* dmd = (MatDesc*)ddesc;
   uint32_t* drr = (uint32_t*)(ddesc + Pm * sizeof(MatDesc));
-  SPG_HIP(ctx, hipMemcpyAsync(dmd, md.data(), Pm * sizeof(MatDesc), hipMemcpyHostToDevice, s));
-  SPG_HIP(ctx, hipMemcpyAsync(drr, rr.data(), 2 * Pm * 4, hipMemcpyHostToDevice, s));
+  {  // matrix descriptors and row ranges in one copy
+    std::vector<uint8_t> h(Pm * sizeof(MatDesc) + 2 * Pm * 4);
+    memcpy(h.data(), md.data(), Pm * sizeof(MatDesc));
+    memcpy(h.data() + Pm * sizeof(MatDesc), rr.data(), 2 * Pm * 4);
+    SPG_HIP(ctx, hipMemcpyAsync(dmd, h.data(), h.size(), hipMemcpyHostToDevice, s));
+  }
   timer_start(ctx);
   int rc = eq_tables(ctx, {{vx, erx}, {vy, ery}});
   if (rc) return rc;
