@@ -16,6 +16,10 @@ for set in "$@"; do
     build) AB_KERNEL=${AB_KERNEL:-sc_phase1_fold_eval,sc_phase2_fold_eval,spark_layer_round,msm_bullet_round} \
              bash scripts/ab_env.sh SPG_LIB "$L/libspg_prev.so $L/libspg.so" ${AB_REPS:-3} ;;
     zside) AB_KERNEL=z_fill,spmv_block,sc_phase1_fold_eval bash scripts/ab_env.sh SPG_Z_SIDE "0 1" ${AB_REPS:-3} ;;
+    # rocprof kernel stats of the previous build, this build, and this build with the Z fill in order (spmv launch time)
+    spmvprof) P="env -u TESTS -u BENCH -u CMD -u SMOKE -u PMC PROF=1 T_PROF=200"
+              $P SPG_LIB=$L/libspg_prev.so TAG=spA_ bash scripts/gpu_run.sh && $P TAG=spB_ bash scripts/gpu_run.sh &&
+              $P SPG_Z_SIDE=0 TAG=spC_ bash scripts/gpu_run.sh ;;
     combwgs) AB_KERNEL=msm_comb bash scripts/ab_env.sh SPG_COMB_WGS "1024 2048 4096" 2 ;;
     bigcomb) AB_KERNEL=msm_comb_single,msm_big_accum,msm_big_sort BENCH_ARGS="--workload msm" \
                bash scripts/ab_env.sh SPG_BIG_COMB "0 1" 3 ;;
