@@ -108,7 +108,14 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
                                               uint32_t Y,
                                               Fq* __restrict__ Az, Fq* __restrict__ Bz, Fq* __restrict__ Cz,
                                               uint64_t total) {
-  uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  // the section descriptors of the block's first instance (nws <= 8) sit in LDS: a nonzero's gather then waits on
+  // an LDS read instead of a dependent global load; lanes of a later instance in the same block read them globally
+  __shared__ SecDesc s_sec[8];
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256;
+  const int pb = find_desc(sd, P, t0);
+  if ((int)threadIdx.x < nws) s_sec[threadIdx.x] = sec[(size_t)threadIdx.x * P + pb];
+  __syncthreads();
+  uint64_t t = t0 + threadIdx.x;
   if (t >= total) return;
   int p = find_desc(sd, P, t);
   const SpDesc d = sd[p];
@@ -125,8 +132,19 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
       uint32_t c = col[e];
       uint32_t w = c / Y, i = c % Y;
       if (w < (uint32_t)nws && i < d.ni) {
-        const SecDesc x = sec[(size_t)w * P + p];
-        if (i < x.ni) s = fq_add(s, fq_mul(val[e], x.w[(size_t)(x.np == 1 ? 0 : q) * x.ni + i]));
+        const Fq* xw;
+        uint32_t xnp, xni;
+        if (p == pb) {
+          xw = s_sec[w].w;
+          xnp = s_sec[w].np;
+          xni = s_sec[w].ni;
+        } else {
+          const SecDesc& x = sec[(size_t)w * P + p];
+          xw = x.w;
+          xnp = x.np;
+          xni = x.ni;
+        }
+        if (i < xni) s = fq_add(s, fq_mul(val[e], xw[(size_t)(xnp == 1 ? 0 : q) * xni + i]));
       }
     }
     outs[m][o] = s;
