@@ -20,6 +20,8 @@ for set in "$@"; do
     spmvprof) P="env -u TESTS -u BENCH -u CMD -u SMOKE -u PMC PROF=1 T_PROF=200"
               $P SPG_LIB=$L/libspg_prev.so TAG=spA_ bash scripts/gpu_run.sh && $P TAG=spB_ bash scripts/gpu_run.sh &&
               $P SPG_Z_SIDE=0 TAG=spC_ bash scripts/gpu_run.sh ;;
+    zafter) AB_KERNEL=sc_phase1_fold_eval bash scripts/ab_env.sh SPG_Z_AFTER "0 2 4" 2 ;;
+    zlateprof) env -u TESTS -u BENCH -u CMD -u SMOKE -u PMC PROF=1 T_PROF=200 TAG=spD_ bash scripts/gpu_run.sh ;;
     combwgs) AB_KERNEL=msm_comb bash scripts/ab_env.sh SPG_COMB_WGS "1024 2048 4096" 2 ;;
     bigcomb) AB_KERNEL=msm_comb_single,msm_big_accum,msm_big_sort BENCH_ARGS="--workload msm" \
                bash scripts/ab_env.sh SPG_BIG_COMB "0 1" 3 ;;

@@ -735,28 +735,6 @@ int Prover::run_inner(Laps& lp) {
     if (!rc) rc = flush_desc();
     if (rc) return rc;
   }
-  {
-    // k_spmv gathers from the witness itself, so the fill only has to land before phase 2: on the second stream
-    // it overlaps Az/Bz/Cz and the phase-1 rounds (same-box A/B: DESIGN §4, round 4)
-    const hipStream_t main_stream = ctx->stream;
-    if (z_side) {
-      SPG_HIP(ctx, hipEventRecord(ctx->ev_pre, main_stream));
-      SPG_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_pre, 0));
-      ctx->stream = ctx->stream2;
-    }
-    {
-      KScope ks(ctx, "z_fill", 64.0 * ztot);
-      hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec, (int)nws,
-                         Zp.d, (uint64_t)ztot);
-    }
-    ctx->stream = main_stream;
-    SPG_HIP(ctx, hipGetLastError());
-    if (z_side) {
-      SPG_HIP(ctx, hipEventRecord(ctx->ev_side, ctx->stream2));
-      z_join.armed = true;
-    }
-  }
-
   // ---- tau tables (identical on every rank)
   FqV tau_p = t.challenges("challenge_tau_p", np);
   FqV tau_q = t.challenges("challenge_tau_q", nq);
@@ -775,6 +753,35 @@ int Prover::run_inner(Laps& lp) {
                        inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
     SPG_HIP(ctx, hipGetLastError());
   }
+  // k_spmv gathers from the witness itself, so the Z fill only has to land before phase 2. On the second stream it
+  // is queued once phase 1's round SPG_Z_AFTER (default 4) has been evaluated, and runs beside the later, smaller
+  // rounds: overlapping k_spmv or the first, HBM-bound rounds, the kernels slow each other (rocprof and same-box
+  // A/Bs: DESIGN §4, round 4). SPG_Z_SIDE=0 fills it in order here.
+  bool z_queued = false;
+  static const size_t z_after = getenv("SPG_Z_AFTER") ? (size_t)atol(getenv("SPG_Z_AFTER")) : 4;
+  auto queue_z_fill = [&]() -> int {
+    if (z_queued) return 0;
+    z_queued = true;
+    const hipStream_t main_stream = ctx->stream;
+    if (z_side) {
+      SPG_HIP(ctx, hipEventRecord(ctx->ev_pre, main_stream));
+      SPG_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_pre, 0));
+      ctx->stream = ctx->stream2;
+    }
+    {
+      KScope ks(ctx, "z_fill", 64.0 * ztot);
+      hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec, (int)nws,
+                         Zp.d, (uint64_t)ztot);
+    }
+    ctx->stream = main_stream;
+    SPG_HIP(ctx, hipGetLastError());
+    if (z_side) {
+      SPG_HIP(ctx, hipEventRecord(ctx->ev_side, ctx->stream2));
+      z_join.armed = true;
+    }
+    return 0;
+  };
+  if (!z_side && (rc = queue_z_fill())) return rc;
 
   lp.lap("setup");
   Fq* partials = (Fq*)ws_get(ctx, WS_PART, 3 * 1024 * sizeof(Fq) + 64);
@@ -851,6 +858,7 @@ int Prover::run_inner(Laps& lp) {
       int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
       Fq e[3];
       rc = eval_wait(ctx, e);
+      if (!rc && j == z_after) rc = queue_z_fill();  // round j is done and round j + 1 not yet queued
       if (!rc && j == 1 && failpoint(ctx, "r1cs_round")) rc = set_err(ctx, SPG_E_HIP, "failpoint r1cs_round");
       if (!rc && mode != MODE_P) rc = sum_ranks(e);
       if (rc) return rc;
@@ -972,7 +980,8 @@ int Prover::run_inner(Laps& lp) {
                        inst.d_cval, eq_rx, (uint32_t)Y, r_A, r_B, r_C, ABC.d, (uint64_t)btot);
     SPG_HIP(ctx, hipGetLastError());
   }
-  rc = z_join.join();  // the Z table's first use
+  rc = queue_z_fill();  // (phase 1 had no rounds)
+  if (!rc) rc = z_join.join();  // the Z table's first use
   if (rc) return rc;
   for (size_t k = 0; k < rq_rev.size(); k++) {  // Z.bound_poly_vars_rq(rq_rev)
     rc = pqx_bound(ctx, Zp, nullptr, nullptr, rq_rev[k], MODE_Q);
