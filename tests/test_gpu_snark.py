@@ -96,6 +96,11 @@ ROUND_FORMS = {
     "layer_persist_one_wg": {"SPG_LAYER_PERSIST": "1", "SPG_PERSIST_WGS": "1", "SPG_PERSIST_MAX": str(1 << 20)},
     "layer_persist_wide": {"SPG_LAYER_PERSIST": "1", "SPG_PERSIST_WGS": "256", "SPG_PERSIST_MAX": str(1 << 20)},
     "layer_persist_no_ends": {"SPG_LAYER_PERSIST": "1", "SPG_LAYER_ENDS": "0"},
+    "z_fill_in_order": {"SPG_Z_SIDE": "0"},
+    "z_fill_after_round_0": {"SPG_Z_AFTER": "0"},
+    "z_fill_at_phase2": {"SPG_Z_AFTER": "100000"},
+    "eq_table_per_launch": {"SPG_EQ_MULTI": "0"},
+    "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
 }
 
 
@@ -106,7 +111,9 @@ def test_round_forms(form):
     quad per point everywhere; phase-1 and phase-2 folds as launches of their own (SPG_SC_FUSE=0) instead of inside the next
     round's evaluation; SPARK layer rounds in the resident launch (SPG_LAYER_PERSIST=1; the default launches each
     round), with workgroup 0 relaying the host's answer or every workgroup polling the host, with one workgroup over
-    every round, with 256 workgroups, and without posting the layer's entries"""
+    every round, with 256 workgroups, and without posting the layer's entries; the R1CS Z fill in stream order
+    (SPG_Z_SIDE=0) or on the second stream after phase-1 round 0 or only at phase 2 (SPG_Z_AFTER); one eq table
+    per launch (SPG_EQ_MULTI=0); device witness parts copied instead of read in place (SPG_WIT_IN_PLACE=0)"""
     import subprocess
     import sys
 
