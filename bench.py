@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--log-proofs", type=int, default=9, help="snark: 2^k executions per block")
     ap.add_argument("--log-nnz", type=int, default=24, help="spark: 2^k nonzeros per matrix (x3 matrices)")
     ap.add_argument("--cpu-log-nnz", type=int, default=16, help="spark: CPU baseline sample size")
+    ap.add_argument("--extras-log-nnz", type=int, default=24,
+                    help="snark: config 5's 2^k nonzeros per matrix in the extras (24 = BASELINE config 5; smaller only "
+                         "for rehearsals with several ranks on one GPU)")
     ap.add_argument("--extras", default="msm,rows,r1cs,spark,cpu1",
                     help="snark at N = 1: the other BASELINE configs measured in the same run "
                          "(msm, rows, r1cs, spark, cpu1; 'none')")
@@ -386,13 +389,30 @@ def main_snark(a):
                "sample": f"full workload ({N} constraints), one SNARK::prove (instances pre-encoded), "
                          f"{tcpu:.2f} s on 1 host thread; oracle verifier status {rc}"}
         bitexact = hashlib.sha256(ref).hexdigest() in proofs
-        cpu_all = all_cores_baseline(
-            lambda: po.snark_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS, label=b"snark_bench"),
-            N, "constraints/s", f"the full workload's SNARK::prove ({N} constraints) incl. SNARK::encode, "
-                                f"R1CSGens derivation and the oracle's own verification")
+        # all cores: one oracle copy per usable core encodes and derives its generators, all meet at a barrier, then
+        # all prove at once; the wall time runs from the first prove's start to the last one's end (SNARK::prove alone,
+        # like the GPU step: encode, R1CSGens and verification outside)
+        k_all = usable_cores()
+        dt_all = po.snark_concurrent_prove(wl, seed, k_all, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS,
+                                           label=b"snark_bench")
+        cpu_all = {"value": round(N * k_all / dt_all, 1), "unit": "constraints/s", "cores": k_all, "kind": "port",
+                   "sample": f"{k_all} concurrent independent copies of the full workload's SNARK::prove ({N} "
+                             f"constraints each), proving together after a barrier (prove only); {dt_all:.2f} s wall "
+                             f"from the first prove's start to the last one's end"}
     extras = {}
-    if env.world == 1 and a.extras != "none":
-        want = set(a.extras.split(","))
+    want = set(a.extras.split(",")) if a.extras != "none" else set()
+    if env.world > 1:
+        # N > 1: the BASELINE configs that shard, each as ONE proof split over the ranks with libspg's exchanges
+        # (RCCL under the nccl backend), strong scaling; every rank must end with the same bytes (ranks_agree), and the
+        # bytes equal the N = 1 line's config4_r1cs / config5_spark (same workload seeds). Measured after the replicas.
+        if "r1cs" in want:
+            extras["config4_r1cs"] = guarded(lambda: r1cs_core(env, ctx, "r1cs_2e22_p8", True, 5, 1, False,
+                                                               TRAFFIC["r1cs22"], a.comm), env)
+        if "spark" in want:
+            extras["config5_spark"] = guarded(lambda: spark_core(env, ctx, a.extras_log_nnz, a.cpu_log_nnz, 5, 1, "shard",
+                                                                 False, TRAFFIC["spark24"] if a.extras_log_nnz == 24
+                                                                 else None, a.comm), env)
+    if env.world == 1 and want:
         cpu_on = not a.no_cpu_baseline
         if "msm" in want:
             extras["config2_msm"] = guarded(lambda: msm_core(env, ctx, 16, a.steps, a.warmup, cpu_on, TRAFFIC["msm16"]))
@@ -402,8 +422,9 @@ def main_snark(a):
             extras["config4_r1cs"] = guarded(lambda: r1cs_core(env, ctx, "r1cs_2e22_p8", False, 5, 1, cpu_on,
                                                                TRAFFIC["r1cs22"]))
         if "spark" in want:
-            extras["config5_spark"] = guarded(lambda: spark_core(env, ctx, 24, a.cpu_log_nnz, 5, 1, "replicas",
-                                                                 cpu_on, TRAFFIC["spark24"]))
+            extras["config5_spark"] = guarded(lambda: spark_core(env, ctx, a.extras_log_nnz, a.cpu_log_nnz, 5, 1,
+                                                                 "replicas", cpu_on, TRAFFIC["spark24"]
+                                                                 if a.extras_log_nnz == 24 else None))
         if "cpu1" in want and cpu_on:
             extras["config1_cpu"] = guarded(cpu1_core)
     if env.rank == 0:
@@ -435,12 +456,19 @@ def main_snark(a):
     env.close()
 
 
-def guarded(fn):
-    """an extra config's result, or the error it raised (the headline line is printed either way)"""
+def guarded(fn, env=None):
+    """an extra config's result, or the error it raised (the headline line is printed either way). With several ranks
+    (env given) every rank learns whether any rank failed, so no rank goes on into a later collective alone; libspg's
+    own exchanges already fail every rank together (status-framed allgathers)."""
     try:
-        return fn()
+        out, err = fn(), None
     except Exception as e:  # noqa: BLE001
-        return {"error": repr(e)[:500]}
+        out, err = None, {"error": repr(e)[:500]}
+    if env is not None and env.dist is not None:
+        bad = env.max_over_ranks(1.0 if err else 0.0)
+        if bad and not err:
+            err = {"error": "another rank failed in this config"}
+    return err or out
 
 
 # ---------------------------------------------------------------- R1CSProof::prove (config 4)
@@ -479,17 +507,18 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
         return pf
 
     dt, laps, proofs = timed(env, step, steps, warmup)
-    assert len(proofs) == 1, "proof bytes changed between steps"
+    if not shard:
+        assert len(proofs) == 1, "proof bytes changed between steps"
     prof = profile_pass(ctx, step, steps)
     t1 = time.perf_counter()  # PCIe-inclusive variant: witness upload + prove (reported beside value)
     wit = upload()
     step()
     t_incl = time.perf_counter() - t1
     same = None
-    if shard:  # every rank of one sharded proof must hold the same bytes
+    if shard:  # every rank of one sharded proof must hold the same bytes, the same in every step
         hs = [None] * env.world
         env.dist.all_gather_object(hs, sorted(proofs))
-        same = all(h == hs[0] for h in hs)
+        same = all(h == hs[0] for h in hs) and len(hs[0]) == 1
         ctx.set_comm(0, 1)
     N = wl.total_constraints  # one proof's constraints (the whole sharded proof, or one replica's)
     units = N if shard else N * env.world
@@ -497,20 +526,22 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
     cpu = cpu_all = bitexact = None
     if env.rank == 0 and env.world == 1 and cpu_on:
         po = oracle()
-        tc = time.perf_counter()
         ref, _ = po.r1cs_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS, label=b"r1cs_bench")
-        tcpu = time.perf_counter() - tc
+        tcpu = po.last_prove_seconds()  # R1CSProof::prove alone (R1CSGens derivation outside, like the GPU step)
         cpu = {"value": round(N / tcpu, 1), "unit": "constraints/s", "cores": 1, "kind": "port",
-               "sample": f"full workload ({N} constraints), one R1CSProof::prove incl. R1CSGens derivation, "
-                         f"{tcpu:.2f} s on 1 host thread"}
+               "sample": f"full workload ({N} constraints), one R1CSProof::prove (prove only), {tcpu:.2f} s on 1 host "
+                         f"thread"}
         bitexact = hashlib.sha256(ref).hexdigest() in proofs
         ks = 6  # all cores: a 2^6-execution sample of the same shape per core
         ws = workload.R1CSWorkload(nc, [min(x, 1 << ks) for x in npf], num_sections=nws, instances=range(len(nc)))
-        cpu_all = all_cores_baseline(
-            lambda: po.r1cs_prove(ws, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS, label=b"r1cs_bench"),
-            ws.total_constraints, "constraints/s",
-            f"R1CSProof::prove of {ws.P} instances x 2^{ks} executions x {nc[0]} constraints "
-            f"({ws.total_constraints} constraints) incl. R1CSGens derivation")
+        k_all = usable_cores()
+        dt_all = po.r1cs_concurrent_prove(ws, seed, k_all, gens_label=GENS_LABEL, gens_num_vars=GENS_NUM_VARS,
+                                          label=b"r1cs_bench")
+        cpu_all = {"value": round(ws.total_constraints * k_all / dt_all, 1), "unit": "constraints/s", "cores": k_all,
+                   "kind": "port",
+                   "sample": f"{k_all} concurrent independent copies of R1CSProof::prove of {ws.P} instances x 2^{ks} "
+                             f"executions x {nc[0]} constraints ({ws.total_constraints} constraints each; the GPU line "
+                             f"proves {N}), proving together after a barrier (prove only); {dt_all:.2f} s wall"}
     return {
         "metric": "R1CS constraints/sec (R1CSProof::prove, data-parallel)", "value": round(units * steps / dt, 1),
         "unit": "constraints/s", "n_gpus": env.world, "steps": steps, "warmup": warmup,
@@ -525,7 +556,7 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
                    else f"replicas x{env.world}"},
         "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact, "proof_sha256": sorted(proofs)[0][:16],
-        "ranks_agree": same, "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
+        "ranks_agree": same, "transport": transport, "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
         "value_incl_witness_upload": round(units / t_incl, 1), "kernels": kernel_table(prof, steps)}
 
 
@@ -777,12 +808,13 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
     dt, laps, proofs = timed(env, step, steps, warmup)
     prof = profile_pass(ctx, step, steps)
     same = None
-    if shard:  # every rank of one sharded proof must hold the same bytes
+    if shard:  # every rank of one sharded proof must hold the same bytes, the same in every step
         hs = [None] * env.world
         env.dist.all_gather_object(hs, sorted(proofs))
-        same = all(h == hs[0] for h in hs)
+        same = all(h == hs[0] for h in hs) and len(hs[0]) == 1
         ctx.set_comm(0, 1)
-    assert len(proofs) == 1, "proof bytes changed between steps"
+    else:
+        assert len(proofs) == 1, "proof bytes changed between steps"
     nnz = 3 * wl.nnz
     value = nnz * (1 if shard else env.world) * steps / dt
     roof, roof_h, roof_v = rooflines(prof, traffic_file)
@@ -795,7 +827,8 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         rc_[:, 3] &= np.uint64((1 << 60) - 1)
         po.spark_prove(wc, rc_[:kc], rc_[kc:], seed)
         tcpu = po.spark_last_prove_us() * 1e-6
-        sample = (f"3 x 2^{kc} nonzeros (same generator), multi_evaluate + SparseMatPolyEvalProof::prove")
+        sample = (f"3 x 2^{kc} nonzeros (same generator; the GPU line proves 3 x 2^{k}), multi_evaluate + "
+                  f"SparseMatPolyEvalProof::prove")
         cpu = {"value": round(3 * (1 << kc) / tcpu, 1), "unit": "nonzeros/s", "cores": 1, "kind": "port",
                "sample": f"{sample}, {tcpu:.2f} s on 1 host thread (the commitment is preprocessing, untimed)"}
         # all cores: one oracle copy per usable core commits, all meet at a barrier, then all prove at once; the wall
@@ -817,6 +850,7 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
                    "parallelism": f"one proof sharded x{env.world} ({transport})" if shard else f"replicas x{env.world}"},
         "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_sha256": sorted(proofs)[0][:16], "ranks_agree": same,
+        "transport": transport,
         "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
         "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
         "kernels": kernel_table(prof, steps),

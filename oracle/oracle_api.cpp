@@ -1,6 +1,7 @@
 // ORACLE — test infrastructure only. C entry points over the CPU restatement, loaded by tests/
 // (ctypes), __graft_entry__.smoke() and bench.py's cpu_baseline leg. Never linked into the product.
 #include <cstdint>
+#include <chrono>
 #include <cstring>
 #include <vector>
 #include "fq.hpp"
@@ -204,6 +205,13 @@ void orc_dense_eval(const uint64_t* Z, size_t n, const uint64_t* r, size_t ell, 
 }
 }
 
+// (baseline-mode state: see orc_baseline_mode below)
+static void (*g_bl_barrier)() = nullptr;
+static bool g_bl_skip_verify = false;
+static thread_local double g_bl_w0 = 0.0, g_bl_w1 = 0.0;
+static double steady_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 static R1CSInstance inst_from_c(const spg_r1cs_instance* ci) {
   std::vector<std::vector<SparseEntry>> A, B, C;
   for (size_t p = 0; p < ci->num_instances; p++) {
@@ -284,7 +292,10 @@ int orc_r1cs_prove_tr(const spg_r1cs_instance* ci, size_t num_instances, size_t 
     RandomTape tape("proof", ld(tape_seed));
     std::vector<size_t> np(num_proofs, num_proofs + num_instances), ni(num_inputs, num_inputs + num_instances);
     std::vector<FqVec> ch;
+    if (g_bl_barrier) g_bl_barrier();
+    g_bl_w0 = steady_us();
     R1CSProof pf = R1CSProof::prove(num_instances, max_num_proofs, np, max_num_inputs, ni, wp, inst, gens, t, tape, &ch);
+    g_bl_w1 = steady_us();
     Ser s;
     pf.ser(s);
     *proof_len = s.b.size();
@@ -391,26 +402,23 @@ extern "C" {
 // Proves SparseMatPolyEvalProof at (rx, ry) for evals = multi_evaluate(rx, ry) under a fresh
 // Transcript(label) + RandomTape("proof", seed), writes bincode(commitment) and bincode(proof), then runs
 // the verifier on a fresh transcript. Returns 1 if it verifies, 0 if not, <0 on error.
+// CPU-baseline mode (bench.py's all-cores baselines): every orc_spark_prove / orc_r1cs_prove / orc_snark_prove calls
+// `barrier` between its setup (commitment, generator derivation, instance encoding) and its prove, so concurrent copies
+// prove at the same time, and may skip the verification; each thread's prove window (steady clock, microseconds) is
+// kept for the caller to take the concurrent wall time of the proves alone from
+void orc_baseline_mode(void (*barrier)(), int skip_verify) {
+  g_bl_barrier = barrier;
+  g_bl_skip_verify = skip_verify != 0;
+}
+void orc_last_prove_window(double* t0, double* t1) {
+  *t0 = g_bl_w0;
+  *t1 = g_bl_w1;
+}
+void orc_spark_baseline_mode(void (*barrier)(), int skip_verify) { orc_baseline_mode(barrier, skip_verify); }
+void orc_spark_last_prove_window(double* t0, double* t1) { orc_last_prove_window(t0, t1); }
 static thread_local double g_spark_prove_us = 0.0;
 // wall time of the last orc_spark_prove's multi_evaluate + SparseMatPolyEvalProof::prove (CPU baseline)
 double orc_spark_last_prove_us() { return g_spark_prove_us; }
-// CPU-baseline mode (bench.py config 5, all cores): every orc_spark_prove calls `barrier` between its commitment and
-// its prove, so concurrent copies prove at the same time, and may skip the verification; each thread's prove window
-// (steady clock, microseconds) is kept for the caller to take the concurrent wall time from
-static void (*g_spark_barrier)() = nullptr;
-static bool g_spark_skip_verify = false;
-static thread_local double g_spark_w0 = 0.0, g_spark_w1 = 0.0;
-void orc_spark_baseline_mode(void (*barrier)(), int skip_verify) {
-  g_spark_barrier = barrier;
-  g_spark_skip_verify = skip_verify != 0;
-}
-void orc_spark_last_prove_window(double* t0, double* t1) {
-  *t0 = g_spark_w0;
-  *t1 = g_spark_w1;
-}
-static double steady_us() {
-  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // transcript != NULL: prove on that caller's handle (orc_transcript_new) instead of a fresh Transcript(label) and
 // skip the verification (returns 1)
@@ -444,16 +452,16 @@ int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size
     SparkGens g = SparkGens::create(gens_label, nvx, nvy, gens_nnz, gens_batch);
     MultiSparseDense dense;
     SparkCommitment comm = spark_multi_commit(polys, g, &dense);
-    if (g_spark_barrier) g_spark_barrier();
+    if (g_bl_barrier) g_bl_barrier();
     auto t0 = std::chrono::steady_clock::now();
-    g_spark_w0 = steady_us();
+    g_bl_w0 = steady_us();
     FqVec evals = inst.multi_evaluate(vx, vy);
     Transcript tl(label);
     Transcript& t = transcript ? *(Transcript*)transcript : tl;
     RandomTape tape("proof", ld(tape_seed));
     SparkEvalProof pf = spark_prove(dense, vx, vy, evals, g, t, tape);
     g_spark_prove_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    g_spark_w1 = steady_us();
+    g_bl_w1 = steady_us();
     Ser sc, sp;
     comm.ser(sc);
     pf.ser(sp);
@@ -462,7 +470,7 @@ int orc_spark_prove_tr(const spg_r1cs_instance* ci, const char* gens_label, size
     if (sc.b.size() > comm_cap || sp.b.size() > proof_cap) return -1;
     memcpy(comm_out, sc.b.data(), sc.b.size());
     memcpy(proof_out, sp.b.data(), sp.b.size());
-    if (transcript || g_spark_skip_verify) return 1;
+    if (transcript || g_bl_skip_verify) return 1;
     Transcript tv(label);
     return spark_verify(pf, comm, vx, vy, evals, g, tv) ? 1 : 0;
   } catch (const std::string& e) {
@@ -611,11 +619,14 @@ int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* bloc
     SnarkInst block = snark_inst_from_c(block_c, true), pairwise = snark_inst_from_c(pairwise_c, false),
               perm_root = snark_inst_from_c(perm_root_c, false);
     R1CSGens vg = R1CSGens::create(gens_label, gens_num_vars);
+    if (g_bl_barrier) g_bl_barrier();
+    g_bl_w0 = steady_us();
     auto t0 = std::chrono::steady_clock::now();
     Transcript t(label);
     RandomTape tape("proof", ld(tape_seed));
     SNARKProof pf = snark_prove(in, block, pairwise, perm_root, vg, t, tape);
     g_snark_prove_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    g_bl_w1 = steady_us();
     Ser s;
     pf.ser(s);
     *out_len = s.b.size();
@@ -629,6 +640,7 @@ int orc_snark_prove(const spg_snark_inputs* in_c, const spg_snark_instance* bloc
       std::swap(pf.shift_proof.C_orig_evals[0], pf.shift_proof.C_orig_evals[1]);
     if (tamper && std::string(tamper) == "perm_opening" && !pf.proof_eval_perm_poly_prod_list.empty())
       std::swap(pf.proof_eval_perm_poly_prod_list[0], pf.proof_eval_perm_poly_prod_list.back());
+    if (g_bl_skip_verify) return 0;
     Transcript tv(label);
     auto t1 = std::chrono::steady_clock::now();
     const int rc = snark_verify(pf, in, block, pairwise, perm_root, vg, tv);

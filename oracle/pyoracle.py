@@ -331,23 +331,23 @@ def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=No
     return cb[: cl.value].tobytes(), pb[: pl.value].tobytes(), rc == 1
 
 
-def spark_concurrent_prove(wl, rx, ry, tape_seed, k, gens_nnz=None):
-    """k concurrent oracle SPARK proves of the same workload on k threads (the ctypes calls release the GIL): each
-    thread commits, all meet at a barrier, then all prove at once (verification skipped). Returns the wall seconds from
-    the first prove's start to the last one's end."""
+def concurrent_proves(fn, k):
+    """fn() on k threads at once in the oracle's baseline mode (the ctypes calls release the GIL): every copy does its
+    setup (commitments, generator derivation, instance encoding), all meet at a barrier, then all prove at once with
+    the verification skipped. Returns the wall seconds from the first prove's start to the last one's end."""
     import threading
 
     bar = threading.Barrier(k)
     cb = ctypes.CFUNCTYPE(None)(lambda: bar.wait())
-    f = lib().orc_spark_baseline_mode
+    f = lib().orc_baseline_mode
     f(cb, ctypes.c_int(1))
     wins, errs = [], []
 
     def body():
         try:
-            spark_prove(wl, rx, ry, tape_seed, gens_nnz=gens_nnz)
+            fn()
             t0, t1 = ctypes.c_double(0), ctypes.c_double(0)
-            lib().orc_spark_last_prove_window(ctypes.byref(t0), ctypes.byref(t1))
+            lib().orc_last_prove_window(ctypes.byref(t0), ctypes.byref(t1))
             wins.append((t0.value, t1.value))
         except Exception as e:  # noqa: BLE001
             errs.append(e)
@@ -364,6 +364,30 @@ def spark_concurrent_prove(wl, rx, ry, tape_seed, k, gens_nnz=None):
     if errs:
         raise errs[0]
     return (max(w[1] for w in wins) - min(w[0] for w in wins)) * 1e-6
+
+
+def last_prove_seconds():
+    """the calling thread's last prove window (orc_r1cs_prove / orc_snark_prove / orc_spark_prove): the prove alone,
+    without setup or verification"""
+    t0, t1 = ctypes.c_double(0), ctypes.c_double(0)
+    lib().orc_last_prove_window(ctypes.byref(t0), ctypes.byref(t1))
+    return (t1.value - t0.value) * 1e-6
+
+
+def spark_concurrent_prove(wl, rx, ry, tape_seed, k, gens_nnz=None):
+    """k concurrent oracle SPARK proves (multi_evaluate + SparseMatPolyEvalProof::prove) of the same workload"""
+    return concurrent_proves(lambda: spark_prove(wl, rx, ry, tape_seed, gens_nnz=gens_nnz), k)
+
+
+def snark_concurrent_prove(wl, tape_seed, k, **kw):
+    """k concurrent oracle SNARK::prove calls of the same workload, timed prove-only (SNARK::encode, the R1CSGens
+    derivation and the verification outside the window)"""
+    return concurrent_proves(lambda: snark_prove(wl, tape_seed, **kw), k)
+
+
+def r1cs_concurrent_prove(wl, tape_seed, k, **kw):
+    """k concurrent oracle R1CSProof::prove calls of the same workload, timed prove-only (R1CSGens derivation outside)"""
+    return concurrent_proves(lambda: r1cs_prove(wl, tape_seed, **kw), k)
 
 
 def spark_last_prove_us():

@@ -180,7 +180,8 @@ __global__ void __launch_bounds__(256) k_comb_join(const Ext* __restrict__ part,
   if (q == 0) out[b] = acc;
 }
 
-// comb tables of all live generator sets, against the process-wide cap (SPG_COMB_GB, default 96)
+// comb tables of all live generator sets of this process, against the process-wide cap (SPG_COMB_GB, default 96 GiB;
+// a table replaced by a wider one stays allocated until spg_gens_free, see spg_gens::comb_retired)
 static std::atomic<size_t> g_comb_bytes{0};
 
 void comb_free(const spg_gens* g) {
@@ -222,8 +223,21 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
   const int NS = (int)cn + 1, C = comb_c_for(cn);
   const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
-  static const size_t cap = (size_t)(getenv("SPG_COMB_GB") ? atof(getenv("SPG_COMB_GB")) : 96.0) * (1ull << 30);
+  // the cap is per process (SPG_COMB_GB, default 96 GiB); without an explicit setting a table is also built only when
+  // the device keeps kCombHeadroom free beside it, so co-located provers (several processes on one GPU) cannot starve
+  // each other's workspaces into SPG_E_NOMEM: a table that does not fit leaves the rows on the buckets
+  static const bool cap_set = getenv("SPG_COMB_GB") != nullptr;
+  static const size_t cap = (size_t)(cap_set ? atof(getenv("SPG_COMB_GB")) : 96.0) * (1ull << 30);
   if (g_comb_bytes.load() + bytes > cap) return 1;
+  if (!cap_set) {
+    static const size_t kCombHeadroom = (size_t)24 << 30;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+      (void)hipGetLastError();
+      return 1;
+    }
+    if (bytes + kCombHeadroom > free_b) return 1;
+  }
   Niels* comb = nullptr;
   Fp* zs = nullptr;
   const size_t lanes = entries / kCombRun;

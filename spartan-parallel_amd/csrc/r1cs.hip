@@ -1020,9 +1020,12 @@ int Prover::run_inner(Laps& lp) {
       return phase2_eval(ctx, *TA, *TZ, mode, instance_len, ws_len, nws, single, sc_ni, eq_l, partials,
                          nullptr, fold);
     };
-    // one ABC serving every instance is folded into this buffer by a fused round (then the two swap)
+    // one ABC serving every instance is folded into this buffer by a fused round (then the two swap). The fused fold
+    // writes it from the points of local instance 0 (global p0): only when that instance spans ABC's whole width
+    // (num_inputs[0]) -- a sharded rank whose first instance is narrower takes the separate fold
+    const bool fuse2 = sc_fuse_on() && (!single || num_inputs[p0] == num_inputs[0]);
     Fq* ABC2 = nullptr;
-    if (sc_fuse_on() && single) {
+    if (fuse2 && single) {
       ABC2 = (Fq*)ws_get(ctx, WS_ABC2, btot * sizeof(Fq) + 64);
       if (!ABC2) return set_err(ctx, SPG_E_NOMEM, "ABC");
     }
@@ -1060,7 +1063,7 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p2_host");
       const bool compact_next = j + 1 == ny + nw && np > 0;
       const int next_mode = j + 1 < ny ? MODE_X : (j + 1 < ny + nw ? MODE_W : MODE_P);
-      if (sc_fuse_on() && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
+      if (fuse2 && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
         // the fold rides in the next round's evaluation (k_phase2_eval<true>)
         Fold2 f;
         rc = pqx_fold_plan(ctx, *TA, mode, &f.a);
@@ -1599,13 +1602,14 @@ int witness_from_parts(spg_ctx* ctx, const std::vector<WPart>& secs, spg_r1cs_wi
   }
   // parts already resident on this device (SNARK::prove's block_vars and exec buffers, alive and unchanged for
   // the whole prove) are read in place; only host parts are copied into d_w
-  auto on_device = [](const void* q) {
+  // (a buffer on another GPU is copied like a host part: k_spmv / k_z_fill would otherwise read it across devices)
+  auto on_device = [ctx](const void* q) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, q) != hipSuccess) {
       (void)hipGetLastError();  // an unregistered host pointer: not an error of the prove
       return false;
     }
-    return a.type == hipMemoryTypeDevice;
+    return a.type == hipMemoryTypeDevice && a.device == ctx->device;
   };
   static const bool in_place = !getenv("SPG_WIT_IN_PLACE") || atoi(getenv("SPG_WIT_IN_PLACE")) != 0;
   std::vector<std::vector<char>> dev(secs.size());

@@ -790,7 +790,12 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         FqV ev(last_round && ends ? 3 + 6 * nt : 3);
         const int rc2 = mbox_wait(ctx, A.seq0 + (uint32_t)k, ev.data(), (int)ev.size());
         if (rc2) {
-          if (!last_round) down_post(ctx, kDownAbort, fq_zero());  // every workgroup leaves its wait
+          if (!last_round) {
+            down_post(ctx, kDownAbort, fq_zero());  // every workgroup leaves its wait
+            // ... and has left before the next launch clears the abort word: the stream drains here
+            (void)hipStreamSynchronize(s);
+            (void)hipGetLastError();
+          }
           return rc2;
         }
         lp.lap("round_eval_wait");

@@ -50,10 +50,12 @@ class R1CSWorkload:
     """Inputs of R1CSProof::prove (src/r1csproof.rs:210-230) for the synthetic circuit."""
 
     def __init__(self, num_cons, num_proofs, num_sections=1, max_num_inputs=None, seed=0x5350415254414E31,
-                 shared_instance=False, instances=None):
+                 shared_instance=False, instances=None, num_inputs=None):
         """instances: generate witness data only for these instance indices (sharded proving); every
         instance then draws from its own stream seed ^ (p+1)*0x9E3779B97F4A7C15, so any rank can build its
-        shard alone. None: all instances from one sequential stream (the layout the fixtures pin)."""
+        shard alone. None: all instances from one sequential stream (the layout the fixtures pin).
+        num_inputs: per-instance witness widths (powers of two <= max_num_inputs) instead of the derived ones, e.g.
+        one shared matrix serving instances of different widths (check_prove_args accepts it; ADVICE r4 case)."""
         self.P = len(num_cons)
         assert len(num_proofs) == self.P
         for x in list(num_cons) + list(num_proofs):
@@ -66,6 +68,10 @@ class R1CSWorkload:
         self.max_num_inputs = max_num_inputs or max(4, 2 * self.max_num_cons)
         self.num_inputs = [min(max(4, 2 * x), self.max_num_inputs) if not shared_instance else self.max_num_inputs
                            for x in num_cons]
+        if num_inputs is not None:
+            assert len(num_inputs) == self.P
+            assert all(y & (y - 1) == 0 and 4 <= y <= self.max_num_inputs for y in num_inputs)
+            self.num_inputs = list(num_inputs)
         if shared_instance:
             assert len(set(num_cons)) == 1
         self.num_vars = (1 << (num_sections - 1).bit_length()) * self.max_num_inputs

@@ -16,7 +16,18 @@ CASES = {
     "p4_shared": ([64] * 4, [8, 8, 4, 8], 2, True),
     "p3_uneven": ([16, 16, 16], [4, 4, 4], 1, False),
     "p5_uneven": ([16, 32, 16, 8, 16], [4, 2, 4, 4, 2], 2, False),
+    # one shared matrix, instances of different widths: rank 1's first instance (2) is narrower than the matrix
+    # (instance 0's width), so its fused phase-2 fold could not write the ABC ping-pong buffer
+    "p4_shared_mixed_inputs": ([64] * 4, [8, 8, 4, 8], 2, True, [128, 128, 64, 128]),
 }
+
+
+def _wl(case, **kw):
+    import workload
+
+    nc, npf, nws, shared, *rest = CASES[case]
+    return workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared,
+                                 num_inputs=rest[0] if rest else None, **kw)
 WORLD = {"p5_uneven": 4}  # ceil split would leave rank 3 empty; the balanced split gives 2,1,1,1
 
 
@@ -45,8 +56,7 @@ def _worker(rank, world, port, case, q, bad_shard=False, failpoint=None, cb_fail
     os.environ["SPG_PIN"] = "0"  # several ranks share the test box's GPU (and would pick the same CPU domain)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        nc, npf, nws, shared = CASES[case]
-        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+        wl = _wl(case)
         ctx = spg.Context(0)
         ctx.set_comm(rank, world, spg.torch_allgather(dist))
         gens = spg.R1CSGens(ctx, b"gens_r1cs_sat", 1 << 24)
@@ -117,8 +127,7 @@ def _run(case, world, bad_shard=False, failpoint=None, cb_fail=False, timeout=30
 def test_sharded_proof_matches_oracle(oracle, case):
     import workload
 
-    nc, npf, nws, shared = CASES[case]
-    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+    wl = _wl(case)
     ref, _ = oracle.r1cs_prove(wl, workload.tape_seed())
     for rank, pf, err in _run(case, WORLD.get(case, 2)):
         assert err is None, err
@@ -310,8 +319,7 @@ def _rccl_worker(rank, world, port, case, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        nc, npf, nws, shared = CASES[case]
-        wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+        wl = _wl(case)
         ctx = spg.Context(rank)
         ctx.set_comm_rccl(rank, world, dist)
         gens = spg.R1CSGens(ctx, b"gens_r1cs_sat", 1 << 24)
@@ -336,9 +344,7 @@ def test_rccl_two_gpus_sharded_r1cs(oracle):
     if torch.cuda.device_count() < 2:
         pytest.skip("RCCL needs one GPU per rank; this box has one")
     case = "p4_ragged_3secs"
-    nc, npf, nws, shared = CASES[case]
-    ref, _ = oracle.r1cs_prove(workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared),
-                               workload.tape_seed())
+    ref, _ = oracle.r1cs_prove(_wl(case), workload.tape_seed())
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
