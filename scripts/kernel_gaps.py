@@ -1,0 +1,37 @@
+"""Per-kernel duration and the idle gap before each launch (previous kernel's end -> this kernel's start on the
+device), from a rocprofv3 --kernel-trace CSV: where a transcript-sequential round's wall time goes besides the kernel.
+kernel_gaps.py DIR [name-substring ...]  (DIR searched for *kernel_trace.csv; only the main queue's kernels count)"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def main(d, pats):
+    fs = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for f in fs:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    acc = defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # launches, duration ns, gap ns, max gap
+    prev_end = None
+    for s, e, n in rows:
+        key = n.split("(")[0].replace("void ", "")[:60]
+        if prev_end is not None and (not pats or any(p in key for p in pats)):
+            g = max(0, s - prev_end)
+            a = acc[key]
+            a[0] += 1
+            a[1] += e - s
+            a[2] += g
+            a[3] = max(a[3], g)
+        prev_end = max(prev_end or 0, e)
+    for k, (n, du, ga, mx) in sorted(acc.items(), key=lambda kv: -kv[1][1] - kv[1][2])[:25]:
+        print(f"{k:62s} n={n:6d} dur={du / n / 1e3:7.2f} us gap_before={ga / n / 1e3:7.2f} us (total dur "
+              f"{du / 1e6:7.2f} ms, gaps {ga / 1e6:7.2f} ms)")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2:])

@@ -144,6 +144,66 @@ static void run(int nt, int log_len, int fold, unsigned K, Fq* vec, Fq* cin, Fq*
          K == 1 ? (p[3] - p[2]) * 0.01 : 0.0);
 }
 
+// the paired launch (k_layer_pair) of rounds (len, len / 2) against the two single quad rounds it replaces
+template <int BS>
+static void run_pair(int nt, int log_len, int nf, Fq* cin, Fq* cout, Triple* dtr, Fq* dcoef, Fq* part, unsigned* ctr,
+                     uint32_t* mb_dev, volatile uint32_t* mb_host, unsigned long long* probe) {
+  PairArgs P;
+  P.tr = dtr;
+  P.coeff = dcoef;
+  P.nt = nt;
+  P.log_len = log_len;
+  P.nf = nf;
+  for (int i = 0; i < 8; i++) P.r1.l[i] = P.r2.l[i] = P.r12.l[i] = 0x01234567u * (i + 3);
+  P.r1.l[7] = P.r2.l[7] = P.r12.l[7] = 0x01000000u;
+  P.cin = cin;
+  P.cout = cout;
+  P.partials = part;
+  P.counter = ctr;
+  P.mb = mb_dev;
+  P.ends = 0;
+  P.probe = nullptr;
+  const long lanes = 16L * nt * (1L << (log_len - 1));
+  const unsigned K = (unsigned)((lanes + BS - 1) / BS);
+  uint32_t seq = 70000;
+  for (int w = 0; w < 3; w++) {
+    P.seq = ++seq;
+    hipLaunchKernelGGL(k_layer_pair<BS>, dim3(K), dim3(BS), 0, 0, P);
+  }
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int R = 20;
+  hipEventRecord(e0, 0);
+  for (int i = 0; i < R; i++) {
+    P.seq = ++seq;
+    hipLaunchKernelGGL(k_layer_pair<BS>, dim3(K), dim3(BS), 0, 0, P);
+  }
+  hipEventRecord(e1, 0);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < R; i++) {
+    P.seq = ++seq;
+    hipLaunchKernelGGL(k_layer_pair<BS>, dim3(K), dim3(BS), 0, 0, P);
+    while (__atomic_load_n(mb_host, __ATOMIC_ACQUIRE) != P.seq) {
+    }
+  }
+  const double rt = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
+  hipDeviceSynchronize();
+  P.seq = ++seq;
+  P.probe = probe;
+  hipLaunchKernelGGL(k_layer_pair<BS>, dim3(K), dim3(BS), 0, 0, P);
+  hipDeviceSynchronize();
+  unsigned long long p[8];
+  hipMemcpy(p, probe, 64, hipMemcpyDeviceToHost);
+  printf("pair nt=%2d len=%5d nf=%d K=%4u BS=%3d: event %.1f us/launch, launch+mailbox round trip %.1f us | block 0: "
+         "fold %.2f, points %.2f, reduce %.2f, post %.2f us\n",
+         nt, 1 << log_len, nf, K, BS, ms * 1000 / R, rt, (p[1] - p[0]) * 0.01, (p[2] - p[1]) * 0.01,
+         (p[3] - p[2]) * 0.01, K == 1 ? (p[4] - p[3]) * 0.01 : 0.0);
+}
+
 int main() {
   const int NT = 32, MAXL = 4096;
   Fq *vec, *cin, *cout, *dcoef, *part;
@@ -179,6 +239,29 @@ int main() {
     run_armed<256>(6, 5, cin, cout, dtr, dcoef, mbd, (volatile uint32_t*)mbh, dbd, (volatile uint32_t*)dbh);
   }
   if (getenv("ARMED_ONLY")) return 0;
+  if (getenv("PAIR_ONLY")) {
+    const int shapes[][2] = {{24, 1}, {24, 2}, {24, 4}, {24, 6}, {24, 8}, {4, 1}, {4, 4}, {4, 8}, {4, 10}};
+    for (auto& sh : shapes) {
+      const int nt = sh[0], lg = sh[1];
+      for (int nf = 1; nf <= 2; nf++) {
+        if (16L * nt * (1L << (lg - 1)) <= 64)
+          run_pair<64>(nt, lg, nf, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
+        else
+          run_pair<256>(nt, lg, nf, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
+      }
+      // the single quad rounds it replaces (fold = 1): len and len / 2, the prover's grid
+      for (int l = lg; l >= lg - 1 && l >= 0; l--) {
+        const long W = (long)nt << l;
+        const unsigned K = (unsigned)std::min<long>((W * 4 + 255) / 256, 2048);
+        if (W <= 16)
+          run<64, true>(nt, l, 1, (unsigned)((W * 4 + 63) / 64), vec, cin, cout, dtr, dcoef, part, ctr, mbd,
+                        (volatile uint32_t*)mbh, probe);
+        else
+          run<256, true>(nt, l, 1, K, vec, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
+      }
+    }
+    return 0;
+  }
   for (int fold = 0; fold < 2; fold++) {
     run<64, true>(1, 0, fold, 1, vec, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
     run<256, true>(8, 3, fold, 1, vec, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);

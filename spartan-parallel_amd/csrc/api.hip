@@ -132,8 +132,14 @@ int mbox_wait(spg_ctx* ctx, uint32_t seq, Fq* out, int n) {
         return set_err(ctx, SPG_E_HIP, "mailbox: timed out");
     }
   }
-  for (int k = 0; k < n; k++)
-    for (int i = 0; i < 8; i++) out[k].l[i] = ctx->mbox[8 + 8 * k + i];
+  // the posted scalars: their cache lines were written by the device (snooped out of this core's caches), so each is a
+  // miss; touch every line first so the misses overlap (one DRAM latency for the lot instead of one per line: a layer's
+  // last round posts up to ~300 scalars), then copy. The acquire load of the sequence number above orders these reads
+  // after the device's stores; the page does not change again before the next launch.
+  const uint8_t* src = (const uint8_t*)(ctx->mbox + 8);
+  const size_t bytes = (size_t)n * sizeof(Fq);
+  for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch(src + o, 0, 0);
+  memcpy(out, src, bytes);
   return 0;
 }
 
@@ -186,6 +192,7 @@ int d2h_multi(spg_ctx* ctx, const FqSeg* segs, int k, Fq* h) {
   hipLaunchKernelGGL(k_gather_res, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, ctx->stream, a, ctx->d_res);
   SPG_HIP(ctx, hipGetLastError());
   SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (size_t o = 0; o < total * sizeof(Fq); o += 64) __builtin_prefetch((const uint8_t*)ctx->res + o, 0, 0);  // (mbox_wait)
   memcpy(h, ctx->res, total * sizeof(Fq));
   return 0;
 }

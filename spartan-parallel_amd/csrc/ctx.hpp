@@ -248,10 +248,20 @@ __device__ __forceinline__ void st_sc1(Fq* p, const Fq& v) {
     __hip_atomic_store(w + i, (uint64_t)v.l[2 * i] | ((uint64_t)v.l[2 * i + 1] << 32), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
+// A scalar into coherent (fine-grained) host memory as two plain 16-byte stores, made visible by the system-scope
+// release fence that every post puts before its sequence number. Per-word system-scope atomic stores (what the posts
+// used through round 4) go out as one host write transaction per 4-byte word, serialised at ~45 ns each: a round's 3
+// scalars cost 2.2 us more from launch to host-visible, a layer's 147 posted entries 53 us
+// (scripts/micro/mbox_post.hip, profiles/r05_mbox_post.txt). Addresses are 32-byte aligned (mailbox slots).
+__device__ __forceinline__ void host_put(uint32_t* p, const Fq& v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4* q = (u32x4*)p;
+  q[0] = u32x4{v.l[0], v.l[1], v.l[2], v.l[3]};
+  q[1] = u32x4{v.l[4], v.l[5], v.l[6], v.l[7]};
+}
 // device side of the mailbox: the scalars, then (after a system-scope release fence) the sequence number
 __device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* v, int n) {
-  for (int k = 0; k < n; k++)
-    for (int i = 0; i < 8; i++) __hip_atomic_store(mb + 8 + 8 * k + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int k = 0; k < n; k++) host_put(mb + 8 + 8 * k, v[k]);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -259,12 +269,9 @@ __device__ __forceinline__ void mbox_post(uint32_t* mb, uint32_t seq, const Fq* 
 // three scalars (a sumcheck round's e0, e2, e3) without a local array: the array form's runtime-indexed loop put it
 // in scratch memory, and a kernel with a private segment costs more to dispatch
 __device__ __forceinline__ void mbox_post3(uint32_t* mb, uint32_t seq, const Fq& a, const Fq& b, const Fq& c) {
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    __hip_atomic_store(mb + 8 + i, a.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(mb + 16 + i, b.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(mb + 24 + i, c.l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  host_put(mb + 8, a);
+  host_put(mb + 16, b);
+  host_put(mb + 24, c);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -174,9 +174,7 @@ __global__ void __launch_bounds__(256) k_layer_close(const Triple* __restrict__ 
     const Fq* Cp = x.C ? x.C : cin;
     const Fq v[3] = {do_fold ? fold_at(x.A, 0, 1, r) : x.A[0], do_fold ? fold_at(x.B, 0, 1, r) : x.B[0],
                      do_fold ? fold_at(Cp, 0, 1, r) : Cp[0]};
-    for (int k = 0; k < 3; k++)
-      for (int i = 0; i < 8; i++)
-        __hip_atomic_store(mb + 8 + 8 * (3 * c + k) + i, v[k].l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int k = 0; k < 3; k++) host_put(mb + 8 + 8 * (3 * c + k), v[k]);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
@@ -228,10 +226,8 @@ __device__ __forceinline__ Fq layer_round_elems(const Triple* __restrict__ tr, c
     }
     if (ends && q < 3) {
       uint32_t* d = ends + 8 + 8 * (3 + 6 * c + 2 * q);
-      for (int j = 0; j < 8; j++) {
-        __hip_atomic_store(d + j, lo.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(d + 8 + j, hi.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      host_put(d, lo);
+      host_put(d + 8, hi);
     }
     const Fq al = fq_qbcast<0>(lo), ah = fq_qbcast<0>(hi), bl = fq_qbcast<1>(lo), bh = fq_qbcast<1>(hi);
     const Fq cl = fq_qbcast<2>(lo), ch = fq_qbcast<2>(hi);
@@ -261,7 +257,7 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
   if (gridDim.x == 1) {  // lanes 0..2 of wave 0 post e0, e2, e3, then lane 0 the sequence number
     if (ends) __syncthreads();
     if (t < 3) {
-      for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      host_put(mb + 8 + 8 * t, e);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     if (t == 0) {
@@ -294,12 +290,187 @@ __global__ void __launch_bounds__(BS) k_layer_round_q(const Triple* __restrict__
     }
   quad_block_sum<BS>(a);
   if (t < 3) {
-    for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    host_put(mb + 8 + 8 * t, a);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
   if (t == 0) {
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---- two rounds per launch (the small, latency-bound rounds) ---------------------------------------------------------
+// A small round is a host round trip (launch, dispatch, mailbox) around a few us of work, and a layer's rounds are
+// transcript-sequential. Round j + 1's evaluations need round j's challenge r, but only as the argument of a cubic:
+// with W the vectors of round j (2 len entries, the pending folds applied) and the 2 x 2 cube of element i < h = len / 2,
+//   P(t, s) = p00 + t (p10 - p00) + s (p01 - p00) + t s (p11 - p10 - p01 + p00),  p_ts = W[i + (2 t + s) h]
+// (t: round j's variable, offset len; s: round j + 1's, offset h), and F(t, s) = k A(t, s) B(t, s) C(t, s) summed over
+// every element, round j's evaluation at X is F(X, 0) + F(X, 1), and round j + 1's at Y is the cubic t -> F(t, Y) taken
+// at t = r (the fold by r is P(r, .)). So one launch posts F at 15 points -- t = 0..3 on the lines s = 0, 2, 3, and
+// t = 0, 2, 3 on s = 1 -- and the host draws r_j, interpolates round j + 1 at r_j and draws r_j+1 with no device round
+// trip between them. The next launch applies both folds at once (nf = 2: W[k] = a + r1 (c - a) + r2 (b - a) +
+// r1 r2 (d - c - b + a) over V[k + {0, 2, 4, 6} len], r1 bound first), so a pair costs one launch instead of two.
+// Lanes: 16 per element (a DPP row). Stage 1: lane g < 12 computes corner m = g & 3 of vector g >> 2 (A, B, C) and
+// writes it back in place (every entry is read and written by its own lane: no grid barrier; the shared eq vector C
+// goes cin -> cout, written by circuit 0); lane 12 loads the coefficient k. Stage 2: row broadcasts (DPP row_newbcast)
+// give every lane the 12 corners and k. Stage 3: lane g forms its point's three values and k A B C. The row sums
+// meet in LDS like the quad sums, and the posted scalars are the 15 point sums in lane order:
+//   g 0..3: (t, s) = (g, 0); 4..7: (g - 4, 2); 8..11: (g - 8, 3); 12, 13, 14: (0, 1), (2, 1), (3, 1).
+// ends (a layer's last pair, h = 1): lane g < 12 also posts its corner as scalar 15 + 12 c + g, so the host folds the
+// final claims itself.
+template <int N>
+__device__ __forceinline__ Fq fq_rowbcast(const Fq& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], 0x150 + N, 0xf, 0xf, false);
+  return r;
+}
+// word-wise select (no scratch: a select of whole structs put the quad kernels' values in private memory)
+__device__ __forceinline__ Fq fq_sel(bool c, const Fq& a, const Fq& b) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+// n x (n in 0..3, lane-varying)
+__device__ __forceinline__ Fq fq_small(const Fq& x, int n) {
+  const Fq x2 = fq_add(x, x), x3 = fq_add(x2, x);
+  return fq_sel(n == 3, x3, fq_sel(n == 2, x2, fq_sel(n == 1, x, fq_zero())));
+}
+// P(t, s) from the corners (p00, p01, p10, p11)
+__device__ __forceinline__ Fq cube_at(const Fq& p00, const Fq& p01, const Fq& p10, const Fq& p11, int t, int s) {
+  const Fq ds = fq_sub(p01, p00), dt = fq_sub(p10, p00), dd = fq_sub(fq_sub(p11, p10), ds);
+  const Fq base = fq_add(p00, fq_small(ds, s)), slope = fq_add(dt, fq_small(dd, s));
+  return fq_add(base, fq_small(slope, t));
+}
+// sums of the values of lanes with equal (thread & 15) over a block of BS threads; the sum for g is left in thread g
+template <int BS>
+__device__ __forceinline__ void row_block_sum(Fq& e) {
+  constexpr int NW = BS / 64;
+  __shared__ uint32_t wsum[NW > 1 ? NW : 1][16][8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  e = fq_add(e, fq_shfl_xor(e, 16));
+  e = fq_add(e, fq_shfl_xor(e, 32));
+  if (NW > 1) {
+    if (lane < 16)
+      for (int j = 0; j < 8; j++) wsum[w][lane][j] = e.l[j];
+    __syncthreads();
+    if (w == 0 && lane < 16)
+      for (int v = 1; v < NW; v++) {
+        Fq o;
+        for (int j = 0; j < 8; j++) o.l[j] = wsum[v][lane][j];
+        e = fq_add(e, o);
+      }
+    __syncthreads();
+  }
+}
+struct PairArgs {
+  const Triple* tr;
+  const Fq* coeff;
+  int nt;
+  int log_len;  // round j's half length len = 2^log_len (>= 2: h = len / 2 >= 1)
+  int nf;       // pending folds: 0, 1 (r1) or 2 (r1, then r2; r12 = r1 r2)
+  Fq r1, r2, r12;
+  const Fq* cin;
+  Fq* cout;
+  Fq* partials;  // 16 per workgroup
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq;
+  int ends;
+  unsigned long long* probe;  // phase timestamps (scripts/micro), null in the prover
+};
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_pair(PairArgs A) {
+  __shared__ bool last;
+  const int t = threadIdx.x, g = t & 15;
+  unsigned long long* pr = A.probe ? A.probe + 8 * blockIdx.x : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
+  const int len = 1 << A.log_len, h = len >> 1;
+  const long total = (long)A.nt << (A.log_len - 1);
+  const long u = ((long)blockIdx.x * BS + t) >> 4;  // this row's element (rows past the end idle, contribute zero)
+  // this lane's point (t, s)
+  const int pt = g < 4 ? g : (g < 8 ? g - 4 : (g < 12 ? g - 8 : (g == 12 ? 0 : (g == 13 ? 2 : 3))));
+  const int ps = g < 4 ? 0 : (g < 8 ? 2 : (g < 12 ? 3 : 1));
+  Fq e = fq_zero();
+  if (u < total) {
+    const int c = (int)(u >> (A.log_len - 1)), i = (int)(u & (h - 1));
+    const Triple x = A.tr[c];
+    // stage 1: corner m of vector v
+    Fq w = fq_zero();
+    if (g < 12) {
+      const int v = g >> 2, m = g & 3, k = i + m * h;
+      const Fq* src = v == 0 ? x.A : (v == 1 ? x.B : (x.C ? x.C : A.cin));
+      if (A.nf == 0) {
+        w = src[k];
+      } else if (A.nf == 1) {
+        const Fq a = src[k], b = src[k + 2 * len];
+        w = fq_add(a, fq_mul(A.r1, fq_sub(b, a)));
+      } else {
+        const Fq a = src[k], b = src[k + 2 * len], cc = src[k + 4 * len], d = src[k + 6 * len];
+        const Fq t1 = fq_mul(A.r1, fq_sub(cc, a)), t2 = fq_mul(A.r2, fq_sub(b, a)),
+                 t3 = fq_mul(A.r12, fq_add(fq_sub(d, cc), fq_sub(a, b)));
+        w = fq_add(fq_add(a, t1), fq_add(t2, t3));
+      }
+      if (A.nf > 0) {
+        Fq* dst = v == 0 ? x.A : (v == 1 ? x.B : (x.C ? x.C : (c == 0 ? A.cout : nullptr)));
+        if (dst) dst[k] = w;
+      }
+      if (A.ends) {
+        uint32_t* d = A.mb + 8 + 8 * (15 + 12 * c + g);
+        host_put(d, w);
+      }
+    } else if (g == 12) {
+      w = A.coeff[c];
+    }
+    if (pr && t == 0) pr[1] = wall_clock64();
+    // stage 2: every lane of the row takes the corners and k
+    const Fq a00 = fq_rowbcast<0>(w), a01 = fq_rowbcast<1>(w), a10 = fq_rowbcast<2>(w), a11 = fq_rowbcast<3>(w);
+    const Fq b00 = fq_rowbcast<4>(w), b01 = fq_rowbcast<5>(w), b10 = fq_rowbcast<6>(w), b11 = fq_rowbcast<7>(w);
+    const Fq c00 = fq_rowbcast<8>(w), c01 = fq_rowbcast<9>(w), c10 = fq_rowbcast<10>(w), c11 = fq_rowbcast<11>(w);
+    const Fq kk = fq_rowbcast<12>(w);
+    // stage 3: this lane's point
+    const Fq av = cube_at(a00, a01, a10, a11, pt, ps), bv = cube_at(b00, b01, b10, b11, pt, ps),
+             cv = cube_at(c00, c01, c10, c11, pt, ps);
+    const Fq ab = fq_mul(av, bv), kc = fq_mul(kk, cv);
+    e = fq_mul(ab, kc);
+  }
+  if (A.ends) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the corners reach the host before any ticket / post
+  if (pr && t == 0) pr[2] = wall_clock64();
+  row_block_sum<BS>(e);
+  if (pr && t == 0) pr[3] = wall_clock64();
+  if (gridDim.x == 1) {  // lanes 0..14 of wave 0 post the 15 point sums, then lane 0 the sequence number
+    if (A.ends) __syncthreads();
+    if (t < 15) {
+      host_put(A.mb + 8 + 8 * t, e);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (pr) pr[4] = wall_clock64();
+    }
+    return;
+  }
+  // several workgroups: partials by sc1 stores and a ticket (as quad_grid_post)
+  if (t < 16) st_sc1(&A.partials[16 * blockIdx.x + t], e);
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(A.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  Fq s = fq_zero();
+  for (unsigned j = t >> 4; j < gridDim.x; j += BS / 16) s = fq_add(s, ld_sc1(&A.partials[16 * j + g]));
+  row_block_sum<BS>(s);
+  if (t < 15) {
+    host_put(A.mb + 8 + 8 * t, s);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -412,14 +583,12 @@ __global__ void __launch_bounds__(BS) k_layer_persist(PersistArgs A) {
           const Fq* v = p == 0 ? x.A : (p == 1 ? x.B : (x.C ? x.C : A.cb[cur]));
           const Fq lo = ld_sc1(v), hi = ld_sc1(v + 1);
           uint32_t* d = A.mb + 8 + 8 * (3 + 6 * c + 2 * p);
-          for (int j = 0; j < 8; j++) {
-            __hip_atomic_store(d + j, lo.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(d + 8 + j, hi.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
+          host_put(d, lo);
+          host_put(d + 8, hi);
         }
       }
       if (t < 3)
-        for (int j = 0; j < 8; j++) __hip_atomic_store(A.mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        host_put(A.mb + 8 + 8 * t, a);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __syncthreads();
       if (t == 0) {

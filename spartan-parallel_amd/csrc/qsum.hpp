@@ -53,7 +53,7 @@ __device__ __forceinline__ void quad_grid_post(Fq e, Fq* __restrict__ partials, 
   quad_block_sum<BS>(e);
   if (gridDim.x == 1) {  // lanes 0..2 of wave 0 post e0, e2, e3, then lane 0 the sequence number
     if (t < 3) {
-      for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, e.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      host_put(mb + 8 + 8 * t, e);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
     if (t == 0) __hip_atomic_store(mb, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -71,7 +71,7 @@ __device__ __forceinline__ void quad_grid_post(Fq e, Fq* __restrict__ partials, 
     for (unsigned j = t >> 2; j < gridDim.x; j += BS / 4) a = fq_add(a, ld_sc1(&partials[3 * j + q]));
   quad_block_sum<BS>(a);
   if (t < 3) {
-    for (int j = 0; j < 8; j++) __hip_atomic_store(mb + 8 + 8 * t + j, a.l[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    host_put(mb + 8 + 8 * t, a);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
   if (t == 0) {

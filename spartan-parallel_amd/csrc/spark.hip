@@ -724,8 +724,13 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     FqV r_prod;
     bool pending = false;  // a bound_poly_var_top with r_pend not yet applied
     Fq r_pend = fq_zero();
+    // after a paired launch (k_layer_pair): a second pending fold, with r_pend2 (bound after r_pend); only a paired
+    // launch applies two, and once a layer's rounds pair up they pair up to the layer's end
+    bool pend2 = false;
+    Fq r_pend2 = fq_zero();
     // A[0], B[0], C[0] of every triple (after the pending fold, if any), by mailbox
     auto close = [&](FqV& fin) -> int {
+      if (pend2) return set_err(ctx, SPG_E_ARG, "layer close after a paired round");  // (the last pair posts its ends)
       fin.resize(3 * tr.size());
       KScope ks(ctx, "spark_layer_close");
       const uint32_t seq = ++ctx->mbox_seq;
@@ -833,8 +838,92 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       static const bool quad = !getenv("SPG_LAYER_QUAD") || atoi(getenv("SPG_LAYER_QUAD")) != 0;
       static const size_t wide_min = getenv("SPG_WIDE_MIN") ? (size_t)atol(getenv("SPG_WIDE_MIN")) : ((size_t)1 << 19);
       static const size_t persist_max = getenv("SPG_PERSIST_MAX") ? (size_t)atol(getenv("SPG_PERSIST_MAX")) : 4096;
+      static const bool pair_on = !getenv("SPG_LAYER_PAIR") || atoi(getenv("SPG_LAYER_PAIR")) != 0;
+      static const size_t pair_max = getenv("SPG_PAIR_MAX") ? (size_t)atol(getenv("SPG_PAIR_MAX")) : 4096;
       while (log_len > 0) {
         const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
+        // two rounds in one launch (k_layer_pair): small rounds of an unsharded layer, an even number of them left
+        // (an odd count first runs one single round), every element's 16 lanes within pair_max elements, the last
+        // pair's corners within the mailbox
+        if (pair_on && quad && !local && close_after && log_len >= 2 && log_len % 2 == 0 &&
+            (tr.size() << (log_len - 2)) <= std::min<size_t>(pair_max, 6144) && 15 + 12 * tr.size() <= kMboxScalars &&
+            ngroups * ((size_t)1 << (log_len - 1)) < wide_min && !(persist_on && ctx->nranks == 1)) {
+          const int lgj = (int)log_len - 1;  // round j's half length 2^lgj; round j + 1's 2^(lgj - 1)
+          log_len -= 2;
+          const size_t nt = tr.size(), h = (size_t)1 << (lgj - 1), lanes = 16 * nt * h;
+          static const int pair_bs = getenv("SPG_PAIR_BS") ? atoi(getenv("SPG_PAIR_BS")) : 0;  // 64: more workgroups
+          const int BSp = lanes <= 64 || pair_bs == 64 ? 64 : 256;
+          const unsigned Kp = (unsigned)((lanes + BSp - 1) / BSp);
+          const bool ends = log_len == 0;  // the layer's last pair posts every vector's 2 x 2 corners
+          const int nf = pend2 ? 2 : (pending ? 1 : 0);
+          PairArgs P;
+          P.tr = dtr;
+          P.coeff = dcoef;
+          P.nt = (int)nt;
+          P.log_len = lgj;
+          P.nf = nf;
+          P.r1 = r_pend;
+          P.r2 = r_pend2;
+          P.r12 = fq_mul(r_pend, r_pend2);
+          P.cin = cbuf[cur];
+          P.cout = cbuf[cur ^ 1];
+          P.partials = part;
+          P.counter = ctx->d_counter;
+          P.mb = ctx->d_mbox;
+          P.seq = ++ctx->mbox_seq;
+          P.ends = ends ? 1 : 0;
+          P.probe = nullptr;
+          {
+            // algorithmic bytes: per distinct vector and element, 4 corners from 4 2^nf entries, written back when folded
+            const double per = 32.0 * (4.0 * (double)(1 << nf) + (nf ? 4.0 : 0.0));
+            KScope ks(ctx, "spark_layer_pair", per * (double)h * (double)(2 * nt + ngroups));
+            if (BSp == 64)
+              hipLaunchKernelGGL(k_layer_pair<64>, dim3(Kp), dim3(64), 0, s, P);
+            else
+              hipLaunchKernelGGL(k_layer_pair<256>, dim3(Kp), dim3(256), 0, s, P);
+          }
+          if (nf) cur ^= 1;
+          FqV ev(15 + (ends ? 12 * nt : 0));
+          const hipError_t le = hipGetLastError();
+          lp.lap(ends ? "pair_launch_end" : "pair_launch");
+          const int rc2 = le != hipSuccess ? set_err(ctx, SPG_E_HIP, std::string("layer pair: ") + hipGetErrorString(le))
+                                           : mbox_wait(ctx, P.seq, ev.data(), (int)ev.size());
+          if (rc2) return rc2;
+          lp.lap(ends ? "pair_wait_end" : "pair_wait");
+          // round j: F(X, 0) + F(X, 1) at X = 0, 2, 3
+          const Fq ej[3] = {fq_add(ev[0], ev[12]), fq_add(ev[2], ev[13]), fq_add(ev[3], ev[14])};
+          const Fq rj = host_round(ej);
+          // round j + 1: the cubics t -> F(t, Y) through t = 0..3 (lines Y = 0, 2, 3) at t = r_j
+          static const Fq inv2 = fq_inv(fq_from_u64(2)), inv6 = fq_inv(fq_from_u64(6));
+          const Fq a0 = rj, a1 = fq_sub(rj, fq_one()), a2 = fq_sub(a1, fq_one()), a3 = fq_sub(a2, fq_one());
+          const Fq a01 = fq_mul(a0, a1), a23 = fq_mul(a2, a3);
+          const Fq L[4] = {fq_neg(fq_mul(fq_mul(a1, a23), inv6)), fq_mul(fq_mul(a0, a23), inv2),
+                           fq_neg(fq_mul(fq_mul(a01, a3), inv2)), fq_mul(fq_mul(a01, a2), inv6)};
+          Fq ej1[3];
+          for (int y = 0; y < 3; y++) {
+            Fq acc = fq_zero();
+            for (int k = 0; k < 4; k++) acc = fq_add(acc, fq_mul(L[k], ev[4 * y + k]));
+            ej1[y] = acc;
+          }
+          const Fq rj1 = host_round(ej1);
+          lp.lap("pair_host");
+          if (ends) {  // the 2 x 2 cube of every vector folded at (r_j, r_j+1): the layer's final claims
+            fin->resize(3 * nt);
+            for (size_t c = 0; c < 3 * nt; c++) {
+              const Fq* w = &ev[15 + 4 * c];  // p00, p01, p10, p11 of vector c % 3 of triple c / 3
+              const Fq q0 = fq_add(w[0], fq_mul(rj, fq_sub(w[2], w[0]))), q1 = fq_add(w[1], fq_mul(rj, fq_sub(w[3], w[1])));
+              (*fin)[c] = fq_add(q0, fq_mul(rj1, fq_sub(q1, q0)));
+            }
+            pending = pend2 = false;
+            lp.lap("pair_fin");
+            return 0;
+          }
+          pending = pend2 = true;
+          r_pend = rj;
+          r_pend2 = rj1;
+          continue;
+        }
+        if (pend2) return set_err(ctx, SPG_E_ARG, "single layer round after a paired one");
         // every remaining round is a quad round of at most persist_max elements: one persistent launch for them all
         // (one process per GPU only: processes sharing a GPU time-slice its queues, and a resident loop could then
         // wait out its timeout while descheduled)

@@ -100,6 +100,9 @@ ROUND_FORMS = {
     "z_fill_after_round_0": {"SPG_Z_AFTER": "0"},
     "z_fill_at_phase2": {"SPG_Z_AFTER": "100000"},
     "eq_table_per_launch": {"SPG_EQ_MULTI": "0"},
+    "layer_single_rounds": {"SPG_LAYER_PAIR": "0"},
+    "layer_pairs_small_wgs": {"SPG_PAIR_BS": "64"},
+    "layer_pairs_everywhere": {"SPG_PAIR_MAX": "6144", "SPG_WIDE_MIN": str(1 << 40)},
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
 }
 
@@ -113,7 +116,10 @@ def test_round_forms(form):
     round), with workgroup 0 relaying the host's answer or every workgroup polling the host, with one workgroup over
     every round, with 256 workgroups, and without posting the layer's entries; the R1CS Z fill in stream order
     (SPG_Z_SIDE=0) or on the second stream after phase-1 round 0 or only at phase 2 (SPG_Z_AFTER); one eq table
-    per launch (SPG_EQ_MULTI=0); device witness parts copied instead of read in place (SPG_WIT_IN_PLACE=0)"""
+    per launch (SPG_EQ_MULTI=0); device witness parts copied instead of read in place (SPG_WIT_IN_PLACE=0); SPARK layer
+    rounds one per launch (SPG_LAYER_PAIR=0) instead of two per launch where they are small, paired rounds over 64-thread
+    workgroups (more of them: the ticketed sums and the last pair's corners from several workgroups), and pairs for every
+    round that fits (SPG_PAIR_MAX, no throughput-form rounds)"""
     import subprocess
     import sys
 
