@@ -31,6 +31,22 @@ def main(d, pats):
     for k, (n, du, ga, mx) in sorted(acc.items(), key=lambda kv: -kv[1][1] - kv[1][2])[:25]:
         print(f"{k:62s} n={n:6d} dur={du / n / 1e3:7.2f} us gap_before={ga / n / 1e3:7.2f} us (total dur "
               f"{du / 1e6:7.2f} ms, gaps {ga / 1e6:7.2f} ms)")
+    # idle device time by the (previous kernel -> next kernel) transition: where the host holds the device up
+    tr = defaultdict(lambda: [0, 0.0])
+    prev = None
+    busy_end = None
+    for s, e, n in rows:
+        key = n.split("(")[0].replace("void ", "").replace("spg::", "")[:34]
+        if prev is not None and busy_end is not None and s > busy_end:
+            t = tr[(prev, key)]
+            t[0] += 1
+            t[1] += s - busy_end
+        prev = key
+        busy_end = max(busy_end or 0, e)
+    tot = sum(v[1] for v in tr.values())
+    print(f"-- idle gaps by transition (total {tot / 1e6:.2f} ms):")
+    for (a, b), (n, g) in sorted(tr.items(), key=lambda kv: -kv[1][1])[:30]:
+        print(f"  {a:34s} -> {b:34s} n={n:6d} avg {g / n / 1e3:7.2f} us total {g / 1e6:7.2f} ms")
 
 
 if __name__ == "__main__":

@@ -207,6 +207,9 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extr
   pool().parallel_for((int)(B * K), [&](int task) {
     const size_t b = task / K;
     const int lo = (task % K) * per;
+    for (const uint8_t* q = (const uint8_t*)(bk + b * stride + lo); q < (const uint8_t*)(bk + b * stride + lo + per);
+         q += 64)
+      __builtin_prefetch(q, 0, 0);  // (as parts_finals)
     h::HExt run = h::hext_identity(), acc = h::hext_identity();
     for (int v = lo + per; v > lo; v--) {
       run = h::hext_add(run, h::hext_from_dev(bk[b * stride + v - 1]));
@@ -235,6 +238,10 @@ static void parts_finals(const Ext* bk, size_t B, size_t per, Pt* out, const h::
   pool().parallel_for((int)(B * K), [&](int task) {
     const size_t b = task / K, c = task % K;
     const size_t lo = per * c / K, hi = per * (c + 1) / K;
+    // the parts' lines were written by the device (coherent host memory, so not in this core's caches): every line
+    // of the chunk requested at once, their misses overlapping, before the dependent additions read them
+    for (const uint8_t* q = (const uint8_t*)(bk + b * per + lo); q < (const uint8_t*)(bk + b * per + hi); q += 64)
+      __builtin_prefetch(q, 0, 0);
     h::HExt acc = h::hext_from_dev(bk[b * per + lo]);
     for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(bk[b * per + i]));
     part[task] = acc;
