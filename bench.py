@@ -54,6 +54,11 @@ MADD_PEAK = 3.0e10
 # VALU instruction per 2 cycles at 2.4 GHz bound it at 1024 * 2.4e9 / (2 * 1527) * 64 = 5.15e10 madd/s if every
 # instruction were full rate -- an upper bound (64-bit multiply-adds are not), of which MADD_PEAK is 0.58
 MADD_ISSUE_CEILING = 1024 * 2.4e9 / (2 * 1527) * 64
+# whole-GPU throughput of the device Fq product (fq_mul_ps, the scalar field's Montgomery product) with 4 independent
+# chains per lane and 8 resident 256-thread blocks per CU: 1.44e11/s, measured on MI355X by
+# scripts/micro/fq_throughput.hip (output: profiles/r05_fq_throughput.txt) -- the peak the Fq-product-bound kernels
+# (R1CSProof sumcheck evaluations, SPARK layer rounds) are priced against in `roofline_fq`
+FQ_PEAK = 1.44e11
 GENS_LABEL = b"gens_r1cs_sat"
 GENS_NUM_VARS = 1 << 24  # TOTAL_NUM_VARS_BOUND = 10^7 -> 2^24 (examples/interface.rs:557-563)
 CONFIGS = {
@@ -257,6 +262,29 @@ def roofline_valu(prof, traffic_file=None):
     return out
 
 
+def roofline_fq(prof, traffic_file=None):
+    """VALU roofline of the modelled-Fq-products kernel with the largest device time: scalar-field products per
+    second (DESIGN.md 3.9 per-launch models) against the measured whole-GPU fq_mul throughput, beside the same launches'
+    algorithmic HBM rate"""
+    cand = {k: v for k, v in prof.items() if len(v) > 4 and v[4] > 0}
+    if not cand:
+        return None
+    dom = max(cand, key=lambda k: cand[k][1])
+    launches, us, nbytes, _, fqm = cand[dom][:5]
+    achieved = fqm / (us * 1e-6)
+    out = {"bound": "valu_fq", "kernel": dom, "achieved": round(achieved, 1), "peak": FQ_PEAK, "unit": "Fq products/s",
+           "frac": round(achieved / FQ_PEAK, 5), "traffic": traffic_of(dom, traffic_file),
+           "algorithmic_fq_products_per_launch": fqm / launches, "avg_launch_us": us / launches, "launches": launches,
+           "peak_source": "measured whole-GPU fq_mul throughput, scripts/micro/fq_throughput.hip, ILP 4, 8 blocks/CU "
+                          "(profiles/r05_fq_throughput.txt)"}
+    if nbytes:
+        gbs = nbytes / launches / (us / launches * 1e-6) / 1e9
+        out["algorithmic_bytes_per_launch"] = nbytes / launches
+        out["hbm_GBps"] = round(gbs, 1)
+        out["hbm_frac"] = round(gbs / HBM_PEAK_GBS, 5)
+    return out
+
+
 def rooflines(prof, traffic_file=None):
     """(roofline of the kernel with the most device time among the modelled ones, hbm one, valu one)"""
     h, v = roofline_hbm(prof, traffic_file), roofline_valu(prof, traffic_file)
@@ -271,7 +299,9 @@ def kernel_table(prof, steps, top=10):
     rows = sorted(prof.items(), key=lambda kv: -kv[1][1])[:top]
     return {k: {"launches_per_step": v[0] / steps, "ms_per_step": round(v[1] / steps / 1e3, 3),
                 "GBps": round(v[2] / (v[1] * 1e-6) / 1e9, 1) if v[2] else None,
-                "madds_per_s": round(v[3] / (v[1] * 1e-6), 1) if len(v) > 3 and v[3] else None} for k, v in rows}
+                "madds_per_s": round(v[3] / (v[1] * 1e-6), 1) if len(v) > 3 and v[3] else None,
+                "fq_products_per_s": round(v[4] / (v[1] * 1e-6), 1) if len(v) > 4 and v[4] else None}
+            for k, v in rows}
 
 
 def usable_cores():
@@ -438,7 +468,7 @@ def main_snark(a):
                        "constraints_per_block": 1 << a.log_cons, "executions_per_block": 1 << a.log_proofs,
                        "constraints_per_gpu": N, "num_vars": wl.num_vars, "num_ios": wl.num_ios,
                        "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{env.world}"},
-            "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
+            "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "roofline_fq": roofline_fq(prof),
             "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16],
             "device_busy_ms_per_step": round(prof.busy_us / a.steps / 1e3, 3),
@@ -554,7 +584,8 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
                    "gens": "R1CSGens(gens_r1cs_sat, 2^24)",
                    "parallelism": f"instance-sharded single proof x{env.world} ({transport})" if shard
                    else f"replicas x{env.world}"},
-        "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
+        "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
+        "roofline_fq": roofline_fq(prof, traffic_file), "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact, "proof_sha256": sorted(proofs)[0][:16],
         "ranks_agree": same, "transport": transport, "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
         "value_incl_witness_upload": round(units / t_incl, 1), "kernels": kernel_table(prof, steps)}
@@ -848,7 +879,8 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         "config": {"workload": "SparseMatPolyEvalProof::prove, batch 3 (src/sparse_mlpoly.rs:1497-1564)",
                    "log_nnz": k, "num_vars_x": k, "num_vars_y": k,
                    "parallelism": f"one proof sharded x{env.world} ({transport})" if shard else f"replicas x{env.world}"},
-        "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "cpu_baseline": cpu,
+        "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
+        "roofline_fq": roofline_fq(prof, traffic_file), "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_sha256": sorted(proofs)[0][:16], "ranks_agree": same,
         "transport": transport,
         "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),

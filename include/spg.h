@@ -78,6 +78,10 @@ int spg_prof_read(spg_ctx* ctx, char* names, long* launches, double* total_us, d
  * one per nonzero signed window digit of the MSM kernels */
 int spg_prof_read2(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, double* ops, int max,
                    int reset);
+/* the same plus the modelled VALU work in Fq (scalar-field Montgomery) products (fqm; 0 where not modelled): the
+ * sumcheck evaluations and SPARK layer rounds, priced against the measured whole-GPU Fq product rate */
+int spg_prof_read3(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, double* ops,
+                   double* fqm, int max, int reset);
 
 /* ---- device-resident scalar vectors (HBM) ----------------------------------------------------
  * Tables the prover keeps resident between calls (witness polynomials, sumcheck tables). */

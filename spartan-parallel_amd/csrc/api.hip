@@ -327,12 +327,13 @@ static hipEvent_t pool_event(spg_ctx* c) {
   return e;
 }
 
-KScope::KScope(spg_ctx* ctx, const char* name, double bytes, double ops) : c(ctx), idx(-1) {
+KScope::KScope(spg_ctx* ctx, const char* name, double bytes, double ops, double fqm) : c(ctx), idx(-1) {
   if (!c->prof_on) return;
   spg_ctx::ProfRec r;
   r.name = name;
   r.bytes = bytes;
   r.ops = ops;
+  r.fqm = fqm;
   r.a = pool_event(c);
   r.b = pool_event(c);
   hipEventRecord(r.a, c->stream);
@@ -472,10 +473,10 @@ extern "C" int spg_prof_enable(spg_ctx* c, int on) {
   return SPG_OK;
 }
 
-// Resolves pending kernel timings; writes up to `max` (name, launches, total_us, bytes, ops) records.
+// Resolves pending kernel timings; writes up to `max` (name, launches, total_us, bytes, ops, fq products) records.
 // names: max x 32 chars (NUL-terminated). Returns the number of records, or a negative error.
-extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, double* ops,
-                              int max, int reset) {
+extern "C" int spg_prof_read3(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, double* ops,
+                              double* fqm, int max, int reset) {
   if (!c) return SPG_E_ARG;
   hipStreamSynchronize(c->stream);
   hipStreamSynchronize(c->stream2);
@@ -521,6 +522,7 @@ extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* t
     acc.us += ms * 1000.0;
     acc.bytes += r.bytes;
     acc.ops += r.ops;
+    acc.fqm += r.fqm;
     c->ev_pool.push_back(r.a);
     c->ev_pool.push_back(r.b);
   }
@@ -536,10 +538,15 @@ extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* t
     if (total_us) total_us[k] = kv.second.us;
     if (bytes) bytes[k] = kv.second.bytes;
     if (ops) ops[k] = kv.second.ops;
+    if (fqm) fqm[k] = kv.second.fqm;
     k++;
   }
   if (reset) c->prof_acc.clear();
   return k;
+}
+extern "C" int spg_prof_read2(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, double* ops,
+                              int max, int reset) {
+  return spg_prof_read3(c, names, launches, total_us, bytes, ops, nullptr, max, reset);
 }
 extern "C" int spg_prof_read(spg_ctx* c, char* names, long* launches, double* total_us, double* bytes, int max,
                              int reset) {

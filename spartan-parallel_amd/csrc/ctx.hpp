@@ -81,10 +81,11 @@ struct spg_ctx {
     hipEvent_t a, b;
     double bytes;  // algorithmic HBM bytes of the launch (0 = not modelled)
     double ops;    // algorithmic VALU work of the launch in curve mixed additions (0 = not modelled)
+    double fqm;    // algorithmic VALU work of the launch in Fq (scalar-field) products (0 = not modelled)
   };
   struct ProfAcc {
     long launches = 0;
-    double us = 0.0, bytes = 0.0, ops = 0.0;
+    double us = 0.0, bytes = 0.0, ops = 0.0, fqm = 0.0;
   };
   std::vector<ProfRec> prof_pending;
   std::vector<hipEvent_t> ev_pool;
@@ -298,7 +299,7 @@ int comm_sum_fq(spg_ctx* c, const Shard& sh, int status, Fq* v, size_t n);
 struct KScope {
   spg_ctx* c;
   int idx;
-  KScope(spg_ctx* ctx, const char* name, double bytes = 0.0, double ops = 0.0);
+  KScope(spg_ctx* ctx, const char* name, double bytes = 0.0, double ops = 0.0, double fqm = 0.0);
   ~KScope();
 };
 

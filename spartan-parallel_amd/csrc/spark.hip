@@ -876,7 +876,9 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
           {
             // algorithmic bytes: per distinct vector and element, 4 corners from 4 2^nf entries, written back when folded
             const double per = 32.0 * (4.0 * (double)(1 << nf) + (nf ? 4.0 : 0.0));
-            KScope ks(ctx, "spark_layer_pair", per * (double)h * (double)(2 * nt + ngroups));
+            // Fq products per element: the corners folded (12 x 3 with two pending folds, 12 with one), 15 points x 3
+            KScope ks(ctx, "spark_layer_pair", per * (double)h * (double)(2 * nt + ngroups), 0.0,
+                      (double)nt * (double)h * (45.0 + (nf == 2 ? 36.0 : nf == 1 ? 12.0 : 0.0)));
             if (BSp == 64)
               hipLaunchKernelGGL(k_layer_pair<64>, dim3(Kp), dim3(64), 0, s, P);
             else
@@ -939,7 +941,11 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         const double layer_bytes = (pending ? 192.0 : 64.0) * (double)len * (double)(2 * tr.size() + ngroups);
         if (ngroups * len >= wide_min) {  // throughput form for rounds that fill the chip
           K = (unsigned)std::min<size_t>((ngroups * len + 255) / 256, 2048);
-          KScope ks(ctx, "spark_layer_round", layer_bytes);
+          // Fq products per index: per product circuit k A B at 3 points from the folded A, B (3 + 2 + 4 folds), the
+          // shared C folded once (2) and multiplied in (3); a dot-product circuit 14 (its own C folded too)
+          const double fqm_w = (double)len * ((pending ? 2.0 : 0.0) + 3.0 + (double)nc * (pending ? 9.0 : 5.0) +
+                                              (double)(tr.size() - nc) * (pending ? 14.0 : 8.0));
+          KScope ks(ctx, "spark_layer_round", layer_bytes, 0.0, fqm_w);
           hipLaunchKernelGGL(k_layer_round_wide<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, (int)nc, (int)tr.size(),
                              (int)log_len, pending ? 1 : 0, r_pend, cbuf[cur], cbuf[cur ^ 1], part, ctx->d_counter,
                              ctx->d_mbox, ++ctx->mbox_seq);
@@ -955,7 +961,8 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
         const bool ends = close_after && log_len == 0 && quad && K == 1 && 3 + 6 * tr.size() <= kMboxScalars &&
                           ngroups * len < wide_min && ends_on;
         if (ngroups * len < wide_min) {
-          KScope ks(ctx, "spark_layer_round", layer_bytes);
+          // Fq products per element: lanes 0..2 fold their vector's two entries (6) and form k A B C at their point (9)
+          KScope ks(ctx, "spark_layer_round", layer_bytes, 0.0, (double)tr.size() * (double)len * (pending ? 15.0 : 9.0));
           const int nt = (int)tr.size(), lg = (int)log_len, df = pending ? 1 : 0;
           const uint32_t seq = ++ctx->mbox_seq;
           if (quad && BS == 64)

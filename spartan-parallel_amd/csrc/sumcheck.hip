@@ -859,13 +859,17 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
   const int nb = quad ? grid_for((uint32_t)(4 * dom)) : grid_for((uint32_t)dom);
   if (!fold) {
     // B, C, D lo+hi per domain point, plus the three eq factor tables once
-    KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len));
+    // Fq products per point: the eq factor at lo and hi (x rounds share Ap Aq: 3; else 4), then A (B C - D) at 3 points
+    KScope ks(ctx, "sc_phase1_eval", 192.0 * dom + 64.0 * (instance_len + proof_len + cons_len), 0.0,
+              (double)dom * ((mode == MODE_X ? 3 : 4) + 6));
     hipLaunchKernelGGL(quad ? k_phase1_eval_q<false> : k_phase1_eval<false>, dim3(nb), dim3(256), 0, ctx->stream, a,
                        mode, (uint32_t)dom, (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq,
                        Ax, B, C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, FoldArg{});
   } else {
     // per point: B, C, D lo + hi and their fold partners read, lo + hi written; the side table's half once
-    KScope ks(ctx, "sc_phase1_fold_eval", 576.0 * dom + 96.0 * fold->arg.side_half + 64.0 * (instance_len + proof_len));
+    // Fq products per point: as sc_phase1_eval, plus B, C, D folded at lo and hi (6) and the side table's entries (1)
+    KScope ks(ctx, "sc_phase1_fold_eval", 576.0 * dom + 96.0 * fold->arg.side_half + 64.0 * (instance_len + proof_len),
+              0.0, (double)dom * ((mode == MODE_X ? 3 : 4) + 6 + 7));
     hipLaunchKernelGGL(quad ? k_phase1_eval_q<true> : k_phase1_eval<true>, dim3(nb), dim3(256), 0, ctx->stream, a,
                        mode, (uint32_t)dom, (uint32_t)proof_len, (uint32_t)cons_len, (uint32_t)instance_len, Ap, Aq,
                        Ax, B, C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, fold->arg);
@@ -905,7 +909,9 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
   const Fold2Arg fa = fold ? fold->arg : Fold2Arg{};
   {
     // ABC and Z lo+hi per domain point; fused: their fold partners read and the folded entries written too
-    KScope ks(ctx, fold ? "sc_phase2_fold_eval" : "sc_phase2_eval", (fold ? 384.0 : 128.0) * dom);
+    // Fq products per point: eq ABC Z at 3 points (6), plus ABC and Z folded at lo and hi when fused (4)
+    KScope ks(ctx, fold ? "sc_phase2_fold_eval" : "sc_phase2_eval", (fold ? 384.0 : 128.0) * dom, 0.0,
+              (double)dom * (fold ? 10 : 6));
     if (quad)
       hipLaunchKernelGGL(fold ? k_phase2_eval_q<true> : k_phase2_eval_q<false>, dim3(nb), dim3(256), 0, ctx->stream,
                          ab, zz, mode, (uint32_t)dom, single, (uint32_t)instance_len, eq, AB.d, Z.d, partials,

@@ -131,23 +131,25 @@ class Context:
 
     def prof_read(self, reset=True, ops=False):
         """{kernel_name: (launches, total_us, algorithmic_bytes)} of the kernels timed since the last reset;
-        ops=True appends the modelled VALU work (curve mixed additions) of those launches to each tuple."""
+        ops=True appends the modelled VALU work of those launches to each tuple: curve mixed additions, then Fq
+        products."""
         mx = 128
         names = ctypes.create_string_buffer(32 * mx)
         launches = np.zeros(mx, dtype=np.int64)
         tot = np.zeros(mx, dtype=np.float64)
         nbytes = np.zeros(mx, dtype=np.float64)
         nops = np.zeros(mx, dtype=np.float64)
-        k = lib().spg_prof_read2(self._h, names, _p(launches), _p(tot), _p(nbytes), _p(nops), ctypes.c_int(mx),
-                                 ctypes.c_int(1 if reset else 0))
+        nfqm = np.zeros(mx, dtype=np.float64)
+        k = lib().spg_prof_read3(self._h, names, _p(launches), _p(tot), _p(nbytes), _p(nops), _p(nfqm),
+                                 ctypes.c_int(mx), ctypes.c_int(1 if reset else 0))
         if k < 0:
-            self.check(k, "spg_prof_read2")
+            self.check(k, "spg_prof_read3")
         raw = names.raw
         out = {}
         for i in range(k):
             nm = raw[32 * i:32 * i + 32].split(b"\0", 1)[0].decode()
             rec = (int(launches[i]), float(tot[i]), float(nbytes[i]))
-            out[nm] = rec + (float(nops[i]),) if ops else rec
+            out[nm] = rec + (float(nops[i]), float(nfqm[i])) if ops else rec
         return out
 
     def close(self):
