@@ -16,6 +16,18 @@ def main(d, pats):
             for r in csv.DictReader(fh):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
+    # MARK=substring [SKIP=k]: keep the window from the (k+1)-th launch of the marker kernel (the first of each prove)
+    # to the end, and report per-prove figures (the warm-up prove and the setup before it left out)
+    mark = os.environ.get("MARK")
+    nprove = 1
+    if mark:
+        ix = [i for i, r in enumerate(rows) if mark in r[2]]
+        skip = int(os.environ.get("SKIP", "1"))
+        if len(ix) > skip:
+            rows = rows[ix[skip]:]
+            nprove = len(ix) - skip
+        print(f"window: {nprove} proves from launch {skip} of {mark!r}; wall {(rows[-1][1] - rows[0][0]) / 1e6 / nprove:.2f} "
+              f"ms per prove")
     acc = defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # launches, duration ns, gap ns, max gap
     prev_end = None
     for s, e, n in rows:
@@ -44,9 +56,10 @@ def main(d, pats):
         prev = key
         busy_end = max(busy_end or 0, e)
     tot = sum(v[1] for v in tr.values())
-    print(f"-- idle gaps by transition (total {tot / 1e6:.2f} ms):")
-    for (a, b), (n, g) in sorted(tr.items(), key=lambda kv: -kv[1][1])[:30]:
-        print(f"  {a:34s} -> {b:34s} n={n:6d} avg {g / n / 1e3:7.2f} us total {g / 1e6:7.2f} ms")
+    busy = sum(e - s for s, e, _ in rows)
+    print(f"-- idle gaps by transition, per prove (idle {tot / 1e6 / nprove:.2f} ms, kernel time {busy / 1e6 / nprove:.2f} ms):")
+    for (a, b), (n, g) in sorted(tr.items(), key=lambda kv: -kv[1][1])[:40]:
+        print(f"  {a:34s} -> {b:34s} n={n / nprove:7.1f} avg {g / n / 1e3:7.2f} us total {g / 1e6 / nprove:6.3f} ms")
 
 
 if __name__ == "__main__":

@@ -63,10 +63,11 @@ std::vector<Pt> commit_batch(ProverGens& g, const std::vector<CJob>& jobs) {
 }
 
 // src/nizk/mod.rs:27-53
-KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C) {
+KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C,
+                                const Pt* pre) {
   t.protocol("knowledge proof");
   Fq t1 = tape.scalar("t1"), t2 = tape.scalar("t2");
-  std::vector<Pt> c = commit_batch(g, {CJob(k, {x}, r), CJob(k, {t1}, t2)});
+  std::vector<Pt> c = pre ? std::vector<Pt>(pre, pre + 2) : commit_batch(g, {CJob(k, {x}, r), CJob(k, {t1}, t2)});
   *C = c[0];
   t.point("C", *C);
   KnowledgeProofP p;
@@ -80,10 +81,11 @@ KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& ta
 
 // src/nizk/mod.rs:87-115
 EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& v1, const Fq& s1,
-                              const Fq& v2, const Fq& s2) {
+                              const Fq& v2, const Fq& s2, const Pt* pre) {
   t.protocol("equality proof");
   Fq r = tape.scalar("r");
-  std::vector<Pt> c = commit_batch(g, {CJob(k, {v1}, s1), CJob(k, {v2}, s2), CJob(k.h, r)});
+  std::vector<Pt> c =
+      pre ? std::vector<Pt>(pre, pre + 3) : commit_batch(g, {CJob(k, {v1}, s1), CJob(k, {v2}, s2), CJob(k.h, r)});
   t.point("C1", c[0]);
   t.point("C2", c[1]);
   EqualityProofP p;
@@ -96,12 +98,13 @@ EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape
 
 // src/nizk/mod.rs:159-226
 ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& rX, const Fq& y,
-                            const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z) {
+                            const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z, const Pt* pre) {
   t.protocol("product proof");
   Fq b1 = tape.scalar("b1"), b2 = tape.scalar("b2"), b3 = tape.scalar("b3"), b4 = tape.scalar("b4"),
      b5 = tape.scalar("b5");
-  std::vector<Pt> c = commit_batch(
-      g, {CJob(k, {x}, rX), CJob(k, {y}, rY), CJob(k, {z}, rZ), CJob(k, {b1}, b2), CJob(k, {b3}, b4)});
+  std::vector<Pt> c =
+      pre ? std::vector<Pt>(pre, pre + 5)
+          : commit_batch(g, {CJob(k, {x}, rX), CJob(k, {y}, rY), CJob(k, {z}, rZ), CJob(k, {b1}, b2), CJob(k, {b3}, b4)});
   *X = c[0];
   *Y = c[1];
   *Z = c[2];
@@ -113,11 +116,15 @@ ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, 
   t.point("alpha", p.alpha);
   p.beta = c[4];
   t.point("beta", p.beta);
-  // gens_X = {G: [X.decompress()], h}: X is used through its encoding, as the reference does
-  h::HExt Xd;
-  h::hext_decompress(X->b, Xd);
-  h::HExt dl = h::hext_add(var_mul(Xd, b3), g.host.msm({k.h}, {b5}));
-  p.delta = compress(dl);
+  if (pre) {
+    p.delta = pre[5];  // (b3 x) G + (b3 rX + b5) h = b3 X + b5 h (sigma1_points)
+  } else {
+    // gens_X = {G: [X.decompress()], h}: X is used through its encoding, as the reference does
+    h::HExt Xd;
+    h::hext_decompress(X->b, Xd);
+    h::HExt dl = h::hext_add(var_mul(Xd, b3), g.host.msm({k.h}, {b5}));
+    p.delta = compress(dl);
+  }
   t.point("delta", p.delta);
   Fq ch = t.challenge("c");
   p.z[0] = fq_add(b1, fq_mul(ch, x));
@@ -126,6 +133,23 @@ ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, 
   p.z[3] = fq_add(b4, fq_mul(ch, rY));
   p.z[4] = fq_add(b5, fq_mul(ch, fq_sub(rZ, fq_mul(rX, y))));
   return p;
+}
+
+void sigma1_points(ProverGens& g, const KeyView& k, const Tape& tape, const Fq& cz, const Fq& cz_blind, const Fq& az,
+                   const Fq& az_blind, const Fq& bz, const Fq& bz_blind, const Fq& prod, const Fq& prod_blind,
+                   const Fq& v1, const Fq& s1, const Fq& v2, const Fq& s2, Sigma1Pre* out) {
+  Tape tp = tape;  // the draws knowledge_prove, product_prove and equality_prove make next, in their order
+  const Fq t1 = tp.scalar("t1"), t2 = tp.scalar("t2");
+  const Fq b1 = tp.scalar("b1"), b2 = tp.scalar("b2"), b3 = tp.scalar("b3"), b4 = tp.scalar("b4"), b5 = tp.scalar("b5");
+  const Fq r = tp.scalar("r");
+  std::vector<Pt> c = commit_batch(
+      g, {CJob(k, {cz}, cz_blind), CJob(k, {t1}, t2), CJob(k, {az}, az_blind), CJob(k, {bz}, bz_blind),
+          CJob(k, {prod}, prod_blind), CJob(k, {b1}, b2), CJob(k, {b3}, b4),
+          CJob(k, {fq_mul(b3, az)}, fq_add(fq_mul(b3, az_blind), b5)), CJob(k, {v1}, s1), CJob(k, {v2}, s2),
+          CJob(k.h, r)});
+  for (int i = 0; i < 2; i++) out->k[i] = c[i];
+  for (int i = 0; i < 6; i++) out->p[i] = c[2 + i];
+  for (int i = 0; i < 3; i++) out->e[i] = c[8 + i];
 }
 
 // src/nizk/mod.rs:306-370 (n = 4 in every sumcheck round). Cx_known: the caller already holds

@@ -117,11 +117,27 @@ struct CommitStats {
 };
 extern CommitStats g_commit_stats;  // SPG_TRACE >= 2
 std::vector<Pt> commit_batch(ProverGens& g, const std::vector<CJob>& jobs);
-KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C);
+// pre (optional): the protocol's points computed ahead (sigma1_points), in the order the protocol appends them; the
+// protocol still draws its tape scalars itself (the same values), so the tape advances exactly as without them
+KnowledgeProofP knowledge_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& r, Pt* C,
+                                const Pt* pre = nullptr);
 EqualityProofP equality_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& v1, const Fq& s1,
-                              const Fq& v2, const Fq& s2);
+                              const Fq& v2, const Fq& s2, const Pt* pre = nullptr);
 ProductProofP product_prove(ProverGens& g, const KeyView& k, Tr& t, Tape& tape, const Fq& x, const Fq& rX, const Fq& y,
-                            const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z);
+                            const Fq& rY, const Fq& z, const Fq& rZ, Pt* X, Pt* Y, Pt* Z, const Pt* pre = nullptr);
+// The eleven points of R1CSProof::prove's sigma protocols after phase 1 (src/r1csproof.rs:403-456: the knowledge proof
+// of Cz, the product proof Az Bz = prod, the equality proof of the two post-phase-1 claims) depend on claims, blinds
+// and RandomTape draws alone, never on the transcript: one pool burst computes them all (encodings side by side) from
+// a fork of the tape, before the transcript sequence runs. The product proof's delta = b3 X + b5 h is the fixed-base
+// commitment (b3 x) G + (b3 rX + b5) h of the same group element (X = x G + rX h), so no variable-base multiple.
+struct Sigma1Pre {
+  Pt k[2];  // knowledge: C, alpha
+  Pt p[6];  // product: X, Y, Z, alpha, beta, delta
+  Pt e[3];  // equality: C1, C2, alpha
+};
+void sigma1_points(ProverGens& g, const KeyView& k, const Tape& tape, const Fq& cz, const Fq& cz_blind, const Fq& az,
+                   const Fq& az_blind, const Fq& bz, const Fq& bz_blind, const Fq& prod, const Fq& prod_blind,
+                   const Fq& v1, const Fq& s1, const Fq& v2, const Fq& s2, Sigma1Pre* out);
 // the prover randomness of one DotProductProof drawn ahead of time (d_vec, r_delta, r_beta from a fork of the
 // RandomTape at the same position) with its randomness-only points: delta = d.commit(r_delta, gens_n) and
 // r_beta * h of gens_1

@@ -908,34 +908,42 @@ int Prover::run_inner(Laps& lp) {
     pf.sc1 = std::move(zk.out);
   }
   lp.lap("p1_claims");
+  FqV rx_rev(rx_all.begin(), rx_all.begin() + nx), rq_rev(rx_all.begin() + nx, rx_all.begin() + nx + nq),
+      rp(rx_all.begin() + nx + nq, rx_all.end());
+  FqV rx(rx_rev.rbegin(), rx_rev.rend()), rq(rq_rev.rbegin(), rq_rev.rend());
+  // eq(rx) of phase 2 depends on phase 1's challenges alone: on the device while the host runs the sigma protocols
+  Fq* eq_rx = (Fq*)ws_get(ctx, WS_EQRX, (sizeof(Fq) << nx) + 64);
+  if (!eq_rx) return set_err(ctx, SPG_E_NOMEM, "eq(rx)");
+  rc = eq_table(ctx, rx, eq_rx);
+  if (rc) return rc;
   Fq tau_claim = claims1[0], Az_claim = claims1[1], Bz_claim = claims1[2], Cz_claim = claims1[3];
   Fq Az_blind = tape.scalar("Az_blind"), Bz_blind = tape.scalar("Bz_blind"), Cz_blind = tape.scalar("Cz_blind"),
      prod_blind = tape.scalar("prod_Az_Bz_blind");
   Pt comm_Cz, comm_Az, comm_Bz, comm_prod;
-  pf.pok = knowledge_prove(g, g.gens_1, t, tape, Cz_claim, Cz_blind, &comm_Cz);
   Fq prod = fq_mul(Az_claim, Bz_claim);
+  Fq blind_expected1 = fq_mul(tau_claim, fq_sub(prod_blind, Cz_blind));
+  Fq claim_post1 = fq_mul(fq_sub(prod, Cz_claim), tau_claim);
+  // every point of the three sigma protocols in one host burst ahead of the transcript sequence (SPG_SIGMA_AHEAD=0:
+  // each protocol commits on its own)
+  static const bool sigma_ahead = !getenv("SPG_SIGMA_AHEAD") || atoi(getenv("SPG_SIGMA_AHEAD")) != 0;
+  Sigma1Pre sp;
+  if (sigma_ahead)
+    sigma1_points(g, g.gens_1, tape, Cz_claim, Cz_blind, Az_claim, Az_blind, Bz_claim, Bz_blind, prod, prod_blind,
+                  claim_post1, blind_expected1, claim_post1, blind_post1, &sp);
+  pf.pok = knowledge_prove(g, g.gens_1, t, tape, Cz_claim, Cz_blind, &comm_Cz, sigma_ahead ? sp.k : nullptr);
   pf.prod = product_prove(g, g.gens_1, t, tape, Az_claim, Az_blind, Bz_claim, Bz_blind, prod, prod_blind, &comm_Az,
-                          &comm_Bz, &comm_prod);
+                          &comm_Bz, &comm_prod, sigma_ahead ? sp.p : nullptr);
   t.point("comm_Az_claim", comm_Az);
   t.point("comm_Bz_claim", comm_Bz);
   t.point("comm_Cz_claim", comm_Cz);
   t.point("comm_prod_Az_Bz_claims", comm_prod);
-  Fq blind_expected1 = fq_mul(tau_claim, fq_sub(prod_blind, Cz_blind));
-  Fq claim_post1 = fq_mul(fq_sub(prod, Cz_claim), tau_claim);
-  pf.eq1 = equality_prove(g, g.gens_1, t, tape, claim_post1, blind_expected1, claim_post1, blind_post1);
-  FqV rx_rev(rx_all.begin(), rx_all.begin() + nx), rq_rev(rx_all.begin() + nx, rx_all.begin() + nx + nq),
-      rp(rx_all.begin() + nx + nq, rx_all.end());
-  FqV rx(rx_rev.rbegin(), rx_rev.rend()), rq(rq_rev.rbegin(), rq_rev.rend());
-
+  pf.eq1 = equality_prove(g, g.gens_1, t, tape, claim_post1, blind_expected1, claim_post1, blind_post1,
+                          sigma_ahead ? sp.e : nullptr);
   lp.lap("sigma1");
   // ---- phase 2 inputs
   Fq r_A = t.challenge("challenge_Az"), r_B = t.challenge("challenge_Bz"), r_C = t.challenge("challenge_Cz");
   Fq claim2 = fq_add(fq_add(fq_mul(r_A, Az_claim), fq_mul(r_B, Bz_claim)), fq_mul(r_C, Cz_claim));
   Fq blind2 = fq_add(fq_add(fq_mul(r_A, Az_blind), fq_mul(r_B, Bz_blind)), fq_mul(r_C, Cz_blind));
-  Fq* eq_rx = (Fq*)ws_get(ctx, WS_EQRX, (sizeof(Fq) << nx) + 64);
-  if (!eq_rx) return set_err(ctx, SPG_E_NOMEM, "eq(rx)");
-  rc = eq_table(ctx, rx, eq_rx);
-  if (rc) return rc;
   const bool single = inst.num_instances == 1;
   // ABC: the shared matrix once (every rank), or this rank's instances
   const size_t Ab0 = single ? 0 : p0, Abn = single ? 1 : PLn;
