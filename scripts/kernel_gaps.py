@@ -62,5 +62,56 @@ def main(d, pats):
         print(f"  {a:34s} -> {b:34s} n={n / nprove:7.1f} avg {g / n / 1e3:7.2f} us total {g / 1e6 / nprove:6.3f} ms")
 
 
+def events_in_gaps(d, evfile, top=40):
+    """the largest idle gaps of the device in the MARK window, each with the host laps (SPG_TRACE_EVENTS lines of
+    evfile: [spgev] <ns> <title>:<lap> <us>) that ended inside it: which host phase held the device up"""
+    fs = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for f in fs:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][-40:]))
+    rows.sort()
+    ev = []
+    for line in open(evfile):
+        if line.startswith("[spgev]"):
+            _, ns, nm, us = line.split()
+            ev.append((int(ns), nm, float(us)))
+    ev.sort()
+    mark = os.environ.get("MARK")
+    if mark:
+        ix = [i for i, r in enumerate(rows) if mark in r[2]]
+        skip = int(os.environ.get("SKIP", "1"))
+        rows = rows[ix[skip]:]
+    gaps = []
+    end = rows[0][1]
+    for i in range(1, len(rows)):
+        s, e, n = rows[i]
+        if s > end:
+            gaps.append((s - end, end, s, rows[i - 1][2], n))
+        end = max(end, e)
+    import bisect
+    keys = [x[0] for x in ev]
+    by_lap = defaultdict(float)
+    maxlap = max((x[2] for x in ev), default=0) * 1e3
+    for g, a, b, pn, nn in gaps:
+        # every lap whose interval [end - us, end] overlaps the gap, by the overlap (nested Laps objects overlap each
+        # other: read the innermost names)
+        lo, hi = bisect.bisect_left(keys, a), bisect.bisect_right(keys, b + maxlap)
+        for j in range(lo, hi):
+            e1 = ev[j][0]
+            e0 = e1 - ev[j][2] * 1e3
+            ov = min(e1, b) - max(e0, a)
+            if ov > 0:
+                by_lap[ev[j][1]] += ov
+    tot = sum(g[0] for g in gaps)
+    print(f"-- idle {tot / 1e6:.2f} ms in {len(gaps)} gaps; host laps ending inside them (lap time, capped at the gap):")
+    for k, v in sorted(by_lap.items(), key=lambda kv: -kv[1])[:top]:
+        print(f"  {k:60s} {v / 1e6:8.3f} ms")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2:])
+    if os.environ.get("EVENTS"):
+        events_in_gaps(sys.argv[1], os.environ["EVENTS"])
+    else:
+        main(sys.argv[1], sys.argv[2:])

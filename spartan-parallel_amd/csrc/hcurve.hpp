@@ -49,6 +49,19 @@ inline Fe fe_sub(const Fe& a, const Fe& b) {
   return fe_carry(r);
 }
 inline Fe fe_neg(const Fe& a) { return fe_sub(fe_zero(), a); }
+// without the carry (the point additions' sums and differences feed a multiply directly, which takes limbs < 2^54:
+// 5 products of < 2^54 x 19 * 2^54 stay below 2^128). Inputs: limbs < 2^52 (a multiply's or a carry's output).
+inline Fe fe_add_nc(const Fe& a, const Fe& b) {
+  Fe r;
+  for (int i = 0; i < 5; i++) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+inline Fe fe_sub_nc(const Fe& a, const Fe& b) {
+  Fe r;
+  r.v[0] = a.v[0] + 0x1fffffffffffb4ULL - b.v[0];
+  for (int i = 1; i < 5; i++) r.v[i] = a.v[i] + 0x1ffffffffffffcULL - b.v[i];
+  return r;
+}
 
 inline Fe fe_mul(const Fe& a, const Fe& b) {
   const uint64_t b1 = b.v[1] * 19, b2 = b.v[2] * 19, b3 = b.v[3] * 19, b4 = b.v[4] * 19;
@@ -225,20 +238,22 @@ inline HExt hext_from_dev(const Ext& p) {
   return HExt{fe_from_fp(p.X), fe_from_fp(p.Y), fe_from_fp(p.Z), fe_from_fp(p.T)};
 }
 // add-2008-hwcd-3
+// (the coordinates of a point here are multiply or carry outputs, limbs < 2^52, so the sums and differences that feed
+// the next multiplies skip their carries)
 inline HExt hext_add(const HExt& p, const HExt& q) {
-  Fe A = fe_mul(fe_sub(p.Y, p.X), fe_sub(q.Y, q.X));
-  Fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));
+  Fe A = fe_mul(fe_sub_nc(p.Y, p.X), fe_sub_nc(q.Y, q.X));
+  Fe B = fe_mul(fe_add_nc(p.Y, p.X), fe_add_nc(q.Y, q.X));
   Fe C = fe_mul(fe_mul(p.T, K().d2), q.T);
-  Fe D = fe_mul(fe_add(p.Z, p.Z), q.Z);
-  Fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  Fe D = fe_mul(fe_add_nc(p.Z, p.Z), q.Z);
+  Fe E = fe_sub_nc(B, A), F = fe_sub_nc(D, C), G = fe_add_nc(D, C), H = fe_add_nc(B, A);
   return HExt{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 inline HExt hext_madd(const HExt& p, const HNiels& q) {
-  Fe A = fe_mul(fe_sub(p.Y, p.X), q.ymx);
-  Fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);
+  Fe A = fe_mul(fe_sub_nc(p.Y, p.X), q.ymx);
+  Fe B = fe_mul(fe_add_nc(p.Y, p.X), q.ypx);
   Fe C = fe_mul(p.T, q.t2d);
-  Fe D = fe_add(p.Z, p.Z);
-  Fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  Fe D = fe_add_nc(p.Z, p.Z);
+  Fe E = fe_sub_nc(B, A), F = fe_sub_nc(D, C), G = fe_add_nc(D, C), H = fe_add_nc(B, A);
   return HExt{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 inline HExt hext_dbl(const HExt& p) {

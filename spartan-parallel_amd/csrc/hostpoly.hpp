@@ -58,6 +58,13 @@ struct Laps {  // SPG_TRACE=1: wall-time breakdown of a host orchestration
     auto now = std::chrono::steady_clock::now();
     double us = std::chrono::duration<double, std::micro>(now - t).count();
     t = now;
+    // SPG_TRACE_EVENTS=1: every lap's end on stderr with its CLOCK_MONOTONIC time (the clock of rocprofv3's kernel
+    // trace), so scripts/kernel_gaps.py can name the host phase behind each idle gap of the device
+    static const bool ev = getenv("SPG_TRACE_EVENTS") != nullptr;
+    if (ev)
+      fprintf(stderr, "[spgev] %lld %s:%s %.1f\n",
+              (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(now.time_since_epoch()).count(), title,
+              name, us);
     for (auto& a : acc)
       if (a.first == name) {
         a.second += us;

@@ -210,8 +210,10 @@ __device__ __forceinline__ Fq layer_round_elems(const Triple* __restrict__ tr, c
     const Triple x = tr[c];
     const Fq* Cp = x.C ? x.C : cin;
     const Fq* src = pt == 0 ? x.A : (pt == 1 ? x.B : Cp);
-    Fq lo, hi;
-    if (do_fold) {
+    Fq lo = fq_zero(), hi = fq_zero();
+    if (q == 3) {
+      // lane 3 holds no vector: nothing is broadcast from it, so it loads nothing (its lanes' product below is unused)
+    } else if (do_fold) {
       const int fl = 2 * len;
       lo = fold_at(src, i, fl, r);
       hi = fold_at(src, i + len, fl, r);
@@ -232,7 +234,8 @@ __device__ __forceinline__ Fq layer_round_elems(const Triple* __restrict__ tr, c
     const Fq al = fq_qbcast<0>(lo), ah = fq_qbcast<0>(hi), bl = fq_qbcast<1>(lo), bh = fq_qbcast<1>(hi);
     const Fq cl = fq_qbcast<2>(lo), ch = fq_qbcast<2>(hi);
     const Fq k = coeff[c];
-    e = fq_add(e, fq_mul(fq_mul(fq_mul(line_at(al, ah, pt), line_at(bl, bh, pt)), line_at(cl, ch, pt)), k));
+    // (A B) (C k): two independent products, then one -- a dependent chain of two products instead of three
+    e = fq_add(e, fq_mul(fq_mul(line_at(al, ah, pt), line_at(bl, bh, pt)), fq_mul(line_at(cl, ch, pt), k)));
   }
   return e;
 }
