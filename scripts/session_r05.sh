@@ -2,6 +2,7 @@
 # round-5 GPU session pieces (each step under its own time limit, chained by the caller with &&):
 #   tests K            pytest -m gpu -k K
 #   ab VAR "v1 v2" n   traced A/B of one switch (scripts/ab_trace.sh)
+#   bench TAG ENV...   one bench line (default workload, or BENCH_ARGS) under the given env assignments
 #   gaps TAG           kernel trace + host lap events of 6 proves -> per-prove idle gaps by transition and by host lap
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -13,6 +14,11 @@ case "$1" in
     rc=$?; tail -3 gpurun_out/${TAG:-}gpu_tests.log; exit $rc ;;
   ab)
     timeout -k 10 ${T:-700} bash scripts/ab_trace.sh "$2" "$3" "$4" ;;
+  bench)
+    tag=$2; shift 2
+    env "$@" timeout -k 10 ${T:-600} python3 bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > gpurun_out/bench_$tag.json \
+      2> gpurun_out/bench_$tag.err || { tail -5 gpurun_out/bench_$tag.err; exit 1; }
+    tail -c 600 gpurun_out/bench_$tag.json ;;
   gaps)
     export TMPDIR=/tmp
     (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 TRACE_REPS=6 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \

@@ -145,9 +145,10 @@ __global__ void __launch_bounds__(BS) k_bullet_round_q(BulletArgs a) {
 
 // ---- one Bullet round from the comb table (the default device form) -------------------------------------
 // The same round as k_bullet_round_q, without buckets. The L and R MSMs are over the ORIGINAL generators G_0..G_{n-1}
-// of the proof, whose generator set keeps the comb table of comb.hip: comb[w][s][m - 1] = m 2^(12 w) G_s. A 12-bit
-// signed digit d of scalar p in window w is then one entry +-comb[w][gidx_p][|d| - 1], and an MSM is a plain sum of
-// its 22 P entries -- no bucket weights, so the host finishes with a plain sum of partial points instead of the
+// of the proof, whose generator set keeps the comb table of comb.hip: comb[w][s][m - 1] = m 2^(C w) G_s (C = 12, or
+// 13 for the 2^14-generator tables). A C-bit signed digit d of scalar p in window w is then one entry
+// +-comb[w][gidx_p][|d| - 1] (packed as a 31-bit entry index: < 2^31 for every table comb.hip builds at C >= 12), and
+// an MSM is a plain sum of its W P entries (W = 22, or 20 at C = 13) -- no bucket weights, so the host finishes with a plain sum of partial points instead of the
 // buckets' running sums, and no workgroup needs more than its own scalars:
 //   quad (p, j) of MSM b (G quads per scalar) adds the entries of windows j*WG .. j*WG + WG - 1 of scalar p
 //   (WG = ceil(22 / G) dependent quad mixed additions), its Niels coordinates all loaded up front;
@@ -165,7 +166,7 @@ struct BulletCombArgs {
   Fq u, uinv;
   int k, n, nk;
   const Niels* comb;
-  int NS;        // comb slots + 1 (the h slot): the stride between windows is NS * 2048 entries
+  int NS;        // comb slots + 1 (the h slot): the stride between windows is NS * 2^(C-1) entries
   int R;         // points each workgroup leaves (a power of two <= BS / 4)
   Ext* parts;    // [2][gridDim.x][R] (mapped host memory)
   unsigned* counter;
@@ -184,9 +185,9 @@ __device__ __forceinline__ Fq fq_qbcast_lane(const Fq& a, int lane) {
   return o;
 }
 
-template <int G, int BS>
+template <int C, int G, int BS>
 __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
-  constexpr int C = 12, W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
+  constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
   constexpr uint32_t MASK = (1u << C) - 1u;
   __shared__ uint32_t pts[soa_words<Ext, S>()];
   __shared__ bool last;
@@ -218,7 +219,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
     }
     const Fq k = fq_mul(av, cv);  // canonical scalar (cw is a plain integer)
     const int s = (int)a.gidx[j];
-    // signed 12-bit digits; the entries of windows w0 .. w0 + WG - 1 shift into ent[] in window order (static
+    // signed C-bit digits; the entries of windows w0 .. w0 + WG - 1 shift into ent[] in window order (static
     // register indices; a short last group leaves its leading slots empty)
     uint32_t ent[WG];
 #pragma unroll
@@ -276,11 +277,11 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
 // B plain MSMs from the comb table, sum_i s_{b,i} G_{idx_{b,i}} (Montgomery scalars), left as partial points: the Cx
 // commitment of a device DotProductProofLog (its blind term is added on the host). The same quads, window groups and
 // workgroup trees as k_bullet_comb; parts[b][wg][0..R).
-template <int G, int BS>
+template <int C, int G, int BS>
 __global__ void __launch_bounds__(BS) k_comb_msm_parts(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
                                                        int n, const Niels* __restrict__ comb, int NS, int R,
                                                        Ext* __restrict__ parts) {
-  constexpr int C = 12, W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
+  constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
   constexpr uint32_t MASK = (1u << C) - 1u;
   __shared__ uint32_t pts[soa_words<Ext, S>()];
   const int b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;

@@ -31,19 +31,25 @@
 namespace spg {
 
 // window width: 12 (22 windows, 2048 multiples: 4.4 GB at 1024 generators); SPG_COMB_C = 10 / 11 trade more windows
-// for a smaller table
+// for a smaller table, 13 forces the big tables' width (for tests at small sizes)
 static int comb_c() {
-  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(12, atoi(getenv("SPG_COMB_C")))) : 12;
+  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(13, atoi(getenv("SPG_COMB_C")))) : 12;
   return c;
 }
 static constexpr int kCombRun = 64;                 // multiples per build lane
 static constexpr size_t kCombMaxR = 65536;          // most generators a table covers
 static constexpr size_t kCombWide = 16384;          // tables past this many generators take the narrow window
+static constexpr size_t kCombBig = 16384;           // tables of this many generators take the big window when it fits
 // wider tables take c = 9 (SPG_COMB_C_WIDE: 9 or 10): 2^16 generators are 29 x 65537 x 256 x 96 B = 47 GB, where
-// c = 12 would need 283 GB
+// c = 12 would need 283 GB. Tables of exactly kCombBig generators (the SPARK derefs rows of 2^14 at 2^24 nonzeros)
+// take c = 13 (SPG_COMB_C_BIG: 12 or 13): 20 windows instead of 22, so 9 % fewer mixed additions per scalar, for a
+// 129 GB table instead of 70 GB; where that does not fit (cap, free HBM) the table falls back to c = 12
 static int comb_c_for(size_t slots) {
   static const int cw = getenv("SPG_COMB_C_WIDE") ? std::max(9, std::min(10, atoi(getenv("SPG_COMB_C_WIDE")))) : 9;
-  return slots > kCombWide ? cw : comb_c();
+  static const int cb = getenv("SPG_COMB_C_BIG") ? std::max(12, std::min(13, atoi(getenv("SPG_COMB_C_BIG")))) : 13;
+  if (slots > kCombWide) return cw;
+  if (slots == kCombBig && !getenv("SPG_COMB_C")) return cb;
+  return comb_c();
 }
 
 // lane L = ((w * NS + s) * runs + k): multiples k * Run + 1 .. (k + 1) * Run of 2^(c w) G_gen, gen = s (s < NS - 1)
@@ -221,23 +227,31 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   while (cn < need) cn *= 2;
   cn = std::min(cn, g->n);
   if (cn < need || hgen < 0 || (size_t)hgen > g->n) return 1;
-  const int NS = (int)cn + 1, C = comb_c_for(cn);
-  const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
-  // the cap is per process (SPG_COMB_GB, default 96 GiB); without an explicit setting a table is also built only when
+  const int NS = (int)cn + 1;
+  // the cap is per process (SPG_COMB_GB, default 144 GiB); without an explicit setting a table is also built only when
   // the device keeps kCombHeadroom free beside it, so co-located provers (several processes on one GPU) cannot starve
-  // each other's workspaces into SPG_E_NOMEM: a table that does not fit leaves the rows on the buckets
+  // each other's workspaces into SPG_E_NOMEM: a table that does not fit at the preferred width tries 12,
+  // and one that does not fit at all leaves the rows on the buckets
   static const bool cap_set = getenv("SPG_COMB_GB") != nullptr;
-  static const size_t cap = (size_t)(cap_set ? atof(getenv("SPG_COMB_GB")) : 96.0) * (1ull << 30);
-  if (g_comb_bytes.load() + bytes > cap) return 1;
-  if (!cap_set) {
+  static const size_t cap = (size_t)(cap_set ? atof(getenv("SPG_COMB_GB")) : 144.0) * (1ull << 30);
+  auto table_bytes = [&](int c) { return (size_t)(253 / c + 1) * NS * ((size_t)1 << (c - 1)) * sizeof(Niels); };
+  auto fits = [&](size_t bytes) {
+    if (g_comb_bytes.load() + bytes > cap) return false;
+    if (cap_set) return true;
     static const size_t kCombHeadroom = (size_t)24 << 30;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
       (void)hipGetLastError();
-      return 1;
+      return false;
     }
-    if (bytes + kCombHeadroom > free_b) return 1;
+    return bytes + kCombHeadroom <= free_b;
+  };
+  int C = comb_c_for(cn);
+  if (!fits(table_bytes(C))) {
+    if (C <= 12 || !fits(table_bytes(12))) return 1;
+    C = 12;
   }
+  const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
   Niels* comb = nullptr;
   Fp* zs = nullptr;
   const size_t lanes = entries / kCombRun;
@@ -260,6 +274,8 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
       hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
     else if (C == 11)
       hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+    else if (C == 13)
+      hipLaunchKernelGGL(k_comb_build<13>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
     else
       hipLaunchKernelGGL(k_comb_build<12>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
   }
@@ -326,6 +342,9 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
       case 11 * 8 + 4: SPG_COMB_LAUNCH(11, 4); break;
       case 12 * 8 + 1: SPG_COMB_LAUNCH(12, 1); break;
       case 12 * 8 + 2: SPG_COMB_LAUNCH(12, 2); break;
+      case 13 * 8 + 1: SPG_COMB_LAUNCH(13, 1); break;
+      case 13 * 8 + 2: SPG_COMB_LAUNCH(13, 2); break;
+      case 13 * 8 + 4: SPG_COMB_LAUNCH(13, 4); break;
       default: SPG_COMB_LAUNCH(12, 4); break;
     }
 #undef SPG_COMB_LAUNCH
@@ -373,6 +392,9 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
       case 11 * 8 + 4: SPG_CS(11, 4); break;
       case 12 * 8 + 1: SPG_CS(12, 1); break;
       case 12 * 8 + 2: SPG_CS(12, 2); break;
+      case 13 * 8 + 1: SPG_CS(13, 1); break;
+      case 13 * 8 + 2: SPG_CS(13, 2); break;
+      case 13 * 8 + 4: SPG_CS(13, 4); break;
       default: SPG_CS(12, 4); break;
     }
 #undef SPG_CS

@@ -652,31 +652,35 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   spg_gens::Comb cb;
   const int rc = comb_get(ctx, g, gmax, &cb);
   if (rc) return rc == 1 ? 1 : rc;
-  if (cb.c != 12) return 1;  // the kernels take 12-bit windows
+  if (cb.c != 12 && cb.c != 13) return 1;  // the kernels take 12- or 13-bit windows
   int G, BS, R;
   bullet_comb_shape(n / 2, &G, &BS, &R);
+  if (cb.c == 13 && G != 4) G = 10;  // 20 windows: groups of 2 (11 would leave one empty)
   const int S = BS / 4, quads = (n / 2) * G, wgs = (quads + S - 1) / S;
   if (wgs * R > kBulletPartsMax) return 1;
   BulletCombArgs a{aa_in, cw_in, aa_out, cw_out, gidx, u, uinv, k, n, nk, cb.p, (int)cb.slots + 1, R, d_parts,
                    ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq};
   *seq_out = a.seq;
   *per_msm = wgs * R;
-  const int W = 22, WG = (W + G - 1) / G;
-  (void)WG;
-  // VALU model: one mixed addition per nonzero signed 12-bit digit of the n/2 scalars of each of the two MSMs
+  // VALU model: one mixed addition per nonzero signed C-bit digit of the n/2 scalars of each of the two MSMs
   // algorithmic bytes: every nonzero digit's 96-byte comb entry, the fold's reads and writes (aa: 2 nk in, nk out;
   // cw: n in, n out; gidx: n)
-  const double entries = (double)n * 22.0 * (1.0 - 1.0 / 4096.0);
+  const double W = 253 / cb.c + 1, entries = (double)n * W * (1.0 - 1.0 / (double)(1 << cb.c));
   KScope ks(ctx, "msm_bullet_round", 96.0 * entries + 96.0 * nk + 68.0 * n, entries);
   const dim3 grid((unsigned)wgs, 2);
-#define SPG_BCOMB(GG, BB) hipLaunchKernelGGL((k_bullet_comb<GG, BB>), grid, dim3(BB), 0, ctx->stream, a)
-  if (G == 4) {
-    if (BS == 64) SPG_BCOMB(4, 64); else if (BS == 128) SPG_BCOMB(4, 128); else SPG_BCOMB(4, 256);
+#define SPG_BCOMB(CC, GG, BB) hipLaunchKernelGGL((k_bullet_comb<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, a)
+#define SPG_BCOMB_BS(CC, GG) \
+  do { if (BS == 64) SPG_BCOMB(CC, GG, 64); else if (BS == 128) SPG_BCOMB(CC, GG, 128); else SPG_BCOMB(CC, GG, 256); } while (0)
+  if (cb.c == 13) {
+    if (G == 4) SPG_BCOMB_BS(13, 4); else SPG_BCOMB_BS(13, 10);
+  } else if (G == 4) {
+    SPG_BCOMB_BS(12, 4);
   } else if (G == 8) {
-    if (BS == 64) SPG_BCOMB(8, 64); else if (BS == 128) SPG_BCOMB(8, 128); else SPG_BCOMB(8, 256);
+    SPG_BCOMB_BS(12, 8);
   } else {
-    if (BS == 64) SPG_BCOMB(11, 64); else if (BS == 128) SPG_BCOMB(11, 128); else SPG_BCOMB(11, 256);
+    SPG_BCOMB_BS(12, 11);
   }
+#undef SPG_BCOMB_BS
 #undef SPG_BCOMB
   SPG_HIP(ctx, hipGetLastError());
   return 0;
@@ -689,24 +693,30 @@ int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const u
   spg_gens::Comb cb;
   const int rc = comb_get(ctx, g, gmax, &cb);
   if (rc) return rc == 1 ? 1 : rc;
-  if (cb.c != 12) return 1;
+  if (cb.c != 12 && cb.c != 13) return 1;
   int G, BS, R;
   bullet_comb_shape(std::max(2, n), &G, &BS, &R);
+  if (cb.c == 13 && G != 4) G = 10;
   const int S = BS / 4, wgs = (n * G + S - 1) / S;
   if (wgs * R > kBulletPartsMax) return 1;
   *per_msm = wgs * R;
-  KScope ks(ctx, "msm_comb_parts", 0.0, (double)B * n * 22.0 * (1.0 - 1.0 / 4096.0));
+  KScope ks(ctx, "msm_comb_parts", 0.0, (double)B * n * (253 / cb.c + 1) * (1.0 - 1.0 / (double)(1 << cb.c)));
   const dim3 grid((unsigned)wgs, (unsigned)B);
   const int NS = (int)cb.slots + 1;
-#define SPG_CMP(GG, BB) \
-  hipLaunchKernelGGL((k_comb_msm_parts<GG, BB>), grid, dim3(BB), 0, ctx->stream, d_scalars, d_idx, n, cb.p, NS, R, d_parts)
-  if (G == 4) {
-    if (BS == 64) SPG_CMP(4, 64); else if (BS == 128) SPG_CMP(4, 128); else SPG_CMP(4, 256);
+#define SPG_CMP(CC, GG, BB) \
+  hipLaunchKernelGGL((k_comb_msm_parts<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, d_scalars, d_idx, n, cb.p, NS, R, d_parts)
+#define SPG_CMP_BS(CC, GG) \
+  do { if (BS == 64) SPG_CMP(CC, GG, 64); else if (BS == 128) SPG_CMP(CC, GG, 128); else SPG_CMP(CC, GG, 256); } while (0)
+  if (cb.c == 13) {
+    if (G == 4) SPG_CMP_BS(13, 4); else SPG_CMP_BS(13, 10);
+  } else if (G == 4) {
+    SPG_CMP_BS(12, 4);
   } else if (G == 8) {
-    if (BS == 64) SPG_CMP(8, 64); else if (BS == 128) SPG_CMP(8, 128); else SPG_CMP(8, 256);
+    SPG_CMP_BS(12, 8);
   } else {
-    if (BS == 64) SPG_CMP(11, 64); else if (BS == 128) SPG_CMP(11, 128); else SPG_CMP(11, 256);
+    SPG_CMP_BS(12, 11);
   }
+#undef SPG_CMP_BS
 #undef SPG_CMP
   SPG_HIP(ctx, hipGetLastError());
   return 0;

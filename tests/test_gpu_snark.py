@@ -104,6 +104,7 @@ ROUND_FORMS = {
     "layer_pairs_small_wgs": {"SPG_PAIR_BS": "64"},
     "layer_pairs_everywhere": {"SPG_PAIR_MAX": "6144", "SPG_WIDE_MIN": str(1 << 40)},
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
+    "comb_13_bit_windows": {"SPG_COMB_C": "13"},
 }
 
 
@@ -119,7 +120,8 @@ def test_round_forms(form):
     per launch (SPG_EQ_MULTI=0); device witness parts copied instead of read in place (SPG_WIT_IN_PLACE=0); SPARK layer
     rounds one per launch (SPG_LAYER_PAIR=0) instead of two per launch where they are small, paired rounds over 64-thread
     workgroups (more of them: the ticketed sums and the last pair's corners from several workgroups), and pairs for every
-    round that fits (SPG_PAIR_MAX, no throughput-form rounds)"""
+    round that fits (SPG_PAIR_MAX, no throughput-form rounds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
+    the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds"""
     import subprocess
     import sys
 
