@@ -245,7 +245,7 @@ def roofline_valu(prof, traffic_file=None):
     if not cand:
         return None
     dom = max(cand, key=lambda k: cand[k][1])
-    launches, us, nbytes, ops = cand[dom]
+    launches, us, nbytes, ops = cand[dom][:4]
     achieved = ops / (us * 1e-6)
     traffic = traffic_of(dom, traffic_file)
     out = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 1), "peak": MADD_PEAK, "unit": "ext_madd/s",
