@@ -75,8 +75,8 @@ def events_in_gaps(d, evfile, top=40):
     ev = []
     for line in open(evfile):
         if line.startswith("[spgev]"):
-            _, ns, nm, us = line.split()
-            ev.append((int(ns), nm, float(us)))
+            f = line.split()  # lap titles may hold spaces
+            ev.append((int(f[1]), " ".join(f[2:-1]), float(f[-1])))
     ev.sort()
     mark = os.environ.get("MARK")
     if mark:
@@ -94,6 +94,10 @@ def events_in_gaps(d, evfile, top=40):
     keys = [x[0] for x in ev]
     by_lap = defaultdict(float)
     maxlap = max((x[2] for x in ev), default=0) * 1e3
+    only = os.environ.get("TRANS")  # "prev->next": only the gaps of that kernel transition
+    if only:
+        pa, pb = [x.strip() for x in only.split("->")]
+        gaps = [x for x in gaps if pa in x[3] and pb in x[4]]
     for g, a, b, pn, nn in gaps:
         # every lap whose interval [end - us, end] overlaps the gap, by the overlap (nested Laps objects overlap each
         # other: read the innermost names)
@@ -104,6 +108,26 @@ def events_in_gaps(d, evfile, top=40):
             ov = min(e1, b) - max(e0, a)
             if ov > 0:
                 by_lap[ev[j][1]] += ov
+    if os.environ.get("DUMP"):
+        # one prove's timeline: every gap over DUMP us between the first two MARK launches, with the laps that
+        # overlap it (start offset in the gap, us)
+        lim = float(os.environ["DUMP"]) * 1e3
+        m2 = [r for r in rows if mark and mark in r[2]]
+        stop = m2[1][0] if len(m2) > 1 else rows[-1][1]
+        t0 = rows[0][0]
+        for g, a, b, pn, nn in gaps:
+            if b > stop:
+                break
+            if g < lim:
+                continue
+            lo, hi = bisect.bisect_left(keys, a), bisect.bisect_right(keys, b + maxlap)
+            laps = []
+            for j in range(lo, hi):
+                e1 = ev[j][0]
+                e0 = e1 - ev[j][2] * 1e3
+                if min(e1, b) - max(e0, a) > 0 and ev[j][2] * 1e3 < 4 * g:
+                    laps.append(f"{ev[j][1].split(':')[-1]}[{(e0 - a) / 1e3:.0f},{ev[j][2]:.0f}]")
+            print(f"{(a - t0) / 1e3:9.0f} {g / 1e3:7.1f} us {pn[-24:]:>24s} -> {nn[-24:]:24s} {' '.join(laps)}")
     tot = sum(g[0] for g in gaps)
     print(f"-- idle {tot / 1e6:.2f} ms in {len(gaps)} gaps; host laps ending inside them (lap time, capped at the gap):")
     for k, v in sorted(by_lap.items(), key=lambda kv: -kv[1])[:top]:

@@ -634,7 +634,10 @@ static void bullet_comb_shape(int P, int* G, int* BS, int* R) {
   // fewer, twice the host-summed parts): 1.89 -> 1.74, R = 16: 1.85
   *G = P >= 2048 ? 4 : 11;
   *BS = P <= 64 ? 64 : (P <= 128 ? 128 : 256);
-  *R = P >= 2048 ? 1 : 8;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
+  // R: round 4 chose 8 on device time alone; on the prover's wall clock the host's part sums weigh more (91 ns per
+  // addition on the box, K <= 4 chunks per MSM: scripts/micro/parts_finals_cpu.cpp, profiles/r05_parts_finals.txt),
+  // and R = 2 was fastest (2-rep A/B, SNARK median ms: R 8: 16.66 / 17.13, 2: 16.08 / 16.13, 1: 17.56 / 16.71)
+  *R = P >= 2048 ? 1 : 2;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
   if (eg == 4 || eg == 8 || eg == 11) *G = eg;
   if (ebs == 64 || ebs == 128 || ebs == 256) *BS = ebs;
   if (er >= 1 && er <= *BS / 4 && (er & (er - 1)) == 0) *R = er;
