@@ -34,6 +34,7 @@ layer-round launches (their intervals include the host's answers between rounds)
 workload, and `cpu_baseline_all_cores` the same work run as one independent prove per usable host core at once.
 """
 import argparse
+import faulthandler
 import hashlib
 import json
 import math
@@ -41,6 +42,10 @@ import os
 import sys
 import threading
 import time
+
+# a native fault (libspg, the oracle, the HIP runtime) prints every thread's Python stack on stderr before the process
+# dies, so a crash in a driver run names the step it happened in
+faulthandler.enable()
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spartan-parallel_amd"))

@@ -407,7 +407,8 @@ struct PhaseTimer {
     t0 = t1;
   }
 };
-static PhaseTimer g_snark_phases;
+// per thread: the all-cores baselines run SNARK::prove on several threads at once (a shared lap list raced)
+static thread_local PhaseTimer g_snark_phases;
 
 // SNARK::prove (lib.rs:971-2746)
 static inline SNARKProof snark_prove(const SnarkIn& in0, SnarkInst& block, SnarkInst& pairwise, SnarkInst& perm_root,

@@ -12,6 +12,7 @@
 #include <memory>
 
 #include "hcurve.hpp"
+#include "hvec.hpp"
 #include "hpool.hpp"
 
 using namespace spg;
@@ -88,6 +89,37 @@ int main(int argc, char** argv) {
     sink += acc.X.v[0];
   }
   printf("hext_add %.1f ns each\n", us_since(t0) * 1e3 / R / (per - 1));
+  if (h::ifma_on()) {
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) sink += h::ext_sum8(hx.data(), per).X.v[0];
+    printf("ext_sum8 (8-lane IFMA full additions): %.1f ns per point\n", us_since(t0) * 1e3 / R / per);
+    std::vector<h::HNiels> nl;
+    h::hext_batch_to_niels(hx, nl);
+    std::vector<const h::HNiels*> np(per);
+    for (size_t i = 0; i < per; i++) np[i] = &nl[(i * 7919) % per];
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) {
+      h::HExt acc = h::hext_identity();
+      for (size_t i = 0; i < per; i++) acc = h::hext_madd(acc, *np[i]);
+      sink += acc.X.v[0];
+    }
+    printf("hext_madd (scalar mixed additions): %.1f ns each\n", us_since(t0) * 1e3 / R / per);
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) sink += h::niels_sum8(np.data(), per).X.v[0];
+    printf("niels_sum8 (8-lane IFMA mixed additions): %.1f ns per entry\n", us_since(t0) * 1e3 / R / per);
+    for (size_t m : {8, 16, 32, 64}) {
+      t0 = clk::now();
+      for (int r = 0; r < R; r++) sink += h::niels_sum8(np.data(), m).X.v[0];
+      const double v = us_since(t0) / R;
+      t0 = clk::now();
+      for (int r = 0; r < R; r++) {
+        h::HExt acc = h::hext_identity();
+        for (size_t i = 0; i < m; i++) acc = h::hext_madd(acc, *np[i]);
+        sink += acc.X.v[0];
+      }
+      printf("  %zu entries: niels_sum8 %.2f us, scalar %.2f us\n", m, v, us_since(t0) / R);
+    }
+  }
   t0 = clk::now();
   for (int r = 0; r < R; r++) {
     uint8_t out[32];

@@ -18,6 +18,7 @@
 #include "../../include/spg.h"
 #include "curve.hpp"
 #include "hcurve.hpp"
+#include "hvec.hpp"
 #include "hpool.hpp"
 #include "keccak.hpp"
 
@@ -265,12 +266,39 @@ struct HostGens {
     // ~1 MB tables per generator, which mostly miss the caches (host-path proofs 1.63 -> 0.98 ms per SNARK::prove in
     // situ, session r03zm; a standalone micro with warm tables showed no gain). SPG_HOST_PREFETCH=0: off.
     static const size_t kPf = getenv("SPG_HOST_PREFETCH") ? (size_t)atol(getenv("SPG_HOST_PREFETCH")) : 3;
+    // with AVX-512 IFMA a job's run of at least kVecMin units goes through the 8-lane sums (hvec.hpp): the entries of
+    // its nonzero bytes, 8 accumulators, one reduction (SPG_VEC_MIN: the threshold; 0 = never)
+    static const size_t kVecMin = getenv("SPG_VEC_MIN") ? (size_t)atol(getenv("SPG_VEC_MIN")) : 16;
+    const bool vec = kVecMin && h::ifma_on();
     pool().parallel_for((int)S, [&](int si) {
       const size_t s = (size_t)si, u0 = slice_lo(s), u1 = slice_lo(s + 1);
       size_t u = u0;
       while (u < u1) {
         const size_t j = tjob[u / 32], ue = std::min(u1, 32 * tfirst[j + 1]);
         h::HExt acc = h::hext_identity();
+        if (vec && ue - u >= kVecMin) {
+          constexpr size_t kCap = 256;
+          const h::HNiels* ent[kCap];
+          size_t m = 0;
+          bool any = false;
+          for (; u < ue; u++) {
+            const Term& tm = terms[u / 32];
+            const int w = (int)(u % 32);
+            if (!tm.b[w]) continue;
+            ent[m] = &tm.fb->tab[w * 256 + tm.b[w]];
+            if (m < 16) __builtin_prefetch(ent[m]);
+            if (++m == kCap) {
+              const h::HExt part = h::niels_sum8(ent, m);
+              acc = any ? h::hext_add(acc, part) : part;
+              any = true;
+              m = 0;
+            }
+          }
+          if (m) {
+            const h::HExt part = h::niels_sum8(ent, m);
+            acc = any ? h::hext_add(acc, part) : part;
+          }
+        }
         for (; u < ue; u++) {
           if (kPf && u + kPf < u1) {
             const Term& tp = terms[(u + kPf) / 32];

@@ -12,6 +12,7 @@
 #include "comm.hpp"
 #include "curve.hpp"
 #include "hcurve.hpp"
+#include "hvec.hpp"
 #include "hostmath.hpp"
 #include "hpool.hpp"
 #include "keccak.hpp"
@@ -158,6 +159,36 @@ int spgh_hcurve_check(const uint8_t* uni, const uint8_t* k, size_t n) {
   memset(bad_enc, 0xff, 32);
   h::HExt X;
   bad += h::hext_decompress(bad_enc, X);  // non-canonical must be rejected
+  return bad;
+}
+
+// The 8-lane IFMA sums (hvec.hpp) against the scalar additions: for m = 0 .. n entries, the sum of the first m Niels
+// forms (mixed additions) and of the first m extended points (full additions), compared by encoding. Returns the
+// number of mismatches, or -1 when this CPU has no AVX-512 IFMA (nothing to check).
+int spgh_vec_check(const uint8_t* uni, size_t n) {
+  using namespace spg;
+  if (!h::ifma_on()) return -1;
+  int bad = 0;
+  std::vector<h::HExt> H(n);
+  for (size_t i = 0; i < n; i++) H[i] = h::hext_from_dev(ristretto_from_uniform_bytes(uni + 64 * i));
+  std::vector<h::HNiels> N;
+  h::hext_batch_to_niels(H, N);
+  std::vector<const h::HNiels*> ptr(n);
+  for (size_t i = 0; i < n; i++) ptr[i] = &N[i];
+  h::HExt s1 = h::hext_identity(), s2 = h::hext_identity();
+  for (size_t m = 0; m <= n; m++) {
+    if (m) {
+      s1 = h::hext_madd(s1, N[m - 1]);
+      s2 = h::hext_add(s2, H[m - 1]);
+    }
+    uint8_t a[32], b[32];
+    h::hext_compress(s1, a);
+    h::hext_compress(h::niels_sum8(ptr.data(), m), b);
+    bad += memcmp(a, b, 32) != 0;
+    h::hext_compress(s2, a);
+    h::hext_compress(h::ext_sum8(H.data(), m), b);
+    bad += memcmp(a, b, 32) != 0;
+  }
   return bad;
 }
 

@@ -255,7 +255,10 @@ void bucket_finals(const Ext* bk, size_t B, int NB, Pt* out, const h::HExt* extr
 // finish adds the chunk sums and encodes
 static void parts_finals(const Ext* bk, size_t B, size_t per, Pt* out, const h::HExt* extra) {
   const int threads = pool().size() + 1;
-  const int K = (int)std::max<size_t>(1, std::min<size_t>(per / 8, (size_t)threads / std::max<size_t>(B, 1)));
+  // chunks of >= 8 parts (>= 48 with the 8-lane IFMA sums, whose lanes want several points each)
+  static const bool vec = h::ifma_on() && !(getenv("SPG_VEC_MIN") && atol(getenv("SPG_VEC_MIN")) == 0);
+  const size_t cmin = vec ? 48 : 8;
+  const int K = (int)std::max<size_t>(1, std::min<size_t>(per / cmin, (size_t)threads / std::max<size_t>(B, 1)));
   std::vector<h::HExt> part(B * K);
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[B]);
   for (size_t b = 0; b < B; b++) left[b].store(K);
@@ -266,8 +269,16 @@ static void parts_finals(const Ext* bk, size_t B, size_t per, Pt* out, const h::
     // of the chunk requested at once, their misses overlapping, before the dependent additions read them
     for (const uint8_t* q = (const uint8_t*)(bk + b * per + lo); q < (const uint8_t*)(bk + b * per + hi); q += 64)
       __builtin_prefetch(q, 0, 0);
-    h::HExt acc = h::hext_from_dev(bk[b * per + lo]);
-    for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(bk[b * per + i]));
+    h::HExt acc;
+    if (vec && hi - lo >= 16) {
+      thread_local std::vector<h::HExt> hx;
+      hx.resize(hi - lo);
+      for (size_t i = lo; i < hi; i++) hx[i - lo] = h::hext_from_dev(bk[b * per + i]);
+      acc = h::ext_sum8(hx.data(), hi - lo);
+    } else {
+      acc = h::hext_from_dev(bk[b * per + lo]);
+      for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(bk[b * per + i]));
+    }
     part[task] = acc;
     if (left[b].fetch_sub(1, std::memory_order_acq_rel) == 1) {
       h::HExt sum = part[b * K];

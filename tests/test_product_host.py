@@ -216,6 +216,19 @@ def test_host_radix51_curve_matches_device_form(hc):
     assert bad == 0
 
 
+def test_host_ifma_sums_match_scalar(hc):
+    """hvec.hpp's 8-lane AVX-512 IFMA sums (mixed additions of Niels entries, full additions of extended points) give
+    the scalar additions' points for every length 0 .. 70 (lane padding, one partial group, several groups); skipped
+    on a CPU without IFMA, where the prover takes the scalar additions"""
+    rng = np.random.default_rng(11)
+    n = 70
+    uni = rng.integers(0, 256, 64 * n, dtype=np.uint8)
+    bad = hc.spgh_vec_check(uni.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n))
+    if bad == -1:
+        pytest.skip("no AVX-512 IFMA on this CPU")
+    assert bad == 0
+
+
 def _mont(x):
     R = 2**256
     v = x * R % Q
