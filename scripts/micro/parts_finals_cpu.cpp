@@ -6,6 +6,7 @@
 // hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../spartan-parallel_amd/csrc -o parts_finals_cpu parts_finals_cpu.cpp -lpthread
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <atomic>
 #include <chrono>
@@ -49,6 +50,18 @@ static void finals(const Ext* bk, size_t per, int K, bool prefetch, uint8_t outb
 
 int main(int argc, char** argv) {
   const size_t per = argc > 1 ? (size_t)atol(argv[1]) : 704;
+  // argv[2] = "pin": the pool on the first 8 CPUs of this process' mask (the prover pins it to one L3 domain)
+  if (argc > 2 && !strcmp(argv[2], "pin")) {
+    cpu_set_t set;
+    sched_getaffinity(0, sizeof(set), &set);
+    std::vector<int> c;
+    for (int i = 0; i < CPU_SETSIZE && c.size() < 8; i++)
+      if (CPU_ISSET(i, &set)) c.push_back(i);
+    pool_cpus() = c;
+    (void)pool();  // workers start pinned (the pool is sized from this thread's mask, so before pinning it)
+    pin_thread({c[0]});
+    printf("pool pinned to cpus %d..%d\n", c.front(), c.back());
+  }
   const int R = 2000;
   // device-format points: random multiples of a fixed point, Z scaled, as the device leaves them
   std::vector<Ext> bk(2 * per);

@@ -149,14 +149,18 @@ class Pool {
   }
 
  private:
+  // claims and runs tasks of burst g until none is left; the tasks this thread ran leave remaining_ in one step at the
+  // end (one contended update per thread and burst, not per task)
   void work(uint32_t g, const std::function<void(int)>* f, int n) {
+    int ran = 0;
     for (;;) {
       uint64_t v = next_.load();
-      if ((uint32_t)(v >> 32) != g || (uint32_t)v >= (uint32_t)n) return;  // kClosed >= any n
+      if ((uint32_t)(v >> 32) != g || (uint32_t)v >= (uint32_t)n) break;  // kClosed >= any n
       if (!next_.compare_exchange_weak(v, v + 1)) continue;
       (*f)((int)(uint32_t)v);
-      remaining_.fetch_sub(1);
+      ran++;
     }
+    if (ran) remaining_.fetch_sub(ran);
   }
   void worker() {
     uint32_t seen = 0;
@@ -193,16 +197,18 @@ class Pool {
   std::vector<std::thread> threads_;
   std::mutex mu_, call_mu_;
   std::condition_variable cv_;
-  std::atomic<const std::function<void(int)>*> fn_{nullptr};
+  // the words every burst moves between cores, one cache line each: spinning workers poll gen_pub_, and the claims
+  // (next_) and completions (remaining_) of a burst would otherwise invalidate the line they poll on every task
+  alignas(64) std::atomic<const std::function<void(int)>*> fn_{nullptr};
   std::atomic<int> n_{0};
   uint32_t gen_ = 0;  // written by the (serialised) caller only
   uint64_t bursts_ = 0;
-  std::atomic<uint64_t> next_{0};
-  std::atomic<int> remaining_{0};
-  bool quit_ = false;
-  std::atomic<int> sleepers_{0};
-  std::atomic<uint32_t> gen_pub_{0};
+  alignas(64) std::atomic<uint64_t> next_{0};
+  alignas(64) std::atomic<int> remaining_{0};
+  alignas(64) std::atomic<uint32_t> gen_pub_{0};
   std::atomic<bool> quit_pub_{false};
+  alignas(64) bool quit_ = false;
+  std::atomic<int> sleepers_{0};
   std::chrono::microseconds spin_{20000};
 };
 
