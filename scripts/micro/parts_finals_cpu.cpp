@@ -176,6 +176,16 @@ int main(int argc, char** argv) {
                pf ? ", prefetch" : "", tot / RR);
       }
   }
+  {  // the host scalar-field inverse (binary GCD, field.hpp fq_inv_host): u^-1 of every Bullet round
+    Fq x = fq_from_u64(123456789);
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) {
+      Fq y = fq_inv(x);
+      x = fq_add(x, y);
+    }
+    printf("fq_inv (host) %.2f us each\n", us_since(t0) / R);
+    sink += x.l[0];
+  }
   t0 = clk::now();
   for (int r = 0; r < R; r++) pool().parallel_for(threads, [&](int) { sink += 1; });
   printf("empty parallel_for over %d tasks: %.2f us\n", threads, us_since(t0) / R);

@@ -3,6 +3,7 @@
 #   tests K            pytest -m gpu -k K
 #   ab VAR "v1 v2" n   traced A/B of one switch (scripts/ab_trace.sh)
 #   bench TAG ENV...   one bench line (default workload, or BENCH_ARGS) under the given env assignments
+#   hipt TAG           kernel + HIP runtime API + memory-copy trace of the same proves (csv), lap events in TAG.err
 #   gaps TAG           kernel trace + host lap events of 6 proves -> per-prove idle gaps by transition and by host lap
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -19,6 +20,12 @@ case "$1" in
     env "$@" timeout -k 10 ${T:-600} python3 bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > gpurun_out/bench_$tag.json \
       2> gpurun_out/bench_$tag.err || { tail -5 gpurun_out/bench_$tag.err; exit 1; }
     tail -c 600 gpurun_out/bench_$tag.json ;;
+  hipt)
+    export TMPDIR=/tmp
+    (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 TRACE_REPS=4 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace \
+      --memory-copy-trace --output-format csv -d "$R/gpurun_out/kt_$2" -o kt -- python3 "$R/scripts/trace_snark.py" \
+      > /dev/null 2> "$R/gpurun_out/kt_$2.err") || exit 1
+    ls gpurun_out/kt_$2 ;;
   gaps)
     export TMPDIR=/tmp
     (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 TRACE_REPS=6 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
