@@ -14,6 +14,7 @@
 
 #include "hcurve.hpp"
 #include "hvec.hpp"
+#include "keccak.hpp"
 #include "hpool.hpp"
 
 using namespace spg;
@@ -175,6 +176,25 @@ int main(int argc, char** argv) {
         printf("parts_finals B=2 K=%2d on parts a kernel just wrote (mapped coherent)%s: %.2f us\n", K,
                pf ? ", prefetch" : "", tot / RR);
       }
+  }
+  {  // merlin transcript operations (keccak-f[1600] per 166 bytes absorbed and per challenge)
+    Merlin m("bench");
+    uint8_t b[64] = {1};
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) {
+      KeccakState st;
+      memset(st.a, r, sizeof(st.a));
+      st.permute();
+      sink += st.a[0];
+    }
+    printf("keccak-f[1600] %.3f us\n", us_since(t0) / R);
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) m.message("claim_prod_left", b, 32);
+    printf("merlin append 32 B %.3f us\n", us_since(t0) / R);
+    t0 = clk::now();
+    for (int r = 0; r < R; r++) m.challenge("rand_coeffs_next_layer", b, 64);
+    printf("merlin challenge 64 B %.3f us\n", us_since(t0) / R);
+    sink += b[0];
   }
   {  // the host scalar-field inverse (binary GCD, field.hpp fq_inv_host): u^-1 of every Bullet round
     Fq x = fq_from_u64(123456789);

@@ -690,6 +690,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   Fq x_hat = aa[0], a_hat = bb[0];
   Fq y_hat = fq_mul(x_hat, a_hat);
   // delta = d * g_hat + r_delta * h with g_hat = sum_j cw[j] G_j
+  bool beta_done = false;
   if (on_host) {
     HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), FqV(n)};
     for (size_t i = 0; i < n; i++) j.second[i] = fq_mul(d, cw[i]);
@@ -697,17 +698,43 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     j.second.push_back(r_delta);
     pts = g.host.commit_many({j});
   } else {
-    std::vector<Fq> s(n2, fq_zero());
-    par_range(n, [&](size_t lo, size_t hi) {
-      for (size_t j = lo; j < hi; j++) s[j] = fq_mul(d, cw[j]);
-    });
-    s[n + 1] = r_delta;
-    int rc = device_msm_flat(ctx, g, s, n2, 1, d_idx, &pts);
-    if (rc) return rc;
+    // device rounds: d g_hat from the comb table as partial points (as Cx), r_delta h and beta on the host meanwhile;
+    // the bucket form (device_msm_flat) where the comb does not apply
+    static const bool delta_comb = !getenv("SPG_DELTA_COMB") || atoi(getenv("SPG_DELTA_COMB")) != 0;
+    int cper = 0, rc = 1;
+    if (mbk && delta_comb) {  // (the mapped region's Cx part and slot 26 are free again: Cx is done, the rounds are over)
+      Fq* d_s = (Fq*)ws_get(ctx, 26, n * sizeof(Fq) + 64);
+      Fq* stage = (Fq*)pinned_get(ctx, n * sizeof(Fq) + 64);
+      if (!d_s || !stage) return set_err(ctx, SPG_E_NOMEM, "delta scalars");
+      par_range(n, [&](size_t lo, size_t hi) {
+        for (size_t j = lo; j < hi; j++) stage[j] = fq_mul(d, cw[j]);
+      });
+      SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+      rc = comb_msm_parts(ctx, g.dev, d_s, d_idx, gmax, (int)n, 1, (Ext*)d_map, &cper);
+      if (rc != 0 && rc != 1) return rc;
+    }
+    if (rc == 0) {
+      SPG_HIP(ctx, hipEventRecord(ctx->ev_cx, ctx->stream));
+      const h::HExt rdh = g.host.sum_many({{{(size_t)H}, {r_delta}}})[0];
+      out->beta = g.host.commit_many({{{(size_t)G1, (size_t)H}, {fq_mul(d, r), r_beta}}})[0];
+      beta_done = true;
+      SPG_HIP(ctx, hipEventSynchronize(ctx->ev_cx));
+      pts.resize(1);
+      parts_finals((const Ext*)mapped, 1, (size_t)cper, pts.data(), &rdh);
+    } else {
+      std::vector<Fq> s(n2, fq_zero());
+      par_range(n, [&](size_t lo, size_t hi) {
+        for (size_t j = lo; j < hi; j++) s[j] = fq_mul(d, cw[j]);
+      });
+      s[n + 1] = r_delta;
+      rc = device_msm_flat(ctx, g, s, n2, 1, d_idx, &pts);
+      if (rc) return rc;
+    }
   }
   out->delta = pts[0];
   t.point("delta", out->delta);
-  out->beta = g.host.commit_many({{{(size_t)G1, (size_t)H}, {fq_mul(d, r), r_beta}}})[0];
+  if (!beta_done)
+    out->beta = g.host.commit_many({{{(size_t)G1, (size_t)H}, {fq_mul(d, r), r_beta}}})[0];
   t.point("beta", out->beta);
   Fq c = t.challenge("c");
   out->z1 = fq_add(d, fq_mul(c, y_hat));

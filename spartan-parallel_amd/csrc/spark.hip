@@ -120,6 +120,20 @@ __global__ void k_tree_level(Fq* __restrict__ tree, size_t nc, size_t stride, si
   Fq* v = tree + c * stride;
   v[off_k1 + i] = fq_mul(v[off_k + i], v[off_k + i + half]);
 }
+// The levels of every circuit's tree from level k0 up, and its top product, in one launch: workgroup c builds circuit c's
+// levels (each level's products read the level below, which this workgroup wrote: a barrier between levels) -- the
+// small top levels would otherwise be one launch each, ~3 us of work behind a ~4 us launch
+__global__ void __launch_bounds__(256) k_tree_top(Fq* __restrict__ tree, size_t stride, int log_m, int k0,
+                                                  Fq* __restrict__ tops) {
+  Fq* v = tree + blockIdx.x * stride;
+  const size_t M = (size_t)1 << log_m;
+  for (int k = k0; k + 1 < log_m; k++) {
+    const size_t ok = 2 * M - 2 * (M >> k), ok1 = 2 * M - 2 * (M >> (k + 1)), half = M >> (k + 1);
+    for (size_t i = threadIdx.x; i < half; i += 256) v[ok1 + i] = fq_mul(v[ok + i], v[ok + i + half]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tops[blockIdx.x] = fq_mul(v[2 * M - 4], v[2 * M - 3]);
+}
 // ProductCircuit::evaluate of every circuit: product of the top level's two entries
 __global__ void k_tops(const Fq* __restrict__ tree, size_t nc, size_t stride, size_t off, Fq* __restrict__ out) {
   size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -1549,13 +1563,26 @@ int spark_prove_core(spg_ctx* ctx, spg_spark* S, FqV ex, FqV ey, const FqV& eval
     Fq* tree = which ? tsm.loc : tso.loc;
     const size_t M = which ? mm : mo, nc = which ? 4 : 4 * B;
     KScope ks(ctx, "spark_product_tree", 96.0 * nc * M / 2);
-    for (size_t k = 0; k + 1 < lg2(M); k++) {
+    // levels of more than kTopHalf products per circuit: one grid-wide launch each; the rest and the tops: k_tree_top
+    static const size_t kTopHalf = getenv("SPG_TREE_TOP") ? (size_t)atol(getenv("SPG_TREE_TOP")) : 1024;
+    size_t k = 0;
+    for (; k + 1 < lg2(M) && (M >> (k + 1)) > kTopHalf; k++) {
       size_t ok = 2 * M - 2 * (M >> k), ok1 = 2 * M - 2 * (M >> (k + 1));
       hipLaunchKernelGGL(k_tree_level, dim3(nblk(nc * (M >> (k + 1)))), dim3(256), 0, s, tree, nc, 2 * M, ok, ok1,
                          (int)lg2(M >> (k + 1)));
     }
-    const size_t top = 2 * M - 4;  // v_{L-1}
-    hipLaunchKernelGGL(k_tops, dim3(nblk(nc)), dim3(256), 0, s, tree, nc, 2 * M, top, dtops + (which ? 4 * B : 0));
+    if (kTopHalf) {
+      hipLaunchKernelGGL(k_tree_top, dim3((unsigned)nc), dim3(256), 0, s, tree, 2 * M, (int)lg2(M), (int)k,
+                         dtops + (which ? 4 * B : 0));
+    } else {
+      for (; k + 1 < lg2(M); k++) {
+        size_t ok = 2 * M - 2 * (M >> k), ok1 = 2 * M - 2 * (M >> (k + 1));
+        hipLaunchKernelGGL(k_tree_level, dim3(nblk(nc * (M >> (k + 1)))), dim3(256), 0, s, tree, nc, 2 * M, ok, ok1,
+                           (int)lg2(M >> (k + 1)));
+      }
+      const size_t top = 2 * M - 4;  // v_{L-1}
+      hipLaunchKernelGGL(k_tops, dim3(nblk(nc)), dim3(256), 0, s, tree, nc, 2 * M, top, dtops + (which ? 4 * B : 0));
+    }
   }
   SPG_HIP(ctx, hipGetLastError());
   FqV tops(4 * B + 4);

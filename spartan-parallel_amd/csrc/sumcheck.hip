@@ -25,34 +25,41 @@ __device__ __forceinline__ int find_inst(const PqxArgs& a, uint32_t t) {
   return p;
 }
 
-// block-wide sums of three Fq values; the result is valid in thread 0
+// block-wide sums of three Fq values over a 256-thread block, valid in every thread: butterflies across each wave
+// (six shuffle steps), then the four wave sums through 384 bytes of LDS, added by every thread in one order. (A
+// 256-entry LDS tree here held 24.6 KB of LDS per workgroup, which capped k_phase1_eval at 6 workgroups per CU.)
 __device__ __forceinline__ void block_sum3(Fq& v0, Fq& v1, Fq& v2) {
-  __shared__ uint32_t sh[3][soa_words<Fq, 256>()];  // component-major: no bank conflicts
-  int t = threadIdx.x;
-  for (int d = 128; d >= 1; d >>= 1) {
-    if (t >= d && t < 2 * d) {
-      soa_put<256>(sh[0], t - d, v0);
-      soa_put<256>(sh[1], t - d, v1);
-      soa_put<256>(sh[2], t - d, v2);
-    }
-    __syncthreads();
-    if (t < d) {
-      v0 = fq_add(v0, soa_get<256, Fq>(sh[0], t));
-      v1 = fq_add(v1, soa_get<256, Fq>(sh[1], t));
-      v2 = fq_add(v2, soa_get<256, Fq>(sh[2], t));
-    }
-    __syncthreads();
+  __shared__ uint32_t sh[4][3][8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    v0 = fq_add(v0, fq_shfl_xor(v0, m));
+    v1 = fq_add(v1, fq_shfl_xor(v1, m));
+    v2 = fq_add(v2, fq_shfl_xor(v2, m));
   }
-  // broadcast thread 0's sums
-  if (t == 0) {
-    soa_put<256>(sh[0], 0, v0);
-    soa_put<256>(sh[1], 0, v1);
-    soa_put<256>(sh[2], 0, v2);
-  }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      sh[w][0][j] = v0.l[j];
+      sh[w][1][j] = v1.l[j];
+      sh[w][2][j] = v2.l[j];
+    }
   __syncthreads();
-  v0 = soa_get<256, Fq>(sh[0], 0);
-  v1 = soa_get<256, Fq>(sh[1], 0);
-  v2 = soa_get<256, Fq>(sh[2], 0);
+  Fq s[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) s[k].l[j] = sh[0][k][j];
+    for (int v = 1; v < 4; v++) {
+      Fq o;
+#pragma unroll
+      for (int j = 0; j < 8; j++) o.l[j] = sh[v][k][j];
+      s[k] = fq_add(s[k], o);
+    }
+  }
+  v0 = s[0];
+  v1 = s[1];
+  v2 = s[2];
   __syncthreads();
 }
 

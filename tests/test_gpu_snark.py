@@ -105,6 +105,9 @@ ROUND_FORMS = {
     "layer_pairs_everywhere": {"SPG_PAIR_MAX": "6144", "SPG_WIDE_MIN": str(1 << 40)},
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
     "comb_13_bit_windows": {"SPG_COMB_C": "13"},
+    "tree_levels_per_launch": {"SPG_TREE_TOP": "0"},
+    "tree_one_launch": {"SPG_TREE_TOP": str(1 << 40)},
+    "delta_bucket_msm": {"SPG_DELTA_COMB": "0"},
 }
 
 
@@ -121,7 +124,9 @@ def test_round_forms(form):
     rounds one per launch (SPG_LAYER_PAIR=0) instead of two per launch where they are small, paired rounds over 64-thread
     workgroups (more of them: the ticketed sums and the last pair's corners from several workgroups), and pairs for every
     round that fits (SPG_PAIR_MAX, no throughput-form rounds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
-    the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds"""
+    the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds; SPARK product trees one
+    level per launch (SPG_TREE_TOP=0) or every level in the per-circuit workgroup launch; the device Bullet proofs' delta
+    on the bucket MSM (SPG_DELTA_COMB=0) instead of the comb parts"""
     import subprocess
     import sys
 

@@ -23,10 +23,10 @@ READELF = os.path.join(LLVM, "llvm-readelf")
 HOT = ("k_phase1_eval", "k_phase2_eval", "k_pqx_fold", "k_cubic_eval", "k_eq_table", "k_fold_top",
        "k_layer_round", "k_layer_pair", "k_layer_close", "k_layer_persist", "k_bullet_comb", "k_bullet_round_q", "k_comb_msm_parts",
        "k_smsm_bucket_q", "k_smsm_final", "k_gather_res", "k_spmv", "k_z_fill", "k_abc", "k_bound_part_multi",
-       "k_sum_cols_multi", "k_seg_dot", "k_bound_rows", "k_tree_level", "k_hash_ops", "k_hash_mem")
+       "k_sum_cols_multi", "k_seg_dot", "k_bound_rows", "k_tree_level", "k_tree_top", "k_hash_ops", "k_hash_mem")
 
 
-def private_segments(tmp_path):
+def private_segments(tmp_path, field="private_segment_fixed_size"):
     if not (os.path.exists(LIB) and os.path.exists(BUNDLER) and os.path.exists(READELF) and shutil.which("objcopy")):
         pytest.skip("needs the built libspg.so and the ROCm llvm tools")
     fat = tmp_path / "fat.bin"
@@ -47,7 +47,7 @@ def private_segments(tmp_path):
         notes = subprocess.run([READELF, "--notes", str(co)], capture_output=True, text=True, check=True).stdout
         for blk in notes.split("  - .agpr_count")[1:]:
             name = re.search(r"\.name:\s+(\S+)", blk)
-            ps = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+            ps = re.search(r"\." + field + r":\s+(\d+)", blk)
             if name and ps:
                 sizes[name.group(1)] = int(ps.group(1))
     return sizes
@@ -60,3 +60,12 @@ def test_round_kernels_have_no_scratch(tmp_path):
     assert any("k_phase1_eval_q" in k for k in hot) and any("k_bullet_comb" in k for k in hot)
     bad = {k: v for k, v in hot.items() if v}
     assert not bad, bad
+
+
+def test_evaluation_kernels_lds(tmp_path):
+    """the thread-per-point R1CSProof evaluations reduce through wave shuffles and a few hundred bytes of LDS (a
+    24.6 KB LDS tree capped them at 6 workgroups per CU)"""
+    lds = private_segments(tmp_path, "group_segment_fixed_size")
+    ev = {k: v for k, v in lds.items() if re.search(r"k_phase[12]_evalILb[01]E", k)}
+    assert len(ev) >= 4, sorted(lds)[:20]
+    assert max(ev.values()) <= 4096, ev
