@@ -330,6 +330,70 @@ __global__ void __launch_bounds__(256) k_phase1_eval(PqxArgs a, int mode, uint32
   grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
+// x-mode rounds whose rows (one (p, q) pair: sc_ni consecutive domain points) hold >= 64 J points: a wave takes 64 J
+// consecutive points of one row (lane l: points l, l + 64, .., coalesced), and since every point of a row shares the
+// eq factor Ap[p] Aq[q] -- e_X = sum_(p,q) Ap Aq sum_x Ax(X) (B C - D)(X) -- a lane sums Ax(X) (B C - D)(X) over its J
+// points and multiplies by the row factor once: 6 Fq products per point (+ the folds) instead of 9, the row factor's
+// 1 + 3 per J points. The same field sums as k_phase1_eval's, so the same (e0, e2, e3).
+template <bool FOLD, int J>
+__global__ void __launch_bounds__(256) k_phase1_eval_x(PqxArgs a, uint32_t total, uint32_t cons_len,
+                                                       const Fq* __restrict__ Ap, const Fq* __restrict__ Aq,
+                                                       const Fq* __restrict__ Ax, Fq* __restrict__ B,
+                                                       Fq* __restrict__ C, Fq* __restrict__ D, Fq* __restrict__ partials,
+                                                       unsigned* __restrict__ counter, uint32_t* __restrict__ mb,
+                                                       uint32_t seq, FoldArg F) {
+  const uint32_t nchunk = total / (64u * J);
+  if (FOLD) fold_side_pass(F, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256, nchunk * 64u);
+  const Fq omr = fq_sub(fq_one(), F.r);
+  const bool fx_side = FOLD && F.fmode == MODE_X;
+  const uint32_t lane = threadIdx.x & 63;
+  Fq e0 = fq_zero(), e2 = fq_zero(), e3 = fq_zero();
+  for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < nchunk; c += gridDim.x * 4) {  // uniform per wave
+    const uint32_t t0 = c * 64u * J;
+    const int p = find_inst(a, t0);
+    const PqxInst& d = pinst(a, p);
+    const uint32_t loc0 = t0 - d.dom_off, q = loc0 / d.sc_ni, x0 = loc0 % d.sc_ni;
+    const Fq apq = fq_mul(Ap[p], Aq[q * d.step_q]);
+    const size_t row = pqx_off(d) + (size_t)q * d.anw * d.ani;
+    const bool zero_hi = d.ni == 1;
+    Fq i0 = fq_zero(), i2 = fq_zero(), i3 = fq_zero();
+#pragma unroll 1
+    for (int j = 0; j < J; j++) {
+      const uint32_t x = x0 + lane + 64u * j, ix = x * d.step_x;
+      const Fq ax_lo = fx_side ? fold_side(F, ix) : Ax[ix];
+      const Fq ax_hi = fx_side ? fold_side(F, ix + cons_len) : Ax[ix + cons_len];
+      const size_t base = row + x, hi = base + d.ni / 2;
+      Fq b_lo, c_lo, d_lo, b_hi = fq_zero(), c_hi = fq_zero(), d_hi = fq_zero();
+      if (FOLD) {
+        const uint32_t fs = d.fstride;
+        fold_pair_rw(B, base, hi, !zero_hi, fs, F.r, omr, b_lo, b_hi);
+        fold_pair_rw(C, base, hi, !zero_hi, fs, F.r, omr, c_lo, c_hi);
+        fold_pair_rw(D, base, hi, !zero_hi, fs, F.r, omr, d_lo, d_hi);
+      } else {
+        b_lo = B[base];
+        c_lo = C[base];
+        d_lo = D[base];
+        if (!zero_hi) {
+          b_hi = B[hi];
+          c_hi = C[hi];
+          d_hi = D[hi];
+        }
+      }
+      i0 = fq_add(i0, fq_mul(ax_lo, fq_sub(fq_mul(b_lo, c_lo), d_lo)));
+      const Fq a2 = fq_sub(fq_dbl(ax_hi), ax_lo), b2 = fq_sub(fq_dbl(b_hi), b_lo);
+      const Fq c2 = fq_sub(fq_dbl(c_hi), c_lo), d2 = fq_sub(fq_dbl(d_hi), d_lo);
+      i2 = fq_add(i2, fq_mul(a2, fq_sub(fq_mul(b2, c2), d2)));
+      const Fq a3 = fq_sub(fq_add(a2, ax_hi), ax_lo), b3 = fq_sub(fq_add(b2, b_hi), b_lo);
+      const Fq c3 = fq_sub(fq_add(c2, c_hi), c_lo), d3 = fq_sub(fq_add(d2, d_hi), d_lo);
+      i3 = fq_add(i3, fq_mul(a3, fq_sub(fq_mul(b3, c3), d3)));
+    }
+    e0 = fq_add(e0, fq_mul(apq, i0));
+    e2 = fq_add(e2, fq_mul(apq, i2));
+    e3 = fq_add(e3, fq_mul(apq, i3));
+  }
+  grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
+}
+
 // ---- quad forms of the round evaluations (small rounds: latency-bound) ------------------------------------------
 // A round whose domain leaves the chip mostly idle is bound by the dependent chain of one thread's products (about
 // ten Fq products per point in phase 1, each ~0.6 us on one wave). Here a quad (4 lanes) takes each point and its
@@ -694,9 +758,12 @@ static size_t sc_quad_max() {
   static const size_t m = getenv("SPG_SC_QUAD_MAX") ? (size_t)atol(getenv("SPG_SC_QUAD_MAX")) : ((size_t)1 << 16);
   return m;
 }
+// workgroups of a round's evaluation: one per 256 threads of work, at most SPG_SC_GRID (default 1024, <= kScGridMax:
+// the partials buffer)
 static int grid_for(uint32_t total) {
+  static const int cap = getenv("SPG_SC_GRID") ? std::max(1, std::min(kScGridMax, atoi(getenv("SPG_SC_GRID")))) : 1024;
   int nb = (int)((total + 255) / 256);
-  if (nb > 1024) nb = 1024;
+  if (nb > cap) nb = cap;
   return nb < 1 ? 1 : nb;
 }
 
@@ -864,6 +931,37 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
   if (int rc = pqx_pack(ctx, v, a, kWsPqxA)) return rc;
   const bool quad = dom <= sc_quad_max();
   const int nb = quad ? grid_for((uint32_t)(4 * dom)) : grid_for((uint32_t)dom);
+  // x-mode rounds over rows of >= 128 points: the row-factored kernel, J points per lane (SPG_P1_ROWS=0: off)
+  static const bool rows_on = !getenv("SPG_P1_ROWS") || atoi(getenv("SPG_P1_ROWS")) != 0;
+  int J = 0;
+  if (rows_on && !quad && mode == MODE_X && (!fold || fold->arg.fmode == MODE_X)) {
+    size_t mn = ~(size_t)0;
+    for (size_t p = 0; p < P; p++) mn = std::min(mn, (size_t)v[p].sc_ni);
+    J = mn >= 512 ? 8 : (mn >= 256 ? 4 : (mn >= 128 ? 2 : 0));
+    // every row a multiple of 64 J points (power-of-two rows), so no wave's chunk straddles two rows
+    for (size_t p = 0; p < P && J; p++)
+      if (v[p].sc_ni % (64 * (size_t)J)) J = 0;
+  }
+  if (J) {
+    const uint32_t nchunk = (uint32_t)(dom / (64 * (size_t)J));
+    const int nbx = std::max(1, std::min(nb, (int)((nchunk + 3) / 4)));
+    // Fq products per point: the folds as k_phase1_eval, 6 for A (B C - D) at 3 points, the row factor per J points
+    KScope ks(ctx, fold ? "sc_phase1_fold_eval" : "sc_phase1_eval",
+              (fold ? 576.0 : 192.0) * dom + (fold ? 96.0 * fold->arg.side_half : 0.0) + 64.0 * (instance_len + proof_len),
+              0.0, (double)dom * (6.0 + (fold ? 7.0 : 0.0) + 4.0 / J));
+    const FoldArg fa = fold ? fold->arg : FoldArg{};
+#define SPG_P1X(FF, JJ)                                                                                              \
+  hipLaunchKernelGGL((k_phase1_eval_x<FF, JJ>), dim3(nbx), dim3(256), 0, ctx->stream, a, (uint32_t)dom,              \
+                     (uint32_t)cons_len, Ap, Aq, Ax, B, C, D, partials, ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, fa)
+    if (fold) {
+      if (J == 8) SPG_P1X(true, 8); else if (J == 4) SPG_P1X(true, 4); else SPG_P1X(true, 2);
+    } else {
+      if (J == 8) SPG_P1X(false, 8); else if (J == 4) SPG_P1X(false, 4); else SPG_P1X(false, 2);
+    }
+#undef SPG_P1X
+    SPG_HIP(ctx, hipGetLastError());
+    return eval_reduce_finish(ctx, out3);
+  }
   if (!fold) {
     // B, C, D lo+hi per domain point, plus the three eq factor tables once
     // Fq products per point: the eq factor at lo and hi (x rounds share Ap Aq: 3; else 4), then A (B C - D) at 3 points

@@ -73,6 +73,8 @@ struct Fold2 {
 };
 
 // one phase-1 round: (e0, e2, e3) of eq(p,q,x) * (B*C - D)  (src/sumcheck.rs:1173-1245)
+// most workgroups a round evaluation launches (its partials buffer holds 3 scalars per workgroup)
+constexpr int kScGridMax = 4096;
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
                 const Fq* Ax, Fq* B, Fq* C, Fq* D, Fq* partials, Fq* out3, const FoldPlan* fold = nullptr);

@@ -56,3 +56,4 @@ GPU_SNARK_CASES = {
     "mem_both_b2_x256_q32": dict(num_blocks=2, log_cons=8, log_proofs=5, num_vars=256, phy_ops=3, vir_ops=2,
                                  init_phy=20, init_vir=7, niu=5),
 }
+ALL_R1CS = dict(CASES, **GPU_CASES)

@@ -140,3 +140,43 @@ def test_r1cs_verify(ctx, r1cs_gens, case):
         ok, _, _ = spg.r1cs_verify(*args[:6], other, wl.max_num_cons, workload.to_mont_limbs(bound),
                                    spg.Transcript(b"r1cs_test"), proof)
         assert not ok
+
+
+@pytest.mark.parametrize("case,env", [
+    ("p2_x1024_q64", {"SPG_SC_QUAD_MAX": "0"}),                       # row-factored x rounds, J = 8, 4, 2
+    ("p2_x1024_q64", {"SPG_SC_QUAD_MAX": "0", "SPG_P1_ROWS": "0"}),   # the per-point thread form throughout
+    ("p8_x256_q32_shared", {"SPG_SC_QUAD_MAX": "0"}),                 # shared matrix, J = 2 at round 0
+    ("p2_x256_2secs", {"SPG_SC_QUAD_MAX": "0", "SPG_SC_FUSE": "0"}),  # row form without the fused folds
+])
+def test_r1cs_thread_form_rounds(oracle, case, env):
+    """the thread-per-point phase-1 evaluations (k_phase1_eval, and k_phase1_eval_x's row-factored x rounds: one eq
+    factor Ap Aq per row and J points per lane) at sizes the oracle proves in seconds, forced by SPG_SC_QUAD_MAX=0 in
+    a fresh process: the oracle's bytes"""
+    import os
+    import subprocess
+    import sys
+
+    import workload
+
+    nc, npf, nws, shared = ALL[case]
+    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+    seed = workload.tape_seed()
+    ref, _ = oracle.r1cs_prove(wl, seed, gens_label=GENS_LABEL, gens_num_vars=GENS_NV)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, hashlib; sys.path[:0] = [%r, %r]\n"
+        "import spg, workload\n"
+        "from r1cs_cases import ALL_R1CS\n"
+        "from test_gpu_r1cs import gpu_prove, GENS_LABEL, GENS_NV\n"
+        "ctx = spg.Context(0)\n"
+        "nc, npf, nws, shared = ALL_R1CS[%r]\n"
+        "wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)\n"
+        "p, _ = gpu_prove(ctx, spg.R1CSGens(ctx, GENS_LABEL, GENS_NV), wl, workload.tape_seed())\n"
+        "print(hashlib.sha256(p).hexdigest())\n"
+    ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "tests"), case)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import hashlib
+
+    assert out.stdout.split()[-1] == hashlib.sha256(ref).hexdigest()
