@@ -26,6 +26,12 @@ case "$1" in
       --memory-copy-trace --output-format csv -d "$R/gpurun_out/kt_$2" -o kt -- python3 "$R/scripts/trace_snark.py" \
       > /dev/null 2> "$R/gpurun_out/kt_$2.err") || exit 1
     ls gpurun_out/kt_$2 ;;
+  gapsb)  # kernel trace + lap events of bench.py $BENCH_ARGS (no profile pass lines needed: --steps 3)
+    export TMPDIR=/tmp
+    (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+      -d "$R/gpurun_out/kt_$2" -o kt -- python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --extras none \
+      $BENCH_ARGS > /dev/null 2> "$R/gpurun_out/kt_$2.err") || exit 1
+    ls gpurun_out/kt_$2 ;;
   gaps)
     export TMPDIR=/tmp
     (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 TRACE_REPS=6 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \

@@ -1143,6 +1143,8 @@ int Prover::run_inner(Laps& lp) {
     std::vector<BoundJob> jobs;
     size_t o = 0, totL = 0, totP = 0;
     bool all_mine = true;
+    std::vector<FqV> rr_of(polys.size());  // each polynomial's right point; R = eq(rr) once per distinct point, below
+    size_t pk = 0;
     for (auto& pr : polys) {
       size_t lnp = lg2(pr.np), lni = lg2(pr.ni);
       FqV r(rq.begin() + (nq - lnp), rq.end());
@@ -1155,7 +1157,7 @@ int Prover::run_inner(Laps& lp) {
       size_t nv = r.size(), ln = nv / 2;
       FqV rl(r.begin(), r.begin() + ln), rr(r.begin() + ln, r.end());
       size_t Ls = (size_t)1 << ln, Rs = (size_t)1 << (nv - ln);
-      pr.R = eq_evals_host(rr);
+      rr_of[pk++] = std::move(rr);
       if (pr.mine) {
         size_t S = std::min<size_t>(Ls, 32);  // 32 partial rows: short column sums
         const size_t chunk = (Ls + S - 1) / S;
@@ -1167,6 +1169,21 @@ int Prover::run_inner(Laps& lp) {
         all_mine = false;
       }
       o += Rs;
+    }
+    // the host eq tables of the distinct right points (instances of one shape share theirs), on the pool
+    {
+      std::vector<size_t> uniq, at(polys.size());
+      for (size_t k = 0; k < polys.size(); k++) {
+        size_t u = 0;
+        while (u < uniq.size() && !(rr_of[uniq[u]].size() == rr_of[k].size() &&
+                                    memcmp(rr_of[uniq[u]].data(), rr_of[k].data(), rr_of[k].size() * sizeof(Fq)) == 0))
+          u++;
+        if (u == uniq.size()) uniq.push_back(k);
+        at[k] = u;
+      }
+      std::vector<FqV> tabs(uniq.size());
+      pool().parallel_for((int)uniq.size(), [&](int u) { tabs[u] = eq_evals_host(rr_of[uniq[u]]); });
+      for (size_t k = 0; k < polys.size(); k++) polys[k].R = tabs[at[k]];
     }
     if (!jobs.empty()) {
       Fq* dL = (Fq*)ws_get(ctx, WS_L, totL * sizeof(Fq) + 64);
@@ -1235,13 +1252,18 @@ int Prover::run_inner(Laps& lp) {
   {
     size_t k = 0;
     std::vector<CJob> cj;  // every evaluation's commitment in one host burst
+    // <LZ, R> of every polynomial, one pool task each
+    pool().parallel_for((int)polys.size(), [&](int q) {
+      PolyRef& pr = polys[q];
+      Fq ev = fq_zero();
+      for (size_t m = 0; m < pr.Rs; m++) ev = fq_add(ev, fq_mul(pr.LZ[m], pr.R[m]));
+      pr.ev = ev;
+    });
     for (size_t i = 0; i < nws; i++) {
       eval_list.push_back({});
       for (size_t p = 0; p < wit.num_proofs[i].size(); p++, k++) {
         PolyRef& pr = polys[k];
-        Fq ev = fq_zero();
-        for (size_t m = 0; m < pr.Rs; m++) ev = fq_add(ev, fq_mul(pr.LZ[m], pr.R[m]));
-        pr.ev = ev;
+        const Fq ev = pr.ev;
         size_t lni = lg2(pr.ni);
         eval_list[i].push_back(pr.ni >= Y ? ev : fq_mul(ev, ry_factors[ny - lni]));
         cj.push_back(CJob(g.gens_1, {ev}, fq_zero()));
