@@ -9,6 +9,12 @@ static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "keccak lanes assume a 
 
 namespace spg {
 
+// permutations run on this thread (SPG_TRACE=2 prints the count per SNARK::prove)
+inline uint64_t& keccak_count() {
+  static thread_local uint64_t n = 0;
+  return n;
+}
+
 struct KeccakState {
   uint64_t a[25];
 
@@ -27,6 +33,7 @@ struct KeccakState {
     // rho offset of lane x + 5 y
     static constexpr unsigned rho[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
                                          25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+    keccak_count()++;
     uint64_t A[25], B[25], C[5], D[5];
     for (int i = 0; i < 25; i++) A[i] = a[i];
     for (int r = 0; r < 24; r++) {

@@ -1390,9 +1390,11 @@ static int spg_snark_prove_impl(spg_ctx* ctx, spg_snark_comp* block, spg_snark_c
     fprintf(stderr, "[spg] sigma-protocol commitments: %zu calls, %zu commitments, %.0f us on the host\n",
                     g_commit_stats.calls, g_commit_stats.points, g_commit_stats.us);
     g_commit_stats = CommitStats();
-    static uint64_t bursts0 = 0;
-    fprintf(stderr, "[spg] host pool bursts: %llu\n", (unsigned long long)(pool().bursts() - bursts0));
+    static uint64_t bursts0 = 0, keccak0 = 0;
+    fprintf(stderr, "[spg] host pool bursts: %llu, keccak-f permutations on this thread: %llu\n",
+            (unsigned long long)(pool().bursts() - bursts0), (unsigned long long)(keccak_count() - keccak0));
     bursts0 = pool().bursts();
+    keccak0 = keccak_count();
   }
   if (getenv("SPG_COPY_TRACE") && atoi(getenv("SPG_COPY_TRACE"))) print_copy_counts();
   *proof_len = w.out.size();
