@@ -130,7 +130,18 @@ class Env:
         if self.world > 1:
             import torch.distributed as dist
 
-            dist.init_process_group(self.backend)
+            # the gloo library reports its connections on stdout; the bench's stdout carries one JSON line only, so
+            # the process group comes up (and connects, at its first barrier) with fd 1 pointed at stderr
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group(self.backend)
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
         ndev = torch.cuda.device_count()
         self.gpu = self.local % ndev if ndev else self.local  # ranks share a GPU only in rehearsals
