@@ -485,7 +485,8 @@ def main_snark(a):
                        "constraints_per_block": 1 << a.log_cons, "executions_per_block": 1 << a.log_proofs,
                        "constraints_per_gpu": N, "num_vars": wl.num_vars, "num_ios": wl.num_ios,
                        "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{env.world}"},
-            "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v, "roofline_fq": roofline_fq(prof),
+            "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
+            "roofline_fq": roofline_fq(prof, a.traffic or TRAFFIC["snark"]),
             "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact,
             "proof_sha256": sorted(proofs)[0][:16],
             "device_busy_ms_per_step": round(prof.busy_us / a.steps / 1e3, 3),
