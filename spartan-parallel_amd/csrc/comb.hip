@@ -24,6 +24,7 @@
 
 #include "ctx.hpp"
 #include "hcurve.hpp"
+#include "hvec.hpp"
 #include "hpool.hpp"
 #include "lds.hpp"
 #include "quad.hpp"
@@ -401,11 +402,20 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
   }
   SPG_HIP(ctx, hipGetLastError());
   SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  // the S parts over the pool: contiguous chunks, then their sums on this thread
-  const int K = (int)std::max<size_t>(1, std::min<size_t>(S / 16, (size_t)pool().size() + 1));
+  // the S parts over the pool: contiguous chunks (8-lane IFMA sums where the CPU has them), then their sums here
+  static const bool vec = h::ifma_on() && !(getenv("SPG_VEC_MIN") && atol(getenv("SPG_VEC_MIN")) == 0);
+  const int K = (int)std::max<size_t>(1, std::min<size_t>(S / (vec ? 64 : 16), (size_t)pool().size() + 1));
   std::vector<h::HExt> part(K);
   pool().parallel_for(K, [&](int c) {
     const size_t lo = S * c / K, hi = S * (c + 1) / K;
+    for (const uint8_t* q = (const uint8_t*)(parts + lo); q < (const uint8_t*)(parts + hi); q += 64)
+      __builtin_prefetch(q, 0, 0);
+    if (vec && hi - lo >= 16) {
+      std::vector<h::HExt> hx(hi - lo);
+      for (size_t i = lo; i < hi; i++) hx[i - lo] = h::hext_from_dev(parts[i]);
+      part[c] = h::ext_sum8(hx.data(), hi - lo);
+      return;
+    }
     h::HExt acc = h::hext_from_dev(parts[lo]);
     for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(parts[i]));
     part[c] = acc;
