@@ -204,6 +204,73 @@ static void run_pair(int nt, int log_len, int nf, Fq* cin, Fq* cout, Triple* dtr
          (p[3] - p[2]) * 0.01, K == 1 ? (p[4] - p[3]) * 0.01 : 0.0);
 }
 
+// the tripled launch (k_layer_triple) of rounds (len, len / 2, len / 4), the prover's workgroup choice
+static void run_triple(int nt, int log_len, int nf, Fq* cin, Fq* cout, Triple* dtr, Fq* dcoef, Fq* part, unsigned* ctr,
+                       uint32_t* mb_dev, volatile uint32_t* mb_host, unsigned long long* probe) {
+  TripleArgs P;
+  P.tr = dtr;
+  P.coeff = dcoef;
+  P.nt = nt;
+  P.log_len = log_len;
+  P.nf = nf;
+  for (int i = 0; i < 8; i++) P.r1.l[i] = 0x01234567u * (i + 3);
+  P.r1.l[7] = 0x01000000u;
+  P.r2 = P.r3 = P.r12 = P.r13 = P.r23 = P.r123 = P.r1;
+  P.cin = cin;
+  P.cout = cout;
+  P.partials = part;
+  P.counter = ctr;
+  P.mb = mb_dev;
+  P.ends = 0;
+  P.probe = nullptr;
+  const long E = (long)nt << (log_len - 2);
+  const int BS = E <= 1 ? 64 : 256;
+  const unsigned K = (unsigned)((E + BS / 64 - 1) / (BS / 64));
+  auto launch = [&]() {
+    if (BS == 64)
+      hipLaunchKernelGGL(k_layer_triple<64>, dim3(K), dim3(64), 0, 0, P);
+    else
+      hipLaunchKernelGGL(k_layer_triple<256>, dim3(K), dim3(256), 0, 0, P);
+  };
+  uint32_t seq = 90000;
+  for (int w = 0; w < 3; w++) {
+    P.seq = ++seq;
+    launch();
+  }
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int R = 20;
+  hipEventRecord(e0, 0);
+  for (int i = 0; i < R; i++) {
+    P.seq = ++seq;
+    launch();
+  }
+  hipEventRecord(e1, 0);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < R; i++) {
+    P.seq = ++seq;
+    launch();
+    while (__atomic_load_n(mb_host, __ATOMIC_ACQUIRE) != P.seq) {
+    }
+  }
+  const double rt = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / R;
+  hipDeviceSynchronize();
+  P.seq = ++seq;
+  P.probe = probe;
+  launch();
+  hipDeviceSynchronize();
+  unsigned long long p[8];
+  hipMemcpy(p, probe, 64, hipMemcpyDeviceToHost);
+  printf("triple nt=%2d len=%5d nf=%d K=%4u BS=%4d: event %.1f us/launch, launch+mailbox round trip %.1f us | block 0: "
+         "fold %.2f, grid %.2f, products %.2f, post %.2f us\n",
+         nt, 1 << log_len, nf, K, BS, ms * 1000 / R, rt, (p[1] - p[0]) * 0.01, (p[2] - p[1]) * 0.01,
+         (p[3] - p[2]) * 0.01, K == 1 ? (p[4] - p[3]) * 0.01 : 0.0);
+}
+
 int main() {
   const int NT = 32, MAXL = 4096;
   Fq *vec, *cin, *cout, *dcoef, *part;
@@ -239,6 +306,21 @@ int main() {
     run_armed<256>(6, 5, cin, cout, dtr, dcoef, mbd, (volatile uint32_t*)mbh, dbd, (volatile uint32_t*)dbh);
   }
   if (getenv("ARMED_ONLY")) return 0;
+  if (getenv("TRIPLE_ONLY")) {  // a triple against the pair at the same round j (len) and at len / 2
+    const int shapes[][2] = {{24, 2}, {24, 3}, {24, 4}, {24, 5}, {24, 6}, {4, 2}, {4, 4}, {4, 6}, {4, 8}};
+    for (auto& sh : shapes) {
+      const int nt = sh[0], lg = sh[1];
+      for (int nf = 1; nf <= 3; nf++)
+        run_triple(nt, lg, nf, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
+      for (int l = lg; l >= lg - 1 && l >= 1; l--) {
+        if (16L * nt * (1L << (l - 1)) <= 64)
+          run_pair<64>(nt, l, 2, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
+        else
+          run_pair<256>(nt, l, 2, cin, cout, dtr, dcoef, part, ctr, mbd, (volatile uint32_t*)mbh, probe);
+      }
+    }
+    return 0;
+  }
   if (getenv("PAIR_ONLY")) {
     const int shapes[][2] = {{24, 1}, {24, 2}, {24, 4}, {24, 6}, {24, 8}, {4, 1}, {4, 4}, {4, 8}, {4, 10}};
     for (auto& sh : shapes) {

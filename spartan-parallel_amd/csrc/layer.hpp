@@ -477,6 +477,203 @@ __global__ void __launch_bounds__(BS) k_layer_pair(PairArgs A) {
   }
 }
 
+// ---- three rounds per launch ------------------------------------------------------------------------------------------
+// The pair argument one level further: with the 2 x 2 x 2 cube of element i < h = len / 4 (t: round j's variable, offset
+// len; s: round j + 1's, offset len / 2; u: round j + 2's, offset h), P(t, s, u) trilinear in the eight corners and
+// F = k A B C, round j's evaluation at X is the sum of F(X, s, u) over s, u in {0, 1}, round j + 1's at Y the cubic
+// t -> F(t, Y, 0) + F(t, Y, 1) taken at t = r_j, and round j + 2's at Z the bicubic (t, s) -> F(t, s, Z) taken at
+// (r_j, r_j+1). So one launch posts F on the 4 x 4 x 4 grid (lane g = t + 4 s + 16 u; (1, 1, 1) is not needed) and
+// the host draws r_j, r_j+1 and r_j+2 with no device round trip between them. A wave per element:
+//   fold: lanes g < 48 compute corner q = g % 24 (vector q >> 3, m = q & 7 = 4 t + 2 s + u) with up to three pending
+//     folds (nf; the previous launch's r1, r2, r3 bound in that order, r1 on the top variable) in the multilinear
+//     form V_000 + sum_S r_S D_S (D_S: the differences of the 2^nf entries, r_S the products the host forms), half of
+//     the products in lane g, half in lane g + 24 (the same instruction stream on selected operands), the halves
+//     meeting in LDS; the corner goes back in place like the pair's; lane 48 loads the coefficient
+//   points: the grid by tensor extension through LDS, one small-integer lerp per value: u (48 values: 16 per vector),
+//     then s (96), then t (192: three per lane), instead of 7 lerps per value
+// Sums over the workgroup's waves in LDS, over the workgroups by sc1 partials and a ticket (as the pair).
+// ends (a layer's last triple, h = 1): the corner of q is also posted as scalar 64 + 24 c + q.
+struct TripleArgs {
+  const Triple* tr;
+  const Fq* coeff;
+  int nt;
+  int log_len;  // round j's half length len = 2^log_len (>= 2: h = len / 4 >= 1)
+  int nf;       // pending folds 0..3
+  Fq r1, r2, r3, r12, r13, r23, r123;
+  const Fq* cin;
+  Fq* cout;
+  Fq* partials;  // 64 per workgroup
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq;
+  int ends;
+  unsigned long long* probe;
+};
+__device__ __forceinline__ Fq fq_lerp_small(const Fq& a, const Fq& b, int n) { return fq_add(a, fq_small(fq_sub(b, a), n)); }
+__device__ __forceinline__ Fq lds_fq(const uint32_t* p) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = p[i];
+  return r;
+}
+__device__ __forceinline__ void lds_put(uint32_t* p, const Fq& v) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = v.l[i];
+}
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_triple(TripleArgs A) {
+  constexpr int NW = BS / 64;
+  // per wave: corners (24) + coefficient, the folds' second halves (24), the u-extension (48), the s-extension (96)
+  __shared__ uint32_t cs[NW][25][8], xs[NW][24][8], us[NW][48][8], ss[NW][96][8];
+  __shared__ uint32_t es[NW > 1 ? NW : 1][64][8];
+  __shared__ bool last;
+  const int t = threadIdx.x, g = t & 63, wv = t >> 6;
+  unsigned long long* pr = A.probe ? A.probe + 8 * blockIdx.x : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
+  const int len = 1 << A.log_len, h = len >> 2;
+  const long total = (long)A.nt << (A.log_len - 2);
+  const long u = (long)blockIdx.x * NW + wv;  // this wave's element (waves past the end contribute zero)
+  const bool live = u < total;
+  const int c = live ? (int)(u >> (A.log_len - 2)) : 0, i = (int)(u & (h - 1));
+  const int q = g < 24 ? g : g - 24, part = g < 24 ? 0 : 1;  // lanes 0..47: corner q, half `part`
+  const int v = q >> 3, m = q & 7, k = i + m * h;
+  const int L2 = 2 * len;  // the folded vector's length: the pending folds' innermost stride
+  Triple x;
+  const Fq* src = nullptr;
+  Fq w = fq_zero();
+  if (live && g < 48) {
+    x = A.tr[c];
+    src = v == 0 ? x.A : (v == 1 ? x.B : (x.C ? x.C : A.cin));
+    if (A.nf == 0) {
+      if (!part) w = src[k];
+    } else if (A.nf == 1) {
+      if (!part) {
+        const Fq a = src[k];
+        w = fq_add(a, fq_mul(A.r1, fq_sub(src[k + L2], a)));
+      }
+    } else if (A.nf == 2) {  // V[2 a + b]: a bound by r1 (offset 2 L2), b by r2
+      const Fq v00 = src[k], v01 = src[k + L2], v10 = src[k + 2 * L2], v11 = src[k + 3 * L2];
+      const Fq d1 = fq_sub(v10, v00), d2 = fq_sub(v01, v00), d12 = fq_sub(fq_sub(v11, v10), d2);
+      const Fq p0 = fq_mul(fq_sel(part, A.r12, A.r1), fq_sel(part, d12, d1));
+      const Fq p1 = fq_mul(fq_sel(part, fq_zero(), A.r2), d2);
+      w = fq_add(fq_sel(part, fq_zero(), v00), fq_add(p0, p1));
+    } else {  // V[4 a + 2 b + c]: a by r1 (offset 4 L2), b by r2, c by r3
+      Fq V[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) V[j] = src[k + j * L2];
+      // the multilinear coefficients D_S (butterflies over the three bits)
+#pragma unroll
+      for (int bit = 1; bit < 8; bit <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (j & bit) V[j] = fq_sub(V[j], V[j ^ bit]);
+      // V[1] = D3, V[2] = D2, V[3] = D23, V[4] = D1, V[5] = D13, V[6] = D12, V[7] = D123
+      const Fq p0 = fq_mul(fq_sel(part, A.r13, A.r1), fq_sel(part, V[5], V[4]));
+      const Fq p1 = fq_mul(fq_sel(part, A.r23, A.r2), fq_sel(part, V[3], V[2]));
+      const Fq p2 = fq_mul(fq_sel(part, A.r123, A.r3), fq_sel(part, V[7], V[1]));
+      const Fq p3 = fq_mul(fq_sel(part, fq_zero(), A.r12), V[6]);
+      w = fq_add(fq_add(fq_sel(part, fq_zero(), V[0]), p0), fq_add(p1, fq_add(p2, p3)));
+    }
+  }
+  if (A.nf >= 2) {  // the second halves join the first
+    if (live && part && g < 48) lds_put(xs[wv][q], w);
+    __syncthreads();
+    if (live && !part) w = fq_add(w, lds_fq(xs[wv][q]));
+  }
+  if (live && g < 24) {
+    if (A.nf > 0) {
+      Fq* dst = v == 0 ? x.A : (v == 1 ? x.B : (x.C ? x.C : (c == 0 ? A.cout : nullptr)));
+      if (dst) dst[k] = w;
+    }
+    if (A.ends) host_put(A.mb + 8 + 8 * (64 + 24 * c + g), w);
+    lds_put(cs[wv][g], w);
+  } else if (live && g == 48) {
+    lds_put(cs[wv][24], A.coeff[c]);
+  }
+  if (pr && t == 0) pr[1] = wall_clock64();
+  __syncthreads();
+  // u: value (vector g >> 4, t' = g & 1, s' = (g >> 1) & 1, u = (g >> 2) & 3) from corners 4 t' + 2 s' + {0, 1}
+  if (g < 48) {
+    const int vv = g >> 4, tt = g & 1, sp = (g >> 1) & 1, uu = (g >> 2) & 3, b = 8 * vv + 4 * tt + 2 * sp;
+    lds_put(us[wv][g], fq_lerp_small(lds_fq(cs[wv][b]), lds_fq(cs[wv][b + 1]), uu));
+  }
+  __syncthreads();
+  // s: value (vector idx >> 5, t' = idx & 1, s = (idx >> 1) & 3, u = (idx >> 3) & 3), idx = g and g + 64 (< 96)
+#pragma unroll
+  for (int rep = 0; rep < 2; rep++) {
+    const int idx = g + 64 * rep;
+    if (idx < 96) {
+      const int vv = idx >> 5, tt = idx & 1, sv = (idx >> 1) & 3, uu = (idx >> 3) & 3;
+      const int b = 16 * vv + tt + 4 * uu;  // us index of (vv, tt, s' = 0, uu); s' = 1 is b + 2
+      lds_put(ss[wv][idx], fq_lerp_small(lds_fq(us[wv][b]), lds_fq(us[wv][b + 2]), sv));
+    }
+  }
+  __syncthreads();
+  if (pr && t == 0) pr[2] = wall_clock64();
+  // t: this lane's point (t, s, u) = (g & 3, (g >> 2) & 3, g >> 4) for the three vectors, then k A B C
+  Fq e = fq_zero();
+  if (live) {
+    const int tt = g & 3, b = 2 * ((g >> 2) & 3) + 8 * (g >> 4);  // ss index of (v, t' = 0, s, u), minus 32 v
+    const Fq av = fq_lerp_small(lds_fq(ss[wv][b]), lds_fq(ss[wv][b + 1]), tt);
+    const Fq bv = fq_lerp_small(lds_fq(ss[wv][32 + b]), lds_fq(ss[wv][33 + b]), tt);
+    const Fq cv = fq_lerp_small(lds_fq(ss[wv][64 + b]), lds_fq(ss[wv][65 + b]), tt);
+    e = fq_mul(fq_mul(av, bv), fq_mul(lds_fq(cs[wv][24]), cv));
+  }
+  if (A.ends) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the corners reach the host before any ticket / post
+  if (pr && t == 0) pr[3] = wall_clock64();
+  if (NW > 1) {
+    lds_put(es[wv][g], e);
+    __syncthreads();
+    if (wv == 0)
+      for (int o = 1; o < NW; o++) e = fq_add(e, lds_fq(es[o][g]));
+  }
+  if (gridDim.x == 1) {  // wave 0 posts the 64 point sums, then lane 0 the sequence number
+    if (t < 64) {
+      host_put(A.mb + 8 + 8 * t, e);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (pr) pr[4] = wall_clock64();
+    }
+    return;
+  }
+  if (t < 64) st_sc1(&A.partials[64 * blockIdx.x + t], e);
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(A.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  // the last workgroup: wave w adds the partials of workgroups w, w + NW, ..., four loads in flight at a time
+  Fq s0 = fq_zero(), s1 = fq_zero();
+  unsigned j = wv;
+  for (; j + 3 * NW < gridDim.x; j += 4 * NW) {
+    const Fq a0 = ld_sc1(&A.partials[64 * j + g]), a1 = ld_sc1(&A.partials[64 * (j + NW) + g]);
+    const Fq a2 = ld_sc1(&A.partials[64 * (j + 2 * NW) + g]), a3 = ld_sc1(&A.partials[64 * (j + 3 * NW) + g]);
+    s0 = fq_add(s0, fq_add(a0, a1));
+    s1 = fq_add(s1, fq_add(a2, a3));
+  }
+  for (; j < gridDim.x; j += NW) s0 = fq_add(s0, ld_sc1(&A.partials[64 * j + g]));
+  Fq sum = fq_add(s0, s1);
+  if (NW > 1) {
+    lds_put(es[wv][g], sum);
+    __syncthreads();
+    if (wv == 0)
+      for (int o = 1; o < NW; o++) sum = fq_add(sum, lds_fq(es[o][g]));
+  }
+  if (t < 64) {
+    host_put(A.mb + 8 + 8 * t, sum);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ---- persistent form: the remaining rounds of a layer in one launch ------------------------------------------------
 // A launched round costs a host launch (~4 us) and a doorbell-to-first-wave delay (~5 us) on top of its work, and the
 // layer rounds are transcript-sequential. Here the workgroups stay resident over the rounds: after posting round k's

@@ -19,6 +19,7 @@
 //                    two halves of v_k, and v_{k+1}[i] = v_k[i] * v_k[i + |v_k|/2].
 // All O(N) work stays in HBM; the host runs the transcript and one UniPoly per sumcheck round.
 #include <algorithm>
+#include <array>
 
 #include <hipcub/hipcub.hpp>
 
@@ -742,9 +743,12 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
     // launch applies two, and once a layer's rounds pair up they pair up to the layer's end
     bool pend2 = false;
     Fq r_pend2 = fq_zero();
+    // after a tripled launch (k_layer_triple): a third, r_pend3; only a triple follows it
+    bool pend3 = false;
+    Fq r_pend3 = fq_zero();
     // A[0], B[0], C[0] of every triple (after the pending fold, if any), by mailbox
     auto close = [&](FqV& fin) -> int {
-      if (pend2) return set_err(ctx, SPG_E_ARG, "layer close after a paired round");  // (the last pair posts its ends)
+      if (pend2 || pend3) return set_err(ctx, SPG_E_ARG, "layer close after a paired round");  // (the last pair posts its ends)
       fin.resize(3 * tr.size());
       KScope ks(ctx, "spark_layer_close");
       const uint32_t seq = ++ctx->mbox_seq;
@@ -854,14 +858,165 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       static const size_t persist_max = getenv("SPG_PERSIST_MAX") ? (size_t)atol(getenv("SPG_PERSIST_MAX")) : 4096;
       static const bool pair_on = !getenv("SPG_LAYER_PAIR") || atoi(getenv("SPG_LAYER_PAIR")) != 0;
       static const size_t pair_max = getenv("SPG_PAIR_MAX") ? (size_t)atol(getenv("SPG_PAIR_MAX")) : 4096;
+      static const bool triple_on = !getenv("SPG_LAYER_TRIPLE") || atoi(getenv("SPG_LAYER_TRIPLE")) != 0;
+      // elements (a wave each, four per workgroup) of a tripled launch: 64 partials per workgroup in `part`
+      static const size_t triple_max =
+          std::min<size_t>(getenv("SPG_TRIPLE_MAX") ? (size_t)atol(getenv("SPG_TRIPLE_MAX")) : 384, 384);
+      // relative wall of a launched single / paired / tripled round trip, for the launch plan below
+      static const std::vector<int> step_cost = [] {
+        std::vector<int> c = {18, 25, 30};
+        if (const char* e = getenv("SPG_STEP_COSTS")) sscanf(e, "%d,%d,%d", &c[0], &c[1], &c[2]);
+        return c;
+      }();
+      const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
+      const size_t nt_all = tr.size();
+      const bool multi = quad && !local && close_after && !(persist_on && ctx->nranks == 1);
+      // two rounds in one launch (k_layer_pair): small rounds of an unsharded layer, every element's 16 lanes within
+      // pair_max elements, the last pair's corners within the mailbox; three (k_layer_triple): a wave per element
+      // within triple_max elements, the last triple's corners within the mailbox
+      auto pair_ok = [&](size_t k) {
+        return pair_on && multi && k >= 2 && (nt_all << (k - 2)) <= std::min<size_t>(pair_max, 6144) &&
+               15 + 12 * nt_all <= kMboxScalars && ngroups * ((size_t)1 << (k - 1)) < wide_min;
+      };
+      auto triple_ok = [&](size_t k) {
+        return triple_on && multi && k >= 3 && (nt_all << (k - 3)) <= triple_max && 64 + 24 * nt_all <= kMboxScalars &&
+               ngroups * ((size_t)1 << (k - 1)) < wide_min;
+      };
+      // the launch plan: single rounds first, then pairs, then triples (a pair leaves two pending folds, which only
+      // a pair or a triple applies; a triple three, which only a triple applies), the cheapest by step_cost.
+      // Returns the rounds of the first launch from k rounds left in state mode (0: free, 1: after a pair, 2: after a
+      // triple), 0 when none finishes the layer.
+      auto plan = [&](size_t k, int mode) -> int {
+        const int inf = 1 << 28;
+        std::vector<std::array<int, 3>> best(k + 1), first(k + 1);
+        for (size_t j = 0; j <= k; j++)
+          for (int md = 0; md < 3; md++) {
+            int b = j == 0 ? 0 : inf, f = 0;
+            if (j >= 1 && md == 0 && best[j - 1][0] < inf && step_cost[0] + best[j - 1][0] < b)
+              b = step_cost[0] + best[j - 1][0], f = 1;
+            if (md <= 1 && pair_ok(j) && best[j - 2][1] < inf && step_cost[1] + best[j - 2][1] < b)
+              b = step_cost[1] + best[j - 2][1], f = 2;
+            if (triple_ok(j) && best[j - 3][2] < inf && step_cost[2] + best[j - 3][2] < b)
+              b = step_cost[2] + best[j - 3][2], f = 3;
+            best[j][md] = b;
+            first[j][md] = f;
+          }
+        return first[k][mode];
+      };
+      auto lagrange4 = [](const Fq& r, Fq L[4]) {  // the cubic Lagrange basis on 0..3 at r
+        static const Fq inv2 = fq_inv(fq_from_u64(2)), inv6 = fq_inv(fq_from_u64(6));
+        const Fq a0 = r, a1 = fq_sub(r, fq_one()), a2 = fq_sub(a1, fq_one()), a3 = fq_sub(a2, fq_one());
+        const Fq a01 = fq_mul(a0, a1), a23 = fq_mul(a2, a3);
+        L[0] = fq_neg(fq_mul(fq_mul(a1, a23), inv6));
+        L[1] = fq_mul(fq_mul(a0, a23), inv2);
+        L[2] = fq_neg(fq_mul(fq_mul(a01, a3), inv2));
+        L[3] = fq_mul(fq_mul(a01, a2), inv6);
+      };
       while (log_len > 0) {
-        const size_t ngroups = (nc ? 1 : 0) + (tr.size() - nc);  // product circuits share one thread per index
-        // two rounds in one launch (k_layer_pair): small rounds of an unsharded layer, an even number of them left
-        // (an odd count first runs one single round), every element's 16 lanes within pair_max elements, the last
-        // pair's corners within the mailbox
-        if (pair_on && quad && !local && close_after && log_len >= 2 && log_len % 2 == 0 &&
-            (tr.size() << (log_len - 2)) <= std::min<size_t>(pair_max, 6144) && 15 + 12 * tr.size() <= kMboxScalars &&
-            ngroups * ((size_t)1 << (log_len - 1)) < wide_min && !(persist_on && ctx->nranks == 1)) {
+        const int step = plan(log_len, pend3 ? 2 : (pend2 ? 1 : 0));
+        if (step == 0) return set_err(ctx, SPG_E_ARG, "layer rounds: no launch plan");
+        if (step == 3) {
+          const int lgj = (int)log_len - 1;  // round j's half length 2^lgj; h = 2^(lgj - 2) elements per vector
+          log_len -= 3;
+          const size_t nt = tr.size(), h = (size_t)1 << (lgj - 2), E = nt * h;
+          const int BSt = E <= 1 ? 64 : 256;
+          const unsigned Kt = (unsigned)((E + BSt / 64 - 1) / (BSt / 64));
+          const bool ends = log_len == 0;  // the layer's last triple posts every vector's 2 x 2 x 2 corners
+          const int nf = pend3 ? 3 : (pend2 ? 2 : (pending ? 1 : 0));
+          TripleArgs P;
+          P.tr = dtr;
+          P.coeff = dcoef;
+          P.nt = (int)nt;
+          P.log_len = lgj;
+          P.nf = nf;
+          P.r1 = r_pend;
+          P.r2 = r_pend2;
+          P.r3 = r_pend3;
+          P.r12 = fq_mul(r_pend, r_pend2);
+          P.r13 = fq_mul(r_pend, r_pend3);
+          P.r23 = fq_mul(r_pend2, r_pend3);
+          P.r123 = fq_mul(P.r12, r_pend3);
+          P.cin = cbuf[cur];
+          P.cout = cbuf[cur ^ 1];
+          P.partials = part;
+          P.counter = ctx->d_counter;
+          P.mb = ctx->d_mbox;
+          P.seq = ++ctx->mbox_seq;
+          P.ends = ends ? 1 : 0;
+          P.probe = nullptr;
+          {
+            // algorithmic bytes: per distinct vector and element, 8 corners from 8 2^nf entries, written back when folded
+            const double per = 32.0 * (8.0 * (double)(1 << nf) + (nf ? 8.0 : 0.0));
+            // Fq products per element: the 24 corners folded (2^nf - 1 each), 64 points x 3
+            KScope ks(ctx, "spark_layer_triple", per * (double)h * (double)(2 * nt + ngroups), 0.0,
+                      (double)nt * (double)h * (192.0 + 24.0 * (double)((1 << nf) - 1)));
+            if (BSt == 64)
+              hipLaunchKernelGGL(k_layer_triple<64>, dim3(Kt), dim3(64), 0, s, P);
+            else
+              hipLaunchKernelGGL(k_layer_triple<256>, dim3(Kt), dim3(256), 0, s, P);
+          }
+          if (nf) cur ^= 1;
+          FqV ev(64 + (ends ? 24 * nt : 0));  // F(t, s, u) = ev[t + 4 s + 16 u], then the corners
+          const hipError_t le = hipGetLastError();
+          lp.lap(ends ? "triple_launch_end" : "triple_launch");
+          const int rc2 = le != hipSuccess ? set_err(ctx, SPG_E_HIP, std::string("layer triple: ") + hipGetErrorString(le))
+                                           : mbox_wait(ctx, P.seq, ev.data(), (int)ev.size());
+          if (rc2) return rc2;
+          lp.lap(ends ? "triple_wait_end" : "triple_wait");
+          // round j: F(X, s, u) over s, u in {0, 1} at X = 0, 2, 3
+          Fq ej[3];
+          for (int xi = 0; xi < 3; xi++) {
+            const int X = xi == 0 ? 0 : xi + 1;
+            ej[xi] = fq_add(fq_add(ev[X], ev[X + 4]), fq_add(ev[X + 16], ev[X + 20]));
+          }
+          const Fq rj = host_round(ej);
+          Fq L[4], M[4];
+          lagrange4(rj, L);
+          // round j + 1: t -> F(t, Y, 0) + F(t, Y, 1) at t = r_j, Y = 0, 2, 3
+          Fq ej1[3];
+          for (int yi = 0; yi < 3; yi++) {
+            const int Y = yi == 0 ? 0 : yi + 1;
+            Fq acc = fq_zero();
+            for (int a = 0; a < 4; a++) acc = fq_add(acc, fq_mul(L[a], fq_add(ev[a + 4 * Y], ev[a + 4 * Y + 16])));
+            ej1[yi] = acc;
+          }
+          const Fq rj1 = host_round(ej1);
+          lagrange4(rj1, M);
+          // round j + 2: (t, s) -> F(t, s, Z) at (r_j, r_j+1), Z = 0, 2, 3
+          Fq ej2[3];
+          for (int zi = 0; zi < 3; zi++) {
+            const int Z = zi == 0 ? 0 : zi + 1;
+            Fq acc = fq_zero();
+            for (int b = 0; b < 4; b++) {
+              Fq row = fq_zero();
+              for (int a = 0; a < 4; a++) row = fq_add(row, fq_mul(L[a], ev[a + 4 * b + 16 * Z]));
+              acc = fq_add(acc, fq_mul(M[b], row));
+            }
+            ej2[zi] = acc;
+          }
+          const Fq rj2 = host_round(ej2);
+          lp.lap("triple_host");
+          if (ends) {  // the 2 x 2 x 2 cube of every vector folded at (r_j, r_j+1, r_j+2): the layer's final claims
+            fin->resize(3 * nt);
+            for (size_t c = 0; c < 3 * nt; c++) {
+              const Fq* w = &ev[64 + 8 * c];  // corner m = 4 t + 2 s + u of vector c % 3 of triple c / 3
+              Fq q[4];
+              for (int j = 0; j < 4; j++) q[j] = fq_add(w[j], fq_mul(rj, fq_sub(w[j + 4], w[j])));
+              const Fq y0 = fq_add(q[0], fq_mul(rj1, fq_sub(q[2], q[0]))), y1 = fq_add(q[1], fq_mul(rj1, fq_sub(q[3], q[1])));
+              (*fin)[c] = fq_add(y0, fq_mul(rj2, fq_sub(y1, y0)));
+            }
+            pending = pend2 = pend3 = false;
+            lp.lap("triple_fin");
+            return 0;
+          }
+          pending = pend2 = pend3 = true;
+          r_pend = rj;
+          r_pend2 = rj1;
+          r_pend3 = rj2;
+          continue;
+        }
+        if (step == 2) {
+          if (pend3) return set_err(ctx, SPG_E_ARG, "paired layer round after a tripled one");
           const int lgj = (int)log_len - 1;  // round j's half length 2^lgj; round j + 1's 2^(lgj - 1)
           log_len -= 2;
           const size_t nt = tr.size(), h = (size_t)1 << (lgj - 1), lanes = 16 * nt * h;
@@ -910,11 +1065,8 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
           const Fq ej[3] = {fq_add(ev[0], ev[12]), fq_add(ev[2], ev[13]), fq_add(ev[3], ev[14])};
           const Fq rj = host_round(ej);
           // round j + 1: the cubics t -> F(t, Y) through t = 0..3 (lines Y = 0, 2, 3) at t = r_j
-          static const Fq inv2 = fq_inv(fq_from_u64(2)), inv6 = fq_inv(fq_from_u64(6));
-          const Fq a0 = rj, a1 = fq_sub(rj, fq_one()), a2 = fq_sub(a1, fq_one()), a3 = fq_sub(a2, fq_one());
-          const Fq a01 = fq_mul(a0, a1), a23 = fq_mul(a2, a3);
-          const Fq L[4] = {fq_neg(fq_mul(fq_mul(a1, a23), inv6)), fq_mul(fq_mul(a0, a23), inv2),
-                           fq_neg(fq_mul(fq_mul(a01, a3), inv2)), fq_mul(fq_mul(a01, a2), inv6)};
+          Fq L[4];
+          lagrange4(rj, L);
           Fq ej1[3];
           for (int y = 0; y < 3; y++) {
             Fq acc = fq_zero();
@@ -939,7 +1091,7 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
           r_pend2 = rj1;
           continue;
         }
-        if (pend2) return set_err(ctx, SPG_E_ARG, "single layer round after a paired one");
+        if (pend2 || pend3) return set_err(ctx, SPG_E_ARG, "single layer round after a paired one");
         // every remaining round is a quad round of at most persist_max elements: one persistent launch for them all
         // (one process per GPU only: processes sharing a GPU time-slice its queues, and a resident loop could then
         // wait out its timeout while descheduled)

@@ -103,6 +103,9 @@ ROUND_FORMS = {
     "layer_single_rounds": {"SPG_LAYER_PAIR": "0"},
     "layer_pairs_small_wgs": {"SPG_PAIR_BS": "64"},
     "layer_pairs_everywhere": {"SPG_PAIR_MAX": "6144", "SPG_WIDE_MIN": str(1 << 40)},
+    "layer_pairs_no_triples": {"SPG_LAYER_TRIPLE": "0"},
+    "layer_triples_everywhere": {"SPG_TRIPLE_MAX": "1536", "SPG_WIDE_MIN": str(1 << 40), "SPG_STEP_COSTS": "18,25,1"},
+    "layer_triples_after_pairs": {"SPG_STEP_COSTS": "18,10,12"},
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
     "comb_13_bit_windows": {"SPG_COMB_C": "13"},
     "tree_levels_per_launch": {"SPG_TREE_TOP": "0"},
@@ -123,7 +126,9 @@ def test_round_forms(form):
     per launch (SPG_EQ_MULTI=0); device witness parts copied instead of read in place (SPG_WIT_IN_PLACE=0); SPARK layer
     rounds one per launch (SPG_LAYER_PAIR=0) instead of two per launch where they are small, paired rounds over 64-thread
     workgroups (more of them: the ticketed sums and the last pair's corners from several workgroups), and pairs for every
-    round that fits (SPG_PAIR_MAX, no throughput-form rounds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
+    round that fits (SPG_PAIR_MAX, no throughput-form rounds); pairs without triples (SPG_LAYER_TRIPLE=0), triples
+    wherever they fit (SPG_TRIPLE_MAX, SPG_STEP_COSTS: up to 1536 elements, 1024-thread workgroups) and pairs preferred
+    before the triples (a triple applying two pending folds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
     the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds; SPARK product trees one
     level per launch (SPG_TREE_TOP=0) or every level in the per-circuit workgroup launch; the device Bullet proofs' delta
     on the bucket MSM (SPG_DELTA_COMB=0) instead of the comb parts"""

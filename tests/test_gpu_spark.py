@@ -74,11 +74,14 @@ def test_spark_repeatable(ctx, oracle):
 
 
 @pytest.mark.parametrize("env", [{"SPG_WIDE_MIN": "1"}, {"SPG_LAYER_QUAD": "0", "SPG_WIDE_MIN": "1000000000000"},
-                                 {"SPG_LAYER_DESC_COPY": "1"}])
+                                 {"SPG_LAYER_DESC_COPY": "1"}, {"SPG_LAYER_TRIPLE": "0"},
+                                 {"SPG_TRIPLE_MAX": "1536", "SPG_WIDE_MIN": "1000000000000", "SPG_STEP_COSTS": "18,25,1"},
+                                 {"SPG_STEP_COSTS": "18,10,12"}])
 def test_spark_round_kernel_forms(oracle, env):
     """every layer round through the throughput form (k_layer_round_wide, normally only for rounds that fill the
     chip) or through the one-lane form, or the layer descriptors uploaded by a copy instead of riding in the
-    eq-table launch: same proof bytes as the oracle (a fresh process reads the switches)"""
+    eq-table launch; the small rounds paired only (no k_layer_triple), tripled wherever they fit, or paired before
+    the triples: same proof bytes as the oracle (a fresh process reads the switches)"""
     import subprocess
     import sys
 

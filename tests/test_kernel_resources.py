@@ -21,7 +21,7 @@ READELF = os.path.join(LLVM, "llvm-readelf")
 
 # kernels every sumcheck / layer / Bullet round launches, and the commit kernels of every prove
 HOT = ("k_phase1_eval", "k_phase2_eval", "k_pqx_fold", "k_cubic_eval", "k_eq_table", "k_fold_top",
-       "k_layer_round", "k_layer_pair", "k_layer_close", "k_layer_persist", "k_bullet_comb", "k_bullet_round_q", "k_comb_msm_parts",
+       "k_layer_round", "k_layer_pair", "k_layer_triple", "k_layer_close", "k_layer_persist", "k_bullet_comb", "k_bullet_round_q", "k_comb_msm_parts",
        "k_smsm_bucket_q", "k_smsm_final", "k_gather_res", "k_spmv", "k_z_fill", "k_abc", "k_bound_part_multi",
        "k_sum_cols_multi", "k_seg_dot", "k_bound_rows", "k_tree_level", "k_tree_top", "k_hash_ops", "k_hash_mem")
 
