@@ -172,6 +172,7 @@ struct BulletCombArgs {
   unsigned* counter;
   uint32_t* mb;
   uint32_t seq;
+  int st;        // comb entry stride (32-byte coordinates)
 };
 
 __device__ __forceinline__ Fq fq_qbcast_lane(const Fq& a, int lane) {
@@ -246,7 +247,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
     bool ng[WG];
 #pragma unroll
     for (int x = 0; x < WG; x++)
-      if (ent[x] != 0xffffffffu) qv[x] = niels_coord(a.comb, ent[x], q, &ng[x]);
+      if (ent[x] != 0xffffffffu) qv[x] = niels_coord(a.comb, ent[x], q, &ng[x], a.st);
 #pragma unroll
     for (int x = 0; x < WG; x++)
       if (ent[x] != 0xffffffffu) acc = quad_madd(acc, qv[x], ng[x], q);
@@ -280,7 +281,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
 template <int C, int G, int BS>
 __global__ void __launch_bounds__(BS) k_comb_msm_parts(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
                                                        int n, const Niels* __restrict__ comb, int NS, int R,
-                                                       Ext* __restrict__ parts) {
+                                                       Ext* __restrict__ parts, int st) {
   constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
   constexpr uint32_t MASK = (1u << C) - 1u;
   __shared__ uint32_t pts[soa_words<Ext, S>()];
@@ -315,7 +316,7 @@ __global__ void __launch_bounds__(BS) k_comb_msm_parts(const Fq* __restrict__ sc
     bool ng[WG];
 #pragma unroll
     for (int x = 0; x < WG; x++)
-      if (ent[x] != 0xffffffffu) qv[x] = niels_coord(comb, ent[x], q, &ng[x]);
+      if (ent[x] != 0xffffffffu) qv[x] = niels_coord(comb, ent[x], q, &ng[x], st);
 #pragma unroll
     for (int x = 0; x < WG; x++)
       if (ent[x] != 0xffffffffu) acc = quad_madd(acc, qv[x], ng[x], q);

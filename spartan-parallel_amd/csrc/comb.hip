@@ -59,7 +59,7 @@ static int comb_c_for(size_t slots) {
 template <int C>
 __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab, int n1, int NS, int hgen,
                                                    Niels* __restrict__ comb, Fp* __restrict__ zs, size_t lanes,
-                                                   size_t lane0) {
+                                                   size_t lane0, int st) {
   constexpr int NB = 1 << (C - 1);
   const size_t L = lane0 + (size_t)blockIdx.x * 64 + threadIdx.x;
   if (L >= lanes) return;
@@ -76,29 +76,29 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
     P = ext_dbl(P);
     if ((m0 >> b) & 1u) P = ext_madd(P, bn, false);
   }
-  Niels* out = comb + ws * NB + (size_t)k * kCombRun;
+  // entry j of the run: coordinates out[j * st + 0..2] (ypx, ymx, t2d; st = 4 leaves a pad coordinate)
+  Fp* out = reinterpret_cast<Fp*>(comb) + (ws * NB + (size_t)k * kCombRun) * st;
   Fp* z = zs + (L - lane0) * kCombRun;
   // forward: X, Y parked in the entry, the prefix product of the Z's in its third field, Z in the scratch
   Fp pp = fp_one();
   for (int j = 0; j < kCombRun; j++) {
     if (j) P = ext_madd(P, bn, false);
     pp = fp_mul(pp, P.Z);
-    out[j].ypx = P.X;
-    out[j].ymx = P.Y;
-    out[j].t2d = pp;
+    out[j * st] = P.X;
+    out[j * st + 1] = P.Y;
+    out[j * st + 2] = pp;
     z[j] = P.Z;
   }
   // backward: 1/Z_j = (1 / prod_{i <= j} Z_i) * prod_{i < j} Z_i
   Fp inv = fp_inv(pp);
   for (int j = kCombRun - 1; j >= 0; j--) {
-    const Fp zi = j ? fp_mul(inv, out[j - 1].t2d) : inv;
+    const Fp zi = j ? fp_mul(inv, out[(j - 1) * st + 2]) : inv;
     if (j) inv = fp_mul(inv, z[j]);
-    const Fp x = fp_mul(out[j].ypx, zi), y = fp_mul(out[j].ymx, zi);
-    Niels r;
-    r.ypx = fp_canon(fp_add(y, x));
-    r.ymx = fp_canon(fp_sub(y, x));
-    r.t2d = fp_canon(fp_mul(fp_mul(x, y), c_d2()));
-    out[j] = r;
+    const Fp x = fp_mul(out[j * st], zi), y = fp_mul(out[j * st + 1], zi);
+    out[j * st] = fp_canon(fp_add(y, x));
+    out[j * st + 1] = fp_canon(fp_sub(y, x));
+    out[j * st + 2] = fp_canon(fp_mul(fp_mul(x, y), c_d2()));
+    if (st == 4) out[j * st + 3] = fp_zero();
   }
 }
 
@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
 template <int C, int G>
 __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
                                                     int n, int gen_offset, const Niels* __restrict__ comb, int NS,
-                                                    int S, Ext* __restrict__ part) {
+                                                    int S, Ext* __restrict__ part, int st) {
   constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, SPW = 256 / G;
   constexpr uint32_t MASK = (1u << C) - 1u;
   __shared__ int16_t dg[WG * 256];  // this lane's digits of its group (lane-major: a lane reads its own)
@@ -147,11 +147,19 @@ __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scala
       d -= carry << C;
       if (w >= w0) dg[(w - w0) * 256 + t] = (int16_t)d;
     }
-    const Niels* cs = comb + (size_t)s * NB + (size_t)w0 * wstride;
+    const size_t e0 = (size_t)s * NB + (size_t)w0 * wstride;  // entry index of window w0, multiple 1
+    const Fp* cf = reinterpret_cast<const Fp*>(comb);
 #pragma unroll 1
     for (int x = 0; x < nx; x++) {
       const int d = dg[x * 256 + t];
-      if (d) P = ext_madd(P, cs[(size_t)x * wstride + (d < 0 ? -d : d) - 1], d < 0);
+      if (d) {
+        const Fp* c = cf + (e0 + (size_t)x * wstride + (d < 0 ? -d : d) - 1) * st;
+        Niels ne;
+        ne.ypx = c[0];
+        ne.ymx = c[1];
+        ne.t2d = c[2];
+        P = ext_madd(P, ne, d < 0);
+      }
     }
   }
   // the quad's four lane sums, broadcast to the quad one after another
@@ -235,7 +243,10 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   // and one that does not fit at all leaves the rows on the buckets
   static const bool cap_set = getenv("SPG_COMB_GB") != nullptr;
   static const size_t cap = (size_t)(cap_set ? atof(getenv("SPG_COMB_GB")) : 144.0) * (1ull << 30);
-  auto table_bytes = [&](int c) { return (size_t)(253 / c + 1) * NS * ((size_t)1 << (c - 1)) * sizeof(Niels); };
+  // entries padded to one 128-byte line each (SPG_COMB_PAD, default on) where the padded table fits: a 96-byte entry
+  // gathered at random straddles two lines two times in three (~2x the algorithmic bytes, PMC-measured)
+  static const bool pad_on = !getenv("SPG_COMB_PAD") || atoi(getenv("SPG_COMB_PAD")) != 0;
+  auto table_bytes = [&](int c, int st) { return (size_t)(253 / c + 1) * NS * ((size_t)1 << (c - 1)) * 32 * st; };
   auto fits = [&](size_t bytes) {
     if (g_comb_bytes.load() + bytes > cap) return false;
     if (cap_set) return true;
@@ -247,12 +258,17 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
     }
     return bytes + kCombHeadroom <= free_b;
   };
-  int C = comb_c_for(cn);
-  if (!fits(table_bytes(C))) {
-    if (C <= 12 || !fits(table_bytes(12))) return 1;
-    C = 12;
-  }
-  const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = entries * sizeof(Niels);
+  // the preferred width padded, then packed; then 12-bit windows padded, then packed
+  const int C0 = comb_c_for(cn);
+  int C = 0, st = 0;
+  const int cands[4][2] = {{C0, 4}, {C0, 3}, {12, 4}, {12, 3}};
+  for (int i = 0; i < (C0 > 12 ? 4 : 2) && !st; i++)
+    if ((cands[i][1] == 3 || pad_on) && fits(table_bytes(cands[i][0], cands[i][1]))) {
+      C = cands[i][0];
+      st = cands[i][1];
+    }
+  if (!st) return 1;
+  const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = table_bytes(C, st);
   Niels* comb = nullptr;
   Fp* zs = nullptr;
   const size_t lanes = entries / kCombRun;
@@ -270,15 +286,15 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   const dim3 gb((unsigned)((chunk + 63) / 64)), tb(64);
   for (size_t l0 = 0; l0 < lanes; l0 += chunk) {
     if (C == 9)
-      hipLaunchKernelGGL(k_comb_build<9>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+      hipLaunchKernelGGL(k_comb_build<9>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0, st);
     else if (C == 10)
-      hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+      hipLaunchKernelGGL(k_comb_build<10>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0, st);
     else if (C == 11)
-      hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+      hipLaunchKernelGGL(k_comb_build<11>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0, st);
     else if (C == 13)
-      hipLaunchKernelGGL(k_comb_build<13>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+      hipLaunchKernelGGL(k_comb_build<13>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0, st);
     else
-      hipLaunchKernelGGL(k_comb_build<12>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0);
+      hipLaunchKernelGGL(k_comb_build<12>, gb, tb, 0, ctx->stream, g->table, (int)(g->n + 1), NS, hgen, comb, zs, lanes, l0, st);
   }
   const hipError_t e = hipGetLastError();
   const hipError_t e2 = hipStreamSynchronize(ctx->stream);
@@ -288,7 +304,7 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
     return set_err(ctx, SPG_E_HIP, "comb table build");
   }
   if (cur.p) g->comb_retired.push_back(cur);
-  g->comb = spg_gens::Comb{comb, cn, bytes, hgen, C};
+  g->comb = spg_gens::Comb{comb, cn, bytes, hgen, C, st};
   g_comb_bytes += bytes;
   *use = g->comb;
   return 0;
@@ -329,7 +345,7 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
     const int NS = (int)cb.slots + 1;
 #define SPG_COMB_LAUNCH(CC, GG)                                                                                  \
   hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, \
-                     cb.p, NS, (int)S, part)
+                     cb.p, NS, (int)S, part, cb.st)
     const int key = C * 8 + (int)G;
     switch (key) {
       case 9 * 8 + 1: SPG_COMB_LAUNCH(9, 1); break;
@@ -379,7 +395,7 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
     const dim3 ga((unsigned)S), ta(256);
 #define SPG_CS(CC, GG)                                                                                          \
   hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blind, (int)n, (int)gen_offset, \
-                     cb.p, NS, (int)S, (Ext*)d_map)
+                     cb.p, NS, (int)S, (Ext*)d_map, cb.st)
     const int key = C * 8 + (int)G;
     switch (key) {
       case 9 * 8 + 1: SPG_CS(9, 1); break;

@@ -111,6 +111,7 @@ struct spg_gens {
     size_t slots = 0, bytes = 0;
     int h = -1;
     int c = 12;  // window width: 253 / c + 1 windows of 2^(c-1) multiples per generator
+    int st = 3;  // entry stride in 32-byte coordinates: 3 (96-byte Niels) or 4 (padded to one 128-byte line)
   };
   mutable std::mutex comb_mu;
   mutable Comb comb;

@@ -663,7 +663,7 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   const int S = BS / 4, quads = (n / 2) * G, wgs = (quads + S - 1) / S;
   if (wgs * R > kBulletPartsMax) return 1;
   BulletCombArgs a{aa_in, cw_in, aa_out, cw_out, gidx, u, uinv, k, n, nk, cb.p, (int)cb.slots + 1, R, d_parts,
-                   ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq};
+                   ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq, cb.st};
   *seq_out = a.seq;
   *per_msm = wgs * R;
   // VALU model: one mixed addition per nonzero signed C-bit digit of the n/2 scalars of each of the two MSMs
@@ -708,7 +708,8 @@ int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const u
   const dim3 grid((unsigned)wgs, (unsigned)B);
   const int NS = (int)cb.slots + 1;
 #define SPG_CMP(CC, GG, BB) \
-  hipLaunchKernelGGL((k_comb_msm_parts<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, d_scalars, d_idx, n, cb.p, NS, R, d_parts)
+  hipLaunchKernelGGL((k_comb_msm_parts<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, d_scalars, d_idx, n, cb.p, NS, R, d_parts, \
+                     cb.st)
 #define SPG_CMP_BS(CC, GG) \
   do { if (BS == 64) SPG_CMP(CC, GG, 64); else if (BS == 128) SPG_CMP(CC, GG, 128); else SPG_CMP(CC, GG, 256); } while (0)
   if (cb.c == 13) {

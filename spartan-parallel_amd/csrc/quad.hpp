@@ -70,10 +70,12 @@ __device__ __forceinline__ Fp quad_operand(const Ext& P, int q) {
 }
 // the Niels coordinate lane q of a quad needs for table entry ent (index | neg << 31): lane 0 the "minus" one
 // (neg ? ypx : ymx), lane 1 the "plus" one, lanes 2, 3 t2d; one 32-byte load per lane
-__device__ __forceinline__ Fp niels_coord(const Niels* __restrict__ tab, uint32_t ent, int q, bool* neg) {
+// (st: the table's entry stride in 32-byte coordinates, 3 for packed 96-byte entries, 4 for the comb tables padded
+// to one 128-byte line per entry)
+__device__ __forceinline__ Fp niels_coord(const Niels* __restrict__ tab, uint32_t ent, int q, bool* neg, int st = 3) {
   *neg = ent >> 31;
   const int which = q >= 2 ? 2 : ((q == 0) != *neg ? 1 : 0);  // Niels field order: ypx, ymx, t2d
-  return reinterpret_cast<const Fp*>(tab + (ent & 0x7fffffffu))[which];
+  return reinterpret_cast<const Fp*>(tab)[(size_t)(ent & 0x7fffffffu) * st + which];
 }
 // table entry (index | sign << 31) as an extended point, negated when the sign bit is set
 __device__ __forceinline__ Ext load_signed(const Niels* __restrict__ tab, uint32_t e) {

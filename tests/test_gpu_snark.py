@@ -108,6 +108,7 @@ ROUND_FORMS = {
     "layer_triples_after_pairs": {"SPG_STEP_COSTS": "18,10,12"},
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
     "comb_13_bit_windows": {"SPG_COMB_C": "13"},
+    "comb_packed_entries": {"SPG_COMB_PAD": "0"},
     "tree_levels_per_launch": {"SPG_TREE_TOP": "0"},
     "tree_one_launch": {"SPG_TREE_TOP": str(1 << 40)},
     "delta_bucket_msm": {"SPG_DELTA_COMB": "0"},
@@ -129,7 +130,8 @@ def test_round_forms(form):
     round that fits (SPG_PAIR_MAX, no throughput-form rounds); pairs without triples (SPG_LAYER_TRIPLE=0), triples
     wherever they fit (SPG_TRIPLE_MAX, SPG_STEP_COSTS: up to 1536 elements, 1024-thread workgroups) and pairs preferred
     before the triples (a triple applying two pending folds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
-    the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds; SPARK product trees one
+    the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds, and comb entries packed at
+    96 bytes (SPG_COMB_PAD=0) instead of one 128-byte line each; SPARK product trees one
     level per launch (SPG_TREE_TOP=0) or every level in the per-circuit workgroup launch; the device Bullet proofs' delta
     on the bucket MSM (SPG_DELTA_COMB=0) instead of the comb parts"""
     import subprocess
