@@ -13,6 +13,7 @@
 #include <atomic>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/spg.h"
@@ -178,7 +179,17 @@ struct HostGens {
     h::hext_decompress(comp.data() + 32 * idx, P);
     return P;
   }
+  // the table map of every HostGens is guarded by one process-wide lock (contexts on several threads may share a
+  // generator set; a table, once built, never moves: std::map nodes are stable)
+  static std::mutex& table_mu() {
+    static std::mutex m;
+    return m;
+  }
   const FixedBase& get(size_t idx) {
+    std::lock_guard<std::mutex> lk(table_mu());
+    return get_locked(idx);
+  }
+  const FixedBase& get_locked(size_t idx) {
     auto it = fb.find(idx);
     if (it != fb.end()) return it->second;
     FixedBase& f = fb[idx];
@@ -224,14 +235,17 @@ struct HostGens {
     };
     std::vector<Term> terms;
     std::vector<size_t> tfirst(J + 1, 0);  // terms of job j: [tfirst[j], tfirst[j + 1])
-    for (size_t j = 0; j < J; j++) {
-      for (size_t i = 0; i < jobs[j].first.size(); i++) {
-        Term tm;
-        tm.fb = &get(jobs[j].first[i]);  // build tables on this thread (map insertion is not thread-safe)
-        fq_le_bytes(jobs[j].second[i], tm.b);
-        terms.push_back(tm);
+    {
+      std::lock_guard<std::mutex> lk(table_mu());  // tables are built on this thread, under the lock
+      for (size_t j = 0; j < J; j++) {
+        for (size_t i = 0; i < jobs[j].first.size(); i++) {
+          Term tm;
+          tm.fb = &get_locked(jobs[j].first[i]);
+          fq_le_bytes(jobs[j].second[i], tm.b);
+          terms.push_back(tm);
+        }
+        tfirst[j + 1] = terms.size();
       }
-      tfirst[j + 1] = terms.size();
     }
     const size_t U = 32 * terms.size();
     const size_t threads = (size_t)pool().size() + 1;

@@ -388,10 +388,30 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
   uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsCommit, 32 * chunk + 64);
   if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit out");
   static const bool trace2 = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2;
+  // SPG_HOST_COMMIT_MAX (256): row batches of at most this many scalars in all are committed on the host pool against
+  // the generators' fixed-base byte tables (HostGens, built once per generator set): the scalars come down (<= 32 KB)
+  // and 32 mixed additions per scalar spread over the pool, instead of a device bucket launch, its host finals and a
+  // synchronisation (8 scalars: 35-40 us against 44-49 us; 256: 69 against 79 us; 512 scalars already take longer there,
+  // 115 against 86 us, profiles/r05_ab_host_commit.txt)
+  static const size_t host_commit_max =
+      getenv("SPG_HOST_COMMIT_MAX") ? (size_t)atol(getenv("SPG_HOST_COMMIT_MAX")) : 256;
   for (size_t r0 = 0; r0 < L; r0 += chunk) {
     size_t nb = std::min(chunk, L - r0);
     auto t0 = std::chrono::steady_clock::now();
-    if (small && nb <= kHostFinalRows) {
+    if (small && nb * R <= host_commit_max) {
+      FqV hz(nb * R);
+      SPG_HIP(ctx, hipMemcpyAsync(hz.data(), d_Z + r0 * R, nb * R * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      std::vector<std::pair<std::vector<size_t>, FqV>> jobs(nb);
+      std::vector<size_t> idx(R);
+      for (size_t i = 0; i < R; i++) idx[i] = g.gens_n.G[i];
+      for (size_t b = 0; b < nb; b++) {
+        jobs[b].first = idx;
+        jobs[b].second.assign(hz.begin() + b * R, hz.begin() + (b + 1) * R);
+      }
+      const std::vector<Pt> pts = g.host.commit_many(jobs);
+      std::copy(pts.begin(), pts.end(), out + r0);
+    } else if (small && nb <= kHostFinalRows) {
       // few rows: the bucket running sums and encodings are cheaper on host cores than the device's
       // one-lane-per-row final + compress (~0.25 ms floor)
       void* d_map = nullptr;
@@ -419,7 +439,8 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
       SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
     }
     if (trace2)
-      fprintf(stderr, "[spg] commit rows=%zu R=%zu %s %.0f us\n", nb, R, small ? "small" : "batch",
+      fprintf(stderr, "[spg] commit rows=%zu R=%zu %s %.0f us\n", nb, R,
+              small && nb * R <= host_commit_max ? "host" : (small ? "small" : "batch"),
               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   }
   return 0;
