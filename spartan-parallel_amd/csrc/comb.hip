@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(64) k_comb_build(const Niels* __restrict__ tab
 template <int C, int G>
 __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scalars, const Fq* __restrict__ blinds,
                                                     int n, int gen_offset, const Niels* __restrict__ comb, int NS,
-                                                    int S, Ext* __restrict__ part, int st) {
+                                                    int S, Ext* __restrict__ part, int st, Fq mulc) {
   constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, SPW = 256 / G;
   constexpr uint32_t MASK = (1u << C) - 1u;
   __shared__ int16_t dg[WG * 256];  // this lane's digits of its group (lane-major: a lane reads its own)
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) k_comb_accum(const Fq* __restrict__ scala
       sm = blinds[b];
       s = NS - 1;
     }
-    const Fq k = fq_from_mont(sm);
+    const Fq k = fq_mul(sm, mulc);  // out of Montgomery form (mulc = 1), halved on the way (mulc = (l + 1) / 2)
     int carry = 0;
 #pragma unroll
     for (int w = 0; w < W; w++) {
@@ -317,8 +317,22 @@ int comb_get(spg_ctx* ctx, const spg_gens* g, size_t need, spg_gens::Comb* out) 
 // B row MSMs of n contiguous generators from gen_offset (+ blinds on h): SPG_OK with the rows' points in ext
 // (B Ext, device) and, when d_out is set, their encodings; kCombSkip when the comb does not apply (the caller
 // runs the bucket pipeline); or an SPG error code
+// the plain (not Montgomery) multiplier that takes a Montgomery scalar to its canonical value (1) or to half of it
+static Fq comb_mulc(bool halve) {
+  Fq c = fq_zero();
+  if (!halve) {
+    c.l[0] = 1;
+    return c;
+  }
+  // (l + 1) / 2
+  const uint32_t h[8] = {0x2e7ae9f7u, 0x2c09318du, 0x517bce6bu, 0x0a6f7cefu, 0u, 0u, 0u, 0x08000000u};
+  for (int i = 0; i < 8; i++) c.l[i] = h[i];
+  return c;
+}
+
 int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
-             const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext) {
+             const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext, bool halve) {
+  if (halve && d_out) return set_err(ctx, SPG_E_ARG, "msm_comb: halved points have no device encoding");
   spg_gens::Comb cb;
   const int rc = comb_ensure(ctx, g, gen_offset + n, h_index, &cb);
   if (rc == 1) return kCombSkip;
@@ -345,7 +359,7 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
     const int NS = (int)cb.slots + 1;
 #define SPG_COMB_LAUNCH(CC, GG)                                                                                  \
   hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blinds, (int)n, (int)gen_offset, \
-                     cb.p, NS, (int)S, part, cb.st)
+                     cb.p, NS, (int)S, part, cb.st, comb_mulc(halve))
     const int key = C * 8 + (int)G;
     switch (key) {
       case 9 * 8 + 1: SPG_COMB_LAUNCH(9, 1); break;
@@ -395,7 +409,7 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
     const dim3 ga((unsigned)S), ta(256);
 #define SPG_CS(CC, GG)                                                                                          \
   hipLaunchKernelGGL((k_comb_accum<CC, GG>), ga, ta, 0, ctx->stream, d_scalars, d_blind, (int)n, (int)gen_offset, \
-                     cb.p, NS, (int)S, (Ext*)d_map, cb.st)
+                     cb.p, NS, (int)S, (Ext*)d_map, cb.st, comb_mulc(false))
     const int key = C * 8 + (int)G;
     switch (key) {
       case 9 * 8 + 1: SPG_CS(9, 1); break;

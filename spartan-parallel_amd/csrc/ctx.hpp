@@ -166,14 +166,20 @@ void timer_stop(spg_ctx* c);
 // h_index (-1: g->n). d_out: B x 32 compressed bytes (device). Stream-ordered, no host sync.
 // comb.hip: batches of row MSMs from per-generator-set comb tables (kCombSkip: not applicable, use the buckets)
 static const int kCombSkip = -1;
+// halve: every scalar times 2^-1 mod l (the points are P / 2, for the host's batched encoding of doubles,
+// hcurve.hpp hext_double_and_compress_batch; d_out must then be null)
 int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
-             const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext);
+             const Fq* d_blinds, uint8_t* d_out, int h_index, Ext* ext, bool halve = false);
 void comb_free(const spg_gens* g);
 // g's comb table covering generators [0, need) (built on first use): 0 with *out set, 1 when the comb does not
 // apply (disabled, too wide, over the memory cap), or an SPG error code
 int comb_get(spg_ctx* ctx, const spg_gens* g, size_t need, spg_gens::Comb* out);
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext = nullptr);
+// the same rows (gen_offset 0) with their 32-byte encodings on the host in out (msm.hip: halved comb points encoded as
+// doubles on the host pool where the comb applies); synchronous
+int msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, size_t n, size_t B, const Fq* d_blinds,
+                      long h_index, uint8_t* out);
 
 // latency path for small batches (B * n up to a few thousand): same inputs, results left in extended
 // coordinates in d_out (B x Ext, device); the caller encodes them (host).

@@ -318,6 +318,58 @@ inline void hext_compress(const HExt& P, uint8_t out[32]) {
   Fe s = fe_abs(fe_mul(den_inv, fe_sub(P.Z, y)));
   fe_to_bytes(s, out);
 }
+// RFC 9496 ENCODE of 2 P_i for a batch with ONE field inversion (the batched encoding of curve25519-dalek's
+// RistrettoPoint::double_and_compress_batch): with e = 2XY, f = Z^2 + d T^2, g = Y^2 + X^2, h = Z^2 - d T^2 of P, the
+// double's encoding needs 1 / (e g f h), inverted for the whole batch by Montgomery's trick, where a lone encoding
+// needs an inverse square root (~250 squarings). A caller that wants encode(P) halves P first -- its MSM scalars
+// times 2^-1 mod l -- so the host encodes a batch at ~25 products per point instead of ~265. Points whose e g f h
+// vanishes (torsion representatives of the identity, whose double encodes to 0) take the lone encoding of 2 P.
+inline void hext_double_and_compress_batch(const HExt* P, size_t n, uint8_t (*out)[32]) {
+  struct St {
+    Fe e, f, g, h, eg, fh, efgh, pre;
+    bool zero;
+  };
+  std::vector<St> st(n);
+  Fe run = fe_one();
+  for (size_t i = 0; i < n; i++) {
+    St& s = st[i];
+    const Fe XX = fe_sqr(P[i].X), YY = fe_sqr(P[i].Y), ZZ = fe_sqr(P[i].Z);
+    const Fe dTT = fe_mul(fe_sqr(P[i].T), K().d);
+    s.e = fe_mul(P[i].X, fe_add(P[i].Y, P[i].Y));
+    s.f = fe_add(ZZ, dTT);
+    s.g = fe_add(YY, XX);
+    s.h = fe_sub(ZZ, dTT);
+    s.eg = fe_mul(s.e, s.g);
+    s.fh = fe_mul(s.f, s.h);
+    s.efgh = fe_mul(s.eg, s.fh);
+    s.zero = fe_is_zero(s.efgh);
+    s.pre = run;
+    if (!s.zero) run = fe_mul(run, s.efgh);
+  }
+  Fe inv = fe_invert(run);  // 1 / (product of the nonzero e g f h)
+  for (size_t i = n; i-- > 0;) {
+    const St& s = st[i];
+    if (s.zero) {
+      hext_compress(hext_dbl(P[i]), out[i]);
+      continue;
+    }
+    const Fe inv_i = fe_mul(inv, s.pre);
+    inv = fe_mul(inv, s.efgh);
+    const Fe Zinv = fe_mul(s.eg, inv_i), Tinv = fe_mul(s.fh, inv_i);
+    Fe magic = K().invsqrt_a_minus_d, e = s.e, g = s.g, h = s.h;
+    if (fe_is_negative(fe_mul(s.eg, Zinv))) {
+      const Fe minus_e = fe_neg(s.e);
+      e = s.g;
+      g = minus_e;
+      h = fe_mul(s.f, K().sqrt_m1);
+      magic = K().sqrt_m1;
+    }
+    if (fe_is_negative(fe_mul(fe_mul(h, e), Zinv))) g = fe_neg(g);
+    Fe r = fe_mul(fe_sub(h, g), fe_mul(magic, fe_mul(g, Tinv)));
+    if (fe_is_negative(r)) r = fe_neg(r);
+    fe_to_bytes(r, out[i]);
+  }
+}
 // RFC 9496 DECODE
 inline bool hext_decompress(const uint8_t in[32], HExt& out) {
   Fe s = fe_from_bytes(in);

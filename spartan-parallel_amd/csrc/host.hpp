@@ -9,6 +9,7 @@
 #pragma once
 #include <string.h>
 
+#include <algorithm>
 #include <functional>
 #include <atomic>
 #include <map>
@@ -142,6 +143,23 @@ inline Pt compress(const h::HExt& p) {
   Pt c;
   h::hext_compress(p, c.b);
   return c;
+}
+// encodings of B device points that are halves (a comb MSM with halved scalars: encode(2 P') = encode(P)), as the
+// doubles' batched encodings on the pool (hext_double_and_compress_batch), chunks of >= 32 points, one inversion each
+inline void encode_halved_host(const Ext* d, size_t B, Pt* out) {
+  static_assert(sizeof(Pt) == 32, "Pt is the 32-byte encoding");
+  const int C = (int)std::max<size_t>(1, std::min<size_t>(B / 32, (size_t)pool().size() + 1));
+  auto enc = [&](int c) {
+    const size_t lo = B * c / C, hi = B * (c + 1) / C;
+    thread_local std::vector<h::HExt> P;
+    P.resize(hi - lo);
+    for (size_t i = lo; i < hi; i++) P[i - lo] = h::hext_from_dev(d[i]);
+    h::hext_double_and_compress_batch(P.data(), hi - lo, reinterpret_cast<uint8_t(*)[32]>(out + lo));
+  };
+  if (C == 1)
+    enc(0);
+  else
+    pool().parallel_for(C, enc);
 }
 
 // Fixed-base host scalar multiplication: tab[w][j] = j * 2^(8w) * P (affine Niels), 32 windows of 8

@@ -192,6 +192,37 @@ int spgh_vec_check(const uint8_t* uni, size_t n) {
   return bad;
 }
 
+// The batched encoding of doubles (hcurve.hpp, hext_double_and_compress_batch) against the lone encoding of 2 Q, over
+// n hash-to-group points, each also moved by the 2- and 4-torsion points, and the identity and the torsion points
+// themselves (zero e g f h). Returns the mismatches (0), or -1 for n == 0.
+int spgh_dbl_compress_check(const uint8_t* uni, size_t n) {
+  using namespace spg;
+  if (!n) return -1;
+  const h::HExt T2{h::fe_zero(), h::fe_neg(h::fe_one()), h::fe_one(), h::fe_zero()};
+  const h::HExt T4{h::K().sqrt_m1, h::fe_zero(), h::fe_one(), h::fe_zero()};
+  std::vector<h::HExt> Q;
+  for (size_t i = 0; i < n; i++) {
+    const h::HExt P = h::hext_from_dev(ristretto_from_uniform_bytes(uni + 64 * i));
+    Q.push_back(P);
+    Q.push_back(h::hext_add(P, T2));
+    Q.push_back(h::hext_add(P, T4));
+    if (i == n / 2) {
+      Q.push_back(h::hext_identity());
+      Q.push_back(T2);
+      Q.push_back(T4);
+    }
+  }
+  std::vector<uint8_t> got(32 * Q.size());
+  h::hext_double_and_compress_batch(Q.data(), Q.size(), (uint8_t(*)[32])got.data());
+  int bad = 0;
+  for (size_t i = 0; i < Q.size(); i++) {
+    uint8_t want[32];
+    h::hext_compress(h::hext_dbl(Q[i]), want);
+    bad += memcmp(want, got.data() + 32 * i, 32) != 0;
+  }
+  return bad;
+}
+
 // The cross-rank exchange of every sharded call (comm.hpp: api.hip's comm_sum_fq, which Prover::sum_ranks and the
 // SPARK / multi_evaluate shards use): gather every rank's status and n partial scalars through the caller's
 // allgather and sum them mod q. Returns the transport's error (-1), else the first non-zero status of any rank

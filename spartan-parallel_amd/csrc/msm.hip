@@ -25,6 +25,7 @@
 
 #include "ctx.hpp"
 #include "hcurve.hpp"
+#include "host.hpp"
 #include "keccak.hpp"
 #include "lds.hpp"
 #include "bullet.hpp"
@@ -1410,6 +1411,40 @@ extern "C" int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* 
   return msm_host(ctx, g, 0, Z_mont, R, L, blinds_mont, out);
 }
 
+// B row MSMs of n device scalars (as msm_batch_device, gen_offset 0) with their encodings on the host (out: 32 B each):
+// where the comb applies (msm_batch_device's size rule), the rows' halves (scalars and blinds times 2^-1 mod l) come
+// back for the host pool's batched encoding of doubles (encode_halved_host) instead of k_compress_ext's lane-per-point
+// inverse square roots; else msm_batch_device's device encodings, downloaded. SPG_HALVED_ENC=0: always the latter.
+int spg::msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, size_t n, size_t B,
+                           const Fq* d_blinds, long h_index, uint8_t* out) {
+  static const bool halve = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
+  hipStream_t s = ctx->stream;
+  const size_t tot = B * (n + (d_blinds ? 1 : 0));
+  const bool comb = B >= 64 && (n <= 1024 ? tot >= ((size_t)1 << 14) : (n <= 16384 && tot >= ((size_t)1 << 22)));
+  if (halve && comb) {
+    Ext* ext = (Ext*)ws_get(ctx, 17, B * sizeof(Ext) + 64);
+    if (!ext) return set_err(ctx, SPG_E_NOMEM, "msm comb points");
+    const int hi = !d_blinds ? -1 : (h_index < 0 ? (int)g->n : (int)h_index);
+    const int rc = msm_comb(ctx, g, 0, d_scalars, n, B, d_blinds, nullptr, hi, ext, true);
+    if (rc == SPG_OK) {
+      Ext* h = (Ext*)enc_stage_get(ctx, B * sizeof(Ext));
+      if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
+      SPG_HIP(ctx, hipMemcpyAsync(h, ext, B * sizeof(Ext), hipMemcpyDeviceToHost, s));
+      SPG_HIP(ctx, hipStreamSynchronize(s));
+      encode_halved_host(h, B, reinterpret_cast<Pt*>(out));
+      return SPG_OK;
+    }
+    if (rc != kCombSkip) return rc;
+  }
+  uint8_t* d_out = (uint8_t*)ws_get(ctx, 12, 32 * B + 64);
+  if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit rows out");
+  const int rc = msm_batch_device(ctx, g, 0, d_scalars, n, B, d_blinds, d_out, nullptr, h_index);
+  if (rc) return rc;
+  SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, s));
+  SPG_HIP(ctx, hipStreamSynchronize(s));
+  return SPG_OK;
+}
+
 extern "C" int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_buf* Z, size_t offset, size_t L,
                                    size_t R, const spg_buf* blinds, uint8_t* out) {
   if (!ctx || !g || !Z || !out) return SPG_E_ARG;
@@ -1417,15 +1452,11 @@ extern "C" int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_bu
   if (blinds && blinds->n < L) return set_err(ctx, SPG_E_ARG, "commit_rows_buf: blinds too short");
   if (R > g->n) return set_err(ctx, SPG_E_ARG, "commit_rows_buf: R exceeds generators");
   if (L == 0) return SPG_OK;
-  hipStream_t s = ctx->stream;
-  uint8_t* d_out = (uint8_t*)ws_get(ctx, 12, 32 * L);
-  if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit_rows_buf out");
   timer_start(ctx);
-  int rc = msm_batch_device(ctx, g, 0, Z->d + offset, R, L, blinds ? blinds->d : nullptr, d_out, nullptr, -1);
+  const int rc = msm_rows_host_enc(ctx, g, Z->d + offset, R, L, blinds ? blinds->d : nullptr, -1, out);
   if (rc) return rc;
-  timer_stop(ctx);
-  SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * L, hipMemcpyDeviceToHost, s));
-  SPG_HIP(ctx, hipStreamSynchronize(s));
+  timer_stop(ctx);  // (recorded after the host encodings: device time plus the host's share)
+  SPG_HIP(ctx, hipEventSynchronize(ctx->ev1));
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
   ctx->last_us = ms * 1000.0;

@@ -177,6 +177,16 @@ struct RowJob {
   Pt* out;
 };
 int commit_rows_many(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs);
+// the same in two steps: launch queues the merged sets' points on ctx->stream, finish (same stream) encodes them and
+// commits the other sets; the caller may do other host work in between
+struct RowsPending {
+  Ext* d_ext = nullptr;
+  uint8_t* d_out = nullptr;
+  size_t tot = 0;
+  std::vector<char> hv;  // per merged set: its points are halves (encoded as doubles on the host)
+};
+int commit_rows_many_launch(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs, RowsPending* p);
+int commit_rows_many_finish(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs, RowsPending& p);
 // the same split over the ranks of sh (every rank returns all L commitments)
 int commit_rows_sh(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Pt* out, const Shard& sh);
 // PolyCommitment::append_to_transcript

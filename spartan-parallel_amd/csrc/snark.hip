@@ -451,6 +451,7 @@ struct CQ {
   std::vector<const Fq*> early_dev;
   size_t early_R = 0, early_L = 0;
   uint8_t* early_out = nullptr;
+  const Ext* early_ext = nullptr;  // halved comb points (encoded on the host at flush), else early_out's encodings
   int launch_early(spg_ctx* ctx, ProverGens& g, const std::vector<std::pair<const Fq*, size_t>>& its) {
     size_t R = 0, total = 0;
     for (auto& it : its) {
@@ -470,8 +471,17 @@ struct CQ {
       SPG_HIP(ctx, hipMemcpyAsync(d + o, it.first, it.second * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
       o += it.second;
     }
-    int rc = msm_batch_device(ctx, g.dev, 0, d, R, total / R, nullptr, out, nullptr, (long)(g.n_pc + 1));
+    // the comb rows with halved scalars: flush() encodes the points' doubles on the host in one batch (~50 us on the
+    // pool for 1024 rows) instead of a k_compress_ext launch (~140 us of dependent squarings per lane)
+    static const bool halve = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
+    Ext* ext = halve ? (Ext*)ws_get(ctx, 94, sizeof(Ext) * (total / R) + 64) : nullptr;
+    int rc = ext ? msm_comb(ctx, g.dev, 0, d, R, total / R, nullptr, nullptr, -1, ext, true) : kCombSkip;
+    if (rc == kCombSkip) {
+      ext = nullptr;
+      rc = msm_batch_device(ctx, g.dev, 0, d, R, total / R, nullptr, out, nullptr, (long)(g.n_pc + 1));
+    }
     if (rc) return rc;
+    early_ext = ext;
     for (auto& it : its) early_dev.push_back(it.first);
     early_R = R;
     early_L = total / R;
@@ -506,14 +516,24 @@ struct CQ {
       SPG_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_pre, 0));
       ctx->stream = ctx->stream2;
     }
-    int rc = flush_rows(ctx, g, widths);
+    int rc = flush_rows_launch(ctx, g, widths);
     ctx->stream = main_stream;
     if (rc) return rc;
-    lp.lap(side ? "rows_side" : "rows");
+    lp.lap(side ? "rows_side_launch" : "rows_launch");
+    // the early group's encodings while the other rows' points are computed
     if (early_L) {
       std::vector<Pt> rows(early_L);
-      SPG_HIP(ctx, hipMemcpyAsync(rows.data(), early_out, 32 * early_L, hipMemcpyDeviceToHost, ctx->stream));
-      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      if (early_ext) {
+        Ext* h = (Ext*)enc_stage_get(ctx, early_L * sizeof(Ext));
+        if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
+        SPG_HIP(ctx, hipMemcpyAsync(h, early_ext, early_L * sizeof(Ext), hipMemcpyDeviceToHost, ctx->stream));
+        SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        encode_halved_host(h, early_L, rows.data());
+        early_ext = nullptr;
+      } else {
+        SPG_HIP(ctx, hipMemcpyAsync(rows.data(), early_out, 32 * early_L, hipMemcpyDeviceToHost, ctx->stream));
+        SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      }
       size_t o = 0;
       for (const Fq* d : early_dev)  // rows in launch order
         for (auto& it : items)
@@ -525,14 +545,38 @@ struct CQ {
       early_L = 0;
     }
     lp.lap("early_wait");
+    if (side) ctx->stream = ctx->stream2;
+    rc = flush_rows_finish(ctx, g, widths);
+    ctx->stream = main_stream;
+    if (rc) return rc;
+    lp.lap(side ? "rows_side_finish" : "rows_finish");
     for (auto& it : items) append_polycomm(t, "poly_commitment", *it.out);
     items.clear();
     lp.lap("append");
     lp.print();
     return 0;
   }
-  // the rows of every item outside the early group, on ctx->stream; synchronous
-  int flush_rows(spg_ctx* ctx, ProverGens& g, const std::vector<size_t>& widths) {
+  // the rows of every item outside the early group, on ctx->stream: launched (uploads and points), then finished
+  // (encodings; the host may encode the early group in between)
+  std::vector<std::vector<Pt>> rows;
+  std::vector<RowJob> jobs;
+  RowsPending pend;
+  int flush_rows_finish(spg_ctx* ctx, ProverGens& g, const std::vector<size_t>& widths) {
+    int rc = commit_rows_many_finish(ctx, g, jobs, pend);
+    if (rc) return rc;
+    for (size_t w = 0; w < widths.size(); w++) {
+      size_t ro = 0;
+      for (auto& it : items) {
+        if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != widths[w]) continue;
+        std::copy(rows[w].begin() + ro, rows[w].begin() + ro + it.out->size(), it.out->begin());
+        ro += it.out->size();
+      }
+    }
+    rows.clear();
+    jobs.clear();
+    return 0;
+  }
+  int flush_rows_launch(spg_ctx* ctx, ProverGens& g, const std::vector<size_t>& widths) {
     // one staging range per width, every width's rows committed together (the latency-path widths share one
     // encoding launch and one download)
     size_t total = 0;
@@ -540,8 +584,8 @@ struct CQ {
       if (!is_early(it)) total += it.len;
     Fq* d = (Fq*)ws_get(ctx, 91, total * sizeof(Fq) + 64);
     if (total && !d) return set_err(ctx, SPG_E_NOMEM, "commit staging");
-    std::vector<std::vector<Pt>> rows(widths.size());
-    std::vector<RowJob> jobs;
+    rows.assign(widths.size(), {});
+    jobs.clear();
     size_t o = 0;
     for (size_t w = 0; w < widths.size(); w++) {
       const size_t R = widths[w], o0 = o;
@@ -556,17 +600,7 @@ struct CQ {
       rows[w].resize((o - o0) / R);
       jobs.push_back({d + o0, R, (o - o0) / R, rows[w].data()});
     }
-    int rc = commit_rows_many(ctx, g, jobs);
-    if (rc) return rc;
-    for (size_t w = 0; w < widths.size(); w++) {
-      size_t ro = 0;
-      for (auto& it : items) {
-        if (is_early(it) || ((size_t)1 << (lg2(it.len) - lg2(it.len) / 2)) != widths[w]) continue;
-        std::copy(rows[w].begin() + ro, rows[w].begin() + ro + it.out->size(), it.out->begin());
-        ro += it.out->size();
-      }
-    }
-    return 0;
+    return commit_rows_many_launch(ctx, g, jobs, &pend);
   }
 };
 

@@ -321,7 +321,7 @@ enum : size_t {
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
   kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp,  // 60 .. 89
   kWsRelay = 94,
-  kWsMultiExt = 120, kWsMultiOut, kWsCommitExt  // (snark.hip uses 91 .. 93, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
+  kWsMultiExt = 120, kWsMultiOut, kWsCommitExt  // (snark.hip uses 91 .. 94, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -343,8 +343,19 @@ ProverGens gens_view(spg_gens* dev, size_t nv) {
 // and are encoded on the host pool: one encoding is a ~2.4 us inverse square root on a host core, while
 // k_compress_ext gives each point one GPU lane whose ~250 dependent squarings take ~130 us whatever the count.
 // Larger batches encode on the device (d_out: 32 B per point of device scratch).
-static int encode_points(spg_ctx* ctx, const Ext* d_ext, size_t B, Pt* out, uint8_t* d_out) {
+// halved: the device points are P / 2 (msm_comb's halve), encoded as the doubles on the host pool in chunks of one
+// field inversion each (hext_double_and_compress_batch: ~25 products per point instead of a ~265-step inverse square
+// root on a GPU lane or a host core), at any count
+static int encode_points(spg_ctx* ctx, const Ext* d_ext, size_t B, Pt* out, uint8_t* d_out, bool halved = false) {
   static const size_t host_max = getenv("SPG_HOST_ENC_MAX") ? (size_t)atol(getenv("SPG_HOST_ENC_MAX")) : 384;
+  if (halved) {
+    Ext* h = (Ext*)enc_stage_get(ctx, B * sizeof(Ext));
+    if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
+    SPG_HIP(ctx, hipMemcpyAsync(h, d_ext, B * sizeof(Ext), hipMemcpyDeviceToHost, ctx->stream));
+    SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    encode_halved_host(h, B, out);
+    return 0;
+  }
   if (B <= host_max) {
     Ext* h = (Ext*)enc_stage_get(ctx, B * sizeof(Ext));
     if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
@@ -369,10 +380,16 @@ static int encode_points(spg_ctx* ctx, const Ext* d_ext, size_t B, Pt* out, uint
 
 // L rows of R device scalars on the latency-path generators into device points: the comb tables when they apply
 // (>= 64 rows, >= 2^14 scalars in all), else the latency-path bucket kernels
-static int rows_to_points(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Ext* d_ext) {
+// (*halved: the comb path left P / 2, encode_points' halved form; SPG_HALVED_ENC=0 keeps the device encodings)
+static int rows_to_points(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Ext* d_ext, bool* halved) {
+  static const bool halve = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
+  *halved = false;
   if (L >= 64 && L * R >= ((size_t)1 << 14)) {
-    const int rc = msm_comb(ctx, g.dev, 0, d_Z, R, L, nullptr, nullptr, -1, d_ext);
-    if (rc != kCombSkip) return rc;
+    const int rc = msm_comb(ctx, g.dev, 0, d_Z, R, L, nullptr, nullptr, -1, d_ext, halve);
+    if (rc != kCombSkip) {
+      *halved = halve;
+      return rc;
+    }
   }
   return msm_small_device(ctx, g.dev, 0, d_Z, R, L, nullptr, d_ext, nullptr, -1);
 }
@@ -429,14 +446,13 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
     } else if (small) {
       Ext* d_ext = (Ext*)ws_get(ctx, kWsCommitExt, sizeof(Ext) * nb + 64);
       if (!d_ext) return set_err(ctx, SPG_E_NOMEM, "commit points");
-      int rc = rows_to_points(ctx, g, d_Z + r0 * R, R, nb, d_ext);
-      if (!rc) rc = encode_points(ctx, d_ext, nb, out + r0, d_out);  // synchronous: d_ext, d_out reused next chunk
+      bool halved = false;
+      int rc = rows_to_points(ctx, g, d_Z + r0 * R, R, nb, d_ext, &halved);
+      if (!rc) rc = encode_points(ctx, d_ext, nb, out + r0, d_out, halved);  // synchronous: d_ext, d_out reused next chunk
       if (rc) return rc;
-    } else {
-      int rc = msm_batch_device(ctx, g.dev, 0, d_Z + r0 * R, R, nb, nullptr, d_out, nullptr, (long)(g.n_pc + 1));
+    } else {  // (halved comb points encoded on the host where the comb applies; synchronous)
+      const int rc = msm_rows_host_enc(ctx, g.dev, d_Z + r0 * R, R, nb, nullptr, (long)(g.n_pc + 1), (uint8_t*)(out + r0));
       if (rc) return rc;
-      SPG_HIP(ctx, hipMemcpyAsync(out + r0, d_out, 32 * nb, hipMemcpyDeviceToHost, ctx->stream));
-      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));  // d_out is reused by the next chunk
     }
     if (trace2)
       fprintf(stderr, "[spg] commit rows=%zu R=%zu %s %.0f us\n", nb, R,
@@ -446,40 +462,64 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
   return 0;
 }
 
-int commit_rows_many(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs) {
-  auto merged = [&](const RowJob& j) { return j.R <= kSmallRowMax && j.L > kHostFinalRows && j.L <= 65535; };
-  size_t tot = 0;
+static bool rows_merged(const RowJob& j) { return j.R <= kSmallRowMax && j.L > kHostFinalRows && j.L <= 65535; }
+
+int commit_rows_many_launch(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs, RowsPending* p) {
+  p->tot = 0;
+  p->hv.clear();
   for (const RowJob& j : jobs) {
     if (j.R > g.n_pc) return set_err(ctx, SPG_E_ARG, "commit: rows wider than the generators");
-    if (merged(j)) tot += j.L;
+    if (rows_merged(j)) p->tot += j.L;
   }
-  if (tot) {
-    Ext* d_ext = (Ext*)ws_get(ctx, kWsMultiExt, tot * sizeof(Ext) + 64);
-    uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsMultiOut, 32 * tot + 64);
-    if (!d_ext || !d_out) return set_err(ctx, SPG_E_NOMEM, "commit rows");
-    size_t o = 0;
-    for (const RowJob& j : jobs) {
-      if (!merged(j)) continue;
-      int rc = rows_to_points(ctx, g, j.d_Z, j.R, j.L, d_ext + o);
-      if (rc) return rc;
-      o += j.L;
-    }
-    std::vector<Pt> rows(tot);
-    int rc = encode_points(ctx, d_ext, tot, rows.data(), d_out);
+  if (!p->tot) return 0;
+  p->d_ext = (Ext*)ws_get(ctx, kWsMultiExt, p->tot * sizeof(Ext) + 64);
+  p->d_out = (uint8_t*)ws_get(ctx, kWsMultiOut, 32 * p->tot + 64);
+  if (!p->d_ext || !p->d_out) return set_err(ctx, SPG_E_NOMEM, "commit rows");
+  size_t o = 0;
+  for (const RowJob& j : jobs) {
+    if (!rows_merged(j)) continue;
+    bool h = false;
+    const int rc = rows_to_points(ctx, g, j.d_Z, j.R, j.L, p->d_ext + o, &h);
     if (rc) return rc;
+    p->hv.push_back(h);
+    o += j.L;
+  }
+  return 0;
+}
+
+int commit_rows_many_finish(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs, RowsPending& p) {
+  if (p.tot) {  // the encodings of each run of merged jobs with the same form (halved comb points or not)
+    std::vector<Pt> rows(p.tot);
+    size_t k = 0, a = 0, o = 0;
+    for (const RowJob& j : jobs) {
+      if (!rows_merged(j)) continue;
+      o += j.L;
+      k++;
+      if (k == p.hv.size() || p.hv[k] != p.hv[k - 1]) {  // the run [a, o) ends here
+        const int rc = encode_points(ctx, p.d_ext + a, o - a, rows.data() + a, p.d_out + 32 * a, p.hv[k - 1] != 0);
+        if (rc) return rc;
+        a = o;
+      }
+    }
     o = 0;
     for (const RowJob& j : jobs) {
-      if (!merged(j)) continue;
+      if (!rows_merged(j)) continue;
       std::copy(rows.begin() + o, rows.begin() + o + j.L, j.out);
       o += j.L;
     }
   }
   for (const RowJob& j : jobs) {
-    if (merged(j)) continue;
+    if (rows_merged(j)) continue;
     int rc = commit_rows(ctx, g, j.d_Z, j.R, j.L, j.out);
     if (rc) return rc;
   }
   return 0;
+}
+
+int commit_rows_many(spg_ctx* ctx, ProverGens& g, const std::vector<RowJob>& jobs) {
+  RowsPending p;
+  const int rc = commit_rows_many_launch(ctx, g, jobs, &p);
+  return rc ? rc : commit_rows_many_finish(ctx, g, jobs, p);
 }
 
 // Hyrax rows split over the ranks of sh (SURVEY 8e "Hyrax commits: rows per GPU, allgather of the 32-byte

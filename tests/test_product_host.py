@@ -229,6 +229,16 @@ def test_host_ifma_sums_match_scalar(hc):
     assert bad == 0
 
 
+def test_host_double_and_compress_batch(hc):
+    """hcurve.hpp's batched encoding of doubles (one inversion for the batch) gives the bytes of the lone RFC 9496
+    encoding of 2 Q for 200 hash-to-group points, each also moved by the 2- and 4-torsion points (same Ristretto
+    element, other representatives), and for the identity and the torsion points (zero e g f h: the lone path)"""
+    rng = np.random.default_rng(12)
+    n = 200
+    uni = rng.integers(0, 256, 64 * n, dtype=np.uint8)
+    assert hc.spgh_dbl_compress_check(uni.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n)) == 0
+
+
 def _mont(x):
     R = 2**256
     v = x * R % Q
