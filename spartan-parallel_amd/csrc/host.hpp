@@ -154,7 +154,10 @@ inline void encode_halved_host(const Ext* d, size_t B, Pt* out) {
     thread_local std::vector<h::HExt> P;
     P.resize(hi - lo);
     for (size_t i = lo; i < hi; i++) P[i - lo] = h::hext_from_dev(d[i]);
-    h::hext_double_and_compress_batch(P.data(), hi - lo, reinterpret_cast<uint8_t(*)[32]>(out + lo));
+    if (h::ifma_on())  // 8 points per step on AVX-512 IFMA (~2.5x the scalar batch)
+      h::double_and_compress_batch8(P.data(), hi - lo, reinterpret_cast<uint8_t(*)[32]>(out + lo));
+    else
+      h::hext_double_and_compress_batch(P.data(), hi - lo, reinterpret_cast<uint8_t(*)[32]>(out + lo));
   };
   if (C == 1)
     enc(0);

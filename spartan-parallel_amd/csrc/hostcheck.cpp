@@ -214,11 +214,20 @@ int spgh_dbl_compress_check(const uint8_t* uni, size_t n) {
   }
   std::vector<uint8_t> got(32 * Q.size());
   h::hext_double_and_compress_batch(Q.data(), Q.size(), (uint8_t(*)[32])got.data());
+  std::vector<uint8_t> got8(32 * Q.size());
+  const bool vec = h::ifma_on();
+  if (vec) h::double_and_compress_batch8(Q.data(), Q.size(), (uint8_t(*)[32])got8.data());
   int bad = 0;
   for (size_t i = 0; i < Q.size(); i++) {
     uint8_t want[32];
     h::hext_compress(h::hext_dbl(Q[i]), want);
     bad += memcmp(want, got.data() + 32 * i, 32) != 0;
+    if (vec) bad += memcmp(want, got8.data() + 32 * i, 32) != 0;
+  }
+  // every length 1 .. 20 through the 8-lane form (partial groups)
+  for (size_t m = 1; vec && m <= 20 && m <= Q.size(); m++) {
+    h::double_and_compress_batch8(Q.data(), m, (uint8_t(*)[32])got8.data());
+    for (size_t i = 0; i < m; i++) bad += memcmp(got.data() + 32 * i, got8.data() + 32 * i, 32) != 0;
   }
   return bad;
 }

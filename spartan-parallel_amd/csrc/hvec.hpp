@@ -17,6 +17,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "hcurve.hpp"
 
 namespace spg {
@@ -149,7 +152,143 @@ SPG_IFMA HExt reduce(const Ext8& a) {
   return s[0];
 }
 
+SPG_IFMA Fe8 neg(const Fe8& a) { return sub(splat(fe_zero()), a); }
+SPG_IFMA Fe8 select(__mmask8 m, const Fe8& a, const Fe8& b) {  // lane l: m_l ? a : b
+  Fe8 r;
+  for (int i = 0; i < 5; i++) r.v[i] = _mm512_mask_blend_epi64(m, b.v[i], a.v[i]);
+  return r;
+}
+// fully reduced (canonical) limbs, as hcurve.hpp's fe_canon lane by lane: sequential carries, then p subtracted once
+// when the value is >= p
+SPG_IFMA Fe8 canon(const Fe8& x) {
+  const __m512i M = m51();
+  Fe8 a = x;
+  for (int pass = 0; pass < 2; pass++) {
+    for (int i = 0; i < 4; i++) {
+      a.v[i + 1] = _mm512_add_epi64(a.v[i + 1], _mm512_srli_epi64(a.v[i], 51));
+      a.v[i] = _mm512_and_si512(a.v[i], M);
+    }
+    a.v[0] = _mm512_add_epi64(a.v[0], times19(_mm512_srli_epi64(a.v[4], 51)));
+    a.v[4] = _mm512_and_si512(a.v[4], M);
+    a.v[1] = _mm512_add_epi64(a.v[1], _mm512_srli_epi64(a.v[0], 51));
+    a.v[0] = _mm512_and_si512(a.v[0], M);
+  }
+  __m512i q = _mm512_srli_epi64(_mm512_add_epi64(a.v[0], _mm512_set1_epi64(19)), 51);
+  for (int i = 1; i < 5; i++) q = _mm512_srli_epi64(_mm512_add_epi64(a.v[i], q), 51);
+  a.v[0] = _mm512_add_epi64(a.v[0], times19(q));
+  for (int i = 0; i < 4; i++) {
+    a.v[i + 1] = _mm512_add_epi64(a.v[i + 1], _mm512_srli_epi64(a.v[i], 51));
+    a.v[i] = _mm512_and_si512(a.v[i], M);
+  }
+  a.v[4] = _mm512_and_si512(a.v[4], M);
+  return a;
+}
+SPG_IFMA __mmask8 is_negative(const Fe8& a) {
+  return _mm512_test_epi64_mask(canon(a).v[0], _mm512_set1_epi64(1));
+}
+SPG_IFMA __mmask8 is_zero(const Fe8& a) {
+  const Fe8 c = canon(a);
+  __m512i o = c.v[0];
+  for (int i = 1; i < 5; i++) o = _mm512_or_si512(o, c.v[i]);
+  return _mm512_cmpeq_epi64_mask(o, _mm512_setzero_si512());
+}
+
 }  // namespace v8
+
+// hcurve.hpp's hext_double_and_compress_batch with 8 points per step: lane l of every step takes the points l, l + 8,
+// ..., its own chain of prefix products; the 8 lane products are inverted together (scalar Montgomery trick, one
+// inversion), then the backward pass and the encodings run 8 points per step. Lanes whose e g f h vanishes take the
+// lone encoding of 2 P. Same bytes (tests/test_product_host.py::test_host_double_and_compress_batch).
+SPG_IFMA_FN inline void double_and_compress_batch8(const HExt* P, size_t n, uint8_t (*out)[32]) {
+  using namespace v8;
+  if (!n) return;
+  const size_t G = (n + 7) / 8;
+  struct St8 {
+    Fe8 e, f, g, h, eg, fh, efgh, pre;
+    __mmask8 zero;
+  };
+  // per-thread scratch, 64-byte aligned by hand (a std::vector of a 64-byte-aligned type is not aligned here: its
+  // allocation is instantiated outside this target's code)
+  thread_local St8* st = nullptr;
+  thread_local size_t cap = 0;
+  if (G > cap) {
+    free(st);
+    cap = std::max<size_t>(G, 16);
+    st = (St8*)aligned_alloc(64, cap * sizeof(St8));
+    if (!st) {
+      cap = 0;
+      for (size_t i = 0; i < n; i++) hext_compress(hext_dbl(P[i]), out[i]);
+      return;
+    }
+  }
+  const Fe8 one = splat(fe_one()), d = splat(K().d), sqrt_m1 = splat(K().sqrt_m1),
+            isqrt_amd = splat(K().invsqrt_a_minus_d);
+  Fe8 run = one;
+  for (size_t k = 0; k < G; k++) {
+    alignas(64) uint64_t ad[8];
+    for (int l = 0; l < 8; l++) ad[l] = (uint64_t)&P[std::min(8 * k + l, n - 1)];  // the last group repeats a point
+    const __m512i addr = _mm512_load_si512((const void*)ad);
+    const Fe8 X = gather(addr, 0), Y = gather(addr, 5), Z = gather(addr, 10), T = gather(addr, 15);
+    const Fe8 XX = mul(X, X), YY = mul(Y, Y), ZZ = mul(Z, Z), dTT = mul(mul(T, T), d);
+    St8& s = st[k];
+    s.e = mul(X, add(Y, Y));
+    s.f = add(ZZ, dTT);
+    s.g = add(YY, XX);
+    s.h = sub(ZZ, dTT);
+    s.eg = mul(s.e, s.g);
+    s.fh = mul(s.f, s.h);
+    s.efgh = mul(s.eg, s.fh);
+    s.zero = is_zero(s.efgh);
+    s.pre = run;
+    run = mul(run, select(s.zero, one, s.efgh));
+  }
+  // the 8 lane products' inverses (Montgomery's trick over the lanes, one inversion)
+  Fe lp[8], pre[8], li[8];
+  Fe acc = fe_one();
+  for (int l = 0; l < 8; l++) {
+    lp[l] = lane(run, l);
+    pre[l] = acc;
+    acc = fe_mul(acc, lp[l]);
+  }
+  Fe inv = fe_invert(acc);
+  for (int l = 7; l >= 0; l--) {
+    li[l] = fe_mul(inv, pre[l]);
+    inv = fe_mul(inv, lp[l]);
+  }
+  alignas(64) uint64_t w[5][8];
+  for (int i = 0; i < 5; i++)
+    for (int l = 0; l < 8; l++) w[i][l] = li[l].v[i];
+  Fe8 inv8;
+  for (int i = 0; i < 5; i++) inv8.v[i] = _mm512_load_si512((const void*)w[i]);
+  for (size_t k = G; k-- > 0;) {
+    const St8& s = st[k];
+    const Fe8 inv_i = mul(inv8, s.pre);
+    inv8 = mul(inv8, select(s.zero, one, s.efgh));
+    const Fe8 Zinv = mul(s.eg, inv_i), Tinv = mul(s.fh, inv_i);
+    const __mmask8 m1 = is_negative(mul(s.eg, Zinv));
+    const Fe8 e = select(m1, s.g, s.e), g = select(m1, neg(s.e), s.g), h = select(m1, mul(s.f, sqrt_m1), s.h),
+              magic = select(m1, sqrt_m1, isqrt_amd);
+    const __mmask8 m2 = is_negative(mul(mul(h, e), Zinv));
+    const Fe8 g2 = select(m2, neg(g), g);
+    Fe8 r = mul(sub(h, g2), mul(magic, mul(g2, Tinv)));
+    r = select(is_negative(r), neg(r), r);
+    const Fe8 c = canon(r);
+    alignas(64) uint64_t cw[5][8];
+    for (int i = 0; i < 5; i++) _mm512_store_si512((void*)cw[i], c.v[i]);
+    for (int l = 0; l < 8 && 8 * k + l < n; l++) {
+      uint8_t* o = out[8 * k + l];
+      if ((s.zero >> l) & 1) {  // the lone path (identity representatives)
+        hext_compress(hext_dbl(P[8 * k + l]), o);
+        continue;
+      }
+      const uint64_t q0 = cw[0][l] | (cw[1][l] << 51), q1 = (cw[1][l] >> 13) | (cw[2][l] << 38),
+                     q2 = (cw[2][l] >> 26) | (cw[3][l] << 25), q3 = (cw[3][l] >> 39) | (cw[4][l] << 12);
+      const uint64_t q[4] = {q0, q1, q2, q3};
+      for (int i = 0; i < 4; i++)
+        for (int b = 0; b < 8; b++) o[8 * i + b] = (uint8_t)(q[i] >> (8 * b));
+    }
+  }
+}
 
 // sum of n affine Niels entries (pointers), from the identity; entries of lanes past the end are the identity's
 // Niels form (1, 1, 0), whose mixed addition leaves a point unchanged (projectively)
