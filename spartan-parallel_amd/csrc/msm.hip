@@ -638,8 +638,10 @@ static void bullet_comb_shape(int P, int* G, int* BS, int* R) {
   // R: round 4 chose 8 on device time alone; on the prover's wall clock the host's part sums weigh more (91 ns per
   // addition on the box, K <= 4 chunks per MSM: scripts/micro/parts_finals_cpu.cpp, profiles/r05_parts_finals.txt),
   // and R = 2 was fastest (2-rep A/B, SNARK median ms: R 8: 16.66 / 17.13, 2: 16.08 / 16.13, 1: 17.56 / 16.71); with the
-  // IFMA part sums (hvec.hpp) R = 4 is (ABBA A/B: 15.23 / 15.93 / 16.39 / 15.67 -> 15.13 / 15.04 / 15.84 / 15.02)
-  *R = P >= 2048 ? 1 : 4;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
+  // IFMA part sums (hvec.hpp) R = 4 was (ABBA A/B: 15.23 / 15.93 / 16.39 / 15.67 -> 15.13 / 15.04 / 15.84 / 15.02), and
+  // later in the round R = 8 (ABBA, 3 blocks: mean 16.03 -> 15.34 ms, device busy 8.65 -> 8.53 ms; R = 16 15.29 against
+  // 15.40; profiles/r05_ab_bcomb_r8.txt)
+  *R = P >= 2048 ? 1 : 8;  // the SPARK PolyEvalProofs at 2^24 nonzeros (P = 4096): 256 workgroups per MSM
   if (eg == 4 || eg == 8 || eg == 11) *G = eg;
   if (ebs == 64 || ebs == 128 || ebs == 256) *BS = ebs;
   if (er >= 1 && er <= *BS / 4 && (er & (er - 1)) == 0) *R = er;
