@@ -397,7 +397,7 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
   if (rc) return rc;
   const size_t per = n + (d_blind ? 1 : 0);
   // window groups per scalar (a lane's chain is W / G mixed additions) and workgroups: ~4 waves per SIMD
-  static const size_t gsel = getenv("SPG_BIG_COMB_G") ? (size_t)atol(getenv("SPG_BIG_COMB_G")) : 4;
+  static const size_t gsel = getenv("SPG_BIG_COMB_G") ? (size_t)atol(getenv("SPG_BIG_COMB_G")) : 2;
   const size_t G = gsel == 1 || gsel == 2 ? gsel : 4, spw = 256 / G;
   const size_t S = std::max<size_t>(1, (per + spw - 1) / spw);
   void* d_map = nullptr;

@@ -392,10 +392,12 @@ int msm_single_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq
 // sum_i s_i G[gen_offset + i] (+ blind h) of n device scalars, into *out (host point)
 int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n,
                    const Fq* d_blind, h::HExt* out) {
-  // SPG_BIG_COMB=1: large MSMs over a generator set that can keep a comb table (comb.hip; <= 2^16 generators, 47 GB
-  // at c = 9) take it -- no digit sort, no bucket reduction. Off by default: same-box A/B at 2^16 points, 0.204-0.209
-  // ms per call for the buckets below against 0.210-0.213 ms (profiles/r04_ab_combwgs_bigcomb.txt)
-  static const bool comb_on = getenv("SPG_BIG_COMB") && atoi(getenv("SPG_BIG_COMB")) != 0;
+  // Large MSMs over a generator set that can keep a comb table (comb.hip; <= 2^16 generators, 47 GB at c = 9, 62 GB
+  // with 128-byte entries) take it -- no digit sort, no bucket reduction (SPG_BIG_COMB=0: the buckets below). Round 4
+  // measured the comb level with the buckets (0.210-0.213 against 0.204-0.209 ms, profiles/r04_ab_combwgs_bigcomb.txt);
+  // with the entries padded to one line and the parts summed on the host's IFMA lanes it is ahead: 0.171-0.179 ms with
+  // 4 window groups per scalar, 0.146 ms with 2 (SPG_BIG_COMB_G), against 0.204-0.206 ms (profiles/r05_ab_big_comb.txt)
+  static const bool comb_on = !getenv("SPG_BIG_COMB") || atoi(getenv("SPG_BIG_COMB")) != 0;
   if (comb_on && n >= ((size_t)1 << 14)) {
     const int rc = msm_single_comb(ctx, g, gen_offset, d_scalars, n, d_blind, out);
     if (rc != 1) return rc;

@@ -188,15 +188,17 @@ def gens_big(ctx):
 
 
 def test_msm_big_edge_and_skew(ctx, oracle, gens_big):
-    """one MSM larger than the latency path (msm_big.hip's bucket pipeline, the default): edge scalars, an all-zero
-    stretch, a bucket holding most entries (one scalar repeated: its digits pile into a few buckets, which split into
-    many chunks), a blind, and a generator offset, against the oracle"""
+    """one MSM larger than the latency path (the default: comb.hip msm_single_comb, c = 9 windows over the 20001-slot
+    comb table, two window groups per scalar): edge scalars, an all-zero stretch, one scalar repeated (a skewed
+    distribution), a blind, and a generator offset, against the oracle"""
     edge_and_skew_checks(oracle, gens_big)
 
 
-def test_msm_single_comb_edge_and_skew():
-    """the same checks through the comb table (SPG_BIG_COMB=1: comb.hip msm_single_comb, c = 9 windows over the
-    20001-slot table), in a fresh process that reads the switch"""
+@pytest.mark.parametrize("env", [{"SPG_BIG_COMB": "0"}, {"SPG_BIG_COMB_G": "4"}, {"SPG_BIG_COMB_G": "1"}])
+def test_msm_single_comb_edge_and_skew(env):
+    """the same checks through msm_big.hip's bucket pipeline (SPG_BIG_COMB=0: a bucket holding most entries splits
+    into many chunks) and through the comb with 4 or 1 window groups per scalar, in a fresh process that reads the
+    switch"""
     import subprocess
     import sys
 
@@ -209,8 +211,8 @@ def test_msm_single_comb_edge_and_skew():
         "edge_and_skew_checks(pyoracle, spg.Gens(ctx, 20000, b'spg_big_msm'))\n"
         "print('ok')\n"
     ) % (os.path.join(root, "spartan-parallel_amd"), os.path.join(root, "oracle"), os.path.join(root, "tests"))
-    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SPG_BIG_COMB="1"), capture_output=True,
-                         text=True, timeout=240)
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                         timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.split()[-1] == "ok"
 
