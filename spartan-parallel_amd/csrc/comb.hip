@@ -341,7 +341,8 @@ int msm_comb(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_sca
   static const size_t want = getenv("SPG_COMB_WGS") ? (size_t)atol(getenv("SPG_COMB_WGS")) : 2048;
   // window groups per scalar: few rows get up to 4 lanes per scalar (>= 2^17 lanes when there are that few)
   static const size_t gmax = getenv("SPG_COMB_GMAX") ? (size_t)atol(getenv("SPG_COMB_GMAX")) : 4;
-  size_t G = 1;
+  static const size_t gmin = getenv("SPG_COMB_GMIN") ? (size_t)atol(getenv("SPG_COMB_GMIN")) : 1;
+  size_t G = gmin == 2 || gmin == 4 ? gmin : 1;
   while (G < gmax && G < 4 && B * per * G < ((size_t)1 << 17)) G *= 2;
   const size_t spw = 256 / G;
   const size_t S = std::max<size_t>(1, std::min((want + B - 1) / B, (per + spw - 1) / spw));
