@@ -122,10 +122,15 @@ class Merlin {
     meta_len(label, (uint32_t)n);
     op(kI | kA | kC);
     uint8_t* d = (uint8_t*)dst;
-    for (size_t i = 0; i < n; i++) {
-      d[i] = s_.get(pos_);
-      s_.put(pos_, 0);
-      if (++pos_ == kR) run_f();
+    uint8_t* st = reinterpret_cast<uint8_t*>(s_.a);
+    while (n) {  // runs of bytes up to the end of the rate: copied out, then zeroed (PRF output, STROBE's "I" flag)
+      const size_t c = n < (size_t)(kR - pos_) ? n : (size_t)(kR - pos_);
+      memcpy(d, st + pos_, c);
+      memset(st + pos_, 0, c);
+      pos_ = (uint8_t)(pos_ + c);
+      d += c;
+      n -= c;
+      if (pos_ == kR) run_f();
     }
   }
 
