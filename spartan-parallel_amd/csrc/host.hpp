@@ -145,10 +145,12 @@ inline Pt compress(const h::HExt& p) {
   return c;
 }
 // encodings of B device points that are halves (a comb MSM with halved scalars: encode(2 P') = encode(P)), as the
-// doubles' batched encodings on the pool (hext_double_and_compress_batch), chunks of >= 32 points, one inversion each
+// doubles' batched encodings (hext_double_and_compress_batch), on the pool in chunks of >= 64 points (one inversion each)
 inline void encode_halved_host(const Ext* d, size_t B, Pt* out) {
   static_assert(sizeof(Pt) == 32, "Pt is the 32-byte encoding");
-  const int C = (int)std::max<size_t>(1, std::min<size_t>(B / 32, (size_t)pool().size() + 1));
+  // (batches under 384 points stay on the calling thread: a 128-point batch took 84-99 us through a pool burst inside
+  // config 4's R1CSProof, against 34 us single-threaded in scripts/micro/enc_batch.cpp)
+  const int C = B < 384 ? 1 : (int)std::max<size_t>(1, std::min<size_t>(B / 64, (size_t)pool().size() + 1));
   auto enc = [&](int c) {
     const size_t lo = B * c / C, hi = B * (c + 1) / C;
     thread_local std::vector<h::HExt> P;

@@ -1423,7 +1423,7 @@ int spg::msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars,
   hipStream_t s = ctx->stream;
   const size_t tot = B * (n + (d_blinds ? 1 : 0));
   const bool comb = B >= 64 && (n <= 1024 ? tot >= ((size_t)1 << 14) : (n <= 16384 && tot >= ((size_t)1 << 22)));
-  if (halve && comb) {
+  if (halve && comb && B >= 384) {  // (fewer rows: spark.hip kHalvedMin)
     Ext* ext = (Ext*)ws_get(ctx, 17, B * sizeof(Ext) + 64);
     if (!ext) return set_err(ctx, SPG_E_NOMEM, "msm comb points");
     const int hi = !d_blinds ? -1 : (h_index < 0 ? (int)g->n : (int)h_index);

@@ -351,9 +351,16 @@ static int encode_points(spg_ctx* ctx, const Ext* d_ext, size_t B, Pt* out, uint
   if (halved) {
     Ext* h = (Ext*)enc_stage_get(ctx, B * sizeof(Ext));
     if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
+    static const bool tr3 = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 3;
+    const auto t0 = std::chrono::steady_clock::now();
     SPG_HIP(ctx, hipMemcpyAsync(h, d_ext, B * sizeof(Ext), hipMemcpyDeviceToHost, ctx->stream));
     SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const auto t1 = std::chrono::steady_clock::now();
     encode_halved_host(h, B, out);
+    if (tr3)
+      fprintf(stderr, "[spg] halved encodings of %zu points: device + download %.0f us, host %.0f us\n", B,
+              std::chrono::duration<double, std::micro>(t1 - t0).count(),
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count());
     return 0;
   }
   if (B <= host_max) {
@@ -380,9 +387,14 @@ static int encode_points(spg_ctx* ctx, const Ext* d_ext, size_t B, Pt* out, uint
 
 // L rows of R device scalars on the latency-path generators into device points: the comb tables when they apply
 // (>= 64 rows, >= 2^14 scalars in all), else the latency-path bucket kernels
-// (*halved: the comb path left P / 2, encode_points' halved form; SPG_HALVED_ENC=0 keeps the device encodings)
-static int rows_to_points(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Ext* d_ext, bool* halved) {
-  static const bool halve = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
+// (*halved: the comb path left P / 2, encode_points' halved form, when `want` -- batches of >= kHalvedMin points: below
+// that the host's lone encodings on the pool were as fast in the prover, 142 against 190 us for 128 rows;
+// SPG_HALVED_ENC=0 keeps the device / lone encodings everywhere)
+static const size_t kHalvedMin = 384;
+static int rows_to_points(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, Ext* d_ext, bool* halved,
+                          bool want) {
+  static const bool on = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
+  const bool halve = on && want;
   *halved = false;
   if (L >= 64 && L * R >= ((size_t)1 << 14)) {
     const int rc = msm_comb(ctx, g.dev, 0, d_Z, R, L, nullptr, nullptr, -1, d_ext, halve);
@@ -405,13 +417,15 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
   uint8_t* d_out = (uint8_t*)ws_get(ctx, kWsCommit, 32 * chunk + 64);
   if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit out");
   static const bool trace2 = getenv("SPG_TRACE") && atoi(getenv("SPG_TRACE")) >= 2;
-  // SPG_HOST_COMMIT_MAX (256): row batches of at most this many scalars in all are committed on the host pool against
+  // SPG_HOST_COMMIT_MAX (default 0: off): row batches of at most this many scalars are committed on the host pool against
   // the generators' fixed-base byte tables (HostGens, built once per generator set): the scalars come down (<= 32 KB)
   // and 32 mixed additions per scalar spread over the pool, instead of a device bucket launch, its host finals and a
   // synchronisation (8 scalars: 35-40 us against 44-49 us; 256: 69 against 79 us; 512 scalars already take longer there,
-  // 115 against 86 us, profiles/r05_ab_host_commit.txt)
+  // 115 against 86 us, profiles/r05_ab_host_commit.txt). Off: a generator's table is built on its first use (11-24 ms
+  // for the 8- and 16-generator rows of config 4's first proof), and config 4 measured 4.03 against 3.86 ms with it
+  // (ABBA, profiles/r05_ab_host_commit_c4.txt)
   static const size_t host_commit_max =
-      getenv("SPG_HOST_COMMIT_MAX") ? (size_t)atol(getenv("SPG_HOST_COMMIT_MAX")) : 256;
+      getenv("SPG_HOST_COMMIT_MAX") ? (size_t)atol(getenv("SPG_HOST_COMMIT_MAX")) : 0;
   for (size_t r0 = 0; r0 < L; r0 += chunk) {
     size_t nb = std::min(chunk, L - r0);
     auto t0 = std::chrono::steady_clock::now();
@@ -447,7 +461,7 @@ int commit_rows(spg_ctx* ctx, ProverGens& g, const Fq* d_Z, size_t R, size_t L, 
       Ext* d_ext = (Ext*)ws_get(ctx, kWsCommitExt, sizeof(Ext) * nb + 64);
       if (!d_ext) return set_err(ctx, SPG_E_NOMEM, "commit points");
       bool halved = false;
-      int rc = rows_to_points(ctx, g, d_Z + r0 * R, R, nb, d_ext, &halved);
+      int rc = rows_to_points(ctx, g, d_Z + r0 * R, R, nb, d_ext, &halved, nb >= kHalvedMin);
       if (!rc) rc = encode_points(ctx, d_ext, nb, out + r0, d_out, halved);  // synchronous: d_ext, d_out reused next chunk
       if (rc) return rc;
     } else {  // (halved comb points encoded on the host where the comb applies; synchronous)
@@ -479,7 +493,7 @@ int commit_rows_many_launch(spg_ctx* ctx, ProverGens& g, const std::vector<RowJo
   for (const RowJob& j : jobs) {
     if (!rows_merged(j)) continue;
     bool h = false;
-    const int rc = rows_to_points(ctx, g, j.d_Z, j.R, j.L, p->d_ext + o, &h);
+    const int rc = rows_to_points(ctx, g, j.d_Z, j.R, j.L, p->d_ext + o, &h, p->tot >= kHalvedMin);
     if (rc) return rc;
     p->hv.push_back(h);
     o += j.L;

@@ -109,7 +109,7 @@ ROUND_FORMS = {
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
     "comb_13_bit_windows": {"SPG_COMB_C": "13"},
     "comb_packed_entries": {"SPG_COMB_PAD": "0"},
-    "tiny_row_commits_on_device": {"SPG_HOST_COMMIT_MAX": "0"},
+    "tiny_row_commits_on_host": {"SPG_HOST_COMMIT_MAX": "256"},
     "row_encodings_on_device": {"SPG_HALVED_ENC": "0"},
     "tree_levels_per_launch": {"SPG_TREE_TOP": "0"},
     "tree_one_launch": {"SPG_TREE_TOP": str(1 << 40)},
@@ -133,8 +133,8 @@ def test_round_forms(form):
     wherever they fit (SPG_TRIPLE_MAX, SPG_STEP_COSTS: up to 1536 elements, 1024-thread workgroups) and pairs preferred
     before the triples (a triple applying two pending folds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
     the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds, and comb entries packed at
-    96 bytes (SPG_COMB_PAD=0) instead of one 128-byte line each; row commitments of at most 1024 scalars on the device
-    (SPG_HOST_COMMIT_MAX=0) instead of the host pool; comb row commitments encoded by k_compress_ext
+    96 bytes (SPG_COMB_PAD=0) instead of one 128-byte line each; row commitments of at most 256 scalars on the host pool
+    (SPG_HOST_COMMIT_MAX=256) instead of the device; comb row commitments encoded by k_compress_ext
     (SPG_HALVED_ENC=0) instead of from halved points as the host's batched encodings of doubles; SPARK product trees one
     level per launch (SPG_TREE_TOP=0) or every level in the per-circuit workgroup launch; the device Bullet proofs' delta
     on the bucket MSM (SPG_DELTA_COMB=0) instead of the comb parts"""
