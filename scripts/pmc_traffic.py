@@ -27,7 +27,7 @@ NAMES = {
     "k_layer_eval": "spark_layer_eval", "k_layer_tiny": "spark_layer_tiny", "k_fold_many": "spark_fold", "k_seg_dot": "spark_evaluate",
     "k_gather": "spark_deref", "k_bound_rows": "spark_bound", "k_dot3": "spark_dotp_eval",
     "k_tree_level": "spark_product_tree", "k_tree_top": "spark_product_tree", "k_hash_ops": "spark_hash_layer",
-    "k_layer_pair": "spark_layer_pair",
+    "k_layer_pair": "spark_layer_pair", "k_layer_triple": "spark_layer_triple",
     "k_layer_round_q": "spark_layer_round", "k_layer_round": "spark_layer_round", "k_layer_close": "spark_layer_close",
     "k_bullet_round_q": "msm_bullet_round", "k_big_accum": "msm_big_accum", "k_big_digits": "msm_big_sort",
     "k_big_scatter": "msm_big_sort", "k_smsm_bucket_q": "msm_small_bucket", "k_digits_rows": "msm_digits_rows",
