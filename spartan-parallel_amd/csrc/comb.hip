@@ -245,7 +245,11 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   static const size_t cap = (size_t)(cap_set ? atof(getenv("SPG_COMB_GB")) : 144.0) * (1ull << 30);
   // entries padded to one 128-byte line each (SPG_COMB_PAD, default on) where the padded table fits: a 96-byte entry
   // gathered at random straddles two lines two times in three (~2x the algorithmic bytes, PMC-measured)
+  // Padded tables up to SPG_COMB_PAD_GB (default 64: the 1024-generator tables, 5.9 GB, and config 2's 2^16-generator
+  // one, 62 GB); larger ones stay packed -- the config-5 derefs tables run at the madd peak already, and a 93 GB padded
+  // 12-bit fallback beside another process's table left two ranks sharing one GPU without room for their workspaces
   static const bool pad_on = !getenv("SPG_COMB_PAD") || atoi(getenv("SPG_COMB_PAD")) != 0;
+  static const size_t pad_max = (size_t)(getenv("SPG_COMB_PAD_GB") ? atof(getenv("SPG_COMB_PAD_GB")) : 64.0) * (1ull << 30);
   auto table_bytes = [&](int c, int st) { return (size_t)(253 / c + 1) * NS * ((size_t)1 << (c - 1)) * 32 * st; };
   auto fits = [&](size_t bytes) {
     if (g_comb_bytes.load() + bytes > cap) return false;
@@ -263,7 +267,7 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   int C = 0, st = 0;
   const int cands[4][2] = {{C0, 4}, {C0, 3}, {12, 4}, {12, 3}};
   for (int i = 0; i < (C0 > 12 ? 4 : 2) && !st; i++)
-    if ((cands[i][1] == 3 || pad_on) && fits(table_bytes(cands[i][0], cands[i][1]))) {
+    if ((cands[i][1] == 3 || (pad_on && table_bytes(cands[i][0], 4) <= pad_max)) && fits(table_bytes(cands[i][0], cands[i][1]))) {
       C = cands[i][0];
       st = cands[i][1];
     }
