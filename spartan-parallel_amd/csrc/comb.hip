@@ -31,10 +31,11 @@
 
 namespace spg {
 
-// window width: 12 (22 windows, 2048 multiples: 4.4 GB at 1024 generators); SPG_COMB_C = 10 / 11 trade more windows
-// for a smaller table, 13 forces the big tables' width (for tests at small sizes)
+// window width: 13 (20 windows, 4096 multiples: 10.7 GB at 1024 generators with 128-byte entries; the 1024 x 1024 row
+// batch 1.02 -> 0.93 ms against 12, profiles/r05_ab_comb_c13.txt); SPG_COMB_C = 10 .. 12 trade more windows for a
+// smaller table
 static int comb_c() {
-  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(13, atoi(getenv("SPG_COMB_C")))) : 12;
+  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(13, atoi(getenv("SPG_COMB_C")))) : 13;
   return c;
 }
 static constexpr int kCombRun = 64;                 // multiples per build lane

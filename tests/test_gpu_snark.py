@@ -107,7 +107,7 @@ ROUND_FORMS = {
     "layer_triples_everywhere": {"SPG_TRIPLE_MAX": "1536", "SPG_WIDE_MIN": str(1 << 40), "SPG_STEP_COSTS": "18,25,1"},
     "layer_triples_after_pairs": {"SPG_STEP_COSTS": "18,10,12"},
     "witness_parts_copied": {"SPG_WIT_IN_PLACE": "0"},
-    "comb_13_bit_windows": {"SPG_COMB_C": "13"},
+    "comb_12_bit_windows": {"SPG_COMB_C": "12"},
     "comb_packed_entries": {"SPG_COMB_PAD": "0"},
     "tiny_row_commits_on_host": {"SPG_HOST_COMMIT_MAX": "256"},
     "row_encodings_on_device": {"SPG_HALVED_ENC": "0"},
@@ -130,9 +130,9 @@ def test_round_forms(form):
     rounds one per launch (SPG_LAYER_PAIR=0) instead of two per launch where they are small, paired rounds over 64-thread
     workgroups (more of them: the ticketed sums and the last pair's corners from several workgroups), and pairs for every
     round that fits (SPG_PAIR_MAX, no throughput-form rounds); pairs without triples (SPG_LAYER_TRIPLE=0), triples
-    wherever they fit (SPG_TRIPLE_MAX, SPG_STEP_COSTS: up to 1536 elements, 1024-thread workgroups) and pairs preferred
-    before the triples (a triple applying two pending folds); comb tables of 13-bit windows (SPG_COMB_C=13, the width
-    the 2^14-generator derefs tables take) under the row commitments and the Bullet rounds, and comb entries packed at
+    wherever they fit (SPG_TRIPLE_MAX, SPG_STEP_COSTS: up to 384 elements, 96 workgroups) and pairs preferred
+    before the triples (a triple applying two pending folds); comb tables of 12-bit windows (SPG_COMB_C=12; the default
+    is 13) under the row commitments and the Bullet rounds, and comb entries packed at
     96 bytes (SPG_COMB_PAD=0) instead of one 128-byte line each; row commitments of at most 256 scalars on the host pool
     (SPG_HOST_COMMIT_MAX=256) instead of the device; comb row commitments encoded by k_compress_ext
     (SPG_HALVED_ENC=0) instead of from halved points as the host's batched encodings of doubles; SPARK product trees one
