@@ -31,12 +31,15 @@
 
 namespace spg {
 
-// window width: 13 (20 windows, 4096 multiples: 10.7 GB at 1024 generators with 128-byte entries; the 1024 x 1024 row
-// batch 1.02 -> 0.93 ms against 12, profiles/r05_ab_comb_c13.txt); SPG_COMB_C = 10 .. 12 trade more windows for a
-// smaller table
-static int comb_c() {
-  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(13, atoi(getenv("SPG_COMB_C")))) : 13;
-  return c;
+// window width of the tables up to kCombSmall generators: 13 (20 windows, 4096 multiples: 10.7 GB at 1024 generators
+// with 128-byte entries; the 1024 x 1024 row batch 1.02 -> 0.93 ms against 12, profiles/r05_ab_comb_c13.txt); of the
+// tables between that and kCombWide: 12 (config 5's ops / memory tables: at 13 they crowd its 2^14-generator derefs
+// table out of the memory cap, which then falls back to 12-bit windows, 183 -> 189 ms per proof). SPG_COMB_C = 10 .. 13
+// sets both.
+static constexpr size_t kCombSmall = 1024;
+static int comb_c(size_t slots) {
+  static const int c = getenv("SPG_COMB_C") ? std::max(10, std::min(13, atoi(getenv("SPG_COMB_C")))) : 0;
+  return c ? c : (slots <= kCombSmall ? 13 : 12);
 }
 static constexpr int kCombRun = 64;                 // multiples per build lane
 static constexpr size_t kCombMaxR = 65536;          // most generators a table covers
@@ -51,7 +54,7 @@ static int comb_c_for(size_t slots) {
   static const int cb = getenv("SPG_COMB_C_BIG") ? std::max(12, std::min(13, atoi(getenv("SPG_COMB_C_BIG")))) : 13;
   if (slots > kCombWide) return cw;
   if (slots == kCombBig && !getenv("SPG_COMB_C")) return cb;
-  return comb_c();
+  return comb_c(slots);
 }
 
 // lane L = ((w * NS + s) * runs + k): multiples k * Run + 1 .. (k + 1) * Run of 2^(c w) G_gen, gen = s (s < NS - 1)
