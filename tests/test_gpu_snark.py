@@ -132,7 +132,7 @@ def test_round_forms(form):
     round that fits (SPG_PAIR_MAX, no throughput-form rounds); pairs without triples (SPG_LAYER_TRIPLE=0), triples
     wherever they fit (SPG_TRIPLE_MAX, SPG_STEP_COSTS: up to 384 elements, 96 workgroups) and pairs preferred
     before the triples (a triple applying two pending folds); comb tables of 12-bit windows (SPG_COMB_C=12; the default
-    is 13) under the row commitments and the Bullet rounds, and comb entries packed at
+    is 13 up to 1024 generators) under the row commitments and the Bullet rounds, and comb entries packed at
     96 bytes (SPG_COMB_PAD=0) instead of one 128-byte line each; row commitments of at most 256 scalars on the host pool
     (SPG_HOST_COMMIT_MAX=256) instead of the device; comb row commitments encoded by k_compress_ext
     (SPG_HALVED_ENC=0) instead of from halved points as the host's batched encodings of doubles; SPARK product trees one
