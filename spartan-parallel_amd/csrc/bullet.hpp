@@ -173,6 +173,7 @@ struct BulletCombArgs {
   uint32_t* mb;
   uint32_t seq;
   int st;        // comb entry stride (32-byte coordinates)
+  unsigned long long* probe = nullptr;  // per-workgroup phase clocks (scripts/micro/bullet_comb_phases.hip), or null
 };
 
 __device__ __forceinline__ Fq fq_qbcast_lane(const Fq& a, int lane) {
@@ -186,16 +187,45 @@ __device__ __forceinline__ Fq fq_qbcast_lane(const Fq& a, int lane) {
   return o;
 }
 
+// The comb entries of windows w0 .. w0 + WG - 1 of canonical scalar k on generator slot s (signed C-bit digits):
+// ent[x] = entry index of window w0 + x | sign << 31, or ~0 for a zero digit or a window past the last (a short last
+// group). Selects, no branches: the recode sits on a Bullet round's latency path (scripts/micro/bullet_comb_phases:
+// recode + entry loads 2.5 -> 1.25 us against the shift-register form with its per-window branches).
+template <int C, int WG>
+__device__ __forceinline__ void comb_window_entries(const Fq& k, int w0, int s, int NS, uint32_t (&ent)[WG]) {
+  constexpr int W = 253 / C + 1, NB = 1 << (C - 1);
+  constexpr uint32_t MASK = (1u << C) - 1u;
+#pragma unroll
+  for (int x = 0; x < WG; x++) ent[x] = 0xffffffffu;
+  int carry = 0;
+  const uint32_t sb = (uint32_t)s * NB - 1u, wst = (uint32_t)NS * NB;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int bit = w * C;
+    const int li = bit >> 5, of = bit & 31;
+    uint32_t v = k.l[li] >> of;
+    if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
+    int d = (int)(v & MASK) + carry;
+    carry = d > NB ? 1 : 0;
+    d -= carry << C;
+    // (w NS + s) NB + |d| - 1, the sign in bit 31; all ones for d = 0
+    const uint32_t e = (w * wst + sb + (uint32_t)abs(d)) | ((uint32_t)d & 0x80000000u) | (uint32_t)-(int)(d == 0);
+#pragma unroll
+    for (int x = 0; x < WG; x++) ent[x] = w == w0 + x ? e : ent[x];
+  }
+}
+
 template <int C, int G, int BS>
 __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
-  constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
-  constexpr uint32_t MASK = (1u << C) - 1u;
+  constexpr int W = 253 / C + 1, WG = (W + G - 1) / G, S = BS / 4;
   __shared__ uint32_t pts[soa_words<Ext, S>()];
   __shared__ bool last;
   const int b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
   const int P = a.n / 2, nk = a.nk, nh = nk / 2;
   const int gq = blockIdx.x * S + slot;  // quad index within MSM b
   const int p = gq / G, jg = gq - p * G, w0 = jg * WG;
+  unsigned long long* pr = a.probe ? a.probe + 8 * (blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
   Ext acc = ext_identity();
   if (p < P) {
     const int blk = p / nh, off = p - blk * nh;
@@ -219,38 +249,21 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
       a.cw_out[j] = cv;
     }
     const Fq k = fq_mul(av, cv);  // canonical scalar (cw is a plain integer)
+    if (pr) { asm volatile("" ::"v"(k.l[0])); if (t == 0) pr[1] = wall_clock64(); }
     const int s = (int)a.gidx[j];
-    // signed C-bit digits; the entries of windows w0 .. w0 + WG - 1 shift into ent[] in window order (static
-    // register indices; a short last group leaves its leading slots empty)
     uint32_t ent[WG];
-#pragma unroll
-    for (int x = 0; x < WG; x++) ent[x] = 0xffffffffu;
-    int carry = 0;
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      const int bit = w * C;
-      const int li = bit >> 5, of = bit & 31;
-      uint32_t v = k.l[li] >> of;
-      if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
-      int d = (int)(v & MASK) + carry;
-      carry = d > NB ? 1 : 0;
-      d -= carry << C;
-      if (w >= w0 && w < w0 + WG) {
-#pragma unroll
-        for (int x = 0; x + 1 < WG; x++) ent[x] = ent[x + 1];
-        ent[WG - 1] = d == 0 ? 0xffffffffu
-                             : ((uint32_t)((w * a.NS + s) * NB + (d < 0 ? -d : d) - 1) | (d < 0 ? 0x80000000u : 0u));
-      }
-    }
+    comb_window_entries<C, WG>(k, w0, s, a.NS, ent);
     // every entry's coordinate in flight before the first addition
     Fp qv[WG];
     bool ng[WG];
 #pragma unroll
     for (int x = 0; x < WG; x++)
       if (ent[x] != 0xffffffffu) qv[x] = niels_coord(a.comb, ent[x], q, &ng[x], a.st);
+    if (pr) { asm volatile("" ::"v"(qv[WG - 1].l[0])); if (t == 0) pr[2] = wall_clock64(); }
 #pragma unroll
     for (int x = 0; x < WG; x++)
       if (ent[x] != 0xffffffffu) acc = quad_madd(acc, qv[x], ng[x], q);
+    if (pr) { asm volatile("" ::"v"(acc.X.l[0])); if (t == 0) pr[3] = wall_clock64(); }
   }
   for (int d = S / 2; d >= a.R; d >>= 1) {
     if (slot >= d && slot < 2 * d) quad_put_op<S>(pts, slot - d, acc, q);
@@ -258,6 +271,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
     if (slot < d) acc = quad_add_op(acc, quad_get_op<S>(pts, slot, q), q);
     __syncthreads();
   }
+  if (pr) { asm volatile("" ::"v"(acc.X.l[0])); if (t == 0) pr[4] = wall_clock64(); }
   if (slot < a.R && q == 0) a.parts[((size_t)b * gridDim.x + blockIdx.x) * a.R + slot] = acc;
   __syncthreads();
   if (t == 0) {
@@ -265,6 +279,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pr) pr[5] = wall_clock64();
     last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
            gridDim.x * gridDim.y - 1;
     if (last) {
@@ -272,6 +287,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
       __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       mbox_post(a.mb, a.seq, nullptr, 0);
     }
+    if (pr) pr[6] = wall_clock64();
   }
 }
 
@@ -282,8 +298,7 @@ template <int C, int G, int BS>
 __global__ void __launch_bounds__(BS) k_comb_msm_parts(const Fq* __restrict__ scalars, const uint32_t* __restrict__ idx,
                                                        int n, const Niels* __restrict__ comb, int NS, int R,
                                                        Ext* __restrict__ parts, int st) {
-  constexpr int W = 253 / C + 1, NB = 1 << (C - 1), WG = (W + G - 1) / G, S = BS / 4;
-  constexpr uint32_t MASK = (1u << C) - 1u;
+  constexpr int W = 253 / C + 1, WG = (W + G - 1) / G, S = BS / 4;
   __shared__ uint32_t pts[soa_words<Ext, S>()];
   const int b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
   const int gq = blockIdx.x * S + slot;
@@ -293,25 +308,7 @@ __global__ void __launch_bounds__(BS) k_comb_msm_parts(const Fq* __restrict__ sc
     const Fq k = fq_from_mont(scalars[(size_t)b * n + p]);
     const int s = (int)idx[(size_t)b * n + p];
     uint32_t ent[WG];
-#pragma unroll
-    for (int x = 0; x < WG; x++) ent[x] = 0xffffffffu;
-    int carry = 0;
-#pragma unroll
-    for (int w = 0; w < W; w++) {
-      const int bit = w * C;
-      const int li = bit >> 5, of = bit & 31;
-      uint32_t v = k.l[li] >> of;
-      if (of + C > 32 && li + 1 < 8) v |= k.l[li + 1] << (32 - of);
-      int d = (int)(v & MASK) + carry;
-      carry = d > NB ? 1 : 0;
-      d -= carry << C;
-      if (w >= w0 && w < w0 + WG) {
-#pragma unroll
-        for (int x = 0; x + 1 < WG; x++) ent[x] = ent[x + 1];
-        ent[WG - 1] = d == 0 ? 0xffffffffu
-                             : ((uint32_t)((w * NS + s) * NB + (d < 0 ? -d : d) - 1) | (d < 0 ? 0x80000000u : 0u));
-      }
-    }
+    comb_window_entries<C, WG>(k, w0, s, NS, ent);
     Fp qv[WG];
     bool ng[WG];
 #pragma unroll
