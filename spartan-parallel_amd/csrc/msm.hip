@@ -645,6 +645,10 @@ static void bullet_comb_shape(int P, int* G, int* BS, int* R) {
   if (eg == 4 || eg == 8 || eg == 11) *G = eg;
   if (ebs == 64 || ebs == 128 || ebs == 256) *BS = ebs;
   if (er >= 1 && er <= *BS / 4 && (er & (er - 1)) == 0) *R = er;
+  // the last rounds (P <= SPG_BCOMB_NOTREE): every quad its own part, no LDS tree (one level is a full quad addition,
+  // ~2.1 us on the round's latency path, scripts/micro/bullet_comb_phases) for at most 2 x 16 parts per MSM
+  static const int notree = getenv("SPG_BCOMB_NOTREE") ? atoi(getenv("SPG_BCOMB_NOTREE")) : 0;
+  if (P <= notree) *R = *BS / 4;
   // at most kBulletPartsMax parts per MSM (the host staging): fewer points per workgroup for the largest proofs
   const int wgs = (P * *G + *BS / 4 - 1) / (*BS / 4);
   while (*R > 1 && wgs * *R > kBulletPartsMax) *R /= 2;
