@@ -237,8 +237,13 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
       cv = fq_zero();
       cv.l[0] = 1u;  // cw = 1: the product below takes av out of Montgomery form
     } else {
-      // lanes 0, 1, 2: u a[ia], u^-1 a[ia + nk], cw[j] f; lane 3 repeats lane 0
-      const Fq x = q == 1 ? a.aa_in[ia + nk] : (q == 2 ? a.cw_in[j] : a.aa_in[ia]);
+      // lanes 0, 1, 2: u a[ia], u^-1 a[ia + nk], cw[j] f; lane 3 repeats lane 0. Every lane loads both operands
+      // and selects after: a per-lane choice between the by-value struct's two base pointers otherwise becomes a vector
+      // load of the pointer from the kernel arguments that the operand load waits on (one memory latency more on the
+      // round's path)
+      const Fq xa = a.aa_in[q == 1 ? ia + nk : ia];
+      const Fq xc = a.cw_in[j];
+      const Fq x = q == 2 ? xc : xa;
       const Fq y = q == 1 ? a.uinv : (q == 2 ? ((j & (2 * nk - 1)) < nk ? a.uinv : a.u) : a.u);
       const Fq r = fq_mul(x, y);
       av = fq_add(fq_qbcast_lane(r, 0), fq_qbcast_lane(r, 1));
