@@ -66,30 +66,73 @@ __device__ __forceinline__ void mac_ov(uint64_t& acc, uint32_t& ov, uint32_t a, 
   asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(ov), "=s"(cy) : "s"(cy));
 }
 #endif
+// A product-scanning column accumulator whose overflow additions trail their products by two: on gfx950 a VALU
+// write of the carry SGPR pair needs two wait states before a VALU reads it as carry-in, so mac_ov's v_addc right
+// after its v_mad_u64_u32 costs an s_nop per limb product; here the next two products fill those slots. flush()
+// before the column's ov is read. (Host: plain mac_ov.)
+struct MacAcc {
+  uint64_t acc = 0;
+  uint32_t ov = 0;
+  uint64_t c0 = 0, c1 = 0;  // carries of the last two products not yet added into ov (device)
+  int np = 0;               // how many (a compile-time constant once the column loops unroll)
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void mac_addc(uint32_t& ov, uint64_t cy) {
+  uint64_t d;
+  asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(ov), "=s"(d) : "s"(cy));
+}
+__device__ __forceinline__ void mac(MacAcc& m, uint32_t a, uint32_t b) {
+  uint64_t c;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(m.acc), "=s"(c) : "v"(a), "v"(b));
+  if (m.np == 2) {
+    mac_addc(m.ov, m.c0);
+    m.c0 = m.c1;
+    m.c1 = c;
+  } else if (m.np == 1) {
+    m.c1 = c;
+    m.np = 2;
+  } else {
+    m.c0 = c;
+    m.np = 1;
+  }
+}
+__device__ __forceinline__ void mac_flush(MacAcc& m) {
+  if (m.np >= 1) mac_addc(m.ov, m.c0);
+  if (m.np == 2) mac_addc(m.ov, m.c1);
+  m.np = 0;
+}
+#else
+inline void mac(MacAcc& m, uint32_t a, uint32_t b) { mac_ov(m.acc, m.ov, a, b); }
+inline void mac_flush(MacAcc&) {}
+#endif
+// column done: its low limb out, the accumulator shifted down with the overflow count on top
+SPG_HD uint32_t mac_next(MacAcc& m) {
+  mac_flush(m);
+  const uint32_t lo = (uint32_t)m.acc;
+  m.acc = (m.acc >> 32) | ((uint64_t)m.ov << 32);
+  m.ov = 0;
+  return lo;
+}
 // The device's product-scanning forms, compiled for the host too (through the host mac_ov above), so
 // tests/test_product_host.py checks them against the oracle without a GPU (fp ops 6 and 7 of hostcheck).
 // t[0..16) = a * b (8 x 32-bit limbs each), product scanning
 SPG_HD void mul_8x8(const uint32_t* a, const uint32_t* b, uint32_t* t) {
-  uint64_t acc = 0;
-  uint32_t ov = 0;
+  MacAcc m;
 #pragma unroll
   for (int k = 0; k < 15; k++) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j < 0 || j > 7) continue;
-      mac_ov(acc, ov, a[i], b[j]);
+      mac(m, a[i], b[j]);
     }
-    t[k] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)ov << 32);
-    ov = 0;
+    t[k] = mac_next(m);
   }
-  t[15] = (uint32_t)acc;
+  t[15] = (uint32_t)m.acc;
 }
 // t[0..16) = a^2: the 28 off-diagonal products once (product scanning), doubled, plus the 8 squares
 SPG_HD void sqr_8(const uint32_t* a, uint32_t* t) {
-  uint64_t acc = 0;
-  uint32_t ov = 0;
+  MacAcc m;
   t[0] = 0;
 #pragma unroll
   for (int k = 1; k < 14; k++) {
@@ -97,14 +140,12 @@ SPG_HD void sqr_8(const uint32_t* a, uint32_t* t) {
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j <= i || j > 7) continue;
-      mac_ov(acc, ov, a[i], a[j]);
+      mac(m, a[i], a[j]);
     }
-    t[k] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)ov << 32);
-    ov = 0;
+    t[k] = mac_next(m);
   }
-  t[14] = (uint32_t)acc;
-  t[15] = (uint32_t)(acc >> 32);
+  t[14] = (uint32_t)m.acc;
+  t[15] = (uint32_t)(m.acc >> 32);
 #pragma unroll
   for (int i = 15; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
   t[0] <<= 1;
@@ -208,31 +249,29 @@ SPG_HD void add_ov(uint64_t& acc, uint32_t& ov, uint64_t x) {
 SPG_HD Fq fq_mul_ps(const Fq& a, const Fq& b) {
   const uint32_t Q[4] = {SPG_Q0, SPG_Q1, SPG_Q2, SPG_Q3};
   uint32_t m[8], r[8];
-  uint64_t acc = 0;
-  uint32_t ov = 0;
+  MacAcc c;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
-      if (j >= 0 && j < 8) mac_ov(acc, ov, a.l[i], b.l[j]);
+      if (j >= 0 && j < 8) mac(c, a.l[i], b.l[j]);
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;  // m_i * q_j, j in 1..3 (q_0 is folded in below when m_k is fixed)
-      if (i < k && j >= 1 && j <= 3) mac_ov(acc, ov, m[i], Q[j]);
+      if (i < k && j >= 1 && j <= 3) mac(c, m[i], Q[j]);
     }
-    if (k >= 7 && k - 7 < 8) add_ov(acc, ov, (uint64_t)m[k - 7] << 28);  // m_{k-7} * q_7
+    if (k >= 7 && k - 7 < 8) add_ov(c.acc, c.ov, (uint64_t)m[k - 7] << 28);  // m_{k-7} * q_7
     if (k < 8) {
-      m[k] = (uint32_t)acc * SPG_QINV;
-      mac_ov(acc, ov, m[k], Q[0]);  // clears the low 32 bits
+      m[k] = (uint32_t)c.acc * SPG_QINV;
+      mac(c, m[k], Q[0]);  // clears the low 32 bits
+      mac_next(c);
     } else {
-      r[k - 8] = (uint32_t)acc;
+      r[k - 8] = mac_next(c);
     }
-    acc = (acc >> 32) | ((uint64_t)ov << 32);
-    ov = 0;
   }
-  return fq_cond_sub(r, (uint32_t)acc);
+  return fq_cond_sub(r, (uint32_t)c.acc);
 }
 
 // CIOS Montgomery product a*b*2^-256 mod q over 8 x 32-bit limbs (the device form: v_mad_u64_u32)
