@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Benchmark for the MI355X Spartan prover (libspg.so), one JSON line on rank 0.
 
-Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched under
-torch.distributed.run, one rank per GPU.
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 either launched under
+torch.distributed.run (WORLD_SIZE must equal N, or the run exits 2 before any work), or started plainly, in which case
+bench.py starts the N ranks itself (child processes, env:// rendezvous on 127.0.0.1, one GPU per LOCAL_RANK) before
+anything touches a GPU, and rank 0 prints the line.
 
 --workload snark (default, the headline metric): SNARK::prove (src/lib.rs:971-2746)
     on a synthetic 2^20-constraint program (2 block types x 2^9 executions x 2^10 constraints), instances
@@ -93,7 +95,7 @@ def parse():
                          "default: shard for --workload spark / msm, replicas otherwise")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl with a GPU)")
     ap.add_argument("--log-msm", type=int, default=16, help="msm: 2^k (scalar, generator) pairs")
-    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark", "msm", "rows"],
+    ap.add_argument("--workload", default="snark", choices=["snark", "r1cs", "spark", "msm", "rows", "launchcheck"],
                     help="snark: the headline metric (SNARK::prove, SURVEY 8d config 3); r1cs: its block "
                          "R1CSProof::prove alone; spark: SURVEY 8d config 5 (SPARK); msm: config 2; rows: config 2's "
                          "1024 x 1024 row batch")
@@ -144,6 +146,7 @@ class Env:
                 os.close(saved)
             self.dist = dist
         ndev = torch.cuda.device_count()
+        self.ndev = ndev
         self.gpu = self.local % ndev if ndev else self.local  # ranks share a GPU only in rehearsals
         if torch.cuda.is_available():
             torch.cuda.set_device(self.gpu)
@@ -374,6 +377,33 @@ def all_cores_baseline(fn, units, unit, sample):
             "sample": f"{k} concurrent independent copies of: {sample}; {dt:.2f} s wall"}
 
 
+def precomputation(c0, c1, note):
+    """the fixed-base tables a workload built (spg_comb_stats before / after its first steps): comb tables' HBM bytes
+    and build seconds, and the 2^k G_i tables of every live generator set"""
+    return {"comb_table_bytes": c1[0] - c0[0], "comb_tables_built": c1[1] - c0[1],
+            "comb_build_s": round(c1[2] - c0[2], 4), "gens_table_bytes_process": c1[3], "note": note}
+
+
+def no_table_leg(env, ctx, step, steps, warmup, outs):
+    """the same steps with this context's comb tables switched off (spg_set_comb 0: the bucket Pippenger pipelines
+    over the 2^k G_i tables), so the MSM comparison with the CPU's table-free vartime Pippenger can be read like for
+    like; the result must be the same bytes"""
+    ctx.set_comb(False)
+    try:
+        got = set()
+
+        def st():
+            r = step()
+            got.add(r if isinstance(r, bytes) else r.tobytes())
+            return r if isinstance(r, bytes) else r.tobytes()
+
+        dt, laps, _ = timed(env, st, steps, warmup)
+    finally:
+        ctx.set_comb(True)
+    return {"ms_per_step": round(dt / steps * 1e3, 3), "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
+            "same_result": got == outs, "path": "bucket Pippenger over the 2^k G_i tables (spg_set_comb 0)"}
+
+
 # ---------------------------------------------------------------- SNARK::prove (headline, config 3)
 def main_snark(a):
     """The headline metric (SURVEY 8d config 3): SNARK::prove (src/lib.rs:971-2746) on the synthetic program of
@@ -405,8 +435,18 @@ def main_snark(a):
         return spg.snark_prove(ctx, block, pairwise, perm_root, w, gens, spg.Transcript(b"snark_bench"),
                                spg.RandomTape(b"proof", seed))
 
+    comb0 = spg.comb_stats()
     dt, laps, proofs = timed(env, lambda: prove(wit), a.steps, a.warmup)
     assert len(proofs) == 1, "proof bytes changed between steps"
+    comb1 = spg.comb_stats()
+    # the drop-in mode: every append / challenge of the prove goes through C callbacks
+    # into a caller-owned merlin transcript (libspg_hostcheck's native merlin, as a Rust caller's extern "C" trampolines
+    # over &mut Transcript would) instead of libspg's own; same steps, timed the same way, right after the timed region
+    def prove_cb(w):
+        return spg.snark_prove(ctx, block, pairwise, perm_root, w, gens, spg.Transcript.from_native_merlin(b"snark_bench"),
+                               spg.RandomTape(b"proof", seed))
+
+    dt_cb, laps_cb, proofs_cb = timed(env, lambda: prove_cb(wit), a.steps, 1)
     prof = profile_pass(ctx, lambda: prove(wit), a.steps)
     # per-call input work of a drop-in SNARK::prove (it receives Vec<Vec<VarsAssignment>> on every call): the
     # witness upload (spg_snark_witness_new, PCIe + io-row parsing) + the prove, median of 5 (beside value)
@@ -484,7 +524,9 @@ def main_snark(a):
             "config": {"workload": "SNARK::prove (src/lib.rs:971-2746)", "block_types": 2,
                        "constraints_per_block": 1 << a.log_cons, "executions_per_block": 1 << a.log_proofs,
                        "constraints_per_gpu": N, "num_vars": wl.num_vars, "num_ios": wl.num_ios,
-                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{env.world}"},
+                       "gens": "R1CSGens(gens_r1cs_sat, 2^24)", "parallelism": f"replicas x{env.world}",
+                       "devices_visible": env.ndev, "ranks_share_a_gpu": env.world > env.ndev,
+                       "launcher": os.environ.get("SPG_BENCH_LAUNCHER") or ("torchrun" if env.world > 1 else None)},
             "roofline": roof, "roofline_hbm": roof_h, "roofline_valu": roof_v,
             "roofline_fq": roofline_fq(prof, a.traffic or TRAFFIC["snark"]),
             "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact,
@@ -493,6 +535,18 @@ def main_snark(a):
             "device_busy_incl_resident_ms_per_step": round(prof.busy_resident_us / a.steps / 1e3, 3),
             "value_incl_witness_upload": round(N * env.world / t_incl, 1),
             "ms_per_step_incl_witness_upload": round(t_incl * 1e3, 3),
+            "transcript_mode": {
+                "value": "native (libspg's own merlin transcript)",
+                "callback": {"transcript": "caller-owned merlin behind spg_transcript_new_callbacks (C callbacks, "
+                                           "libspg_hostcheck spgh_merlin_*)",
+                             "value": round(N * env.world * a.steps / dt_cb, 1),
+                             "ms_per_step": round(dt_cb / a.steps * 1e3, 3),
+                             "ms_per_step_median": round(sorted(laps_cb)[len(laps_cb) // 2] * 1e3, 3),
+                             "over_native": round(dt_cb / dt, 4), "same_bytes": proofs_cb == proofs}},
+            "precomputation": precomputation(
+                comb0, comb1, "fixed-base tables over the public generators, built once per generator set on first use "
+                              "(in the warmup steps here, outside value) and kept in HBM; the reference's SNARK::prove "
+                              "runs vartime MSMs without tables"),
             "ms_per_step_median": round(sorted(laps)[len(laps) // 2] * 1e3, 3),
             "ms_per_step_min": round(min(laps) * 1e3, 3), "verify_ms": round(t_verify * 1e3, 2),
             "ms_per_step_laps": [round(x * 1e3, 2) for x in laps],
@@ -506,8 +560,12 @@ def main_snark(a):
 
 def guarded(fn, env=None):
     """an extra config's result, or the error it raised (the headline line is printed either way). With several ranks
-    (env given) every rank learns whether any rank failed, so no rank goes on into a later collective alone; libspg's
-    own exchanges already fail every rank together (status-framed allgathers)."""
+    (env given) the ranks exchange a failure flag after fn. That keeps them in step when every rank fails together --
+    libspg's own exchanges fail all ranks at once (status-framed allgathers) -- or when a rank fails before fn's first
+    collective. A rank that fails between two of fn's torch collectives (the barrier or max-over-ranks of timed(), the
+    all_gather_object of the rank check) meets the others' next collective with this flag exchange instead; that can
+    hang or raise in the backend, and the launcher (or the driver's time limit) then ends the run: the guarantee does
+    not extend to that case."""
     try:
         out, err = fn(), None
     except Exception as e:  # noqa: BLE001
@@ -548,6 +606,7 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
         return spg.R1CSWitness(ctx, views.secs, wl.nws, shard=(p0, p1) if shard else None)
 
     wit = upload()
+    c0 = spg.comb_stats()
 
     def step():
         pf, _ = spg.r1cs_prove(ctx, gens, inst, wit, wl.P, wl.max_num_proofs, wl.num_proofs, wl.max_num_inputs,
@@ -555,6 +614,8 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
         return pf
 
     dt, laps, proofs = timed(env, step, steps, warmup)
+    pre = precomputation(c0, spg.comb_stats(), "comb tables over R1CSGens' generators, built in the first (warmup) "
+                                               "proof and kept in HBM; the CPU baseline uses no tables")
     if not shard:
         assert len(proofs) == 1, "proof bytes changed between steps"
     prof = profile_pass(ctx, step, steps)
@@ -606,6 +667,7 @@ def r1cs_core(env, ctx, cfg, shard, steps, warmup, cpu_on, traffic_file=None, co
         "roofline_fq": roofline_fq(prof, traffic_file), "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_bitexact_vs_cpu": bitexact, "proof_sha256": sorted(proofs)[0][:16],
         "ranks_agree": same, "transport": transport, "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
+        "precomputation": pre,
         "value_incl_witness_upload": round(units / t_incl, 1), "kernels": kernel_table(prof, steps)}
 
 
@@ -647,8 +709,12 @@ def rows_core(env, ctx, steps, warmup, cpu_on, traffic_file=None, log_rows=10, l
         outs.add(r.tobytes())
         return r.tobytes()
 
+    c0 = spg.comb_stats()
     dt, laps, _ = timed(env, step, steps, warmup)
     assert len(outs) == 1, "row commitments changed between steps"
+    pre = precomputation(c0, spg.comb_stats(), "comb table of MultiCommitGens(1024, spg_bench_rows), built in the first "
+                                               "(warmup) step and kept in HBM; the CPU baseline uses no tables")
+    no_tab = no_table_leg(env, ctx, step, steps, warmup, outs)
     prof = profile_pass(ctx, step, steps)
     roof, roof_h, roof_v = rooflines(prof, traffic_file)
     dev_us = prof.busy_us / steps
@@ -680,6 +746,7 @@ def rows_core(env, ctx, steps, warmup, cpu_on, traffic_file=None, log_rows=10, l
         "valu_whole_commit": {"madds_per_commit": madds, "device_us_per_commit": round(dev_us, 1),
                               "madds_per_s": round(madds / (dev_us * 1e-6), 1) if dev_us else None,
                               "frac_of_peak": round(madds / (dev_us * 1e-6) / MADD_PEAK, 4) if dev_us else None},
+        "precomputation": pre, "no_table": no_tab,
         "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "rows_bitexact_vs_cpu": bitexact,
         "rows_sha256": hashlib.sha256(sorted(outs)[0]).hexdigest()[:16], "kernels": kernel_table(prof, steps, top=8),
     }
@@ -756,7 +823,13 @@ def msm_core(env, ctx, log_msm, steps, warmup, cpu_on, traffic_file=None):
         outs_raw.add(r)
         return r
 
+    c0 = spg.comb_stats()
     dt, laps, _ = timed(env, step_keep, steps, warmup)
+    pre = precomputation(c0, spg.comb_stats(), "comb table of MultiCommitGens(2^k, spg_bench_msm) (c = 9 windows, "
+                                               "128-byte entries), built in the first (warmup) step and kept in HBM; the "
+                                               "CPU baseline is the table-free vartime Pippenger")
+    no_tab = no_table_leg(env, ctx, step, steps, warmup, outs_raw)
+
     def step_host():
         r = run(partial_host)
         outs_raw.add(r)
@@ -802,6 +875,7 @@ def msm_core(env, ctx, log_msm, steps, warmup, cpu_on, traffic_file=None):
         "valu_whole_msm": {"madds_per_msm": madds, "device_us_per_msm": round(dev_us, 1),
                            "madds_per_s": round(madds / (dev_us * 1e-6), 1) if dev_us else None,
                            "frac_of_peak": round(madds / (dev_us * 1e-6) / MADD_PEAK, 4) if dev_us else None},
+        "precomputation": pre, "no_table": no_tab,
         "cpu_baseline": cpu, "cpu_baseline_all_cores": cpu_all, "result_bitexact_vs_cpu": bitexact,
         "result": sorted(outs_raw)[0].hex(), "kernels": kernel_table(prof, steps, top=12),
     }
@@ -844,6 +918,7 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
     r = rng.integers(0, 1 << 63, size=(2 * k, 4), dtype=np.uint64)
     r[:, 3] &= np.uint64((1 << 60) - 1)
     rx, ry = r[:k], r[k:]
+    c0 = spg.comb_stats()
     t0 = time.perf_counter()
     comm = spg.SparkCommitment(ctx, views.inst, b"gens_r1cs_eval", wl.nnz, 3)
     t_commit = time.perf_counter() - t0
@@ -855,6 +930,9 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         return comm.prove(rx, ry, evals, spg.Transcript(b"spark_bench"), spg.RandomTape(b"proof", seed))
 
     dt, laps, proofs = timed(env, step, steps, warmup)
+    pre = precomputation(c0, spg.comb_stats(), "comb tables of the gens_r1cs_eval generator sets (comb_ops / comb_mem "
+                                               "rows at the commitment, the derefs rows in the first proof), kept in HBM; "
+                                               "the CPU baseline uses no tables")
     prof = profile_pass(ctx, step, steps)
     same = None
     if shard:  # every rank of one sharded proof must hold the same bytes, the same in every step
@@ -901,7 +979,7 @@ def spark_core(env, ctx, k, cpu_log_nnz, steps, warmup, mode, cpu_on, traffic_fi
         "roofline_fq": roofline_fq(prof, traffic_file), "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all, "proof_sha256": sorted(proofs)[0][:16], "ranks_agree": same,
         "transport": transport,
-        "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3),
+        "commit_s": round(t_commit, 3), "host_gen_s": round(t_gen, 3), "precomputation": pre,
         "device_busy_ms_per_step": round(prof.busy_us / steps / 1e3, 3),
         "kernels": kernel_table(prof, steps),
     }
@@ -932,9 +1010,94 @@ def main_rows(a):
     env.close()
 
 
+def main_launchcheck(a):
+    """the launcher's own check (tests/test_bench_launch.py, CPU): every rank joins the process group and rank 0
+    prints the world it saw and the sum of the ranks -- no libspg, no GPU"""
+    env = Env(a)
+    s = env.world * (env.world - 1) // 2
+    if env.dist is not None:
+        t = env.torch.tensor([float(env.rank)])
+        env.dist.all_reduce(t)
+        s = int(t.item())
+    if env.rank == 0:
+        print(json.dumps({"n_gpus": env.world, "rank_sum": s, "launcher": os.environ.get("SPG_BENCH_LAUNCHER")}))
+    env.close()
+
+
+# ---------------------------------------------------------------- N ranks without torchrun
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def child_envs(n, base, port):
+    """the torch.distributed env:// variables of n local ranks (one per GPU: LOCAL_RANK r drives GPU r)"""
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPG_BENCH_LAUNCHER="bench.py")
+        out.append(e)
+    return out
+
+
+def check_world(gpus, environ):
+    """a rank started by torchrun (WORLD_SIZE set) must be one of --gpus ranks: returns an error string or None"""
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return None
+    if not ws.isdigit() or int(ws) != gpus:
+        return f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}; launch --gpus N under torchrun with --nproc-per-node N"
+    return None
+
+
+def launch(gpus, argv):
+    """`bench.py --gpus N` with N > 1 and no torchrun: start N child ranks of this same command (one per GPU,
+    env:// rendezvous on 127.0.0.1) before anything here touches a GPU; rank 0's stdout is the line, the others'
+    goes to stderr. Returns the exit code: the first failing rank's, after the others are stopped."""
+    import signal
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r, e in enumerate(child_envs(gpus, os.environ, port)):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    signal.signal(signal.SIGTERM, lambda *x: (stop(), sys.exit(143)))
+    rc = 0
+    while procs and any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            stop()
+            break
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return rc
+
+
 def main():
     a = parse()
-    {"snark": main_snark, "r1cs": main_r1cs, "spark": main_spark, "msm": main_msm, "rows": main_rows}[a.workload](a)
+    err = check_world(a.gpus, os.environ)
+    if err:
+        print(err, file=sys.stderr)
+        sys.exit(2)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(a.gpus, sys.argv[1:]))
+    {"snark": main_snark, "r1cs": main_r1cs, "spark": main_spark, "msm": main_msm, "rows": main_rows,
+     "launchcheck": main_launchcheck}[a.workload](a)
 
 
 if __name__ == "__main__":

@@ -82,6 +82,16 @@ int spg_prof_read2(spg_ctx* ctx, char* names, long* launches, double* total_us, 
  * sumcheck evaluations and SPARK layer rounds, priced against the measured whole-GPU Fq product rate */
 int spg_prof_read3(spg_ctx* ctx, char* names, long* launches, double* total_us, double* bytes, double* ops,
                    double* fqm, int max, int reset);
+/* Fixed-base precomputation of this process: the HBM bytes of the comb tables currently allocated
+ * for every live generator set, the number of comb tables built so far and their total build time in seconds (device
+ * build + synchronisation, wall clock), and the HBM bytes of the 2^k G_i tables every generator set keeps (254 rows of
+ * n + 1 Niels points, built by spg_gens_derive / spg_gens_upload). Comb tables are built on first use of a generator
+ * set and live until spg_gens_free; the figures let a caller (bench.py) disclose the precomputation behind an
+ * MSM-throughput number. Any pointer may be NULL. */
+int spg_comb_stats(uint64_t* bytes, int* tables_built, double* build_seconds, uint64_t* gens_table_bytes);
+/* on = 0: this context's MSMs and row commitments skip the comb tables and run the bucket Pippenger pipelines (over
+ * the 2^k G_i generator tables only); on = 1 (default) restores them. Results are identical either way. */
+int spg_set_comb(spg_ctx* ctx, int on);
 
 /* ---- device-resident scalar vectors (HBM) ----------------------------------------------------
  * Tables the prover keeps resident between calls (witness polynomials, sumcheck tables). */

@@ -5,6 +5,11 @@
 #   BENCH=1     python bench.py $BENCH_ARGS > gpurun_out/${TAG}bench.json (T_BENCH, default 600 s)
 #   PROF=1      rocprofv3 --kernel-trace --stats of bench.py $PROF_ARGS (csv under gpurun_out/${TAG}prof)
 #   PMC=1       two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of bench.py $PROF_ARGS -> ${TAG}pmc_traffic.json
+#   TRACE=hipt  kernel + HIP runtime API + memory-copy trace of traced proves (scripts/trace_snark.py), lap events in
+#               gpurun_out/${TAG}kt.err (csv under gpurun_out/${TAG}kt)
+#   TRACE=gaps  kernel trace + host lap events of 6 proves -> per-prove idle gaps by transition and by host lap
+#               (scripts/kernel_gaps.py -> gpurun_out/${TAG}kt_gaps.txt; MARK: the kernel that opens a prove)
+#   AB="VAR 'v1 v2' n"  traced same-box A/B of one switch (scripts/ab_trace.sh)
 #   CMD="..."   one extra command, run last under its own time limit (T_CMD, default 300 s)
 # Every step runs under its own `timeout -k 10`; the session stops at the first failing step.
 set -u
@@ -46,6 +51,28 @@ if [ "${PMC:-0}" = "1" ]; then
   rc=$?; echo "pmc write rc=$rc"; [ $rc -eq 0 ] || exit $rc
   python3 scripts/pmc_traffic.py "$R/gpurun_out/${TAG}pmc_fetch" "$R/gpurun_out/${TAG}pmc_write" \
     "$R/gpurun_out/${TAG}pmc_traffic.json"
+fi
+if [ -n "${TRACE:-}" ]; then
+  export TMPDIR=/tmp
+  if [ "$TRACE" = "hipt" ]; then
+    (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 TRACE_REPS=4 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace \
+      --memory-copy-trace --output-format csv -d "$R/gpurun_out/${TAG}kt" -o kt -- python3 "$R/scripts/trace_snark.py" \
+      > /dev/null 2> "$R/gpurun_out/${TAG}kt.err")
+    rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  else
+    (cd /tmp && SPG_TRACE=2 SPG_TRACE_EVENTS=1 TRACE_REPS=6 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+      -d "$R/gpurun_out/${TAG}kt" -o kt -- python3 "$R/scripts/trace_snark.py" > /dev/null 2> "$R/gpurun_out/${TAG}kt.err")
+    rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    MARK="${MARK:-k_comb_accum<13, 1>}" SKIP=1 python3 scripts/kernel_gaps.py gpurun_out/${TAG}kt XX > gpurun_out/${TAG}kt_gaps.txt
+    MARK="${MARK:-k_comb_accum<13, 1>}" SKIP=1 EVENTS=gpurun_out/${TAG}kt.err python3 scripts/kernel_gaps.py gpurun_out/${TAG}kt \
+      >> gpurun_out/${TAG}kt_gaps.txt
+    head -3 gpurun_out/${TAG}kt_gaps.txt
+  fi
+fi
+if [ -n "${AB:-}" ]; then
+  eval "set -- $AB"
+  timeout -k 10 ${T_AB:-700} bash scripts/ab_trace.sh "$1" "$2" "$3" > gpurun_out/${TAG}ab.txt 2>&1
+  rc=$?; echo "ab rc=$rc"; tail -8 gpurun_out/${TAG}ab.txt; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "${CMD:-}" ]; then
   timeout -k 10 ${T_CMD:-300} bash -c "$CMD" > gpurun_out/${TAG}cmd.log 2>&1

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 
 #include "ctx.hpp"
 #include "hcurve.hpp"
@@ -202,6 +203,9 @@ __global__ void __launch_bounds__(256) k_comb_join(const Ext* __restrict__ part,
 // comb tables of all live generator sets of this process, against the process-wide cap (SPG_COMB_GB, default 96 GiB;
 // a table replaced by a wider one stays allocated until spg_gens_free, see spg_gens::comb_retired)
 static std::atomic<size_t> g_comb_bytes{0};
+// tables built by this process and their summed build time (spg_comb_stats: the precomputation the bench discloses)
+static std::atomic<int> g_comb_built{0};
+static std::atomic<uint64_t> g_comb_build_ns{0};
 
 void comb_free(const spg_gens* g) {
   if (!g) return;
@@ -226,7 +230,7 @@ static bool comb_enabled() {
 // another h exists: blinded rows on a second h take the bucket path rather than rebuilding gigabytes), or an SPG
 // error code. *use stays valid until the gens is freed.
 static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, spg_gens::Comb* use) {
-  if (!comb_enabled() || need > kCombMaxR) return 1;
+  if (!comb_enabled() || ctx->comb_off || need > kCombMaxR) return 1;
   std::lock_guard<std::mutex> lk(g->comb_mu);
   const spg_gens::Comb cur = g->comb;
   if (cur.p && hgen >= 0 && cur.h != hgen) return 1;
@@ -277,6 +281,7 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
     }
   if (!st) return 1;
   const size_t entries = (size_t)(253 / C + 1) * NS * ((size_t)1 << (C - 1)), bytes = table_bytes(C, st);
+  const auto t_build = std::chrono::steady_clock::now();
   Niels* comb = nullptr;
   Fp* zs = nullptr;
   const size_t lanes = entries / kCombRun;
@@ -314,6 +319,9 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
   if (cur.p) g->comb_retired.push_back(cur);
   g->comb = spg_gens::Comb{comb, cn, bytes, hgen, C, st};
   g_comb_bytes += bytes;
+  g_comb_built++;
+  g_comb_build_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now() - t_build).count();
   *use = g->comb;
   return 0;
 }
@@ -321,6 +329,28 @@ static int comb_ensure(spg_ctx* ctx, const spg_gens* g, size_t need, int hgen, s
 int comb_get(spg_ctx* ctx, const spg_gens* g, size_t need, spg_gens::Comb* out) {
   return comb_ensure(ctx, g, need, -1, out);
 }
+
+}  // namespace spg
+
+extern "C" int spg_set_comb(spg_ctx* ctx, int on) {
+  if (!ctx) return SPG_E_ARG;
+  ctx->comb_off = !on;
+  return SPG_OK;
+}
+
+namespace spg {
+extern std::atomic<size_t> g_gens_table_bytes;  // msm.hip
+}
+
+extern "C" int spg_comb_stats(uint64_t* bytes, int* tables_built, double* build_seconds, uint64_t* gens_table_bytes) {
+  if (bytes) *bytes = spg::g_comb_bytes.load();
+  if (gens_table_bytes) *gens_table_bytes = spg::g_gens_table_bytes.load();
+  if (tables_built) *tables_built = spg::g_comb_built.load();
+  if (build_seconds) *build_seconds = (double)spg::g_comb_build_ns.load() * 1e-9;
+  return SPG_OK;
+}
+
+namespace spg {
 
 // B row MSMs of n contiguous generators from gen_offset (+ blinds on h): SPG_OK with the rows' points in ext
 // (B Ext, device) and, when d_out is set, their encodings; kCombSkip when the comb does not apply (the caller

@@ -14,6 +14,9 @@
 
 struct spg_ctx {
   int device = -1;
+  // spg_set_comb(ctx, 0): this context's MSMs skip the comb tables (comb.hip) and run the bucket pipelines, for an
+  // A/B against the fixed-base precomputation (bench.py config 2's no-table leg)
+  bool comb_off = false;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_cx = nullptr;  // DotProductProofLog: the Cx MSM's completion, ahead of Bullet round 0 on the stream
@@ -177,9 +180,10 @@ int comb_get(spg_ctx* ctx, const spg_gens* g, size_t need, spg_gens::Comb* out);
 int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq* d_scalars, size_t n, size_t B,
                      const Fq* d_blinds, uint8_t* d_out, const uint32_t* d_idx, long h_index, Ext* d_ext = nullptr);
 // the same rows (gen_offset 0) with their 32-byte encodings on the host in out (msm.hip: halved comb points encoded as
-// doubles on the host pool where the comb applies); synchronous
+// doubles on the host pool where the comb applies); synchronous. timed: record the context's stop event right after
+// the device work (before the download and the host encodings), for spg_last_kernel_us
 int msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, size_t n, size_t B, const Fq* d_blinds,
-                      long h_index, uint8_t* out);
+                      long h_index, uint8_t* out, bool timed = false);
 
 // latency path for small batches (B * n up to a few thousand): same inputs, results left in extended
 // coordinates in d_out (B x Ext, device); the caller encodes them (host).

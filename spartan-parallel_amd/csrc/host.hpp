@@ -202,12 +202,11 @@ struct HostGens {
     h::hext_decompress(comp.data() + 32 * idx, P);
     return P;
   }
-  // the table map of every HostGens is guarded by one process-wide lock (contexts on several threads may share a
-  // generator set; a table, once built, never moves: std::map nodes are stable)
-  static std::mutex& table_mu() {
-    static std::mutex m;
-    return m;
-  }
+  // each HostGens guards its own table map (contexts on several threads may share a generator set; a table, once
+  // built, never moves: std::map nodes are stable). Per set, not process-wide: contexts proving with
+  // different generator sets no longer wait on each other's table builds (11-24 ms each) and lookups
+  std::shared_ptr<std::mutex> mu_ = std::make_shared<std::mutex>();
+  std::mutex& table_mu() { return *mu_; }
   const FixedBase& get(size_t idx) {
     std::lock_guard<std::mutex> lk(table_mu());
     return get_locked(idx);

@@ -114,6 +114,21 @@ void spgh_merlin_simple(const char* label, const char* l1, const uint8_t* m1, si
   t.challenge(l2, out, m);
 }
 
+// A caller-owned merlin::Transcript behind spg_transcript_new_callbacks, in native code: what the Rust caller's
+// `extern "C"` trampolines over `&mut Transcript` do (src/lib.rs:1022). The two
+// callbacks have the spg_transcript_append_fn / spg_transcript_challenge_fn signatures and take the Merlin as `user`,
+// so bench.py can time a prove in the drop-in mode with no Python on the transcript path.
+void* spgh_merlin_new(const char* label) { return new Merlin(label); }
+void spgh_merlin_free(void* t) { delete static_cast<Merlin*>(t); }
+int spgh_merlin_append_cb(void* user, const char* label, const uint8_t* msg, size_t len) {
+  static_cast<Merlin*>(user)->message(label, msg, len);
+  return 0;
+}
+int spgh_merlin_challenge_cb(void* user, const char* label, uint8_t* out, size_t len) {
+  static_cast<Merlin*>(user)->challenge(label, out, len);
+  return 0;
+}
+
 // Host radix-2^51 curve (hcurve.hpp) against the device-form curve on the same inputs: for n uniform
 // 64-byte strings, P_i = from_uniform_bytes; checks compress, decompress->compress, add, dbl, mixed add
 // through batch-normalised Niels, and scalar multiplication by the 32-byte scalars k. Returns the

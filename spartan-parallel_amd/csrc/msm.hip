@@ -1141,11 +1141,15 @@ int msm_batch_device(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const F
 }
 
 // ------------------------------------------------------------------ generator handles
+// HBM bytes of the 2^k G_i tables of all live generator sets (spg_comb_stats)
+std::atomic<size_t> g_gens_table_bytes{0};
+
 static int gens_finish(spg_ctx* ctx, spg_gens* g) {
   hipStream_t s = ctx->stream;
   size_t n1 = g->n + 1;
   size_t tab_entries = n1 * (size_t)kTableRows;
   SPG_HIP(ctx, hipMalloc(&g->table, tab_entries * sizeof(Niels)));
+  g_gens_table_bytes += tab_entries * sizeof(Niels);
   hipLaunchKernelGGL(k_table, dim3((unsigned)((tab_entries + 255) / 256)), dim3(256), 0, s, g->niels, g->table,
                      (int)n1);
   SPG_HIP(ctx, hipGetLastError());
@@ -1249,7 +1253,10 @@ extern "C" int spg_gens_free(spg_ctx* ctx, spg_gens* g) {
   (void)ctx;
   if (!g) return SPG_OK;
   if (g->niels) hipFree(g->niels);
-  if (g->table) hipFree(g->table);
+  if (g->table) {
+    hipFree(g->table);
+    g_gens_table_bytes -= (g->n + 1) * (size_t)kTableRows * sizeof(Niels);
+  }
   comb_free(g);
   delete[] g->compressed;
   delete g;
@@ -1422,7 +1429,7 @@ extern "C" int spg_commit_rows(spg_ctx* ctx, const spg_gens* g, const uint64_t* 
 // back for the host pool's batched encoding of doubles (encode_halved_host) instead of k_compress_ext's lane-per-point
 // inverse square roots; else msm_batch_device's device encodings, downloaded. SPG_HALVED_ENC=0: always the latter.
 int spg::msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, size_t n, size_t B,
-                           const Fq* d_blinds, long h_index, uint8_t* out) {
+                           const Fq* d_blinds, long h_index, uint8_t* out, bool timed) {
   static const bool halve = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
   hipStream_t s = ctx->stream;
   const size_t tot = B * (n + (d_blinds ? 1 : 0));
@@ -1433,6 +1440,7 @@ int spg::msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars,
     const int hi = !d_blinds ? -1 : (h_index < 0 ? (int)g->n : (int)h_index);
     const int rc = msm_comb(ctx, g, 0, d_scalars, n, B, d_blinds, nullptr, hi, ext, true);
     if (rc == SPG_OK) {
+      if (timed) timer_stop(ctx);
       Ext* h = (Ext*)enc_stage_get(ctx, B * sizeof(Ext));
       if (!h) return set_err(ctx, SPG_E_NOMEM, "encoding staging");
       SPG_HIP(ctx, hipMemcpyAsync(h, ext, B * sizeof(Ext), hipMemcpyDeviceToHost, s));
@@ -1446,6 +1454,7 @@ int spg::msm_rows_host_enc(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars,
   if (!d_out) return set_err(ctx, SPG_E_NOMEM, "commit rows out");
   const int rc = msm_batch_device(ctx, g, 0, d_scalars, n, B, d_blinds, d_out, nullptr, h_index);
   if (rc) return rc;
+  if (timed) timer_stop(ctx);
   SPG_HIP(ctx, hipMemcpyAsync(out, d_out, 32 * B, hipMemcpyDeviceToHost, s));
   SPG_HIP(ctx, hipStreamSynchronize(s));
   return SPG_OK;
@@ -1459,9 +1468,10 @@ extern "C" int spg_commit_rows_buf(spg_ctx* ctx, const spg_gens* g, const spg_bu
   if (R > g->n) return set_err(ctx, SPG_E_ARG, "commit_rows_buf: R exceeds generators");
   if (L == 0) return SPG_OK;
   timer_start(ctx);
-  const int rc = msm_rows_host_enc(ctx, g, Z->d + offset, R, L, blinds ? blinds->d : nullptr, -1, out);
+  // the stop event is recorded after the device work, before the download and the host encodings, so
+  // spg_last_kernel_us is device time like every other MSM entry point's
+  const int rc = msm_rows_host_enc(ctx, g, Z->d + offset, R, L, blinds ? blinds->d : nullptr, -1, out, true);
   if (rc) return rc;
-  timer_stop(ctx);  // (recorded after the host encodings: device time plus the host's share)
   SPG_HIP(ctx, hipEventSynchronize(ctx->ev1));
   float ms = 0.f;
   hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);

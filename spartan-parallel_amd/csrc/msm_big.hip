@@ -398,7 +398,7 @@ int msm_single_big(spg_ctx* ctx, const spg_gens* g, size_t gen_offset, const Fq*
   // with the entries padded to one line and the parts summed on the host's IFMA lanes it is ahead: 0.171-0.179 ms with
   // 4 window groups per scalar, 0.146 ms with 2 (SPG_BIG_COMB_G), against 0.204-0.206 ms (profiles/r05_ab_big_comb.txt)
   static const bool comb_on = !getenv("SPG_BIG_COMB") || atoi(getenv("SPG_BIG_COMB")) != 0;
-  if (comb_on && n >= ((size_t)1 << 14)) {
+  if (comb_on && !ctx->comb_off && n >= ((size_t)1 << 14)) {
     const int rc = msm_single_comb(ctx, g, gen_offset, d_scalars, n, d_blind, out);
     if (rc != 1) return rc;
   }

@@ -474,7 +474,8 @@ struct CQ {
     // the comb rows with halved scalars: flush() encodes the points' doubles on the host in one batch (~50 us on the
     // pool for 1024 rows) instead of a k_compress_ext launch (~140 us of dependent squarings per lane)
     static const bool halve = !getenv("SPG_HALVED_ENC") || atoi(getenv("SPG_HALVED_ENC")) != 0;
-    Ext* ext = halve && total / R >= 384 ? (Ext*)ws_get(ctx, 94, sizeof(Ext) * (total / R) + 64) : nullptr;
+    // slot 95: 94 is spark.hip's kWsRelay (the persistent layer kernel's relay word)
+    Ext* ext = halve && total / R >= 384 ? (Ext*)ws_get(ctx, 95, sizeof(Ext) * (total / R) + 64) : nullptr;
     int rc = ext ? msm_comb(ctx, g.dev, 0, d, R, total / R, nullptr, nullptr, -1, ext, true) : kCombSkip;
     if (rc == kCombSkip) {
       ext = nullptr;

@@ -321,7 +321,8 @@ enum : size_t {
   kWsPart, kWs3, kWsMemRx, kWsMemRy, kWsDerefs, kWsTreeOps, kWsTreeMem, kWsDotp, kWsFinals, kWsEqOps, kWsEqMem,
   kWsTops, kWsCommitBk, kWsC2, kWsGather, kWsTopOps, kWsTopMem, kWsStage, kWsTsKeys, kWsTsTemp,  // 60 .. 89
   kWsRelay = 94,
-  kWsMultiExt = 120, kWsMultiOut, kWsCommitExt  // (snark.hip uses 91 .. 94, msm_big.hip 100 .. 108, sumcheck.hip 110 .. 111)
+  kWsMultiExt = 120, kWsMultiOut, kWsCommitExt  // (snark.hip uses 91 .. 93 and 95, verify.hip 96, msm_big.hip
+                                                // 100 .. 108, sumcheck.hip 110 .. 111)
 };
 
 // PolyCommitmentGens::new(nv, label) as a view of one derived generator stream (dense_mlpoly.rs:88-98)
@@ -949,8 +950,13 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
       // two rounds in one launch (k_layer_pair): small rounds of an unsharded layer, every element's 16 lanes within
       // pair_max elements, the last pair's corners within the mailbox; three (k_layer_triple): a wave per element
       // within triple_max elements, the last triple's corners within the mailbox
+      // a paired launch of E elements stores 16 partials per workgroup of BSp / 16 elements into `part` (3 x 2048
+      // scalars): 16 E / BSp * 16 <= 6144, so E <= 6144 with 256-thread workgroups and E <= 1536 with 64-thread ones
+      // (SPG_PAIR_BS = 64)
+      static const int pair_bs = getenv("SPG_PAIR_BS") ? atoi(getenv("SPG_PAIR_BS")) : 0;  // 64: more workgroups
+      const size_t pair_part_cap = pair_bs == 64 ? 1536 : 6144;
       auto pair_ok = [&](size_t k) {
-        return pair_on && multi && k >= 2 && (nt_all << (k - 2)) <= std::min<size_t>(pair_max, 6144) &&
+        return pair_on && multi && k >= 2 && (nt_all << (k - 2)) <= std::min<size_t>(pair_max, pair_part_cap) &&
                15 + 12 * nt_all <= kMboxScalars && ngroups * ((size_t)1 << (k - 1)) < wide_min;
       };
       auto triple_ok = [&](size_t k) {
@@ -1105,7 +1111,6 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
           const int lgj = (int)log_len - 1;  // round j's half length 2^lgj; round j + 1's 2^(lgj - 1)
           log_len -= 2;
           const size_t nt = tr.size(), h = (size_t)1 << (lgj - 1), lanes = 16 * nt * h;
-          static const int pair_bs = getenv("SPG_PAIR_BS") ? atoi(getenv("SPG_PAIR_BS")) : 0;  // 64: more workgroups
           const int BSp = lanes <= 64 || pair_bs == 64 ? 64 : 256;
           const unsigned Kp = (unsigned)((lanes + BSp - 1) / BSp);
           const bool ends = log_len == 0;  // the layer's last pair posts every vector's 2 x 2 corners

@@ -34,6 +34,37 @@ def lib():
     return _lib
 
 
+def comb_stats():
+    """spg_comb_stats: (HBM bytes of this process's comb tables now allocated, comb tables built so far, their summed
+    build seconds, HBM bytes of the live generator sets' 2^k G_i tables) -- the fixed-base precomputation behind the MSM
+    paths"""
+    b = ctypes.c_uint64()
+    k = ctypes.c_int()
+    s = ctypes.c_double()
+    g = ctypes.c_uint64()
+    rc = lib().spg_comb_stats(ctypes.byref(b), ctypes.byref(k), ctypes.byref(s), ctypes.byref(g))
+    if rc != 0:
+        raise SpgError(f"spg_comb_stats: {SPG_ERRORS.get(rc, rc)}")
+    return int(b.value), int(k.value), float(s.value), int(g.value)
+
+
+_hc = None
+
+
+def hostcheck():
+    """lib/libspg_hostcheck.so: the host build of the product's field / curve / transcript code (tests, and the
+    caller-side merlin of Transcript.from_native_merlin)"""
+    global _hc
+    if _hc is None:
+        path = os.environ.get("SPG_HOSTCHECK_LIB") or os.path.join(_HERE, "lib", "libspg_hostcheck.so")
+        _hc = ctypes.CDLL(path)
+        _hc.spgh_merlin_new.restype = ctypes.c_void_p
+        _hc.spgh_merlin_new.argtypes = [ctypes.c_char_p]
+        _hc.spgh_merlin_free.argtypes = [ctypes.c_void_p]
+        _hc.spgh_merlin_challenge_cb.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t]
+    return _hc
+
+
 def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
@@ -122,6 +153,10 @@ class Context:
         self.check(lib().spg_comm_allgather(self._h, src, ctypes.c_size_t(n), dst), "spg_comm_allgather")
         raw = bytes(dst)
         return [raw[k * n:(k + 1) * n] for k in range(nranks)]
+
+    def set_comb(self, on=True):
+        """spg_set_comb: off -> this context's MSMs skip the comb tables (bucket Pippenger pipelines only)"""
+        self.check(lib().spg_set_comb(self._h, ctypes.c_int(1 if on else 0)), "spg_set_comb")
 
     def last_kernel_us(self):
         return lib().spg_last_kernel_us(self._h)
@@ -352,6 +387,30 @@ class Transcript:
             raise SpgError(f"spg_transcript_new_callbacks: {SPG_ERRORS.get(rc, rc)}")
         return t
 
+    @classmethod
+    def from_native_merlin(cls, label):
+        """spg_transcript_new_callbacks over a caller-owned merlin::Transcript in native code (libspg_hostcheck's
+        spgh_merlin_*: C callbacks, no Python per append / challenge) -- the drop-in mode a Rust caller gets with
+        extern "C" trampolines over its &mut Transcript. The returned object also holds
+        the caller's transcript: caller_challenge(label, n) reads challenge bytes from it after a prove."""
+        hc = hostcheck()
+        t = cls.__new__(cls)
+        t._merlin = ctypes.c_void_p(hc.spgh_merlin_new(ctypes.c_char_p(bytes(label))))
+        t._free_merlin = hc.spgh_merlin_free
+        t._h = ctypes.c_void_p()
+        rc = lib().spg_transcript_new_callbacks(ctypes.cast(hc.spgh_merlin_append_cb, ctypes.c_void_p),
+                                                ctypes.cast(hc.spgh_merlin_challenge_cb, ctypes.c_void_p),
+                                                t._merlin, ctypes.byref(t._h))
+        if rc != 0:
+            hc.spgh_merlin_free(t._merlin)
+            raise SpgError(f"spg_transcript_new_callbacks: {SPG_ERRORS.get(rc, rc)}")
+        return t
+
+    def caller_challenge(self, label, n):
+        out = (ctypes.c_uint8 * max(n, 1))()
+        hostcheck().spgh_merlin_challenge_cb(self._merlin, ctypes.c_char_p(bytes(label)), out, ctypes.c_size_t(n))
+        return bytes(out)[:n]
+
     @property
     def handle(self):
         return self._h
@@ -383,6 +442,10 @@ class Transcript:
             if self._h:
                 lib().spg_transcript_free(self._h)
                 self._h = ctypes.c_void_p()
+            m = getattr(self, "_merlin", None)
+            if m:
+                self._free_merlin(m)
+                self._merlin = None
         except Exception:
             pass
 

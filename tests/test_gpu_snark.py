@@ -102,6 +102,9 @@ ROUND_FORMS = {
     "eq_table_per_launch": {"SPG_EQ_MULTI": "0"},
     "layer_single_rounds": {"SPG_LAYER_PAIR": "0"},
     "layer_pairs_small_wgs": {"SPG_PAIR_BS": "64"},
+    # 64-thread pairs asked for up to 6144 elements: the launch plan must cap them at 1536 (the partials workspace)
+    "layer_pairs_small_wgs_everywhere": {"SPG_PAIR_BS": "64", "SPG_PAIR_MAX": "6144", "SPG_WIDE_MIN": str(1 << 40),
+                                         "SPG_LAYER_TRIPLE": "0"},
     "layer_pairs_everywhere": {"SPG_PAIR_MAX": "6144", "SPG_WIDE_MIN": str(1 << 40)},
     "layer_pairs_no_triples": {"SPG_LAYER_TRIPLE": "0"},
     "layer_triples_everywhere": {"SPG_TRIPLE_MAX": "1536", "SPG_WIDE_MIN": str(1 << 40), "SPG_STEP_COSTS": "18,25,1"},

@@ -92,3 +92,19 @@ def test_callback_transcript_failure_is_latched():
     with pytest.raises(spg.SpgError, match="SPG_E_CALLBACK"):
         t.challenge_bytes(b"after", 4)
     assert calls == [b"ok", b"bad"]
+
+
+def test_native_merlin_callbacks_match_library_transcript():
+    """Transcript.from_native_merlin: the drop-in mode bench.py times (C callbacks over a caller-owned merlin in
+    libspg_hostcheck, no Python on the transcript path) ends in the same state as the library's own transcript"""
+    import spg
+
+    cb = spg.Transcript.from_native_merlin(b"drop-in")
+    ref = spg.Transcript(b"drop-in")
+    for t in (cb, ref):
+        t.append_message(b"protocol-name", b"Spartan SNARK proof")
+        t.append_scalar(b"num_ios", np.array([5, 6, 7, 8], dtype=np.uint64))
+    assert np.array_equal(cb.challenge_scalar(b"tau"), ref.challenge_scalar(b"tau"))
+    assert cb.challenge_bytes(b"c", 200) == ref.challenge_bytes(b"c", 200)
+    # the caller's own transcript object holds the state: reading it directly continues the same stream
+    assert cb.caller_challenge(b"final", 32) == ref.challenge_bytes(b"final", 32)
