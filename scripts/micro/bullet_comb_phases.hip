@@ -3,6 +3,7 @@
 // layout, 681 MB); parts and mailbox in coherent mapped host memory as in the product. Per round size: HIP-event time
 // back to back and after 20 us host gaps, and from the kernel's wall_clock64 probes (100 MHz) the per-workgroup
 // phases: start skew, fold products, recode + entry loads, mixed additions, LDS tree, parts + fence, ticket + post.
+// Both forms (k_bullet_comb, k_bullet_comb_roll) alternate per size.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o scripts/micro/bullet_comb_phases scripts/micro/bullet_comb_phases.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -30,7 +31,15 @@ static void fill(std::vector<uint32_t>& v, uint32_t seed) {
 
 constexpr int C = 13, G = 10, NS = 65, ST = 4;
 
-template <int BS>
+template <int BS, bool ROLL>
+static void launch(dim3 grid, const BulletCombArgs& a) {
+  if (ROLL)
+    hipLaunchKernelGGL((k_bullet_comb_roll<C, G, BS>), grid, dim3(BS), 0, 0, a);
+  else
+    hipLaunchKernelGGL((k_bullet_comb<C, G, BS>), grid, dim3(BS), 0, 0, a);
+}
+
+template <int BS, bool ROLL = false>
 static void run(int n, const Niels* tab, Fq* st, uint32_t* gidx, unsigned* ctr, uint32_t* mb, Ext* parts,
                 unsigned long long* probe, int gap_us) {
   const int R = 8, S = BS / 4, P = n / 2, wgs = (P * G + S - 1) / S;
@@ -49,7 +58,7 @@ static void run(int n, const Niels* tab, Fq* st, uint32_t* gidx, unsigned* ctr, 
   for (int r = 0; r < reps + 3; r++) {
     if (gap_us) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
     hipEventRecord(e0, 0);
-    hipLaunchKernelGGL((k_bullet_comb<C, G, BS>), grid, dim3(BS), 0, 0, a);
+    launch<BS, ROLL>(grid, a);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     float ms;
@@ -60,7 +69,7 @@ static void run(int n, const Niels* tab, Fq* st, uint32_t* gidx, unsigned* ctr, 
   const int nb = 2 * wgs;
   hipMemset(probe, 0, (size_t)8 * nb * 8);
   if (gap_us) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
-  hipLaunchKernelGGL((k_bullet_comb<C, G, BS>), grid, dim3(BS), 0, 0, a);
+  launch<BS, ROLL>(grid, a);
   hipDeviceSynchronize();
   std::vector<unsigned long long> p((size_t)8 * nb);
   hipMemcpy(p.data(), probe, p.size() * 8, hipMemcpyDeviceToHost);
@@ -81,10 +90,10 @@ static void run(int n, const Niels* tab, Fq* st, uint32_t* gidx, unsigned* ctr, 
     tend = std::max(tend, q[6]);
   }
   for (int i = 0; i < 6; i++) ph[i] /= std::max(cnt, 1);
-  printf("n=%5d BS=%3d wgs=%4d gap %3d us: event %.2f us/launch | probes avg/max us: skew %.2f, fold %.2f/%.2f, "
+  printf("%s n=%5d BS=%3d wgs=%4d gap %3d us: event %.2f us/launch | probes avg/max us: skew %.2f, fold %.2f/%.2f, "
          "recode+loads %.2f/%.2f, madds %.2f/%.2f, tree %.2f/%.2f, parts+fence %.2f/%.2f, ticket+post %.2f/%.2f, "
          "first start -> last end %.2f\n",
-         n, BS, nb, gap_us, tot * 1000 / reps, skew, ph[0], mx[0], ph[1], mx[1], ph[2], mx[2], ph[3], mx[3], ph[4],
+         ROLL ? "roll  " : "unroll", n, BS, nb, gap_us, tot * 1000 / reps, skew, ph[0], mx[0], ph[1], mx[1], ph[2], mx[2], ph[3], mx[3], ph[4],
          mx[4], ph[5], mx[5], (tend - t0) * 0.01);
 }
 
@@ -130,13 +139,19 @@ int main() {
   hipHostGetDevicePointer((void**)&parts, parts_h, 0);
   unsigned long long* probe;
   hipMalloc(&probe, (size_t)8 * 2048 * 8);
-  for (int gap : {0, 20}) {
-    run<64>(2, tab, st, gidx, ctr, mb, parts, probe, gap);
-    run<64>(8, tab, st, gidx, ctr, mb, parts, probe, gap);
-    run<64>(32, tab, st, gidx, ctr, mb, parts, probe, gap);
-    run<64>(128, tab, st, gidx, ctr, mb, parts, probe, gap);
-    run<128>(256, tab, st, gidx, ctr, mb, parts, probe, gap);
-    run<256>(1024, tab, st, gidx, ctr, mb, parts, probe, gap);
-  }
+  // the unrolled (k_bullet_comb) and rolled (k_bullet_comb_roll) forms alternated, twice
+  for (int rep = 0; rep < 2; rep++)
+    for (int gap : {0, 20}) {
+      run<64, false>(2, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<64, true>(2, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<64, false>(32, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<64, true>(32, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<64, false>(128, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<64, true>(128, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<128, false>(256, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<128, true>(256, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<256, false>(1024, tab, st, gidx, ctr, mb, parts, probe, gap);
+      run<256, true>(1024, tab, st, gidx, ctr, mb, parts, probe, gap);
+    }
   return 0;
 }

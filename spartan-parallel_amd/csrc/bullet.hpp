@@ -296,6 +296,137 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
   }
 }
 
+// ---- the same round with rolled loops (round 6; the default, SPG_BCOMB_ROLL=0 selects k_bullet_comb above) -------
+// A Bullet round is a latency-bound launch whose code runs once per launch: k_bullet_comb's fully unrolled form is
+// 4,033 straight-line instructions (hipcc -S, <13, 10, 64>), ~29 KiB that every launch fetches into cold instruction
+// caches (profiles/r05_bcomb_micro_fetch.txt: PMC FETCH_SIZE of back-to-back launches, ~29 KiB per workgroup up to the
+// 8 XCDs). Here every field product of a kind has ONE site in the code:
+//  * the fold's operand product and k = av cv are two iterations of one Fq-product loop;
+//  * the quad's mixed additions (WG of them) and the workgroup's LDS tree levels are iterations of one loop around one
+//    quad step: lane q's first-round product quad_operand(acc, q) * y -- y = the entry's Niels coordinate (2 on lane 3)
+//    for an addition, the partner quad's first-round operand for a tree level, which also scales by its small
+//    constant (quad_add_op) -- then quad_finish. The entries shift down one register slot per addition, so no loop
+//    indexes a register array.
+// Same group elements, same parts, same bytes (tests/test_gpu_snark.py goldens; test_round_forms keeps the unrolled form).
+template <int C, int G, int BS>
+__global__ void __launch_bounds__(BS) k_bullet_comb_roll(BulletCombArgs a) {
+  constexpr int W = 253 / C + 1, WG = (W + G - 1) / G, S = BS / 4;
+  __shared__ uint32_t pts[soa_words<Ext, S>()];
+  __shared__ bool last;
+  const int b = blockIdx.y, t = threadIdx.x, q = t & 3, slot = t >> 2;
+  const int P = a.n / 2, nk = a.nk, nh = nk / 2;
+  const int gq = blockIdx.x * S + slot;  // quad index within MSM b
+  const int p = gq / G, jg = gq - p * G, w0 = jg * WG;
+  unsigned long long* pr = a.probe ? a.probe + 8 * (blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
+  if (pr && t == 0) pr[0] = wall_clock64();
+  Ext acc = ext_identity();
+  uint32_t ent[WG];
+  Fp qv[WG];
+  bool ng[WG];
+#pragma unroll
+  for (int x = 0; x < WG; x++) {
+    ent[x] = 0xffffffffu;
+    ng[x] = false;
+  }
+  if (p < P) {
+    const int blk = p / nh, off = p - blk * nh;
+    const int ia = b ? off + nh : off;
+    const int j = blk * nk + (b ? 0 : nh) + off;
+    Fq av, cv, x, y;
+    int it = 0;
+    if (a.k == 0) {
+      av = a.aa_in[ia];
+      cv = fq_zero();
+      cv.l[0] = 1u;  // cw = 1: the product below takes av out of Montgomery form
+      x = av;
+      y = cv;
+      it = 1;
+    } else {
+      // lanes 0, 1, 2: u a[ia], u^-1 a[ia + nk], cw[j] f; lane 3 repeats lane 0 (operands selected after both loads,
+      // as in k_bullet_comb)
+      const Fq xa = a.aa_in[q == 1 ? ia + nk : ia];
+      const Fq xc = a.cw_in[j];
+      x = q == 2 ? xc : xa;
+      y = q == 1 ? a.uinv : (q == 2 ? ((j & (2 * nk - 1)) < nk ? a.uinv : a.u) : a.u);
+    }
+    Fq k;
+#pragma unroll 1
+    for (; it < 2; it++) {  // uniform per launch: iteration 0 the fold (k >= 1 only), iteration 1 k = av cv
+      const Fq r = fq_mul(x, y);
+      if (it == 0) {
+        av = fq_add(fq_qbcast_lane(r, 0), fq_qbcast_lane(r, 1));
+        cv = fq_qbcast_lane(r, 2);
+        x = av;
+        y = cv;
+      } else {
+        k = r;  // canonical scalar (cw is a plain integer)
+      }
+    }
+    if (jg == 0 && q == 0) {  // the folded state, every (ia, j) once over the two MSMs
+      if (blk == 0) a.aa_out[ia] = av;
+      a.cw_out[j] = cv;
+    }
+    if (pr) { asm volatile("" ::"v"(k.l[0])); if (t == 0) pr[1] = wall_clock64(); }
+    const int s = (int)a.gidx[j];
+    comb_window_entries<C, WG>(k, w0, s, a.NS, ent);
+#pragma unroll
+    for (int x2 = 0; x2 < WG; x2++)
+      if (ent[x2] != 0xffffffffu) qv[x2] = niels_coord(a.comb, ent[x2], q, &ng[x2], a.st);
+    if (pr) { asm volatile("" ::"v"(qv[WG - 1].l[0])); if (t == 0) pr[2] = wall_clock64(); }
+  }
+  // WG mixed additions, then log2(S / R) tree levels (d = S/2, S/4, .., R), through one quad step
+  const int levels = __builtin_ctz((unsigned)S) - __builtin_ctz((unsigned)a.R);
+#pragma unroll 1
+  for (int it = 0; it < WG + levels; it++) {
+    const bool tree = it >= WG;  // uniform
+    Fp y;
+    bool cneg, use;
+    if (tree) {
+      const int d = (S / 2) >> (it - WG);
+      if (slot >= d && slot < 2 * d) quad_put_op<S>(pts, slot - d, acc, q);
+      __syncthreads();
+      y = quad_get_op<S>(pts, slot, q);  // read by every quad, used by slot < d
+      __syncthreads();
+      cneg = true;
+      use = slot < d;
+    } else {
+      y = q == 3 ? fp_small(2) : qv[0];
+      cneg = ng[0];
+      use = ent[0] != 0xffffffffu;
+#pragma unroll
+      for (int x = 0; x + 1 < WG; x++) {
+        ent[x] = ent[x + 1];
+        qv[x] = qv[x + 1];
+        ng[x] = ng[x + 1];
+      }
+      ent[WG - 1] = 0xffffffffu;
+    }
+    Fp prd = fp_mul(quad_operand(acc, q), y);
+    if (tree) prd = fp_mul_k(prd, q == 2 ? 243330u : (q == 3 ? 243332u : 121666u));
+    const Ext r = quad_finish(prd, q, cneg);
+    if (use) acc = r;
+    if (pr && it + 1 == WG) { asm volatile("" ::"v"(acc.X.l[0])); if (t == 0) pr[3] = wall_clock64(); }
+  }
+  if (pr) { asm volatile("" ::"v"(acc.X.l[0])); if (t == 0) pr[4] = wall_clock64(); }
+  if (slot < a.R && q == 0) a.parts[((size_t)b * gridDim.x + blockIdx.x) * a.R + slot] = acc;
+  __syncthreads();
+  if (t == 0) {
+    // the parts (mapped host memory) and the folded state (HBM) before the ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pr) pr[5] = wall_clock64();
+    last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.x * gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mbox_post(a.mb, a.seq, nullptr, 0);
+    }
+    if (pr) pr[6] = wall_clock64();
+  }
+}
+
 // B plain MSMs from the comb table, sum_i s_{b,i} G_{idx_{b,i}} (Montgomery scalars), left as partial points: the Cx
 // commitment of a device DotProductProofLog (its blind term is added on the host). The same quads, window groups and
 // workgroup trees as k_bullet_comb; parts[b][wg][0..R).

@@ -679,7 +679,15 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   const double W = 253 / cb.c + 1, entries = (double)n * W * (1.0 - 1.0 / (double)(1 << cb.c));
   KScope ks(ctx, "msm_bullet_round", 96.0 * entries + 96.0 * nk + 68.0 * n, entries);
   const dim3 grid((unsigned)wgs, 2);
-#define SPG_BCOMB(CC, GG, BB) hipLaunchKernelGGL((k_bullet_comb<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, a)
+  // rolled loops (k_bullet_comb_roll, bullet.hpp) by default; SPG_BCOMB_ROLL=0: the unrolled k_bullet_comb
+  static const bool roll = !getenv("SPG_BCOMB_ROLL") || atoi(getenv("SPG_BCOMB_ROLL")) != 0;
+#define SPG_BCOMB(CC, GG, BB)                                                                      \
+  do {                                                                                             \
+    if (roll)                                                                                      \
+      hipLaunchKernelGGL((k_bullet_comb_roll<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, a);     \
+    else                                                                                           \
+      hipLaunchKernelGGL((k_bullet_comb<CC, GG, BB>), grid, dim3(BB), 0, ctx->stream, a);          \
+  } while (0)
 #define SPG_BCOMB_BS(CC, GG) \
   do { if (BS == 64) SPG_BCOMB(CC, GG, 64); else if (BS == 128) SPG_BCOMB(CC, GG, 128); else SPG_BCOMB(CC, GG, 256); } while (0)
   if (cb.c == 13) {
