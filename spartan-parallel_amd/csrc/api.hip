@@ -51,6 +51,56 @@ void* enc_stage_get(spg_ctx* c, size_t bytes) {
   return c->enc_stage;
 }
 
+// the upload ring of h2d_stream: kUpSlots chunks of kUpChunk bytes (32 MB page-locked per context)
+static constexpr size_t kUpChunk = (size_t)4 << 20;
+static constexpr int kUpSlots = 8;
+
+int h2d_stream(spg_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return 0;
+  if (!c->up_ring) {
+    if (hipHostMalloc(&c->up_ring, kUpChunk * kUpSlots) != hipSuccess) {
+      c->up_ring = nullptr;
+      return set_err(c, SPG_E_NOMEM, "upload ring");
+    }
+    if (hipStreamCreateWithFlags(&c->stream_up, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_up_done, hipEventDisableTiming) != hipSuccess)
+      return set_err(c, SPG_E_HIP, "upload stream");
+    for (int i = 0; i < kUpSlots; i++)
+      if (hipEventCreateWithFlags(&c->ev_up[i], hipEventDisableTiming) != hipSuccess)
+        return set_err(c, SPG_E_HIP, "upload events");
+  }
+  const uint8_t* s = (const uint8_t*)src;
+  uint8_t* d = (uint8_t*)dst;
+  const int threads = pool().size() + 1;
+  for (size_t off = 0; off < bytes; off += kUpChunk) {
+    const int slot = c->up_next;
+    c->up_next = (slot + 1) % kUpSlots;
+    if (c->up_used[slot]) SPG_HIP(c, hipEventSynchronize(c->ev_up[slot]));  // the slot's previous DMA has read it
+    const size_t len = std::min(kUpChunk, bytes - off);
+    uint8_t* stg = (uint8_t*)c->up_ring + (size_t)slot * kUpChunk;
+    // one piece per pool thread (>= 256 KB each; 64-byte aligned cuts)
+    const int K = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, len >> 18));
+    if (K == 1) {
+      memcpy(stg, s + off, len);
+    } else {
+      pool().parallel_for(K, [&](int k) {
+        const size_t a = (len * k / K) & ~(size_t)63, b = k + 1 == K ? len : (len * (k + 1) / K) & ~(size_t)63;
+        memcpy(stg + a, s + off + a, b - a);
+      });
+    }
+    SPG_HIP(c, hipMemcpyAsync(d + off, stg, len, hipMemcpyHostToDevice, c->stream_up));
+    SPG_HIP(c, hipEventRecord(c->ev_up[slot], c->stream_up));
+    c->up_used[slot] = true;
+  }
+  SPG_HIP(c, hipEventRecord(c->ev_up_done, c->stream_up));
+  SPG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_up_done, 0));
+  return 0;
+}
+
+void h2d_sync(spg_ctx* c) {
+  if (c->stream_up) hipStreamSynchronize(c->stream_up);
+}
+
 void* mapped_get(spg_ctx* c, size_t bytes, void** dev) {
   static const bool on = !getenv("SPG_MAPPED_BUCKETS") || atoi(getenv("SPG_MAPPED_BUCKETS")) != 0;
   if (!on) return nullptr;
@@ -403,6 +453,14 @@ extern "C" int spg_free(spg_ctx* c) {
   for (auto* space : {&c->ws, &c->ws2})
     for (auto& s : *space)
       if (s.p) hipFree(s.p);
+  if (c->stream_up) {
+    hipStreamSynchronize(c->stream_up);
+    for (auto& e : c->ev_up)
+      if (e) hipEventDestroy(e);
+    if (c->ev_up_done) hipEventDestroy(c->ev_up_done);
+    hipStreamDestroy(c->stream_up);
+  }
+  if (c->up_ring) hipHostFree(c->up_ring);
   if (c->pinned) hipHostFree(c->pinned);
   if (c->enc_stage) hipHostFree(c->enc_stage);
   if (c->mapped) hipHostFree(c->mapped);

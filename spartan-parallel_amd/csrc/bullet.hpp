@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(BS) k_bullet_comb(BulletCombArgs a) {
   }
 }
 
-// ---- the same round with rolled loops (round 6; the default, SPG_BCOMB_ROLL=0 selects k_bullet_comb above) -------
+// ---- the same round with rolled loops (round 6; SPG_BCOMB_ROLL=1, measured slower than k_bullet_comb, see msm.hip) ----
 // A Bullet round is a latency-bound launch whose code runs once per launch: k_bullet_comb's fully unrolled form is
 // 4,033 straight-line instructions (hipcc -S, <13, 10, 64>), ~29 KiB that every launch fetches into cold instruction
 // caches (profiles/r05_bcomb_micro_fetch.txt: PMC FETCH_SIZE of back-to-back launches, ~29 KiB per workgroup up to the

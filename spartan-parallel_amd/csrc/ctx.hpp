@@ -30,6 +30,14 @@ struct spg_ctx {
   size_t pinned_bytes = 0;
   void* enc_stage = nullptr;       // page-locked staging of points encoded on the host (enc_stage_get)
   size_t enc_stage_bytes = 0;
+  // streamed uploads of caller host data (h2d_stream): a ring of page-locked chunks filled by the host pool, each DMA'd
+  // on its own copy stream; ev_up[slot] marks the chunk's copy, ev_up_done the last one (the context stream waits on it)
+  void* up_ring = nullptr;
+  hipStream_t stream_up = nullptr;
+  hipEvent_t ev_up[8] = {};
+  bool up_used[8] = {};
+  int up_next = 0;
+  hipEvent_t ev_up_done = nullptr;
   // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into
   // directly (mapped_get): the host reads them after the stream synchronisation, no D2H copy launch
   void* mapped = nullptr;
@@ -154,6 +162,13 @@ void* ws_get(spg_ctx* c, size_t slot, size_t bytes);
 // which synchronises the stream before freeing the old buffer)
 void* pinned_get(spg_ctx* c, size_t bytes);
 void* enc_stage_get(spg_ctx* c, size_t bytes);  // callers synchronise before returning: no copy is ever in flight
+// bytes of caller host memory (pageable) to device memory: copied chunk by chunk into the page-locked ring by the host
+// pool and DMA'd on the upload stream, so the host copy of chunk i + 1 overlaps the DMA of chunk i. Returns once every
+// byte has left `src` (the caller's buffer is free again); the DMAs may still be in flight, and the context stream waits
+// for them (work queued on it afterwards, and on stream2 behind it, sees the data). Returns 0 or an SPG error code.
+int h2d_stream(spg_ctx* c, void* dst, const void* src, size_t bytes);
+// waits for every streamed upload of the context (before device memory they target is freed)
+void h2d_sync(spg_ctx* c);
 
 // coherent mapped host memory of at least `bytes`: host pointer returned, device alias in *dev (contents
 // undefined; a larger request synchronises the stream before freeing the old buffer). Null when

@@ -679,8 +679,12 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   const double W = 253 / cb.c + 1, entries = (double)n * W * (1.0 - 1.0 / (double)(1 << cb.c));
   KScope ks(ctx, "msm_bullet_round", 96.0 * entries + 96.0 * nk + 68.0 * n, entries);
   const dim3 grid((unsigned)wgs, 2);
-  // rolled loops (k_bullet_comb_roll, bullet.hpp) by default; SPG_BCOMB_ROLL=0: the unrolled k_bullet_comb
-  static const bool roll = !getenv("SPG_BCOMB_ROLL") || atoi(getenv("SPG_BCOMB_ROLL")) != 0;
+  // SPG_BCOMB_ROLL=1: the rolled-loop form (k_bullet_comb_roll, bullet.hpp: 2,256 instead of 4,033 instructions).
+  // Measured slower, so off by default: +0.35 us per dependent pair of quad additions, +0.9 us per three tree levels,
+  // event time +0.1..1.2 us per launch (scripts/micro/bullet_comb_phases, profiles/r06_bcomb_roll_phases.txt), bench
+  // kernel average 17.2 -> 17.8 us (ABBA x3, profiles/r06_ab_bcomb_roll.txt): the round is bound by its dependent
+  // field-product chain, not by fetching its straight-line code
+  static const bool roll = getenv("SPG_BCOMB_ROLL") && atoi(getenv("SPG_BCOMB_ROLL")) != 0;
 #define SPG_BCOMB(CC, GG, BB)                                                                      \
   do {                                                                                             \
     if (roll)                                                                                      \

@@ -1601,17 +1601,15 @@ static int witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, si
     for (size_t p = 0; p < secs[w].num_instances; p++) {
       if (W->off[w][p] == kNotResident) continue;
       size_t n = W->num_proofs[w][p] * W->num_inputs[w][p];
-      // Scalar([u64; 4]) and Fq(u32[8]) share the little-endian byte image
-      if (hipMemcpyAsync(W->d_w + W->off[w][p], secs[w].w[p], n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream) !=
-          hipSuccess) {
+      // Scalar([u64; 4]) and Fq(u32[8]) share the little-endian byte image. Streamed through the page-locked ring
+      // (h2d_stream: host pool copies, DMA on the upload stream): the call returns once the caller's buffers are read,
+      // with the last chunks' DMAs in flight and the context stream ordered after them (round 6; a pageable
+      // hipMemcpyAsync ran at ~26 GB/s and was synchronised here)
+      if (int rc = h2d_stream(ctx, W->d_w + W->off[w][p], secs[w].w[p], n * sizeof(Fq))) {
         spg_r1cs_witness_free(ctx, W);
-        return set_err(ctx, SPG_E_HIP, "witness upload");
+        return rc;
       }
     }
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
-    spg_r1cs_witness_free(ctx, W);
-    return set_err(ctx, SPG_E_HIP, "witness upload");
-  }
   *out = W;
   return SPG_OK;
 }
@@ -1699,8 +1697,8 @@ extern "C" int spg_r1cs_witness_new_shard(spg_ctx* ctx, const spg_witness_sec* s
   return witness_new(ctx, secs, nws, p0, p1, out);
 }
 extern "C" int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* W) {
-  (void)ctx;
   if (!W) return SPG_OK;
+  if (ctx) h2d_sync(ctx);  // a streamed upload into it may still be in flight
   hipFree(W->d_w);
   delete W;
   return SPG_OK;

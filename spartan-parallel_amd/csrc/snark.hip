@@ -746,6 +746,7 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
     return m;
   };
   auto fail = [&](int rc, const char* msg) {
+    h2d_sync(ctx);
     for (auto* d : W->d_block_vars) hipFree(d);
     hipFree(W->d_exec);
     delete W;
@@ -768,9 +769,14 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
     const size_t rows_p = npow2(std::max<size_t>(n, 1));
     if (hipMalloc(&d, rows_p * w * sizeof(Fq) + 64) != hipSuccess) return fail(SPG_E_NOMEM, "block_vars");
     W->d_block_vars.push_back(d);
-    if (hipMemsetAsync(d, 0, rows_p * w * sizeof(Fq), ctx->stream) != hipSuccess ||
-        (n && hipMemcpyAsync(d, a->block_vars[i], n * w * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
+    // the padding rows zeroed on the context stream, the rows themselves streamed (h2d_stream: page-locked ring, host
+    // pool copies, DMA on the upload stream; disjoint bytes, and the context stream waits for the DMAs)
+    if (rows_p > n && hipMemsetAsync(d + n * w, 0, (rows_p - n) * w * sizeof(Fq), ctx->stream) != hipSuccess)
       return fail(SPG_E_HIP, "block_vars upload");
+    if (n) {
+      const int rc = h2d_stream(ctx, d, a->block_vars[i], n * w * sizeof(Fq));
+      if (rc) return fail(rc, "block_vars upload");
+    }
   }
   const size_t ce = npow2(a->consis_num_proofs);
   W->exec = rows(a->exec_inputs, a->consis_num_proofs, a->num_ios, a->num_ios);
@@ -791,13 +797,13 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
     W->addr_vir = rows(a->addr_vir_mems, a->total_num_vir_mem_accesses, VIR_MEM_WIDTH, VIR_MEM_WIDTH);
     W->ts_bits = rows(a->addr_ts_bits, a->total_num_vir_mem_accesses, a->mem_addr_ts_bits_size, a->mem_addr_ts_bits_size);
   }
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(SPG_E_HIP, "witness upload");
+  // (no synchronisation: the streamed DMAs complete on their own, ahead of everything later on the context stream)
   *out = W;
   return SPG_OK;
 }
 extern "C" int spg_snark_witness_free(spg_ctx* ctx, spg_snark_wit* W) {
-  (void)ctx;
   if (!W) return SPG_OK;
+  if (ctx) h2d_sync(ctx);  // a streamed upload into it may still be in flight
   for (auto* d : W->d_block_vars) hipFree(d);
   hipFree(W->d_exec);
   delete W;

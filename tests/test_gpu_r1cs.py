@@ -180,3 +180,35 @@ def test_r1cs_thread_form_rounds(oracle, case, env):
     import hashlib
 
     assert out.stdout.split()[-1] == hashlib.sha256(ref).hexdigest()
+
+
+def test_witness_upload_releases_caller_buffers(ctx, r1cs_gens):
+    """spg_r1cs_witness_new streams the witness through the page-locked upload ring (h2d_stream) and returns once the
+    caller's buffers have been read, with DMAs still in flight: overwriting the caller's arrays right after the call
+    must not change the proof, and freeing a witness whose upload may be in flight must be safe. 3 x 2^10 executions x
+    512 inputs = 48 MiB, so the 32 MiB ring wraps."""
+    import spg
+    import workload
+
+    shape = ([256] * 3, [1024] * 3)
+    seed = workload.tape_seed()
+
+    def prove(wl, scribble):
+        v = workload.CViews(wl)
+        inst = spg.R1CSInst(ctx, v.inst)
+        spg.R1CSWitness(ctx, v.secs, wl.nws)  # dropped at once: freed with its upload possibly in flight
+        wit = spg.R1CSWitness(ctx, v.secs, wl.nws)
+        if scribble:
+            for mats in wl.sections:
+                for m in mats:
+                    m[...] = 0xFFFFFFFFFFFFFFFF  # the caller reuses its buffers
+            for arr in v.keep:
+                if arr.ndim == 3:
+                    arr[...] = 0xFFFFFFFFFFFFFFFF
+        pf, _ = spg.r1cs_prove(ctx, r1cs_gens, inst, wit, wl.P, wl.max_num_proofs, wl.num_proofs, wl.max_num_inputs,
+                               wl.num_inputs, spg.Transcript(b"upload_test"), spg.RandomTape(b"proof", seed))
+        return pf
+
+    a = prove(workload.R1CSWorkload(*shape), scribble=True)
+    b = prove(workload.R1CSWorkload(*shape), scribble=False)
+    assert a == b

@@ -117,6 +117,7 @@ ROUND_FORMS = {
     "tree_levels_per_launch": {"SPG_TREE_TOP": "0"},
     "tree_one_launch": {"SPG_TREE_TOP": str(1 << 40)},
     "delta_bucket_msm": {"SPG_DELTA_COMB": "0"},
+    "bullet_comb_rolled": {"SPG_BCOMB_ROLL": "1"},
 }
 
 
