@@ -101,6 +101,49 @@ void h2d_sync(spg_ctx* c) {
   if (c->stream_up) hipStreamSynchronize(c->stream_up);
 }
 
+static constexpr size_t kDevCacheBlocks = 4;
+static constexpr size_t kDevCacheBytes = (size_t)2 << 30;
+
+static void dev_cache_trim(spg_ctx* c, size_t keep_blocks, size_t keep_bytes) {
+  size_t tot = 0;
+  for (auto& b : c->dcache) tot += b.second;
+  while (!c->dcache.empty() && (c->dcache.size() > keep_blocks || tot > keep_bytes)) {
+    tot -= c->dcache.front().second;
+    hipFree(c->dcache.front().first);
+    c->dcache.erase(c->dcache.begin());
+  }
+}
+
+void* dev_cache_get(spg_ctx* c, size_t bytes) {
+  int best = -1;
+  for (size_t i = 0; i < c->dcache.size(); i++) {
+    const size_t b = c->dcache[i].second;
+    if (b >= bytes && b <= 2 * bytes && (best < 0 || b < c->dcache[best].second)) best = (int)i;
+  }
+  if (best >= 0) {
+    void* p = c->dcache[best].first;
+    c->dcache.erase(c->dcache.begin() + best);
+    return p;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) == hipSuccess) return p;
+  (void)hipGetLastError();
+  dev_cache_trim(c, 0, 0);
+  if (hipMalloc(&p, bytes) == hipSuccess) return p;
+  (void)hipGetLastError();
+  return nullptr;
+}
+
+void dev_cache_put(spg_ctx* c, void* p, size_t bytes) {
+  if (!p) return;
+  if (bytes > kDevCacheBytes) {
+    hipFree(p);
+    return;
+  }
+  c->dcache.push_back({p, bytes});
+  dev_cache_trim(c, kDevCacheBlocks, kDevCacheBytes);
+}
+
 void* mapped_get(spg_ctx* c, size_t bytes, void** dev) {
   static const bool on = !getenv("SPG_MAPPED_BUCKETS") || atoi(getenv("SPG_MAPPED_BUCKETS")) != 0;
   if (!on) return nullptr;
@@ -450,6 +493,7 @@ extern "C" int spg_free(spg_ctx* c) {
   if (c->stream2) hipStreamSynchronize(c->stream2);
   if (c->comm_owned_free) c->comm_owned_free(c->comm_owned);
   if (c->wt_cache) spg_r1cs_witness_free(c, c->wt_cache);
+  spg::dev_cache_trim(c, 0, 0);
   for (auto* space : {&c->ws, &c->ws2})
     for (auto& s : *space)
       if (s.p) hipFree(s.p);

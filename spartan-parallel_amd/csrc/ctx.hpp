@@ -38,6 +38,8 @@ struct spg_ctx {
   bool up_used[8] = {};
   int up_next = 0;
   hipEvent_t ev_up_done = nullptr;
+  // device blocks of freed witnesses kept for the next upload (dev_cache_get / dev_cache_put)
+  std::vector<std::pair<void*, size_t>> dcache;
   // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into
   // directly (mapped_get): the host reads them after the stream synchronisation, no D2H copy launch
   void* mapped = nullptr;
@@ -169,6 +171,12 @@ void* enc_stage_get(spg_ctx* c, size_t bytes);  // callers synchronise before re
 int h2d_stream(spg_ctx* c, void* dst, const void* src, size_t bytes);
 // waits for every streamed upload of the context (before device memory they target is freed)
 void h2d_sync(spg_ctx* c);
+// device memory for per-call uploads (witnesses): a block freed earlier by dev_cache_put when one fits (at most twice
+// the size asked for), else hipMalloc (after releasing the cached blocks if the first attempt fails); nullptr on failure.
+// dev_cache_put keeps a block for reuse (up to 4 blocks / 2 GiB per context; the oldest are freed). A per-prove
+// upload of the same shape then skips hipMalloc / hipFree of 10^8-byte buffers.
+void* dev_cache_get(spg_ctx* c, size_t bytes);
+void dev_cache_put(spg_ctx* c, void* p, size_t bytes);
 
 // coherent mapped host memory of at least `bytes`: host pointer returned, device alias in *dev (contents
 // undefined; a larger request synchronises the stream before freeing the old buffer). Null when

@@ -1590,7 +1590,7 @@ static int witness_new(spg_ctx* ctx, const spg_witness_sec* secs, size_t nws, si
     }
   }
   W->total = total;
-  if (hipMalloc(&W->d_w, total * sizeof(Fq) + 64) != hipSuccess) {
+  if (!(W->d_w = (Fq*)dev_cache_get(ctx, total * sizeof(Fq) + 64))) {
     delete W;
     return set_err(ctx, SPG_E_NOMEM, "witness upload");
   }
@@ -1698,8 +1698,12 @@ extern "C" int spg_r1cs_witness_new_shard(spg_ctx* ctx, const spg_witness_sec* s
 }
 extern "C" int spg_r1cs_witness_free(spg_ctx* ctx, spg_r1cs_witness* W) {
   if (!W) return SPG_OK;
-  if (ctx) h2d_sync(ctx);  // a streamed upload into it may still be in flight
-  hipFree(W->d_w);
+  if (ctx) {
+    h2d_sync(ctx);  // a streamed upload into it may still be in flight
+    dev_cache_put(ctx, W->d_w, W->total * sizeof(Fq) + 64);  // kept for the next witness of this size
+  } else {
+    hipFree(W->d_w);
+  }
   delete W;
   return SPG_OK;
 }

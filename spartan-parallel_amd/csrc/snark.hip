@@ -121,6 +121,7 @@ struct spg_snark_wit {
   std::vector<size_t> phy_ops, vir_ops, nvars, nproofs;
   std::vector<Rows> block_io;  // [b][q] first 2 * num_inputs_unpadded entries of every block_vars row
   std::vector<Fq*> d_block_vars;
+  std::vector<size_t> d_block_bytes;  // their allocation sizes (dev_cache_put on free)
   Rows exec, init_phy, init_vir, addr_phy, addr_vir, ts_bits;
   Fq* d_exec = nullptr;
 };
@@ -747,7 +748,7 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
   };
   auto fail = [&](int rc, const char* msg) {
     h2d_sync(ctx);
-    for (auto* d : W->d_block_vars) hipFree(d);
+    for (size_t i = 0; i < W->d_block_vars.size(); i++) dev_cache_put(ctx, W->d_block_vars[i], W->d_block_bytes[i]);
     hipFree(W->d_exec);
     delete W;
     return set_err(ctx, rc, msg);
@@ -767,8 +768,9 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
     // resident copy, padded to next_pow2(num_proofs) rows of zeros (lib.rs:1209-1216)
     Fq* d = nullptr;
     const size_t rows_p = npow2(std::max<size_t>(n, 1));
-    if (hipMalloc(&d, rows_p * w * sizeof(Fq) + 64) != hipSuccess) return fail(SPG_E_NOMEM, "block_vars");
+    if (!(d = (Fq*)dev_cache_get(ctx, rows_p * w * sizeof(Fq) + 64))) return fail(SPG_E_NOMEM, "block_vars");
     W->d_block_vars.push_back(d);
+    W->d_block_bytes.push_back(rows_p * w * sizeof(Fq) + 64);
     // the padding rows zeroed on the context stream, the rows themselves streamed (h2d_stream: page-locked ring, host
     // pool copies, DMA on the upload stream; disjoint bytes, and the context stream waits for the DMAs)
     if (rows_p > n && hipMemsetAsync(d + n * w, 0, (rows_p - n) * w * sizeof(Fq), ctx->stream) != hipSuccess)
@@ -803,8 +805,12 @@ extern "C" int spg_snark_witness_new(spg_ctx* ctx, const spg_snark_inputs* a, sp
 }
 extern "C" int spg_snark_witness_free(spg_ctx* ctx, spg_snark_wit* W) {
   if (!W) return SPG_OK;
-  if (ctx) h2d_sync(ctx);  // a streamed upload into it may still be in flight
-  for (auto* d : W->d_block_vars) hipFree(d);
+  if (ctx) {
+    h2d_sync(ctx);  // a streamed upload into it may still be in flight
+    for (size_t i = 0; i < W->d_block_vars.size(); i++) dev_cache_put(ctx, W->d_block_vars[i], W->d_block_bytes[i]);
+  } else {
+    for (auto* d : W->d_block_vars) hipFree(d);
+  }
   hipFree(W->d_exec);
   delete W;
   return SPG_OK;
