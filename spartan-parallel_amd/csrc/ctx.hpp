@@ -12,6 +12,10 @@
 #include "../../include/spg.h"
 #include "curve.hpp"
 
+namespace spg {
+struct Uploader;  // api.hip
+}
+
 struct spg_ctx {
   int device = -1;
   // spg_set_comb(ctx, 0): this context's MSMs skip the comb tables (comb.hip) and run the bucket pipelines, for an
@@ -32,7 +36,7 @@ struct spg_ctx {
   size_t enc_stage_bytes = 0;
   // streamed uploads of caller host data (h2d_stream, api.hip): upload workers, each with its own copy stream and two
   // page-locked chunk slots (created on first use, joined by spg_free)
-  struct Uploader* up = nullptr;
+  spg::Uploader* up = nullptr;
   // device blocks of freed witnesses kept for the next upload (dev_cache_get / dev_cache_put)
   std::vector<std::pair<void*, size_t>> dcache;
   // fine-grained (coherent, mapped) host buffer that latency-path kernels write their bucket sums into
