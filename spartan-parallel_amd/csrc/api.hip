@@ -123,8 +123,9 @@ struct Uploader {
     src = s;
     bytes = n;
     // about two chunks per worker, 256 KB .. 4 MB, 64 KB multiples
+    static const size_t fixed = getenv("SPG_H2D_CHUNK_KB") ? (size_t)atol(getenv("SPG_H2D_CHUNK_KB")) << 10 : 0;
     const size_t want = (n / (2 * lanes.size()) + 65535) & ~(size_t)65535;
-    ch = std::min(kUpChunk, std::max<size_t>((size_t)256 << 10, want));
+    ch = fixed ? std::min(kUpChunk, fixed) : std::min(kUpChunk, std::max<size_t>((size_t)256 << 10, want));
     err = 0;
     remaining = (int)lanes.size();
     gen++;
@@ -173,7 +174,12 @@ int h2d_stream(spg_ctx* c, void* dst, const void* src, size_t bytes) {
       return set_err(c, rc, "upload workers");
     }
   }
+  static const bool trace = getenv("SPG_H2D_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   if (int rc = c->up->run((uint8_t*)dst, (const uint8_t*)src, bytes)) return set_err(c, rc, "streamed upload");
+  if (trace)
+    fprintf(stderr, "[spg h2d] %zu bytes, chunk %zu, %d workers: %.1f us\n", bytes, c->up->ch, (int)c->up->lanes.size(),
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   // the context stream waits for every worker's last DMA
   for (auto& L : c->up->lanes)
     if (L.used[L.u ^ 1]) SPG_HIP(c, hipStreamWaitEvent(c->stream, L.ev[L.u ^ 1], 0));
