@@ -158,7 +158,11 @@ struct Uploader {
 
 int h2d_stream(spg_ctx* c, void* dst, const void* src, size_t bytes) {
   if (!bytes) return 0;
-  static const bool on = !getenv("SPG_H2D") || atoi(getenv("SPG_H2D")) != 0;
+  // default: one pageable hipMemcpyAsync (HIP stages it through its own page-locked buffers at ~56 GB/s on the box, and
+  // returns once the caller's bytes are staged). SPG_H2D=1: the upload workers below -- as fast when they run, but 8 more
+  // busy threads beside the pool's spinning workers pass the job's CPU quota and the process is throttled for ~9 ms at
+  // a time (scripts/upload_probe.py, profiles/r06_upload_probe.txt: 268 MB in 4.7 ms either way, 13-80 ms with stalls)
+  static const bool on = getenv("SPG_H2D") && atoi(getenv("SPG_H2D")) != 0;
   if (!on) {
     SPG_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     return 0;

@@ -168,7 +168,8 @@ void* enc_stage_get(spg_ctx* c, size_t bytes);  // callers synchronise before re
 // chunks overlap (scripts/micro/h2d_upload.hip on the box: 8 workers ~2.7 ms for 134 MB, 50 GB/s, against 4.5 ms for one
 // pageable hipMemcpyAsync). Returns once every byte has left `src` (the caller's buffer is free again); the last DMAs may
 // still be in flight, and the context stream waits for them (work queued on it afterwards, and on stream2 behind it, sees
-// the data). SPG_H2D=0: one pageable hipMemcpyAsync on the context stream instead. Returns 0 or an SPG error code.
+// the data). Default (SPG_H2D unset or 0): one pageable hipMemcpyAsync on the context stream instead, which returns
+// once HIP has staged the bytes (measured as fast, and no extra threads; api.hip). Returns 0 or an SPG error code.
 int h2d_stream(spg_ctx* c, void* dst, const void* src, size_t bytes);
 // waits for every streamed upload of the context (before device memory they target is freed)
 void h2d_sync(spg_ctx* c);

@@ -804,19 +804,26 @@ int Prover::run_inner(Laps& lp) {
     const Fq* Ap_l = Ap + p0;  // eq(tau_p) indexed by the global instance in the x / q rounds
     // round j's evaluation is enqueued right after round j-1's folds, so it runs on the device while the
     // host finishes round j-1's proof (comm_eval, DotProductProof); eval_wait then collects (e0, e2, e3)
-    auto launch_eval = [&](size_t j, const FoldPlan* fold) -> int {
-      int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
+    auto mode_of = [&](size_t j) { return j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P); };
+    // round j's sizes: the half lengths of the reference's loop and the per-instance domain sizes of the round
+    auto advance = [&](size_t j) -> int {
+      const int mode = mode_of(j);
       if (cons_len > 1) cons_len /= 2;
       else if (proof_len > 1) proof_len /= 2;
       else instance_len /= 2;
+      if (mode != MODE_P)
+        for (size_t p = 0; p < sc_np.size(); p++) {  // instance_len >= P here: every instance takes part
+          if (mode == MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
+          if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
+        }
+      return mode;
+    };
+    auto launch_eval = [&](size_t j, const FoldPlan* fold) -> int {
+      const int mode = advance(j);
       if (mode == MODE_P) {
         std::vector<size_t> ones(P, 1);
         return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, ones, ones, Ap, Aq, Ax, T->d, TB, TC,
                            partials, nullptr);
-      }
-      for (size_t p = 0; p < sc_np.size(); p++) {  // instance_len >= P here: every instance takes part
-        if (mode == MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
-        if (mode == MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
       }
       return phase1_eval(ctx, *T, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap_l, Aq, Ax, T->d, TB,
                          TC, partials, nullptr, fold);
@@ -850,12 +857,167 @@ int Prover::run_inner(Laps& lp) {
       TC = Cc;
       return 0;
     };
+    // ---- two rounds per launch (sumcheck.hip k_phase1_pair; SPG_P1_PAIR=0: one per launch). A pair takes rounds j,
+    // j + 1 of one mode (x or q) when every instance's size in that mode is >= 4 and round j + 1's domain holds at most
+    // SPG_P1_PAIR_MAX (default 8192) points: the latency-bound rounds. Unsharded proofs only (a sharded round sums 3
+    // scalars over the ranks, a pair would sum 15).
+    static const bool pair_on = !getenv("SPG_P1_PAIR") || atoi(getenv("SPG_P1_PAIR")) != 0;
+    static const size_t pair_max = std::min<size_t>(
+        kP1PairMax, getenv("SPG_P1_PAIR_MAX") ? (size_t)atol(getenv("SPG_P1_PAIR_MAX")) : (size_t)8192);
+    auto pair_ok = [&](size_t j) -> bool {
+      if (!pair_on || !Aq2 || nranks != 1 || j + 1 >= rounds || T != &Az) return false;
+      const int m = mode_of(j);
+      if (m == MODE_P || mode_of(j + 1) != m) return false;
+      size_t dom = 0;
+      for (size_t p = 0; p < sc_np.size(); p++) {
+        const size_t N = m == MODE_X ? T->num_inputs[p] : T->num_proofs[p];
+        const size_t Nl = m == MODE_X ? sc_nc[p] : sc_np[p];  // the round's local size before its halving
+        if (N < 4 || N != Nl) return false;
+        dom += m == MODE_X ? sc_np[p] * (N / 4) : (N / 4) * sc_nc[p];
+      }
+      return dom > 0 && dom <= pair_max;
+    };
+    // rounds j, j + 1 in one launch; nf = 1: round j - 1's pending fold (fp), 2: the previous pair's (r1, r2)
+    auto launch_pair = [&](size_t j, int nf, const FoldPlan* fp, const Fq& r1, const Fq& r2) -> int {
+      const int m = advance(j);
+      P1Pair pp;
+      pp.mode = m;
+      pp.c = m == MODE_X ? cons_len : proof_len;  // round j's half length of the mode's eq table
+      for (size_t p = 0; p < sc_np.size(); p++) {
+        const size_t N = m == MODE_X ? T->num_inputs[p] : T->num_proofs[p];
+        if (m == MODE_X) {
+          pp.rows.push_back(sc_np[p]);
+          pp.cols.push_back(N / 4);
+          pp.step_x.push_back(pp.c / (N / 2));
+          pp.step_q.push_back(proof_len / sc_np[p]);
+        } else {
+          pp.rows.push_back(N / 4);
+          pp.cols.push_back(sc_nc[p]);
+          pp.step_q.push_back(pp.c / (N / 2));
+          pp.step_x.push_back(cons_len / sc_nc[p]);
+        }
+      }
+      advance(j + 1);
+      pp.nf = nf;
+      pp.r1 = r1;
+      pp.r2 = r2;
+      Fq*& E = m == MODE_X ? Ax : Aq;
+      Fq*& Ealt = m == MODE_X ? Ax2 : Aq2;
+      size_t& lenE = m == MODE_X ? lenX : lenQ;
+      if (nf == 1) {
+        pp.fstride = fp->stride;
+        pp.fmode = fp->arg.fmode;
+        pp.side_in = fp->arg.side_in;
+        pp.side_out = fp->arg.side_out;
+        pp.side_live = fp->arg.side_half;
+      } else if (nf == 2) {  // the previous pair's folds of this mode's eq table: E (live lenE) -> Ealt (lenE / 4)
+        pp.fmode = m;
+        pp.side_in = E;
+        pp.side_out = Ealt;
+        pp.side_live = lenE / 4;
+        std::swap(E, Ealt);
+        lenE /= 4;
+      }
+      pp.Ap = Ap_l;
+      pp.Aq = Aq;
+      pp.Ax = Ax;
+      pp.B = T->d;
+      pp.C = TB;
+      pp.D = TC;
+      int r = phase1_pair(ctx, *T, pp, partials, nullptr);
+      if (r) return r;
+      // the size bookkeeping of both rounds' folds (the folds themselves ride in the next launch)
+      FoldPlan tmp;
+      if ((r = pqx_fold_plan(ctx, *T, m, &tmp)) || (r = pqx_fold_plan(ctx, *T, m, &tmp))) return r;
+      return 0;
+    };
+    // a pair's pending folds (r1, r2) on their own launch, before a single round or the instance rounds
+    auto fold2x = [&](int m, const Fq& r1, const Fq& r2) -> int {
+      P1Pair pp;
+      pp.mode = m;
+      for (size_t p = 0; p < sc_np.size(); p++) {
+        pp.rows.push_back(T->num_proofs[p]);
+        pp.cols.push_back(T->num_inputs[p]);
+      }
+      Fq*& E = m == MODE_X ? Ax : Aq;
+      Fq*& Ealt = m == MODE_X ? Ax2 : Aq2;
+      size_t& lenE = m == MODE_X ? lenX : lenQ;
+      pp.r1 = r1;
+      pp.r2 = r2;
+      pp.side_in = E;
+      pp.side_out = Ealt;
+      pp.side_live = lenE / 4;
+      pp.B = T->d;
+      pp.C = TB;
+      pp.D = TC;
+      std::swap(E, Ealt);
+      lenE /= 4;
+      return phase1_fold2x(ctx, *T, pp);
+    };
+    auto lagrange4 = [](const Fq& r, Fq L[4]) {  // the cubic Lagrange basis on 0..3 at r
+      static const Fq inv2 = fq_inv(fq_from_u64(2)), inv6 = fq_inv(fq_from_u64(6));
+      const Fq a0 = r, a1 = fq_sub(r, fq_one()), a2 = fq_sub(a1, fq_one()), a3 = fq_sub(a2, fq_one());
+      const Fq a01 = fq_mul(a0, a1), a23 = fq_mul(a2, a3);
+      L[0] = fq_neg(fq_mul(fq_mul(a1, a23), inv6));
+      L[1] = fq_mul(fq_mul(a0, a23), inv2);
+      L[2] = fq_neg(fq_mul(fq_mul(a01, a3), inv2));
+      L[3] = fq_mul(fq_mul(a01, a2), inv6);
+    };
     if (rounds && nx + nq == 0) rc = to_compact();
-    if (!rc && rounds) rc = launch_eval(0, nullptr);
+    bool cur_pair = false;  // the launch in flight evaluates rounds j, j + 1
+    if (!rc && rounds) {
+      cur_pair = pair_ok(0);
+      rc = cur_pair ? launch_pair(0, 0, nullptr, fq_zero(), fq_zero()) : launch_eval(0, nullptr);
+    }
     if (rc) return rc;
     zk.init(g, tape, rounds, fq_zero(), fq_zero());  // host precomputation while round 0 evaluates
-    for (size_t j = 0; j < rounds; j++) {
-      int mode = j < nx ? MODE_X : (j < nx + nq ? MODE_Q : MODE_P);
+    for (size_t j = 0; j < rounds;) {
+      if (cur_pair) {
+        const int mode = mode_of(j);
+        Fq ev[15];
+        rc = pair_wait(ctx, ev);
+        if (!rc && (j == z_after || j + 1 == z_after)) rc = queue_z_fill();
+        if (!rc && (j == 1 || j + 1 == 1) && failpoint(ctx, "r1cs_round")) rc = set_err(ctx, SPG_E_HIP, "failpoint r1cs_round");
+        if (rc) return rc;
+        lp.lap("p1_eval");
+        // round j: F(X, 0) + F(X, 1) at X = 0, 2, 3
+        const Fq ej[3] = {fq_add(ev[0], ev[12]), fq_add(ev[2], ev[13]), fq_add(ev[3], ev[14])};
+        const Fq r_j = zk.begin(g, t, j, ej);
+        zk.finish(g, t, tape, j, r_j);
+        rx_all.push_back(r_j);
+        // round j + 1: the cubics t -> F(t, Y) (Y = 0, 2, 3) at t = r_j
+        Fq L[4];
+        lagrange4(r_j, L);
+        Fq ej1[3];
+        for (int y = 0; y < 3; y++) {
+          Fq acc = fq_zero();
+          for (int k = 0; k < 4; k++) acc = fq_add(acc, fq_mul(L[k], ev[4 * y + k]));
+          ej1[y] = acc;
+        }
+        const Fq r_j1 = zk.begin(g, t, j + 1, ej1);
+        lp.lap("p1_host");
+        // the next launch: another pair of this mode (the two folds ride in it), else the folds on their own launch
+        // and a single round (or the compaction before the instance rounds)
+        if (j + 2 < rounds && mode_of(j + 2) == mode && pair_ok(j + 2)) {
+          rc = launch_pair(j + 2, 2, nullptr, r_j, r_j1);
+          cur_pair = true;
+        } else {
+          rc = fold2x(mode, r_j, r_j1);
+          if (!rc && j + 2 == nx + nq && np > 0) rc = to_compact();
+          if (!rc && j + 2 < rounds) {
+            cur_pair = pair_ok(j + 2);
+            rc = cur_pair ? launch_pair(j + 2, 0, nullptr, fq_zero(), fq_zero()) : launch_eval(j + 2, nullptr);
+          }
+        }
+        if (rc) return rc;
+        lp.lap("p1_fold");
+        zk.finish(g, t, tape, j + 1, r_j1);
+        lp.lap("p1_host");
+        rx_all.push_back(r_j1);
+        j += 2;
+        continue;
+      }
+      int mode = mode_of(j);
       Fq e[3];
       rc = eval_wait(ctx, e);
       if (!rc && j == z_after) rc = queue_z_fill();  // round j is done and round j + 1 not yet queued
@@ -870,7 +1032,8 @@ int Prover::run_inner(Laps& lp) {
       Fq* side = mode == MODE_P ? Ap : (mode == MODE_Q ? Aq : Ax);
       size_t& side_len = mode == MODE_P ? lenP : (mode == MODE_Q ? lenQ : lenX);
       const bool compact_next = j + 1 == nx + nq && np > 0;
-      const int next_mode = j + 1 < nx ? MODE_X : (j + 1 < nx + nq ? MODE_Q : MODE_P);
+      const int next_mode = mode_of(j + 1);
+      cur_pair = false;
       if (Aq2 && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
         FoldPlan fp;
         rc = pqx_fold_plan(ctx, *T, mode, &fp);
@@ -883,18 +1046,25 @@ int Prover::run_inner(Laps& lp) {
         fp.arg.side_half = (uint32_t)(side_len / 2);
         std::swap(cur, alt);
         side_len /= 2;
-        if (!rc) rc = launch_eval(j + 1, &fp);
+        if (!rc) {
+          cur_pair = pair_ok(j + 1);
+          rc = cur_pair ? launch_pair(j + 1, 1, &fp, r_j, fq_zero()) : launch_eval(j + 1, &fp);
+        }
       } else {
         rc = pqx_bound(ctx, *T, TB, TC, r_j, mode, side, side_len);
         side_len /= 2;
         if (!rc && compact_next) rc = to_compact();
-        if (!rc && j + 1 < rounds) rc = launch_eval(j + 1, nullptr);
+        if (!rc && j + 1 < rounds) {
+          cur_pair = pair_ok(j + 1);
+          rc = cur_pair ? launch_pair(j + 1, 0, nullptr, fq_zero(), fq_zero()) : launch_eval(j + 1, nullptr);
+        }
       }
       if (rc) return rc;
       lp.lap("p1_fold");
       zk.finish(g, t, tape, j, r_j);
       lp.lap("p1_host");
       rx_all.push_back(r_j);
+      j++;
     }
     Fq a[6];  // eq factors, then Az, Bz, Cz (a single instance: it sits on this (only) rank's local tables)
     rc = np == 0 ? d2h_multi(ctx, {{Ap, 1}, {Aq, 1}, {Ax, 1}, {Az.d, 1}, {Bz, 1}, {Cz, 1}}, a)

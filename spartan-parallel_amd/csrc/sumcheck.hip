@@ -12,6 +12,7 @@
 // and a one-block kernel sums the block partials. Reduction order is irrelevant (exact arithmetic).
 #include <string.h>
 
+#include "cube.hpp"
 #include "lds.hpp"
 #include "qsum.hpp"
 #include "sumcheck.hpp"
@@ -751,6 +752,179 @@ __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, co
   grid_reduce3(e0, e2, e3, partials, counter, mb, seq);
 }
 
+
+// ---- phase 1, two rounds per launch (round 6; SPG_P1_PAIR=0 keeps one round per launch) -------------------------------
+// The latency-bound rounds of a ZK sumcheck are host round trips (launch, dispatch, mailbox) around a few us of work.
+// As the SPARK layer pairs (layer.hpp, k_layer_pair): with every factor of round j's summand F = A (B C - D) multilinear
+// in round j's variable t and round j + 1's variable s, round j's evaluation at X is sum F(X, 0) + F(X, 1) and round
+// j + 1's at Y is the cubic t -> sum F(t, Y) at t = r_j, so one launch posts F at 15 points of the 4 x 4 grid and the
+// host forms round j + 1's (e0, e2, e3) by Lagrange interpolation at r_j -- between the two rounds' commitments and
+// sigma proofs, with no device round trip. Pairs run inside one mode (x: bound_poly_x, q: bound_poly_q) where every
+// instance's size in that mode is >= 4, so neither round meets the ragged cases (a size-1 dimension's (1 - r) fold,
+// a missing hi entry). Element = one point of round j + 1's domain: x mode (p, q, x' < N/4), q mode (p, q' < N/4, x),
+// N = the instance's live size in the mode; its 2 x 2 cube is T[k + {0, N/4, N/2, 3N/4} u] (order 00, 01 (s), 10 (t),
+// 11; u = 1 in x mode, the row stride anw ani in q mode) and the eq table E of the mode (Ax / Aq) at ie + {0, c/2, c,
+// 3c/2} (c: round j's half length), times the other factors Ap[p] Aq[iq] (x mode) or Ap[p] Ax[ix] (q mode).
+// Pending folds (nf), applied to what the launch reads, folded entries written back in place:
+//   nf = 1, the previous single round's (FoldPlan: per-instance partner stride, 0 = the (1 - r) case; its side table
+//     fmode folded on the fly and written to side_out by a grid-stride pass), as k_phase1_eval<true>;
+//   nf = 2, the previous pair's (same mode): W = a + r1 (c - a) + r2 (b - a) + r1 r2 (d - c - b + a) over
+//     T[k + {0, 1, 2, 3} Q] (Q = the live size N u; r1 the previous pair's round-j challenge), the eq table likewise
+//     over its live size.
+// A run of pairs ends with k_phase1_fold2x (the last pair's two folds, one launch, no host wait) before the next
+// single round. Lanes: 16 per element, as k_layer_pair: g < 12 corner g & 3 of B, C, D (g >> 2); g 12..15 corner
+// g - 12 of E times the element's other eq factors; DPP row broadcasts; lane g < 15 forms point g's A (B C - D).
+struct P1PairArgs {
+  PqxArgs a;           // np / ni: live sizes at round j (N = ni in x mode, np in q mode); sc_np x sc_ni the element grid
+  int mode;            // MODE_X or MODE_Q
+  uint32_t total;      // elements
+  uint32_t c;          // round j's half length of the mode's eq table (its live size is 2 c)
+  int nf;              // pending folds: 0, 1 or 2
+  Fq r1, r2, r12;      // nf 1: r1 (omr = 1 - r1); nf 2: r1, r2 and their product
+  int fmode;           // nf >= 1: the table the pending fold binds (MODE_X: Ax, MODE_Q: Aq)
+  const Fq* side_in;   // that table before the pending fold(s)
+  Fq* side_out;        // its folded live entries (the other ping-pong buffer)
+  uint32_t side_live;  // entries after the pending fold(s) (nf 1: the half; nf 2: a quarter of side_in's live size)
+  const Fq* Ap;
+  const Fq* Aq;        // the current tables (a pending fold's table is read through side_in)
+  const Fq* Ax;
+  Fq* B;
+  Fq* C;
+  Fq* D;
+  Fq* partials;        // 16 per workgroup
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq;
+};
+__device__ __forceinline__ Fq bilerp(const Fq& a, const Fq& b, const Fq& c, const Fq& d, const Fq& r1, const Fq& r2,
+                                     const Fq& r12) {
+  // a: (0, 0), b: (0, 1) (r2's variable), c: (1, 0) (r1's), d: (1, 1)
+  const Fq t1 = fq_mul(r1, fq_sub(c, a)), t2 = fq_mul(r2, fq_sub(b, a)), t3 = fq_mul(r12, fq_add(fq_sub(d, c), fq_sub(a, b)));
+  return fq_add(fq_add(a, t1), fq_add(t2, t3));
+}
+// entry i of the side table as the pending fold(s) leave it
+__device__ __forceinline__ Fq p1_side_at(const P1PairArgs& A, uint32_t i) {
+  const Fq* s = A.side_in;
+  const uint32_t L = A.side_live;
+  if (A.nf == 1) {
+    const Fq lo = s[i];
+    return fq_add(lo, fq_mul(A.r1, fq_sub(s[i + L], lo)));
+  }
+  return bilerp(s[i], s[i + L], s[i + 2 * L], s[i + 3 * L], A.r1, A.r2, A.r12);
+}
+template <int BS>
+__global__ void __launch_bounds__(BS) k_phase1_pair(P1PairArgs A) {
+  __shared__ bool last;
+  const int t = threadIdx.x, g = t & 15;
+  const uint32_t gt = blockIdx.x * BS + t, gstride = gridDim.x * BS;
+  // the pending fold's side table: its folded live entries into side_out (idle lanes first, then grid-stride)
+  if (A.nf > 0)
+    for (uint32_t i = gt; i < A.side_live; i += gstride) A.side_out[i] = p1_side_at(A, i);
+  const uint32_t u = gt >> 4;  // this row's element (rows past the end idle, contribute zero)
+  const int pt = g < 4 ? g : (g < 8 ? g - 4 : (g < 12 ? g - 8 : (g == 12 ? 0 : (g == 13 ? 2 : 3))));
+  const int ps = g < 4 ? 0 : (g < 8 ? 2 : (g < 12 ? 3 : 1));
+  Fq e = fq_zero();
+  if (u < A.total) {
+    const int p = find_inst(A.a, u);
+    const PqxInst& d = pinst(A.a, p);
+    const uint32_t loc = u - d.dom_off;
+    const uint32_t r = loc / d.sc_ni, col = loc % d.sc_ni;  // x mode: (q, x'); q mode: (q', x)
+    const bool xm = A.mode == MODE_X;
+    const size_t unit = xm ? 1 : (size_t)d.anw * d.ani;
+    const uint32_t N = xm ? d.ni : d.np;
+    const size_t base = pqx_off(d) + (size_t)r * d.anw * d.ani + col;
+    const int m = g & 3;  // corner: 0 (0, 0), 1 (0, s), 2 (t, 0), 3 (t, s)
+    const uint32_t cq = (m & 1 ? N / 4 : 0) + (m & 2 ? N / 2 : 0);
+    const bool side_x = A.nf > 0 && A.fmode == MODE_X, side_q = A.nf > 0 && A.fmode == MODE_Q;
+    Fq w = fq_zero();
+    if (g < 12) {
+      Fq* T = g < 4 ? A.B : (g < 8 ? A.C : A.D);
+      const size_t k = base + (size_t)cq * unit;
+      if (A.nf == 0) {
+        w = T[k];
+      } else if (A.nf == 1) {
+        const uint32_t fs = d.fstride;
+        const Fq lo = T[k];
+        w = fs ? fq_add(lo, fq_mul(A.r1, fq_sub(T[k + fs], lo))) : fq_mul(fq_sub(fq_one(), A.r1), lo);
+        T[k] = w;
+      } else {
+        const size_t Q = (size_t)N * unit;
+        w = bilerp(T[k], T[k + Q], T[k + 2 * Q], T[k + 3 * Q], A.r1, A.r2, A.r12);
+        T[k] = w;
+      }
+    } else {
+      // E corner m of the mode's eq table times the element's other eq factors
+      const uint32_t cm = (m & 1 ? A.c / 2 : 0) + (m & 2 ? A.c : 0);
+      Fq ev, other;
+      if (xm) {
+        const uint32_t ie = col * d.step_x + cm, iq = r * d.step_q;
+        ev = side_x ? p1_side_at(A, ie) : A.Ax[ie];
+        other = fq_mul(A.Ap[p], side_q ? p1_side_at(A, iq) : A.Aq[iq]);
+      } else {
+        const uint32_t ie = r * d.step_q + cm, ix = col * d.step_x;
+        ev = side_q ? p1_side_at(A, ie) : A.Aq[ie];
+        other = fq_mul(A.Ap[p], side_x ? p1_side_at(A, ix) : A.Ax[ix]);
+      }
+      w = fq_mul(other, ev);
+    }
+    const Fq b00 = fq_rowbcast<0>(w), b01 = fq_rowbcast<1>(w), b10 = fq_rowbcast<2>(w), b11 = fq_rowbcast<3>(w);
+    const Fq c00 = fq_rowbcast<4>(w), c01 = fq_rowbcast<5>(w), c10 = fq_rowbcast<6>(w), c11 = fq_rowbcast<7>(w);
+    const Fq d00 = fq_rowbcast<8>(w), d01 = fq_rowbcast<9>(w), d10 = fq_rowbcast<10>(w), d11 = fq_rowbcast<11>(w);
+    const Fq a00 = fq_rowbcast<12>(w), a01 = fq_rowbcast<13>(w), a10 = fq_rowbcast<14>(w), a11 = fq_rowbcast<15>(w);
+    const Fq bv = cube_at(b00, b01, b10, b11, pt, ps), cv = cube_at(c00, c01, c10, c11, pt, ps),
+             dv = cube_at(d00, d01, d10, d11, pt, ps), av = cube_at(a00, a01, a10, a11, pt, ps);
+    e = g < 15 ? fq_mul(av, fq_sub(fq_mul(bv, cv), dv)) : fq_zero();
+  }
+  row_block_sum<BS>(e);
+  if (gridDim.x == 1) {  // lanes 0..14 of wave 0 post the 15 point sums, then lane 0 the sequence number
+    if (t < 15) {
+      host_put(A.mb + 8 + 8 * t, e);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  // several workgroups: partials by sc1 stores and a ticket (as k_layer_pair)
+  if (t < 16) st_sc1(&A.partials[16 * blockIdx.x + t], e);
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(A.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  Fq sum = fq_zero();
+  for (unsigned j = t >> 4; j < gridDim.x; j += BS / 16) sum = fq_add(sum, ld_sc1(&A.partials[16 * j + g]));
+  row_block_sum<BS>(sum);
+  if (t < 15) {
+    host_put(A.mb + 8 + 8 * t, sum);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+// the last pair's two folds of B, C, D (every live entry, in place: T[k] from T[k + {0, 1, 2, 3} Q]) and of its eq
+// table (side_in -> side_out), before the next single round
+__global__ void __launch_bounds__(256) k_phase1_fold2x(P1PairArgs A) {
+  const uint32_t gt = blockIdx.x * 256 + threadIdx.x, gstride = gridDim.x * 256;
+  for (uint32_t i = gt; i < A.side_live; i += gstride) A.side_out[i] = p1_side_at(A, i);
+  for (uint32_t u = gt; u < A.total; u += gstride) {
+    const int p = find_inst(A.a, u);
+    const PqxInst& d = pinst(A.a, p);
+    const uint32_t loc = u - d.dom_off, r = loc / d.sc_ni, col = loc % d.sc_ni;
+    const bool xm = A.mode == MODE_X;
+    const size_t unit = xm ? 1 : (size_t)d.anw * d.ani;
+    const size_t Q = (size_t)(xm ? d.ni : d.np) * unit;
+    const size_t k = pqx_off(d) + (size_t)r * d.anw * d.ani + col;
+    A.B[k] = bilerp(A.B[k], A.B[k + Q], A.B[k + 2 * Q], A.B[k + 3 * Q], A.r1, A.r2, A.r12);
+    A.C[k] = bilerp(A.C[k], A.C[k + Q], A.C[k + 2 * Q], A.C[k + 3 * Q], A.r1, A.r2, A.r12);
+    A.D[k] = bilerp(A.D[k], A.D[k + Q], A.D[k + 2 * Q], A.D[k + 3 * Q], A.r1, A.r2, A.r12);
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 // round evaluations over at most this many domain points take the quad form (SPG_SC_QUAD_MAX; 0 = never): below it
 // the chip is not full and a point's chain of products sets the time
@@ -981,6 +1155,107 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
   }
   SPG_HIP(ctx, hipGetLastError());
   return eval_reduce_finish(ctx, out3);
+}
+
+// two phase-1 rounds in one launch (k_phase1_pair); the 15 point sums land in out15 (nullptr: collect them with
+// pair_wait). rows / cols: the element grid per instance (x mode: live q rows x N/4; q mode: N/4 x live x columns),
+// step_q / step_x the eq index steps of round j, c round j's half length of the mode's eq table.
+int phase1_pair(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp, Fq* partials, Fq* out15) {
+  P1PairArgs A;
+  std::vector<PqxInst> v;
+  pqx_fill_args(T, A.a, v);
+  const size_t P = pp.rows.size();
+  if (P > T.zlen || pp.cols.size() != P || pp.step_q.size() != P || pp.step_x.size() != P)
+    return set_err(ctx, SPG_E_ARG, "phase-1 pair: bad shape");
+  A.a.P = (int)P;
+  size_t dom = 0;
+  for (size_t p = 0; p < P; p++) {
+    PqxInst& d = v[p];
+    d.dom_off = (uint32_t)dom;
+    d.sc_np = (uint32_t)pp.rows[p];
+    d.sc_ni = (uint32_t)pp.cols[p];
+    d.step_q = (uint32_t)pp.step_q[p];
+    d.step_x = (uint32_t)pp.step_x[p];
+    const uint32_t N = pp.mode == MODE_X ? d.ni : d.np;
+    if (N < 4 || (N & (N - 1))) return set_err(ctx, SPG_E_ARG, "phase-1 pair: a size below 4");
+    if (pp.nf == 1) d.fstride = pp.fstride.at(p);
+    dom += pp.rows[p] * pp.cols[p];
+  }
+  if (dom == 0 || dom > kP1PairMax) return set_err(ctx, SPG_E_ARG, "phase-1 pair: domain size");
+  if (int rc = pqx_pack(ctx, v, A.a, kWsPqxA)) return rc;
+  A.mode = pp.mode;
+  A.total = (uint32_t)dom;
+  A.c = (uint32_t)pp.c;
+  A.nf = pp.nf;
+  A.r1 = pp.r1;
+  A.r2 = pp.r2;
+  A.r12 = fq_mul(pp.r1, pp.r2);
+  A.fmode = pp.fmode;
+  A.side_in = pp.side_in;
+  A.side_out = pp.side_out;
+  A.side_live = pp.nf ? (uint32_t)pp.side_live : 0;
+  A.Ap = pp.Ap;
+  A.Aq = pp.Aq;
+  A.Ax = pp.Ax;
+  A.B = pp.B;
+  A.C = pp.C;
+  A.D = pp.D;
+  A.partials = partials;
+  A.counter = ctx->d_counter;
+  A.mb = ctx->d_mbox;
+  A.seq = ++ctx->mbox_seq;
+  const unsigned nb = (unsigned)((16 * dom + 255) / 256);
+  {
+    // per element: 3 tables x 4 corners (x 4 entries read + 1 written with two pending folds) and the eq corners;
+    // Fq products: the folds (3 per corner at nf 2, 1 at nf 1), the eq corners (2 each), 15 points x 2
+    const double per = 32.0 * (12.0 * (pp.nf == 2 ? 5.0 : (pp.nf == 1 ? 3.0 : 1.0)) + 8.0);
+    KScope ks(ctx, "sc_phase1_pair", per * (double)dom + 32.0 * (pp.nf == 2 ? 5.0 : 3.0) * (double)A.side_live, 0.0,
+              (double)dom * (30.0 + 8.0 + 12.0 * (pp.nf == 2 ? 3.0 : (pp.nf == 1 ? 1.0 : 0.0))));
+    hipLaunchKernelGGL(k_phase1_pair<256>, dim3(nb), dim3(256), 0, ctx->stream, A);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return out15 ? mbox_wait(ctx, ctx->mbox_seq, out15, 15) : 0;
+}
+int pair_wait(spg_ctx* ctx, Fq* out15) { return mbox_wait(ctx, ctx->mbox_seq, out15, 15); }
+
+// the last pair's two folds (k_phase1_fold2x): T's sizes are those after both folds (pqx_fold_plan done twice);
+// rows / cols the live entry grid per instance, side: the pair's eq table (side_live entries after the folds)
+int phase1_fold2x(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp) {
+  P1PairArgs A;
+  std::vector<PqxInst> v;
+  pqx_fill_args(T, A.a, v);
+  const size_t P = pp.rows.size();
+  if (P > T.zlen || pp.cols.size() != P) return set_err(ctx, SPG_E_ARG, "phase-1 fold2x: bad shape");
+  A.a.P = (int)P;
+  size_t dom = 0;
+  for (size_t p = 0; p < P; p++) {
+    v[p].dom_off = (uint32_t)dom;
+    v[p].sc_np = (uint32_t)pp.rows[p];
+    v[p].sc_ni = (uint32_t)pp.cols[p];
+    dom += pp.rows[p] * pp.cols[p];
+  }
+  if (dom >= 0xffffffffULL) return set_err(ctx, SPG_E_ARG, "phase-1 fold2x: domain size");
+  if (int rc = pqx_pack(ctx, v, A.a, kWsPqxA)) return rc;
+  A.mode = pp.mode;
+  A.total = (uint32_t)dom;
+  A.nf = 2;
+  A.r1 = pp.r1;
+  A.r2 = pp.r2;
+  A.r12 = fq_mul(pp.r1, pp.r2);
+  A.side_in = pp.side_in;
+  A.side_out = pp.side_out;
+  A.side_live = (uint32_t)pp.side_live;
+  A.B = pp.B;
+  A.C = pp.C;
+  A.D = pp.D;
+  const size_t n = std::max(dom, pp.side_live);
+  {
+    KScope ks(ctx, "sc_fold", 32.0 * 5.0 * (3.0 * (double)dom + (double)pp.side_live));
+    hipLaunchKernelGGL(k_phase1_fold2x, dim3((unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 4096))),
+                       dim3(256), 0, ctx->stream, A);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
 }
 
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,

@@ -78,6 +78,27 @@ constexpr int kScGridMax = 4096;
 int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_t cons_len, size_t instance_len,
                 const std::vector<size_t>& sc_np, const std::vector<size_t>& sc_nc, const Fq* Ap, const Fq* Aq,
                 const Fq* Ax, Fq* B, Fq* C, Fq* D, Fq* partials, Fq* out3, const FoldPlan* fold = nullptr);
+// two phase-1 rounds in one launch (sumcheck.hip, k_phase1_pair): F = A (B C - D) posted on 15 points of round j's and
+// round j + 1's 4 x 4 grid -- g 0..3: (t, s) = (g, 0); 4..7: (g - 4, 2); 8..11: (g - 8, 3); 12, 13, 14: (0, 1),
+// (2, 1), (3, 1) -- with the pending fold(s) applied on the way (nf 0, 1: fstride per instance, 2: the previous pair's)
+constexpr size_t kP1PairMax = 8192;  // elements (16 lanes each; 16 partials per 256-thread workgroup in `partials`)
+struct P1Pair {
+  int mode = MODE_X;
+  std::vector<size_t> rows, cols, step_q, step_x;
+  size_t c = 0;
+  int nf = 0;
+  Fq r1 = fq_zero(), r2 = fq_zero();
+  int fmode = MODE_X;
+  std::vector<uint32_t> fstride;
+  const Fq* side_in = nullptr;
+  Fq* side_out = nullptr;
+  size_t side_live = 0;
+  const Fq *Ap = nullptr, *Aq = nullptr, *Ax = nullptr;
+  Fq *B = nullptr, *C = nullptr, *D = nullptr;
+};
+int phase1_pair(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp, Fq* partials, Fq* out15);
+int pair_wait(spg_ctx* ctx, Fq* out15);
+int phase1_fold2x(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp);
 // one phase-2 round: (e0, e2, e3) of eq(p) * ABC * Z  (src/sumcheck.rs:881-941)
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,

@@ -147,6 +147,8 @@ def test_r1cs_verify(ctx, r1cs_gens, case):
     ("p2_x1024_q64", {"SPG_SC_QUAD_MAX": "0", "SPG_P1_ROWS": "0"}),   # the per-point thread form throughout
     ("p8_x256_q32_shared", {"SPG_SC_QUAD_MAX": "0"}),                 # shared matrix, J = 2 at round 0
     ("p2_x256_2secs", {"SPG_SC_QUAD_MAX": "0", "SPG_SC_FUSE": "0"}),  # row form without the fused folds
+    ("p2_x1024_q64", {"SPG_P1_PAIR": "0"}),                           # phase 1 one round per launch throughout
+    ("p8_x256_q32_shared", {"SPG_P1_PAIR_MAX": "32"}),                # phase-1 pairs only for each mode's last rounds
 ])
 def test_r1cs_thread_form_rounds(oracle, case, env):
     """the thread-per-point phase-1 evaluations (k_phase1_eval, and k_phase1_eval_x's row-factored x rounds: one eq
