@@ -77,9 +77,9 @@ CONFIGS = {
 # per-launch HBM bytes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, scripts/pmc_traffic.py) of each workload's own
 # run: a kernel's traffic depends on its launch size, so one workload's figures are never reported for another
 TRAFFIC = {w: os.path.join(ROOT, "profiles", f) for w, f in (
-    ("snark", "r05_pmc_traffic.json"), ("msm16", "r05_pmc_traffic_msm_2e16.json"),
+    ("snark", "r06_pmc_traffic.json"), ("msm16", "r05_pmc_traffic_msm_2e16.json"),
     ("spark24", "r05_pmc_traffic_spark_2e24.json"), ("rows", "r05_pmc_traffic_rows_1024.json"),
-    ("r1cs22", "r05_pmc_traffic_r1cs_2e22.json"))}
+    ("r1cs22", "r06_pmc_traffic_r1cs_2e22.json"))}
 
 
 def parse():

@@ -536,6 +536,15 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   bool pre0 = false;
   uint32_t seq0 = 0;
   int per0 = 0;
+  // Cy = y.commit(blind_y, gens_1) depends on no challenge: it is computed beside Cx (in Cx's host burst, or on the
+  // pool while the device computes Cx) instead of in a burst of its own after it; the transcript still takes Cx first
+  // (SPG_DOTLOG_EARLY=0: Cy and beta in bursts of their own, in transcript order)
+  static const bool early = !getenv("SPG_DOTLOG_EARLY") || atoi(getenv("SPG_DOTLOG_EARLY")) != 0;
+  Pt Cy;
+  bool cy_done = false;
+  auto cy_job = [&]() -> HostJob {
+    return HostJob{{(size_t)g.gens_1.G[0], (size_t)g.gens_1.h}, {y, blind_y}};
+  };
   if (mbk && ahead) {
     // the Cx bucket sums, then Bullet round 0 (which needs no challenge), on the stream before the host waits
     // for Cx: one device round trip fewer per proof
@@ -564,6 +573,10 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     pre0 = true;
     h::HExt blind_h;
     if (cper) blind_h = g.host.sum_many({{{(size_t)H}, {blind_x}}})[0];  // while the device works
+    if (early) {
+      Cy = g.host.commit_many({cy_job()})[0];
+      cy_done = true;
+    }
     SPG_HIP(ctx, hipEventSynchronize(ctx->ev_cx));
     pts.resize(1);
     if (cper)
@@ -574,7 +587,11 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), x};
     j.first.push_back(kn.h);
     j.second.push_back(blind_x);
-    pts = g.host.commit_many({j});
+    pts = early ? g.host.commit_many({j, cy_job()}) : g.host.commit_many({j});
+    if (early) {
+      Cy = pts[1];
+      cy_done = true;
+    }
   } else {
     std::vector<Fq> hs(n2, fq_zero());
     std::copy(x.begin(), x.end(), hs.begin());
@@ -585,7 +602,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   Pt Cx = pts[0];
   t.point("Cx", Cx);
   g_msm_laps.lap("bp_cx");
-  Pt Cy = commit_batch(g, {CJob(g.gens_1, {y}, blind_y)})[0];
+  if (!cy_done) Cy = commit_batch(g, {CJob(g.gens_1, {y}, blind_y)})[0];
   g_msm_laps.lap("bp_cy");
   t.point("Cy", Cy);
   t.scalars("a", a);
@@ -603,6 +620,7 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
     ic[b * hn + n / 2 + 1] = H;
   }
   size_t nk = n, k = 0;
+  bool beta_done = false;
   g_msm_laps.lap("bullet_prep");
   if (mbk) {
     int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, gmax, mbk, d_mbk, &aa, &bb, &cw, &blind_fin, out,
@@ -638,7 +656,14 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
         jobs[b].first.assign(ic.begin() + b * hn, ic.begin() + (b + 1) * hn);
         jobs[b].second.assign(hc.begin() + b * hn, hc.begin() + (b + 1) * hn);
       }
+      // beta = (d r) G_1 + r_beta h needs r alone: it rides in round 0's burst (appended to the transcript at the end)
+      const bool with_beta = early && k == 0;
+      if (with_beta) jobs.push_back(HostJob{{(size_t)G1, (size_t)H}, {fq_mul(d, r), r_beta}});
       pts = g.host.commit_many(jobs);
+      if (with_beta) {
+        out->beta = pts[2];
+        beta_done = true;
+      }
     } else {
       int rc = device_msm_flat(ctx, g, hc, hn, 2, nullptr, &pts, &ic);
       if (rc) return rc;
@@ -692,7 +717,6 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   Fq x_hat = aa[0], a_hat = bb[0];
   Fq y_hat = fq_mul(x_hat, a_hat);
   // delta = d * g_hat + r_delta * h with g_hat = sum_j cw[j] G_j
-  bool beta_done = false;
   if (on_host) {
     HostJob j{std::vector<size_t>(kn.G.begin(), kn.G.begin() + n), FqV(n)};
     for (size_t i = 0; i < n; i++) j.second[i] = fq_mul(d, cw[i]);

@@ -91,6 +91,39 @@ __global__ void k_z_fill(const ZDesc* __restrict__ zd, int P, const SecDesc* __r
   Z[d.z_off + ((size_t)brev(q, d.lg_q) * nws + w) * d.ni + brev(i, d.lg_ni)] = v;
 }
 
+// The same fill when every instance has ni >= 256: one workgroup per 16 x 16 tile of a (q, w) row, i = a 2^(lg-4) +
+// m 16 + b (a, b < 16; m the tile). brev(i) = brev4(b) 2^(lg-4) + brev(m) 16 + brev4(a), so the tile's reads (b
+// contiguous for each a) and its writes (a contiguous for each b) are both 16 runs of 512 bytes; the tile turns
+// through LDS. The one-element form's stores land one 32-byte sector per line at bit-reversed positions.
+__global__ void __launch_bounds__(256) k_z_fill_tiled(const ZDesc* __restrict__ zd, int P,
+                                                      const SecDesc* __restrict__ sd, int nws, Fq* __restrict__ Z) {
+  __shared__ uint32_t sh[8][16 * 17];  // component-major, row pitch 17: conflict-free both ways
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256;
+  const int p = find_desc(zd, P, t0);
+  const ZDesc d = zd[p];
+  const uint64_t loc0 = t0 - d.dom_off;
+  const uint64_t rest = loc0 / d.ni;
+  const uint32_t m = (uint32_t)(loc0 % d.ni) >> 8;
+  const uint32_t w = (uint32_t)(rest % nws), q = (uint32_t)(rest / nws);
+  const SecDesc s = sd[(size_t)w * P + p];
+  const uint32_t k = threadIdx.x, sh_hi = d.lg_ni - 4;
+  {
+    const uint32_t a = k >> 4, b = k & 15;
+    const uint32_t i = (a << sh_hi) + (m << 4) + b;
+    Fq v = fq_zero();
+    if (i < s.ni) v = s.w[(size_t)(s.np == 1 ? 0 : q) * s.ni + i];
+#pragma unroll
+    for (int c = 0; c < 8; c++) sh[c][a * 17 + b] = v.l[c];
+  }
+  __syncthreads();
+  const uint32_t a = k & 15, b = k >> 4;
+  Fq v;
+#pragma unroll
+  for (int c = 0; c < 8; c++) v.l[c] = sh[c][a * 17 + b];
+  const uint32_t ri = (brev(b, 4) << sh_hi) + (brev(m, d.lg_ni - 8) << 4) + brev(a, 4);
+  Z[d.z_off + ((size_t)brev(q, d.lg_q) * nws + w) * d.ni + ri] = v;
+}
+
 struct SpDesc {
   uint64_t dom_off, out_off;
   uint32_t pi, lg_q, nrows, lg_rows, ni, lg_ni;
@@ -101,13 +134,17 @@ struct MatDesc {
 };
 
 // Az/Bz/Cz[p][q_rev][x_rev] = sum_e val_e * z[p][q][col_e / Y][col_e % Y], z gathered from the witness sections
-// themselves (the mapping k_z_fill applies), so the Z table's fill is off this kernel's path
+// themselves (the mapping k_z_fill applies), so the Z table's fill is off this kernel's path.
+// out_major: consecutive lanes take consecutive OUTPUT positions (row = brev(position)), so the three 32-byte
+// stores of a wave fill whole lines; the rows' CSR reads go scattered instead, but an instance's matrices are a few
+// KB to MB and stay in L2, where the bit-reversed stores (one 32-byte sector per line per lane) went to HBM
+// (SPG_SPMV_OUT_MAJOR=0: lanes by row)
 __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int P, const MatDesc* __restrict__ md,
                                               const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
                                               const Fq* __restrict__ val, const SecDesc* __restrict__ sec, int nws,
                                               uint32_t Y,
                                               Fq* __restrict__ Az, Fq* __restrict__ Bz, Fq* __restrict__ Cz,
-                                              uint64_t total) {
+                                              uint64_t total, int out_major) {
   // the section descriptors of the block's first instance (nws <= 8) sit in LDS: a nonzero's gather then waits on
   // an LDS read instead of a dependent global load; lanes of a later instance in the same block read them globally
   __shared__ SecDesc s_sec[8];
@@ -120,8 +157,9 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
   int p = find_desc(sd, P, t);
   const SpDesc d = sd[p];
   uint64_t loc = t - d.dom_off;
-  uint32_t row = (uint32_t)(loc % d.nrows), q = (uint32_t)(loc / d.nrows);
-  size_t o = d.out_off + (size_t)brev(q, d.lg_q) * d.nrows + brev(row, d.lg_rows);
+  const uint32_t pos = (uint32_t)(loc % d.nrows), q = (uint32_t)(loc / d.nrows);
+  const uint32_t row = out_major ? brev(pos, d.lg_rows) : pos;  // (nrows is a power of two: brev is a bijection)
+  size_t o = d.out_off + (size_t)brev(q, d.lg_q) * d.nrows + (out_major ? pos : brev(row, d.lg_rows));
   Fq* outs[3] = {Az, Bz, Cz};
 #pragma unroll
   for (int m = 0; m < 3; m++) {
@@ -638,9 +676,12 @@ int Prover::run_inner(Laps& lp) {
   Zp.anw.assign(PLn, nws);
   Zp.ani = l_inputs;
   size_t ztot = 0;
+  static const bool z_tiles_on = !getenv("SPG_Z_TILED") || atoi(getenv("SPG_Z_TILED")) != 0;
+  bool z_tiled = z_tiles_on;  // k_z_fill_tiled: every instance's row is whole 256-element tiles
   for (size_t p = 0; p < PLn; p++) {
     Zp.off[p] = ztot;
     ztot += l_proofs[p] * nws * l_inputs[p];
+    if (l_inputs[p] < 256) z_tiled = false;
   }
   Zp.total = ztot;
   Zp.num_instances = npow2(P);
@@ -749,8 +790,9 @@ int Prover::run_inner(Laps& lp) {
 
   {  // ---- Az, Bz, Cz: outputs, CSR row pointers, and per visited entry its column, value and z gather
     KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
+    static const int out_major = !getenv("SPG_SPMV_OUT_MAJOR") || atoi(getenv("SPG_SPMV_OUT_MAJOR")) != 0;
     hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr, inst.d_col,
-                       inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
+                       inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot, out_major);
     SPG_HIP(ctx, hipGetLastError());
   }
   // k_spmv gathers from the witness itself, so the Z fill only has to land before phase 2. On the second stream it
@@ -770,8 +812,12 @@ int Prover::run_inner(Laps& lp) {
     }
     {
       KScope ks(ctx, "z_fill", 64.0 * ztot);
-      hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec, (int)nws,
-                         Zp.d, (uint64_t)ztot);
+      if (z_tiled)  // (ztot is a multiple of 256 then, and so is every instance's offset)
+        hipLaunchKernelGGL(k_z_fill_tiled, dim3((uint32_t)(ztot / 256)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec,
+                           (int)nws, Zp.d);
+      else
+        hipLaunchKernelGGL(k_z_fill, dim3(blocks_for(ztot)), dim3(256), 0, ctx->stream, dz, (int)PLn, dsec, (int)nws,
+                           Zp.d, (uint64_t)ztot);
     }
     ctx->stream = main_stream;
     SPG_HIP(ctx, hipGetLastError());

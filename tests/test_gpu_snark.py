@@ -118,6 +118,8 @@ ROUND_FORMS = {
     "tree_one_launch": {"SPG_TREE_TOP": str(1 << 40)},
     "delta_bucket_msm": {"SPG_DELTA_COMB": "0"},
     "bullet_comb_rolled": {"SPG_BCOMB_ROLL": "1"},
+    "dotlog_cy_beta_in_order": {"SPG_DOTLOG_EARLY": "0"},
+    "spmv_lanes_by_row_z_one_element": {"SPG_SPMV_OUT_MAJOR": "0", "SPG_Z_TILED": "0"},
     "phase1_single_rounds": {"SPG_P1_PAIR": "0"},
     "phase1_pairs_small_only": {"SPG_P1_PAIR_MAX": "16"},
     "witness_upload_workers": {"SPG_H2D": "1"},
