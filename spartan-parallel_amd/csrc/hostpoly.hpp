@@ -48,6 +48,35 @@ inline int eq_tables(spg_ctx* ctx, std::initializer_list<EqOut> l) {
   return dev_eq_tables(ctx, j.data(), (int)j.size());
 }
 
+// dst += c src for every job (over min(|dst|, |src|) entries), on the host pool in index chunks: the random linear
+// combinations of PolyEvalProof's batched openings (dense_mlpoly.rs:531-1130, r1csproof.rs's witness opening). Jobs
+// into one dst run in job order within a chunk; the sums are exact field sums, so the vectors are the serial loop's.
+struct Axpy {
+  FqV* dst;
+  Fq c;
+  const FqV* src;
+};
+inline void axpy_pool(const std::vector<Axpy>& jobs) {
+  size_t work = 0, n = 0;
+  for (const Axpy& j : jobs) {
+    const size_t m = std::min(j.dst->size(), j.src->size());
+    work += m;
+    n = std::max(n, m);
+  }
+  // (1024 products are ~25 us on one core, a burst ~3; SPG_AXPY_POOL=0: always on the calling thread)
+  static const bool on = !getenv("SPG_AXPY_POOL") || atoi(getenv("SPG_AXPY_POOL")) != 0;
+  const int C = on && work >= 1024 ? 8 : 1;
+  pool().parallel_for(C, [&](int ch) {
+    const size_t lo = n * ch / C, hi = n * (ch + 1) / C;
+    for (const Axpy& j : jobs) {
+      FqV& d = *j.dst;
+      const FqV& s = *j.src;
+      const size_t e = std::min(hi, std::min(d.size(), s.size()));
+      for (size_t k = lo; k < e; k++) d[k] = fq_add(d[k], fq_mul(j.c, s[k]));
+    }
+  });
+}
+
 struct Laps {  // SPG_TRACE=1: wall-time breakdown of a host orchestration
   const char* title = "R1CSProof::prove";
   bool on = getenv("SPG_TRACE") != nullptr;

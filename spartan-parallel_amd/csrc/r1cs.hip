@@ -135,16 +135,18 @@ struct MatDesc {
 
 // Az/Bz/Cz[p][q_rev][x_rev] = sum_e val_e * z[p][q][col_e / Y][col_e % Y], z gathered from the witness sections
 // themselves (the mapping k_z_fill applies), so the Z table's fill is off this kernel's path.
-// out_major: consecutive lanes take consecutive OUTPUT positions (row = brev(position)), so the three 32-byte
-// stores of a wave fill whole lines; the rows' CSR reads go scattered instead, but an instance's matrices are a few
-// KB to MB and stay in L2, where the bit-reversed stores (one 32-byte sector per line per lane) went to HBM
-// (SPG_SPMV_OUT_MAJOR=0: lanes by row)
+// TILED (every instance has >= 256 rows): as k_z_fill_tiled, a workgroup takes a 16 x 16 tile of one q row, lanes read
+// 16 consecutive CSR rows each (row = a 2^(lg-4) + m 16 + b) and the three outputs turn through LDS so that the stores
+// are 16 runs of 512 bytes at the bit-reversed positions, instead of one 32-byte sector per line per lane. (Mapping the
+// lanes to consecutive output positions instead, row = brev(position), made the CSR reads scatter: 289 -> 341 us on
+// config 4.) SPG_SPMV_TILED=0: lanes by row, stores scattered.
+template <bool TILED>
 __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int P, const MatDesc* __restrict__ md,
                                               const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
                                               const Fq* __restrict__ val, const SecDesc* __restrict__ sec, int nws,
                                               uint32_t Y,
                                               Fq* __restrict__ Az, Fq* __restrict__ Bz, Fq* __restrict__ Cz,
-                                              uint64_t total, int out_major) {
+                                              uint64_t total) {
   // the section descriptors of the block's first instance (nws <= 8) sit in LDS: a nonzero's gather then waits on
   // an LDS read instead of a dependent global load; lanes of a later instance in the same block read them globally
   __shared__ SecDesc s_sec[8];
@@ -153,14 +155,13 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
   if ((int)threadIdx.x < nws) s_sec[threadIdx.x] = sec[(size_t)threadIdx.x * P + pb];
   __syncthreads();
   uint64_t t = t0 + threadIdx.x;
-  if (t >= total) return;
-  int p = find_desc(sd, P, t);
+  if (!TILED && t >= total) return;  // (tiled: total is whole tiles, every lane is live up to the LDS turn)
+  const int p = TILED ? pb : find_desc(sd, P, t);
   const SpDesc d = sd[p];
-  uint64_t loc = t - d.dom_off;
-  const uint32_t pos = (uint32_t)(loc % d.nrows), q = (uint32_t)(loc / d.nrows);
-  const uint32_t row = out_major ? brev(pos, d.lg_rows) : pos;  // (nrows is a power of two: brev is a bijection)
-  size_t o = d.out_off + (size_t)brev(q, d.lg_q) * d.nrows + (out_major ? pos : brev(row, d.lg_rows));
-  Fq* outs[3] = {Az, Bz, Cz};
+  const uint64_t loc = t - d.dom_off;
+  const uint32_t q = (uint32_t)(loc / d.nrows), k = threadIdx.x, mt = (uint32_t)(loc % d.nrows) >> 8;
+  const uint32_t row = TILED ? ((k >> 4) << (d.lg_rows - 4)) + (mt << 4) + (k & 15) : (uint32_t)(loc % d.nrows);
+  Fq sums[3];
 #pragma unroll
   for (int m = 0; m < 3; m++) {
     const uint32_t* rp = rowptr + md[d.pi].rp[m];
@@ -185,7 +186,29 @@ __global__ void __launch_bounds__(256) k_spmv(const SpDesc* __restrict__ sd, int
         if (i < xni) s = fq_add(s, fq_mul(val[e], xw[(size_t)(xnp == 1 ? 0 : q) * xni + i]));
       }
     }
-    outs[m][o] = s;
+    sums[m] = s;
+  }
+  Fq* outs[3] = {Az, Bz, Cz};
+  const size_t rowbase = d.out_off + (size_t)brev(q, d.lg_q) * d.nrows;
+  if (!TILED) {
+#pragma unroll
+    for (int m = 0; m < 3; m++) outs[m][rowbase + brev(row, d.lg_rows)] = sums[m];
+    return;
+  }
+  __shared__ uint32_t sh[3][8][16 * 17];  // component-major, row pitch 17: conflict-free both ways
+#pragma unroll
+  for (int m = 0; m < 3; m++)
+#pragma unroll
+    for (int c = 0; c < 8; c++) sh[m][c][(k >> 4) * 17 + (k & 15)] = sums[m].l[c];
+  __syncthreads();
+  const uint32_t a = k & 15, b = k >> 4;
+  const uint32_t ri = (brev(b, 4) << (d.lg_rows - 4)) + (brev(mt, d.lg_rows - 8) << 4) + brev(a, 4);
+#pragma unroll
+  for (int m = 0; m < 3; m++) {
+    Fq v;
+#pragma unroll
+    for (int c = 0; c < 8; c++) v.l[c] = sh[m][c][a * 17 + b];
+    outs[m][rowbase + ri] = v;
   }
 }
 
@@ -445,7 +468,8 @@ struct ZKRounds {
 // workspace slots used here (msm.hip uses 0..12, proto.hip 20..22)
 enum {
   WS_AZ = 30, WS_BZ, WS_CZ, WS_Z, WS_ABC, WS_TP, WS_TQ, WS_TX, WS_EQRX, WS_EQP, WS_PART, WS_OUT3, WS_DESC,
-  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2, WS_TQ2, WS_TX2, WS_ABC2
+  WS_L, WS_BPART, WS_BOUT, WS_EV_RX, WS_EV_RY, WS_EV_PART, WS_EV_OUT, WS_EV_DESC, WS_C1, WS_C2, WS_TQ2, WS_TX2, WS_ABC2,
+  WS_EQQ  // (56; spark.hip starts at 60)
 };
 // phase-1 rounds in modes x and q fold inside the next round's evaluation (sumcheck.hip, FOLD kernels); SPG_SC_FUSE=0
 // restores the separate fold launch
@@ -790,9 +814,16 @@ int Prover::run_inner(Laps& lp) {
 
   {  // ---- Az, Bz, Cz: outputs, CSR row pointers, and per visited entry its column, value and z gather
     KScope ks(ctx, "spmv_block", 96.0 * atot + 12.0 * atot + 68.0 * visits);
-    static const int out_major = !getenv("SPG_SPMV_OUT_MAJOR") || atoi(getenv("SPG_SPMV_OUT_MAJOR")) != 0;
-    hipLaunchKernelGGL(k_spmv, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr, inst.d_col,
-                       inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot, out_major);
+    static const bool tiles_on = !getenv("SPG_SPMV_TILED") || atoi(getenv("SPG_SPMV_TILED")) != 0;
+    bool tiled = tiles_on;  // every instance's q rows are whole 256-row tiles
+    for (size_t p = 0; p < PLn; p++)
+      if (l_cons[p] < 256) tiled = false;
+    if (tiled)
+      hipLaunchKernelGGL(k_spmv<true>, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr,
+                         inst.d_col, inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
+    else
+      hipLaunchKernelGGL(k_spmv<false>, dim3(blocks_for(atot)), dim3(256), 0, s, dsd, (int)PLn, dmd, inst.d_rowptr,
+                         inst.d_col, inst.d_val, dsec, (int)nws, (uint32_t)Y, Az.d, Bz, Cz, (uint64_t)atot);
     SPG_HIP(ctx, hipGetLastError());
   }
   // k_spmv gathers from the witness itself, so the Z fill only has to land before phase 2. On the second stream it
@@ -1207,9 +1238,20 @@ int Prover::run_inner(Laps& lp) {
   rc = queue_z_fill();  // (phase 1 had no rounds)
   if (!rc) rc = z_join.join();  // the Z table's first use
   if (rc) return rc;
-  for (size_t k = 0; k < rq_rev.size(); k++) {  // Z.bound_poly_vars_rq(rq_rev)
-    rc = pqx_bound(ctx, Zp, nullptr, nullptr, rq_rev[k], MODE_Q);
+  // Z.bound_poly_vars_rq(rq_rev): every q fold in one pass over Z against eq(rq_rev) (k_pqx_bound_q; SPG_Q_BOUND_ALL=0:
+  // one fold launch per challenge, each a read-write pass over the live rows)
+  static const bool q_all = !getenv("SPG_Q_BOUND_ALL") || atoi(getenv("SPG_Q_BOUND_ALL")) != 0;
+  if (q_all && rq_rev.size() >= 2) {
+    Fq* eq_q = (Fq*)ws_get(ctx, WS_EQQ, (sizeof(Fq) << rq_rev.size()) + 64);
+    if (!eq_q) return set_err(ctx, SPG_E_NOMEM, "eq(rq)");
+    rc = eq_table(ctx, rq_rev, eq_q);
+    if (!rc) rc = pqx_bound_q_all(ctx, Zp, eq_q, rq_rev.size());
     if (rc) return rc;
+  } else {
+    for (size_t k = 0; k < rq_rev.size(); k++) {
+      rc = pqx_bound(ctx, Zp, nullptr, nullptr, rq_rev[k], MODE_Q);
+      if (rc) return rc;
+    }
   }
   Fq* eq_p = (Fq*)ws_get(ctx, WS_EQP, (sizeof(Fq) << np) + 64);
   if (!eq_p) return set_err(ctx, SPG_E_NOMEM, "eq(rp)");
@@ -1386,8 +1428,9 @@ int Prover::run_inner(Laps& lp) {
       }
       o += Rs;
     }
-    // the host eq tables of the distinct right points (instances of one shape share theirs), on the pool
-    {
+    // the host eq tables of the distinct right points (instances of one shape share theirs), on the pool, while the
+    // device computes the LZ (queued first; d2h_fq below waits for them)
+    auto right_tables = [&]() {
       std::vector<size_t> uniq, at(polys.size());
       for (size_t k = 0; k < polys.size(); k++) {
         size_t u = 0;
@@ -1400,7 +1443,8 @@ int Prover::run_inner(Laps& lp) {
       std::vector<FqV> tabs(uniq.size());
       pool().parallel_for((int)uniq.size(), [&](int u) { tabs[u] = eq_evals_host(rr_of[uniq[u]]); });
       for (size_t k = 0; k < polys.size(); k++) polys[k].R = tabs[at[k]];
-    }
+    };
+    if (jobs.empty()) right_tables();
     if (!jobs.empty()) {
       Fq* dL = (Fq*)ws_get(ctx, WS_L, totL * sizeof(Fq) + 64);
       Fq* dpart = (Fq*)ws_get(ctx, WS_BPART, totP * sizeof(Fq) + 64);
@@ -1446,6 +1490,7 @@ int Prover::run_inner(Laps& lp) {
         hipLaunchKernelGGL(k_sum_cols_multi, dim3(nc), dim3(256), 0, s, bj, dpart, dout);
       }
       SPG_HIP(ctx, hipGetLastError());
+      right_tables();
       rc = d2h_fq(ctx, dout, lz_mine.data(), lz_total);
       if (rc) return rc;
     }
@@ -1501,14 +1546,20 @@ int Prover::run_inner(Laps& lp) {
     FqV Zc;
     Fq c_base = t.challenge("challenge_c");
     Fq c = fq_one();
-    for (auto& pr : polys) {
+    // the coefficients in the reference's order (c advances once per polynomial joining an earlier shape), then every
+    // LZ_list[idx] += c LZ over the pool (axpy_pool; config 4 adds 7 x 1024 products here, ~170 us on one thread)
+    std::vector<int> into(polys.size(), -1);
+    std::vector<Fq> coef(polys.size());
+    for (size_t q = 0; q < polys.size(); q++) {
+      const PolyRef& pr = polys[q];
       std::pair<size_t, size_t> key = {pr.np, pr.ni};
       size_t idx = keys.size();
       for (size_t k = 0; k < keys.size(); k++)
         if (keys[k] == key) { idx = k; break; }
       if (idx < keys.size()) {
         c = fq_mul(c, c_base);
-        for (size_t k = 0; k < pr.LZ.size(); k++) LZ_list[idx][k] = fq_add(LZ_list[idx][k], fq_mul(c, pr.LZ[k]));
+        into[q] = (int)idx;
+        coef[q] = c;
         Zc[idx] = fq_add(Zc[idx], fq_mul(c, pr.ev));
       } else {
         keys.push_back(key);
@@ -1517,6 +1568,10 @@ int Prover::run_inner(Laps& lp) {
         R_list.push_back(pr.R);
       }
     }
+    std::vector<Axpy> ax;  // (LZ_list no longer grows: its element addresses are stable)
+    for (size_t q = 0; q < polys.size(); q++)
+      if (into[q] >= 0) ax.push_back({&LZ_list[into[q]], coef[q], &polys[q].LZ});
+    axpy_pool(ax);
     for (size_t k = 0; k < LZ_list.size(); k++) {
       DotProductProofLogP dp;
       Pt cy;

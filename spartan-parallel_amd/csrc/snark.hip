@@ -223,8 +223,11 @@ int prove_batched_points(spg_ctx* ctx, ProverGens& g, const FqV& Z, const std::v
   std::vector<FqV> keys, Ls, Rs;
   FqV Zc;
   Fq c_base = t.challenge("challenge_c"), c = fq_one();
+  std::vector<FqV> Rv(r_list.size());
+  std::vector<std::pair<size_t, Fq>> acc(r_list.size(), {SIZE_MAX, fq_zero()});  // Rs[idx] += c R_i (axpy_pool)
   for (size_t i = 0; i < r_list.size(); i++) {
-    FqV L, R;
+    FqV L;
+    FqV& R = Rv[i];
     eq_factored(r_list[i], &L, &R);
     FqV key(r_list[i].begin(), r_list[i].begin() + ln);
     size_t idx = keys.size();
@@ -236,7 +239,7 @@ int prove_batched_points(spg_ctx* ctx, ProverGens& g, const FqV& Z, const std::v
       }
     if (idx < keys.size()) {
       c = fq_mul(c, c_base);
-      for (size_t j = 0; j < Rs[idx].size(); j++) Rs[idx][j] = fq_add(Rs[idx][j], fq_mul(c, R[j]));
+      acc[i] = {idx, c};
       Zc[idx] = fq_add(Zc[idx], fq_mul(c, Zr[i]));
     } else {
       keys.push_back(key);
@@ -244,6 +247,12 @@ int prove_batched_points(spg_ctx* ctx, ProverGens& g, const FqV& Z, const std::v
       Rs.push_back(R);
       Zc.push_back(Zr[i]);
     }
+  }
+  {
+    std::vector<Axpy> ax;
+    for (size_t i = 0; i < r_list.size(); i++)
+      if (acc[i].first != SIZE_MAX) ax.push_back({&Rs[acc[i].first], acc[i].second, &Rv[i]});
+    axpy_pool(ax);
   }
   w.u64(Ls.size());
   // every distinct point's L.Z bound up front, in one pool burst
@@ -282,6 +291,7 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
     bj.push_back({polys[i], &Lv[i]});
   }
   std::vector<FqV> LZall = host_bounds(bj);
+  std::vector<std::pair<size_t, Fq>> acc(polys.size(), {SIZE_MAX, fq_zero()});  // LZs[idx] += c LZ_i (axpy_pool)
   for (size_t i = 0; i < polys.size(); i++) {
     const size_t nv = lg2(polys[i]->size());
     const FqV& R = Rv[i];
@@ -295,7 +305,7 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
     FqV& LZ = LZall[i];
     if (idx < keys.size()) {
       c = fq_mul(c, c_base);
-      for (size_t j = 0; j < LZ.size(); j++) LZs[idx][j] = fq_add(LZs[idx][j], fq_mul(c, LZ[j]));
+      acc[i] = {idx, c};
       Zc[idx] = fq_add(Zc[idx], fq_mul(c, Zr[i]));
     } else {
       keys.push_back({nv, R});
@@ -303,6 +313,12 @@ int prove_batched_instances(spg_ctx* ctx, ProverGens& g, const std::vector<const
       LZs.push_back(LZ);
       Rs.push_back(R);
     }
+  }
+  {
+    std::vector<Axpy> ax;
+    for (size_t i = 0; i < polys.size(); i++)
+      if (acc[i].first != SIZE_MAX) ax.push_back({&LZs[acc[i].first], acc[i].second, &LZall[i]});
+    axpy_pool(ax);
   }
   w.u64(LZs.size());
   for (size_t i = 0; i < LZs.size(); i++) {
@@ -361,12 +377,13 @@ int prove_uni_batched(spg_ctx* ctx, ProverGens& g, const std::vector<const FqV*>
   Fq c_base = t.challenge("challenge_c"), c = fq_one();
   FqV LZc(R_size, fq_zero());
   Fq Zrc = fq_zero();
+  std::vector<Axpy> ax;
   for (size_t i = 0; i < polys.size(); i++) {
-    const FqV& LZ = LZs[i];
-    for (size_t k = 0; k < R_size && k < LZ.size(); k++) LZc[k] = fq_add(LZc[k], fq_mul(c, LZ[k]));
+    ax.push_back({&LZc, c, &LZs[i]});
     Zrc = fq_add(Zrc, fq_mul(c, Zr[i]));
     c = fq_mul(c, c_base);
   }
+  axpy_pool(ax);
   DotProductProofLogP p;
   Pt cy;
   int rc = dotproduct_log_prove(ctx, g, t, tape, LZc, fq_zero(), R, Zrc, fq_zero(), &p, &cy);

@@ -736,6 +736,43 @@ __global__ void k_pqx_fold2(PqxArgs a, uint32_t total_a, Fq* __restrict__ A, Pqx
   else if (t - total_a < total_b) pqx_fold_at(b, mode, t - total_a, r, B, nullptr, nullptr);
 }
 
+// Every q-mode fold of DensePolynomialPqx::bound_poly_vars_rq (custom_dense_mlpoly.rs, phase 2's Z prep; round j binds
+// the top live row bit of each instance with r_j, or scales a one-row instance by 1 - r_j) in one pass: an instance of
+// np = 2^k rows ends as out(w, x) = sum_s W(s) T[s][w][x] with W(s) = prod_{j < k} (bit k-1-j of s ? r_j : 1 - r_j)
+// prod_{j >= k} (1 - r_j) = E[s << (nq - k)], E = eq(r_0 .. r_{nq-1}) (most significant index bit <-> r_0). The same field
+// element as nq folds (exact arithmetic), one read of the table instead of nq read-write passes. Workgroup: 16 outputs
+// (consecutive x: 512-byte rows) x 16 row groups; the 16 partial sums of an output meet in LDS and the sum is written to
+// row 0 in place (only this workgroup reads that output's rows). Domain: per instance nw x cols outputs rounded up to 16.
+__global__ void __launch_bounds__(256) k_pqx_bound_q(PqxArgs a, const Fq* __restrict__ E, int nq, Fq* __restrict__ T) {
+  __shared__ uint32_t sh[8][256];
+  const uint32_t o0 = blockIdx.x * 16;
+  const int p = find_inst(a, o0);
+  const PqxInst& d = pinst(a, p);
+  const uint32_t lo = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const uint32_t o = o0 - d.dom_off + lo, cols = d.sc_ni, np = d.np;
+  const bool live = o < d.step_q * cols;
+  const uint32_t w = live ? o / cols : 0, x = live ? o % cols : 0;
+  int lgn = 0;
+  while ((1u << lgn) < np) lgn++;
+  const int se = nq - lgn;
+  const size_t base = pqx_off(d) + (size_t)w * d.ani + x, row = (size_t)d.anw * d.ani;
+  Fq acc = fq_zero();
+  if (live)
+    for (uint32_t s = g; s < np; s += 16) acc = fq_add(acc, fq_mul(E[(size_t)s << se], T[base + s * row]));
+#pragma unroll
+  for (int c = 0; c < 8; c++) sh[c][threadIdx.x] = acc.l[c];
+  __syncthreads();
+  if (g == 0 && live) {
+    for (int k = 1; k < 16; k++) {
+      Fq v;
+#pragma unroll
+      for (int c = 0; c < 8; c++) v.l[c] = sh[c][k * 16 + lo];
+      acc = fq_add(acc, v);
+    }
+    T[base] = acc;
+  }
+}
+
 // ---------------------------------------------------------------- plain cubic (product trees), A*B*C
 __global__ void __launch_bounds__(256) k_cubic_eval(const Fq* __restrict__ A, const Fq* __restrict__ B,
                                                     const Fq* __restrict__ C, uint32_t len, Fq* __restrict__ partials,
@@ -1417,6 +1454,37 @@ int pqx_bound2(spg_ctx* ctx, PqxDev& TA, PqxDev& TB, const Fq& r, int mode) {
     KScope ks(ctx, "sc_fold", 96.0 * (double)(da + db));
     hipLaunchKernelGGL(k_pqx_fold2, dim3((unsigned)((da + db + 255) / 256)), dim3(256), 0, ctx->stream, a,
                        (uint32_t)da, TA.d, b, (uint32_t)db, TB.d, mode, r);
+    SPG_HIP(ctx, hipGetLastError());
+  }
+  return 0;
+}
+
+int pqx_bound_q_all(spg_ctx* ctx, PqxDev& T, const Fq* E, size_t nq) {
+  PqxArgs a;
+  std::vector<PqxInst> v;
+  pqx_fill_args(T, a, v);  // the sizes before the folds
+  const size_t P = std::min(T.num_instances, T.zlen);
+  a.P = (int)P;
+  size_t dom = 0, reads = 0;
+  for (size_t p = 0; p < P; p++) {
+    PqxInst& d = v[p];
+    const size_t nw = std::min(T.num_witness_secs, T.anw[p]), cols = T.num_inputs[p];
+    if (T.num_proofs[p] > ((size_t)1 << nq) || nq > 31) return set_err(ctx, SPG_E_ARG, "q bound: rows exceed 2^nq");
+    d.dom_off = (uint32_t)dom;
+    d.sc_ni = (uint32_t)cols;
+    d.step_q = (uint32_t)nw;
+    dom += (nw * cols + 15) / 16 * 16;
+    reads += T.num_proofs[p] * nw * cols;
+  }
+  if (dom >= ((size_t)1 << 32)) return set_err(ctx, SPG_E_ARG, "q bound: domain");
+  // the bookkeeping of nq pqx_prepare(MODE_Q) calls: every local instance ends with one row
+  for (size_t j = 0; j < nq; j++) T.max_num_proofs /= 2;
+  for (size_t p = 0; p < P; p++) T.num_proofs[p] = 1;
+  int rc = pqx_pack(ctx, v, a, kWsPqxA);
+  if (rc) return rc;
+  if (dom) {
+    KScope ks(ctx, "sc_fold_q_all", 32.0 * (double)(reads + dom));
+    hipLaunchKernelGGL(k_pqx_bound_q, dim3((unsigned)(dom / 16)), dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
     SPG_HIP(ctx, hipGetLastError());
   }
   return 0;

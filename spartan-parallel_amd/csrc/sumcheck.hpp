@@ -109,6 +109,8 @@ int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_
 int pqx_bound(spg_ctx* ctx, PqxDev& T, Fq* d1, Fq* d2, const Fq& r, int mode, Fq* side = nullptr, size_t side_len = 0);
 // two single-table folds of different shapes with the same r in one launch
 int pqx_bound2(spg_ctx* ctx, PqxDev& TA, PqxDev& TB, const Fq& r, int mode);
+// nq q-mode folds (r_0 .. r_{nq-1}) of T in one launch (k_pqx_bound_q); E: eq(r_0 .. r_{nq-1}) on the device
+int pqx_bound_q_all(spg_ctx* ctx, PqxDev& T, const Fq* E, size_t nq);
 // SumcheckInstanceProof::prove_cubic round on dense A, B, C of length 2*len_half
 int cubic_eval(spg_ctx* ctx, const Fq* A, const Fq* B, const Fq* C, size_t len_half, Fq* partials,
                Fq* out3);

@@ -149,7 +149,8 @@ def test_r1cs_verify(ctx, r1cs_gens, case):
     ("p2_x256_2secs", {"SPG_SC_QUAD_MAX": "0", "SPG_SC_FUSE": "0"}),  # row form without the fused folds
     ("p2_x1024_q64", {"SPG_P1_PAIR": "0"}),                           # phase 1 one round per launch throughout
     ("p8_x256_q32_shared", {"SPG_P1_PAIR_MAX": "32"}),                # phase-1 pairs only for each mode's last rounds
-    ("p2_x1024_q64", {"SPG_Z_TILED": "0", "SPG_SPMV_OUT_MAJOR": "0"}),  # one-element Z fill, Az/Bz/Cz lanes by row
+    ("p2_x1024_q64", {"SPG_Z_TILED": "0", "SPG_SPMV_TILED": "0"}),  # one-element Z fill and Az/Bz/Cz stores
+    ("p40_ragged_2secs", {"SPG_Q_BOUND_ALL": "0"}),                   # phase 2's Z prep one q fold per challenge
 ])
 def test_r1cs_thread_form_rounds(oracle, case, env):
     """the thread-per-point phase-1 evaluations (k_phase1_eval, and k_phase1_eval_x's row-factored x rounds: one eq

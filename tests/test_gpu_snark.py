@@ -119,7 +119,9 @@ ROUND_FORMS = {
     "delta_bucket_msm": {"SPG_DELTA_COMB": "0"},
     "bullet_comb_rolled": {"SPG_BCOMB_ROLL": "1"},
     "dotlog_cy_beta_in_order": {"SPG_DOTLOG_EARLY": "0"},
-    "spmv_lanes_by_row_z_one_element": {"SPG_SPMV_OUT_MAJOR": "0", "SPG_Z_TILED": "0"},
+    "spmv_and_z_fill_untiled": {"SPG_SPMV_TILED": "0", "SPG_Z_TILED": "0"},
+    "q_folds_one_per_challenge": {"SPG_Q_BOUND_ALL": "0"},
+    "opening_combinations_on_calling_thread": {"SPG_AXPY_POOL": "0"},
     "phase1_single_rounds": {"SPG_P1_PAIR": "0"},
     "phase1_pairs_small_only": {"SPG_P1_PAIR_MAX": "16"},
     "witness_upload_workers": {"SPG_H2D": "1"},
