@@ -1471,6 +1471,17 @@ extern "C" int spg_snark_prove(spg_ctx* ctx, spg_snark_comp* block, spg_snark_co
                                const spg_snark_wit* W, spg_r1cs_gens* vars_gens, spg_transcript* transcript,
                                spg_random_tape* tape_h, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
   if (!ctx || !transcript) return SPG_E_ARG;
-  spg::HostPin pin;
-  return spg::tr_status(ctx, transcript->t, spg_snark_prove_impl(ctx, block, pairwise, perm_root, W, vars_gens, transcript, tape_h, proof, proof_cap, proof_len));
+  // SPG_TRACE: the whole call's wall time (the laps end at the io proofs; this adds the proof copy-out and the
+  // release of the prove's host state)
+  static const bool tr = getenv("SPG_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc;
+  {
+    spg::HostPin pin;
+    rc = spg::tr_status(ctx, transcript->t, spg_snark_prove_impl(ctx, block, pairwise, perm_root, W, vars_gens, transcript, tape_h, proof, proof_cap, proof_len));
+  }
+  if (tr)
+    fprintf(stderr, "[spg] spg_snark_prove call: %.0f us\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  return rc;
 }
