@@ -115,6 +115,15 @@ class Context:
             msg = lib().spg_last_error(self._h).decode(errors="replace")
             raise SpgError(f"{what}: {SPG_ERRORS.get(rc, rc)}: {msg}")
 
+    def out_buf(self, cap):
+        """the proof output buffer of this context's calls, kept between calls (a context runs one call at a time;
+        each wrapper copies its bytes out): a fresh 16 MB np.zeros per prove cost ~0.3 ms of mmap / munmap and page
+        faults beside the pool's spinning threads"""
+        b = getattr(self, "_out", None)
+        if b is None or b.shape[0] < cap:
+            b = self._out = np.empty(cap, dtype=np.uint8)
+        return b
+
     @property
     def handle(self):
         return self._h
@@ -571,7 +580,7 @@ class R1CSWitness:
 def r1cs_prove(ctx, gens, inst, witness, num_instances, max_num_proofs, num_proofs, max_num_inputs, num_inputs,
                transcript, tape, cap=1 << 22):
     """R1CSProof::prove -> (bincode bytes, [rp, rq_rev, rx, rw||ry] as (k, 4) uint64 arrays)."""
-    buf = np.zeros(cap, dtype=np.uint8)
+    buf = ctx.out_buf(cap)
     ln = ctypes.c_size_t(0)
     ch = np.zeros((4096, 4), dtype=np.uint64)
     chl = (ctypes.c_size_t * 4)()
@@ -671,7 +680,7 @@ class SparkCommitment:
         rx = _scalars(rx)
         ry = _scalars(ry)
         ev = _scalars(evals)
-        buf = np.zeros(cap, dtype=np.uint8)
+        buf = self.ctx.out_buf(cap)
         ln = ctypes.c_size_t(0)
         self.ctx.check(lib().spg_spark_prove(self.ctx.handle, self._h, _p(rx), ctypes.c_size_t(rx.shape[0]), _p(ry),
                                              ctypes.c_size_t(ry.shape[0]), _p(ev), ctypes.c_size_t(ev.shape[0]),
@@ -789,7 +798,7 @@ class SnarkWitness:
 
 def snark_prove(ctx, block, pairwise, perm_root, witness, vars_gens, transcript, tape, cap=1 << 24):
     """SNARK::prove (src/lib.rs:971-2746) -> bincode(SNARK)"""
-    buf = np.zeros(cap, dtype=np.uint8)
+    buf = ctx.out_buf(cap)
     ln = ctypes.c_size_t(0)
     ctx.check(lib().spg_snark_prove(ctx.handle, block.handle, pairwise.handle, perm_root.handle, witness.handle,
                                     vars_gens.handle, transcript.handle, tape.handle, _p(buf), ctypes.c_size_t(cap),
