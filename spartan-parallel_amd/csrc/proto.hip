@@ -289,60 +289,6 @@ static void parts_finals(const Ext* bk, size_t B, size_t per, Pt* out, const h::
   });
 }
 
-// parts_finals of a device round with the mailbox wait inside the burst (SPG_FINALS_WAIT, default on): the burst is
-// published as soon as the host has nothing left but to wait; task 0 waits for the post (mbox_wait: its stream checks
-// and timeout) and flips a flag, the chunk tasks spin on that flag and sum their parts the moment it flips. The workers
-// are running when the parts land instead of being handed a burst after the wait.
-static int parts_finals_wait(spg_ctx* ctx, uint32_t seq, const Ext* bk, size_t B, size_t per, Pt* out,
-                             const h::HExt* extra) {
-  const int threads = pool().size() + 1;
-  static const bool vec = h::ifma_on() && !(getenv("SPG_VEC_MIN") && atol(getenv("SPG_VEC_MIN")) == 0);
-  const size_t cmin = vec ? 48 : 8;
-  // (B K chunk tasks + the waiter fit the pool at once: every task spins until the flag flips)
-  const int K = (int)std::max<size_t>(1, std::min<size_t>(per / cmin, (size_t)std::max(1, threads - 1) / std::max<size_t>(B, 1)));
-  std::vector<h::HExt> part(B * K);
-  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[B]);
-  for (size_t b = 0; b < B; b++) left[b].store(K);
-  std::atomic<int> ready{0};
-  int rc = 0;
-  pool().parallel_for((int)(B * K) + 1, [&](int task) {
-    if (task == 0) {
-      rc = mbox_wait(ctx, seq, nullptr, 0);
-      ready.store(rc ? -1 : 1, std::memory_order_release);
-      return;
-    }
-    int f;
-    while ((f = ready.load(std::memory_order_acquire)) == 0) {
-#if defined(__x86_64__)
-      __builtin_ia32_pause();
-#endif
-    }
-    if (f < 0) return;
-    const size_t b = (size_t)(task - 1) / K, c = (size_t)(task - 1) % K;
-    const size_t lo = per * c / K, hi = per * (c + 1) / K;
-    for (const uint8_t* q = (const uint8_t*)(bk + b * per + lo); q < (const uint8_t*)(bk + b * per + hi); q += 64)
-      __builtin_prefetch(q, 0, 0);
-    h::HExt acc;
-    if (vec && hi - lo >= 16) {
-      thread_local std::vector<h::HExt> hx;
-      hx.resize(hi - lo);
-      for (size_t i = lo; i < hi; i++) hx[i - lo] = h::hext_from_dev(bk[b * per + i]);
-      acc = h::ext_sum8(hx.data(), hi - lo);
-    } else {
-      acc = h::hext_from_dev(bk[b * per + lo]);
-      for (size_t i = lo + 1; i < hi; i++) acc = h::hext_add(acc, h::hext_from_dev(bk[b * per + i]));
-    }
-    part[task - 1] = acc;
-    if (left[b].fetch_sub(1, std::memory_order_acq_rel) == 1) {
-      h::HExt sum = part[b * K];
-      for (int k = 1; k < K; k++) sum = h::hext_add(sum, part[b * K + k]);
-      if (extra) sum = h::hext_add(sum, extra[b]);
-      out[b] = compress(sum);
-    }
-  });
-  return rc;
-}
-
 // B fixed-base MSMs of n host scalars each over generator indices already on the device (d_idx: B x n)
 // h_idx (optional, host, B x n): generator indices uploaded with the scalars in the same copy, d_idx unused
 static int device_msm_flat(spg_ctx* ctx, ProverGens& g, const std::vector<Fq>& hs, size_t n, size_t B,
@@ -499,21 +445,14 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
     const Fq blind_L = v1[k], blind_R = v2[k];
     std::vector<h::HExt> ex = g.host.sum_many({{{G1, H}, {fq_mul(cL, r), blind_L}}, {{G1, H}, {fq_mul(cR, r), blind_R}}});
     g_msm_laps.lap("bullet_host_overlap");
-    static const bool finals_wait = !getenv("SPG_FINALS_WAIT") || atoi(getenv("SPG_FINALS_WAIT")) != 0;
+    rc = mbox_wait(ctx, seq, nullptr, 0);
+    if (rc) return rc;
+    g_msm_laps.lap("msm_device");
     Pt LR[2];
-    if (per && finals_wait) {
-      rc = parts_finals_wait(ctx, seq, mbk, 2, (size_t)per, LR, ex.data());
-      if (rc) return rc;
-      g_msm_laps.lap("msm_device");
-    } else {
-      rc = mbox_wait(ctx, seq, nullptr, 0);
-      if (rc) return rc;
-      g_msm_laps.lap("msm_device");
-      if (per)
-        parts_finals(mbk, 2, (size_t)per, LR, ex.data());
-      else
-        bucket_finals(mbk, 2, kBulletNB, LR, ex.data(), true);
-    }
+    if (per)
+      parts_finals(mbk, 2, (size_t)per, LR, ex.data());
+    else
+      bucket_finals(mbk, 2, kBulletNB, LR, ex.data(), true);
     g_msm_laps.lap("msm_host_final");
     t.point("L", LR[0]);
     t.point("R", LR[1]);
