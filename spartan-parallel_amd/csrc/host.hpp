@@ -274,8 +274,13 @@ struct HostGens {
     // >= 64 units per slice: with the IFMA sums a slice's run is cheap, and fewer slices mean less burst hand-off
     // (2-rep A/B, SNARK median ms: 8: 16.91 / 16.80, 32: 16.79 / 16.26, 64: 16.32 / 16.38)
     static const size_t min_slice = getenv("SPG_SLICE_MIN") ? (size_t)atol(getenv("SPG_SLICE_MIN")) : 64;
-    const size_t S = std::max<size_t>(1, std::min(threads, U / min_slice));
-    auto slice_lo = [&](size_t s) { return U * s / S; };
+    // several small jobs (a DotProductProof's Cy and beta: 96 units) get a slice each, so their encodings (~2.4 us
+    // inverse square roots) run side by side instead of one after another on the calling thread (SPG_ENC_SPLIT=0: off)
+    static const bool enc_split = !getenv("SPG_ENC_SPLIT") || atoi(getenv("SPG_ENC_SPLIT")) != 0;
+    size_t S = std::max<size_t>(1, std::min(threads, U / min_slice));
+    const bool per_job = enc_split && J > S && J <= threads;
+    if (per_job) S = J;  // slice s = job s
+    auto slice_lo = [&](size_t s) { return per_job ? 32 * tfirst[s] : U * s / S; };
     // slices touching job j: [sfirst[j], slast[j]]
     std::vector<size_t> sfirst(J), slast(J);
     std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[J]);

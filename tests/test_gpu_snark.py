@@ -122,6 +122,7 @@ ROUND_FORMS = {
     "spmv_and_z_fill_untiled": {"SPG_SPMV_TILED": "0", "SPG_Z_TILED": "0"},
     "q_folds_one_per_challenge": {"SPG_Q_BOUND_ALL": "0"},
     "opening_combinations_on_calling_thread": {"SPG_AXPY_POOL": "0"},
+    "small_commit_jobs_one_slice": {"SPG_ENC_SPLIT": "0"},
     "phase1_single_rounds": {"SPG_P1_PAIR": "0"},
     "phase1_pairs_small_only": {"SPG_P1_PAIR_MAX": "16"},
     "witness_upload_workers": {"SPG_H2D": "1"},
