@@ -473,6 +473,31 @@ enum {
 };
 // phase-1 rounds in modes x and q fold inside the next round's evaluation (sumcheck.hip, FOLD kernels); SPG_SC_FUSE=0
 // restores the separate fold launch
+// the cubic Lagrange basis on the nodes 0..3 at r (a pair's round j + 1 from its grid at t = r_j)
+static void lagrange4(const Fq& r, Fq L[4]) {
+  static const Fq inv2 = fq_inv(fq_from_u64(2)), inv6 = fq_inv(fq_from_u64(6));
+  const Fq a0 = r, a1 = fq_sub(r, fq_one()), a2 = fq_sub(a1, fq_one()), a3 = fq_sub(a2, fq_one());
+  const Fq a01 = fq_mul(a0, a1), a23 = fq_mul(a2, a3);
+  L[0] = fq_neg(fq_mul(fq_mul(a1, a23), inv6));
+  L[1] = fq_mul(fq_mul(a0, a23), inv2);
+  L[2] = fq_neg(fq_mul(fq_mul(a01, a3), inv2));
+  L[3] = fq_mul(fq_mul(a01, a2), inv6);
+}
+// a pair's posted grid (k_phase1_pair / k_phase2_pair) -> round j's (e0, e2, e3) and, once r_j is drawn, round j + 1's
+static void pair_round_j(const Fq ev[15], Fq ej[3]) {
+  ej[0] = fq_add(ev[0], ev[12]);
+  ej[1] = fq_add(ev[2], ev[13]);
+  ej[2] = fq_add(ev[3], ev[14]);
+}
+static void pair_round_j1(const Fq ev[15], const Fq& r_j, Fq ej1[3]) {
+  Fq L[4];
+  lagrange4(r_j, L);
+  for (int y = 0; y < 3; y++) {
+    Fq acc = fq_zero();
+    for (int k = 0; k < 4; k++) acc = fq_add(acc, fq_mul(L[k], ev[4 * y + k]));
+    ej1[y] = acc;
+  }
+}
 static bool sc_fuse_on() {
   static const bool on = !getenv("SPG_SC_FUSE") || atoi(getenv("SPG_SC_FUSE")) != 0;
   return on;
@@ -1031,15 +1056,6 @@ int Prover::run_inner(Laps& lp) {
       lenE /= 4;
       return phase1_fold2x(ctx, *T, pp);
     };
-    auto lagrange4 = [](const Fq& r, Fq L[4]) {  // the cubic Lagrange basis on 0..3 at r
-      static const Fq inv2 = fq_inv(fq_from_u64(2)), inv6 = fq_inv(fq_from_u64(6));
-      const Fq a0 = r, a1 = fq_sub(r, fq_one()), a2 = fq_sub(a1, fq_one()), a3 = fq_sub(a2, fq_one());
-      const Fq a01 = fq_mul(a0, a1), a23 = fq_mul(a2, a3);
-      L[0] = fq_neg(fq_mul(fq_mul(a1, a23), inv6));
-      L[1] = fq_mul(fq_mul(a0, a23), inv2);
-      L[2] = fq_neg(fq_mul(fq_mul(a01, a3), inv2));
-      L[3] = fq_mul(fq_mul(a01, a2), inv6);
-    };
     if (rounds && nx + nq == 0) rc = to_compact();
     bool cur_pair = false;  // the launch in flight evaluates rounds j, j + 1
     if (!rc && rounds) {
@@ -1058,19 +1074,13 @@ int Prover::run_inner(Laps& lp) {
         if (rc) return rc;
         lp.lap("p1_eval");
         // round j: F(X, 0) + F(X, 1) at X = 0, 2, 3
-        const Fq ej[3] = {fq_add(ev[0], ev[12]), fq_add(ev[2], ev[13]), fq_add(ev[3], ev[14])};
+        Fq ej[3], ej1[3];
+        pair_round_j(ev, ej);
         const Fq r_j = zk.begin(g, t, j, ej);
         zk.finish(g, t, tape, j, r_j);
         rx_all.push_back(r_j);
         // round j + 1: the cubics t -> F(t, Y) (Y = 0, 2, 3) at t = r_j
-        Fq L[4];
-        lagrange4(r_j, L);
-        Fq ej1[3];
-        for (int y = 0; y < 3; y++) {
-          Fq acc = fq_zero();
-          for (int k = 0; k < 4; k++) acc = fq_add(acc, fq_mul(L[k], ev[4 * y + k]));
-          ej1[y] = acc;
-        }
+        pair_round_j1(ev, r_j, ej1);
         const Fq r_j1 = zk.begin(g, t, j + 1, ej1);
         lp.lap("p1_host");
         // the next launch: another pair of this mode (the two folds ride in it), else the folds on their own launch
@@ -1314,11 +1324,94 @@ int Prover::run_inner(Laps& lp) {
       TA = &ABCc;
       return 0;
     };
+    // ---- two y rounds per launch (sumcheck.hip k_phase2_pair; SPG_P2_PAIR=0: one per launch): rounds j, j + 1 both y
+    // rounds, ABC per instance, every instance's live y size >= 4 (the same in ABC and Z), at most SPG_P2_PAIR_MAX
+    // (default 8192) elements, unsharded. A run of pairs starts with no fold pending (a single round's fold before it is
+    // launched on its own) and ends with k_phase2_fold2x.
+    static const bool p2_pair_on = !getenv("SPG_P2_PAIR") || atoi(getenv("SPG_P2_PAIR")) != 0;
+    static const size_t p2_pair_max = std::min<size_t>(
+        kP1PairMax, getenv("SPG_P2_PAIR_MAX") ? (size_t)atol(getenv("SPG_P2_PAIR_MAX")) : (size_t)8192);
+    const size_t W2 = std::min(ws_len, nws);
+    // (fold_pending: round j - 1's fold is not yet in the tables' sizes; the caller launches it first)
+    auto p2_pair_ok = [&](size_t j, bool fold_pending) -> bool {
+      if (!p2_pair_on || single || nranks != 1 || j + 1 >= ny || TA != &ABC || TZ != &Zp || ABC.zlen != Zp.zlen)
+        return false;
+      auto live = [&](size_t n) { return fold_pending && n > 1 ? n / 2 : n; };
+      size_t dom = 0;
+      for (size_t p = 0; p < sc_ni.size(); p++) {
+        const size_t N = live(Zp.num_inputs[p]);
+        if (N < 4 || live(ABC.num_inputs[p]) != N || sc_ni[p] != N) return false;
+        dom += W2 * (N / 4);
+      }
+      return dom > 0 && dom <= p2_pair_max;
+    };
+    // rounds j, j + 1 in one launch; nf = 2: the previous pair's folds (r1, r2) ride in it
+    auto launch_p2pair = [&](int nf, const Fq& r1, const Fq& r2) -> int {
+      for (int k = 0; k < 2; k++) {  // launch_eval's size bookkeeping for both y rounds
+        if (inputs_len > 1) inputs_len /= 2;
+        for (size_t p = 0; p < sc_ni.size(); p++)
+          if (sc_ni[p] > 1) sc_ni[p] /= 2;
+      }
+      P2Pair pp;
+      pp.nf = nf;
+      pp.r1 = r1;
+      pp.r2 = r2;
+      pp.W = W2;
+      pp.eq = eq_l;
+      int r = phase2_pair(ctx, ABC, Zp, pp, partials);
+      if (r) return r;
+      FoldPlan tmp;  // the table bookkeeping of both rounds' folds (the folds ride in the next launch)
+      for (int k = 0; k < 2 && !r; k++) {
+        r = pqx_fold_plan(ctx, ABC, MODE_X, &tmp);
+        if (!r) r = pqx_fold_plan(ctx, Zp, MODE_X, &tmp);
+      }
+      return r;
+    };
+    auto p2_fold2x = [&](const Fq& r1, const Fq& r2) -> int {
+      P2Pair pp;
+      pp.nf = 2;
+      pp.r1 = r1;
+      pp.r2 = r2;
+      pp.W = W2;
+      return phase2_fold2x(ctx, ABC, Zp, pp);
+    };
+    bool cur_pair = false;  // the launch in flight evaluates rounds j, j + 1
     if (rounds && ny + nw == 0) rc = to_compact();
-    if (!rc && rounds) rc = launch_eval(0, nullptr);
+    if (!rc && rounds) {
+      cur_pair = p2_pair_ok(0, false);
+      rc = cur_pair ? launch_p2pair(0, fq_zero(), fq_zero()) : launch_eval(0, nullptr);
+    }
     if (rc) return rc;
     zk.init(g, tape, rounds, claim2, blind2);  // host precomputation while round 0 evaluates
-    for (size_t j = 0; j < rounds; j++) {
+    for (size_t j = 0; j < rounds;) {
+      if (cur_pair) {
+        Fq ev[15], ej[3], ej1[3];
+        rc = pair_wait(ctx, ev);
+        if (rc) return rc;
+        lp.lap("p2_eval");
+        pair_round_j(ev, ej);
+        const Fq r_j = zk.begin(g, t, j, ej);
+        zk.finish(g, t, tape, j, r_j);
+        ry_all.push_back(r_j);
+        pair_round_j1(ev, r_j, ej1);
+        const Fq r_j1 = zk.begin(g, t, j + 1, ej1);
+        lp.lap("p2_host");
+        if (j + 2 < ny && p2_pair_ok(j + 2, false)) {
+          rc = launch_p2pair(2, r_j, r_j1);
+        } else {
+          cur_pair = false;
+          rc = p2_fold2x(r_j, r_j1);
+          if (!rc && j + 2 == ny + nw && np > 0) rc = to_compact();
+          if (!rc && j + 2 < rounds) rc = launch_eval(j + 2, nullptr);
+        }
+        if (rc) return rc;
+        lp.lap("p2_fold");
+        zk.finish(g, t, tape, j + 1, r_j1);
+        lp.lap("p2_host");
+        ry_all.push_back(r_j1);
+        j += 2;
+        continue;
+      }
       int mode = j < ny ? MODE_X : (j < ny + nw ? MODE_W : MODE_P);
       Fq e[3];
       rc = eval_wait(ctx, e);
@@ -1329,7 +1422,12 @@ int Prover::run_inner(Laps& lp) {
       lp.lap("p2_host");
       const bool compact_next = j + 1 == ny + nw && np > 0;
       const int next_mode = j + 1 < ny ? MODE_X : (j + 1 < ny + nw ? MODE_W : MODE_P);
-      if (fuse2 && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
+      if (mode == MODE_X && p2_pair_ok(j + 1, true)) {
+        // a run of pairs starts here: this round's fold on its own launch, then the pair (no fold pending in it)
+        rc = pqx_bound2(ctx, *TA, *TZ, r_j, mode);
+        if (!rc) rc = launch_p2pair(0, fq_zero(), fq_zero());
+        cur_pair = true;
+      } else if (fuse2 && mode != MODE_P && j + 1 < rounds && !compact_next && next_mode != MODE_P) {
         // the fold rides in the next round's evaluation (k_phase2_eval<true>)
         Fold2 f;
         rc = pqx_fold_plan(ctx, *TA, mode, &f.a);
@@ -1353,6 +1451,7 @@ int Prover::run_inner(Laps& lp) {
       zk.finish(g, t, tape, j, r_j);
       lp.lap("p2_host");
       ry_all.push_back(r_j);
+      j++;
     }
     rc = d2h_multi(ctx, {{eq_p, 1}, {TA->d, 1}, {TZ->d, 1}}, claims2);
     if (rc) return rc;

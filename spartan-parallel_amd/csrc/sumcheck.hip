@@ -962,6 +962,106 @@ __global__ void __launch_bounds__(256) k_phase1_fold2x(P1PairArgs A) {
   }
 }
 
+// ---- phase 2, two y rounds per launch (round 6; SPG_P2_PAIR=0 keeps one round per launch) ------------------------------
+// The phase-1 pair argument on phase 2's y rounds (src/sumcheck.rs:881-941): the summand eq(p) ABC(p, w, y) Z(p, w, y)
+// has eq(p) constant over the y rounds and ABC, Z multilinear in round j's and round j + 1's variables, so the launch
+// posts F = eq ABC Z on the same 15 points of the 4 x 4 grid and the host interpolates round j + 1 at r_j. Element =
+// (instance p, section row w < W, y' < N/4), N = the instance's live y size (the same in ABC and Z); corners at
+// y' + {0, N/4, N/2, 3N/4}. ABC is per instance here (a shared ABC is read by every instance and folded by one: those
+// proofs keep single rounds). nf = 2: the previous pair's two folds, bilinear over T[k + {0, 1, 2, 3} N], written
+// back in place. Lanes as k_phase1_pair with its D factor zero and its A factor the constant eq(p).
+struct P2PairArgs {
+  PqxArgs ab, zz;  // zz: dom_off (element offset), sc_ni (N/4 elements per row); ni: N
+  uint32_t total;
+  int nf;
+  Fq r1, r2, r12;
+  const Fq* eq;
+  Fq* B;  // ABC
+  Fq* C;  // Z
+  Fq* partials;
+  unsigned* counter;
+  uint32_t* mb;
+  uint32_t seq;
+};
+static_assert(sizeof(P2PairArgs) <= 4096, "phase-2 pair arguments exceed the kernel-argument budget");
+template <int BS>
+__global__ void __launch_bounds__(BS) k_phase2_pair(P2PairArgs A) {
+  __shared__ bool last;
+  const int t = threadIdx.x, g = t & 15;
+  const uint32_t u = (blockIdx.x * BS + t) >> 4;
+  const int pt = g < 4 ? g : (g < 8 ? g - 4 : (g < 12 ? g - 8 : (g == 12 ? 0 : (g == 13 ? 2 : 3))));
+  const int ps = g < 4 ? 0 : (g < 8 ? 2 : (g < 12 ? 3 : 1));
+  Fq e = fq_zero();
+  if (u < A.total) {
+    const int p = find_inst(A.zz, u);
+    const PqxInst& dz = pinst(A.zz, p);
+    const uint32_t loc = u - dz.dom_off, w = loc / dz.sc_ni, y = loc % dz.sc_ni, N = dz.ni;
+    const int m = g & 3;  // corner: 0 (0, 0), 1 (0, s), 2 (t, 0), 3 (t, s)
+    Fq v = fq_zero();
+    if (g < 8) {
+      const PqxInst& d = g < 4 ? pinst(A.ab, p) : dz;
+      Fq* T = g < 4 ? A.B : A.C;
+      const size_t k = pqx_off(d) + (size_t)w * d.ani + y + (m & 1 ? N / 4 : 0) + (m & 2 ? N / 2 : 0);
+      if (A.nf == 0) {
+        v = T[k];
+      } else {
+        v = bilerp(T[k], T[k + N], T[k + 2 * (size_t)N], T[k + 3 * (size_t)N], A.r1, A.r2, A.r12);
+        T[k] = v;
+      }
+    } else if (g >= 12) {
+      v = A.eq[p];
+    }
+    const Fq b00 = fq_rowbcast<0>(v), b01 = fq_rowbcast<1>(v), b10 = fq_rowbcast<2>(v), b11 = fq_rowbcast<3>(v);
+    const Fq c00 = fq_rowbcast<4>(v), c01 = fq_rowbcast<5>(v), c10 = fq_rowbcast<6>(v), c11 = fq_rowbcast<7>(v);
+    const Fq a = fq_rowbcast<12>(v);
+    const Fq bv = cube_at(b00, b01, b10, b11, pt, ps), cv = cube_at(c00, c01, c10, c11, pt, ps);
+    e = g < 15 ? fq_mul(a, fq_mul(bv, cv)) : fq_zero();
+  }
+  row_block_sum<BS>(e);
+  if (gridDim.x == 1) {  // lanes 0..14 of wave 0 post the 15 point sums, then lane 0 the sequence number
+    if (t < 15) {
+      host_put(A.mb + 8 + 8 * t, e);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  if (t < 16) st_sc1(&A.partials[16 * blockIdx.x + t], e);
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(A.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  Fq sum = fq_zero();
+  for (unsigned j = t >> 4; j < gridDim.x; j += BS / 16) sum = fq_add(sum, ld_sc1(&A.partials[16 * j + g]));
+  row_block_sum<BS>(sum);
+  if (t < 15) {
+    host_put(A.mb + 8 + 8 * t, sum);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(A.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(A.mb, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+// the last pair's two folds of ABC and Z (every live entry, in place: T[k] from T[k + {0, 1, 2, 3} N], N the live size
+// after both folds)
+__global__ void __launch_bounds__(256) k_phase2_fold2x(P2PairArgs A) {
+  for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < A.total; u += gridDim.x * 256) {
+    const int p = find_inst(A.zz, u);
+    const PqxInst& dz = pinst(A.zz, p);
+    const PqxInst& da = pinst(A.ab, p);
+    const uint32_t loc = u - dz.dom_off, w = loc / dz.sc_ni, y = loc % dz.sc_ni;
+    const size_t N = dz.ni;
+    const size_t ka = pqx_off(da) + (size_t)w * da.ani + y, kz = pqx_off(dz) + (size_t)w * dz.ani + y;
+    A.B[ka] = bilerp(A.B[ka], A.B[ka + N], A.B[ka + 2 * N], A.B[ka + 3 * N], A.r1, A.r2, A.r12);
+    A.C[kz] = bilerp(A.C[kz], A.C[kz + N], A.C[kz + 2 * N], A.C[kz + 3 * N], A.r1, A.r2, A.r12);
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 // round evaluations over at most this many domain points take the quad form (SPG_SC_QUAD_MAX; 0 = never): below it
 // the chip is not full and a point's chain of products sets the time
@@ -1289,6 +1389,74 @@ int phase1_fold2x(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp) {
   {
     KScope ks(ctx, "sc_fold", 32.0 * 5.0 * (3.0 * (double)dom + (double)pp.side_live));
     hipLaunchKernelGGL(k_phase1_fold2x, dim3((unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 4096))),
+                       dim3(256), 0, ctx->stream, A);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+// the descriptors of a phase-2 pair launch (els: elements per w row, N / 4 for a pair, N for its folds)
+static int p2_args(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair& pp, bool fold, P2PairArgs& A,
+                   size_t* dom_out) {
+  std::vector<PqxInst> va, vz;
+  pqx_fill_args(AB, A.ab, va);
+  pqx_fill_args(Z, A.zz, vz);
+  const size_t P = std::min(Z.num_instances, Z.zlen);
+  if (AB.zlen != Z.zlen || P == 0) return set_err(ctx, SPG_E_ARG, "phase-2 pair: ABC is not per instance");
+  A.ab.P = (int)P;
+  A.zz.P = (int)P;
+  size_t dom = 0;
+  for (size_t p = 0; p < P; p++) {
+    const uint32_t N = vz[p].ni;
+    if (va[p].ni != N || N < (fold ? 1u : 4u) || (N & (N - 1)) || pp.W > vz[p].anw || pp.W > va[p].anw)
+      return set_err(ctx, SPG_E_ARG, "phase-2 pair: sizes");
+    vz[p].dom_off = (uint32_t)dom;
+    vz[p].sc_ni = fold ? N : N / 4;
+    dom += pp.W * vz[p].sc_ni;
+  }
+  if (dom == 0 || dom > (fold ? (size_t)0xffffffffULL : (size_t)kP1PairMax))
+    return set_err(ctx, SPG_E_ARG, "phase-2 pair: domain size");
+  if (int rc = pqx_pack(ctx, va, A.ab, kWsPqxA)) return rc;
+  if (int rc = pqx_pack(ctx, vz, A.zz, kWsPqxB)) return rc;
+  A.total = (uint32_t)dom;
+  A.nf = fold ? 2 : pp.nf;
+  A.r1 = pp.r1;
+  A.r2 = pp.r2;
+  A.r12 = fq_mul(pp.r1, pp.r2);
+  A.eq = pp.eq;
+  A.B = AB.d;
+  A.C = Z.d;
+  *dom_out = dom;
+  return 0;
+}
+
+int phase2_pair(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair& pp, Fq* partials) {
+  P2PairArgs A;
+  size_t dom = 0;
+  if (int rc = p2_args(ctx, AB, Z, pp, false, A, &dom)) return rc;
+  A.partials = partials;
+  A.counter = ctx->d_counter;
+  A.mb = ctx->d_mbox;
+  A.seq = ++ctx->mbox_seq;
+  const unsigned nb = (unsigned)((16 * dom + 255) / 256);
+  {
+    // per element: 2 tables x 4 corners (4 entries read + 1 written with the pending folds); Fq products: the folds
+    // (3 per corner), 15 points x 2
+    KScope ks(ctx, "sc_phase2_pair", 32.0 * 8.0 * (pp.nf == 2 ? 5.0 : 1.0) * (double)dom, 0.0,
+              (double)dom * (30.0 + 8.0 * (pp.nf == 2 ? 3.0 : 0.0)));
+    hipLaunchKernelGGL(k_phase2_pair<256>, dim3(nb), dim3(256), 0, ctx->stream, A);
+  }
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
+int phase2_fold2x(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair& pp) {
+  P2PairArgs A;
+  size_t dom = 0;
+  if (int rc = p2_args(ctx, AB, Z, pp, true, A, &dom)) return rc;
+  {
+    KScope ks(ctx, "sc_fold", 32.0 * 5.0 * 2.0 * (double)dom);
+    hipLaunchKernelGGL(k_phase2_fold2x, dim3((unsigned)std::max<size_t>(1, std::min<size_t>((dom + 255) / 256, 4096))),
                        dim3(256), 0, ctx->stream, A);
   }
   SPG_HIP(ctx, hipGetLastError());

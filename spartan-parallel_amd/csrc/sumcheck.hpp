@@ -99,6 +99,18 @@ struct P1Pair {
 int phase1_pair(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp, Fq* partials, Fq* out15);
 int pair_wait(spg_ctx* ctx, Fq* out15);
 int phase1_fold2x(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp);
+// two phase-2 y rounds in one launch (k_phase2_pair): eq(p) ABC Z on the 4 x 4 grid of rounds j, j + 1, with ABC
+// per instance (not shared) and every instance's live y size >= 4 in both tables; nf = 2: the previous pair's folds
+// (r1, r2) pending in both tables. W: witness-section rows per instance; eq: eq(rp) at the local instances.
+struct P2Pair {
+  int nf = 0;
+  Fq r1 = fq_zero(), r2 = fq_zero();
+  size_t W = 0;
+  const Fq* eq = nullptr;
+};
+int phase2_pair(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair& pp, Fq* partials);
+// the last pair's two y folds of ABC and Z (sizes: after both folds), before the next single round
+int phase2_fold2x(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair& pp);
 // one phase-2 round: (e0, e2, e3) of eq(p) * ABC * Z  (src/sumcheck.rs:881-941)
 int phase2_eval(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, int mode, size_t instance_len,
                 size_t witness_secs_len, size_t nws_actual, bool single, const std::vector<size_t>& sc_ni,

@@ -151,6 +151,8 @@ def test_r1cs_verify(ctx, r1cs_gens, case):
     ("p8_x256_q32_shared", {"SPG_P1_PAIR_MAX": "32"}),                # phase-1 pairs only for each mode's last rounds
     ("p2_x1024_q64", {"SPG_Z_TILED": "0", "SPG_SPMV_TILED": "0"}),  # one-element Z fill and Az/Bz/Cz stores
     ("p40_ragged_2secs", {"SPG_Q_BOUND_ALL": "0"}),                   # phase 2's Z prep one q fold per challenge
+    ("p2_x1024_q64", {"SPG_P2_PAIR": "0"}),                           # phase 2 one y round per launch throughout
+    ("p2_x256_2secs", {"SPG_P2_PAIR_MAX": "32"}),                     # phase-2 pairs only after single y rounds
 ])
 def test_r1cs_thread_form_rounds(oracle, case, env):
     """the thread-per-point phase-1 evaluations (k_phase1_eval, and k_phase1_eval_x's row-factored x rounds: one eq

@@ -124,6 +124,8 @@ ROUND_FORMS = {
     "opening_combinations_on_calling_thread": {"SPG_AXPY_POOL": "0"},
     "small_commit_jobs_one_slice": {"SPG_ENC_SPLIT": "0"},
     "phase1_single_rounds": {"SPG_P1_PAIR": "0"},
+    "phase2_single_rounds": {"SPG_P2_PAIR": "0"},
+    "phase2_pairs_small_only": {"SPG_P2_PAIR_MAX": "16"},
     "phase1_pairs_small_only": {"SPG_P1_PAIR_MAX": "16"},
     "witness_upload_workers": {"SPG_H2D": "1"},
 }
