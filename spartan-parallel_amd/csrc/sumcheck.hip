@@ -740,15 +740,19 @@ __global__ void k_pqx_fold2(PqxArgs a, uint32_t total_a, Fq* __restrict__ A, Pqx
 // the top live row bit of each instance with r_j, or scales a one-row instance by 1 - r_j) in one pass: an instance of
 // np = 2^k rows ends as out(w, x) = sum_s W(s) T[s][w][x] with W(s) = prod_{j < k} (bit k-1-j of s ? r_j : 1 - r_j)
 // prod_{j >= k} (1 - r_j) = E[s << (nq - k)], E = eq(r_0 .. r_{nq-1}) (most significant index bit <-> r_0). The same field
-// element as nq folds (exact arithmetic), one read of the table instead of nq read-write passes. Workgroup: 16 outputs
-// (consecutive x: 512-byte rows) x 16 row groups; the 16 partial sums of an output meet in LDS and the sum is written to
-// row 0 in place (only this workgroup reads that output's rows). Domain: per instance nw x cols outputs rounded up to 16.
+// element as nq folds (exact arithmetic), one read of the table instead of nq read-write passes. Workgroup: 256 / G
+// outputs (consecutive x) x G row groups, G chosen by the host so that few outputs still fill the chip (a 2^20 SNARK's
+// block Z has 2048 outputs of 512 rows); the G partial sums of an output meet in an LDS tree and the sum is written to
+// row 0 in place (only this workgroup reads that output's rows). Domain: per instance nw x cols outputs rounded up to
+// 256 / G.
+template <int G>
 __global__ void __launch_bounds__(256) k_pqx_bound_q(PqxArgs a, const Fq* __restrict__ E, int nq, Fq* __restrict__ T) {
+  constexpr int O = 256 / G;
   __shared__ uint32_t sh[8][256];
-  const uint32_t o0 = blockIdx.x * 16;
+  const uint32_t o0 = blockIdx.x * O;
   const int p = find_inst(a, o0);
   const PqxInst& d = pinst(a, p);
-  const uint32_t lo = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const uint32_t lo = threadIdx.x % O, g = threadIdx.x / O;
   const uint32_t o = o0 - d.dom_off + lo, cols = d.sc_ni, np = d.np;
   const bool live = o < d.step_q * cols;
   const uint32_t w = live ? o / cols : 0, x = live ? o % cols : 0;
@@ -758,19 +762,23 @@ __global__ void __launch_bounds__(256) k_pqx_bound_q(PqxArgs a, const Fq* __rest
   const size_t base = pqx_off(d) + (size_t)w * d.ani + x, row = (size_t)d.anw * d.ani;
   Fq acc = fq_zero();
   if (live)
-    for (uint32_t s = g; s < np; s += 16) acc = fq_add(acc, fq_mul(E[(size_t)s << se], T[base + s * row]));
+    for (uint32_t s = g; s < np; s += G) acc = fq_add(acc, fq_mul(E[(size_t)s << se], T[base + s * row]));
 #pragma unroll
   for (int c = 0; c < 8; c++) sh[c][threadIdx.x] = acc.l[c];
   __syncthreads();
-  if (g == 0 && live) {
-    for (int k = 1; k < 16; k++) {
+#pragma unroll
+  for (int h = G / 2; h >= 1; h >>= 1) {
+    if ((int)g < h) {
       Fq v;
 #pragma unroll
-      for (int c = 0; c < 8; c++) v.l[c] = sh[c][k * 16 + lo];
+      for (int c = 0; c < 8; c++) v.l[c] = sh[c][(g + h) * O + lo];
       acc = fq_add(acc, v);
+#pragma unroll
+      for (int c = 0; c < 8; c++) sh[c][threadIdx.x] = acc.l[c];
     }
-    T[base] = acc;
+    __syncthreads();
   }
+  if (g == 0 && live) T[base] = acc;
 }
 
 // ---------------------------------------------------------------- plain cubic (product trees), A*B*C
@@ -1633,6 +1641,15 @@ int pqx_bound_q_all(spg_ctx* ctx, PqxDev& T, const Fq* E, size_t nq) {
   pqx_fill_args(T, a, v);  // the sizes before the folds
   const size_t P = std::min(T.num_instances, T.zlen);
   a.P = (int)P;
+  // row groups per output: enough lanes for ~2^19 (two per lane slot of the chip), at most 256 and the rows there are
+  size_t outs = 0, rows = 1;
+  for (size_t p = 0; p < P; p++) {
+    outs += std::min(T.num_witness_secs, T.anw[p]) * T.num_inputs[p];
+    rows = std::max(rows, T.num_proofs[p]);
+  }
+  int G = 16;
+  while (G < 256 && outs * (size_t)G < ((size_t)1 << 19) && (size_t)G < rows) G *= 2;
+  const size_t O = 256 / G;
   size_t dom = 0, reads = 0;
   for (size_t p = 0; p < P; p++) {
     PqxInst& d = v[p];
@@ -1641,7 +1658,7 @@ int pqx_bound_q_all(spg_ctx* ctx, PqxDev& T, const Fq* E, size_t nq) {
     d.dom_off = (uint32_t)dom;
     d.sc_ni = (uint32_t)cols;
     d.step_q = (uint32_t)nw;
-    dom += (nw * cols + 15) / 16 * 16;
+    dom += (nw * cols + O - 1) / O * O;
     reads += T.num_proofs[p] * nw * cols;
   }
   if (dom >= ((size_t)1 << 32)) return set_err(ctx, SPG_E_ARG, "q bound: domain");
@@ -1652,7 +1669,12 @@ int pqx_bound_q_all(spg_ctx* ctx, PqxDev& T, const Fq* E, size_t nq) {
   if (rc) return rc;
   if (dom) {
     KScope ks(ctx, "sc_fold_q_all", 32.0 * (double)(reads + dom));
-    hipLaunchKernelGGL(k_pqx_bound_q, dim3((unsigned)(dom / 16)), dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
+    const dim3 grid((unsigned)(dom / O));
+    if (G == 16) hipLaunchKernelGGL(k_pqx_bound_q<16>, grid, dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
+    else if (G == 32) hipLaunchKernelGGL(k_pqx_bound_q<32>, grid, dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
+    else if (G == 64) hipLaunchKernelGGL(k_pqx_bound_q<64>, grid, dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
+    else if (G == 128) hipLaunchKernelGGL(k_pqx_bound_q<128>, grid, dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
+    else hipLaunchKernelGGL(k_pqx_bound_q<256>, grid, dim3(256), 0, ctx->stream, a, E, (int)nq, T.d);
     SPG_HIP(ctx, hipGetLastError());
   }
   return 0;
