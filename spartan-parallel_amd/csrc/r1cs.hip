@@ -1334,13 +1334,15 @@ int Prover::run_inner(Laps& lp) {
     const size_t W2 = std::min(ws_len, nws);
     // (fold_pending: round j - 1's fold is not yet in the tables' sizes; the caller launches it first)
     auto p2_pair_ok = [&](size_t j, bool fold_pending) -> bool {
-      if (!p2_pair_on || single || nranks != 1 || j + 1 >= ny || TA != &ABC || TZ != &Zp || ABC.zlen != Zp.zlen)
+      // (one ABC shared by every instance folds through its ping-pong buffer, as the fused single rounds do)
+      if (!p2_pair_on || (single && !ABC2) || nranks != 1 || j + 1 >= ny || TA != &ABC || TZ != &Zp ||
+          ABC.zlen != (single ? 1 : Zp.zlen))
         return false;
       auto live = [&](size_t n) { return fold_pending && n > 1 ? n / 2 : n; };
       size_t dom = 0;
       for (size_t p = 0; p < sc_ni.size(); p++) {
         const size_t N = live(Zp.num_inputs[p]);
-        if (N < 4 || live(ABC.num_inputs[p]) != N || sc_ni[p] != N) return false;
+        if (N < 4 || live(ABC.num_inputs[single ? 0 : p]) != N || sc_ni[p] != N) return false;
         dom += W2 * (N / 4);
       }
       return dom > 0 && dom <= p2_pair_max;
@@ -1358,8 +1360,10 @@ int Prover::run_inner(Laps& lp) {
       pp.r2 = r2;
       pp.W = W2;
       pp.eq = eq_l;
+      pp.B_out = single ? ABC2 : nullptr;
       int r = phase2_pair(ctx, ABC, Zp, pp, partials);
       if (r) return r;
+      if (single && nf == 2) std::swap(ABC.d, ABC2);  // the folded shared ABC is in the other buffer now
       FoldPlan tmp;  // the table bookkeeping of both rounds' folds (the folds ride in the next launch)
       for (int k = 0; k < 2 && !r; k++) {
         r = pqx_fold_plan(ctx, ABC, MODE_X, &tmp);
@@ -1373,7 +1377,10 @@ int Prover::run_inner(Laps& lp) {
       pp.r1 = r1;
       pp.r2 = r2;
       pp.W = W2;
-      return phase2_fold2x(ctx, ABC, Zp, pp);
+      pp.B_out = single ? ABC2 : nullptr;
+      const int r = phase2_fold2x(ctx, ABC, Zp, pp);
+      if (!r && single) std::swap(ABC.d, ABC2);
+      return r;
     };
     bool cur_pair = false;  // the launch in flight evaluates rounds j, j + 1
     if (rounds && ny + nw == 0) rc = to_compact();

@@ -761,8 +761,17 @@ __global__ void __launch_bounds__(256) k_pqx_bound_q(PqxArgs a, const Fq* __rest
   const int se = nq - lgn;
   const size_t base = pqx_off(d) + (size_t)w * d.ani + x, row = (size_t)d.anw * d.ani;
   Fq acc = fq_zero();
-  if (live)
-    for (uint32_t s = g; s < np; s += G) acc = fq_add(acc, fq_mul(E[(size_t)s << se], T[base + s * row]));
+  if (live) {
+    uint32_t s = g;
+    for (; s + 3 * G < np; s += 4 * G) {  // four rows' loads in flight per lane
+      const Fq t0 = T[base + s * row], t1 = T[base + (s + G) * row], t2 = T[base + (s + 2 * G) * row],
+               t3 = T[base + (s + 3 * G) * row];
+      const Fq e0 = E[(size_t)s << se], e1 = E[(size_t)(s + G) << se], e2 = E[(size_t)(s + 2 * G) << se],
+               e3 = E[(size_t)(s + 3 * G) << se];
+      acc = fq_add(acc, fq_add(fq_add(fq_mul(e0, t0), fq_mul(e1, t1)), fq_add(fq_mul(e2, t2), fq_mul(e3, t3))));
+    }
+    for (; s < np; s += G) acc = fq_add(acc, fq_mul(E[(size_t)s << se], T[base + s * row]));
+  }
 #pragma unroll
   for (int c = 0; c < 8; c++) sh[c][threadIdx.x] = acc.l[c];
   __syncthreads();
@@ -984,8 +993,10 @@ struct P2PairArgs {
   int nf;
   Fq r1, r2, r12;
   const Fq* eq;
-  Fq* B;  // ABC
-  Fq* C;  // Z
+  Fq* B;      // ABC
+  Fq* B_out;  // shared ABC (one instance serving all): its folded entries go here, written by instance 0's elements
+  int shared;
+  Fq* C;      // Z
   Fq* partials;
   unsigned* counter;
   uint32_t* mb;
@@ -1007,14 +1018,15 @@ __global__ void __launch_bounds__(BS) k_phase2_pair(P2PairArgs A) {
     const int m = g & 3;  // corner: 0 (0, 0), 1 (0, s), 2 (t, 0), 3 (t, s)
     Fq v = fq_zero();
     if (g < 8) {
-      const PqxInst& d = g < 4 ? pinst(A.ab, p) : dz;
+      const PqxInst& d = g < 4 ? pinst(A.ab, A.shared ? 0 : p) : dz;
       Fq* T = g < 4 ? A.B : A.C;
       const size_t k = pqx_off(d) + (size_t)w * d.ani + y + (m & 1 ? N / 4 : 0) + (m & 2 ? N / 2 : 0);
       if (A.nf == 0) {
         v = T[k];
       } else {
         v = bilerp(T[k], T[k + N], T[k + 2 * (size_t)N], T[k + 3 * (size_t)N], A.r1, A.r2, A.r12);
-        T[k] = v;
+        if (g >= 4 || !A.shared) T[k] = v;  // in place: every entry is this element's alone
+        else if (p == 0) A.B_out[k] = v;    // the shared ABC is read by every instance: ping-pong
       }
     } else if (g >= 12) {
       v = A.eq[p];
@@ -1061,11 +1073,12 @@ __global__ void __launch_bounds__(256) k_phase2_fold2x(P2PairArgs A) {
   for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < A.total; u += gridDim.x * 256) {
     const int p = find_inst(A.zz, u);
     const PqxInst& dz = pinst(A.zz, p);
-    const PqxInst& da = pinst(A.ab, p);
+    const PqxInst& da = pinst(A.ab, A.shared ? 0 : p);
     const uint32_t loc = u - dz.dom_off, w = loc / dz.sc_ni, y = loc % dz.sc_ni;
     const size_t N = dz.ni;
     const size_t ka = pqx_off(da) + (size_t)w * da.ani + y, kz = pqx_off(dz) + (size_t)w * dz.ani + y;
-    A.B[ka] = bilerp(A.B[ka], A.B[ka + N], A.B[ka + 2 * N], A.B[ka + 3 * N], A.r1, A.r2, A.r12);
+    if (!A.shared || p == 0)
+      (A.shared ? A.B_out : A.B)[ka] = bilerp(A.B[ka], A.B[ka + N], A.B[ka + 2 * N], A.B[ka + 3 * N], A.r1, A.r2, A.r12);
     A.C[kz] = bilerp(A.C[kz], A.C[kz + N], A.C[kz + 2 * N], A.C[kz + 3 * N], A.r1, A.r2, A.r12);
   }
 }
@@ -1410,13 +1423,15 @@ static int p2_args(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair
   pqx_fill_args(AB, A.ab, va);
   pqx_fill_args(Z, A.zz, vz);
   const size_t P = std::min(Z.num_instances, Z.zlen);
-  if (AB.zlen != Z.zlen || P == 0) return set_err(ctx, SPG_E_ARG, "phase-2 pair: ABC is not per instance");
-  A.ab.P = (int)P;
+  const bool shared = pp.B_out != nullptr;
+  if ((shared ? AB.zlen != 1 : AB.zlen != Z.zlen) || P == 0) return set_err(ctx, SPG_E_ARG, "phase-2 pair: ABC shape");
+  A.ab.P = shared ? 1 : (int)P;
   A.zz.P = (int)P;
   size_t dom = 0;
   for (size_t p = 0; p < P; p++) {
     const uint32_t N = vz[p].ni;
-    if (va[p].ni != N || N < (fold ? 1u : 4u) || (N & (N - 1)) || pp.W > vz[p].anw || pp.W > va[p].anw)
+    const PqxInst& da = va[shared ? 0 : p];
+    if (da.ni != N || N < (fold ? 1u : 4u) || (N & (N - 1)) || pp.W > vz[p].anw || pp.W > da.anw)
       return set_err(ctx, SPG_E_ARG, "phase-2 pair: sizes");
     vz[p].dom_off = (uint32_t)dom;
     vz[p].sc_ni = fold ? N : N / 4;
@@ -1433,6 +1448,8 @@ static int p2_args(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair
   A.r12 = fq_mul(pp.r1, pp.r2);
   A.eq = pp.eq;
   A.B = AB.d;
+  A.B_out = pp.B_out;
+  A.shared = shared ? 1 : 0;
   A.C = Z.d;
   *dom_out = dom;
   return 0;

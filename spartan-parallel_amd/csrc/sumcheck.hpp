@@ -100,13 +100,14 @@ int phase1_pair(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp, Fq* partials, F
 int pair_wait(spg_ctx* ctx, Fq* out15);
 int phase1_fold2x(spg_ctx* ctx, const PqxDev& T, const P1Pair& pp);
 // two phase-2 y rounds in one launch (k_phase2_pair): eq(p) ABC Z on the 4 x 4 grid of rounds j, j + 1, with ABC
-// per instance (not shared) and every instance's live y size >= 4 in both tables; nf = 2: the previous pair's folds
+// per instance or one shared ABC (B_out) and every instance's live y size >= 4 in both tables; nf = 2: the previous pair's folds
 // (r1, r2) pending in both tables. W: witness-section rows per instance; eq: eq(rp) at the local instances.
 struct P2Pair {
   int nf = 0;
   Fq r1 = fq_zero(), r2 = fq_zero();
   size_t W = 0;
   const Fq* eq = nullptr;
+  Fq* B_out = nullptr;  // one ABC shared by every instance: the other buffer of its ping-pong pair (null: per instance)
 };
 int phase2_pair(spg_ctx* ctx, const PqxDev& AB, const PqxDev& Z, const P2Pair& pp, Fq* partials);
 // the last pair's two y folds of ABC and Z (sizes: after both folds), before the next single round
