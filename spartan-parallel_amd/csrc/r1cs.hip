@@ -886,7 +886,8 @@ int Prover::run_inner(Laps& lp) {
   if (!z_side && (rc = queue_z_fill())) return rc;
 
   lp.lap("setup");
-  Fq* partials = (Fq*)ws_get(ctx, WS_PART, 3 * (size_t)kScGridMax * sizeof(Fq) + 64);
+  // (round evaluations: 3 per workgroup; pair launches: one per element)
+  Fq* partials = (Fq*)ws_get(ctx, WS_PART, std::max(3 * (size_t)kScGridMax, kP1PairMax) * sizeof(Fq) + 64);
   if (!partials) return set_err(ctx, SPG_E_NOMEM, "partials");
 
   // ---- phase 1 (sumcheck.rs:1067-1380)

@@ -81,7 +81,9 @@ int phase1_eval(spg_ctx* ctx, const PqxDev& T, int mode, size_t proof_len, size_
 // two phase-1 rounds in one launch (sumcheck.hip, k_phase1_pair): F = A (B C - D) posted on 15 points of round j's and
 // round j + 1's 4 x 4 grid -- g 0..3: (t, s) = (g, 0); 4..7: (g - 4, 2); 8..11: (g - 8, 3); 12, 13, 14: (0, 1),
 // (2, 1), (3, 1) -- with the pending fold(s) applied on the way (nf 0, 1: fstride per instance, 2: the previous pair's)
-constexpr size_t kP1PairMax = 8192;  // elements (16 lanes each; 16 partials per 256-thread workgroup in `partials`)
+// elements (16 lanes each; 16 partials per 256-thread workgroup in `partials`: one Fq per element); the default cap is
+// SPG_P1_PAIR_MAX / SPG_P2_PAIR_MAX (8192), this is the largest a caller may ask
+constexpr size_t kP1PairMax = 32768;
 struct P1Pair {
   int mode = MODE_X;
   std::vector<size_t> rows, cols, step_q, step_x;
