@@ -153,6 +153,7 @@ def test_r1cs_verify(ctx, r1cs_gens, case):
     ("p40_ragged_2secs", {"SPG_Q_BOUND_ALL": "0"}),                   # phase 2's Z prep one q fold per challenge
     ("p2_x1024_q64", {"SPG_P2_PAIR": "0"}),                           # phase 2 one y round per launch throughout
     ("p2_x256_2secs", {"SPG_P2_PAIR_MAX": "32"}),                     # phase-2 pairs only after single y rounds
+    ("p2_x1024_q64", {"SPG_P1_PAIR_MAX": "32768", "SPG_P2_PAIR_MAX": "32768"}),  # pairs at their largest
 ])
 def test_r1cs_thread_form_rounds(oracle, case, env):
     """the thread-per-point phase-1 evaluations (k_phase1_eval, and k_phase1_eval_x's row-factored x rounds: one eq

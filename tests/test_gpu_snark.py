@@ -126,6 +126,7 @@ ROUND_FORMS = {
     "phase1_single_rounds": {"SPG_P1_PAIR": "0"},
     "phase2_single_rounds": {"SPG_P2_PAIR": "0"},
     "phase2_pairs_small_only": {"SPG_P2_PAIR_MAX": "16"},
+    "pairs_up_to_32768_elements": {"SPG_P1_PAIR_MAX": "32768", "SPG_P2_PAIR_MAX": "32768"},
     "phase1_pairs_small_only": {"SPG_P1_PAIR_MAX": "16"},
     "witness_upload_workers": {"SPG_H2D": "1"},
 }
