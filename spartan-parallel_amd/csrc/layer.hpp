@@ -796,10 +796,8 @@ __global__ void __launch_bounds__(BS) k_layer_persist(PersistArgs A) {
 // products A(X) B(X) (X = 0, 2, 3); C(X) multiplies the sums once. Triples np .. nt-1 (dot-product circuits, own C)
 // take one thread per (triple, i). About 9 products per circuit and index instead of the quad form's 20 lane
 // products, for rounds large enough to fill the chip; the reduction (block sums, ticket, mailbox) is k_layer_round's.
-// WAVES: the register budget asks for at least this many waves per SIMD (1: the compiler's choice, 156 VGPRs = 3 waves)
-template <int BS, int WAVES = 1>
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WAVES)))
-k_layer_round_wide(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
+template <int BS>
+__global__ void __launch_bounds__(BS) k_layer_round_wide(const Triple* __restrict__ tr, const Fq* __restrict__ coeff,
                                                          int np, int nt, int log_len, int do_fold, Fq r,
                                                          const Fq* __restrict__ cin, Fq* __restrict__ cout,
                                                          Fq* __restrict__ partials, unsigned* __restrict__ counter,

@@ -1202,16 +1202,9 @@ static int batched_prove_fused(spg_ctx* ctx, const TreeSh& ts, size_t nc, size_t
           const double fqm_w = (double)len * ((pending ? 2.0 : 0.0) + 3.0 + (double)nc * (pending ? 9.0 : 5.0) +
                                               (double)(tr.size() - nc) * (pending ? 14.0 : 8.0));
           KScope ks(ctx, "spark_layer_round", layer_bytes, 0.0, fqm_w);
-          // SPG_WIDE_WAVES=4: the register budget of 4 waves per SIMD (128 VGPRs) instead of the compiler's 3
-          static const int wide_waves = getenv("SPG_WIDE_WAVES") ? atoi(getenv("SPG_WIDE_WAVES")) : 1;
-          if (wide_waves == 4)
-            hipLaunchKernelGGL((k_layer_round_wide<256, 4>), dim3(K), dim3(256), 0, s, dtr, dcoef, (int)nc,
-                               (int)tr.size(), (int)log_len, pending ? 1 : 0, r_pend, cbuf[cur], cbuf[cur ^ 1], part,
-                               ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
-          else
-            hipLaunchKernelGGL((k_layer_round_wide<256, 1>), dim3(K), dim3(256), 0, s, dtr, dcoef, (int)nc,
-                               (int)tr.size(), (int)log_len, pending ? 1 : 0, r_pend, cbuf[cur], cbuf[cur ^ 1], part,
-                               ctx->d_counter, ctx->d_mbox, ++ctx->mbox_seq);
+          hipLaunchKernelGGL(k_layer_round_wide<256>, dim3(K), dim3(256), 0, s, dtr, dcoef, (int)nc, (int)tr.size(),
+                             (int)log_len, pending ? 1 : 0, r_pend, cbuf[cur], cbuf[cur ^ 1], part, ctx->d_counter,
+                             ctx->d_mbox, ++ctx->mbox_seq);
         } else if (quad) {  // a quad per element, about one element per quad
           const size_t Wd = tr.size() * len;
           BS = Wd <= 16 ? 64 : 256;
