@@ -18,6 +18,8 @@ NAMES = {
     # fused fold + evaluation instances first (first match wins)
     "k_phase1_eval_q<true>": "sc_phase1_fold_eval", "k_phase1_eval<true>": "sc_phase1_fold_eval",
     "k_phase2_eval_q<true>": "sc_phase2_fold_eval", "k_phase2_eval<true>": "sc_phase2_fold_eval",
+    "k_phase1_pair": "sc_phase1_pair", "k_phase2_pair": "sc_phase2_pair", "k_phase1_fold2x": "sc_fold",
+    "k_phase2_fold2x": "sc_fold", "k_pqx_bound_q": "sc_fold_q_all",
     "k_bullet_comb": "msm_bullet_round", "k_comb_msm_parts": "msm_comb_parts", "k_comb_accum": "msm_comb",
     "k_layer_persist": "spark_layer_persist",
     "k_phase1_eval": "sc_phase1_eval", "k_phase2_eval": "sc_phase2_eval", "k_pqx_fold": "sc_fold",
