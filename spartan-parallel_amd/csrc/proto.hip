@@ -493,12 +493,12 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   FqV v2 = tape.vec("blinds_vec_2", 2 * lg);
   const KeyView& kn = g.gens_n;
   const uint32_t G1 = (uint32_t)g.gens_1.G[0], H = (uint32_t)kn.h;
-  // Small proofs (n <= SPG_BULLET_HOST_MAX, default 16) run every MSM on the host pool against fixed-base
+  // Small proofs (n <= SPG_BULLET_HOST_MAX, default 32) run every MSM on the host pool against fixed-base
   // tables of their n generators: a round's two MSMs are then 32 n byte-window additions spread over the pool
-  // instead of a device round trip. Round 2 set 32 against the bucket kernel (~40 us per device round); with the comb
-  // round (~17 us) the n = 32 proofs are faster on the device: ABBA on one box (round 6,
-  // profiles/r06_ab_bullet_host_max.txt) 32 -> 8 won 4 of 5 pairs, 8 -> 16 lost 3 of 4.
-  static const size_t host_max = getenv("SPG_BULLET_HOST_MAX") ? (size_t)atol(getenv("SPG_BULLET_HOST_MAX")) : 16;
+  // instead of a device round trip. Early in round 6 (comb rounds ~17 us) 16 beat 32; once the host proof had its
+  // Cy / beta off the chain, side-by-side encodings and the two-chain Fp carries, 32 beat 16 in 9 of 10 alternations
+  // (median -0.5 to -0.9 ms) and tied 64, and 128 lost (profiles/r06_ab_bullet_host_max.txt).
+  static const size_t host_max = getenv("SPG_BULLET_HOST_MAX") ? (size_t)atol(getenv("SPG_BULLET_HOST_MAX")) : 32;
   const bool on_host = n <= host_max;
   // generator indices G_0..G_{n-1}, G_1, h for B = 2 MSMs, uploaded once for all rounds
   const size_t n2 = n + 2;
