@@ -105,6 +105,27 @@ int spg_buf_free(spg_ctx* ctx, spg_buf* b);
  * prover's sumchecks and SPARK build the same tables internally; this entry point exposes them. */
 int spg_eq_evals(spg_ctx* ctx, const uint64_t* r_mont, size_t ell, spg_buf** out);
 
+/* ---- per-operation seams on device vectors (csrc/seams.hip) ---------------------------------
+ * The reference's dense-polynomial and cubic-sumcheck operations one call at a time, for a caller that drives its
+ * own protocol around them. Scalars are Montgomery [u64; 4]; each call returns when its result is ready. */
+/* DensePolynomial::bound_poly_var_top (src/dense_mlpoly.rs:267-275): Z[i] += r (Z[i + n/2] - Z[i]) for i < n/2,
+ * then the length halves (spg_buf_len); n even and >= 2, else SPG_E_ARG */
+int spg_buf_bound_top(spg_ctx* ctx, spg_buf* b, const uint64_t* r_mont);
+/* DensePolynomial::bound_poly_var_bot (src/dense_mlpoly.rs:350-358): Z[i] = Z[2i] + r (Z[2i+1] - Z[2i]), length halves */
+int spg_buf_bound_bot(spg_ctx* ctx, spg_buf* b, const uint64_t* r_mont);
+/* DensePolynomial::evaluate (src/dense_mlpoly.rs:361-367): sum_i Z[i] chi_i(r), r[0] the index's most significant
+ * bit; b holds exactly 2^ell scalars (the reference asserts the same) and is left unchanged */
+int spg_buf_evaluate(spg_ctx* ctx, const spg_buf* b, const uint64_t* r_mont, size_t ell, uint64_t* out_mont);
+/* One round of SumcheckInstanceProof::prove_cubic with the product-circuit comb A B C (src/sumcheck.rs:207-236,
+ * src/product_tree.rs:185-189): out3 = (eval_point_0, eval_point_2, eval_point_3) over A, B, C of one even length */
+int spg_cubic_round_evals(spg_ctx* ctx, const spg_buf* A, const spg_buf* B, const spg_buf* C, uint64_t* out3_mont);
+/* SumcheckInstanceProof::prove_cubic (src/sumcheck.rs:193-262) with comb A B C on A, B, C of 2^k scalars each
+ * (k >= num_rounds; bound in place, their lengths halve every round) against transcript t: polys receives
+ * num_rounds CompressedUniPoly (3 scalars each: the coefficients without the linear term), r the num_rounds
+ * challenges, claims (A[0], B[0], C[0]) after the last round */
+int spg_prove_cubic(spg_ctx* ctx, const uint64_t* claim_mont, size_t num_rounds, spg_buf* A, spg_buf* B, spg_buf* C,
+                    struct spg_transcript* t, uint64_t* polys_mont, uint64_t* r_mont, uint64_t* claims_mont);
+
 /* ---- generators ------------------------------------------------------------------------------
  * MultiCommitGens::new(n, label) (src/commitments.rs:15-33): n+1 points from SHAKE256(label ||
  * RISTRETTO_BASEPOINT_COMPRESSED) mapped with RistrettoPoint::from_uniform_bytes; G = first n, h = last.

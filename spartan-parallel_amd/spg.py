@@ -247,6 +247,45 @@ class Buf:
                   "spg_eq_evals")
         return b
 
+    # per-operation seams (csrc/seams.hip)
+    def bound_top(self, r):
+        """DensePolynomial::bound_poly_var_top (src/dense_mlpoly.rs:267-275), in place; the length halves."""
+        self.ctx.check(lib().spg_buf_bound_top(self.ctx.handle, self._h, _p(_scalars(r))), "spg_buf_bound_top")
+        self.n //= 2
+
+    def bound_bot(self, r):
+        """DensePolynomial::bound_poly_var_bot (src/dense_mlpoly.rs:350-358), in place; the length halves."""
+        self.ctx.check(lib().spg_buf_bound_bot(self.ctx.handle, self._h, _p(_scalars(r))), "spg_buf_bound_bot")
+        self.n //= 2
+
+    def evaluate(self, r):
+        """DensePolynomial::evaluate (src/dense_mlpoly.rs:361-367) at r (len(r) = log2 of the length)."""
+        a = _scalars(r) if len(r) else np.zeros((1, 4), dtype=np.uint64)
+        out = np.zeros(4, dtype=np.uint64)
+        self.ctx.check(lib().spg_buf_evaluate(self.ctx.handle, self._h, _p(a), ctypes.c_size_t(len(r)), _p(out)),
+                       "spg_buf_evaluate")
+        return out
+
+    @staticmethod
+    def cubic_round_evals(A, B, C):
+        """One prove_cubic round's (e0, e2, e3) with comb A B C (src/sumcheck.rs:207-236)."""
+        out = np.zeros((3, 4), dtype=np.uint64)
+        A.ctx.check(lib().spg_cubic_round_evals(A.ctx.handle, A._h, B._h, C._h, _p(out)), "spg_cubic_round_evals")
+        return out
+
+    @staticmethod
+    def prove_cubic(claim, num_rounds, A, B, C, transcript):
+        """SumcheckInstanceProof::prove_cubic with comb A B C (src/sumcheck.rs:193-262): A, B, C bound in place.
+        Returns (compressed polys [num_rounds, 3, 4], r [num_rounds, 4], claims [3, 4])."""
+        polys = np.zeros((max(num_rounds, 1), 3, 4), dtype=np.uint64)
+        r = np.zeros((max(num_rounds, 1), 4), dtype=np.uint64)
+        claims = np.zeros((3, 4), dtype=np.uint64)
+        A.ctx.check(lib().spg_prove_cubic(A.ctx.handle, _p(_scalars(claim)), ctypes.c_size_t(num_rounds), A._h, B._h,
+                                          C._h, transcript.handle, _p(polys), _p(r), _p(claims)), "spg_prove_cubic")
+        for b in (A, B, C):
+            b.n >>= num_rounds
+        return polys[:num_rounds], r[:num_rounds], claims
+
     def free(self):
         if self._h:
             lib().spg_buf_free(self.ctx.handle, self._h)

@@ -1,0 +1,253 @@
+"""The per-operation seams (csrc/seams.hip, include/spg.h "per-operation seams") against the oracle, bit-exact:
+DensePolynomial::bound_poly_var_top / _bot / evaluate (src/dense_mlpoly.rs:267-275, 350-358, 361-367) and
+SumcheckInstanceProof::prove_cubic with the product-circuit comb A B C (src/sumcheck.rs:193-262,
+src/product_tree.rs:185-189), its transcript included. The CPU tests pin the restatement used as the checker: the
+oracle's field ops (fq_op, pinned by the reference's Fq KATs in test_oracle_core.py), its UniPoly (pinned by the
+reference's UniPoly KATs) and its merlin transcript (pinned by the merlin conformance vector)."""
+import numpy as np
+import pytest
+
+Q = 2**252 + 27742317777372353535851937790883648493
+R = 2**256
+
+
+def mont(x):
+    v = x % Q * R % Q
+    return np.array([(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+
+
+def rand_fq(oracle, rng, n):
+    return oracle.fq_from_bytes_wide(rng.integers(0, 256, 64 * n, dtype=np.uint8).tobytes()).reshape(n, 4)
+
+
+def bound_top_ref(oracle, Z, r):
+    """src/dense_mlpoly.rs:267-275"""
+    n = Z.shape[0] // 2
+    lo, hi = Z[:n], Z[n:]
+    rr = np.repeat(r.reshape(1, 4), n, axis=0)
+    return oracle.fq_op("add", lo, oracle.fq_op("mul", rr, oracle.fq_op("sub", hi, lo)))
+
+
+def bound_bot_ref(oracle, Z, r):
+    """src/dense_mlpoly.rs:350-358"""
+    lo, hi = Z[0::2].copy(), Z[1::2].copy()
+    rr = np.repeat(r.reshape(1, 4), lo.shape[0], axis=0)
+    return oracle.fq_op("add", lo, oracle.fq_op("mul", rr, oracle.fq_op("sub", hi, lo)))
+
+
+def cubic_evals_ref(oracle, A, B, C):
+    """src/sumcheck.rs:207-236 with comb_func = A B C (src/product_tree.rs:185-189)"""
+    n = A.shape[0] // 2
+
+    def fsum(v):  # field sum, pairwise
+        v = v.reshape(-1, 4)
+        while v.shape[0] > 1:
+            if v.shape[0] & 1:
+                v = np.concatenate([v, np.zeros((1, 4), np.uint64)])
+            h = v.shape[0] // 2
+            v = oracle.fq_op("add", v[:h], v[h:])
+        return v[0]
+
+    def prod(a, b, c):
+        return oracle.fq_op("mul", oracle.fq_op("mul", a, b), c)
+
+    def pt2(X):
+        return oracle.fq_op("sub", oracle.fq_op("add", X[n:], X[n:]), X[:n])
+
+    def pt3(X, X2):
+        return oracle.fq_op("sub", oracle.fq_op("add", X2, X[n:]), X[:n])
+
+    A2, B2, C2 = pt2(A), pt2(B), pt2(C)
+    e0 = fsum(prod(A[:n], B[:n], C[:n]))
+    e2 = fsum(prod(A2, B2, C2))
+    e3 = fsum(prod(pt3(A, A2), pt3(B, B2), pt3(C, C2)))
+    return np.stack([e0, e2, e3])
+
+
+def prove_cubic_ref(oracle, claim, num_rounds, A, B, C, tr):
+    """src/sumcheck.rs:193-262 on the oracle's field ops, UniPoly and merlin transcript (tr: OracleTranscript)"""
+    e = claim
+    polys, rs = [], []
+    for _ in range(num_rounds):
+        e0, e2, e3 = cubic_evals_ref(oracle, A, B, C)
+        evals = np.stack([e0, oracle.fq_op("sub", e, e0)[0], e2, e3])
+        coeffs, _, _ = oracle.unipoly(evals, np.zeros(4, np.uint64))
+        tr.append_message(b"poly", b"UniPoly_begin")  # src/unipoly.rs:112-120
+        for c in coeffs:
+            tr.append_message(b"coeff", oracle.fq_to_bytes(c.reshape(1, 4)))
+        tr.append_message(b"poly", b"UniPoly_end")
+        r = oracle.fq_from_bytes_wide(tr.challenge_bytes(b"challenge_nextround", 64)).reshape(4)  # transcript.rs:26-30
+        rs.append(r)
+        A, B, C = bound_top_ref(oracle, A, r), bound_top_ref(oracle, B, r), bound_top_ref(oracle, C, r)
+        _, e, _ = oracle.unipoly(evals, r)
+        polys.append(np.stack([coeffs[0], coeffs[2], coeffs[3]]))  # CompressedUniPoly (src/unipoly.rs:82-87)
+    return polys, rs, np.stack([A[0], B[0], C[0]])
+
+
+def test_prove_cubic_ref_is_a_valid_sumcheck(oracle):
+    """CPU: the checker's restatement satisfies the sumcheck relations the reference verifier checks
+    (src/sumcheck.rs:31-78: poly(0) + poly(1) = e each round; the last e = A(r) B(r) C(r) = claims' product)"""
+    rng = np.random.default_rng(5)
+    ell = 4
+    A, B, C = (rand_fq(oracle, rng, 1 << ell) for _ in range(3))
+    claim = cubic_evals_ref(oracle, np.concatenate([A, np.zeros_like(A)]), np.concatenate([B, np.zeros_like(B)]),
+                            np.concatenate([C, np.zeros_like(C)]))[0]  # sum_i A_i B_i C_i
+    tr = oracle.OracleTranscript(b"cubic")
+    polys, rs, claims = prove_cubic_ref(oracle, claim, ell, A, B, C, tr)
+    e = claim
+    for p, r in zip(polys, rs):
+        c0, c2, c3 = p
+        # decompress with hint e: c1 = e - 2 c0 - c2 - c3 (src/unipoly.rs:95-108)
+        c1 = oracle.fq_op("sub", oracle.fq_op("sub", oracle.fq_op("sub", e, oracle.fq_op("add", c0, c0)), c2), c3)[0]
+        at = [c0, c1, c2, c3]
+        ev, pw = c0, r
+        for c in at[1:]:
+            ev = oracle.fq_op("add", ev, oracle.fq_op("mul", c, pw))[0]
+            pw = oracle.fq_op("mul", pw, r)[0]
+        e = ev
+    fin = oracle.fq_op("mul", oracle.fq_op("mul", claims[0], claims[1]), claims[2])[0]
+    assert np.array_equal(e, fin)
+    # and each claim is the MLE of its table at r (DensePolynomial::evaluate)
+    for T, c in zip((A, B, C), claims):
+        assert np.array_equal(oracle.dense_eval(T, np.stack(rs))[0], c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4, 6, 256, 1000, 1 << 16])
+def test_bound_top_and_bot_match_oracle(ctx, oracle, n):
+    import spg
+
+    rng = np.random.default_rng(n)
+    Z, r = rand_fq(oracle, rng, n), rand_fq(oracle, rng, 1)[0]
+    for name, ref in (("bound_top", bound_top_ref), ("bound_bot", bound_bot_ref)):
+        b = spg.Buf(ctx, Z)
+        getattr(b, name)(r)
+        assert b.n == n // 2 and spg.lib().spg_buf_len(b.handle) == n // 2
+        assert np.array_equal(b.download(), ref(oracle, Z, r)), name
+
+
+@pytest.mark.gpu
+def test_bound_chain_and_edge_challenges(ctx, oracle):
+    """r in {0, 1, q - 1} and a chain of folds down to one entry: top then bot alternately, as a caller binding
+    variables from both ends would"""
+    import spg
+
+    rng = np.random.default_rng(3)
+    Z = rand_fq(oracle, rng, 64)
+    b = spg.Buf(ctx, Z)
+    ref = Z
+    rs = [mont(0), mont(1), mont(-1), rand_fq(oracle, rng, 1)[0], mont(2), mont(-1)]
+    for k, r in enumerate(rs):
+        if k % 2:
+            b.bound_bot(r)
+            ref = bound_bot_ref(oracle, ref, r)
+        else:
+            b.bound_top(r)
+            ref = bound_top_ref(oracle, ref, r)
+        assert np.array_equal(b.download(), ref)
+    assert b.n == 1
+
+
+@pytest.mark.gpu
+def test_bound_rejects_odd_or_short(ctx, oracle):
+    import spg
+
+    for n in (1, 3):
+        b = spg.Buf(ctx, rand_fq(oracle, np.random.default_rng(n), n))
+        with pytest.raises(spg.SpgError):
+            b.bound_top(mont(5))
+        with pytest.raises(spg.SpgError):
+            b.bound_bot(mont(5))
+        assert b.n == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ell", [0, 1, 2, 5, 10, 16])
+def test_evaluate_matches_oracle(ctx, oracle, ell):
+    import spg
+
+    rng = np.random.default_rng(40 + ell)
+    Z = rand_fq(oracle, rng, 1 << ell)
+    r = rand_fq(oracle, rng, ell) if ell else np.zeros((0, 4), np.uint64)
+    b = spg.Buf(ctx, Z)
+    got = b.evaluate(r)
+    want = oracle.dense_eval(Z, r)[0] if ell else Z[0]
+    assert np.array_equal(got, want)
+    assert np.array_equal(b.download(), Z)  # left unchanged
+
+
+@pytest.mark.gpu
+def test_evaluate_mle_kat(ctx):
+    """src/dense_mlpoly.rs:1234-1252: Z = [1, 2, 1, 4] at r = [4, 3] is 28"""
+    import spg
+
+    b = spg.Buf(ctx, np.stack([mont(x) for x in (1, 2, 1, 4)]))
+    assert np.array_equal(b.evaluate(np.stack([mont(4), mont(3)])), mont(28))
+    with pytest.raises(spg.SpgError):
+        b.evaluate(np.stack([mont(4)]))  # the reference asserts r.len() == num_vars
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 8, 1 << 12])
+def test_cubic_round_evals_match_oracle(ctx, oracle, n):
+    import spg
+
+    rng = np.random.default_rng(70 + n)
+    A, B, C = (rand_fq(oracle, rng, n) for _ in range(3))
+    got = spg.Buf.cubic_round_evals(spg.Buf(ctx, A), spg.Buf(ctx, B), spg.Buf(ctx, C))
+    assert np.array_equal(got, cubic_evals_ref(oracle, A, B, C))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ell,rounds", [(1, 1), (3, 3), (6, 6), (6, 2), (10, 10)])
+def test_prove_cubic_matches_oracle(ctx, oracle, ell, rounds):
+    """bytes of the proof (compressed polys), the challenges, the final claims and the transcript state after the
+    call (the next challenge) all equal the oracle's; the spg transcript runs over the caller's merlin through the
+    drop-in callbacks, so the same transcript object is what both sides advance"""
+    import spg
+
+    rng = np.random.default_rng(90 + 7 * ell + rounds)
+    A, B, C = (rand_fq(oracle, rng, 1 << ell) for _ in range(3))
+    claim = rand_fq(oracle, rng, 1)[0]
+    want_polys, want_r, want_claims = prove_cubic_ref(oracle, claim, rounds, A, B, C,
+                                                      ref_tr := oracle.OracleTranscript(b"product_tree"))
+    caller = oracle.OracleTranscript(b"product_tree")
+    t = spg.Transcript.from_callbacks(caller.append_message, caller.challenge_bytes)
+    bA, bB, bC = spg.Buf(ctx, A), spg.Buf(ctx, B), spg.Buf(ctx, C)
+    polys, r, claims = spg.Buf.prove_cubic(claim, rounds, bA, bB, bC, t)
+    assert np.array_equal(polys, np.stack(want_polys))
+    assert np.array_equal(r, np.stack(want_r))
+    if rounds == ell:
+        assert np.array_equal(claims, want_claims)
+    else:  # the tables stay partly bound: claims are their first entries, the rest must match too
+        assert np.array_equal(bA.download(), bound_chain(oracle, A, want_r))
+        assert np.array_equal(claims[0], bound_chain(oracle, A, want_r)[0])
+    assert bA.n == 1 << (ell - rounds)
+    assert caller.challenge_bytes(b"after", 32) == ref_tr.challenge_bytes(b"after", 32)
+
+
+def bound_chain(oracle, T, rs):
+    for r in rs:
+        T = bound_top_ref(oracle, T, r)
+    return T
+
+
+@pytest.mark.gpu
+def test_prove_cubic_native_transcript_and_bad_shapes(ctx, oracle):
+    """spg's own transcript gives the same proof as the callback one; non-power-of-two or too-short tables and
+    mismatched lengths are SPG_E_ARG before any round"""
+    import spg
+
+    rng = np.random.default_rng(11)
+    A, B, C = (rand_fq(oracle, rng, 16) for _ in range(3))
+    claim = mont(12345)
+    p1 = spg.Buf.prove_cubic(claim, 4, spg.Buf(ctx, A), spg.Buf(ctx, B), spg.Buf(ctx, C), spg.Transcript(b"pt"))
+    want = prove_cubic_ref(oracle, claim, 4, A, B, C, oracle.OracleTranscript(b"pt"))
+    assert np.array_equal(p1[0], np.stack(want[0])) and np.array_equal(p1[2], want[2])
+    with pytest.raises(spg.SpgError):
+        spg.Buf.prove_cubic(claim, 5, spg.Buf(ctx, A), spg.Buf(ctx, B), spg.Buf(ctx, C), spg.Transcript(b"pt"))
+    with pytest.raises(spg.SpgError):
+        spg.Buf.prove_cubic(claim, 1, spg.Buf(ctx, A), spg.Buf(ctx, B[:8]), spg.Buf(ctx, C), spg.Transcript(b"pt"))
+    with pytest.raises(spg.SpgError):
+        spg.Buf.prove_cubic(claim, 1, spg.Buf(ctx, A[:12]), spg.Buf(ctx, B[:12]), spg.Buf(ctx, C[:12]),
+                            spg.Transcript(b"pt"))
