@@ -74,7 +74,7 @@ def prove_cubic_ref(oracle, claim, num_rounds, A, B, C, tr):
         coeffs, _, _ = oracle.unipoly(evals, np.zeros(4, np.uint64))
         tr.append_message(b"poly", b"UniPoly_begin")  # src/unipoly.rs:112-120
         for c in coeffs:
-            tr.append_message(b"coeff", oracle.fq_to_bytes(c.reshape(1, 4)))
+            tr.append_message(b"coeff", oracle.fq_to_bytes(c.reshape(1, 4)).tobytes())
         tr.append_message(b"poly", b"UniPoly_end")
         r = oracle.fq_from_bytes_wide(tr.challenge_bytes(b"challenge_nextround", 64)).reshape(4)  # transcript.rs:26-30
         rs.append(r)
