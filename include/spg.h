@@ -125,6 +125,26 @@ int spg_cubic_round_evals(spg_ctx* ctx, const spg_buf* A, const spg_buf* B, cons
  * challenges, claims (A[0], B[0], C[0]) after the last round */
 int spg_prove_cubic(spg_ctx* ctx, const uint64_t* claim_mont, size_t num_rounds, spg_buf* A, spg_buf* B, spg_buf* C,
                     struct spg_transcript* t, uint64_t* polys_mont, uint64_t* r_mont, uint64_t* claims_mont);
+/* DensePolynomialPqx (src/custom_dense_mlpoly.rs:22-359), the ragged (p, q_rev, w, x_rev) table of the R1CS proof,
+ * resident in HBM. spg_pqx_new = DensePolynomialPqx::new (:45-64) on z_mat already in (p, q_rev, w, x_rev) order:
+ * instance p's num_proofs[p] x num_witness_secs x num_inputs[p] scalars row-major, instances one after another
+ * (num_proofs[p], num_inputs[p] powers of two <= the maxima, which are powers of two; < 2^31 scalars in all). */
+typedef struct spg_pqx spg_pqx;
+int spg_pqx_new(spg_ctx* ctx, const uint64_t* z_mont, size_t num_instances, const size_t* num_proofs,
+                size_t max_num_proofs, size_t num_witness_secs, const size_t* num_inputs, size_t max_num_inputs,
+                spg_pqx** out);
+int spg_pqx_free(spg_ctx* ctx, spg_pqx* h);
+/* bound_poly(r, mode) (:180-289): mode 1 = first p variable, 2 = q, 3 = w, 4 = x; mode 1 before every q and x
+ * variable is bound is SPG_E_ARG (the reference's assert_eq! in bound_poly_p, :206-207) */
+int spg_pqx_bound(spg_ctx* ctx, spg_pqx* h, const uint64_t* r_mont, int mode);
+/* evaluate(r_p, r_q, r_w, r_x) (:320-333): a clone bound by r_x, r_w, r_q, r_p, then index(0, 0, 0, 0) */
+int spg_pqx_evaluate(spg_ctx* ctx, const spg_pqx* h, const uint64_t* rp, size_t np, const uint64_t* rq, size_t nq,
+                     const uint64_t* rw, size_t nw, const uint64_t* rx, size_t nx, uint64_t* out_mont);
+/* current sizes: dims = (num_instances, max_num_proofs, num_witness_secs, max_num_inputs); num_proofs / num_inputs
+ * (optional) receive one entry per instance; spg_pqx_download: every allocated entry in spg_pqx_new's layout (folds
+ * rewrite the low halves in place and the allocation never shrinks, as the reference's nested Vecs) */
+int spg_pqx_shape(const spg_pqx* h, size_t* dims, size_t* num_proofs, size_t* num_inputs);
+int spg_pqx_download(spg_ctx* ctx, const spg_pqx* h, uint64_t* z_mont);
 
 /* ---- generators ------------------------------------------------------------------------------
  * MultiCommitGens::new(n, label) (src/commitments.rs:15-33): n+1 points from SHAKE256(label ||

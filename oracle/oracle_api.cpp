@@ -203,6 +203,48 @@ void orc_dense_eval(const uint64_t* Z, size_t n, const uint64_t* r, size_t ell, 
   eq_factored_evals(rv, &L, &R);
   st(out + 4, dot(p.bound(L), R));
 }
+// DensePolynomialPqx::new (custom_dense_mlpoly.rs:45-64) from z in (p, q_rev, w, x_rev) order -- instance p holds
+// num_proofs[p] x nws x num_inputs[p] scalars, row-major -- then k binds bound_poly(rs[i], modes[i])
+// (custom_dense_mlpoly.rs:180-289) in order. out: Z afterwards in the same layout (the allocation never shrinks);
+// sizes: num_instances, max_num_proofs, num_witness_secs, max_num_inputs, num_proofs[0..P), num_inputs[0..P).
+// Returns -1 where the reference's bound_poly_p would panic (max_num_proofs or max_num_inputs != 1).
+int orc_pqx_bind(const uint64_t* z, size_t P, const size_t* num_proofs, size_t max_num_proofs, size_t nws,
+                 const size_t* num_inputs, size_t max_num_inputs, const int* modes, const uint64_t* rs, size_t k,
+                 uint64_t* out, size_t* sizes) {
+  Pqx T;
+  T.Z.resize(P);
+  const uint64_t* s = z;
+  for (size_t p = 0; p < P; p++) {
+    T.Z[p].assign(num_proofs[p], std::vector<FqVec>(nws, FqVec(num_inputs[p])));
+    for (size_t q = 0; q < num_proofs[p]; q++)
+      for (size_t w = 0; w < nws; w++)
+        for (size_t x = 0; x < num_inputs[p]; x++, s += 4) T.Z[p][q][w][x] = ld(s);
+  }
+  T.num_instances = next_pow2(P);
+  T.num_proofs.assign(num_proofs, num_proofs + P);
+  T.max_num_proofs = max_num_proofs;
+  T.num_witness_secs = next_pow2(nws);
+  T.num_inputs.assign(num_inputs, num_inputs + P);
+  T.max_num_inputs = max_num_inputs;
+  for (size_t i = 0; i < k; i++) {
+    if (modes[i] == MODE_P && (T.max_num_proofs != 1 || T.max_num_inputs != 1)) return -1;  // :206-207 assert_eq!
+    T.bound_poly(ld(rs + 4 * i), modes[i]);
+  }
+  uint64_t* o = out;
+  for (size_t p = 0; p < P; p++)
+    for (size_t q = 0; q < num_proofs[p]; q++)
+      for (size_t w = 0; w < nws; w++)
+        for (size_t x = 0; x < num_inputs[p]; x++, o += 4) st(o, T.Z[p][q][w][x]);
+  sizes[0] = T.num_instances;
+  sizes[1] = T.max_num_proofs;
+  sizes[2] = T.num_witness_secs;
+  sizes[3] = T.max_num_inputs;
+  for (size_t p = 0; p < P; p++) {
+    sizes[4 + p] = T.num_proofs[p];
+    sizes[4 + P + p] = T.num_inputs[p];
+  }
+  return 0;
+}
 }
 
 // (baseline-mode state: see orc_baseline_mode below)

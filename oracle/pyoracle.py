@@ -117,6 +117,27 @@ def dense_eval(Z, r):
     return out[0], out[1]
 
 
+def pqx_bind(z, num_proofs, max_num_proofs, nws, num_inputs, max_num_inputs, modes, rs):
+    """DensePolynomialPqx::new then bound_poly(r, mode) per step (src/custom_dense_mlpoly.rs:45-64, 180-289) ->
+    (Z afterwards in z's layout, (num_instances, max_num_proofs, num_witness_secs, max_num_inputs), num_proofs,
+    num_inputs); None where the reference would panic (bound_poly_p before q and x are bound)"""
+    P = len(num_proofs)
+    zz = u64s(z).reshape(-1, 4)
+    out = np.zeros_like(zz)
+    sizes = np.zeros(4 + 2 * P, dtype=np.uint64)
+    np_ = np.asarray(num_proofs, dtype=np.uint64)
+    ni_ = np.asarray(num_inputs, dtype=np.uint64)
+    md = np.asarray(list(modes) or [0], dtype=np.int32)
+    rr = u64s(rs).reshape(-1, 4) if len(modes) else np.zeros((1, 4), np.uint64)
+    rc = lib().orc_pqx_bind(_p(zz), ctypes.c_size_t(P), _p(np_), ctypes.c_size_t(max_num_proofs), ctypes.c_size_t(nws),
+                            _p(ni_), ctypes.c_size_t(max_num_inputs), _p(md), _p(rr), ctypes.c_size_t(len(modes)),
+                            _p(out), _p(sizes))
+    if rc != 0:
+        return None
+    s = [int(x) for x in sizes]
+    return out, tuple(s[:4]), s[4:4 + P], s[4 + P:]
+
+
 # ---------------- hashing ----------------
 def keccak_f1600(state200):
     s = np.frombuffer(bytes(state200), dtype=np.uint8).copy()

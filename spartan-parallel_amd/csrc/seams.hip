@@ -6,6 +6,7 @@
 //   spg_buf_evaluate       DensePolynomial::evaluate             src/dense_mlpoly.rs:361-367
 //   spg_cubic_round_evals  one round of prove_cubic, comb A B C  src/sumcheck.rs:207-236, src/product_tree.rs:185-189
 //   spg_prove_cubic        SumcheckInstanceProof::prove_cubic    src/sumcheck.rs:193-262
+//   spg_pqx_*              DensePolynomialPqx new / bound_poly / evaluate   src/custom_dense_mlpoly.rs:45-64, 180-333
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -17,7 +18,7 @@
 namespace spg {
 namespace {
 
-constexpr size_t kWsSeamPart = 110, kWsSeamTmp = 111;
+constexpr size_t kWsSeamPart = 112, kWsSeamTmp = 113;  // (110, 111: the Pqx descriptors, sumcheck.hip)
 
 // bound_poly_var_bot: out[i] = in[2i] + r (in[2i + 1] - in[2i]); out-of-place (in place, a workgroup's outputs would
 // overwrite entries another workgroup still reads)
@@ -157,4 +158,135 @@ extern "C" int spg_prove_cubic(spg_ctx* ctx, const uint64_t* claim_mont, size_t 
   SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
   for (int k = 0; k < 3; k++) spg::st_fq(claims_mont + 4 * k, fin[k]);
   return spg::tr_status(ctx, t->t, SPG_OK);
+}
+
+// ---- DensePolynomialPqx (src/custom_dense_mlpoly.rs:22-359) as a handle over the prover's own ragged HBM layout
+// (pqx.hpp: instance p owns num_proofs[p] x nws x num_inputs[p] scalars at off[p]; folds rewrite the low halves in
+// place and shrink the current sizes, the allocation stays, so index() keeps the reference's bounds semantics)
+struct spg_pqx {
+  spg::PqxDev T;
+};
+
+namespace {
+int pqx_bind_one(spg_ctx* ctx, spg::PqxDev& T, const Fq& r, int mode) {
+  if (mode < spg::MODE_P || mode > spg::MODE_X) return spg::set_err(ctx, SPG_E_ARG, "DensePolynomialPqx: mode 1..4");
+  // bound_poly_p's assert_eq!(max_num_proofs, 1), assert_eq!(max_num_inputs, 1) (custom_dense_mlpoly.rs:206-207)
+  if (mode == spg::MODE_P && (T.max_num_proofs != 1 || T.max_num_inputs != 1))
+    return spg::set_err(ctx, SPG_E_ARG, "DensePolynomialPqx::bound_poly_p: bind every q and x variable first");
+  return spg::pqx_bound(ctx, T, nullptr, nullptr, r, mode);
+}
+}  // namespace
+
+extern "C" int spg_pqx_new(spg_ctx* ctx, const uint64_t* z_mont, size_t num_instances, const size_t* num_proofs,
+                           size_t max_num_proofs, size_t num_witness_secs, const size_t* num_inputs,
+                           size_t max_num_inputs, spg_pqx** out) {
+  if (!ctx || !out || !num_proofs || !num_inputs || num_instances == 0 || num_witness_secs == 0) return SPG_E_ARG;
+  if (!spg::pow2(max_num_proofs) || !spg::pow2(max_num_inputs))
+    return spg::set_err(ctx, SPG_E_ARG, "spg_pqx_new: max_num_proofs / max_num_inputs must be powers of two");
+  spg_pqx* h = new spg_pqx();
+  spg::PqxDev& T = h->T;
+  T.zlen = num_instances;
+  size_t total = 0;
+  for (size_t p = 0; p < num_instances; p++) {
+    if (!spg::pow2(num_proofs[p]) || num_proofs[p] > max_num_proofs || !spg::pow2(num_inputs[p]) ||
+        num_inputs[p] > max_num_inputs) {
+      delete h;
+      return spg::set_err(ctx, SPG_E_ARG, "spg_pqx_new: num_proofs[p] / num_inputs[p] must be powers of two <= max");
+    }
+    T.off.push_back(total);
+    T.anp.push_back(num_proofs[p]);
+    T.anw.push_back(num_witness_secs);
+    T.ani.push_back(num_inputs[p]);
+    total += num_proofs[p] * num_witness_secs * num_inputs[p];
+  }
+  if (total >= ((size_t)1 << 31) || !z_mont) {  // the fold kernels index the domain with 32-bit lanes
+    delete h;
+    return spg::set_err(ctx, SPG_E_ARG, "spg_pqx_new: at most 2^31 scalars, z required");
+  }
+  T.total = total;
+  T.num_instances = 1;
+  while (T.num_instances < num_instances) T.num_instances *= 2;
+  T.num_witness_secs = 1;
+  while (T.num_witness_secs < num_witness_secs) T.num_witness_secs *= 2;
+  T.max_num_proofs = max_num_proofs;
+  T.max_num_inputs = max_num_inputs;
+  T.num_proofs.assign(num_proofs, num_proofs + num_instances);
+  T.num_inputs.assign(num_inputs, num_inputs + num_instances);
+  if (hipMalloc(&T.d, total * sizeof(Fq) + 64) != hipSuccess) {
+    delete h;
+    return spg::set_err(ctx, SPG_E_NOMEM, "spg_pqx_new");
+  }
+  if (hipMemcpy(T.d, z_mont, total * sizeof(Fq), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(T.d);
+    delete h;
+    return spg::set_err(ctx, SPG_E_HIP, "spg_pqx_new: upload");
+  }
+  *out = h;
+  return SPG_OK;
+}
+
+extern "C" int spg_pqx_free(spg_ctx* ctx, spg_pqx* h) {
+  (void)ctx;
+  if (!h) return SPG_OK;
+  hipFree(h->T.d);
+  delete h;
+  return SPG_OK;
+}
+
+// the current sizes: dims = (num_instances, max_num_proofs, num_witness_secs, max_num_inputs); num_proofs /
+// num_inputs (optional) receive Z.len() entries each
+extern "C" int spg_pqx_shape(const spg_pqx* h, size_t* dims, size_t* num_proofs, size_t* num_inputs) {
+  if (!h || !dims) return SPG_E_ARG;
+  const spg::PqxDev& T = h->T;
+  dims[0] = T.num_instances;
+  dims[1] = T.max_num_proofs;
+  dims[2] = T.num_witness_secs;
+  dims[3] = T.max_num_inputs;
+  for (size_t p = 0; p < T.zlen; p++) {
+    if (num_proofs) num_proofs[p] = T.num_proofs[p];
+    if (num_inputs) num_inputs[p] = T.num_inputs[p];
+  }
+  return SPG_OK;
+}
+
+// Z in spg_pqx_new's layout (every allocated entry, folded or not)
+extern "C" int spg_pqx_download(spg_ctx* ctx, const spg_pqx* h, uint64_t* z_mont) {
+  if (!ctx || !h || !z_mont) return SPG_E_ARG;
+  SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  SPG_HIP(ctx, hipMemcpy(z_mont, h->T.d, h->T.total * sizeof(Fq), hipMemcpyDeviceToHost));
+  return SPG_OK;
+}
+
+// DensePolynomialPqx::bound_poly (custom_dense_mlpoly.rs:180-199): mode 1 p, 2 q, 3 w, 4 x
+extern "C" int spg_pqx_bound(spg_ctx* ctx, spg_pqx* h, const uint64_t* r_mont, int mode) {
+  if (!ctx || !h || !r_mont) return SPG_E_ARG;
+  int rc = pqx_bind_one(ctx, h->T, spg::ld_fq(r_mont), mode);
+  if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = spg::set_err(ctx, SPG_E_HIP, "spg_pqx_bound");
+  return rc;
+}
+
+// DensePolynomialPqx::evaluate (custom_dense_mlpoly.rs:320-333): a clone bound by r_x, r_w, r_q, r_p in that order,
+// then index(0, 0, 0, 0); h is left unchanged
+extern "C" int spg_pqx_evaluate(spg_ctx* ctx, const spg_pqx* h, const uint64_t* rp, size_t np, const uint64_t* rq,
+                                size_t nq, const uint64_t* rw, size_t nw, const uint64_t* rx, size_t nx,
+                                uint64_t* out_mont) {
+  if (!ctx || !h || !out_mont || (np && !rp) || (nq && !rq) || (nw && !rw) || (nx && !rx)) return SPG_E_ARG;
+  spg::PqxDev C = h->T;  // the clone: same descriptors and sizes, its own copy of the entries
+  C.d = (Fq*)spg::ws_get(ctx, spg::kWsSeamTmp, C.total * sizeof(Fq) + 64);
+  if (!C.d) return spg::set_err(ctx, SPG_E_NOMEM, "spg_pqx_evaluate");
+  SPG_HIP(ctx, hipMemcpyAsync(C.d, h->T.d, C.total * sizeof(Fq), hipMemcpyDeviceToDevice, ctx->stream));
+  const struct {
+    const uint64_t* r;
+    size_t n;
+    int mode;
+  } secs[4] = {{rx, nx, spg::MODE_X}, {rw, nw, spg::MODE_W}, {rq, nq, spg::MODE_Q}, {rp, np, spg::MODE_P}};
+  for (const auto& s : secs)
+    for (size_t i = 0; i < s.n; i++)
+      if (int rc = pqx_bind_one(ctx, C, spg::ld_fq(s.r + 4 * i), s.mode)) return rc;
+  // index(0, 0, 0, 0): Z[0][0][0][0] when that entry is allocated (custom_dense_mlpoly.rs:118-128)
+  Fq v = spg::fq_zero();
+  if (C.zlen && C.anp[0] && C.anw[0] && C.ani[0])
+    if (int rc = spg::d2h(ctx, &v, C.d, sizeof(Fq))) return rc;
+  spg::st_fq(out_mont, v);
+  return SPG_OK;
 }

@@ -298,6 +298,58 @@ class Buf:
             pass
 
 
+class Pqx:
+    """DensePolynomialPqx (src/custom_dense_mlpoly.rs:22-359) resident in HBM (spg_pqx_*): z holds instance p's
+    num_proofs[p] x num_witness_secs x num_inputs[p] scalars in (q_rev, w, x_rev) order, instances concatenated."""
+
+    def __init__(self, ctx, z, num_proofs, max_num_proofs, num_witness_secs, num_inputs, max_num_inputs):
+        self.ctx = ctx
+        a = _scalars(z)
+        self.P = len(num_proofs)
+        self.n = a.shape[0]
+        np_ = np.asarray(num_proofs, dtype=np.uint64)
+        ni_ = np.asarray(num_inputs, dtype=np.uint64)
+        self._h = ctypes.c_void_p()
+        ctx.check(lib().spg_pqx_new(ctx.handle, _p(a), ctypes.c_size_t(self.P), _p(np_), ctypes.c_size_t(max_num_proofs),
+                                    ctypes.c_size_t(num_witness_secs), _p(ni_), ctypes.c_size_t(max_num_inputs),
+                                    ctypes.byref(self._h)), "spg_pqx_new")
+
+    def bound(self, r, mode):
+        """bound_poly(r, mode): 1 = p, 2 = q, 3 = w, 4 = x (src/custom_dense_mlpoly.rs:180-199)"""
+        self.ctx.check(lib().spg_pqx_bound(self.ctx.handle, self._h, _p(_scalars(r)), ctypes.c_int(mode)),
+                       "spg_pqx_bound")
+
+    def evaluate(self, rp, rq, rw, rx):
+        """evaluate(r_p, r_q, r_w, r_x) (src/custom_dense_mlpoly.rs:320-333); the table is left unchanged"""
+        arrs = [_scalars(r) if len(r) else np.zeros((1, 4), dtype=np.uint64) for r in (rp, rq, rw, rx)]
+        args = []
+        for a, r in zip(arrs, (rp, rq, rw, rx)):
+            args += [_p(a), ctypes.c_size_t(len(r))]
+        out = np.zeros(4, dtype=np.uint64)
+        self.ctx.check(lib().spg_pqx_evaluate(self.ctx.handle, self._h, *args, _p(out)), "spg_pqx_evaluate")
+        return out
+
+    def shape(self):
+        dims = np.zeros(4, dtype=np.uint64)
+        npf = np.zeros(self.P, dtype=np.uint64)
+        nin = np.zeros(self.P, dtype=np.uint64)
+        assert lib().spg_pqx_shape(self._h, _p(dims), _p(npf), _p(nin)) == 0
+        return tuple(int(x) for x in dims), [int(x) for x in npf], [int(x) for x in nin]
+
+    def download(self):
+        out = np.zeros((self.n, 4), dtype=np.uint64)
+        self.ctx.check(lib().spg_pqx_download(self.ctx.handle, self._h, _p(out)), "spg_pqx_download")
+        return out
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().spg_pqx_free(self.ctx.handle, self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
 class Gens:
     """Device-resident MultiCommitGens (G_0..G_{n-1}, h) with fixed-base window tables."""
 

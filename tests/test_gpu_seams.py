@@ -251,3 +251,175 @@ def test_prove_cubic_native_transcript_and_bad_shapes(ctx, oracle):
     with pytest.raises(spg.SpgError):
         spg.Buf.prove_cubic(claim, 1, spg.Buf(ctx, A[:12]), spg.Buf(ctx, B[:12]), spg.Buf(ctx, C[:12]),
                             spg.Transcript(b"pt"))
+
+
+# ---- DensePolynomialPqx (src/custom_dense_mlpoly.rs:22-359) ----
+
+def pqx_py(z, num_proofs, max_np, nws, num_inputs, max_ni, steps):
+    """pure-Python restatement of new + bound_poly (custom_dense_mlpoly.rs:45-64, 205-289) on integers mod q, small
+    sizes only: pins the oracle's C++ (orc_pqx_bind) on the CPU"""
+    P = len(num_proofs)
+    Z, k = [], 0
+    for p in range(P):
+        Z.append([[[z[k + (q * nws + w) * num_inputs[p] + x] for x in range(num_inputs[p])] for w in range(nws)]
+                  for q in range(num_proofs[p])])
+        k += num_proofs[p] * nws * num_inputs[p]
+    ninst, nw2 = 1 << (P - 1).bit_length(), 1 << (nws - 1).bit_length()
+    npf, nin = list(num_proofs), list(num_inputs)
+    for mode, r in steps:
+        if mode == 1:
+            if max_np != 1 or max_ni != 1:
+                return None
+            ninst //= 2
+            for p in range(ninst):
+                for w in range(min(nw2, len(Z[p][0]))):
+                    hi = Z[p + ninst][0][w][0] if p + ninst < P else 0
+                    Z[p][0][w][0] = (Z[p][0][w][0] + r * (hi - Z[p][0][w][0])) % Q
+        elif mode == 2:
+            max_np //= 2
+            for p in range(min(ninst, P)):
+                if npf[p] == 1:
+                    for w in range(min(nw2, len(Z[p][0]))):
+                        for x in range(nin[p]):
+                            Z[p][0][w][x] = (1 - r) * Z[p][0][w][x] % Q
+                else:
+                    npf[p] //= 2
+                    for q in range(npf[p]):
+                        for w in range(min(nw2, len(Z[p][q]))):
+                            for x in range(nin[p]):
+                                Z[p][q][w][x] = (Z[p][q][w][x] + r * (Z[p][q + npf[p]][w][x] - Z[p][q][w][x])) % Q
+        elif mode == 3:
+            nw2 //= 2
+            for p in range(min(ninst, P)):
+                for q in range(npf[p]):
+                    for w in range(nw2):
+                        for x in range(nin[p]):
+                            hi = Z[p][q][w + nw2][x] if w + nw2 < len(Z[p][q]) else 0
+                            Z[p][q][w][x] = (Z[p][q][w][x] + r * (hi - Z[p][q][w][x])) % Q
+        else:
+            max_ni //= 2
+            for p in range(min(ninst, P)):
+                if nin[p] == 1:
+                    for q in range(npf[p]):
+                        for w in range(min(nw2, len(Z[p][q]))):
+                            Z[p][q][w][0] = (1 - r) * Z[p][q][w][0] % Q
+                else:
+                    nin[p] //= 2
+                    for q in range(npf[p]):
+                        for w in range(min(nw2, len(Z[p][q]))):
+                            for x in range(nin[p]):
+                                Z[p][q][w][x] = (Z[p][q][w][x] + r * (Z[p][q][w][x + nin[p]] - Z[p][q][w][x])) % Q
+    flat = [v for p in Z for q in p for w in q for v in w]
+    return flat, (ninst, max_np, nw2, max_ni), npf, nin
+
+
+def to_int(m):
+    return sum(int(m[i]) << (64 * i) for i in range(4)) * pow(R, -1, Q) % Q
+
+
+# (num_proofs, max_num_proofs, num_witness_secs, num_inputs, max_num_inputs): ragged q and x, a w count that is not a
+# power of two (zero hi sections), single-proof / single-input instances, and > 32 instances (descriptors in HBM)
+PQX_SHAPES = [
+    ([4, 1, 2], 4, 3, [8, 2, 1], 8),
+    ([2, 2], 2, 4, [4, 4], 4),
+    ([1], 1, 1, [1], 1),
+    ([8, 4, 4, 2, 1], 8, 2, [16, 16, 4, 8, 2], 16),
+    ([2] * 20 + [1] * 20, 2, 3, [4] * 40, 4),
+]
+
+
+def pqx_plan(shape, order):
+    """a full set of binds: every x, w, q variable, then p (the R1CS proof's order is x first, then w, q, p), or
+    q / w / x interleaved"""
+    npf, max_np, nws, nin, max_ni = shape
+    lx, lq = (max_ni - 1).bit_length(), (max_np - 1).bit_length()
+    lw, lp = (nws - 1).bit_length(), (len(npf) - 1).bit_length()
+    if order == "xwqp":
+        modes = [4] * lx + [3] * lw + [2] * lq
+    else:
+        modes = [2] * lq + [4] * lx + [3] * lw
+        modes = modes[::2] + modes[1::2]
+    return modes + [1] * lp
+
+
+def test_pqx_oracle_matches_python_loops(oracle):
+    """CPU: orc_pqx_bind equals the reference loops restated on Python integers, after every bind, including the
+    panic case (p bound first)"""
+    rng = np.random.default_rng(17)
+    for shape in PQX_SHAPES[:4]:
+        npf, max_np, nws, nin, max_ni = shape
+        n = sum(a * nws * b for a, b in zip(npf, nin))
+        z = rand_fq(oracle, rng, n)
+        for order in ("xwqp", "mixed"):
+            modes = pqx_plan(shape, order)
+            rs = rand_fq(oracle, rng, len(modes)) if modes else np.zeros((0, 4), np.uint64)
+            for k in range(len(modes) + 1):
+                got = oracle.pqx_bind(z, npf, max_np, nws, nin, max_ni, modes[:k], rs[:k])
+                want = pqx_py([to_int(v) for v in z], npf, max_np, nws, nin, max_ni,
+                              [(m, to_int(r)) for m, r in zip(modes[:k], rs[:k])])
+                assert [to_int(v) for v in got[0]] == want[0] and list(got[1:]) == list(want[1:])
+        if max_np > 1 or max_ni > 1:
+            assert oracle.pqx_bind(z, npf, max_np, nws, nin, max_ni, [1], rand_fq(oracle, rng, 1)) is None
+            assert pqx_py([0] * n, npf, max_np, nws, nin, max_ni, [(1, 5)]) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("si", range(len(PQX_SHAPES)))
+@pytest.mark.parametrize("order", ["xwqp", "mixed"])
+def test_pqx_bound_matches_oracle(ctx, oracle, si, order):
+    """every allocated entry and every size field after each bind equal the oracle's"""
+    import spg
+
+    shape = PQX_SHAPES[si]
+    npf, max_np, nws, nin, max_ni = shape
+    rng = np.random.default_rng(200 + si)
+    z = rand_fq(oracle, rng, sum(a * nws * b for a, b in zip(npf, nin)))
+    modes = pqx_plan(shape, order)
+    rs = rand_fq(oracle, rng, max(len(modes), 1))
+    T = spg.Pqx(ctx, z, npf, max_np, nws, nin, max_ni)
+    assert np.array_equal(T.download(), z)
+    for k, m in enumerate(modes):
+        T.bound(rs[k], m)
+        want = oracle.pqx_bind(z, npf, max_np, nws, nin, max_ni, modes[:k + 1], rs[:k + 1])
+        assert np.array_equal(T.download(), want[0]), (k, m)
+        dims, gp, gi = T.shape()
+        assert (dims, gp, gi) == (want[1], want[2], want[3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("si", range(len(PQX_SHAPES)))
+def test_pqx_evaluate_matches_oracle(ctx, oracle, si):
+    """evaluate(r_p, r_q, r_w, r_x) = the oracle's x, w, q, p binds then index(0, 0, 0, 0); the table is unchanged;
+    a p bind before q and x are bound is SPG_E_ARG (the reference's assert)"""
+    import spg
+
+    npf, max_np, nws, nin, max_ni = PQX_SHAPES[si]
+    rng = np.random.default_rng(300 + si)
+    z = rand_fq(oracle, rng, sum(a * nws * b for a, b in zip(npf, nin)))
+    lx, lq = (max_ni - 1).bit_length(), (max_np - 1).bit_length()
+    lw, lp = (nws - 1).bit_length(), (len(npf) - 1).bit_length()
+    rp, rq, rw, rx = (rand_fq(oracle, rng, n) if n else np.zeros((0, 4), np.uint64) for n in (lp, lq, lw, lx))
+    T = spg.Pqx(ctx, z, npf, max_np, nws, nin, max_ni)
+    got = T.evaluate(rp, rq, rw, rx)
+    want = oracle.pqx_bind(z, npf, max_np, nws, nin, max_ni, [4] * lx + [3] * lw + [2] * lq + [1] * lp,
+                           np.concatenate([rx, rw, rq, rp]))
+    assert np.array_equal(got, want[0][0])
+    assert np.array_equal(T.download(), z)
+    if max_np > 1 or max_ni > 1:
+        with pytest.raises(spg.SpgError):
+            T.bound(mont(3), 1)
+        with pytest.raises(spg.SpgError):
+            T.evaluate(rp if lp else np.stack([mont(2)]), [], rw, rx)
+
+
+@pytest.mark.gpu
+def test_pqx_rejects_bad_shapes(ctx, oracle):
+    import spg
+
+    z = rand_fq(oracle, np.random.default_rng(1), 64)
+    for npf, max_np, nin, max_ni in (([3], 4, [4], 4), ([4], 2, [4], 4), ([2], 2, [4], 3)):
+        with pytest.raises(spg.SpgError):
+            spg.Pqx(ctx, z, npf, max_np, 1, nin, max_ni)
+    T = spg.Pqx(ctx, z[:8], [2], 2, 1, [4], 4)
+    with pytest.raises(spg.SpgError):
+        T.bound(mont(1), 5)
