@@ -240,6 +240,8 @@ static const int kBulletPartsMax = 512;
 // points into d_parts (stream-ordered, no completion post); 1 when the comb does not apply
 int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const uint32_t* d_idx, size_t gmax, int n,
                    int B, Ext* d_parts, int* per_msm);
+// out[j] = d cw_j (j odd ? u : u^-1) as Montgomery scalars, from the device Bullet rounds' cw (plain integers)
+int bullet_delta_scalars(spg_ctx* ctx, const Fq* cw, int n, const Fq& d, const Fq& u, const Fq& uinv, Fq* out);
 int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq* cw_in, Fq* aa_out, Fq* cw_out,
                       const uint32_t* gidx, size_t gmax, const Fq& u, const Fq& uinv, int k, int n, int nk,
                       Ext* d_parts, uint32_t* seq_out, int* per_msm);

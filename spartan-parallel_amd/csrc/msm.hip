@@ -709,6 +709,22 @@ int bullet_round_comb(spg_ctx* ctx, const spg_gens* g, const Fq* aa_in, const Fq
   return 0;
 }
 
+// DotProductProofLog's delta scalars d cw_j from the device Bullet state: cw (plain integers, bullet.hpp) as the last
+// round left it, times the last challenge's fold (u for odd j, u^-1 for even j) and d; cu = (d u) R^2, cinv = (d u^-1) R^2
+// (raw limbs), so that one Montgomery product gives the Montgomery scalar d f cw_j R
+__global__ void k_bullet_delta_scalars(const Fq* __restrict__ cw, int n, Fq cu, Fq cinv, Fq* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) out[j] = fq_mul((j & 1) ? cu : cinv, cw[j]);
+}
+
+int bullet_delta_scalars(spg_ctx* ctx, const Fq* cw, int n, const Fq& d, const Fq& u, const Fq& uinv, Fq* out) {
+  const Fq cu = fq_to_mont(fq_mul(d, u)), cinv = fq_to_mont(fq_mul(d, uinv));
+  hipLaunchKernelGGL(k_bullet_delta_scalars, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, cw, n, cu,
+                     cinv, out);
+  SPG_HIP(ctx, hipGetLastError());
+  return 0;
+}
+
 int comb_msm_parts(spg_ctx* ctx, const spg_gens* g, const Fq* d_scalars, const uint32_t* d_idx, size_t gmax, int n,
                    int B, Ext* d_parts, int* per_msm) {
   static const bool on = !getenv("SPG_BULLET_COMB") || atoi(getenv("SPG_BULLET_COMB")) != 0;

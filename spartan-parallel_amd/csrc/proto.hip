@@ -353,7 +353,7 @@ static void par_range(size_t n, const std::function<void(size_t, size_t)>& f) {
 // Folds of one Bullet round on host copies (a, b for the next c_L / c_R, cw for the final g_hat) with u and
 // u^-1 of the round that took the size from 2 nn to nn (when fold), plus the next round's cross products
 // c_L = <a_L, b_R>, c_R = <a_R, b_L> over the halves of nn / 2 entries, in one pool burst.
-static void host_fold_dots(FqV& aa, FqV& bb, FqV& cw, size_t n, size_t nn, bool fold, const Fq& u, const Fq& uinv,
+static void host_fold_dots(FqV& aa, FqV& bb, FqV* cw, size_t n, size_t nn, bool fold, const Fq& u, const Fq& uinv,
                            Fq* cL, Fq* cR) {
   const size_t nh = nn / 2;  // nn: size after the fold (2 nn before it)
   const int C = nh >= 64 ? 8 : 1;
@@ -370,8 +370,8 @@ static void host_fold_dots(FqV& aa, FqV& bb, FqV& cw, size_t n, size_t nn, bool 
       sl = fq_add(sl, fq_mul(aa[i], bb[i + nh]));
       sr = fq_add(sr, fq_mul(aa[i + nh], bb[i]));
     }
-    if (fold)
-      for (size_t j = n * c / C; j < n * (c + 1) / C; j++) cw[j] = fq_mul(cw[j], (j % (2 * nn)) < nn ? uinv : u);
+    if (fold && cw)  // (cw null: delta's scalars come from the device's own cw, DevFinal)
+      for (size_t j = n * c / C; j < n * (c + 1) / C; j++) (*cw)[j] = fq_mul((*cw)[j], (j % (2 * nn)) < nn ? uinv : u);
     pl[c] = sl;
     pr[c] = sr;
   });
@@ -414,10 +414,17 @@ static int bullet_round0_launch(spg_ctx* ctx, ProverGens& g, size_t n, const Fq*
                              d_bk, seq, per);
 }
 
+// what the device rounds leave for delta's scalars (fin != null: the host keeps no copy of cw; the rounds fold the
+// device's)
+struct DevFinal {
+  const Fq* cw = nullptr;  // the device cw before the last challenge's fold (plain integers)
+  Fq u, uinv;              // the last challenge
+};
+
 static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x, const FqV& a, const Fq& r,
                                 const FqV& v1, const FqV& v2, const uint32_t* d_idx, size_t gmax, Ext* mbk, Ext* d_bk,
                                 FqV* aa, FqV* bb, FqV* cw, Fq* blind_fin, DotProductProofLogP* out, bool pre0 = false,
-                                uint32_t seq0 = 0, int per0 = 0) {
+                                uint32_t seq0 = 0, int per0 = 0, DevFinal* fin = nullptr) {
   const size_t n = x.size();
   const size_t G1 = g.gens_1.G[0], H = g.gens_n.h;
   Fq* st = (Fq*)ws_get(ctx, 24, 4 * n * sizeof(Fq) + 64);  // aa[2], cw[2]
@@ -441,7 +448,7 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
     if (rc) return rc;
     g_msm_laps.lap("bullet_launch");
     Fq cL, cR;
-    host_fold_dots(*aa, *bb, *cw, n, nk, k > 0, u, uinv, &cL, &cR);
+    host_fold_dots(*aa, *bb, fin ? nullptr : cw, n, nk, k > 0, u, uinv, &cL, &cR);
     const Fq blind_L = v1[k], blind_R = v2[k];
     std::vector<h::HExt> ex = g.host.sum_many({{{G1, H}, {fq_mul(cL, r), blind_L}}, {{G1, H}, {fq_mul(cR, r), blind_R}}});
     g_msm_laps.lap("bullet_host_overlap");
@@ -464,12 +471,21 @@ static int bullet_rounds_device(spg_ctx* ctx, ProverGens& g, Tr& t, const FqV& x
     g_msm_laps.lap("bullet_challenge");
     nk /= 2;
   }
-  // the last round's fold of the host copies (a_hat, b_hat and the final generator weights)
+  // the last round's fold of the host copies (a_hat, b_hat and the final generator weights; with fin, delta's scalars
+  // come from the device cw instead)
   (*aa)[0] = fq_add(fq_mul((*aa)[0], u), fq_mul(uinv, (*aa)[1]));
   (*bb)[0] = fq_add(fq_mul((*bb)[0], uinv), fq_mul(u, (*bb)[1]));
-  par_range(n, [&](size_t lo, size_t hi) {
-    for (size_t j = lo; j < hi; j++) (*cw)[j] = fq_mul((*cw)[j], (j & 1) ? u : uinv);
-  });
+  if (fin) {
+    size_t lg = 0;
+    while (((size_t)1 << lg) < n) lg++;
+    fin->cw = d_cw[lg & 1];  // round lg - 1 wrote d_cw[lg & 1]
+    fin->u = u;
+    fin->uinv = uinv;
+  } else {
+    par_range(n, [&](size_t lo, size_t hi) {
+      for (size_t j = lo; j < hi; j++) (*cw)[j] = fq_mul((*cw)[j], (j & 1) ? u : uinv);
+    });
+  }
   g_msm_laps.lap("bullet_fold");
   return 0;
 }
@@ -622,9 +638,14 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   size_t nk = n, k = 0;
   bool beta_done = false;
   g_msm_laps.lap("bullet_prep");
+  // delta's scalars d cw_j on the device from the rounds' own cw (no host fold of cw, no upload; SPG_DELTA_DEV=0: host)
+  static const bool delta_dev = !getenv("SPG_DELTA_DEV") || atoi(getenv("SPG_DELTA_DEV")) != 0;
+  static const bool delta_comb = !getenv("SPG_DELTA_COMB") || atoi(getenv("SPG_DELTA_COMB")) != 0;
+  DevFinal dfin;
+  const bool use_dfin = mbk && delta_comb && delta_dev;
   if (mbk) {
     int rc = bullet_rounds_device(ctx, g, t, x, a, r, v1, v2, d_idx, gmax, mbk, d_mbk, &aa, &bb, &cw, &blind_fin, out,
-                                  pre0, seq0, per0);
+                                  pre0, seq0, per0, use_dfin ? &dfin : nullptr);
     if (rc) return rc;
     nk = 1;
   }
@@ -726,18 +747,30 @@ int dotproduct_log_prove(spg_ctx* ctx, ProverGens& g, Tr& t, Tape& tape, const F
   } else {
     // device rounds: d g_hat from the comb table as partial points (as Cx), r_delta h and beta on the host meanwhile;
     // the bucket form (device_msm_flat) where the comb does not apply
-    static const bool delta_comb = !getenv("SPG_DELTA_COMB") || atoi(getenv("SPG_DELTA_COMB")) != 0;
     int cper = 0, rc = 1;
     if (mbk && delta_comb) {  // (the mapped region's Cx part and slot 26 are free again: Cx is done, the rounds are over)
       Fq* d_s = (Fq*)ws_get(ctx, 26, n * sizeof(Fq) + 64);
-      Fq* stage = (Fq*)pinned_get(ctx, n * sizeof(Fq) + 64);
-      if (!d_s || !stage) return set_err(ctx, SPG_E_NOMEM, "delta scalars");
-      par_range(n, [&](size_t lo, size_t hi) {
-        for (size_t j = lo; j < hi; j++) stage[j] = fq_mul(d, cw[j]);
-      });
-      SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+      if (!d_s) return set_err(ctx, SPG_E_NOMEM, "delta scalars");
+      if (use_dfin) {
+        rc = bullet_delta_scalars(ctx, dfin.cw, (int)n, d, dfin.u, dfin.uinv, d_s);
+        if (rc) return rc;
+      } else {
+        Fq* stage = (Fq*)pinned_get(ctx, n * sizeof(Fq) + 64);
+        if (!stage) return set_err(ctx, SPG_E_NOMEM, "delta scalars");
+        par_range(n, [&](size_t lo, size_t hi) {
+          for (size_t j = lo; j < hi; j++) stage[j] = fq_mul(d, cw[j]);
+        });
+        SPG_HIP(ctx, hipMemcpyAsync(d_s, stage, n * sizeof(Fq), hipMemcpyHostToDevice, ctx->stream));
+      }
       rc = comb_msm_parts(ctx, g.dev, d_s, d_idx, gmax, (int)n, 1, (Ext*)d_map, &cper);
       if (rc != 0 && rc != 1) return rc;
+    }
+    if (rc == 1 && use_dfin) {  // the comb does not apply: cw from the device (plain integers), with the last fold
+      SPG_HIP(ctx, hipMemcpyAsync(cw.data(), dfin.cw, n * sizeof(Fq), hipMemcpyDeviceToHost, ctx->stream));
+      SPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      par_range(n, [&](size_t lo, size_t hi) {
+        for (size_t j = lo; j < hi; j++) cw[j] = fq_mul(fq_to_mont(cw[j]), (j & 1) ? dfin.u : dfin.uinv);
+      });
     }
     if (rc == 0) {
       SPG_HIP(ctx, hipEventRecord(ctx->ev_cx, ctx->stream));

@@ -119,6 +119,7 @@ ROUND_FORMS = {
     "delta_bucket_msm": {"SPG_DELTA_COMB": "0"},
     "bullet_comb_rolled": {"SPG_BCOMB_ROLL": "1"},
     "dotlog_cy_beta_in_order": {"SPG_DOTLOG_EARLY": "0"},
+    "delta_scalars_from_host": {"SPG_DELTA_DEV": "0"},
     "spmv_and_z_fill_untiled": {"SPG_SPMV_TILED": "0", "SPG_Z_TILED": "0"},
     "q_folds_one_per_challenge": {"SPG_Q_BOUND_ALL": "0"},
     "opening_combinations_on_calling_thread": {"SPG_AXPY_POOL": "0"},
