@@ -145,6 +145,17 @@ int spg_pqx_evaluate(spg_ctx* ctx, const spg_pqx* h, const uint64_t* rp, size_t 
  * rewrite the low halves in place and the allocation never shrinks, as the reference's nested Vecs) */
 int spg_pqx_shape(const spg_pqx* h, size_t* dims, size_t* num_proofs, size_t* num_inputs);
 int spg_pqx_download(spg_ctx* ctx, const spg_pqx* h, uint64_t* z_mont);
+/* R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436; multiply_vec_disjoint_rounds per (p, q),
+ * src/sparse_mlpoly.rs:454-472) on an instance from spg_r1cs_inst_new: z_mat (p, q, w, x) -- instance p's
+ * num_proofs[p] x num_witness_secs x num_inputs[p] scalars, instances one after another; column c of a matrix reads
+ * z[p][q][c / max_num_inputs][c % max_num_inputs], zero past num_inputs[p] -- into three new DensePolynomialPqx tables
+ * Az, Bz, Cz in new_rev order (num_proofs, max_num_proofs; num_cons, max_num_cons of the instance; one w section).
+ * num_proofs[p] and the instance's num_cons are powers of two; 1..8 witness sections. */
+struct spg_r1cs_inst;
+int spg_r1cs_multiply_vec_block(spg_ctx* ctx, const struct spg_r1cs_inst* inst, size_t num_instances,
+                                const size_t* num_proofs, size_t max_num_proofs, const size_t* num_inputs,
+                                size_t max_num_inputs, size_t num_witness_secs, const uint64_t* z_mont, spg_pqx** Az,
+                                spg_pqx** Bz, spg_pqx** Cz);
 
 /* ---- generators ------------------------------------------------------------------------------
  * MultiCommitGens::new(n, label) (src/commitments.rs:15-33): n+1 points from SHAKE256(label ||

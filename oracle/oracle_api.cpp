@@ -705,3 +705,38 @@ int orc_snark_last_phases(char* names, double* us, int max) {
 }
 double orc_snark_last_verify_us() { return g_snark_verify_us; }
 }
+
+extern "C" {
+// R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436) -> Az, Bz, Cz flattened in DensePolynomialPqx layout
+// (instance p: num_proofs[p] x 1 x num_cons[p], q_rev / x_rev order). z: instance p's num_proofs[p] x nws x
+// num_inputs[p] scalars; each section row is padded with zeros to max_num_inputs for the reference's z[w][c % max].
+int orc_multiply_vec_block(const spg_r1cs_instance* ci, size_t P, const size_t* num_proofs, size_t max_num_proofs,
+                           const size_t* num_inputs, size_t max_num_inputs, size_t nws, const uint64_t* z,
+                           uint64_t* outA, uint64_t* outB, uint64_t* outC) {
+  R1CSInstance inst = inst_from_c(ci);
+  Mat4 zm(P);
+  const uint64_t* s = z;
+  for (size_t p = 0; p < P; p++) {
+    zm[p].assign(num_proofs[p], std::vector<FqVec>(nws, FqVec(max_num_inputs, fq_zero())));
+    for (size_t q = 0; q < num_proofs[p]; q++)
+      for (size_t w = 0; w < nws; w++)
+        for (size_t x = 0; x < num_inputs[p]; x++, s += 4) zm[p][q][w][x] = ld(s);
+  }
+  std::vector<size_t> np(num_proofs, num_proofs + P), ni(num_inputs, num_inputs + P), nc(P);
+  for (size_t p = 0; p < P; p++) nc[p] = inst.num_cons[inst.num_instances == 1 ? 0 : p];
+  Pqx Az, Bz, Cz;
+  inst.multiply_vec_block(P, np, max_num_proofs, ni, max_num_inputs, inst.max_num_cons, nc, zm, &Az, &Bz, &Cz);
+  uint64_t* outs[3] = {outA, outB, outC};
+  const Pqx* T[3] = {&Az, &Bz, &Cz};
+  for (int k = 0; k < 3; k++) {
+    uint64_t* o = outs[k];
+    for (size_t p = 0; p < P; p++)
+      for (size_t q = 0; q < T[k]->Z[p].size(); q++)
+        for (const Fq& v : T[k]->Z[p][q][0]) {
+          st(o, v);
+          o += 4;
+        }
+  }
+  return 0;
+}
+}

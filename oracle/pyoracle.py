@@ -326,6 +326,24 @@ def r1cs_multi_evaluate(wl, rx, ry):
     return out
 
 
+def r1cs_multiply_vec_block(wl, z, num_inputs):
+    """R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436) -> (Az, Bz, Cz) flattened in Pqx order"""
+    import workload
+
+    v = workload.CViews(wl)
+    zz = u64s(z).reshape(-1, 4)
+    npf = np.asarray(wl.num_proofs, dtype=np.uint64)
+    nin = np.asarray(num_inputs, dtype=np.uint64)
+    nc = [wl.num_cons[0 if wl.shared else p] for p in range(wl.P)]
+    n = sum(a * b for a, b in zip(wl.num_proofs, nc))
+    outs = [np.zeros((n, 4), np.uint64) for _ in range(3)]
+    rc = lib().orc_multiply_vec_block(ctypes.byref(v.inst), ctypes.c_size_t(wl.P), _p(npf), ctypes.c_size_t(wl.max_num_proofs),
+                                      _p(nin), ctypes.c_size_t(wl.max_num_inputs), ctypes.c_size_t(wl.nws), _p(zz),
+                                      *[_p(o) for o in outs])
+    assert rc == 0
+    return outs
+
+
 def spark_prove(wl, rx, ry, tape_seed, gens_label=b"gens_r1cs_eval", gens_nnz=None, gens_batch=3,
                 label=b"spark_test", transcript=None):
     """SparseMatPolyEvalProof over [A_0, B_0, C_0, ...] of the workload's instance at (rx, ry):

@@ -52,3 +52,8 @@ struct PqxDev {
 };
 
 }  // namespace spg
+
+// the C-ABI handle of a resident DensePolynomialPqx (seams.hip; spg_r1cs_multiply_vec_block in r1cs.hip makes them too)
+struct spg_pqx {
+  spg::PqxDev T;
+};

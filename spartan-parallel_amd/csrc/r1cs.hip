@@ -2252,3 +2252,143 @@ extern "C" int spg_r1cs_multi_evaluate(spg_ctx* ctx, const spg_r1cs_inst* inst, 
   for (size_t i = 0; i < 3 * Pm; i++) st_fq(out + 4 * i, h[i]);
   return SPG_OK;
 }
+
+// R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436; per (p, q): multiply_vec_disjoint_rounds,
+// src/sparse_mlpoly.rs:454-472) as a seam: z_mat (p, q, w, x) -- instance p's num_proofs[p] x num_witness_secs x
+// num_inputs[p] scalars, instances one after another, column c of a matrix reading z[p][q][c / max_num_inputs]
+// [c % max_num_inputs] (zero past num_inputs[p]) -- into Az, Bz, Cz as new spg_pqx tables in
+// DensePolynomialPqx::new_rev order (p, q_rev, x_rev: num_proofs, max_num_proofs, num_cons, max_num_cons; one w
+// section). The prover's own k_spmv does the work, over section descriptors pointing into one upload of z.
+extern "C" int spg_r1cs_multiply_vec_block(spg_ctx* ctx, const spg_r1cs_inst* inst, size_t num_instances,
+                                           const size_t* num_proofs, size_t max_num_proofs, const size_t* num_inputs,
+                                           size_t max_num_inputs, size_t num_witness_secs, const uint64_t* z_mont,
+                                           spg_pqx** Az, spg_pqx** Bz, spg_pqx** Cz) {
+  if (!ctx || !inst || !num_proofs || !num_inputs || !z_mont || !Az || !Bz || !Cz || num_instances == 0)
+    return SPG_E_ARG;
+  auto pow2 = [](size_t v) { return v && !(v & (v - 1)); };
+  // r1csinstance.rs:375-376: one matrix for every instance, or one per instance
+  if (!(inst->num_instances == 1 || inst->num_instances == num_instances))
+    return set_err(ctx, SPG_E_ARG, "multiply_vec_block: the instance holds 1 or num_instances matrices");
+  if (num_witness_secs == 0 || num_witness_secs > 8)  // (k_spmv keeps one block's section descriptors in LDS)
+    return set_err(ctx, SPG_E_ARG, "multiply_vec_block: 1..8 witness sections");
+  if (!pow2(max_num_proofs) || max_num_inputs == 0 || max_num_inputs > 0xffffffffu)
+    return set_err(ctx, SPG_E_ARG, "multiply_vec_block: max_num_proofs a power of two, max_num_inputs > 0");
+  const size_t P = num_instances;
+  std::vector<size_t> ncons(P);
+  size_t zt = 0, total = 0;
+  for (size_t p = 0; p < P; p++) {
+    const size_t pi = inst->num_instances == 1 ? 0 : p;
+    ncons[p] = inst->num_cons[pi];
+    if (!pow2(num_proofs[p]) || num_proofs[p] > max_num_proofs || num_inputs[p] > max_num_inputs || !pow2(ncons[p]))
+      return set_err(ctx, SPG_E_ARG, "multiply_vec_block: num_proofs[p] (<= max) and num_cons powers of two, "
+                                     "num_inputs[p] <= max_num_inputs");
+    zt += num_proofs[p] * num_witness_secs * num_inputs[p];
+    total += num_proofs[p] * ncons[p];
+  }
+  if (total >= ((size_t)1 << 31)) return set_err(ctx, SPG_E_ARG, "multiply_vec_block: at most 2^31 outputs");
+  // z section-major on the device: section w of instance p as its own (q, x) matrix, as a witness section lies
+  std::vector<Fq> zs(zt);
+  std::vector<SecDesc> sd(num_witness_secs * P);
+  std::vector<size_t> soff(num_witness_secs * P);
+  {
+    size_t o = 0;
+    for (size_t w = 0; w < num_witness_secs; w++)
+      for (size_t p = 0; p < P; p++) {
+        soff[w * P + p] = o;
+        o += num_proofs[p] * num_inputs[p];
+      }
+    const uint64_t* src = z_mont;
+    for (size_t p = 0; p < P; p++)
+      for (size_t q = 0; q < num_proofs[p]; q++)
+        for (size_t w = 0; w < num_witness_secs; w++)
+          for (size_t x = 0; x < num_inputs[p]; x++, src += 4)
+            zs[soff[w * P + p] + q * num_inputs[p] + x] = ld_fq(src);
+  }
+  Fq* d_z = nullptr;
+  void* d_desc = nullptr;
+  std::vector<SpDesc> spd(P);
+  std::vector<MatDesc> md(inst->num_instances);
+  for (size_t p = 0; p < inst->num_instances; p++) {
+    for (int m = 0; m < 3; m++) md[p].rp[m] = inst->rp_off[3 * p + m];
+    md[p].cp = inst->cp_off[p];
+  }
+  size_t off = 0;
+  for (size_t p = 0; p < P; p++) {
+    spd[p].dom_off = spd[p].out_off = off;
+    spd[p].pi = (uint32_t)(inst->num_instances == 1 ? 0 : p);
+    spd[p].lg_q = (uint32_t)lg2(num_proofs[p]);
+    spd[p].nrows = (uint32_t)ncons[p];
+    spd[p].lg_rows = (uint32_t)lg2(ncons[p]);
+    spd[p].ni = (uint32_t)num_inputs[p];
+    spd[p].lg_ni = 0;
+    off += num_proofs[p] * ncons[p];
+  }
+  const size_t b_sec = sd.size() * sizeof(SecDesc), b_sp = spd.size() * sizeof(SpDesc),
+               b_md = md.size() * sizeof(MatDesc);
+  spg_pqx* outs[3] = {new spg_pqx(), new spg_pqx(), new spg_pqx()};
+  int rc = 0;
+  auto fail = [&](int code, const char* msg) {
+    rc = set_err(ctx, code, msg);
+  };
+  if (hipMalloc(&d_z, zt * sizeof(Fq) + 64) != hipSuccess || hipMalloc(&d_desc, b_sec + b_sp + b_md + 64) != hipSuccess)
+    fail(SPG_E_NOMEM, "multiply_vec_block");
+  for (int k = 0; k < 3 && !rc; k++) {
+    PqxDev& T = outs[k]->T;
+    T.zlen = P;
+    size_t o = 0;
+    for (size_t p = 0; p < P; p++) {
+      T.off.push_back(o);
+      T.anp.push_back(num_proofs[p]);
+      T.anw.push_back(1);
+      T.ani.push_back(ncons[p]);
+      o += num_proofs[p] * ncons[p];
+    }
+    T.total = total;
+    T.num_instances = 1;
+    while (T.num_instances < P) T.num_instances *= 2;
+    T.max_num_proofs = max_num_proofs;
+    T.num_witness_secs = 1;
+    T.max_num_inputs = inst->max_num_cons;
+    T.num_proofs.assign(num_proofs, num_proofs + P);
+    T.num_inputs = ncons;
+    if (hipMalloc(&T.d, total * sizeof(Fq) + 64) != hipSuccess) fail(SPG_E_NOMEM, "multiply_vec_block outputs");
+  }
+  if (!rc) {
+    for (size_t w = 0; w < num_witness_secs; w++)
+      for (size_t p = 0; p < P; p++) {
+        SecDesc& s = sd[w * P + p];
+        s.w = d_z + soff[w * P + p];
+        s.np = (uint32_t)num_proofs[p];
+        s.ni = (uint32_t)num_inputs[p];
+      }
+    std::vector<uint8_t> blob(b_sec + b_sp + b_md);
+    memcpy(blob.data(), sd.data(), b_sec);
+    memcpy(blob.data() + b_sec, spd.data(), b_sp);
+    memcpy(blob.data() + b_sec + b_sp, md.data(), b_md);
+    uint8_t* dd = (uint8_t*)d_desc;
+    if (hipMemcpy(d_z, zs.data(), zt * sizeof(Fq), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dd, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess)
+      fail(SPG_E_HIP, "multiply_vec_block upload");
+    if (!rc && total) {
+      hipLaunchKernelGGL(k_spmv<false>, dim3(blocks_for(total)), dim3(256), 0, ctx->stream, (const SpDesc*)(dd + b_sec),
+                         (int)P, (const MatDesc*)(dd + b_sec + b_sp), inst->d_rowptr, inst->d_col, inst->d_val,
+                         (const SecDesc*)dd, (int)num_witness_secs, (uint32_t)max_num_inputs, outs[0]->T.d,
+                         outs[1]->T.d, outs[2]->T.d, (uint64_t)total);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
+        fail(SPG_E_HIP, "multiply_vec_block launch");
+    }
+  }
+  hipFree(d_z);
+  hipFree(d_desc);
+  if (rc) {
+    for (spg_pqx* h : outs) {
+      hipFree(h->T.d);
+      delete h;
+    }
+    return rc;
+  }
+  *Az = outs[0];
+  *Bz = outs[1];
+  *Cz = outs[2];
+  return SPG_OK;
+}

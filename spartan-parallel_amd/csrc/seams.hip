@@ -163,9 +163,6 @@ extern "C" int spg_prove_cubic(spg_ctx* ctx, const uint64_t* claim_mont, size_t 
 // ---- DensePolynomialPqx (src/custom_dense_mlpoly.rs:22-359) as a handle over the prover's own ragged HBM layout
 // (pqx.hpp: instance p owns num_proofs[p] x nws x num_inputs[p] scalars at off[p]; folds rewrite the low halves in
 // place and shrink the current sizes, the allocation stays, so index() keeps the reference's bounds semantics)
-struct spg_pqx {
-  spg::PqxDev T;
-};
 
 namespace {
 int pqx_bind_one(spg_ctx* ctx, spg::PqxDev& T, const Fq& r, int mode) {

@@ -630,6 +630,31 @@ class R1CSInst:
             pass
 
 
+def r1cs_multiply_vec_block(ctx, inst, num_proofs, max_num_proofs, num_inputs, max_num_inputs, num_witness_secs, z):
+    """R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436) -> (Az, Bz, Cz) as resident Pqx tables; z holds
+    instance p's num_proofs[p] x num_witness_secs x num_inputs[p] scalars, instances concatenated"""
+    P = len(num_proofs)
+    a = _scalars(z)
+    np_ = np.asarray(num_proofs, dtype=np.uint64)
+    ni_ = np.asarray(num_inputs, dtype=np.uint64)
+    hs = [ctypes.c_void_p() for _ in range(3)]
+    ctx.check(lib().spg_r1cs_multiply_vec_block(ctx.handle, inst.handle, ctypes.c_size_t(P), _p(np_),
+                                                ctypes.c_size_t(max_num_proofs), _p(ni_), ctypes.c_size_t(max_num_inputs),
+                                                ctypes.c_size_t(num_witness_secs), _p(a), *[ctypes.byref(h) for h in hs]),
+              "spg_r1cs_multiply_vec_block")
+    out = []
+    for h in hs:
+        t = Pqx.__new__(Pqx)
+        t.ctx, t._h, t.P = ctx, h, P
+        dims = np.zeros(4, dtype=np.uint64)
+        npf = np.zeros(P, dtype=np.uint64)
+        nin = np.zeros(P, dtype=np.uint64)
+        assert lib().spg_pqx_shape(h, _p(dims), _p(npf), _p(nin)) == 0
+        t.n = int(sum(int(x) * int(y) for x, y in zip(npf, nin)))
+        out.append(t)
+    return tuple(out)
+
+
 def r1cs_multi_evaluate(ctx, inst, num_instances, rx, ry):
     """R1CSInstance::multi_evaluate -> (3 * num_instances, 4) limbs [A_0, B_0, C_0, A_1, ...]"""
     rx = _scalars(rx)

@@ -423,3 +423,74 @@ def test_pqx_rejects_bad_shapes(ctx, oracle):
     T = spg.Pqx(ctx, z[:8], [2], 2, 1, [4], 4)
     with pytest.raises(spg.SpgError):
         T.bound(mont(1), 5)
+
+
+# ---- R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436) ----
+# (num_cons, num_proofs, witness sections, one shared instance): ragged q, several sections, a shared matrix, and
+# > 32 instances (k_spmv's descriptors in HBM)
+SPMV_CASES = {
+    "ragged3": ([16, 8, 4], [4, 1, 2], 3, False),
+    "shared": ([8, 8], [2, 4], 2, True),
+    "one": ([32], [8], 1, False),
+    "many": ([4] * 36, [2] * 18 + [1] * 18, 2, False),
+}
+
+
+def spmv_workload(oracle, case):
+    import workload
+
+    nc, npf, nws, shared = SPMV_CASES[case]
+    wl = workload.R1CSWorkload(nc, npf, num_sections=nws, shared_instance=shared)
+    rng = np.random.default_rng(len(case))
+    for mats in wl.entries:  # random matrix values instead of the synthetic circuit's ones
+        for m in mats:
+            m[:, 2:] = rand_fq(oracle, rng, m.shape[0])
+    z = np.concatenate([np.stack([wl.sections[w][p][q] for w in range(wl.nws)]).reshape(-1, 4)
+                        for p in range(wl.P) for q in range(wl.num_proofs[p])])
+    return wl, z
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(SPMV_CASES))
+def test_multiply_vec_block_matches_oracle(ctx, oracle, case):
+    """Az, Bz, Cz entry by entry in new_rev order and their sizes; then Az bound through the Pqx seam as the R1CS
+    proof binds it (x rounds first) equals the oracle's"""
+    import spg
+    import workload
+
+    wl, z = spmv_workload(oracle, case)
+    v = workload.CViews(wl)
+    inst = spg.R1CSInst(ctx, v.inst)
+    got = spg.r1cs_multiply_vec_block(ctx, inst, wl.num_proofs, wl.max_num_proofs, wl.num_inputs, wl.max_num_inputs,
+                                      wl.nws, z)
+    want = oracle.r1cs_multiply_vec_block(wl, z, wl.num_inputs)
+    nc = [wl.num_cons[0 if wl.shared else p] for p in range(wl.P)]
+    for T, W in zip(got, want):
+        assert np.array_equal(T.download(), W)
+        dims, gp, gi = T.shape()
+        assert dims == (1 << (wl.P - 1).bit_length(), wl.max_num_proofs, 1, wl.max_num_cons)
+        assert gp == list(wl.num_proofs) and gi == nc
+    lx, lq = (wl.max_num_cons - 1).bit_length(), (wl.max_num_proofs - 1).bit_length()
+    modes = [4] * lx + [2] * lq
+    rs = rand_fq(oracle, np.random.default_rng(9), max(len(modes), 1))
+    for k, m in enumerate(modes):
+        got[0].bound(rs[k], m)
+    ref = oracle.pqx_bind(want[0], wl.num_proofs, wl.max_num_proofs, 1, nc, wl.max_num_cons, modes, rs[:len(modes)])
+    assert np.array_equal(got[0].download(), ref[0])
+
+
+@pytest.mark.gpu
+def test_multiply_vec_block_rejects_bad_shapes(ctx, oracle):
+    import spg
+    import workload
+
+    wl, z = spmv_workload(oracle, "ragged3")
+    inst = spg.R1CSInst(ctx, workload.CViews(wl).inst)
+    with pytest.raises(spg.SpgError):  # 2 instances against a 3-instance matrix list
+        spg.r1cs_multiply_vec_block(ctx, inst, wl.num_proofs[:2], wl.max_num_proofs, wl.num_inputs[:2],
+                                    wl.max_num_inputs, wl.nws, z)
+    with pytest.raises(spg.SpgError):  # num_proofs not a power of two
+        spg.r1cs_multiply_vec_block(ctx, inst, [3, 1, 2], 4, wl.num_inputs, wl.max_num_inputs, wl.nws, z)
+    with pytest.raises(spg.SpgError):  # 9 sections
+        spg.r1cs_multiply_vec_block(ctx, inst, wl.num_proofs, wl.max_num_proofs, wl.num_inputs, wl.max_num_inputs, 9,
+                                    np.zeros((4096, 4), np.uint64))
