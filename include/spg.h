@@ -151,6 +151,13 @@ int spg_pqx_download(spg_ctx* ctx, const spg_pqx* h, uint64_t* z_mont);
  * z[p][q][c / max_num_inputs][c % max_num_inputs], zero past num_inputs[p] -- into three new DensePolynomialPqx tables
  * Az, Bz, Cz in new_rev order (num_proofs, max_num_proofs; num_cons, max_num_cons of the instance; one w section).
  * num_proofs[p] and the instance's num_cons are powers of two; 1..8 witness sections. */
+/* One x or q round of the R1CS proof's phase-1 sumcheck (prove_cubic_with_additive_term_disjoint_rounds,
+ * src/sumcheck.rs:1173-1245, comb A (B C - D)): out3 = (eval_point_0, eval_point_2, eval_point_3) over the eq
+ * factors Ap, Aq, Ax in their current lengths (instance_len = |Ap|; an x round (mode 4) has cons_len = |Ax| / 2, a q
+ * round (mode 2, once |Ax| = 1) proof_len = |Aq| / 2) and the tables B, C, D (one shape, one witness section) in
+ * their current state. The caller then binds Ax or Aq (spg_buf_bound_top) and B, C, D (spg_pqx_bound) with r_j. */
+int spg_phase1_round_evals(spg_ctx* ctx, const spg_buf* Ap, const spg_buf* Aq, const spg_buf* Ax, const spg_pqx* B,
+                           const spg_pqx* C, const spg_pqx* D, int mode, uint64_t* out3_mont);
 struct spg_r1cs_inst;
 int spg_r1cs_multiply_vec_block(spg_ctx* ctx, const struct spg_r1cs_inst* inst, size_t num_instances,
                                 const size_t* num_proofs, size_t max_num_proofs, const size_t* num_inputs,

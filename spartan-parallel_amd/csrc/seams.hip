@@ -287,3 +287,46 @@ extern "C" int spg_pqx_evaluate(spg_ctx* ctx, const spg_pqx* h, const uint64_t* 
   spg::st_fq(out_mont, v);
   return SPG_OK;
 }
+
+// One round of SumcheckInstanceProof::prove_cubic_with_additive_term_disjoint_rounds (src/sumcheck.rs:1067-1380,
+// round loop :1173-1245; comb A (B C - D), src/r1csproof.rs) in an x or q round: (e0, e2, e3) over the eq factors
+// Ap, Aq, Ax (dense, their current lengths: the round's instance_len = |Ap|, proof_len = |Aq| (/ 2 in a q round),
+// cons_len = |Ax| (/ 2 in an x round)) and B, C, D (Pqx tables of one shape, one witness section) in their current
+// state -- the reference's local num_proofs / num_cons are the tables' own sizes, halved at the round start as there.
+// The prover's phase-1 evaluation kernels do the work.
+extern "C" int spg_phase1_round_evals(spg_ctx* ctx, const spg_buf* Ap, const spg_buf* Aq, const spg_buf* Ax,
+                                      const spg_pqx* B, const spg_pqx* C, const spg_pqx* D, int mode,
+                                      uint64_t* out3_mont) {
+  if (!ctx || !Ap || !Aq || !Ax || !B || !C || !D || !out3_mont) return SPG_E_ARG;
+  const spg::PqxDev& T = B->T;
+  for (const spg_pqx* o : {C, D})
+    if (o->T.zlen != T.zlen || o->T.anp != T.anp || o->T.anw != T.anw || o->T.ani != T.ani ||
+        o->T.num_proofs != T.num_proofs || o->T.num_inputs != T.num_inputs)
+      return spg::set_err(ctx, SPG_E_ARG, "phase-1 round: B, C, D must share one shape");
+  if (T.num_witness_secs != 1)  // sumcheck.rs:1099-1102 assert_eq!(poly_B.num_witness_secs, 1)
+    return spg::set_err(ctx, SPG_E_ARG, "phase-1 round: one witness section");
+  if (mode != spg::MODE_X && mode != spg::MODE_Q)
+    return spg::set_err(ctx, SPG_E_ARG, "phase-1 round: mode 4 (x) or 2 (q); the p rounds run on the host-sized tail");
+  if (!spg::pow2(Ap->n) || !spg::pow2(Aq->n) || !spg::pow2(Ax->n) || Ap->n < T.zlen)
+    return spg::set_err(ctx, SPG_E_ARG, "phase-1 round: eq tables of power-of-two lengths, |Ap| >= instances");
+  if (mode == spg::MODE_X ? Ax->n < 2 : (Ax->n != 1 || Aq->n < 2))
+    return spg::set_err(ctx, SPG_E_ARG, "phase-1 round: x rounds first (|Ax| >= 2), q rounds once |Ax| = 1");
+  const size_t instance_len = Ap->n, proof_len = mode == spg::MODE_Q ? Aq->n / 2 : Aq->n,
+               cons_len = mode == spg::MODE_X ? Ax->n / 2 : 1;
+  std::vector<size_t> sc_np = T.num_proofs, sc_nc = T.num_inputs;
+  for (size_t p = 0; p < T.zlen; p++) {
+    if (mode == spg::MODE_X && sc_nc[p] > 1) sc_nc[p] /= 2;
+    if (mode == spg::MODE_Q && sc_np[p] > 1) sc_np[p] /= 2;
+    if (proof_len % sc_np[p] || cons_len % sc_nc[p])
+      return spg::set_err(ctx, SPG_E_ARG, "phase-1 round: table sizes exceed the eq tables");
+  }
+  Fq* partials = (Fq*)spg::ws_get(ctx, spg::kWsSeamPart,
+                                  std::max(3 * (size_t)spg::kScGridMax, spg::kP1PairMax) * sizeof(Fq) + 64);
+  if (!partials) return spg::set_err(ctx, SPG_E_NOMEM, "phase-1 round partials");
+  Fq e[3];
+  const int rc = spg::phase1_eval(ctx, T, mode, proof_len, cons_len, instance_len, sc_np, sc_nc, Ap->d, Aq->d, Ax->d,
+                                  T.d, C->T.d, D->T.d, partials, e);
+  if (rc) return rc;
+  for (int k = 0; k < 3; k++) spg::st_fq(out3_mont + 4 * k, e[k]);
+  return SPG_OK;
+}

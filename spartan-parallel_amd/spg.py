@@ -630,6 +630,14 @@ class R1CSInst:
             pass
 
 
+def phase1_round_evals(Ap, Aq, Ax, B, C, D, mode):
+    """one x (mode 4) or q (mode 2) round of the phase-1 sumcheck (src/sumcheck.rs:1173-1245): (e0, e2, e3)"""
+    out = np.zeros((3, 4), dtype=np.uint64)
+    Ap.ctx.check(lib().spg_phase1_round_evals(Ap.ctx.handle, Ap.handle, Aq.handle, Ax.handle, B._h, C._h, D._h,
+                                              ctypes.c_int(mode), _p(out)), "spg_phase1_round_evals")
+    return out
+
+
 def r1cs_multiply_vec_block(ctx, inst, num_proofs, max_num_proofs, num_inputs, max_num_inputs, num_witness_secs, z):
     """R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436) -> (Az, Bz, Cz) as resident Pqx tables; z holds
     instance p's num_proofs[p] x num_witness_secs x num_inputs[p] scalars, instances concatenated"""

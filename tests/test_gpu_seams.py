@@ -494,3 +494,76 @@ def test_multiply_vec_block_rejects_bad_shapes(ctx, oracle):
     with pytest.raises(spg.SpgError):  # 9 sections
         spg.r1cs_multiply_vec_block(ctx, inst, wl.num_proofs, wl.max_num_proofs, wl.num_inputs, wl.max_num_inputs, 9,
                                     np.zeros((4096, 4), np.uint64))
+
+
+# ---- one phase-1 round (src/sumcheck.rs:1173-1245) ----
+
+def phase1_round_py(Ap, Aq, Ax, tabs, shape, mode):
+    """the reference's round loop on Python integers: tabs = (B, C, D) as integer lists in the Pqx allocation layout,
+    shape = (anp, ani, num_proofs, num_inputs) -- current sizes before the round's halving"""
+    anp, ani, npf, nin = shape
+    P = len(npf)
+    off = [sum(anp[k] * ani[k] for k in range(p)) for p in range(P)]
+    instance_len, proof_len = len(Ap), len(Aq) // 2 if mode == 2 else len(Aq)
+    cons_len = len(Ax) // 2 if mode == 4 else len(Ax)
+
+    def idx(T, p, q, x):
+        return T[off[p] + q * ani[p] + x] if (p < P and q < anp[p] and x < ani[p]) else 0
+
+    def idx_hi(T, p, q, x):
+        if mode == 4:
+            return 0 if nin[p] == 1 else T[off[p] + q * ani[p] + x + nin[p] // 2]
+        return 0 if npf[p] == 1 else T[off[p] + (q + npf[p] // 2) * ani[p] + x]
+
+    e = [0, 0, 0]
+    comb = lambda a, b, c, d: a * (b * c - d)  # noqa: E731 (r1csproof.rs comb_func)
+    for p in range(min(instance_len, P)):
+        lnc = nin[p] // 2 if (mode == 4 and nin[p] > 1) else nin[p]
+        lnp = npf[p] // 2 if (mode == 2 and npf[p] > 1) else npf[p]
+        for q in range(lnp):
+            sq, sx = proof_len // lnp, cons_len // lnc
+            for x in range(lnc):
+                a = Ap[p] * Aq[q * sq] * Ax[x * sx]
+                ah = Ap[p] * (Aq[q * sq + proof_len] * Ax[x * sx] if mode == 2 else Aq[q * sq] * Ax[x * sx + cons_len])
+                lo = [idx(T, p, q, x) for T in tabs]
+                hi = [idx_hi(T, p, q, x) for T in tabs]
+                e[0] += comb(a, *lo)
+                b2 = [2 * h - l for h, l in zip(hi, lo)]
+                a2 = 2 * ah - a
+                e[1] += comb(a2, *b2)
+                b3 = [v + h - l for v, h, l in zip(b2, hi, lo)]
+                e[2] += comb(a2 + ah - a, *b3)
+    return [v % Q for v in e]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["ragged3", "shared", "many"])
+def test_phase1_rounds_match_python_loop(ctx, oracle, case):
+    """every x round then every q round of phase 1 on Az, Bz, Cz from the SpMV seam: (e0, e2, e3) against the
+    reference loop restated on Python integers, the tables bound between rounds through the seams"""
+    import spg
+    import workload
+
+    wl, z = spmv_workload(oracle, case)
+    inst = spg.R1CSInst(ctx, workload.CViews(wl).inst)
+    tabs = spg.r1cs_multiply_vec_block(ctx, inst, wl.num_proofs, wl.max_num_proofs, wl.num_inputs, wl.max_num_inputs,
+                                       wl.nws, z)
+    rng = np.random.default_rng(77)
+    lp = (wl.P - 1).bit_length()
+    eq = [spg.Buf(ctx, rand_fq(oracle, rng, n)) for n in (1 << lp, wl.max_num_proofs, wl.max_num_cons)]
+    Ap, Aq, Ax = eq
+    lx, lq = (wl.max_num_cons - 1).bit_length(), (wl.max_num_proofs - 1).bit_length()
+    anp, ani = list(wl.num_proofs), [wl.num_cons[0 if wl.shared else p] for p in range(wl.P)]
+    for j, mode in enumerate([4] * lx + [2] * lq):
+        got = spg.phase1_round_evals(Ap, Aq, Ax, *tabs, mode)
+        _, npf, nin = tabs[0].shape()
+        want = phase1_round_py([to_int(v) for v in Ap.download()], [to_int(v) for v in Aq.download()],
+                               [to_int(v) for v in Ax.download()],
+                               [[to_int(v) for v in T.download()] for T in tabs], (anp, ani, npf, nin), mode)
+        assert [to_int(v) for v in got] == want, (j, mode)
+        r = rand_fq(oracle, rng, 1)[0]
+        (Ax if mode == 4 else Aq).bound_top(r)
+        for T in tabs:
+            T.bound(r, mode)
+    with pytest.raises(spg.SpgError):  # every x and q variable bound: no x / q round left
+        spg.phase1_round_evals(Ap, Aq, Ax, *tabs, 4)
