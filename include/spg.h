@@ -158,6 +158,12 @@ int spg_pqx_download(spg_ctx* ctx, const spg_pqx* h, uint64_t* z_mont);
  * their current state. The caller then binds Ax or Aq (spg_buf_bound_top) and B, C, D (spg_pqx_bound) with r_j. */
 int spg_phase1_round_evals(spg_ctx* ctx, const spg_buf* Ap, const spg_buf* Aq, const spg_buf* Ax, const spg_pqx* B,
                            const spg_pqx* C, const spg_pqx* D, int mode, uint64_t* out3_mont);
+/* One y (mode 4), w (mode 3) or p (mode 1) round of the R1CS proof's phase-2 sumcheck (prove_cubic_disjoint_rounds,
+ * src/sumcheck.rs:881-941, comb A B C): out3 = (e0, e2, e3) over eq(r_p) (A; instance_len = |A|, / 2 in a p round),
+ * ABC (one instance when single_inst, else one per instance) and Z, both with q bound (one proof row) and in their
+ * current state; num_witness_secs is the reference's argument. The caller binds A (p rounds) and ABC, Z with r_j. */
+int spg_phase2_round_evals(spg_ctx* ctx, const spg_buf* A, const spg_pqx* ABC, const spg_pqx* Z, int mode,
+                           int single_inst, size_t num_witness_secs, uint64_t* out3_mont);
 struct spg_r1cs_inst;
 int spg_r1cs_multiply_vec_block(spg_ctx* ctx, const struct spg_r1cs_inst* inst, size_t num_instances,
                                 const size_t* num_proofs, size_t max_num_proofs, const size_t* num_inputs,

@@ -330,3 +330,41 @@ extern "C" int spg_phase1_round_evals(spg_ctx* ctx, const spg_buf* Ap, const spg
   for (int k = 0; k < 3; k++) spg::st_fq(out3_mont + 4 * k, e[k]);
   return SPG_OK;
 }
+
+// One round of the R1CS proof's phase-2 sumcheck (SumcheckInstanceProof::prove_cubic_disjoint_rounds,
+// src/sumcheck.rs:788-1065, round loop :881-941; comb A B C): (e0, e2, e3) over eq(r_p) (A, current length:
+// instance_len = |A|, / 2 in a p round), ABC (one instance when single_inst, else one per instance) and Z in their
+// current state, in a y (mode 4), w (mode 3) or p (mode 1) round; num_witness_secs: the reference's argument (the
+// sections that exist); witness_secs_len and the local num_inputs are Z's own sizes, halved at the round start.
+extern "C" int spg_phase2_round_evals(spg_ctx* ctx, const spg_buf* A, const spg_pqx* ABC, const spg_pqx* Z, int mode,
+                                      int single_inst, size_t num_witness_secs, uint64_t* out3_mont) {
+  if (!ctx || !A || !ABC || !Z || !out3_mont || num_witness_secs == 0) return SPG_E_ARG;
+  const spg::PqxDev &TA = ABC->T, &TZ = Z->T;
+  if (mode != spg::MODE_X && mode != spg::MODE_W && mode != spg::MODE_P)
+    return spg::set_err(ctx, SPG_E_ARG, "phase-2 round: mode 4 (y), 3 (w) or 1 (p)");
+  if (single_inst ? TA.zlen != 1 : TA.zlen != TZ.zlen)
+    return spg::set_err(ctx, SPG_E_ARG, "phase-2 round: ABC holds one instance (single_inst) or one per instance");
+  if (!spg::pow2(A->n) || (mode == spg::MODE_P && A->n < 2))  // (the loop runs p < min(instance_len, instances))
+    return spg::set_err(ctx, SPG_E_ARG, "phase-2 round: eq(r_p) of power-of-two length (>= 2 in a p round)");
+  if ((mode == spg::MODE_X && TZ.max_num_inputs < 2) ||
+      (mode == spg::MODE_W && (TZ.max_num_inputs != 1 || TZ.num_witness_secs < 2)) ||
+      (mode == spg::MODE_P && (TZ.max_num_inputs != 1 || TZ.num_witness_secs != 1)))
+    return spg::set_err(ctx, SPG_E_ARG, "phase-2 round: y rounds, then w rounds, then p rounds");
+  for (const spg::PqxDev* T : {&TA, &TZ})
+    for (size_t p = 0; p < T->zlen; p++)
+      if (T->anp[p] != 1) return spg::set_err(ctx, SPG_E_ARG, "phase-2 round: tables of one proof row (q bound)");
+  const size_t instance_len = mode == spg::MODE_P ? A->n / 2 : A->n;
+  const size_t ws_len = mode == spg::MODE_W ? TZ.num_witness_secs / 2 : TZ.num_witness_secs;
+  std::vector<size_t> sc_ni = TZ.num_inputs;
+  for (size_t p = 0; p < sc_ni.size(); p++)
+    if (mode == spg::MODE_X && sc_ni[p] > 1) sc_ni[p] /= 2;
+  Fq* partials = (Fq*)spg::ws_get(ctx, spg::kWsSeamPart,
+                                  std::max(3 * (size_t)spg::kScGridMax, spg::kP1PairMax) * sizeof(Fq) + 64);
+  if (!partials) return spg::set_err(ctx, SPG_E_NOMEM, "phase-2 round partials");
+  Fq e[3];
+  const int rc = spg::phase2_eval(ctx, TA, TZ, mode, instance_len, ws_len, num_witness_secs, single_inst != 0, sc_ni,
+                                  A->d, partials, e);
+  if (rc) return rc;
+  for (int k = 0; k < 3; k++) spg::st_fq(out3_mont + 4 * k, e[k]);
+  return SPG_OK;
+}

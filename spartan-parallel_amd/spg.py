@@ -638,6 +638,15 @@ def phase1_round_evals(Ap, Aq, Ax, B, C, D, mode):
     return out
 
 
+def phase2_round_evals(A, ABC, Z, mode, single_inst, num_witness_secs):
+    """one y (4), w (3) or p (1) round of the phase-2 sumcheck (src/sumcheck.rs:881-941): (e0, e2, e3)"""
+    out = np.zeros((3, 4), dtype=np.uint64)
+    A.ctx.check(lib().spg_phase2_round_evals(A.ctx.handle, A.handle, ABC._h, Z._h, ctypes.c_int(mode),
+                                             ctypes.c_int(1 if single_inst else 0), ctypes.c_size_t(num_witness_secs),
+                                             _p(out)), "spg_phase2_round_evals")
+    return out
+
+
 def r1cs_multiply_vec_block(ctx, inst, num_proofs, max_num_proofs, num_inputs, max_num_inputs, num_witness_secs, z):
     """R1CSInstance::multiply_vec_block (src/r1csinstance.rs:363-436) -> (Az, Bz, Cz) as resident Pqx tables; z holds
     instance p's num_proofs[p] x num_witness_secs x num_inputs[p] scalars, instances concatenated"""

@@ -567,3 +567,83 @@ def test_phase1_rounds_match_python_loop(ctx, oracle, case):
             T.bound(r, mode)
     with pytest.raises(spg.SpgError):  # every x and q variable bound: no x / q round left
         spg.phase1_round_evals(Ap, Aq, Ax, *tabs, 4)
+
+
+# ---- one phase-2 round (src/sumcheck.rs:881-941) ----
+
+class PyPqx:
+    """a Pqx table's allocation (integers) and current sizes, with the reference's index / index_high
+    (custom_dense_mlpoly.rs:118-173)"""
+
+    def __init__(self, vals, anp, anw, ani, shape):
+        self.v, self.anp, self.anw, self.ani = vals, anp, anw, ani
+        (self.ninst, _, self.nws, _), self.npf, self.nin = shape
+        self.off = [sum(anp[k] * anw * ani[k] for k in range(p)) for p in range(len(anp))]
+
+    def at(self, p, q, w, x):
+        return self.v[self.off[p] + (q * self.anw + w) * self.ani[p] + x]
+
+    def index(self, p, q, w, x):
+        ok = p < len(self.anp) and q < self.anp[p] and w < self.anw and x < self.ani[p]
+        return self.at(p, q, w, x) if ok else 0
+
+    def index_high(self, p, q, w, x, mode):
+        if mode == 1:
+            ph = p + self.ninst // 2
+            return self.at(ph, q, w, x) if ph < len(self.anp) else 0
+        if mode == 3:
+            wh = w + self.nws // 2
+            return self.at(p, q, wh, x) if wh < self.anw else 0
+        return 0 if self.nin[p] == 1 else self.at(p, q, w, x + self.nin[p] // 2)
+
+
+def phase2_round_py(A, B, C, mode, single, nws_arg):
+    instance_len = len(A) // 2 if mode == 1 else len(A)
+    ws_len = C.nws // 2 if mode == 3 else C.nws
+    e = [0, 0, 0]
+    for p in range(min(instance_len, len(C.nin))):
+        pi = 0 if single else p
+        ni = C.nin[p] // 2 if (mode == 4 and C.nin[p] > 1) else C.nin[p]
+        for w in range(min(ws_len, nws_arg)):
+            for y in range(ni):
+                a, ah = A[p], (A[p + instance_len] if mode == 1 else A[p])
+                bl, bh = B.index(pi, 0, w, y), B.index_high(pi, 0, w, y, mode)
+                cl, ch = C.index(p, 0, w, y), C.index_high(p, 0, w, y, mode)
+                e[0] += a * bl * cl
+                a2, b2, c2 = 2 * ah - a, 2 * bh - bl, 2 * ch - cl
+                e[1] += a2 * b2 * c2
+                e[2] += (a2 + ah - a) * (b2 + bh - bl) * (c2 + ch - cl)
+    return [v % Q for v in e]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("nws", [1, 3, 4])
+def test_phase2_rounds_match_python_loop(ctx, oracle, single, nws):
+    """every y, w and p round of phase 2 on random ABC / Z tables (ragged widths, a section count that is not a
+    power of two, one shared ABC or one per instance): (e0, e2, e3) against the reference loop on Python integers,
+    the tables bound between rounds through the seams as sumcheck.rs:961-967 binds them"""
+    import spg
+
+    rng = np.random.default_rng(500 + nws + 10 * single)
+    ni = [8, 4, 8] if not single else [8, 8, 8]
+    P, max_ni = len(ni), 8
+    z = rand_fq(oracle, rng, sum(nws * x for x in ni))
+    abc_ni = ni[:1] if single else ni
+    abc = rand_fq(oracle, rng, sum(nws * x for x in abc_ni))
+    Z = spg.Pqx(ctx, z, [1] * P, 1, nws, ni, max_ni)
+    B = spg.Pqx(ctx, abc, [1] * len(abc_ni), 1, nws, abc_ni, max_ni)
+    A = spg.Buf(ctx, rand_fq(oracle, rng, 4))
+    ly, lw, lp = 3, (nws - 1).bit_length(), 2
+    for j, mode in enumerate([4] * ly + [3] * lw + [1] * lp):
+        got = spg.phase2_round_evals(A, B, Z, mode, single, nws)
+        Bp = PyPqx([to_int(v) for v in B.download()], [1] * len(abc_ni), nws, abc_ni, B.shape())
+        Zp = PyPqx([to_int(v) for v in Z.download()], [1] * P, nws, ni, Z.shape())
+        want = phase2_round_py([to_int(v) for v in A.download()], Bp, Zp, mode, single, nws)
+        assert [to_int(v) for v in got] == want, (j, mode)
+        r = rand_fq(oracle, rng, 1)[0]
+        if mode == 1:
+            A.bound_top(r)
+        if mode != 1 or not single:
+            B.bound(r, mode)
+        Z.bound(r, mode)
